@@ -1,0 +1,273 @@
+/*
+ * gx.h — C-ABI of the sidecar-gx gossip-convergence engine (Sidecar catalog merge path).
+ *
+ * One engine handle simulates a cluster of H hosts x S services. Every host owns one
+ * catalog view (the reference's `catalog.ServicesState`, catalog/services_state.go:70-80),
+ * its broadcast FIFO (the unbuffered `state.Broadcasts` channel with its blocked senders,
+ * services_state.go:94,377-392,579-604) and its memberlist delegate `pendingBroadcasts`
+ * (services_delegate.go:20-27). The whole-round driver `gx_run_rounds` advances the
+ * simulated cluster one 200 ms gossip round at a time (config/config.go:47).
+ *
+ * The per-host entry points keep the reference method set so a cgo (or ctypes) binding can
+ * expose the same `ServicesState` / `servicesDelegate` API; each declaration cites the
+ * reference function it replaces. See INTEGRATION.md for the cgo binding stub.
+ *
+ * Two implementations export this exact ABI:
+ *   sidecar_amd/libgx.so           the product: HIP kernels for gfx950 (MI355X)
+ *   oracle/liboracle_gx.so         the CPU restatement used ONLY by tests / bench cpu_baseline
+ *
+ * Conventions
+ *   - All buffers are caller-allocated host memory; the engine never retains a caller pointer
+ *     after a call returns (services_delegate.go:131-141 ownership hazard does not exist here).
+ *   - Return codes: 0 = OK, negative errno-style on failure (GX_EINVAL, GX_ENOMEM, GX_EIO,
+ *     GX_ENOSYS). No C++ exception crosses the ABI. Hot-path drops (stale records, full
+ *     queues) are never errors: they are counted in gx_stats (the reference logs and continues,
+ *     services_state.go:302-308, services_delegate.go:50-53).
+ *   - A handle is NOT thread-safe; callers serialise (the reference's sync.RWMutex,
+ *     services_state.go:79). Every call is synchronous at return.
+ *   - "now" is the simulated clock: t0_ns + round * round_ns.
+ */
+#ifndef SIDECAR_GX_H
+#define SIDECAR_GX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GX_ABI_VERSION 1
+
+#define GX_OK 0
+#define GX_EIO (-5)
+#define GX_ENOMEM (-12)
+#define GX_EINVAL (-22)
+#define GX_ENOSYS (-38)
+
+/* service.Service.Status values, service/service.go:17-23. GX_ABSENT marks an empty slot. */
+#define GX_ALIVE 0
+#define GX_TOMBSTONE 1
+#define GX_UNHEALTHY 2
+#define GX_UNKNOWN 3
+#define GX_DRAINING 4
+#define GX_ABSENT 7
+
+/* A view slot is one packed 64-bit word: (updated_ns << 3) | status.
+ * updated_ns must lie in [0, 2^61) (1970 .. 2043). The empty slot is the word GX_SLOT_ABSENT. */
+#define GX_TS_SHIFT 3
+#define GX_SLOT_ABSENT ((uint64_t)GX_ABSENT)
+#define GX_TS_LIMIT ((int64_t)1 << 61)
+
+/* Record across the ABI: the fields of service.Service (service/service.go:32-42) that the
+ * merge path reads. Hostname and ID strings are interned to (host, svc) indices by the caller;
+ * the record key is r = host * S + svc. */
+typedef struct gx_service {
+  int64_t updated_ns; /* Service.Updated, UTC nanoseconds */
+  uint32_t host;      /* Service.Hostname -> owner host index */
+  uint16_t svc;       /* Service.ID -> service index within the owner, < S */
+  uint8_t status;     /* Service.Status, 0..6 */
+  uint8_t flags;      /* reserved, 0 */
+} gx_service;
+
+/* Broadcast-queue job descriptor (read-back only, for parity checks).
+ *   kind NIL_BS / NIL_BT : the `Broadcasts <- nil` of an idle looper (services_state.go:569,628)
+ *   kind RETX            : retransmit of one accepted record (services_state.go:377-392);
+ *                          a = packed record word, c = record key r
+ *   kind SEND            : SendServices job (services_state.go:579-604); list in the host's
+ *                          list arena, c = slot | len << 16
+ *   kind EXPIRE          : SendServices job of ExpireServer (services_state.go:150-192);
+ *                          a = tombstone time ns, b = mask of tombstoned services, c = owner
+ * meta = kind | pass << 8 | n_passes << 16; wake = round the job re-enters the FIFO (sleepers). */
+#define GX_JOB_NIL_BS 0
+#define GX_JOB_NIL_BT 1
+#define GX_JOB_RETX 2
+#define GX_JOB_SEND 3
+#define GX_JOB_EXPIRE 4
+typedef struct gx_job {
+  uint64_t a;
+  uint64_t b;
+  uint32_t c;
+  uint32_t meta;
+  uint32_t wake;
+  uint32_t aux;
+} gx_job;
+
+/* Engine parameters. gx_params_default() fills the reference constants. */
+#define GX_INIT_EMPTY 0 /* no view knows anything; owners announce at their first tick */
+#define GX_INIT_OWN 1   /* each view holds only its own S records (ALIVE, ts = t0 - U[0,1s)) */
+#define GX_INIT_WARM 2  /* every view holds every record (a converged catalog) */
+typedef struct gx_params {
+  uint32_t n_hosts;                   /* H */
+  uint32_t n_services;                /* S, 1..64 */
+  uint32_t fanout;                    /* k: peers per gossip round (memberlist GossipNodes, LAN 3) */
+  uint32_t packet_cap;                /* records per GetBroadcasts packet (broadcast cap, 32) */
+  uint32_t pending_cap;               /* MAX_PENDING_LENGTH, services_delegate.go:17 (100) */
+  uint32_t queue_cap;                 /* Q: broadcast FIFO jobs per host (engine bound) */
+  uint32_t list_slots;                /* A: live SendServices lists per host (engine bound, <=32) */
+  uint32_t gossip_stop_on_empty;      /* memberlist gossip(): stop the round at the first empty packet */
+  uint32_t alive_interval_rounds;     /* ALIVE_SLEEP_INTERVAL 1s = 5 rounds (services_state.go:34) */
+  uint32_t tombstone_interval_rounds; /* TOMBSTONE_SLEEP_INTERVAL 2s = 10 rounds (:30) */
+  uint32_t retransmit_rounds;         /* TOMBSTONE_RETRANSMIT 1s = 5 rounds (:31) */
+  uint32_t alive_count;               /* ALIVE_COUNT 5 (:29) */
+  uint32_t tombstone_count;           /* TOMBSTONE_COUNT 10 (:28) */
+  uint32_t ae_period_rounds;          /* anti-entropy push-pull period, 0 = off */
+  uint32_t ae_phase;                  /* AE rounds are those with round % period == phase */
+  uint32_t init_mode;                 /* GX_INIT_* */
+  int64_t t0_ns;                      /* simulated clock at round 0 */
+  int64_t round_ns;                   /* GossipInterval 200ms (config/config.go:47) */
+  int64_t alive_lifespan_ns;          /* ALIVE_LIFESPAN 80s (:32) */
+  int64_t draining_lifespan_ns;       /* DRAINING_LIFESPAN 10min (:33) */
+  int64_t tombstone_lifespan_ns;      /* TOMBSTONE_LIFESPAN 3h (:27) */
+  int64_t stale_fudge_ns;             /* IsStale clock-drift fudge 1min (service/service.go:71) */
+  int64_t alive_broadcast_interval_ns;/* ALIVE_BROADCAST_INTERVAL 1min (:35) */
+  int64_t pass_increment_ns;          /* SendServices +50ns per pass (:599) */
+  int64_t tombstone_bump_ns;          /* expired records are tombstoned at Updated+1s (:675) */
+  uint64_t seed;                      /* schedule seed (peer sampling, phases, churn, AE pairing) */
+  uint32_t churn_ppm;                 /* per owner per round: probability (ppm) of one start/stop */
+  uint32_t aged_ppm;                  /* init: fraction (ppm) of records with age U[0, aged_max_ns) */
+  int64_t aged_max_ns;
+  int32_t partition_start;            /* rounds [start, end): two halves gossip only internally */
+  int32_t partition_end;
+  int32_t storm_round;                /* round at which every host ExpireServer()s the other half, -1 = none */
+  int32_t device;                     /* HIP device ordinal (ignored by the oracle) */
+} gx_params;
+
+/* Per-host bookkeeping (read-back for parity). */
+typedef struct gx_host_state {
+  uint32_t fifo_head, fifo_tail;   /* broadcast FIFO ring counters (count = tail - head) */
+  uint32_t sleep_head, sleep_tail; /* SendServices jobs sleeping TOMBSTONE_RETRANSMIT */
+  uint32_t dq_head, dq_len;        /* delegate pendingBroadcasts (dq_len <= pending_cap between calls) */
+  uint32_t arena_used;             /* bitmask of live SendServices lists */
+  uint32_t flags;                  /* bit0 BroadcastServices blocked on nil, bit1 BroadcastTombstones blocked */
+  int64_t bs_next;                 /* next BroadcastServices looper round */
+  int64_t bt_next;                 /* next BroadcastTombstones looper round */
+  int64_t last_bcast_ns;           /* BroadcastServices lastTime (services_state.go:526,560) */
+  uint64_t running;                /* owner's local services currently running (discovery) */
+} gx_host_state;
+
+typedef struct gx_stats {
+  int64_t round;             /* current round */
+  uint64_t gossip_merges;    /* AddServiceEntry evaluations from gossip packets */
+  uint64_t ae_merges;        /* ... from anti-entropy push-pull (Merge) */
+  uint64_t local_merges;     /* ... from owners (TrackNewServices) and API calls */
+  uint64_t gossip_accepts;
+  uint64_t ae_accepts;
+  uint64_t local_accepts;
+  uint64_t stale_drops;      /* IsStale gate, services_state.go:302-308 */
+  uint64_t retransmits;      /* RETX jobs enqueued */
+  uint64_t queue_drops;      /* jobs dropped because the FIFO was full (engine bound) */
+  uint64_t list_drops;       /* SendServices jobs dropped because the list arena was full */
+  uint64_t sleep_drops;      /* re-armed passes dropped because the sleep ring was full */
+  uint64_t pending_drops;    /* records cut by MAX_PENDING_LENGTH (services_delegate.go:111-112) */
+  uint64_t dequeues;         /* batches taken off the FIFO (nil included) */
+  uint64_t nil_batches;
+  uint64_t packets;          /* non-empty GetBroadcasts results */
+  uint64_t records_sent;
+  uint64_t expired;          /* records tombstoned by lifespan (services_state.go:655-679) */
+  uint64_t gc;               /* tombstones removed after TOMBSTONE_LIFESPAN (:645-653) */
+  uint64_t own_tombstones;   /* TombstoneServices (:685-715) */
+  uint64_t expire_server;    /* ExpireServer calls that tombstoned something (:150-192) */
+  uint64_t send_jobs;        /* SendServices jobs created */
+  uint64_t ae_exchanges;     /* push-pull pairs */
+  uint64_t churn_events;
+  int64_t last_change_round; /* last round in which any view slot changed, -1 = none */
+  uint64_t reserved[7];
+} gx_stats;
+
+/* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */
+#define GX_K_OWNER 0
+#define GX_K_SCAN 1
+#define GX_K_STORM 2
+#define GX_K_SEND 3
+#define GX_K_ROUTE 4
+#define GX_K_MERGE 5
+#define GX_K_AE 6
+#define GX_K_CONVERGE 7
+#define GX_K_COUNT 8
+typedef struct gx_timing {
+  double ms[GX_K_COUNT];
+  uint64_t launches[GX_K_COUNT];
+  uint64_t bytes[GX_K_COUNT]; /* algorithmic bytes moved ("Algorithmic bytes") */
+  uint64_t units[GX_K_COUNT]; /* slots / records processed */
+} gx_timing;
+
+typedef struct gx_engine gx_engine;
+
+/* ---- lifecycle --------------------------------------------------------------------------- */
+int gx_abi_version(void);
+const char *gx_backend(void);               /* "hip-gfx950" or "oracle-cpu" */
+void gx_params_default(gx_params *p);
+int gx_create(const gx_params *p, gx_engine **out);
+int gx_destroy(gx_engine *e);
+int gx_set_round(gx_engine *e, int64_t round); /* advance the clock; wakes due sleepers */
+int gx_get_round(gx_engine *e, int64_t *round);
+int gx_enable_timing(gx_engine *e, int on);
+
+/* ---- whole-round driver (the hot path) ---------------------------------------------------- */
+/* Runs n_rounds rounds of the seeded schedule (DESIGN.md "Round model"). */
+int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
+
+/* ---- catalog.ServicesState ---------------------------------------------------------------- */
+/* AddServiceEntry, services_state.go:293-347, applied in array order (views[i] <- svcs[i]). */
+int gx_add_service_entries(gx_engine *e, const uint32_t *views, const gx_service *svcs,
+                           uint32_t n, uint32_t *n_accepted);
+/* Merge(otherState), services_state.go:367-373: every present record of src_view -> dst_view. */
+int gx_merge(gx_engine *e, uint32_t dst_view, uint32_t src_view);
+/* TombstoneOthersServices, services_state.go:635-683. Returns the tombstoned records in key
+ * order; n_out = total count (may exceed cap; excess not written). */
+int gx_tombstone_others(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap,
+                        uint32_t *n_out);
+/* TombstoneServices(self, containerList), services_state.go:685-715: own services not in
+ * `running` are tombstoned (each returned twice). */
+int gx_tombstone_services(gx_engine *e, uint32_t host, const uint16_t *running, uint32_t n_running,
+                          gx_service *out, uint32_t cap, uint32_t *n_out);
+/* ExpireServer(hostname), services_state.go:150-192 (incl. SendServices(TOMBSTONE_COUNT)). */
+int gx_expire_server(gx_engine *e, uint32_t view, uint32_t owner, int *expired);
+/* SendServices(services, looper(n_passes)), services_state.go:579-604. */
+int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32_t n,
+                     uint32_t n_passes);
+/* One BroadcastServices looper body with fn() = list, services_state.go:525-574. */
+int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n);
+/* One BroadcastTombstones looper body with fn() = list, services_state.go:606-633. */
+int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n);
+/* IsNewService, services_state.go:509-521. */
+int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *is_new);
+
+/* ---- memberlist Delegate (services_delegate.go) ------------------------------------------- */
+/* NotifyMsg (:72-83) + Start() decode loop (:46-56): the records of one packet -> UpdateService. */
+int gx_notify_msg(gx_engine *e, uint32_t host, const gx_service *recs, uint32_t n);
+/* GetBroadcasts(overhead, limit) (:85-144) with packPacket (:186-223). `limit` is the packet
+ * budget in records (the caller converts memberlist's byte limit and per-message overhead);
+ * GX_LIMIT_DEFAULT = params.packet_cap. 0 means nothing fits (the whole batch stays pending).
+ * n_out = 0 means the reference returned nil. cap must be >= the effective limit. */
+#define GX_LIMIT_DEFAULT 0xffffffffu
+int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *out, uint32_t cap,
+                      uint32_t *n_out);
+/* LocalState (:146-151): present records of the view in key order (n_out = total). */
+int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out);
+/* MergeRemoteState (:153-167): a decoded remote state -> Merge. */
+int gx_merge_remote_state(gx_engine *e, uint32_t view, const gx_service *svcs, uint32_t n);
+/* NotifyLeave (:173-176) -> ExpireServer(node). */
+int gx_notify_leave(gx_engine *e, uint32_t view, uint32_t node);
+
+/* ---- read-back, import, parity ------------------------------------------------------------ */
+int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);
+int gx_write_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, const uint64_t *words);
+int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc); /* raw store, no merge rule */
+int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out);
+int gx_read_queue(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out);
+int gx_read_sleepers(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out);
+int gx_read_pending(gx_engine *e, uint32_t host, gx_service *out, uint32_t cap, uint32_t *n_out);
+int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, uint32_t cap,
+                 uint32_t *n_out);
+/* Order-sensitive 64-bit digest per host of (FIFO jobs, sleepers, pending, live lists). */
+int gx_host_digests(gx_engine *e, uint64_t *out_per_host);
+int gx_stats_get(gx_engine *e, gx_stats *out);
+int gx_timing_get(gx_engine *e, gx_timing *out);
+/* Catalog agreement: n_disagree = records r whose slot word differs between any two views. */
+int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIDECAR_GX_H */

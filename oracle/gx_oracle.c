@@ -1,0 +1,1078 @@
+/*
+ * gx_oracle.c — CPU ORACLE for the sidecar-gx engine. TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is a sequential, plain-C restatement of the reference Go semantics of Sidecar's
+ * catalog merge path under the engine's seeded round model (DESIGN.md "Round model"). It
+ * exports the same C-ABI as the product (include/gx.h) so tests can drive both with the same
+ * calls and compare results bit for bit. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product (sidecar_amd/libgx.so) never links or calls it.
+ *
+ * Parity pinning: the reference (Go, un-vendored deps, no Go toolchain here — SURVEY.md §8c)
+ * cannot be built or run, so this restatement is pinned by the reference's own known-answer
+ * tests, restated in tests/test_oracle_kat.py (services_state_test.go, services_delegate_test.go,
+ * service/service_test.go), plus golden round-model fixtures generated from this file.
+ * Memberlist fork semantics (peer sampling, push-pull pairing) are defined by the seeded
+ * schedule and are "parity unpinned" (SURVEY.md §8c).
+ */
+#include "../include/gx.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct grec {
+  uint64_t w; /* packed (ts << 3) | status */
+  uint32_t r; /* record key owner * S + svc */
+  uint32_t pad;
+} grec;
+
+enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
+enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5,
+       ST_INIT_AGE = 6, ST_AE = 7 };
+
+struct gx_engine {
+  gx_params p;
+  uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  int64_t round;
+  uint64_t *view;       /* H * R packed slots */
+  uint8_t *own_status;  /* H * S local service status (discovery/health) */
+  gx_host_state *hs;    /* H */
+  gx_job *fifo;         /* H * Q */
+  gx_job *sleep;        /* H * SQ */
+  grec *dq;             /* H * DQ  delegate pendingBroadcasts deque */
+  grec *arena;          /* H * A * L SendServices lists */
+  uint32_t *arena_len;  /* H * A */
+  grec *msg;            /* H * K * packet_cap  this round's packets */
+  uint32_t *msg_len;    /* H * K */
+  uint32_t *msg_dst;    /* H * K */
+  uint32_t *in_cnt;     /* H + 1 */
+  uint32_t *in_list;    /* H * K  (sender * K + j), grouped by receiver, sender-ascending */
+  gx_stats st;
+};
+
+/* ---------------------------------------------------------------- helpers / schedule RNG -- */
+static inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static inline uint64_t rng4(uint64_t seed, uint64_t stream, uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t h = mix64(seed ^ (stream * 0xD1B54A32D192ED03ull));
+  h = mix64(h ^ a);
+  h = mix64(h ^ b);
+  return mix64(h ^ c);
+}
+static inline uint32_t unif(uint64_t x, uint32_t m) { /* uniform in [0, m) */
+  return (uint32_t)(((x >> 32) * (uint64_t)m) >> 32);
+}
+static inline int st_of(uint64_t w) { return (int)(w & 7u); }
+static inline int64_t ts_of(uint64_t w) { return (int64_t)(w >> GX_TS_SHIFT); }
+static inline uint64_t pack(int64_t ts, int st) { return ((uint64_t)ts << GX_TS_SHIFT) | (uint64_t)st; }
+static inline int64_t now_of(const gx_engine *e) { return e->p.t0_ns + e->round * e->p.round_ns; }
+static inline uint32_t meta_of(int kind, uint32_t pass, uint32_t np) {
+  return (uint32_t)kind | (pass << 8) | (np << 16);
+}
+static uint32_t pow2_at_least(uint32_t x) {
+  uint32_t v = 1;
+  while (v < x) v <<= 1;
+  return v;
+}
+
+static inline void set_slot(gx_engine *e, uint64_t *slot, uint64_t nw) {
+  if (*slot != nw) {
+    *slot = nw;
+    e->st.last_change_round = e->round;
+  }
+}
+
+/* ------------------------------------------------------------------------ broadcast FIFO -- */
+static void free_list(gx_engine *e, uint32_t v, const gx_job *j) {
+  if ((j->meta & 0xff) == GX_JOB_SEND) e->hs[v].arena_used &= ~(1u << (j->c & 0xffff));
+}
+
+/* Blocked senders on the unbuffered Broadcasts channel (services_state.go:94) form a FIFO.
+ * Engine bound: at most Q jobs; two slots are reserved for the loopers' nil sends so a looper
+ * can never be blocked forever. */
+static int push_job(gx_engine *e, uint32_t v, const gx_job *j) {
+  gx_host_state *h = &e->hs[v];
+  uint32_t count = h->fifo_tail - h->fifo_head;
+  int is_nil = (j->meta & 0xff) <= GX_JOB_NIL_BT;
+  uint32_t limit = is_nil ? e->Q : e->Q - 2;
+  if (count >= limit) {
+    e->st.queue_drops++;
+    free_list(e, v, j);
+    return 0;
+  }
+  e->fifo[(size_t)v * e->Q + (h->fifo_tail % e->Q)] = *j;
+  h->fifo_tail++;
+  return 1;
+}
+
+static void push_sleep(gx_engine *e, uint32_t v, const gx_job *j) {
+  gx_host_state *h = &e->hs[v];
+  if (h->sleep_tail - h->sleep_head >= e->SQ) {
+    e->st.sleep_drops++;
+    free_list(e, v, j);
+    return;
+  }
+  e->sleep[(size_t)v * e->SQ + (h->sleep_tail % e->SQ)] = *j;
+  h->sleep_tail++;
+}
+
+/* TimedLooper re-arm: a SendServices pass sleeps TOMBSTONE_RETRANSMIT after its send
+ * completes (services_state.go:585-601), then blocks on the channel again (FIFO tail). */
+static void wake_host(gx_engine *e, uint32_t v) {
+  gx_host_state *h = &e->hs[v];
+  while (h->sleep_head != h->sleep_tail) {
+    gx_job *j = &e->sleep[(size_t)v * e->SQ + (h->sleep_head % e->SQ)];
+    if ((int64_t)j->wake > e->round) break;
+    gx_job cp = *j;
+    h->sleep_head++;
+    push_job(e, v, &cp);
+  }
+}
+
+/* SendServices(services, looper(n)), services_state.go:579-604. The list is copied at call
+ * time. Only its first packet_cap + pending_cap records can ever leave a GetBroadcasts call
+ * (services_delegate.go:104-115), so the stored list is truncated to that length. */
+static int create_send(gx_engine *e, uint32_t v, const grec *list, uint32_t n, uint32_t npasses) {
+  gx_host_state *h = &e->hs[v];
+  uint32_t slot = 0;
+  while (slot < e->A && (h->arena_used >> slot) & 1u) slot++;
+  if (slot >= e->A) {
+    e->st.list_drops++;
+    return 0;
+  }
+  if (n > e->L) n = e->L;
+  h->arena_used |= 1u << slot;
+  grec *dst = &e->arena[((size_t)v * e->A + slot) * e->L];
+  for (uint32_t i = 0; i < n; i++) dst[i] = list[i];
+  e->arena_len[(size_t)v * e->A + slot] = n;
+  gx_job j = {0, 0, slot | (n << 16), meta_of(GX_JOB_SEND, 0, npasses), 0, 0};
+  e->st.send_jobs++;
+  return push_job(e, v, &j);
+}
+
+/* Records of pass `pass` of a job: Updated + pass * 50ns (services_state.go:588-599). */
+static uint32_t expand(const gx_engine *e, uint32_t v, const gx_job *j, grec *out) {
+  uint32_t kind = j->meta & 0xff, pass = (j->meta >> 8) & 0xff;
+  uint64_t dw = ((uint64_t)pass * (uint64_t)e->p.pass_increment_ns) << GX_TS_SHIFT;
+  uint32_t n = 0;
+  if (kind == GX_JOB_RETX) {
+    out[0].w = j->a;
+    out[0].r = j->c;
+    out[0].pad = 0;
+    n = 1;
+  } else if (kind == GX_JOB_SEND) {
+    uint32_t slot = j->c & 0xffff, len = j->c >> 16;
+    const grec *src = &e->arena[((size_t)v * e->A + slot) * e->L];
+    for (uint32_t i = 0; i < len; i++) {
+      out[i].w = src[i].w + dw;
+      out[i].r = src[i].r;
+      out[i].pad = 0;
+    }
+    n = len;
+  } else if (kind == GX_JOB_EXPIRE) {
+    uint64_t w = pack((int64_t)j->a, GX_TOMBSTONE) + dw;
+    for (uint32_t s = 0; s < e->S; s++)
+      if ((j->b >> s) & 1ull) {
+        out[n].w = w;
+        out[n].r = j->c * e->S + s;
+        out[n].pad = 0;
+        n++;
+      }
+  }
+  return n;
+}
+
+/* GetBroadcasts(overhead, limit), services_delegate.go:85-144, with packPacket (:186-223)
+ * under a record-count limit. Returns the packet length (0 = nil). */
+static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *packet) {
+  gx_host_state *h = &e->hs[v];
+  grec batch[512];
+  uint32_t m = 0;
+  if (h->fifo_head != h->fifo_tail) { /* case broadcast = <-d.state.Broadcasts (:94) */
+    gx_job j = e->fifo[(size_t)v * e->Q + (h->fifo_head % e->Q)];
+    h->fifo_head++;
+    e->st.dequeues++;
+    m = expand(e, v, &j, batch);
+    uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff, np = (j.meta >> 16) & 0xff;
+    if (kind == GX_JOB_NIL_BS) { /* BroadcastServices looper unblocks (:569) */
+      e->st.nil_batches++;
+      h->flags &= ~1u;
+      h->bs_next = e->round + e->p.alive_interval_rounds;
+    } else if (kind == GX_JOB_NIL_BT) { /* BroadcastTombstones looper unblocks (:628) */
+      e->st.nil_batches++;
+      h->flags &= ~2u;
+      h->bt_next = e->round + e->p.tombstone_interval_rounds;
+    } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
+      if (pass + 1 < np) {
+        j.meta = meta_of((int)kind, pass + 1, np);
+        if (e->p.retransmit_rounds == 0) {
+          j.wake = (uint32_t)e->round;
+          push_job(e, v, &j);
+        } else {
+          j.wake = (uint32_t)(e->round + e->p.retransmit_rounds);
+          push_sleep(e, v, &j);
+        }
+      } else {
+        free_list(e, v, &j);
+      }
+    }
+  } else if (h->dq_len == 0) { /* default: nothing pending (:96-98) */
+    return 0;
+  }
+  /* broadcast = batch ++ pendingBroadcasts (:104-106): push the batch to the deque front */
+  uint32_t mask = e->DQ - 1;
+  grec *dq = &e->dq[(size_t)v * e->DQ];
+  h->dq_head = (h->dq_head - m) & mask;
+  for (uint32_t i = 0; i < m; i++) dq[(h->dq_head + i) & mask] = batch[i];
+  h->dq_len += m;
+  /* packPacket: greedy prefix within the limit (:186-223) */
+  uint32_t l = h->dq_len < limit ? h->dq_len : limit;
+  for (uint32_t i = 0; i < l; i++) packet[i] = dq[(h->dq_head + i) & mask];
+  h->dq_head = (h->dq_head + l) & mask;
+  h->dq_len -= l;
+  /* pendingBroadcasts = leftover[:MAX_PENDING_LENGTH] (:109-120) */
+  if (h->dq_len > e->p.pending_cap) {
+    e->st.pending_drops += h->dq_len - e->p.pending_cap;
+    h->dq_len = e->p.pending_cap;
+  }
+  if (l) {
+    e->st.packets++;
+    e->st.records_sent += l;
+  }
+  return l;
+}
+
+/* ---------------------------------------------------------------------- catalog semantics -- */
+/* AddServiceEntry, catalog/services_state.go:293-347 (+ IsStale service/service.go:68-72,
+ * Invalidates :64-66, retransmit :377-392). */
+static int add_entry(gx_engine *e, uint32_t v, grec u, int64_t now, int src) {
+  int64_t ts = ts_of(u.w);
+  if (src == SRC_GOSSIP) e->st.gossip_merges++;
+  else if (src == SRC_AE) e->st.ae_merges++;
+  else e->st.local_merges++;
+  if (ts < now - e->p.tombstone_lifespan_ns - e->p.stale_fudge_ns) { /* IsStale: drop (:302-308) */
+    e->st.stale_drops++;
+    return 0;
+  }
+  uint64_t *slot = &e->view[(size_t)v * e->R + u.r];
+  uint64_t old = *slot, nw;
+  if (st_of(old) == GX_ABSENT) { /* !server.HasService: insert (:317-320) */
+    nw = u.w;
+  } else if (ts > ts_of(old)) { /* Invalidates: strictly newer (:321) */
+    int st = st_of(u.w);
+    if (st_of(old) == GX_DRAINING && st == GX_ALIVE) st = GX_DRAINING; /* (:329-331) */
+    nw = pack(ts, st);
+  } else {
+    return 0; /* equal or older: keep the first arrival */
+  }
+  set_slot(e, slot, nw);
+  if (src == SRC_GOSSIP) e->st.gossip_accepts++;
+  else if (src == SRC_AE) e->st.ae_accepts++;
+  else e->st.local_accepts++;
+  if (u.r / e->S != v) { /* retransmit only foreign records (:380-382) */
+    gx_job j = {nw, 0, u.r, meta_of(GX_JOB_RETX, 0, 1), 0, 0};
+    if (push_job(e, v, &j)) e->st.retransmits++;
+  }
+  return 1;
+}
+
+/* TombstoneOthersServices, services_state.go:635-683. Key order replaces Go map order.
+ * Writes the first `cap` tombstoned records to out; returns the total. */
+static uint32_t scan_view(gx_engine *e, uint32_t v, int64_t now, grec *out, uint32_t cap) {
+  uint32_t n = 0;
+  uint64_t *row = &e->view[(size_t)v * e->R];
+  for (uint32_t r = 0; r < e->R; r++) {
+    uint64_t w = row[r];
+    int st = st_of(w);
+    if (st == GX_ABSENT) continue;
+    int64_t ts = ts_of(w);
+    if (st == GX_TOMBSTONE) {
+      if (ts < now - e->p.tombstone_lifespan_ns) { /* (:645-653) */
+        set_slot(e, &row[r], GX_SLOT_ABSENT);
+        e->st.gc++;
+      }
+    } else {
+      int64_t life = st == GX_DRAINING ? e->p.draining_lifespan_ns : e->p.alive_lifespan_ns;
+      if (ts < now - life) { /* (:655-679): TOMBSTONE at Updated + 1s */
+        uint64_t nw = pack(ts + e->p.tombstone_bump_ns, GX_TOMBSTONE);
+        set_slot(e, &row[r], nw);
+        e->st.expired++;
+        if (n < cap) {
+          out[n].w = nw;
+          out[n].r = r;
+          out[n].pad = 0;
+        }
+        n++;
+      }
+    }
+  }
+  return n;
+}
+
+/* TombstoneServices(self, containerList), services_state.go:685-715. */
+static uint32_t tombstone_services(gx_engine *e, uint32_t o, uint64_t running, int64_t now,
+                                   grec *out, uint32_t cap) {
+  uint32_t n = 0;
+  uint64_t *row = &e->view[(size_t)o * e->R];
+  for (uint32_t s = 0; s < e->S; s++) {
+    uint32_t r = o * e->S + s;
+    uint64_t w = row[r];
+    if (st_of(w) == GX_ABSENT || ((running >> s) & 1ull) || st_of(w) == GX_TOMBSTONE) continue;
+    uint64_t nw = pack(now, GX_TOMBSTONE); /* svc.Tombstone(): Updated = now (service.go:91-94) */
+    set_slot(e, &row[r], nw);
+    e->st.own_tombstones++;
+    for (int k = 0; k < 2; k++) { /* appended twice (:707-710) */
+      if (n < cap) {
+        out[n].w = nw;
+        out[n].r = r;
+        out[n].pad = 0;
+      }
+      n++;
+    }
+  }
+  return n;
+}
+
+/* ExpireServer(hostname), services_state.go:150-192. */
+static int expire_server(gx_engine *e, uint32_t v, uint32_t o, int64_t now) {
+  uint64_t *row = &e->view[(size_t)v * e->R + (size_t)o * e->S];
+  uint64_t mask = 0;
+  int live = 0;
+  for (uint32_t s = 0; s < e->S; s++) {
+    int st = st_of(row[s]);
+    if (st == GX_ABSENT) continue;
+    mask |= 1ull << s;
+    if (st != GX_TOMBSTONE) live = 1;
+  }
+  if (!live) return 0; /* no server / no services / no live services (:154-170) */
+  for (uint32_t s = 0; s < e->S; s++)
+    if ((mask >> s) & 1ull) set_slot(e, &row[s], pack(now, GX_TOMBSTONE)); /* (:176-181) */
+  e->st.expire_server++;
+  gx_job j = {(uint64_t)now, mask, o, meta_of(GX_JOB_EXPIRE, 0, e->p.tombstone_count), 0, 0};
+  push_job(e, v, &j); /* SendServices(tombstones, TOMBSTONE_COUNT) (:188-191) */
+  return 1;
+}
+
+/* IsNewService, services_state.go:509-521. */
+static int is_new(const gx_engine *e, uint32_t o, grec s) {
+  uint64_t w = e->view[(size_t)o * e->R + s.r];
+  return st_of(w) == GX_ABSENT || (st_of(s.w) != GX_TOMBSTONE && st_of(s.w) != st_of(w));
+}
+
+/* BroadcastServices looper body, services_state.go:525-574. Returns the number of records
+ * handed to SendServices (written to inc), or 0 after a nil send. */
+static uint32_t bs_body(gx_engine *e, uint32_t o, const grec *list, uint32_t n, int64_t now,
+                        grec *inc) {
+  gx_host_state *h = &e->hs[o];
+  int refresh = (now - e->p.alive_broadcast_interval_ns) > h->last_bcast_ns; /* (:547) */
+  int any_new = 0;
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (is_new(e, o, list[i])) {
+      any_new = 1;
+      inc[m++] = list[i];
+    } else if (refresh) {
+      inc[m++] = list[i];
+    }
+  }
+  if (m) {
+    h->last_bcast_ns = now;
+    create_send(e, o, inc, m, any_new ? e->p.alive_count : 1);
+  } else {
+    gx_job j = {0, 0, 0, meta_of(GX_JOB_NIL_BS, 0, 1), 0, 0};
+    push_job(e, o, &j);
+    h->flags |= 1u;
+  }
+  return m;
+}
+
+/* ---------------------------------------------------------------------------- round model -- */
+static void bt_tick(gx_engine *e, uint32_t o, int64_t now) {
+  gx_host_state *h = &e->hs[o];
+  grec *others = (grec *)malloc(sizeof(grec) * (e->L + 1));
+  grec *list = (grec *)malloc(sizeof(grec) * (e->L + 2 * 64 + 1));
+  uint32_t n_others = scan_view(e, o, now, others, e->L);         /* (:615) */
+  uint32_t n_own = tombstone_services(e, o, h->running, now, list, 2 * 64); /* (:616) */
+  uint32_t n = n_own;
+  uint32_t keep_o = n_others < e->L ? n_others : e->L;
+  for (uint32_t i = 0; i < keep_o; i++) list[n++] = others[i]; /* tombstones ++ others (:618) */
+  if (n_own + n_others > 0) {
+    create_send(e, o, list, n > e->L ? e->L : n, e->p.tombstone_count); /* (:620-624) */
+    h->bt_next = e->round + e->p.tombstone_interval_rounds;
+  } else {
+    gx_job j = {0, 0, 0, meta_of(GX_JOB_NIL_BT, 0, 1), 0, 0};
+    push_job(e, o, &j);
+    h->flags |= 2u;
+  }
+  free(others);
+  free(list);
+}
+
+static void bs_tick(gx_engine *e, uint32_t o, int64_t now) {
+  gx_host_state *h = &e->hs[o];
+  grec list[64], inc[64];
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < e->S; s++)
+    if ((h->running >> s) & 1ull) { /* fn(): local services, restamped by discovery */
+      list[n].w = pack(now, e->own_status[(size_t)o * e->S + s]);
+      list[n].r = o * e->S + s;
+      list[n].pad = 0;
+      n++;
+    }
+  uint32_t m = bs_body(e, o, list, n, now, inc);
+  if (m) {
+    h->bs_next = e->round + e->p.alive_interval_rounds;
+    for (uint32_t i = 0; i < m; i++) add_entry(e, o, inc[i], now, SRC_LOCAL); /* TrackNewServices */
+  }
+}
+
+static void churn(gx_engine *e, uint32_t o) {
+  if (!e->p.churn_ppm) return;
+  uint64_t x = rng4(e->p.seed, ST_CHURN, (uint64_t)e->round, o, 0);
+  if ((uint32_t)(x & 0xffffffffu) % 1000000u >= e->p.churn_ppm) return;
+  uint32_t s = (uint32_t)((x >> 32) % e->S);
+  e->hs[o].running ^= 1ull << s;
+  if ((e->hs[o].running >> s) & 1ull) e->own_status[(size_t)o * e->S + s] = GX_ALIVE;
+  e->st.churn_events++;
+}
+
+static int partitioned(const gx_engine *e) {
+  return e->round >= e->p.partition_start && e->round < e->p.partition_end;
+}
+
+static void side_of(const gx_engine *e, uint32_t u, uint32_t *base, uint32_t *m) {
+  if (partitioned(e)) {
+    uint32_t half = e->H / 2;
+    if (u < half) { *base = 0; *m = half; }
+    else { *base = half; *m = e->H - half; }
+  } else {
+    *base = 0;
+    *m = e->H;
+  }
+}
+
+/* Peer selection (memberlist kRandomNodes, external; schedule-defined): k distinct peers != u
+ * within u's side. Returns the count. */
+static uint32_t sample_peers(const gx_engine *e, uint32_t u, uint32_t *peers) {
+  uint32_t base, m;
+  side_of(e, u, &base, &m);
+  if (m < 2) return 0;
+  uint32_t want = e->K < m - 1 ? e->K : m - 1, cnt = 0;
+  for (uint32_t a = 0; cnt < want && a < 64u * e->K; a++) {
+    uint64_t x = rng4(e->p.seed, ST_PEER, (uint64_t)e->round, u, a);
+    uint32_t idx = unif(x, m - 1), self = u - base;
+    uint32_t p = base + (idx >= self ? idx + 1 : idx);
+    int dup = 0;
+    for (uint32_t i = 0; i < cnt; i++) dup |= peers[i] == p;
+    if (!dup) peers[cnt++] = p;
+  }
+  return cnt;
+}
+
+/* Push-pull pairing: a keyed Feistel bijection on [0, m) (cycle walking) pairs positions
+ * (2t, 2t+1). memberlist's push-pull partner choice is external and unpinned. */
+static uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
+  uint32_t b = 0;
+  while ((1u << b) < m) b++;
+  uint32_t hb = (b + 1) / 2;
+  if (hb == 0) hb = 1;
+  uint32_t hmask = (1u << hb) - 1;
+  uint32_t x = q;
+  do {
+    uint32_t L = x >> hb, Rr = x & hmask;
+    for (uint32_t i = 0; i < 4; i++) {
+      uint32_t F = (uint32_t)(mix64(key ^ ((uint64_t)i << 32) ^ Rr)) & hmask;
+      uint32_t t = Rr;
+      Rr = L ^ F;
+      L = t;
+    }
+    x = (L << hb) | Rr;
+  } while (x >= m);
+  return x;
+}
+
+static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
+  uint64_t *sa = (uint64_t *)malloc(sizeof(uint64_t) * e->R);
+  memcpy(sa, &e->view[(size_t)a * e->R], sizeof(uint64_t) * e->R);
+  const uint64_t *vb = &e->view[(size_t)b * e->R];
+  for (uint32_t r = 0; r < e->R; r++) { /* a.Merge(b's state) (:367-373) */
+    if (st_of(vb[r]) == GX_ABSENT) continue;
+    grec u = {vb[r], r, 0};
+    add_entry(e, a, u, now, SRC_AE);
+  }
+  for (uint32_t r = 0; r < e->R; r++) { /* b.Merge(a's state snapshot) */
+    if (st_of(sa[r]) == GX_ABSENT) continue;
+    grec u = {sa[r], r, 0};
+    add_entry(e, b, u, now, SRC_AE);
+  }
+  e->st.ae_exchanges++;
+  free(sa);
+}
+
+static void ae_phase(gx_engine *e, int64_t now) {
+  uint32_t groups[2][2];
+  int ng;
+  if (partitioned(e)) {
+    groups[0][0] = 0; groups[0][1] = e->H / 2;
+    groups[1][0] = e->H / 2; groups[1][1] = e->H - e->H / 2;
+    ng = 2;
+  } else {
+    groups[0][0] = 0; groups[0][1] = e->H;
+    ng = 1;
+  }
+  for (int g = 0; g < ng; g++) {
+    uint32_t base = groups[g][0], m = groups[g][1];
+    uint64_t key = rng4(e->p.seed, ST_AE, (uint64_t)e->round, base, 0);
+    for (uint32_t t = 0; t + 1 < m; t += 2) {
+      uint32_t a = base + feistel_perm(key, t, m), b = base + feistel_perm(key, t + 1, m);
+      ae_exchange(e, a, b, now);
+    }
+  }
+}
+
+static void run_one_round(gx_engine *e) {
+  int64_t now = now_of(e);
+  uint32_t H = e->H, K = e->K, cap = e->p.packet_cap;
+  for (uint32_t v = 0; v < H; v++) wake_host(e, v);
+  /* owners: discovery churn, BroadcastServices(+TrackNewServices), BroadcastTombstones */
+  for (uint32_t o = 0; o < H; o++) {
+    churn(e, o);
+    gx_host_state *h = &e->hs[o];
+    if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
+    if (!(h->flags & 2u) && h->bt_next <= e->round) bt_tick(e, o, now);
+  }
+  /* SWIM departure storm: NotifyLeave -> ExpireServer for every host of the other half */
+  if (e->p.storm_round >= 0 && e->round == e->p.storm_round) {
+    uint32_t half = H / 2;
+    for (uint32_t v = 0; v < H; v++) {
+      uint32_t lo = v < half ? half : 0, hi = v < half ? H : half;
+      for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
+    }
+  }
+  /* gossip send: GetBroadcasts once per selected peer */
+  for (uint32_t u = 0; u < H; u++) {
+    uint32_t peers[64];
+    uint32_t np = sample_peers(e, u, peers);
+    for (uint32_t j = 0; j < K; j++) {
+      e->msg_len[(size_t)u * K + j] = 0;
+      e->msg_dst[(size_t)u * K + j] = 0xffffffffu;
+    }
+    for (uint32_t j = 0; j < np; j++) {
+      uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap]);
+      e->msg_len[(size_t)u * K + j] = l;
+      e->msg_dst[(size_t)u * K + j] = peers[j];
+      if (l == 0 && e->p.gossip_stop_on_empty) break;
+    }
+  }
+  /* gossip receive: packets to v in sender order -> NotifyMsg -> AddServiceEntry */
+  memset(e->in_cnt, 0, sizeof(uint32_t) * (H + 1));
+  for (uint32_t u = 0; u < H; u++)
+    for (uint32_t j = 0; j < K; j++)
+      if (e->msg_len[(size_t)u * K + j]) e->in_cnt[e->msg_dst[(size_t)u * K + j] + 1]++;
+  for (uint32_t v = 0; v < H; v++) e->in_cnt[v + 1] += e->in_cnt[v];
+  uint32_t *cur = (uint32_t *)malloc(sizeof(uint32_t) * H);
+  memcpy(cur, e->in_cnt, sizeof(uint32_t) * H);
+  for (uint32_t u = 0; u < H; u++)
+    for (uint32_t j = 0; j < K; j++)
+      if (e->msg_len[(size_t)u * K + j]) e->in_list[cur[e->msg_dst[(size_t)u * K + j]]++] = u * K + j;
+  free(cur);
+  for (uint32_t v = 0; v < H; v++)
+    for (uint32_t i = e->in_cnt[v]; i < e->in_cnt[v + 1]; i++) {
+      uint32_t m = e->in_list[i];
+      for (uint32_t x = 0; x < e->msg_len[m]; x++) add_entry(e, v, e->msg[(size_t)m * cap + x], now, SRC_GOSSIP);
+    }
+  /* anti-entropy push-pull */
+  if (e->p.ae_period_rounds && (uint64_t)e->round % e->p.ae_period_rounds == e->p.ae_phase) ae_phase(e, now);
+  e->round++;
+  e->st.round = e->round;
+  for (uint32_t v = 0; v < H; v++) wake_host(e, v);
+}
+
+/* ---------------------------------------------------------------------------- ABI ------- */
+int gx_abi_version(void) { return GX_ABI_VERSION; }
+const char *gx_backend(void) { return "oracle-cpu"; }
+
+void gx_params_default(gx_params *p) {
+  memset(p, 0, sizeof(*p));
+  p->n_hosts = 64;
+  p->n_services = 8;
+  p->fanout = 3;
+  p->packet_cap = 32;
+  p->pending_cap = 100;
+  p->queue_cap = 1024;
+  p->list_slots = 16;
+  p->gossip_stop_on_empty = 1;
+  p->alive_interval_rounds = 5;
+  p->tombstone_interval_rounds = 10;
+  p->retransmit_rounds = 5;
+  p->alive_count = 5;
+  p->tombstone_count = 10;
+  p->ae_period_rounds = 0;
+  p->ae_phase = 0;
+  p->init_mode = GX_INIT_EMPTY;
+  p->t0_ns = 1700000000000000000ll;
+  p->round_ns = 200000000ll;
+  p->alive_lifespan_ns = 80000000000ll;
+  p->draining_lifespan_ns = 600000000000ll;
+  p->tombstone_lifespan_ns = 10800000000000ll;
+  p->stale_fudge_ns = 60000000000ll;
+  p->alive_broadcast_interval_ns = 60000000000ll;
+  p->pass_increment_ns = 50;
+  p->tombstone_bump_ns = 1000000000ll;
+  p->seed = 0x5EEDull;
+  p->churn_ppm = 0;
+  p->aged_ppm = 0;
+  p->aged_max_ns = 100000000000ll;
+  p->partition_start = 0;
+  p->partition_end = 0;
+  p->storm_round = -1;
+  p->device = 0;
+}
+
+static int check_params(const gx_params *p) {
+  if (!p || p->n_hosts < 1 || p->n_services < 1 || p->n_services > 64) return GX_EINVAL;
+  if (p->fanout > 16 || p->packet_cap < 1 || p->packet_cap > 256 || p->pending_cap > 256) return GX_EINVAL;
+  if (p->queue_cap < 3 || p->list_slots < 1 || p->list_slots > 32) return GX_EINVAL;
+  if (p->alive_interval_rounds < 1 || p->tombstone_interval_rounds < 1) return GX_EINVAL;
+  if (p->retransmit_rounds > 1000) return GX_EINVAL;
+  if (p->alive_count < 1 || p->alive_count > 255 || p->tombstone_count < 1 || p->tombstone_count > 255) return GX_EINVAL;
+  if (p->init_mode > GX_INIT_WARM) return GX_EINVAL;
+  if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
+  if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
+  if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
+  return GX_OK;
+}
+
+static void init_state(gx_engine *e) {
+  const gx_params *p = &e->p;
+  uint32_t H = e->H, S = e->S, R = e->R;
+  for (size_t i = 0; i < (size_t)H * R; i++) e->view[i] = GX_SLOT_ABSENT;
+  for (uint32_t r = 0; r < R && p->init_mode != GX_INIT_EMPTY; r++) {
+    int64_t ts = p->t0_ns - (int64_t)(rng4(p->seed, ST_INIT_TS, r, 0, 0) % 1000000000ull);
+    if (p->aged_ppm && (rng4(p->seed, ST_INIT_AGE, r, 0, 0) % 1000000ull) < p->aged_ppm && p->aged_max_ns > 0)
+      ts = p->t0_ns - (int64_t)(rng4(p->seed, ST_INIT_AGE, r, 1, 0) % (uint64_t)p->aged_max_ns);
+    uint64_t w = pack(ts, GX_ALIVE);
+    if (p->init_mode == GX_INIT_OWN) {
+      e->view[(size_t)(r / S) * R + r] = w;
+    } else {
+      for (uint32_t v = 0; v < H; v++) e->view[(size_t)v * R + r] = w;
+    }
+  }
+  memset(e->own_status, GX_ALIVE, (size_t)H * S);
+  for (uint32_t o = 0; o < H; o++) {
+    gx_host_state *h = &e->hs[o];
+    memset(h, 0, sizeof(*h));
+    h->bs_next = (int64_t)(rng4(p->seed, ST_PHASE_BS, o, 0, 0) % p->alive_interval_rounds);
+    h->bt_next = (int64_t)(rng4(p->seed, ST_PHASE_BT, o, 0, 0) % p->tombstone_interval_rounds);
+    h->last_bcast_ns = p->init_mode == GX_INIT_WARM ? p->t0_ns : 0;
+    h->running = S == 64 ? ~0ull : ((1ull << S) - 1);
+  }
+  memset(&e->st, 0, sizeof(e->st));
+  e->st.last_change_round = -1;
+  e->round = 0;
+}
+
+int gx_create(const gx_params *p, gx_engine **out) {
+  if (!out) return GX_EINVAL;
+  int rc = check_params(p);
+  if (rc) return rc;
+  gx_engine *e = (gx_engine *)calloc(1, sizeof(gx_engine));
+  if (!e) return GX_ENOMEM;
+  e->p = *p;
+  e->H = p->n_hosts;
+  e->S = p->n_services;
+  e->R = p->n_hosts * p->n_services;
+  e->Q = p->queue_cap;
+  e->A = p->list_slots;
+  e->L = p->packet_cap + p->pending_cap;
+  e->K = p->fanout;
+  e->SQ = pow2_at_least(64 > e->K * (p->retransmit_rounds + 1) ? 64 : e->K * (p->retransmit_rounds + 1));
+  e->DQ = pow2_at_least(e->L + p->pending_cap + 64);
+  size_t H = e->H;
+  e->view = (uint64_t *)malloc(sizeof(uint64_t) * H * e->R);
+  e->own_status = (uint8_t *)malloc(H * e->S);
+  e->hs = (gx_host_state *)calloc(H, sizeof(gx_host_state));
+  e->fifo = (gx_job *)calloc(H * e->Q, sizeof(gx_job));
+  e->sleep = (gx_job *)calloc(H * e->SQ, sizeof(gx_job));
+  e->dq = (grec *)calloc(H * e->DQ, sizeof(grec));
+  e->arena = (grec *)calloc(H * e->A * e->L, sizeof(grec));
+  e->arena_len = (uint32_t *)calloc(H * e->A, sizeof(uint32_t));
+  e->msg = (grec *)calloc(H * (e->K ? e->K : 1) * p->packet_cap, sizeof(grec));
+  e->msg_len = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
+  e->msg_dst = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
+  e->in_cnt = (uint32_t *)calloc(H + 1, sizeof(uint32_t));
+  e->in_list = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
+  if (!e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
+      !e->arena_len || !e->msg || !e->msg_len || !e->msg_dst || !e->in_cnt || !e->in_list) {
+    gx_destroy(e);
+    return GX_ENOMEM;
+  }
+  init_state(e);
+  *out = e;
+  return GX_OK;
+}
+
+int gx_destroy(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  free(e->view);
+  free(e->own_status);
+  free(e->hs);
+  free(e->fifo);
+  free(e->sleep);
+  free(e->dq);
+  free(e->arena);
+  free(e->arena_len);
+  free(e->msg);
+  free(e->msg_len);
+  free(e->msg_dst);
+  free(e->in_cnt);
+  free(e->in_list);
+  free(e);
+  return GX_OK;
+}
+
+int gx_set_round(gx_engine *e, int64_t round) {
+  if (!e || round < e->round) return GX_EINVAL;
+  e->round = round;
+  e->st.round = round;
+  for (uint32_t v = 0; v < e->H; v++) wake_host(e, v);
+  return GX_OK;
+}
+int gx_get_round(gx_engine *e, int64_t *round) {
+  if (!e || !round) return GX_EINVAL;
+  *round = e->round;
+  return GX_OK;
+}
+int gx_enable_timing(gx_engine *e, int on) {
+  (void)on;
+  return e ? GX_OK : GX_EINVAL;
+}
+
+int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
+  if (!e) return GX_EINVAL;
+  for (uint32_t i = 0; i < n_rounds; i++) run_one_round(e);
+  return GX_OK;
+}
+
+static int to_grec(const gx_engine *e, const gx_service *s, grec *g) {
+  if (s->host >= e->H || s->svc >= e->S || s->status > 6 || s->updated_ns < 0 || s->updated_ns >= GX_TS_LIMIT)
+    return GX_EINVAL;
+  g->w = pack(s->updated_ns, s->status);
+  g->r = s->host * e->S + s->svc;
+  g->pad = 0;
+  return GX_OK;
+}
+static void to_svc(const gx_engine *e, const grec *g, gx_service *s) {
+  s->updated_ns = ts_of(g->w);
+  s->host = g->r / e->S;
+  s->svc = (uint16_t)(g->r % e->S);
+  s->status = (uint8_t)st_of(g->w);
+  s->flags = 0;
+}
+
+int gx_add_service_entries(gx_engine *e, const uint32_t *views, const gx_service *svcs, uint32_t n,
+                           uint32_t *n_accepted) {
+  if (!e || (n && (!views || !svcs))) return GX_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    if (views[i] >= e->H || to_grec(e, &svcs[i], &g)) return GX_EINVAL;
+  }
+  uint32_t acc = 0;
+  int64_t now = now_of(e);
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    to_grec(e, &svcs[i], &g);
+    acc += (uint32_t)add_entry(e, views[i], g, now, SRC_LOCAL);
+  }
+  if (n_accepted) *n_accepted = acc;
+  return GX_OK;
+}
+
+int gx_merge(gx_engine *e, uint32_t dst, uint32_t src) {
+  if (!e || dst >= e->H || src >= e->H) return GX_EINVAL;
+  uint64_t *snap = (uint64_t *)malloc(sizeof(uint64_t) * e->R);
+  memcpy(snap, &e->view[(size_t)src * e->R], sizeof(uint64_t) * e->R);
+  int64_t now = now_of(e);
+  for (uint32_t r = 0; r < e->R; r++) {
+    if (st_of(snap[r]) == GX_ABSENT) continue;
+    grec u = {snap[r], r, 0};
+    add_entry(e, dst, u, now, SRC_AE);
+  }
+  free(snap);
+  return GX_OK;
+}
+
+int gx_merge_remote_state(gx_engine *e, uint32_t view, const gx_service *svcs, uint32_t n) {
+  if (!e || view >= e->H || (n && !svcs)) return GX_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    if (to_grec(e, &svcs[i], &g)) return GX_EINVAL;
+  }
+  int64_t now = now_of(e);
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    to_grec(e, &svcs[i], &g);
+    add_entry(e, view, g, now, SRC_AE);
+  }
+  return GX_OK;
+}
+
+int gx_tombstone_others(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || view >= e->H || (cap && !out)) return GX_EINVAL;
+  grec *tmp = (grec *)malloc(sizeof(grec) * (cap ? cap : 1));
+  uint32_t n = scan_view(e, view, now_of(e), tmp, cap);
+  for (uint32_t i = 0; i < n && i < cap; i++) to_svc(e, &tmp[i], &out[i]);
+  free(tmp);
+  if (n_out) *n_out = n;
+  return GX_OK;
+}
+
+int gx_tombstone_services(gx_engine *e, uint32_t host, const uint16_t *running, uint32_t n_running,
+                          gx_service *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || host >= e->H || (n_running && !running) || (cap && !out)) return GX_EINVAL;
+  uint64_t mask = 0;
+  for (uint32_t i = 0; i < n_running; i++) {
+    if (running[i] >= e->S) return GX_EINVAL;
+    mask |= 1ull << running[i];
+  }
+  grec tmp[128];
+  uint32_t n = tombstone_services(e, host, mask, now_of(e), tmp, 128);
+  for (uint32_t i = 0; i < n && i < cap; i++) to_svc(e, &tmp[i], &out[i]);
+  if (n_out) *n_out = n;
+  return GX_OK;
+}
+
+int gx_expire_server(gx_engine *e, uint32_t view, uint32_t owner, int *expired) {
+  if (!e || view >= e->H || owner >= e->H) return GX_EINVAL;
+  int x = expire_server(e, view, owner, now_of(e));
+  if (expired) *expired = x;
+  return GX_OK;
+}
+int gx_notify_leave(gx_engine *e, uint32_t view, uint32_t node) { return gx_expire_server(e, view, node, NULL); }
+
+int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32_t n, uint32_t n_passes) {
+  if (!e || host >= e->H || (n && !svcs) || n_passes < 1 || n_passes > 255) return GX_EINVAL;
+  grec *tmp = (grec *)malloc(sizeof(grec) * (n ? n : 1));
+  for (uint32_t i = 0; i < n; i++)
+    if (to_grec(e, &svcs[i], &tmp[i])) {
+      free(tmp);
+      return GX_EINVAL;
+    }
+  create_send(e, host, tmp, n, n_passes);
+  free(tmp);
+  return GX_OK;
+}
+
+int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n) {
+  if (!e || host >= e->H || (n && !list) || n > 4096) return GX_EINVAL;
+  grec *tmp = (grec *)malloc(sizeof(grec) * (n ? n : 1) * 2);
+  for (uint32_t i = 0; i < n; i++)
+    if (list[i].host != host || to_grec(e, &list[i], &tmp[i])) {
+      free(tmp);
+      return GX_EINVAL;
+    }
+  bs_body(e, host, tmp, n, now_of(e), tmp + n);
+  free(tmp);
+  return GX_OK;
+}
+
+int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n) {
+  if (!e || host >= e->H || (n && !list)) return GX_EINVAL;
+  uint64_t mask = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (list[i].host != host || list[i].svc >= e->S) return GX_EINVAL;
+    mask |= 1ull << list[i].svc;
+  }
+  uint64_t saved = e->hs[host].running;
+  e->hs[host].running = mask;
+  bt_tick(e, host, now_of(e));
+  e->hs[host].running = saved;
+  return GX_OK;
+}
+
+int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *out) {
+  grec g;
+  if (!e || !svc || !out || view >= e->H || to_grec(e, svc, &g)) return GX_EINVAL;
+  *out = is_new(e, view, g);
+  return GX_OK;
+}
+
+int gx_notify_msg(gx_engine *e, uint32_t host, const gx_service *recs, uint32_t n) {
+  if (!e || host >= e->H || (n && !recs)) return GX_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    if (to_grec(e, &recs[i], &g)) return GX_EINVAL;
+  }
+  int64_t now = now_of(e);
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    to_grec(e, &recs[i], &g);
+    add_entry(e, host, g, now, SRC_GOSSIP);
+  }
+  return GX_OK;
+}
+
+int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *out, uint32_t cap,
+                      uint32_t *n_out) {
+  if (limit == GX_LIMIT_DEFAULT) limit = e ? e->p.packet_cap : 0;
+  if (!e || host >= e->H || !n_out || limit > 256 || cap < limit || (limit && !out)) return GX_EINVAL;
+  grec pk[256];
+  uint32_t l = get_broadcasts(e, host, limit, pk);
+  for (uint32_t i = 0; i < l; i++) to_svc(e, &pk[i], &out[i]);
+  *n_out = l;
+  return GX_OK;
+}
+
+int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || view >= e->H || (cap && !out)) return GX_EINVAL;
+  uint32_t n = 0;
+  const uint64_t *row = &e->view[(size_t)view * e->R];
+  for (uint32_t r = 0; r < e->R; r++) {
+    if (st_of(row[r]) == GX_ABSENT) continue;
+    if (n < cap) {
+      grec g = {row[r], r, 0};
+      to_svc(e, &g, &out[n]);
+    }
+    n++;
+  }
+  if (n_out) *n_out = n;
+  return GX_OK;
+}
+
+int gx_read_views(gx_engine *e, uint32_t lo, uint32_t hi, uint64_t *out) {
+  if (!e || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
+  memcpy(out, &e->view[(size_t)lo * e->R], sizeof(uint64_t) * (size_t)(hi - lo) * e->R);
+  return GX_OK;
+}
+int gx_write_views(gx_engine *e, uint32_t lo, uint32_t hi, const uint64_t *in) {
+  if (!e || lo > hi || hi > e->H || (hi > lo && !in)) return GX_EINVAL;
+  for (size_t i = 0; i < (size_t)(hi - lo) * e->R; i++) {
+    uint64_t w = in[i];
+    if (st_of(w) == 7 ? w != GX_SLOT_ABSENT : 0) return GX_EINVAL;
+  }
+  memcpy(&e->view[(size_t)lo * e->R], in, sizeof(uint64_t) * (size_t)(hi - lo) * e->R);
+  e->st.last_change_round = e->round;
+  return GX_OK;
+}
+int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc) {
+  grec g;
+  if (!e || !svc || view >= e->H) return GX_EINVAL;
+  if (svc->status == GX_ABSENT) {
+    if (svc->host >= e->H || svc->svc >= e->S) return GX_EINVAL;
+    set_slot(e, &e->view[(size_t)view * e->R + svc->host * e->S + svc->svc], GX_SLOT_ABSENT);
+    return GX_OK;
+  }
+  if (to_grec(e, svc, &g)) return GX_EINVAL;
+  set_slot(e, &e->view[(size_t)view * e->R + g.r], g.w);
+  return GX_OK;
+}
+int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out) {
+  if (!e || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
+  memcpy(out, &e->hs[lo], sizeof(gx_host_state) * (hi - lo));
+  return GX_OK;
+}
+int gx_read_queue(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || host >= e->H || (cap && !out)) return GX_EINVAL;
+  gx_host_state *h = &e->hs[host];
+  uint32_t n = h->fifo_tail - h->fifo_head;
+  for (uint32_t i = 0; i < n && i < cap; i++) out[i] = e->fifo[(size_t)host * e->Q + ((h->fifo_head + i) % e->Q)];
+  if (n_out) *n_out = n;
+  return GX_OK;
+}
+int gx_read_sleepers(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || host >= e->H || (cap && !out)) return GX_EINVAL;
+  gx_host_state *h = &e->hs[host];
+  uint32_t n = h->sleep_tail - h->sleep_head;
+  for (uint32_t i = 0; i < n && i < cap; i++) out[i] = e->sleep[(size_t)host * e->SQ + ((h->sleep_head + i) % e->SQ)];
+  if (n_out) *n_out = n;
+  return GX_OK;
+}
+int gx_read_pending(gx_engine *e, uint32_t host, gx_service *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || host >= e->H || (cap && !out)) return GX_EINVAL;
+  gx_host_state *h = &e->hs[host];
+  for (uint32_t i = 0; i < h->dq_len && i < cap; i++)
+    to_svc(e, &e->dq[(size_t)host * e->DQ + ((h->dq_head + i) & (e->DQ - 1))], &out[i]);
+  if (n_out) *n_out = h->dq_len;
+  return GX_OK;
+}
+int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, uint32_t cap, uint32_t *n_out) {
+  if (!e || host >= e->H || slot >= e->A || (cap && !out)) return GX_EINVAL;
+  uint32_t n = (e->hs[host].arena_used >> slot) & 1u ? e->arena_len[(size_t)host * e->A + slot] : 0;
+  for (uint32_t i = 0; i < n && i < cap; i++) to_svc(e, &e->arena[((size_t)host * e->A + slot) * e->L + i], &out[i]);
+  if (n_out) *n_out = n;
+  return GX_OK;
+}
+
+static inline uint64_t feed(uint64_t h, uint64_t x) { return mix64(h ^ x); }
+static uint64_t feed_job(uint64_t h, const gx_job *j) {
+  h = feed(h, j->a);
+  h = feed(h, j->b);
+  h = feed(h, (uint64_t)j->c | ((uint64_t)j->meta << 32));
+  return feed(h, (uint64_t)j->wake | ((uint64_t)j->aux << 32));
+}
+int gx_host_digests(gx_engine *e, uint64_t *out) {
+  if (!e || !out) return GX_EINVAL;
+  for (uint32_t v = 0; v < e->H; v++) {
+    const gx_host_state *s = &e->hs[v];
+    uint64_t h = 0x243F6A8885A308D3ull;
+    for (uint32_t i = s->fifo_head; i != s->fifo_tail; i++) h = feed_job(h, &e->fifo[(size_t)v * e->Q + (i % e->Q)]);
+    h = feed(h, 0xF1F0);
+    for (uint32_t i = s->sleep_head; i != s->sleep_tail; i++) h = feed_job(h, &e->sleep[(size_t)v * e->SQ + (i % e->SQ)]);
+    h = feed(h, 0x51EE);
+    h = feed(h, s->dq_len);
+    for (uint32_t i = 0; i < s->dq_len; i++) {
+      const grec *g = &e->dq[(size_t)v * e->DQ + ((s->dq_head + i) & (e->DQ - 1))];
+      h = feed(h, g->w);
+      h = feed(h, g->r);
+    }
+    h = feed(h, 0xA7E4);
+    for (uint32_t a = 0; a < e->A; a++) {
+      if (!((s->arena_used >> a) & 1u)) continue;
+      uint32_t len = e->arena_len[(size_t)v * e->A + a];
+      h = feed(h, a);
+      h = feed(h, len);
+      for (uint32_t i = 0; i < len; i++) {
+        const grec *g = &e->arena[((size_t)v * e->A + a) * e->L + i];
+        h = feed(h, g->w);
+        h = feed(h, g->r);
+      }
+    }
+    h = feed(h, s->flags);
+    h = feed(h, (uint64_t)s->bs_next);
+    h = feed(h, (uint64_t)s->bt_next);
+    h = feed(h, (uint64_t)s->last_bcast_ns);
+    h = feed(h, s->running);
+    out[v] = h;
+  }
+  return GX_OK;
+}
+
+int gx_stats_get(gx_engine *e, gx_stats *out) {
+  if (!e || !out) return GX_EINVAL;
+  *out = e->st;
+  out->round = e->round;
+  return GX_OK;
+}
+int gx_timing_get(gx_engine *e, gx_timing *out) {
+  if (!e || !out) return GX_EINVAL;
+  memset(out, 0, sizeof(*out));
+  return GX_OK;
+}
+int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
+  if (!e) return GX_EINVAL;
+  uint64_t bad = 0;
+  for (uint32_t r = 0; r < e->R; r++) {
+    uint64_t w0 = e->view[r];
+    for (uint32_t v = 1; v < e->H; v++)
+      if (e->view[(size_t)v * e->R + r] != w0) {
+        bad++;
+        break;
+      }
+  }
+  if (converged) *converged = bad == 0;
+  if (n_disagree) *n_disagree = bad;
+  return GX_OK;
+}

@@ -1,0 +1,430 @@
+"""ctypes mirror of include/gx.h and a thin Python handle over the C-ABI.
+
+The product library is ``sidecar_amd/libgx.so`` (HIP kernels for gfx950). ``Engine`` loads it by
+default and raises if it is missing — there is no CPU fallback in the product path. Tests may
+pass another library exporting the same ABI (the CPU oracle) explicitly via ``lib=``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBGX_PATH = os.path.join(HERE, "libgx.so")
+
+GX_OK = 0
+GX_EIO = -5
+GX_ENOMEM = -12
+GX_EINVAL = -22
+GX_ENOSYS = -38
+
+ALIVE, TOMBSTONE, UNHEALTHY, UNKNOWN, DRAINING, ABSENT = 0, 1, 2, 3, 4, 7
+SLOT_ABSENT = 7
+TS_SHIFT = 3
+
+JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE = 0, 1, 2, 3, 4
+INIT_EMPTY, INIT_OWN, INIT_WARM = 0, 1, 2
+LIMIT_DEFAULT = 0xFFFFFFFF
+
+K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge"]
+
+
+class GxService(C.Structure):
+    _fields_ = [("updated_ns", C.c_int64), ("host", C.c_uint32), ("svc", C.c_uint16),
+                ("status", C.c_uint8), ("flags", C.c_uint8)]
+
+    def tup(self):
+        return (self.updated_ns, self.host, self.svc, self.status)
+
+    def __repr__(self):
+        return f"Svc(h={self.host},s={self.svc},t={self.updated_ns},st={self.status})"
+
+
+class GxJob(C.Structure):
+    _fields_ = [("a", C.c_uint64), ("b", C.c_uint64), ("c", C.c_uint32), ("meta", C.c_uint32),
+                ("wake", C.c_uint32), ("aux", C.c_uint32)]
+
+    @property
+    def kind(self):
+        return self.meta & 0xFF
+
+    @property
+    def pass_(self):
+        return (self.meta >> 8) & 0xFF
+
+    @property
+    def n_passes(self):
+        return (self.meta >> 16) & 0xFF
+
+    def tup(self):
+        return (self.a, self.b, self.c, self.meta, self.wake, self.aux)
+
+
+class GxParams(C.Structure):
+    _fields_ = [
+        ("n_hosts", C.c_uint32), ("n_services", C.c_uint32), ("fanout", C.c_uint32),
+        ("packet_cap", C.c_uint32), ("pending_cap", C.c_uint32), ("queue_cap", C.c_uint32),
+        ("list_slots", C.c_uint32), ("gossip_stop_on_empty", C.c_uint32),
+        ("alive_interval_rounds", C.c_uint32), ("tombstone_interval_rounds", C.c_uint32),
+        ("retransmit_rounds", C.c_uint32), ("alive_count", C.c_uint32),
+        ("tombstone_count", C.c_uint32), ("ae_period_rounds", C.c_uint32),
+        ("ae_phase", C.c_uint32), ("init_mode", C.c_uint32),
+        ("t0_ns", C.c_int64), ("round_ns", C.c_int64), ("alive_lifespan_ns", C.c_int64),
+        ("draining_lifespan_ns", C.c_int64), ("tombstone_lifespan_ns", C.c_int64),
+        ("stale_fudge_ns", C.c_int64), ("alive_broadcast_interval_ns", C.c_int64),
+        ("pass_increment_ns", C.c_int64), ("tombstone_bump_ns", C.c_int64),
+        ("seed", C.c_uint64), ("churn_ppm", C.c_uint32), ("aged_ppm", C.c_uint32),
+        ("aged_max_ns", C.c_int64), ("partition_start", C.c_int32), ("partition_end", C.c_int32),
+        ("storm_round", C.c_int32), ("device", C.c_int32),
+    ]
+
+
+class GxHostState(C.Structure):
+    _fields_ = [("fifo_head", C.c_uint32), ("fifo_tail", C.c_uint32), ("sleep_head", C.c_uint32),
+                ("sleep_tail", C.c_uint32), ("dq_head", C.c_uint32), ("dq_len", C.c_uint32),
+                ("arena_used", C.c_uint32), ("flags", C.c_uint32), ("bs_next", C.c_int64),
+                ("bt_next", C.c_int64), ("last_bcast_ns", C.c_int64), ("running", C.c_uint64)]
+
+
+class GxStats(C.Structure):
+    _fields_ = [("round", C.c_int64)] + [(n, C.c_uint64) for n in (
+        "gossip_merges", "ae_merges", "local_merges", "gossip_accepts", "ae_accepts",
+        "local_accepts", "stale_drops", "retransmits", "queue_drops", "list_drops", "sleep_drops",
+        "pending_drops", "dequeues", "nil_batches", "packets", "records_sent", "expired", "gc",
+        "own_tombstones", "expire_server", "send_jobs", "ae_exchanges", "churn_events")] + [
+        ("last_change_round", C.c_int64), ("reserved", C.c_uint64 * 7)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
+
+
+class GxTiming(C.Structure):
+    _fields_ = [("ms", C.c_double * 8), ("launches", C.c_uint64 * 8), ("bytes", C.c_uint64 * 8),
+                ("units", C.c_uint64 * 8)]
+
+    def as_dict(self):
+        return {K_NAMES[i]: {"ms": self.ms[i], "launches": self.launches[i],
+                             "bytes": self.bytes[i], "units": self.units[i]} for i in range(8)}
+
+
+ABI_FUNCS = [
+    "gx_abi_version", "gx_backend", "gx_params_default", "gx_create", "gx_destroy", "gx_set_round",
+    "gx_get_round", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
+    "gx_tombstone_others", "gx_tombstone_services", "gx_expire_server", "gx_send_services",
+    "gx_broadcast_services", "gx_broadcast_tombstones", "gx_is_new_service", "gx_notify_msg",
+    "gx_get_broadcasts", "gx_local_state", "gx_merge_remote_state", "gx_notify_leave",
+    "gx_read_views", "gx_write_views", "gx_write_slot", "gx_read_hosts", "gx_read_queue",
+    "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
+    "gx_timing_get", "gx_converged",
+]
+
+
+def _declare(lib):
+    P = C.POINTER
+    vp = C.c_void_p
+    u32, i32, i64, u16 = C.c_uint32, C.c_int, C.c_int64, C.c_uint16
+    sig = {
+        "gx_abi_version": ([], i32), "gx_backend": ([], C.c_char_p),
+        "gx_params_default": ([P(GxParams)], None), "gx_create": ([P(GxParams), P(vp)], i32),
+        "gx_destroy": ([vp], i32), "gx_set_round": ([vp, i64], i32),
+        "gx_get_round": ([vp, P(i64)], i32), "gx_enable_timing": ([vp, i32], i32),
+        "gx_run_rounds": ([vp, u32], i32),
+        "gx_add_service_entries": ([vp, P(u32), P(GxService), u32, P(u32)], i32),
+        "gx_merge": ([vp, u32, u32], i32),
+        "gx_tombstone_others": ([vp, u32, P(GxService), u32, P(u32)], i32),
+        "gx_tombstone_services": ([vp, u32, P(u16), u32, P(GxService), u32, P(u32)], i32),
+        "gx_expire_server": ([vp, u32, u32, P(i32)], i32),
+        "gx_send_services": ([vp, u32, P(GxService), u32, u32], i32),
+        "gx_broadcast_services": ([vp, u32, P(GxService), u32], i32),
+        "gx_broadcast_tombstones": ([vp, u32, P(GxService), u32], i32),
+        "gx_is_new_service": ([vp, u32, P(GxService), P(i32)], i32),
+        "gx_notify_msg": ([vp, u32, P(GxService), u32], i32),
+        "gx_get_broadcasts": ([vp, u32, u32, P(GxService), u32, P(u32)], i32),
+        "gx_local_state": ([vp, u32, P(GxService), u32, P(u32)], i32),
+        "gx_merge_remote_state": ([vp, u32, P(GxService), u32], i32),
+        "gx_notify_leave": ([vp, u32, u32], i32),
+        "gx_read_views": ([vp, u32, u32, vp], i32), "gx_write_views": ([vp, u32, u32, vp], i32),
+        "gx_write_slot": ([vp, u32, P(GxService)], i32),
+        "gx_read_hosts": ([vp, u32, u32, P(GxHostState)], i32),
+        "gx_read_queue": ([vp, u32, P(GxJob), u32, P(u32)], i32),
+        "gx_read_sleepers": ([vp, u32, P(GxJob), u32, P(u32)], i32),
+        "gx_read_pending": ([vp, u32, P(GxService), u32, P(u32)], i32),
+        "gx_read_list": ([vp, u32, u32, P(GxService), u32, P(u32)], i32),
+        "gx_host_digests": ([vp, vp], i32), "gx_stats_get": ([vp, P(GxStats)], i32),
+        "gx_timing_get": ([vp, P(GxTiming)], i32),
+        "gx_converged": ([vp, P(i32), P(C.c_uint64)], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    return lib
+
+
+_LIB_CACHE = {}
+
+
+def load_library(path: str):
+    path = os.path.abspath(path)
+    if path not in _LIB_CACHE:
+        if not os.path.exists(path):
+            raise RuntimeError(f"gx library not found: {path} (build it: python __graft_entry__.py build)")
+        _LIB_CACHE[path] = _declare(C.CDLL(path))
+    return _LIB_CACHE[path]
+
+
+def load_product():
+    """The HIP engine. Raises if the extension was not built — no fallback."""
+    lib = load_library(LIBGX_PATH)
+    be = lib.gx_backend().decode()
+    if not be.startswith("hip"):
+        raise RuntimeError(f"libgx.so reports backend {be!r}, expected the HIP engine")
+    return lib
+
+
+class GxError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = ""):
+    if rc != GX_OK:
+        raise GxError(f"{what} failed with rc={rc}")
+
+
+def default_params(lib=None, **kw) -> GxParams:
+    p = GxParams()
+    (lib or load_product()).gx_params_default(C.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        setattr(p, k, v)
+    return p
+
+
+def svc(host, s, ts, status=ALIVE) -> GxService:
+    return GxService(int(ts), int(host), int(s), int(status), 0)
+
+
+def svc_array(items: Sequence) -> "C.Array":
+    arr = (GxService * max(1, len(items)))()
+    for i, it in enumerate(items):
+        if isinstance(it, GxService):
+            arr[i] = it
+        else:
+            arr[i] = svc(*it)
+    return arr
+
+
+class Engine:
+    """One simulated cluster (H hosts x S services) behind the gx C-ABI."""
+
+    def __init__(self, params: Optional[GxParams] = None, lib=None, **kw):
+        self.lib = lib if lib is not None else load_product()
+        if params is None:
+            params = default_params(self.lib, **kw)
+        else:
+            for k, v in kw.items():
+                setattr(params, k, v)
+        self.params = params
+        self.H = params.n_hosts
+        self.S = params.n_services
+        h = C.c_void_p()
+        check(self.lib.gx_create(C.byref(params), C.byref(h)), "gx_create")
+        self.h = h
+
+    # lifecycle -------------------------------------------------------------------------
+    def close(self):
+        if self.h:
+            self.lib.gx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def backend(self):
+        return self.lib.gx_backend().decode()
+
+    @property
+    def round(self) -> int:
+        r = C.c_int64()
+        check(self.lib.gx_get_round(self.h, C.byref(r)))
+        return r.value
+
+    def now(self, round_=None) -> int:
+        r = self.round if round_ is None else round_
+        return self.params.t0_ns + r * self.params.round_ns
+
+    def set_round(self, r: int):
+        check(self.lib.gx_set_round(self.h, int(r)), "gx_set_round")
+
+    def enable_timing(self, on=True):
+        check(self.lib.gx_enable_timing(self.h, 1 if on else 0))
+
+    def run_rounds(self, n: int):
+        check(self.lib.gx_run_rounds(self.h, int(n)), "gx_run_rounds")
+
+    # ServicesState ---------------------------------------------------------------------
+    def add_service_entries(self, views: Sequence[int], items: Sequence) -> int:
+        n = len(items)
+        va = (C.c_uint32 * max(1, n))(*views)
+        acc = C.c_uint32()
+        check(self.lib.gx_add_service_entries(self.h, va, svc_array(items), n, C.byref(acc)),
+              "gx_add_service_entries")
+        return acc.value
+
+    def add_service_entry(self, view: int, item) -> int:
+        return self.add_service_entries([view], [item])
+
+    def merge(self, dst: int, src: int):
+        check(self.lib.gx_merge(self.h, dst, src), "gx_merge")
+
+    def merge_remote_state(self, view: int, items: Sequence):
+        check(self.lib.gx_merge_remote_state(self.h, view, svc_array(items), len(items)))
+
+    def tombstone_others(self, view: int, cap: int = 4096):
+        out = (GxService * max(1, cap))()
+        n = C.c_uint32()
+        check(self.lib.gx_tombstone_others(self.h, view, out, cap, C.byref(n)))
+        return [out[i] for i in range(min(n.value, cap))], n.value
+
+    def tombstone_services(self, host: int, running: Iterable[int], cap: int = 256):
+        run = list(running)
+        ra = (C.c_uint16 * max(1, len(run)))(*run)
+        out = (GxService * cap)()
+        n = C.c_uint32()
+        check(self.lib.gx_tombstone_services(self.h, host, ra, len(run), out, cap, C.byref(n)))
+        return [out[i] for i in range(min(n.value, cap))]
+
+    def expire_server(self, view: int, owner: int) -> bool:
+        x = C.c_int()
+        check(self.lib.gx_expire_server(self.h, view, owner, C.byref(x)))
+        return bool(x.value)
+
+    def send_services(self, host: int, items: Sequence, n_passes: int):
+        check(self.lib.gx_send_services(self.h, host, svc_array(items), len(items), n_passes))
+
+    def broadcast_services(self, host: int, items: Sequence):
+        check(self.lib.gx_broadcast_services(self.h, host, svc_array(items), len(items)))
+
+    def broadcast_tombstones(self, host: int, items: Sequence):
+        check(self.lib.gx_broadcast_tombstones(self.h, host, svc_array(items), len(items)))
+
+    def is_new_service(self, view: int, item) -> bool:
+        x = C.c_int()
+        a = svc_array([item])
+        check(self.lib.gx_is_new_service(self.h, view, a, C.byref(x)))
+        return bool(x.value)
+
+    # delegate --------------------------------------------------------------------------
+    def notify_msg(self, host: int, items: Sequence):
+        check(self.lib.gx_notify_msg(self.h, host, svc_array(items), len(items)))
+
+    def get_broadcasts(self, host: int, limit: Optional[int] = None):
+        cap = 256
+        out = (GxService * cap)()
+        n = C.c_uint32()
+        lim = LIMIT_DEFAULT if limit is None else int(limit)
+        check(self.lib.gx_get_broadcasts(self.h, host, lim, out, cap, C.byref(n)), "gx_get_broadcasts")
+        if n.value == 0:
+            return None
+        return [out[i] for i in range(n.value)]
+
+    def local_state(self, view: int):
+        n = C.c_uint32()
+        check(self.lib.gx_local_state(self.h, view, None, 0, C.byref(n)))
+        cap = max(1, n.value)
+        out = (GxService * cap)()
+        check(self.lib.gx_local_state(self.h, view, out, cap, C.byref(n)))
+        return [out[i] for i in range(n.value)]
+
+    def notify_leave(self, view: int, node: int):
+        check(self.lib.gx_notify_leave(self.h, view, node))
+
+    # read-back -------------------------------------------------------------------------
+    def read_views(self, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
+        hi = self.H if hi is None else hi
+        out = np.empty((hi - lo, self.H * self.S), dtype=np.uint64)
+        check(self.lib.gx_read_views(self.h, lo, hi, out.ctypes.data_as(C.c_void_p)), "gx_read_views")
+        return out
+
+    def write_views(self, words: np.ndarray, lo: int = 0):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        hi = lo + words.shape[0]
+        check(self.lib.gx_write_views(self.h, lo, hi, words.ctypes.data_as(C.c_void_p)), "gx_write_views")
+
+    def write_slot(self, view: int, item):
+        check(self.lib.gx_write_slot(self.h, view, svc_array([item])), "gx_write_slot")
+
+    def slot(self, view: int, host: int, s: int):
+        """(updated_ns, status) of one slot, or None if absent."""
+        row = self.read_views(view, view + 1)[0]
+        w = int(row[host * self.S + s])
+        if w & 7 == ABSENT:
+            return None
+        return (w >> TS_SHIFT, w & 7)
+
+    def hosts(self, lo=0, hi=None):
+        hi = self.H if hi is None else hi
+        out = (GxHostState * max(1, hi - lo))()
+        check(self.lib.gx_read_hosts(self.h, lo, hi, out))
+        return [out[i] for i in range(hi - lo)]
+
+    def queue(self, host: int):
+        n = C.c_uint32()
+        check(self.lib.gx_read_queue(self.h, host, None, 0, C.byref(n)))
+        out = (GxJob * max(1, n.value))()
+        check(self.lib.gx_read_queue(self.h, host, out, n.value, C.byref(n)))
+        return [out[i] for i in range(n.value)]
+
+    def sleepers(self, host: int):
+        n = C.c_uint32()
+        check(self.lib.gx_read_sleepers(self.h, host, None, 0, C.byref(n)))
+        out = (GxJob * max(1, n.value))()
+        check(self.lib.gx_read_sleepers(self.h, host, out, n.value, C.byref(n)))
+        return [out[i] for i in range(n.value)]
+
+    def pending(self, host: int):
+        out = (GxService * 1024)()
+        n = C.c_uint32()
+        check(self.lib.gx_read_pending(self.h, host, out, 1024, C.byref(n)))
+        return [out[i] for i in range(min(n.value, 1024))]
+
+    def read_list(self, host: int, slot: int):
+        out = (GxService * 1024)()
+        n = C.c_uint32()
+        check(self.lib.gx_read_list(self.h, host, slot, out, 1024, C.byref(n)))
+        return [out[i] for i in range(min(n.value, 1024))]
+
+    def digests(self) -> np.ndarray:
+        out = np.empty(self.H, dtype=np.uint64)
+        check(self.lib.gx_host_digests(self.h, out.ctypes.data_as(C.c_void_p)), "gx_host_digests")
+        return out
+
+    def stats(self) -> dict:
+        s = GxStats()
+        check(self.lib.gx_stats_get(self.h, C.byref(s)))
+        return s.as_dict()
+
+    def timing(self) -> dict:
+        t = GxTiming()
+        check(self.lib.gx_timing_get(self.h, C.byref(t)))
+        return t.as_dict()
+
+    def converged(self):
+        c = C.c_int()
+        n = C.c_uint64()
+        check(self.lib.gx_converged(self.h, C.byref(c), C.byref(n)))
+        return bool(c.value), n.value

@@ -1,0 +1,464 @@
+"""Known-answer tests restated from the reference's own Go tests, written against the gx C-ABI.
+
+Each case cites the reference test it restates (paths relative to the reference root). Every
+case takes a loaded library exporting include/gx.h, so the same cases pin the CPU oracle
+(tests/test_oracle_kat.py) and check the HIP engine (tests/test_gpu_kat.py).
+
+Host-name interning used throughout: LOCAL = the machine's own hostname (state.Hostname after
+NewServicesState()), SH = "shakespeare", CH = "chaucer"; docker1/docker2 for the delegate
+fixtures. The simulated clock replaces time.Now(): "time passes" is a round advance.
+"""
+import datetime as _dt
+
+from sidecar_amd.abi import (ALIVE, DRAINING, Engine, JOB_NIL_BS, JOB_RETX, JOB_SEND, TOMBSTONE,
+                             UNHEALTHY, UNKNOWN, default_params)
+
+LOCAL, SH, CH, OTHER, OTHER2, DOCKER1, DOCKER2 = 0, 1, 2, 3, 4, 5, 6
+SEC = 10**9
+MIN = 60 * SEC
+HOUR = 60 * MIN
+T0 = 1_700_000_000 * SEC  # a whole second, like baseTime.Round(time.Second)
+TOMBSTONE_LIFESPAN = 3 * HOUR
+ALIVE_LIFESPAN = 80 * SEC
+DRAINING_LIFESPAN = 10 * MIN
+
+
+def mk(lib, **kw):
+    p = default_params(lib, n_hosts=8, n_services=8, t0_ns=T0, retransmit_rounds=0,
+                       queue_cap=64, list_slots=8)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return Engine(p, lib=lib)
+
+
+def tup(s):
+    return (s.host, s.svc, s.updated_ns, s.status)
+
+
+# ----------------------------------------------------------------- catalog/services_state_test.go
+def kat_add_merges_new(lib):
+    """services_state_test.go:126-133 — AddServiceEntry merges in a new service."""
+    e = mk(lib)
+    assert e.local_state(LOCAL) == []
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    assert e.slot(LOCAL, CH, 0) == (T0, ALIVE)
+
+
+def kat_older_update_ignored(lib):
+    """services_state_test.go:135-155 — an update older than what we have is not merged."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    assert e.add_service_entry(LOCAL, (CH, 0, T0 - MIN, ALIVE)) == 0
+    assert e.slot(LOCAL, CH, 0) == (T0, ALIVE)
+
+
+def kat_stale_dropped(lib):
+    """services_state_test.go:157-175 — a record older than now-3h-1min is dropped and no server
+    is created. The reference reads time.Now() again inside IsStale, so the record is strictly
+    older than the cut-off; restated by letting one round pass. service.go:68-72 is strict."""
+    e = mk(lib)
+    base = e.now()
+    e.set_round(1)
+    assert e.add_service_entry(LOCAL, (CH, 0, base - MIN - TOMBSTONE_LIFESPAN, ALIVE)) == 0
+    assert all(e.slot(LOCAL, CH, s) is None for s in range(e.S))
+    assert e.stats()["stale_drops"] == 1
+    # boundary: exactly at the cut-off is not Before() it -> accepted
+    now = e.now()
+    assert e.add_service_entry(LOCAL, (CH, 1, now - MIN - TOMBSTONE_LIFESPAN, ALIVE)) == 1
+
+
+def kat_updates_timestamp(lib):
+    """services_state_test.go:177-183 — a newer record replaces the stored Updated."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    nd = T0 + 5 * 24 * HOUR
+    e.add_service_entry(LOCAL, (CH, 0, nd, ALIVE))
+    assert e.slot(LOCAL, CH, 0) == (nd, ALIVE)
+
+
+def kat_retransmit_on_change(lib):
+    """services_state_test.go:214-225 — an accepted foreign change is retransmitted exactly once,
+    as the stored record."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    q = e.queue(LOCAL)
+    assert len(q) == 1 and q[0].kind == JOB_RETX
+    first = e.get_broadcasts(LOCAL)  # catch the retransmit from the initial add
+    assert [tup(s) for s in first] == [(CH, 0, T0, ALIVE)]
+    e.set_round(1)
+    ts = e.now()  # svc.Tombstone(): Updated = now
+    e.add_service_entry(LOCAL, (CH, 0, ts, TOMBSTONE))
+    pkt = e.get_broadcasts(LOCAL)
+    assert len(pkt) == 1 and tup(pkt[0]) == (CH, 0, ts, TOMBSTONE)
+    assert e.get_broadcasts(LOCAL) is None
+
+
+def kat_no_retransmit_own(lib):
+    """services_state_test.go:227-243 — adding a service of this host is not retransmitted."""
+    e = mk(lib)
+    e.add_service_entry(SH, (SH, 0, T0, ALIVE))
+    assert e.queue(SH) == []
+    assert e.get_broadcasts(SH) is None
+
+
+def kat_sets_draining(lib):
+    """services_state_test.go:245-256 — ALIVE -> DRAINING applies."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    e.set_round(1)
+    e.add_service_entry(LOCAL, (CH, 0, e.now(), DRAINING))
+    assert e.slot(LOCAL, CH, 0)[1] == DRAINING
+
+
+def kat_draining_sticky(lib):
+    """services_state_test.go:258-270 — a newer ALIVE does not overwrite DRAINING
+    (services_state.go:329-331); the timestamp still advances."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, DRAINING))
+    e.set_round(1)
+    e.add_service_entry(LOCAL, (CH, 0, e.now(), ALIVE))
+    assert e.slot(LOCAL, CH, 0) == (e.now(), DRAINING)
+
+
+def kat_merge(lib):
+    """services_state_test.go:299-308 — Merge() brings another state's servers in."""
+    e = mk(lib)
+    e.add_service_entry(OTHER, (CH, 0, T0, ALIVE))
+    e.merge(OTHER2, OTHER)
+    assert [s.tup() for s in e.local_state(OTHER2)] == [s.tup() for s in e.local_state(OTHER)]
+
+
+# Test_TrackingAndBroadcasting: state.Hostname = shakespeare, tombstoneRetransmit = 1ns
+def _tb(lib):
+    e = mk(lib)
+    s1 = (SH, 0, T0, ALIVE)
+    s2 = (SH, 1, T0, ALIVE)
+    return e, s1, s2
+
+
+def kat_send_services_count(lib):
+    """services_state_test.go:345-353 — SendServices with a 5-pass looper emits 5 batches;
+    :402-424 — each pass adds 50ns to Updated."""
+    e, s1, s2 = _tb(lib)
+    e.send_services(SH, [s1, s2], 5)
+    for p in range(5):
+        b = e.get_broadcasts(SH)
+        assert [tup(x) for x in b] == [(SH, 0, T0 + 50 * p, ALIVE), (SH, 1, T0 + 50 * p, ALIVE)]
+    assert e.get_broadcasts(SH) is None
+
+
+def kat_track_new_services(lib):
+    """services_state_test.go:355-366 — tracked local services are added to state."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entries([SH, SH], [s1, s2])
+    assert e.slot(SH, SH, 0) == (T0, ALIVE) and e.slot(SH, SH, 1) == (T0, ALIVE)
+
+
+def kat_broadcast_new_in_order(lib):
+    """services_state_test.go:368-378 — BroadcastServices serialises new services in order."""
+    e, s1, s2 = _tb(lib)
+    e.broadcast_services(SH, [s1, s2])
+    q = e.queue(SH)
+    assert len(q) == 1 and q[0].kind == JOB_SEND and q[0].n_passes == 5  # ALIVE_COUNT: new
+    b = e.get_broadcasts(SH)
+    assert [tup(x) for x in b] == [s1[:2] + (T0, ALIVE), s2[:2] + (T0, ALIVE)]
+
+
+def kat_broadcast_nil_when_idle(lib):
+    """services_state_test.go:380-386 — a nil batch when there are no services."""
+    e, s1, s2 = _tb(lib)
+    e.broadcast_services(SH, [])
+    q = e.queue(SH)
+    assert len(q) == 1 and q[0].kind == JOB_NIL_BS
+    assert e.hosts(SH, SH + 1)[0].flags & 1  # the looper is blocked on its nil send
+    assert e.get_broadcasts(SH) is None
+    assert e.queue(SH) == [] and not (e.hosts(SH, SH + 1)[0].flags & 1)
+
+
+def kat_tombstones_serialized(lib):
+    """services_state_test.go:388-400 — an own service missing from discovery is tombstoned and
+    emitted twice with Status 1."""
+    e, s1, s2 = _tb(lib)
+    junk = (SH, 2, T0, ALIVE)
+    e.add_service_entries([SH, SH, SH], [junk, s1, s2])
+    e.broadcast_tombstones(SH, [s1, s2])
+    b = e.get_broadcasts(SH)
+    assert len(b) == 2
+    assert all((x.host, x.svc, x.status) == (SH, 2, TOMBSTONE) for x in b)
+
+
+def kat_alive_not_tombstoned(lib):
+    """services_state_test.go:437-444 — services still alive are not tombstoned (empty batch)."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entries([SH, SH], [s1, s2])
+    e.broadcast_tombstones(SH, [s1, s2])
+    assert e.get_broadcasts(SH) is None
+    assert e.slot(SH, SH, 0) == (T0, ALIVE)
+
+
+def kat_nil_when_no_tombstones(lib):
+    """services_state_test.go:446-452 — nil into the channel when no tombstones."""
+    e, s1, s2 = _tb(lib)
+    e.broadcast_tombstones(SH, [])
+    assert e.get_broadcasts(SH) is None
+    assert e.stats()["nil_batches"] == 1
+
+
+def kat_last_tombstone_gc(lib):
+    """services_state_test.go:467-478 — when the last tombstone expires the server goes away."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, s1)
+    e.write_slot(SH, (SH, 0, T0 - TOMBSTONE_LIFESPAN - MIN, TOMBSTONE))
+    e.tombstone_others(SH)
+    assert all(e.slot(SH, SH, s) is None for s in range(e.S))
+
+
+def kat_alive_lifespan(lib):
+    """services_state_test.go:480-492 — alive services are tombstoned at Updated+1s after
+    ALIVE_LIFESPAN."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, s1)
+    stamp = T0 - ALIVE_LIFESPAN - 5 * SEC
+    e.write_slot(SH, (SH, 0, stamp, ALIVE))
+    out, n = e.tombstone_others(SH)
+    assert n == 1 and tup(out[0]) == (SH, 0, stamp + SEC, TOMBSTONE)
+    assert e.slot(SH, SH, 0) == (stamp + SEC, TOMBSTONE)
+
+
+def kat_draining_lifespan(lib):
+    """services_state_test.go:494-507 — draining services expire after DRAINING_LIFESPAN."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, (SH, 0, T0, DRAINING))
+    stamp = T0 - DRAINING_LIFESPAN - 5 * SEC
+    e.write_slot(SH, (SH, 0, stamp, DRAINING))
+    e.tombstone_others(SH)
+    assert e.slot(SH, SH, 0) == (stamp + SEC, TOMBSTONE)
+
+
+def kat_draining_survives_alive_lifespan(lib):
+    """services_state_test.go:509-522 — draining services outlive ALIVE_LIFESPAN."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, (SH, 0, T0, DRAINING))
+    stamp = T0 - ALIVE_LIFESPAN - 5 * SEC
+    e.write_slot(SH, (SH, 0, stamp, DRAINING))
+    e.tombstone_others(SH)
+    assert e.slot(SH, SH, 0) == (stamp, DRAINING)
+
+
+def kat_unhealthy_unknown_lifespan(lib):
+    """services_state_test.go:524-541 — UNHEALTHY and UNKNOWN use the alive lifespan."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entries([SH, SH], [(SH, 3, T0, UNHEALTHY), (SH, 4, T0, UNKNOWN)])
+    stamp = T0 - ALIVE_LIFESPAN - 5 * SEC
+    e.write_slot(SH, (SH, 3, stamp, UNHEALTHY))
+    e.write_slot(SH, (SH, 4, stamp, UNKNOWN))
+    e.tombstone_others(SH)
+    assert e.slot(SH, SH, 3)[1] == TOMBSTONE and e.slot(SH, SH, 4)[1] == TOMBSTONE
+
+
+def kat_tombstones_not_retombstoned(lib):
+    """services_state_test.go:543-550 — tombstones aren't re-tombstoned."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, (SH, 5, T0, TOMBSTONE))
+    out, n = e.tombstone_others(SH)
+    assert n == 0 and out == []
+
+
+def kat_is_new_service(lib):
+    """services_state_test.go:552-559 — a status change makes a service new."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, (SH, 0, T0, UNHEALTHY))
+    assert e.is_new_service(SH, (SH, 0, T0, ALIVE))
+
+
+def kat_tombstone_not_new(lib):
+    """services_state_test.go:561-568 — tombstones are not called new services."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, (SH, 0, T0, UNHEALTHY))
+    assert not e.is_new_service(SH, (SH, 0, T0, TOMBSTONE))
+
+
+# Test_ClusterMembershipManagement
+def kat_expire_server_tombstones_all(lib):
+    """services_state_test.go:691-714 — ExpireServer tombstones all services of the host and
+    announces them (2 records, Status 1)."""
+    e = mk(lib)
+    e.add_service_entries([SH, SH], [(SH, 0, T0, ALIVE), (SH, 1, T0, ALIVE)])
+    assert e.expire_server(SH, SH)
+    b = e.get_broadcasts(SH)
+    assert len(b) == 2 and all(x.status == TOMBSTONE and x.updated_ns == T0 for x in b)
+    assert e.slot(SH, SH, 0) == (T0, TOMBSTONE) and e.slot(SH, SH, 1) == (T0, TOMBSTONE)
+    # TOMBSTONE_COUNT passes, each +50ns
+    n = 1
+    while e.get_broadcasts(SH) is not None:
+        n += 1
+    assert n == 10
+
+
+def kat_expire_server_no_services(lib):
+    """services_state_test.go:716-720 — no announcement for a host with no services."""
+    e = mk(lib)
+    assert not e.expire_server(SH, SH)
+    assert e.queue(SH) == []
+
+
+def kat_expire_server_only_tombstones(lib):
+    """services_state_test.go:722-729 — no announcement for a host with no live services."""
+    e = mk(lib)
+    e.add_service_entry(SH, (SH, 0, T0, TOMBSTONE))
+    assert not e.expire_server(SH, SH)
+    assert len(e.local_state(SH)) == 1 and e.queue(SH) == []
+
+
+# ------------------------------------------------------------------------ service/service_test.go
+def kat_is_stale(lib):
+    """service/service_test.go:142-159 — IsStale: with a 1h lifespan, now-1h-2min is stale; with
+    a 62min lifespan, now-1h is not."""
+    e = mk(lib, tombstone_lifespan_ns=HOUR)
+    now = e.now()
+    assert e.add_service_entry(LOCAL, (CH, 0, now - HOUR - 2 * MIN, ALIVE)) == 0
+    e2 = mk(lib, tombstone_lifespan_ns=62 * MIN)
+    assert e2.add_service_entry(LOCAL, (CH, 0, now - HOUR, ALIVE)) == 1
+
+
+# ---------------------------------------------------------------------- services_delegate_test.go
+# Fixture records (services_delegate_test.go:15-20): byte lengths drive packPacket.
+_FIX = {
+    "d419": '{"ID":"d419fa7ad1a7","Name":"/dockercon-6adfe629eebc91","Image":"nginx:latest","Created":"2015-02-25T19:04:46Z","Hostname":"docker2","Ports":[{"Type":"tcp","Port":10234}],"Updated":"2015-03-04T01:12:46.669648453Z","Status":0}',
+    "dead": '{"ID":"deadbeefabba","Name":"/dockercon-6c01869525db08","Image":"nginx:latest","Created":"2015-02-25T19:04:46Z","Hostname":"docker2","Ports":[{"Type":"tcp","Port":10234}],"Updated":"2015-03-04T01:12:46.669648453Z","Status":0}',
+    "1b32": '{"ID":"1b3295bf300f","Name":"/romantic_brown","Image":"0415448f2cc2","Created":"2014-10-02T23:58:48Z","Hostname":"docker1","Ports":[{"Type":"tcp","Port":9494}],"Updated":"2015-03-04T01:12:32.630357657Z","Status":0}',
+}
+
+
+def _ns(iso):
+    head, frac = iso.rstrip("Z").split(".")
+    d = _dt.datetime.strptime(head, "%Y-%m-%dT%H:%M:%S").replace(tzinfo=_dt.timezone.utc)
+    return int(d.timestamp()) * SEC + int(frac.ljust(9, "0"))
+
+
+_T46 = _ns("2015-03-04T01:12:46.669648453Z")
+_T32 = _ns("2015-03-04T01:12:32.630357657Z")
+BCAST = [(DOCKER2, 0, _T46, ALIVE), (DOCKER2, 1, _T46, ALIVE)]
+BCAST2 = [(DOCKER1, 0, _T32, ALIVE), (DOCKER2, 1, _T46, ALIVE)]
+_SIZE = {BCAST[0]: len(_FIX["d419"]), BCAST[1]: len(_FIX["dead"]), BCAST2[0]: len(_FIX["1b32"])}
+
+
+def records_fitting(queue, limit, overhead=3):
+    """packPacket (services_delegate.go:186-223) over byte sizes -> the record limit to pass."""
+    total = n = 0
+    for rec in queue:
+        if total + _SIZE[rec] + overhead > limit:
+            break
+        total += _SIZE[rec] + overhead
+        n += 1
+    return n
+
+
+def _delegate(lib):
+    return mk(lib, n_hosts=8, t0_ns=_T46 + 10 * SEC)
+
+
+def _set_pending(e, host, recs):
+    """delegate.pendingBroadcasts = recs, restated through the API: a batch that does not fit."""
+    e.send_services(host, recs, 1)
+    assert e.get_broadcasts(host, limit=0) is None
+    assert [tup(x) for x in e.pending(host)] == [(h, s, t, st) for h, s, t, st in recs]
+
+
+def kat_getbroadcasts_nothing(lib):
+    """services_delegate_test.go:41-43 — nil when there is nothing to send."""
+    e = _delegate(lib)
+    assert e.get_broadcasts(LOCAL, limit=records_fitting([], 1398)) is None
+
+
+def kat_getbroadcasts_pending_only(lib):
+    """services_delegate_test.go:45-52 — returns from the pending list when nothing is new."""
+    e = _delegate(lib)
+    _set_pending(e, LOCAL, [BCAST[0]])
+    r = e.get_broadcasts(LOCAL, limit=records_fitting([BCAST[0]], 1398))
+    assert [tup(x) for x in r] == [BCAST[0]]
+
+
+def kat_getbroadcasts_channel(lib):
+    """services_delegate_test.go:54-63 — returns what's in the channel."""
+    e = _delegate(lib)
+    e.send_services(LOCAL, BCAST, 1)
+    r = e.get_broadcasts(LOCAL, limit=records_fitting(BCAST, 1398))
+    assert [tup(x) for x in r] == BCAST and e.pending(LOCAL) == []
+
+
+def kat_getbroadcasts_leftover(lib):
+    """services_delegate_test.go:65-73 — returns what's left when nothing is new."""
+    e = _delegate(lib)
+    _set_pending(e, LOCAL, BCAST)
+    r = e.get_broadcasts(LOCAL, limit=records_fitting(BCAST, 1398))
+    assert [tup(x) for x in r] == BCAST and e.pending(LOCAL) == []
+
+
+def kat_getbroadcasts_new_and_left(lib):
+    """services_delegate_test.go:75-86 — what's new first, then what's left, when it fits."""
+    e = _delegate(lib)
+    _set_pending(e, LOCAL, BCAST)
+    e.send_services(LOCAL, BCAST2, 1)
+    r = e.get_broadcasts(LOCAL, limit=records_fitting(BCAST2 + BCAST, 1398))
+    assert [tup(x) for x in r] == BCAST2 + BCAST and e.pending(LOCAL) == []
+
+
+def kat_getbroadcasts_many_runs(lib):
+    """services_delegate_test.go:88-103 — many runs with leftovers (limits 100/300/100/1398)."""
+    e = _delegate(lib)
+    _set_pending(e, LOCAL, BCAST)
+    e.send_services(LOCAL, BCAST2 + BCAST, 1)
+    queue = BCAST2 + BCAST + BCAST
+    assert e.get_broadcasts(LOCAL, limit=records_fitting(queue, 100)) is None
+    r = e.get_broadcasts(LOCAL, limit=records_fitting(queue, 300))  # 1 message fits here
+    assert [tup(x) for x in r] == [BCAST2[0]]
+    queue = queue[1:]
+    assert e.get_broadcasts(LOCAL, limit=records_fitting(queue, 100)) is None
+    r = e.get_broadcasts(LOCAL, limit=records_fitting(queue, 1398))
+    assert len(r) == 5
+    assert [tup(x) for x in r][:3] == BCAST2[1:] + BCAST
+    assert e.pending(LOCAL) == []
+
+
+# --------------------------------------------------------------- round-model semantic pins
+def kat_order_dependence(lib):
+    """SURVEY.md §7 hard part: the merge is not a semilattice. old=(t1,DRAINING):
+    (t3,ALIVE) then (t2,TOMBSTONE) -> (t3,DRAINING); the reverse -> (t3,ALIVE)."""
+    t1, t2, t3 = T0 - 3 * SEC, T0 - 2 * SEC, T0 - SEC
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, t1, DRAINING))
+    e.notify_msg(LOCAL, [(CH, 0, t3, ALIVE), (CH, 0, t2, TOMBSTONE)])
+    assert e.slot(LOCAL, CH, 0) == (t3, DRAINING)
+    e2 = mk(lib)
+    e2.add_service_entry(LOCAL, (CH, 0, t1, DRAINING))
+    e2.notify_msg(LOCAL, [(CH, 0, t2, TOMBSTONE), (CH, 0, t3, ALIVE)])
+    assert e2.slot(LOCAL, CH, 0) == (t3, ALIVE)
+
+
+def kat_equal_timestamp_first_wins(lib):
+    """service.go:64-66 — Invalidates is strict: an equal timestamp keeps the first arrival."""
+    e = mk(lib)
+    e.notify_msg(LOCAL, [(CH, 0, T0, ALIVE), (CH, 0, T0, TOMBSTONE)])
+    assert e.slot(LOCAL, CH, 0) == (T0, ALIVE)
+    assert e.stats()["retransmits"] == 1
+
+
+def kat_pending_truncation(lib):
+    """services_delegate.go:109-115 — leftovers beyond MAX_PENDING_LENGTH are dropped; a batch
+    longer than packet_cap + pending_cap can never send its tail."""
+    e = mk(lib, n_hosts=4, n_services=64)
+    recs = [(h, s, T0, ALIVE) for h in range(3) for s in range(64)][:150]
+    e.send_services(LOCAL, recs, 1)
+    b = e.get_broadcasts(LOCAL)
+    assert [tup(x) for x in b] == recs[:32]
+    assert [tup(x) for x in e.pending(LOCAL)] == recs[32:132]
+    assert e.stats()["pending_drops"] == 0  # the stored list was already cut to 132
+    e.send_services(LOCAL, recs[:40], 1)
+    b = e.get_broadcasts(LOCAL)
+    assert [tup(x) for x in b] == recs[:32]
+    assert [tup(x) for x in e.pending(LOCAL)] == recs[32:40] + recs[32:124]
+    assert e.stats()["pending_drops"] == 8
+
+
+ALL = [v for k, v in sorted(globals().items()) if k.startswith("kat_")]
