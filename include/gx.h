@@ -171,7 +171,9 @@ typedef struct gx_stats {
   uint64_t ae_exchanges;     /* push-pull pairs */
   uint64_t churn_events;
   int64_t last_change_round; /* last round in which any view slot changed, -1 = none */
-  uint64_t reserved[7];
+  uint64_t scan_slots;       /* view slots streamed by expiry scans */
+  uint64_t ae_slots;         /* view slots streamed by anti-entropy merges (both directions) */
+  uint64_t reserved[5];
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */

@@ -283,6 +283,7 @@ static int add_entry(gx_engine *e, uint32_t v, grec u, int64_t now, int src) {
  * Writes the first `cap` tombstoned records to out; returns the total. */
 static uint32_t scan_view(gx_engine *e, uint32_t v, int64_t now, grec *out, uint32_t cap) {
   uint32_t n = 0;
+  e->st.scan_slots += e->R;
   uint64_t *row = &e->view[(size_t)v * e->R];
   for (uint32_t r = 0; r < e->R; r++) {
     uint64_t w = row[r];
@@ -509,6 +510,7 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
     add_entry(e, b, u, now, SRC_AE);
   }
   e->st.ae_exchanges++;
+  e->st.ae_slots += 2ull * e->R;
   free(sa);
 }
 
@@ -801,6 +803,7 @@ int gx_merge(gx_engine *e, uint32_t dst, uint32_t src) {
     grec u = {snap[r], r, 0};
     add_entry(e, dst, u, now, SRC_AE);
   }
+  e->st.ae_slots += e->R;
   free(snap);
   return GX_OK;
 }
@@ -867,7 +870,7 @@ int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32
 }
 
 int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n) {
-  if (!e || host >= e->H || (n && !list) || n > 4096) return GX_EINVAL;
+  if (!e || host >= e->H || (n && !list) || n > 64) return GX_EINVAL;
   grec *tmp = (grec *)malloc(sizeof(grec) * (n ? n : 1) * 2);
   for (uint32_t i = 0; i < n; i++)
     if (list[i].host != host || to_grec(e, &list[i], &tmp[i])) {

@@ -95,7 +95,8 @@ class GxStats(C.Structure):
         "local_accepts", "stale_drops", "retransmits", "queue_drops", "list_drops", "sleep_drops",
         "pending_drops", "dequeues", "nil_batches", "packets", "records_sent", "expired", "gc",
         "own_tombstones", "expire_server", "send_jobs", "ae_exchanges", "churn_events")] + [
-        ("last_change_round", C.c_int64), ("reserved", C.c_uint64 * 7)]
+        ("last_change_round", C.c_int64), ("scan_slots", C.c_uint64), ("ae_slots", C.c_uint64),
+        ("reserved", C.c_uint64 * 5)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}

@@ -1,0 +1,480 @@
+// gx_device.hpp — device-side data layout and scalar semantics of the sidecar-gx engine.
+//
+// Layout in HBM (one engine = one GPU = one shard of hosts; DESIGN.md "Data layout"):
+//   view      u64 [H][R]      R = H*S packed slots (ts << 3 | status), one row per host view
+//   hs        gx_host_state[H] per-host broadcast-queue / looper bookkeeping (64 B)
+//   fifo      gx_job [H][Q]   broadcast FIFO ring (the blocked senders of state.Broadcasts)
+//   sleep     gx_job [H][SQ]  SendServices passes sleeping TOMBSTONE_RETRANSMIT
+//   dq        grec [H][DQ]    delegate pendingBroadcasts as a deque (push-front batch, pop packet)
+//   arena     grec [H][A][L]  SendServices lists (L = packet_cap + pending_cap)
+//   msg       grec [H][K][cap] this round's packets, msg_len/msg_dst [H][K]
+//
+// The scalar helpers below are the one-thread-per-host form of the reference semantics. They are
+// used by the per-host round kernels (owner ticks, GetBroadcasts) and by the single-host ABI
+// entry points. The hot, data-parallel phases (gossip merge, anti-entropy, expiry scan,
+// departure storm) have their own wave/block kernels in gx_engine.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gx.h"
+
+#define GXD __device__ __forceinline__
+#define GXHD __host__ __device__ __forceinline__
+
+struct grec {
+  uint64_t w;  // packed (ts << 3) | status
+  uint32_t r;  // record key = owner * S + svc
+  uint32_t pad;
+};
+
+enum {
+  C_GOSSIP_MERGES, C_AE_MERGES, C_LOCAL_MERGES, C_GOSSIP_ACC, C_AE_ACC, C_LOCAL_ACC, C_STALE,
+  C_RETX, C_QDROP, C_LDROP, C_SDROP, C_PDROP, C_DEQ, C_NIL, C_PACKETS, C_RECSENT, C_EXPIRED,
+  C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_NCTR
+};
+
+struct DevCtr {
+  unsigned long long c[32];
+  unsigned long long last_change_p1;  // last round with a slot change, + 1 (0 = none)
+};
+
+enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
+enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5, ST_INIT_AGE = 6,
+       ST_AE = 7 };
+
+struct Dev {
+  gx_params p;
+  uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  int64_t round, now;
+  int partitioned;
+  uint64_t *view;
+  uint8_t *own_status;
+  gx_host_state *hs;
+  gx_job *fifo;
+  gx_job *sleep;
+  grec *dq;
+  grec *arena;
+  uint32_t *arena_len;
+  grec *msg;
+  uint32_t *msg_len;
+  uint32_t *msg_dst;
+  uint32_t *in_cnt;    // [H+1] receiver counts, then exclusive offsets
+  uint32_t *in_cur;    // [H] fill cursors
+  uint32_t *in_fill;   // [H*K] entries in arrival order (atomic fill)
+  uint32_t *in_sorted; // [H*K] entries sender-ordered per receiver
+  grec *scan_list;     // [H][L] first L expired records of this round's scan
+  uint32_t *scan_cnt;  // [H]
+  uint8_t *tick;       // [H] BroadcastTombstones tick this round
+  DevCtr *ctr;
+};
+
+// ------------------------------------------------------------------- schedule RNG (seeded) --
+GXHD uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+GXHD uint64_t rng4(uint64_t seed, uint64_t stream, uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t h = mix64(seed ^ (stream * 0xD1B54A32D192ED03ull));
+  h = mix64(h ^ a);
+  h = mix64(h ^ b);
+  return mix64(h ^ c);
+}
+GXHD uint32_t unif(uint64_t x, uint32_t m) { return (uint32_t)(((x >> 32) * (uint64_t)m) >> 32); }
+GXHD int st_of(uint64_t w) { return (int)(w & 7u); }
+GXHD int64_t ts_of(uint64_t w) { return (int64_t)(w >> GX_TS_SHIFT); }
+GXHD uint64_t pack(int64_t ts, int st) { return ((uint64_t)ts << GX_TS_SHIFT) | (uint64_t)st; }
+GXHD uint32_t meta_of(int kind, uint32_t pass, uint32_t np) {
+  return (uint32_t)kind | (pass << 8) | (np << 16);
+}
+
+// Push-pull pairing bijection on [0, m): 4-round keyed Feistel + cycle walking.
+GXHD uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
+  uint32_t b = 0;
+  while ((1u << b) < m) b++;
+  uint32_t hb = (b + 1) / 2;
+  if (hb == 0) hb = 1;
+  uint32_t hmask = (1u << hb) - 1;
+  uint32_t x = q;
+  do {
+    uint32_t L = x >> hb, Rr = x & hmask;
+    for (uint32_t i = 0; i < 4; i++) {
+      uint32_t F = (uint32_t)(mix64(key ^ ((uint64_t)i << 32) ^ Rr)) & hmask;
+      uint32_t t = Rr;
+      Rr = L ^ F;
+      L = t;
+    }
+    x = (L << hb) | Rr;
+  } while (x >= m);
+  return x;
+}
+
+// ------------------------------------------------------------------------------ counters --
+GXD void ctr_add(const Dev &d, int i, unsigned long long v) {
+  if (v) atomicAdd(&d.ctr->c[i], v);
+}
+GXD void mark_change(const Dev &d) { atomicMax(&d.ctr->last_change_p1, (unsigned long long)(d.round + 1)); }
+GXD void set_slot(const Dev &d, uint64_t *slot, uint64_t nw) {
+  if (*slot != nw) {
+    *slot = nw;
+    mark_change(d);
+  }
+}
+
+// ----------------------------------------------------------------------- broadcast FIFO --
+GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
+  if ((j.meta & 0xff) == GX_JOB_SEND) d.hs[v].arena_used &= ~(1u << (j.c & 0xffff));
+}
+
+// The unbuffered Broadcasts channel's blocked senders (services_state.go:94) as a FIFO bounded
+// at Q jobs, 2 reserved for the loopers' nil sends.
+GXD bool push_job(const Dev &d, uint32_t v, const gx_job &j) {
+  gx_host_state *h = &d.hs[v];
+  uint32_t count = h->fifo_tail - h->fifo_head;
+  bool nil = (j.meta & 0xff) <= GX_JOB_NIL_BT;
+  uint32_t limit = nil ? d.Q : d.Q - 2;
+  if (count >= limit) {
+    ctr_add(d, C_QDROP, 1);
+    free_list(d, v, j);
+    return false;
+  }
+  d.fifo[(size_t)v * d.Q + (h->fifo_tail % d.Q)] = j;
+  h->fifo_tail++;
+  return true;
+}
+
+GXD void push_sleep(const Dev &d, uint32_t v, const gx_job &j) {
+  gx_host_state *h = &d.hs[v];
+  if (h->sleep_tail - h->sleep_head >= d.SQ) {
+    ctr_add(d, C_SDROP, 1);
+    free_list(d, v, j);
+    return;
+  }
+  d.sleep[(size_t)v * d.SQ + (h->sleep_tail % d.SQ)] = j;
+  h->sleep_tail++;
+}
+
+// TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO tail.
+GXD void wake_host(const Dev &d, uint32_t v) {
+  gx_host_state *h = &d.hs[v];
+  while (h->sleep_head != h->sleep_tail) {
+    gx_job j = d.sleep[(size_t)v * d.SQ + (h->sleep_head % d.SQ)];
+    if ((int64_t)j.wake > d.round) break;
+    h->sleep_head++;
+    push_job(d, v, j);
+  }
+}
+
+// Lowest free list slot, or -1 (list_drops).
+GXD int alloc_list(const Dev &d, uint32_t v) {
+  uint32_t used = d.hs[v].arena_used;
+  uint32_t free_bits = ~used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1));
+  if (!free_bits) {
+    ctr_add(d, C_LDROP, 1);
+    return -1;
+  }
+  int slot = __builtin_ctz(free_bits);
+  d.hs[v].arena_used = used | (1u << slot);
+  return slot;
+}
+GXD grec *list_ptr(const Dev &d, uint32_t v, uint32_t slot) {
+  return &d.arena[((size_t)v * d.A + slot) * d.L];
+}
+// SendServices job over an allocated, filled list (services_state.go:579-604).
+GXD void commit_send(const Dev &d, uint32_t v, int slot, uint32_t n, uint32_t npasses) {
+  d.arena_len[(size_t)v * d.A + slot] = n;
+  gx_job j;
+  j.a = 0;
+  j.b = 0;
+  j.c = (uint32_t)slot | (n << 16);
+  j.meta = meta_of(GX_JOB_SEND, 0, npasses);
+  j.wake = 0;
+  j.aux = 0;
+  ctr_add(d, C_SENDJOBS, 1);
+  push_job(d, v, j);
+}
+
+GXD uint32_t job_len(const Dev &d, const gx_job &j) {
+  uint32_t kind = j.meta & 0xff;
+  if (kind == GX_JOB_RETX) return 1;
+  if (kind == GX_JOB_SEND) return j.c >> 16;
+  if (kind == GX_JOB_EXPIRE) return (uint32_t)__popcll(j.b);
+  return 0;
+}
+
+// Record i of pass `pass` of a job: Updated + pass * 50ns (services_state.go:588-599).
+GXD grec job_rec(const Dev &d, uint32_t v, const gx_job &j, uint32_t i, uint32_t &bit_cursor) {
+  uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff;
+  uint64_t dw = ((uint64_t)pass * (uint64_t)d.p.pass_increment_ns) << GX_TS_SHIFT;
+  grec g;
+  g.pad = 0;
+  if (kind == GX_JOB_RETX) {
+    g.w = j.a;
+    g.r = j.c;
+  } else if (kind == GX_JOB_SEND) {
+    grec s = list_ptr(d, v, j.c & 0xffff)[i];
+    g.w = s.w + dw;
+    g.r = s.r;
+  } else {  // EXPIRE: i-th set bit of the mask, walked with a cursor
+    uint64_t m = j.b >> bit_cursor;
+    uint32_t s = bit_cursor + (uint32_t)__builtin_ctzll(m);
+    bit_cursor = s + 1;
+    g.w = pack((int64_t)j.a, GX_TOMBSTONE) + dw;
+    g.r = j.c * d.S + s;
+  }
+  return g;
+}
+
+// GetBroadcasts(overhead, limit) + packPacket (services_delegate.go:85-144, :186-223).
+GXD uint32_t get_broadcasts(const Dev &d, uint32_t v, uint32_t limit, grec *packet) {
+  gx_host_state *h = &d.hs[v];
+  uint32_t m = 0;
+  uint32_t mask = d.DQ - 1;
+  grec *dq = &d.dq[(size_t)v * d.DQ];
+  if (h->fifo_head != h->fifo_tail) {
+    gx_job j = d.fifo[(size_t)v * d.Q + (h->fifo_head % d.Q)];
+    h->fifo_head++;
+    ctr_add(d, C_DEQ, 1);
+    m = job_len(d, j);
+    // broadcast = batch ++ pendingBroadcasts: push the batch to the deque front
+    uint32_t head = (h->dq_head - m) & mask;
+    uint32_t cur = 0;
+    for (uint32_t i = 0; i < m; i++) dq[(head + i) & mask] = job_rec(d, v, j, i, cur);
+    h->dq_head = head;
+    h->dq_len += m;
+    uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff, np = (j.meta >> 16) & 0xff;
+    if (kind == GX_JOB_NIL_BS) {
+      ctr_add(d, C_NIL, 1);
+      h->flags &= ~1u;
+      h->bs_next = d.round + d.p.alive_interval_rounds;
+    } else if (kind == GX_JOB_NIL_BT) {
+      ctr_add(d, C_NIL, 1);
+      h->flags &= ~2u;
+      h->bt_next = d.round + d.p.tombstone_interval_rounds;
+    } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
+      if (pass + 1 < np) {
+        j.meta = meta_of((int)kind, pass + 1, np);
+        if (d.p.retransmit_rounds == 0) {
+          j.wake = (uint32_t)d.round;
+          push_job(d, v, j);
+        } else {
+          j.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
+          push_sleep(d, v, j);
+        }
+      } else {
+        free_list(d, v, j);
+      }
+    }
+  } else if (h->dq_len == 0) {
+    return 0;
+  }
+  uint32_t l = h->dq_len < limit ? h->dq_len : limit;
+  for (uint32_t i = 0; i < l; i++) packet[i] = dq[(h->dq_head + i) & mask];
+  h->dq_head = (h->dq_head + l) & mask;
+  h->dq_len -= l;
+  if (h->dq_len > d.p.pending_cap) {
+    ctr_add(d, C_PDROP, h->dq_len - d.p.pending_cap);
+    h->dq_len = d.p.pending_cap;
+  }
+  if (l) {
+    ctr_add(d, C_PACKETS, 1);
+    ctr_add(d, C_RECSENT, l);
+  }
+  return l;
+}
+
+// ------------------------------------------------------------------------ merge rule (a-5) --
+// AddServiceEntry core on one slot word (services_state.go:293-347): returns the new word and
+// sets *acc when the record was stored; *stale when IsStale dropped it (service.go:68-72).
+GXD uint64_t merge_word(const Dev &d, uint64_t old, uint64_t u, bool &acc, bool &stale) {
+  int64_t ts = ts_of(u);
+  acc = false;
+  stale = false;
+  if (ts < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns) {
+    stale = true;
+    return old;
+  }
+  if (st_of(old) == GX_ABSENT) {
+    acc = true;
+    return u;
+  }
+  if (ts > ts_of(old)) {
+    int st = st_of(u);
+    if (st_of(old) == GX_DRAINING && st == GX_ALIVE) st = GX_DRAINING;
+    acc = true;
+    return pack(ts, st);
+  }
+  return old;
+}
+
+GXD bool add_entry(const Dev &d, uint32_t v, grec u, int src) {
+  ctr_add(d, src == SRC_GOSSIP ? C_GOSSIP_MERGES : src == SRC_AE ? C_AE_MERGES : C_LOCAL_MERGES, 1);
+  uint64_t *slot = &d.view[(size_t)v * d.R + u.r];
+  bool acc, stale;
+  uint64_t nw = merge_word(d, *slot, u.w, acc, stale);
+  if (stale) {
+    ctr_add(d, C_STALE, 1);
+    return false;
+  }
+  if (!acc) return false;
+  set_slot(d, slot, nw);
+  ctr_add(d, src == SRC_GOSSIP ? C_GOSSIP_ACC : src == SRC_AE ? C_AE_ACC : C_LOCAL_ACC, 1);
+  if (u.r / d.S != v) {  // retransmit foreign records only (services_state.go:377-392)
+    gx_job j;
+    j.a = nw;
+    j.b = 0;
+    j.c = u.r;
+    j.meta = meta_of(GX_JOB_RETX, 0, 1);
+    j.wake = 0;
+    j.aux = 0;
+    if (push_job(d, v, j)) ctr_add(d, C_RETX, 1);
+  }
+  return true;
+}
+
+// Expiry rule of TombstoneOthersServices on one slot (services_state.go:645-679).
+// Returns the new word; *expired when it was tombstoned by lifespan, *gc when removed.
+GXD uint64_t expiry_word(const Dev &d, uint64_t w, bool &expired, bool &gc) {
+  expired = false;
+  gc = false;
+  int st = st_of(w);
+  if (st == GX_ABSENT) return w;
+  int64_t ts = ts_of(w);
+  if (st == GX_TOMBSTONE) {
+    if (ts < d.now - d.p.tombstone_lifespan_ns) {
+      gc = true;
+      return GX_SLOT_ABSENT;
+    }
+    return w;
+  }
+  int64_t life = st == GX_DRAINING ? d.p.draining_lifespan_ns : d.p.alive_lifespan_ns;
+  if (ts < d.now - life) {
+    expired = true;
+    return pack(ts + d.p.tombstone_bump_ns, GX_TOMBSTONE);
+  }
+  return w;
+}
+
+// TombstoneServices(self, list) on the owner's own slots (services_state.go:685-715).
+// Returns the mask of services tombstoned (each contributes the record twice).
+GXD uint64_t tombstone_services(const Dev &d, uint32_t o, uint64_t running) {
+  uint64_t *row = &d.view[(size_t)o * d.R + (size_t)o * d.S];
+  uint64_t m = 0;
+  for (uint32_t s = 0; s < d.S; s++) {
+    uint64_t w = row[s];
+    if (st_of(w) == GX_ABSENT || ((running >> s) & 1ull) || st_of(w) == GX_TOMBSTONE) continue;
+    set_slot(d, &row[s], pack(d.now, GX_TOMBSTONE));
+    m |= 1ull << s;
+  }
+  ctr_add(d, C_OWNTOMB, (unsigned long long)__popcll(m));
+  return m;
+}
+
+// ExpireServer (services_state.go:150-192) for one (viewer, owner).
+GXD bool expire_server(const Dev &d, uint32_t v, uint32_t o) {
+  uint64_t *row = &d.view[(size_t)v * d.R + (size_t)o * d.S];
+  uint64_t mask = 0;
+  bool live = false;
+  for (uint32_t s = 0; s < d.S; s++) {
+    int st = st_of(row[s]);
+    if (st == GX_ABSENT) continue;
+    mask |= 1ull << s;
+    if (st != GX_TOMBSTONE) live = true;
+  }
+  if (!live) return false;
+  for (uint32_t s = 0; s < d.S; s++)
+    if ((mask >> s) & 1ull) set_slot(d, &row[s], pack(d.now, GX_TOMBSTONE));
+  ctr_add(d, C_EXPSRV, 1);
+  gx_job j;
+  j.a = (uint64_t)d.now;
+  j.b = mask;
+  j.c = o;
+  j.meta = meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count);
+  j.wake = 0;
+  j.aux = 0;
+  push_job(d, v, j);
+  return true;
+}
+
+GXD bool is_new(const Dev &d, uint32_t o, uint64_t sw, uint32_t r) {
+  uint64_t w = d.view[(size_t)o * d.R + r];
+  return st_of(w) == GX_ABSENT || (st_of(sw) != GX_TOMBSTONE && st_of(sw) != st_of(w));
+}
+
+// BroadcastServices looper body (services_state.go:525-574) over fn() = list (n <= 64).
+// Sets inc = bit i for each list element handed to SendServices (0 = a nil was sent).
+GXD void bs_body_list(const Dev &d, uint32_t o, const grec *list, uint32_t n, uint64_t &inc_out) {
+  gx_host_state *h = &d.hs[o];
+  bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > h->last_bcast_ns;  // (:547)
+  bool any_new = false;
+  uint64_t inc = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (is_new(d, o, list[i].w, list[i].r)) {  // IsNewService (:509-521)
+      any_new = true;
+      inc |= 1ull << i;
+    } else if (refresh) {
+      inc |= 1ull << i;
+    }
+  }
+  inc_out = inc;
+  if (inc) {
+    h->last_bcast_ns = d.now;
+    int slot = alloc_list(d, o);
+    if (slot >= 0) {
+      grec *dst = list_ptr(d, o, slot);
+      uint32_t m = 0;
+      for (uint32_t i = 0; i < n && m < d.L; i++)
+        if ((inc >> i) & 1ull) dst[m++] = list[i];
+      commit_send(d, o, slot, m, any_new ? d.p.alive_count : 1);  // ALIVE_COUNT if new (:555-558)
+    }
+  } else {
+    gx_job j;
+    j.a = 0;
+    j.b = 0;
+    j.c = 0;
+    j.meta = meta_of(GX_JOB_NIL_BS, 0, 1);
+    j.wake = 0;
+    j.aux = 0;
+    push_job(d, o, j);  // Broadcasts <- nil (:569): the looper blocks until it is consumed
+    h->flags |= 1u;
+  }
+}
+
+// Second half of the BroadcastTombstones body (services_state.go:613-629), after the view scan
+// put the first L expired records in scan_list[o] and the total in scan_cnt[o].
+GXD void bt_finish(const Dev &d, uint32_t o, uint64_t running, const grec *others, uint32_t n_others) {
+  gx_host_state *h = &d.hs[o];
+  uint64_t own = tombstone_services(d, o, running);
+  uint32_t n_own = 2u * (uint32_t)__popcll(own);
+  if (n_own + n_others > 0) {
+    int slot = alloc_list(d, o);
+    if (slot >= 0) {
+      grec *dst = list_ptr(d, o, slot);
+      uint32_t m = 0;
+      uint64_t w = pack(d.now, GX_TOMBSTONE);
+      for (uint32_t s = 0; s < d.S && m < d.L; s++)
+        if ((own >> s) & 1ull)
+          for (int k = 0; k < 2 && m < d.L; k++) {
+            dst[m].w = w;
+            dst[m].r = o * d.S + s;
+            dst[m].pad = 0;
+            m++;
+          }
+      for (uint32_t i = 0; i < n_others && m < d.L; i++) dst[m++] = others[i];
+      commit_send(d, o, slot, m, d.p.tombstone_count);
+    }
+    h->bt_next = d.round + d.p.tombstone_interval_rounds;
+  } else {
+    gx_job j;
+    j.a = 0;
+    j.b = 0;
+    j.c = 0;
+    j.meta = meta_of(GX_JOB_NIL_BT, 0, 1);
+    j.wake = 0;
+    j.aux = 0;
+    push_job(d, o, j);
+    h->flags |= 2u;
+  }
+}

@@ -1,0 +1,139 @@
+"""HIP engine vs CPU oracle: bit-exact views, host bookkeeping, queue digests and counters.
+
+Round-model scenarios at sizes the oracle runs in seconds (cfg 1 = 64 hosts x 8 services,
+fanout 3, plus edge configurations), and a seeded fuzz of the single-host ABI calls.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from sidecar_amd.abi import (ALIVE, DRAINING, INIT_EMPTY, INIT_OWN, INIT_WARM, TOMBSTONE, UNHEALTHY,
+                             Engine, default_params)
+from tests.parity import assert_same
+
+pytestmark = pytest.mark.gpu
+
+SCENARIOS = {
+    "cfg1_empty": dict(n_hosts=64, n_services=8, init_mode=INIT_EMPTY),
+    "cfg1_own_ae": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, ae_period_rounds=10),
+    "cfg1_storm": dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, ae_period_rounds=10,
+                       partition_start=0, partition_end=50, storm_round=5, queue_cap=4096),
+    "cfg1_churn_aged": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, churn_ppm=50000,
+                            aged_ppm=50000, ae_period_rounds=20, ae_phase=7),
+    "tight_bounds": dict(n_hosts=48, n_services=8, init_mode=INIT_WARM, queue_cap=12, list_slots=2,
+                         pending_cap=5, packet_cap=4, ae_period_rounds=10, storm_round=3,
+                         partition_start=0, partition_end=20, churn_ppm=100000),
+    "odd_sizes": dict(n_hosts=37, n_services=3, init_mode=INIT_OWN, fanout=5, ae_period_rounds=7,
+                      ae_phase=3, partition_start=10, partition_end=30, churn_ppm=30000),
+    "s64": dict(n_hosts=24, n_services=64, init_mode=INIT_EMPTY, ae_period_rounds=15, churn_ppm=20000),
+    "retransmit0_nostop": dict(n_hosts=40, n_services=6, init_mode=INIT_EMPTY, retransmit_rounds=0,
+                               gossip_stop_on_empty=0, fanout=4),
+    "tiny_h2": dict(n_hosts=2, n_services=2, init_mode=INIT_OWN, ae_period_rounds=3),
+    "h1": dict(n_hosts=1, n_services=4, init_mode=INIT_EMPTY),
+    "high_fanout": dict(n_hosts=20, n_services=4, init_mode=INIT_OWN, fanout=16, packet_cap=8),
+}
+
+
+def pair(oracle_lib, gx_lib, **kw):
+    po = default_params(oracle_lib, **kw)
+    pg = default_params(gx_lib, **kw)
+    return Engine(pg, lib=gx_lib), Engine(po, lib=oracle_lib)
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_round_model_parity(oracle_lib, gx_lib, name):
+    g, o = pair(oracle_lib, gx_lib, **SCENARIOS[name])
+    assert_same(g, o, f"{name} init")
+    for chunk in (1, 4, 10, 35, 50, 150, 200):
+        g.run_rounds(chunk)
+        o.run_rounds(chunk)
+        assert_same(g, o, f"{name} round {g.round}")
+    assert g.converged() == o.converged()
+
+
+def test_cfg2_small_parity(oracle_lib, gx_lib):
+    """A 1024 x 16 cluster with anti-entropy, churn and expiry-age records."""
+    kw = dict(n_hosts=1024, n_services=16, init_mode=INIT_OWN, ae_period_rounds=10, churn_ppm=20000,
+              aged_ppm=20000, queue_cap=512)
+    g, o = pair(oracle_lib, gx_lib, **kw)
+    for chunk in (3, 9, 12):
+        g.run_rounds(chunk)
+        o.run_rounds(chunk)
+        assert_same(g, o, f"cfg2-small round {g.round}")
+
+
+def test_fuzz_single_host_api(oracle_lib, gx_lib):
+    """Seeded random sequences of the ServicesState / delegate entry points."""
+    rnd = random.Random(1234)
+    H, S = 12, 6
+    g, o = pair(oracle_lib, gx_lib, n_hosts=H, n_services=S, queue_cap=40, list_slots=4, pending_cap=20,
+                packet_cap=6, init_mode=INIT_OWN)
+    T0 = g.now(0)
+    for step in range(400):
+        op = rnd.randrange(12)
+        now = g.now()
+        rec = lambda: (rnd.randrange(H), rnd.randrange(S), now - rnd.randrange(0, 200) * 10**9 + rnd.randrange(3) * 50,
+                       rnd.choice([ALIVE, TOMBSTONE, UNHEALTHY, DRAINING]))
+        if op == 0:
+            items = [rec() for _ in range(rnd.randrange(1, 20))]
+            views = [rnd.randrange(H) for _ in items]
+            assert g.add_service_entries(views, items) == o.add_service_entries(views, items)
+        elif op == 1:
+            h = rnd.randrange(H)
+            items = [rec() for _ in range(rnd.randrange(0, 12))]
+            g.notify_msg(h, items)
+            o.notify_msg(h, items)
+        elif op == 2:
+            h = rnd.randrange(H)
+            lim = rnd.choice([None, 0, 1, 3, 6])
+            a, b = g.get_broadcasts(h, lim), o.get_broadcasts(h, lim)
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert [x.tup() for x in a] == [x.tup() for x in b]
+        elif op == 3:
+            v, w = rnd.randrange(H), rnd.randrange(H)
+            assert g.expire_server(v, w) == o.expire_server(v, w)
+        elif op == 4:
+            h = rnd.randrange(H)
+            items = [rec() for _ in range(rnd.randrange(0, 40))]
+            np_ = rnd.randrange(1, 4)
+            g.send_services(h, items, np_)
+            o.send_services(h, items, np_)
+        elif op == 5:
+            h = rnd.randrange(H)
+            items = [(h, s, now, rnd.choice([ALIVE, UNHEALTHY])) for s in sorted(rnd.sample(range(S), rnd.randrange(0, S + 1)))]
+            g.broadcast_services(h, items)
+            o.broadcast_services(h, items)
+        elif op == 6:
+            h = rnd.randrange(H)
+            items = [(h, s, now, ALIVE) for s in sorted(rnd.sample(range(S), rnd.randrange(0, S + 1)))]
+            g.broadcast_tombstones(h, items)
+            o.broadcast_tombstones(h, items)
+        elif op == 7:
+            v = rnd.randrange(H)
+            a, na = g.tombstone_others(v)
+            b, nb = o.tombstone_others(v)
+            assert na == nb and [x.tup() for x in a] == [x.tup() for x in b]
+        elif op == 8:
+            d, s_ = rnd.randrange(H), rnd.randrange(H)
+            g.merge(d, s_)
+            o.merge(d, s_)
+        elif op == 9:
+            r = g.round + rnd.randrange(0, 8)
+            g.set_round(r)
+            o.set_round(r)
+        elif op == 10:
+            n = rnd.randrange(1, 6)
+            g.run_rounds(n)
+            o.run_rounds(n)
+        else:
+            h = rnd.randrange(H)
+            run = sorted(rnd.sample(range(S), rnd.randrange(0, S + 1)))
+            a = g.tombstone_services(h, run)
+            b = o.tombstone_services(h, run)
+            assert [x.tup() for x in a] == [x.tup() for x in b]
+        if step % 20 == 19:
+            assert_same(g, o, f"fuzz step {step}")
+    assert_same(g, o, "fuzz end")
+    assert T0 <= g.now()
