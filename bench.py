@@ -1,0 +1,227 @@
+"""Benchmark: record-merges/sec and rounds-to-converge wall time of the gossip-convergence engine.
+
+A step is one gossip round of the seeded schedule (DESIGN.md "Round model"). The default workload
+is BASELINE.json's headline configuration, H=32768 hosts x S=16 services (cfg 5): a converged
+catalog is split into two halves for 50 rounds, every host NotifyLeave()s the other half after 5
+rounds (ExpireServer storm), the partition heals, and memberlist push-pull anti-entropy runs every
+10 rounds. All state is resident in HBM; the timed region is `gx_run_rounds(K)`.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config cfg5|cfg2|cfg3|cfg4] [--no-converge]
+
+Prints ONE JSON line (rank 0). N>1 runs one process per GPU (torch.distributed.run); each GPU
+simulates an independent replica cluster with its own seed (DESIGN.md "Multi-GPU"), so the
+per-GPU work is fixed (weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "record-merges/sec (whole node) + rounds-to-converge wall time, H=32768 S=16"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # BASELINE.json configs[4]: 32768 x 16, 2-way partition for 50 rounds, departure storm, heal
+    "cfg5": dict(desc="32768 hosts x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds "
+                      "[0,50) + ExpireServer storm at round 5 + heal, push-pull every 10 rounds",
+                 p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
+                        queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                        partition_end=50, storm_round=5, ae_period_rounds=10)),
+    # configs[1]: 4096 x 16, fanout 3, cap 32, one GPU (cold start: every view knows its own records)
+    "cfg2": dict(desc="4096 hosts x 16 services, fanout 3, cap 32 records/msg, own-records start, "
+                      "push-pull every 10 rounds",
+                 p=dict(n_hosts=4096, n_services=16, fanout=3, packet_cap=32, queue_cap=4096,
+                        init_mode=1, ae_period_rounds=10)),
+    # configs[2]: 16384 x 16 with 5% churn/round and alive-lifespan expiry
+    "cfg3": dict(desc="16384 hosts x 16 services, 5% of owners start/stop a service per round, 5% of "
+                      "records aged U[0,100s] (alive-lifespan expiry), push-pull every 10 rounds",
+                 p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2,
+                        churn_ppm=50000, aged_ppm=50000, ae_period_rounds=10)),
+    # configs[3]: 8192 x 64, push-pull every 10 rounds
+    "cfg4": dict(desc="8192 hosts x 64 services, push-pull full-state merge every 10 rounds",
+                 p=dict(n_hosts=8192, n_services=64, fanout=3, queue_cap=4096, init_mode=1,
+                        ae_period_rounds=10)),
+    # small plumbing case (configs[0]); also the CPU-baseline scale model
+    "cfg1": dict(desc="64 hosts x 8 services, fanout 3", p=dict(n_hosts=64, n_services=8, fanout=3,
+                                                                queue_cap=4096, init_mode=0)),
+}
+
+KNAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge"]
+
+
+def make_engine(lib, cfg, seed, device):
+    from sidecar_amd.abi import Engine, default_params
+    p = default_params(lib, **CONFIGS[cfg]["p"])
+    p.seed = seed
+    p.device = device
+    return Engine(p, lib=lib)
+
+
+def merges(st):
+    return st["gossip_merges"] + st["ae_merges"] + st["local_merges"]
+
+
+def run_converge(lib, cfg, seed, device, max_rounds, check_every):
+    """Fresh engine from round 0: chunks of `check_every` rounds, catalog agreement checked
+    between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run)."""
+    e = make_engine(lib, cfg, seed, device)
+    wall = 0.0
+    conv = None
+    try:
+        while e.round < max_rounds:
+            t0 = time.perf_counter()
+            e.run_rounds(check_every)
+            wall += time.perf_counter() - t0
+            ok, _ = e.converged()
+            if ok:
+                lc = e.stats()["last_change_round"]
+                conv = lc + 1  # the catalog stopped changing after round lc and agrees
+                # wall to convergence: the rounds past the convergence point are excluded pro rata
+                wall = wall * conv / e.round if e.round else wall
+                break
+        return conv, wall, e.round
+    finally:
+        e.close()
+
+
+def cpu_baseline(cfg, seconds):
+    """The CPU oracle (single thread) on a bounded sample of the same scenario, scaled down in H
+    so it runs ~`seconds` of CPU work. Returns the cpu_baseline object."""
+    from sidecar_amd.abi import Engine, default_params
+    from tests.oracle_lib import load_oracle
+    orc = load_oracle()
+    p = dict(CONFIGS[cfg]["p"])
+    h_sample = min(p["n_hosts"], 2048)
+    p["n_hosts"] = h_sample
+    pr = default_params(orc, **p)
+    e = Engine(pr, lib=orc)
+    t0 = time.perf_counter()
+    st0 = e.stats()
+    while time.perf_counter() - t0 < seconds:
+        e.run_rounds(10)
+    dt = time.perf_counter() - t0
+    st = e.stats()
+    m = merges(st) - merges(st0)
+    e.close()
+    return {"value": m / dt, "unit": "record-merges/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/gx_oracle.c single-threaded, same {cfg} schedule at H={h_sample} "
+                      f"(S={p['n_services']}), rounds 0..{st['round']} in {dt:.1f}s; "
+                      f"Go reference unavailable (no Go toolchain on the box)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg5", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--no-converge", action="store_true")
+    ap.add_argument("--converge-max", type=int, default=3000)
+    ap.add_argument("--check-every", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    from sidecar_amd.abi import load_product
+    lib = load_product()
+    seed = args.seed + 7919 * rank
+    e = make_engine(lib, args.config, seed, local_rank)
+    e.enable_timing(True)
+    if args.warmup:
+        e.run_rounds(args.warmup)
+    st0, tm0 = e.stats(), e.timing()
+    barrier()
+    t0 = time.perf_counter()
+    e.run_rounds(args.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    st1, tm1 = e.stats(), e.timing()
+    e.close()
+
+    local_merges = merges(st1) - merges(st0)
+    split = {k: st1[k] - st0[k] for k in ("gossip_merges", "ae_merges", "local_merges")}
+    dt_max = dt
+    tot_merges = local_merges
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_max = float(t.item())
+        m = torch.tensor([local_merges], dtype=torch.float64, device="cuda")
+        dist.all_reduce(m, op=dist.ReduceOp.SUM)
+        tot_merges = int(m.item())
+
+    kern = {}
+    for i, k in enumerate(KNAMES):
+        ms = tm1[k]["ms"] - tm0[k]["ms"]
+        nl = tm1[k]["launches"] - tm0[k]["launches"]
+        b = tm1[k]["bytes"] - tm0[k]["bytes"]
+        if nl:
+            kern[k] = {"ms": round(ms, 3), "launches": nl, "bytes": b,
+                       "GBps": round(b / (ms * 1e6), 1) if ms > 0 else None}
+    dom = max(kern, key=lambda k: kern[k]["ms"]) if kern else None
+    roof = None
+    if dom:
+        ach = kern[dom]["GBps"] or 0.0
+        traffic = None
+        try:
+            pmc = json.load(open(args.pmc))
+            ent = pmc.get(args.config, {}).get(dom)
+            if ent:
+                traffic = ent.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4),
+                "bytes_per_launch": kern[dom]["bytes"] // max(1, kern[dom]["launches"]),
+                "traffic": traffic}
+
+    conv = None
+    if not args.no_converge:
+        r, w, ran = run_converge(lib, args.config, seed, local_rank, args.converge_max, args.check_every)
+        conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
+                "rounds_run": ran, "simulated_s": (r * 0.2) if r else None}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.config, args.cpu_seconds)
+
+    if rank == 0:
+        cfgp = CONFIGS[args.config]["p"]
+        out = {
+            "metric": METRIC, "value": tot_merges / dt_max, "unit": "record-merges/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt_max * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeded gossip schedule)",
+            "config": {"workload": f"{args.config}: " + CONFIGS[args.config]["desc"],
+                       "hosts": cfgp["n_hosts"], "services": cfgp["n_services"],
+                       "fanout": cfgp.get("fanout", 3), "parallelism": "replicas" if world > 1 else "single"},
+            "merges": split, "converge": conv, "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

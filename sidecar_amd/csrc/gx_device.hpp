@@ -37,6 +37,8 @@ enum {
 struct DevCtr {
   unsigned long long c[32];
   unsigned long long last_change_p1;  // last round with a slot change, + 1 (0 = none)
+  unsigned long long bytes[8];        // algorithmic HBM bytes per kernel class (GX_K_*)
+  unsigned long long units[8];        // slots / records processed per kernel class
 };
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
@@ -114,6 +116,10 @@ GXHD uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
 // ------------------------------------------------------------------------------ counters --
 GXD void ctr_add(const Dev &d, int i, unsigned long long v) {
   if (v) atomicAdd(&d.ctr->c[i], v);
+}
+GXD void kbytes(const Dev &d, int k, unsigned long long b, unsigned long long u) {
+  if (b) atomicAdd(&d.ctr->bytes[k], b);
+  if (u) atomicAdd(&d.ctr->units[k], u);
 }
 GXD void mark_change(const Dev &d) { atomicMax(&d.ctr->last_change_p1, (unsigned long long)(d.round + 1)); }
 GXD void set_slot(const Dev &d, uint64_t *slot, uint64_t nw) {

@@ -173,6 +173,7 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   uint32_t n_exp = 0;
   unsigned long long c_exp = 0, c_gc = 0;
   bool changed = false;
+  unsigned long long c_wr = 0;
   for (uint32_t base = 0; base < d.R; base += blockDim.x) {
     uint32_t r = base + threadIdx.x;
     uint64_t w = r < d.R ? row[r] : GX_SLOT_ABSENT;
@@ -181,6 +182,7 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
     if (nw != w) {
       row[r] = nw;
       changed = true;
+      c_wr++;
     }
     c_exp += ex;
     c_gc += gc;
@@ -197,6 +199,9 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   }
   if (threadIdx.x == 0) cnt_out[only_host >= 0 ? 0 : o] = n_exp;
   if (changed) mark_change(d);
+  c_wr = wave_sum(c_wr);
+  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SCAN, c_wr * 8, 0);
+  if (threadIdx.x == 0) kbytes(d, GX_K_SCAN, (unsigned long long)d.R * 8 + 16ull * (n_exp < list_cap ? n_exp : list_cap), d.R);
   block_ctr(d, C_EXPIRED, c_exp, s_red);
   block_ctr(d, C_GC, c_gc, s_red);
   block_ctr(d, C_SCANSLOTS, (threadIdx.x == 0) ? d.R : 0, s_red);
@@ -259,6 +264,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   if (threadIdx.x == 0) {
     uint32_t ok = jobs < room ? jobs : room;
     h->fifo_tail = tail0 + ok;
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 8ull * d.S * jobs + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
     ctr_add(d, C_EXPSRV, jobs);
     ctr_add(d, C_QDROP, jobs - ok);
   }
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
   uint32_t n_retx = 0;
-  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0;
+  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0;
   bool changed = false;
   uint64_t *row = &d.view[(size_t)v * d.R];
   for (uint32_t c0 = 0; c0 < deg; c0 += 64) {
@@ -427,6 +433,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
           }
         if (!leader) continue;
         uint64_t w0 = row[key], w = w0;
+        c_rd++;
         for (uint32_t j = i; j < tn; j++) {
           if (s_key[j] != key) continue;
           bool a, st;
@@ -441,6 +448,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
         if (w != w0) {
           row[key] = w;
           changed = true;
+          c_wr++;
         }
       }
       c_merge += (lane == 0) ? tn : 0;
@@ -470,9 +478,12 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   c_merge = wave_sum(c_merge);
   c_acc = wave_sum(c_acc);
   c_stale = wave_sum(c_stale);
+  c_rd = wave_sum(c_rd);
+  c_wr = wave_sum(c_wr);
   bool any = __ballot(changed) != 0;
   if (lane == 0) {
     uint32_t ok = n_retx < room ? n_retx : room;
+    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 8ull * deg, c_merge);
     h->fifo_tail = tail0 + ok;
     ctr_add(d, C_GOSSIP_MERGES, c_merge);
     ctr_add(d, C_GOSSIP_ACC, c_acc);
@@ -493,7 +504,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t *s_wa
   uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
   uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
   uint32_t na = 0, nb = 0;
-  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0;
+  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0;
   bool changed = false;
   for (uint32_t base = 0; base < d.R; base += blockDim.x) {
     uint32_t r = base + threadIdx.x;
@@ -514,6 +525,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t *s_wa
       if (nwa != wa) {
         A[r] = nwa;
         changed = true;
+        c_wr++;
       }
     }
     if (both && st_of(wa) != GX_ABSENT) {  // b.Merge(a's snapshot)
@@ -528,6 +540,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t *s_wa
       if (nwb != wb) {
         B[r] = nwb;
         changed = true;
+        c_wr++;
       }
     }
     uint32_t tota, totb;
@@ -557,6 +570,8 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t *s_wa
     nb += totb;
   }
   if (changed) mark_change(d);
+  c_wr = wave_sum(c_wr);
+  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_AE, 8ull * c_wr, 0);
   block_ctr(d, C_AE_MERGES, c_merge, s_red);
   block_ctr(d, C_AE_ACC, c_acc, s_red);
   block_ctr(d, C_STALE, c_stale, s_red);
@@ -567,6 +582,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t *s_wa
     ctr_add(d, C_RETX, oka + (both ? okb : 0));
     ctr_add(d, C_QDROP, (na - oka) + (both ? nb - okb : 0));
     ctr_add(d, C_AESLOTS, (unsigned long long)d.R * (both ? 2 : 1));
+    kbytes(d, GX_K_AE, 16ull * d.R + 32ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
     if (both) ctr_add(d, C_AEX, 1);
   }
 }
@@ -1452,10 +1468,16 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
   HIPCHK(hipSetDevice(e->device));
   int rc = drain_timing(e);
   if (rc) return rc;
+  DevCtr c;
+  HIPCHK(hipMemcpyAsync(&c, e->d.ctr, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+  rc = sync_check(e);
+  if (rc) return rc;
   memset(out, 0, sizeof(*out));
   for (int i = 0; i < GX_K_COUNT; i++) {
     out->ms[i] = e->ms[i];
     out->launches[i] = e->launches[i];
+    out->bytes[i] = c.bytes[i];
+    out->units[i] = c.units[i];
   }
   return GX_OK;
 }
