@@ -1,7 +1,8 @@
 // gx_device.hpp — device-side data layout and scalar semantics of the sidecar-gx engine.
 //
-// Layout in HBM (one engine = one GPU = one shard of hosts; DESIGN.md "Data layout"):
+// Layout in HBM (one engine = one GPU's cluster):
 //   view      u64 [H][R]      R = H*S packed slots (ts << 3 | status), one row per host view
+//   minexp    u64 [H]         lower bound of min over present slots of (ts + lifespan(status))
 //   hs        gx_host_state[H] per-host broadcast-queue / looper bookkeeping (64 B)
 //   fifo      gx_job [H][Q]   broadcast FIFO ring (the blocked senders of state.Broadcasts)
 //   sleep     gx_job [H][SQ]  SendServices passes sleeping TOMBSTONE_RETRANSMIT
@@ -9,10 +10,11 @@
 //   arena     grec [H][A][L]  SendServices lists (L = packet_cap + pending_cap)
 //   msg       grec [H][K][cap] this round's packets, msg_len/msg_dst [H][K]
 //
-// The scalar helpers below are the one-thread-per-host form of the reference semantics. They are
-// used by the per-host round kernels (owner ticks, GetBroadcasts) and by the single-host ABI
-// entry points. The hot, data-parallel phases (gossip merge, anti-entropy, expiry scan,
-// departure storm) have their own wave/block kernels in gx_engine.hip.
+// The scalar helpers below are the one-thread-per-host form of the reference semantics, used by
+// the per-host round kernels (owner ticks, GetBroadcasts) and by the single-host ABI entry points.
+// They count events into a per-thread accumulator (Acc) that each wave flushes once, so no kernel
+// funnels thousands of atomics into one counter word. The hot data-parallel phases (gossip merge,
+// anti-entropy, expiry scan, departure storm) have their own wave/block kernels in gx_engine.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,11 +36,12 @@ enum {
   C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_NCTR
 };
 
+#define GX_SHARDS 64
 struct DevCtr {
-  unsigned long long c[32];
-  unsigned long long last_change_p1;  // last round with a slot change, + 1 (0 = none)
-  unsigned long long bytes[8];        // algorithmic HBM bytes per kernel class (GX_K_*)
-  unsigned long long units[8];        // slots / records processed per kernel class
+  unsigned long long c[GX_SHARDS][32];              // counter shards (shard = block % 64)
+  unsigned long long last_change_p1[GX_SHARDS][8];  // last round with a slot change + 1
+  unsigned long long bytes[GX_SHARDS][8];           // algorithmic HBM bytes per kernel class
+  unsigned long long units[GX_SHARDS][8];           // slots / records per kernel class
 };
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
@@ -51,6 +54,7 @@ struct Dev {
   int64_t round, now;
   int partitioned;
   uint64_t *view;
+  unsigned long long *minexp;
   uint8_t *own_status;
   gx_host_state *hs;
   gx_job *fifo;
@@ -113,19 +117,64 @@ GXHD uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
   return x;
 }
 
+// Time after which TombstoneOthersServices would change this word (services_state.go:645-662):
+// the slot is rewritten iff exp_time < now. ABSENT never expires.
+GXHD unsigned long long exp_time(const gx_params &p, uint64_t w) {
+  int st = st_of(w);
+  if (st == GX_ABSENT) return ~0ull;
+  int64_t life = st == GX_TOMBSTONE ? p.tombstone_lifespan_ns
+                                    : (st == GX_DRAINING ? p.draining_lifespan_ns : p.alive_lifespan_ns);
+  return (unsigned long long)(ts_of(w) + life);
+}
+
 // ------------------------------------------------------------------------------ counters --
-GXD void ctr_add(const Dev &d, int i, unsigned long long v) {
-  if (v) atomicAdd(&d.ctr->c[i], v);
+GXD uint32_t shard_id() { return blockIdx.x & (GX_SHARDS - 1); }
+
+GXD unsigned long long wave_sum(unsigned long long x) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+GXD unsigned long long wave_min(unsigned long long x) {
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long y = __shfl_xor(x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+// Per-thread event counts; flushed once per wave (all 64 lanes must call acc_flush).
+struct Acc {
+  unsigned c[C_NCTR];
+  bool changed;
+  GXD Acc() : changed(false) {
+    for (int i = 0; i < C_NCTR; i++) c[i] = 0;
+  }
+};
+
+GXD void ctr_atomic(const Dev &d, int i, unsigned long long v) {
+  if (v) atomicAdd(&d.ctr->c[shard_id()][i], v);
+}
+GXD void mark_change(const Dev &d) {
+  atomicMax(&d.ctr->last_change_p1[shard_id()][0], (unsigned long long)(d.round + 1));
 }
 GXD void kbytes(const Dev &d, int k, unsigned long long b, unsigned long long u) {
-  if (b) atomicAdd(&d.ctr->bytes[k], b);
-  if (u) atomicAdd(&d.ctr->units[k], u);
+  if (b) atomicAdd(&d.ctr->bytes[shard_id()][k], b);
+  if (u) atomicAdd(&d.ctr->units[shard_id()][k], u);
 }
-GXD void mark_change(const Dev &d) { atomicMax(&d.ctr->last_change_p1, (unsigned long long)(d.round + 1)); }
-GXD void set_slot(const Dev &d, uint64_t *slot, uint64_t nw) {
+GXD void acc_flush(const Dev &d, const Acc &a) {
+  for (int i = 0; i < C_NCTR; i++) {
+    unsigned long long x = wave_sum((unsigned long long)a.c[i]);
+    if ((threadIdx.x & 63) == 0) ctr_atomic(d, i, x);
+  }
+  bool any = __ballot(a.changed) != 0;
+  if ((threadIdx.x & 63) == 0 && any) mark_change(d);
+}
+
+GXD void set_slot(const Dev &d, Acc &a, uint32_t v, uint64_t *slot, uint64_t nw) {
   if (*slot != nw) {
     *slot = nw;
-    mark_change(d);
+    a.changed = true;
+    atomicMin(&d.minexp[v], exp_time(d.p, nw));
   }
 }
 
@@ -136,13 +185,13 @@ GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
 
 // The unbuffered Broadcasts channel's blocked senders (services_state.go:94) as a FIFO bounded
 // at Q jobs, 2 reserved for the loopers' nil sends.
-GXD bool push_job(const Dev &d, uint32_t v, const gx_job &j) {
+GXD bool push_job(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
   gx_host_state *h = &d.hs[v];
   uint32_t count = h->fifo_tail - h->fifo_head;
   bool nil = (j.meta & 0xff) <= GX_JOB_NIL_BT;
   uint32_t limit = nil ? d.Q : d.Q - 2;
   if (count >= limit) {
-    ctr_add(d, C_QDROP, 1);
+    a.c[C_QDROP]++;
     free_list(d, v, j);
     return false;
   }
@@ -151,10 +200,10 @@ GXD bool push_job(const Dev &d, uint32_t v, const gx_job &j) {
   return true;
 }
 
-GXD void push_sleep(const Dev &d, uint32_t v, const gx_job &j) {
+GXD void push_sleep(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
   gx_host_state *h = &d.hs[v];
   if (h->sleep_tail - h->sleep_head >= d.SQ) {
-    ctr_add(d, C_SDROP, 1);
+    a.c[C_SDROP]++;
     free_list(d, v, j);
     return;
   }
@@ -163,22 +212,33 @@ GXD void push_sleep(const Dev &d, uint32_t v, const gx_job &j) {
 }
 
 // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO tail.
-GXD void wake_host(const Dev &d, uint32_t v) {
+GXD void wake_host(const Dev &d, Acc &a, uint32_t v) {
   gx_host_state *h = &d.hs[v];
   while (h->sleep_head != h->sleep_tail) {
     gx_job j = d.sleep[(size_t)v * d.SQ + (h->sleep_head % d.SQ)];
     if ((int64_t)j.wake > d.round) break;
     h->sleep_head++;
-    push_job(d, v, j);
+    push_job(d, a, v, j);
   }
 }
 
+GXD gx_job make_job(uint64_t a, uint64_t b, uint32_t c, uint32_t meta) {
+  gx_job j;
+  j.a = a;
+  j.b = b;
+  j.c = c;
+  j.meta = meta;
+  j.wake = 0;
+  j.aux = 0;
+  return j;
+}
+
 // Lowest free list slot, or -1 (list_drops).
-GXD int alloc_list(const Dev &d, uint32_t v) {
+GXD int alloc_list(const Dev &d, Acc &a, uint32_t v) {
   uint32_t used = d.hs[v].arena_used;
   uint32_t free_bits = ~used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1));
   if (!free_bits) {
-    ctr_add(d, C_LDROP, 1);
+    a.c[C_LDROP]++;
     return -1;
   }
   int slot = __builtin_ctz(free_bits);
@@ -189,17 +249,10 @@ GXD grec *list_ptr(const Dev &d, uint32_t v, uint32_t slot) {
   return &d.arena[((size_t)v * d.A + slot) * d.L];
 }
 // SendServices job over an allocated, filled list (services_state.go:579-604).
-GXD void commit_send(const Dev &d, uint32_t v, int slot, uint32_t n, uint32_t npasses) {
+GXD void commit_send(const Dev &d, Acc &a, uint32_t v, int slot, uint32_t n, uint32_t npasses) {
   d.arena_len[(size_t)v * d.A + slot] = n;
-  gx_job j;
-  j.a = 0;
-  j.b = 0;
-  j.c = (uint32_t)slot | (n << 16);
-  j.meta = meta_of(GX_JOB_SEND, 0, npasses);
-  j.wake = 0;
-  j.aux = 0;
-  ctr_add(d, C_SENDJOBS, 1);
-  push_job(d, v, j);
+  a.c[C_SENDJOBS]++;
+  push_job(d, a, v, make_job(0, 0, (uint32_t)slot | (n << 16), meta_of(GX_JOB_SEND, 0, npasses)));
 }
 
 GXD uint32_t job_len(const Dev &d, const gx_job &j) {
@@ -234,29 +287,29 @@ GXD grec job_rec(const Dev &d, uint32_t v, const gx_job &j, uint32_t i, uint32_t
 }
 
 // GetBroadcasts(overhead, limit) + packPacket (services_delegate.go:85-144, :186-223).
-GXD uint32_t get_broadcasts(const Dev &d, uint32_t v, uint32_t limit, grec *packet) {
+GXD uint32_t get_broadcasts(const Dev &d, Acc &a, uint32_t v, uint32_t limit, grec *packet) {
   gx_host_state *h = &d.hs[v];
   uint32_t m = 0;
   uint32_t mask = d.DQ - 1;
   grec *dq = &d.dq[(size_t)v * d.DQ];
-  if (h->fifo_head != h->fifo_tail) {
+  if (h->fifo_head != h->fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
     gx_job j = d.fifo[(size_t)v * d.Q + (h->fifo_head % d.Q)];
     h->fifo_head++;
-    ctr_add(d, C_DEQ, 1);
+    a.c[C_DEQ]++;
     m = job_len(d, j);
-    // broadcast = batch ++ pendingBroadcasts: push the batch to the deque front
+    // broadcast = batch ++ pendingBroadcasts (:104-106): push the batch to the deque front
     uint32_t head = (h->dq_head - m) & mask;
     uint32_t cur = 0;
     for (uint32_t i = 0; i < m; i++) dq[(head + i) & mask] = job_rec(d, v, j, i, cur);
     h->dq_head = head;
     h->dq_len += m;
     uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff, np = (j.meta >> 16) & 0xff;
-    if (kind == GX_JOB_NIL_BS) {
-      ctr_add(d, C_NIL, 1);
+    if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
+      a.c[C_NIL]++;
       h->flags &= ~1u;
       h->bs_next = d.round + d.p.alive_interval_rounds;
-    } else if (kind == GX_JOB_NIL_BT) {
-      ctr_add(d, C_NIL, 1);
+    } else if (kind == GX_JOB_NIL_BT) {  // ... BroadcastTombstones (:628)
+      a.c[C_NIL]++;
       h->flags &= ~2u;
       h->bt_next = d.round + d.p.tombstone_interval_rounds;
     } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
@@ -264,36 +317,36 @@ GXD uint32_t get_broadcasts(const Dev &d, uint32_t v, uint32_t limit, grec *pack
         j.meta = meta_of((int)kind, pass + 1, np);
         if (d.p.retransmit_rounds == 0) {
           j.wake = (uint32_t)d.round;
-          push_job(d, v, j);
+          push_job(d, a, v, j);
         } else {
           j.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
-          push_sleep(d, v, j);
+          push_sleep(d, a, v, j);
         }
       } else {
         free_list(d, v, j);
       }
     }
-  } else if (h->dq_len == 0) {
+  } else if (h->dq_len == 0) {  // default: nothing pending (:96-98)
     return 0;
   }
-  uint32_t l = h->dq_len < limit ? h->dq_len : limit;
+  uint32_t l = h->dq_len < limit ? h->dq_len : limit;  // packPacket greedy prefix
   for (uint32_t i = 0; i < l; i++) packet[i] = dq[(h->dq_head + i) & mask];
   h->dq_head = (h->dq_head + l) & mask;
   h->dq_len -= l;
-  if (h->dq_len > d.p.pending_cap) {
-    ctr_add(d, C_PDROP, h->dq_len - d.p.pending_cap);
+  if (h->dq_len > d.p.pending_cap) {  // pendingBroadcasts = leftover[:MAX_PENDING_LENGTH]
+    a.c[C_PDROP] += h->dq_len - d.p.pending_cap;
     h->dq_len = d.p.pending_cap;
   }
   if (l) {
-    ctr_add(d, C_PACKETS, 1);
-    ctr_add(d, C_RECSENT, l);
+    a.c[C_PACKETS]++;
+    a.c[C_RECSENT] += l;
   }
   return l;
 }
 
 // ------------------------------------------------------------------------ merge rule (a-5) --
 // AddServiceEntry core on one slot word (services_state.go:293-347): returns the new word and
-// sets *acc when the record was stored; *stale when IsStale dropped it (service.go:68-72).
+// sets acc when the record was stored; stale when IsStale dropped it (service.go:68-72).
 GXD uint64_t merge_word(const Dev &d, uint64_t old, uint64_t u, bool &acc, bool &stale) {
   int64_t ts = ts_of(u);
   acc = false;
@@ -302,46 +355,38 @@ GXD uint64_t merge_word(const Dev &d, uint64_t old, uint64_t u, bool &acc, bool 
     stale = true;
     return old;
   }
-  if (st_of(old) == GX_ABSENT) {
+  if (st_of(old) == GX_ABSENT) {  // !server.HasService: insert (:317-320)
     acc = true;
     return u;
   }
-  if (ts > ts_of(old)) {
+  if (ts > ts_of(old)) {  // Invalidates: strictly newer (:321)
     int st = st_of(u);
-    if (st_of(old) == GX_DRAINING && st == GX_ALIVE) st = GX_DRAINING;
+    if (st_of(old) == GX_DRAINING && st == GX_ALIVE) st = GX_DRAINING;  // (:329-331)
     acc = true;
     return pack(ts, st);
   }
   return old;
 }
 
-GXD bool add_entry(const Dev &d, uint32_t v, grec u, int src) {
-  ctr_add(d, src == SRC_GOSSIP ? C_GOSSIP_MERGES : src == SRC_AE ? C_AE_MERGES : C_LOCAL_MERGES, 1);
+GXD bool add_entry(const Dev &d, Acc &a, uint32_t v, grec u, int src) {
+  a.c[src == SRC_GOSSIP ? C_GOSSIP_MERGES : src == SRC_AE ? C_AE_MERGES : C_LOCAL_MERGES]++;
   uint64_t *slot = &d.view[(size_t)v * d.R + u.r];
   bool acc, stale;
   uint64_t nw = merge_word(d, *slot, u.w, acc, stale);
   if (stale) {
-    ctr_add(d, C_STALE, 1);
+    a.c[C_STALE]++;
     return false;
   }
   if (!acc) return false;
-  set_slot(d, slot, nw);
-  ctr_add(d, src == SRC_GOSSIP ? C_GOSSIP_ACC : src == SRC_AE ? C_AE_ACC : C_LOCAL_ACC, 1);
+  set_slot(d, a, v, slot, nw);
+  a.c[src == SRC_GOSSIP ? C_GOSSIP_ACC : src == SRC_AE ? C_AE_ACC : C_LOCAL_ACC]++;
   if (u.r / d.S != v) {  // retransmit foreign records only (services_state.go:377-392)
-    gx_job j;
-    j.a = nw;
-    j.b = 0;
-    j.c = u.r;
-    j.meta = meta_of(GX_JOB_RETX, 0, 1);
-    j.wake = 0;
-    j.aux = 0;
-    if (push_job(d, v, j)) ctr_add(d, C_RETX, 1);
+    if (push_job(d, a, v, make_job(nw, 0, u.r, meta_of(GX_JOB_RETX, 0, 1)))) a.c[C_RETX]++;
   }
   return true;
 }
 
 // Expiry rule of TombstoneOthersServices on one slot (services_state.go:645-679).
-// Returns the new word; *expired when it was tombstoned by lifespan, *gc when removed.
 GXD uint64_t expiry_word(const Dev &d, uint64_t w, bool &expired, bool &gc) {
   expired = false;
   gc = false;
@@ -365,21 +410,21 @@ GXD uint64_t expiry_word(const Dev &d, uint64_t w, bool &expired, bool &gc) {
 
 // TombstoneServices(self, list) on the owner's own slots (services_state.go:685-715).
 // Returns the mask of services tombstoned (each contributes the record twice).
-GXD uint64_t tombstone_services(const Dev &d, uint32_t o, uint64_t running) {
+GXD uint64_t tombstone_services(const Dev &d, Acc &a, uint32_t o, uint64_t running) {
   uint64_t *row = &d.view[(size_t)o * d.R + (size_t)o * d.S];
   uint64_t m = 0;
   for (uint32_t s = 0; s < d.S; s++) {
     uint64_t w = row[s];
     if (st_of(w) == GX_ABSENT || ((running >> s) & 1ull) || st_of(w) == GX_TOMBSTONE) continue;
-    set_slot(d, &row[s], pack(d.now, GX_TOMBSTONE));
+    set_slot(d, a, o, &row[s], pack(d.now, GX_TOMBSTONE));  // svc.Tombstone() (service.go:91-94)
     m |= 1ull << s;
   }
-  ctr_add(d, C_OWNTOMB, (unsigned long long)__popcll(m));
+  a.c[C_OWNTOMB] += (unsigned)__popcll(m);
   return m;
 }
 
 // ExpireServer (services_state.go:150-192) for one (viewer, owner).
-GXD bool expire_server(const Dev &d, uint32_t v, uint32_t o) {
+GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
   uint64_t *row = &d.view[(size_t)v * d.R + (size_t)o * d.S];
   uint64_t mask = 0;
   bool live = false;
@@ -389,18 +434,11 @@ GXD bool expire_server(const Dev &d, uint32_t v, uint32_t o) {
     mask |= 1ull << s;
     if (st != GX_TOMBSTONE) live = true;
   }
-  if (!live) return false;
+  if (!live) return false;  // no server / no services / no live services (:154-170)
   for (uint32_t s = 0; s < d.S; s++)
-    if ((mask >> s) & 1ull) set_slot(d, &row[s], pack(d.now, GX_TOMBSTONE));
-  ctr_add(d, C_EXPSRV, 1);
-  gx_job j;
-  j.a = (uint64_t)d.now;
-  j.b = mask;
-  j.c = o;
-  j.meta = meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count);
-  j.wake = 0;
-  j.aux = 0;
-  push_job(d, v, j);
+    if ((mask >> s) & 1ull) set_slot(d, a, v, &row[s], pack(d.now, GX_TOMBSTONE));
+  a.c[C_EXPSRV]++;
+  push_job(d, a, v, make_job((uint64_t)d.now, mask, o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count)));
   return true;
 }
 
@@ -411,7 +449,7 @@ GXD bool is_new(const Dev &d, uint32_t o, uint64_t sw, uint32_t r) {
 
 // BroadcastServices looper body (services_state.go:525-574) over fn() = list (n <= 64).
 // Sets inc = bit i for each list element handed to SendServices (0 = a nil was sent).
-GXD void bs_body_list(const Dev &d, uint32_t o, const grec *list, uint32_t n, uint64_t &inc_out) {
+GXD void bs_body_list(const Dev &d, Acc &a, uint32_t o, const grec *list, uint32_t n, uint64_t &inc_out) {
   gx_host_state *h = &d.hs[o];
   bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > h->last_bcast_ns;  // (:547)
   bool any_new = false;
@@ -427,60 +465,46 @@ GXD void bs_body_list(const Dev &d, uint32_t o, const grec *list, uint32_t n, ui
   inc_out = inc;
   if (inc) {
     h->last_bcast_ns = d.now;
-    int slot = alloc_list(d, o);
+    int slot = alloc_list(d, a, o);
     if (slot >= 0) {
       grec *dst = list_ptr(d, o, slot);
       uint32_t m = 0;
       for (uint32_t i = 0; i < n && m < d.L; i++)
         if ((inc >> i) & 1ull) dst[m++] = list[i];
-      commit_send(d, o, slot, m, any_new ? d.p.alive_count : 1);  // ALIVE_COUNT if new (:555-558)
+      commit_send(d, a, o, slot, m, any_new ? d.p.alive_count : 1);  // ALIVE_COUNT if new (:555-558)
     }
   } else {
-    gx_job j;
-    j.a = 0;
-    j.b = 0;
-    j.c = 0;
-    j.meta = meta_of(GX_JOB_NIL_BS, 0, 1);
-    j.wake = 0;
-    j.aux = 0;
-    push_job(d, o, j);  // Broadcasts <- nil (:569): the looper blocks until it is consumed
-    h->flags |= 1u;
+    push_job(d, a, o, make_job(0, 0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)));  // Broadcasts <- nil (:569)
+    h->flags |= 1u;  // the looper blocks until the nil is consumed
   }
 }
 
 // Second half of the BroadcastTombstones body (services_state.go:613-629), after the view scan
-// put the first L expired records in scan_list[o] and the total in scan_cnt[o].
-GXD void bt_finish(const Dev &d, uint32_t o, uint64_t running, const grec *others, uint32_t n_others) {
+// left the first L expired records (key order) in `others`.
+GXD void bt_finish(const Dev &d, Acc &a, uint32_t o, uint64_t running, const grec *others, uint32_t n_others) {
   gx_host_state *h = &d.hs[o];
-  uint64_t own = tombstone_services(d, o, running);
+  uint64_t own = tombstone_services(d, a, o, running);
   uint32_t n_own = 2u * (uint32_t)__popcll(own);
   if (n_own + n_others > 0) {
-    int slot = alloc_list(d, o);
+    int slot = alloc_list(d, a, o);
     if (slot >= 0) {
       grec *dst = list_ptr(d, o, slot);
       uint32_t m = 0;
       uint64_t w = pack(d.now, GX_TOMBSTONE);
       for (uint32_t s = 0; s < d.S && m < d.L; s++)
         if ((own >> s) & 1ull)
-          for (int k = 0; k < 2 && m < d.L; k++) {
+          for (int k = 0; k < 2 && m < d.L; k++) {  // each own tombstone twice (:707-710)
             dst[m].w = w;
             dst[m].r = o * d.S + s;
             dst[m].pad = 0;
             m++;
           }
-      for (uint32_t i = 0; i < n_others && m < d.L; i++) dst[m++] = others[i];
-      commit_send(d, o, slot, m, d.p.tombstone_count);
+      for (uint32_t i = 0; i < n_others && m < d.L; i++) dst[m++] = others[i];  // own ++ others (:618)
+      commit_send(d, a, o, slot, m, d.p.tombstone_count);
     }
     h->bt_next = d.round + d.p.tombstone_interval_rounds;
   } else {
-    gx_job j;
-    j.a = 0;
-    j.b = 0;
-    j.c = 0;
-    j.meta = meta_of(GX_JOB_NIL_BT, 0, 1);
-    j.wake = 0;
-    j.aux = 0;
-    push_job(d, o, j);
+    push_job(d, a, o, make_job(0, 0, 0, meta_of(GX_JOB_NIL_BT, 0, 1)));  // Broadcasts <- nil (:628)
     h->flags |= 2u;
   }
 }

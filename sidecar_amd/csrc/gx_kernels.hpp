@@ -1,0 +1,864 @@
+// gx_kernels.hpp — round-phase kernels of the sidecar-gx engine (gfx950). Included by
+// gx_engine.hip (single translation unit). DESIGN.md §3 (round model) and §6 (kernels).
+#pragma once
+#include "gx_device.hpp"
+
+// =================================================================== block-level helpers ==
+// Ordered block-wide exclusive scan of packed counts (u64 with independent 16-bit fields: every
+// field's block total must stay < 65536). Returns this thread's exclusive prefix, `total` = sum.
+GXD unsigned long long block_excl_scan64(unsigned long long x, unsigned long long *s_wave,
+                                         unsigned long long &total) {
+  uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  unsigned long long incl = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    unsigned long long y = __shfl_up(incl, o, 64);
+    if ((int)lane >= o) incl += y;
+  }
+  if (lane == 63) s_wave[w] = incl;
+  __syncthreads();
+  unsigned long long off = 0, tot = 0;
+  for (uint32_t i = 0; i < nw; i++) {
+    unsigned long long c = s_wave[i];
+    if (i < w) off += c;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return off + incl - x;
+}
+GXD uint32_t fld(unsigned long long x, int i) { return (uint32_t)((x >> (16 * i)) & 0xffffu); }
+
+// Block reduction of a counter -> one atomic on this block's shard.
+GXD void block_ctr(const Dev &d, int idx, unsigned long long x, unsigned long long *s_red) {
+  x = wave_sum(x);
+  uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if (lane == 0) s_red[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (uint32_t i = 0; i < nw; i++) t += s_red[i];
+    ctr_atomic(d, idx, t);
+  }
+  __syncthreads();
+}
+GXD unsigned long long block_min(unsigned long long x, unsigned long long *s_red) {
+  x = wave_min(x);
+  uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if (lane == 0) s_red[w] = x;
+  __syncthreads();
+  unsigned long long m = ~0ull;
+  for (uint32_t i = 0; i < nw; i++) m = s_red[i] < m ? s_red[i] : m;
+  __syncthreads();
+  return m;
+}
+
+// =================================================================================== init ==
+__global__ void k_init_rec(Dev d, uint64_t *rec_word) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= d.R) return;
+  const gx_params &p = d.p;
+  int64_t ts = p.t0_ns - (int64_t)(rng4(p.seed, ST_INIT_TS, r, 0, 0) % 1000000000ull);
+  if (p.aged_ppm && (rng4(p.seed, ST_INIT_AGE, r, 0, 0) % 1000000ull) < p.aged_ppm && p.aged_max_ns > 0)
+    ts = p.t0_ns - (int64_t)(rng4(p.seed, ST_INIT_AGE, r, 1, 0) % (uint64_t)p.aged_max_ns);
+  rec_word[r] = pack(ts, GX_ALIVE);
+}
+
+__global__ void k_init_views(Dev d, const uint64_t *rec_word) {
+  size_t total = (size_t)d.H * d.R;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t v = (uint32_t)(i / d.R), r = (uint32_t)(i % d.R);
+    uint64_t w = GX_SLOT_ABSENT;
+    if (d.p.init_mode == GX_INIT_WARM || (d.p.init_mode == GX_INIT_OWN && r / d.S == v)) w = rec_word[r];
+    d.view[i] = w;
+  }
+}
+
+__global__ void k_init_hosts(Dev d) {
+  uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= d.H) return;
+  const gx_params &p = d.p;
+  gx_host_state h = {};
+  h.bs_next = (int64_t)(rng4(p.seed, ST_PHASE_BS, o, 0, 0) % p.alive_interval_rounds);
+  h.bt_next = (int64_t)(rng4(p.seed, ST_PHASE_BT, o, 0, 0) % p.tombstone_interval_rounds);
+  h.last_bcast_ns = p.init_mode == GX_INIT_WARM ? p.t0_ns : 0;
+  h.running = d.S == 64 ? ~0ull : ((1ull << d.S) - 1);
+  d.hs[o] = h;
+  for (uint32_t s = 0; s < d.S; s++) d.own_status[(size_t)o * d.S + s] = GX_ALIVE;
+}
+
+// Exact per-view expiry bound (one block per view): used at create and after raw imports.
+__global__ __launch_bounds__(256) void k_minexp_recompute(Dev d, uint32_t lo) {
+  __shared__ unsigned long long s_red[4];
+  uint32_t v = lo + blockIdx.x;
+  const uint64_t *row = &d.view[(size_t)v * d.R];
+  unsigned long long m = ~0ull;
+  for (uint32_t r = threadIdx.x; r < d.R; r += blockDim.x) {
+    unsigned long long x = exp_time(d.p, row[r]);
+    m = x < m ? x : m;
+  }
+  m = block_min(m, s_red);
+  if (threadIdx.x == 0) d.minexp[v] = m;
+}
+
+__global__ void k_wake(Dev d) {
+  Acc a;
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < d.H) wake_host(d, a, v);
+  acc_flush(d, a);
+}
+
+// ================================================================= phase 0+1: owner ticks ==
+// One thread per host: wake re-armed passes, discovery churn, BroadcastServices tick +
+// TrackNewServices, and flag the BroadcastTombstones tick. Also clears this round's CSR counts.
+__global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
+  Acc a;
+  uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < d.H) {
+    d.in_cnt[o] = 0;
+    d.in_cur[o] = 0;
+    if (o == 0) d.in_cnt[d.H] = 0;
+    wake_host(d, a, o);
+    gx_host_state *h = &d.hs[o];
+    if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
+      uint64_t x = rng4(d.p.seed, ST_CHURN, (uint64_t)d.round, o, 0);
+      if ((uint32_t)(x & 0xffffffffu) % 1000000u < d.p.churn_ppm) {
+        uint32_t s = (uint32_t)((x >> 32) % d.S);
+        h->running ^= 1ull << s;
+        if ((h->running >> s) & 1ull) d.own_status[(size_t)o * d.S + s] = GX_ALIVE;
+        a.c[C_CHURN]++;
+      }
+    }
+    if (!(h->flags & 1u) && h->bs_next <= d.round) {
+      grec *list = &own_list[(size_t)o * d.S];  // fn(): running services, restamped now
+      uint32_t n = 0;
+      uint64_t run = h->running;
+      for (uint32_t s = 0; s < d.S; s++)
+        if ((run >> s) & 1ull) {
+          list[n].w = pack(d.now, d.own_status[(size_t)o * d.S + s]);
+          list[n].r = o * d.S + s;
+          list[n].pad = 0;
+          n++;
+        }
+      uint64_t inc = 0;
+      bs_body_list(d, a, o, list, n, inc);
+      if (inc) {
+        h->bs_next = d.round + d.p.alive_interval_rounds;
+        for (uint32_t i = 0; i < n; i++)
+          if ((inc >> i) & 1ull) add_entry(d, a, o, list[i], SRC_LOCAL);  // TrackNewServices
+      }
+    }
+    d.tick[o] = (!(h->flags & 2u) && h->bt_next <= d.round) ? 1 : 0;
+  }
+  acc_flush(d, a);
+}
+
+// ============================================== phase 1: TombstoneOthersServices full scan ==
+// One 256-thread block per scanned view. A view whose expiry bound is >= now cannot change (no
+// slot has ts + lifespan < now), so its scan is skipped: identical results, no HBM traffic.
+// Otherwise the row is streamed with 16-B loads (4 slots per thread per 1024-slot tile), the
+// lifespans applied, and the first list_cap tombstones compacted in key order (packed block scan).
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t list_stride, uint32_t list_cap,
+                                               uint32_t *cnt_out, int only_host) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  uint32_t o = only_host >= 0 ? (uint32_t)only_host : blockIdx.x;
+  if (only_host < 0) {
+    if (!d.tick[o]) return;
+    if (d.minexp[o] >= (unsigned long long)d.now) {  // nothing can expire in this view
+      if (threadIdx.x == 0) {
+        cnt_out[o] = 0;
+        ctr_atomic(d, C_SCANSLOTS, d.R);
+      }
+      return;
+    }
+  }
+  uint64_t *row = &d.view[(size_t)o * d.R];
+  grec *list = &list_base[only_host >= 0 ? 0 : (size_t)o * list_stride];
+  uint32_t n_exp = 0;
+  unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, mexp = ~0ull;
+  uint32_t t = threadIdx.x;
+  for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
+    uint64_t w[4], nw[4];
+    bool ex[4];
+    bool valid[4];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
+      valid[2 * h] = r0 < d.R;
+      valid[2 * h + 1] = r0 + 1 < d.R;
+      if (VEC && valid[2 * h]) {
+        ulonglong2 p = *reinterpret_cast<const ulonglong2 *>(&row[r0]);
+        w[2 * h] = p.x;
+        w[2 * h + 1] = p.y;
+      } else {
+        w[2 * h] = valid[2 * h] ? row[r0] : GX_SLOT_ABSENT;
+        w[2 * h + 1] = valid[2 * h + 1] ? row[r0 + 1] : GX_SLOT_ABSENT;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      bool gc;
+      nw[k] = expiry_word(d, w[k], ex[k], gc);
+      c_exp += ex[k];
+      c_gc += gc;
+      unsigned long long x = exp_time(d.p, nw[k]);
+      mexp = x < mexp ? x : mexp;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
+      bool ch0 = nw[2 * h] != w[2 * h], ch1 = nw[2 * h + 1] != w[2 * h + 1];
+      c_wr += ch0 + ch1;
+      if (VEC && (ch0 || ch1)) {
+        *reinterpret_cast<ulonglong2 *>(&row[r0]) = make_ulonglong2(nw[2 * h], nw[2 * h + 1]);
+      } else if (!VEC) {
+        if (ch0) row[r0] = nw[2 * h];
+        if (ch1) row[r0 + 1] = nw[2 * h + 1];
+      }
+    }
+    unsigned long long cnt = (unsigned long long)(ex[0] + ex[1]) | ((unsigned long long)(ex[2] + ex[3]) << 16);
+    unsigned long long tot;
+    unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
+    uint32_t pos[4];
+    pos[0] = n_exp + fld(pre, 0);
+    pos[1] = pos[0] + ex[0];
+    pos[2] = n_exp + fld(tot, 0) + fld(pre, 1);
+    pos[3] = pos[2] + ex[2];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (ex[k] && pos[k] < list_cap) {
+        uint32_t r0 = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+        grec g;
+        g.w = nw[k];
+        g.r = r0;
+        g.pad = 0;
+        list[pos[k]] = g;
+      }
+    }
+    n_exp += fld(tot, 0) + fld(tot, 1);
+  }
+  mexp = block_min(mexp, s_red);
+  if (threadIdx.x == 0) {
+    cnt_out[only_host >= 0 ? 0 : o] = n_exp;
+    d.minexp[o] = mexp;  // exact bound after the scan
+  }
+  bool changed = c_wr != 0;
+  if (__ballot(changed) != 0 && (threadIdx.x & 63) == 0) mark_change(d);
+  c_wr = wave_sum(c_wr);
+  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SCAN, c_wr * 8, 0);
+  if (threadIdx.x == 0)
+    kbytes(d, GX_K_SCAN, (unsigned long long)d.R * 8 + 16ull * (n_exp < list_cap ? n_exp : list_cap), d.R);
+  block_ctr(d, C_EXPIRED, c_exp, s_red);
+  block_ctr(d, C_GC, c_gc, s_red);
+  block_ctr(d, C_SCANSLOTS, threadIdx.x == 0 ? d.R : 0, s_red);
+}
+
+__global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
+  Acc a;
+  uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < d.H && d.tick[o]) {
+    uint32_t n = d.scan_cnt[o];
+    bt_finish(d, a, o, d.hs[o].running, &d.scan_list[(size_t)o * d.L], n < d.L ? n : d.L);
+  }
+  acc_flush(d, a);
+}
+
+// ===================================================================== phase 2: departure storm ==
+// One block per viewer. The other half's owners are walked in tiles of 1024/S owners whose S
+// slots are contiguous; threads read the tile's words lane-contiguously (coalesced), fold each
+// owner's presence mask and liveness in LDS, tombstone the live owners' present slots, and
+// compact the EXPIRE jobs in owner order.
+#define STORM_TILE 1024
+__global__ __launch_bounds__(256) void k_storm(Dev d) {
+  __shared__ unsigned long long s_mask[STORM_TILE];
+  __shared__ uint32_t s_live[STORM_TILE];
+  __shared__ unsigned long long s_wave[4];
+  uint32_t v = blockIdx.x;
+  uint32_t half = d.H / 2;
+  uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
+  gx_host_state *h = &d.hs[v];
+  uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
+  uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  uint32_t jobs = 0;
+  unsigned long long c_wr = 0;
+  uint64_t tomb = pack(d.now, GX_TOMBSTONE);
+  uint32_t OT = STORM_TILE / d.S;
+  uint32_t t = threadIdx.x;
+  for (uint32_t ob = lo; ob < hi; ob += OT) {
+    uint32_t on = hi - ob < OT ? hi - ob : OT, ns = on * d.S;
+    for (uint32_t i = t; i < on; i += blockDim.x) {
+      s_mask[i] = 0;
+      s_live[i] = 0;
+    }
+    __syncthreads();
+    uint64_t *base = &d.view[(size_t)v * d.R + (size_t)ob * d.S];
+    uint64_t w[STORM_TILE / 256];
+#pragma unroll
+    for (int q = 0; q < STORM_TILE / 256; q++) {
+      uint32_t k = t + 256 * q;
+      w[q] = k < ns ? base[k] : GX_SLOT_ABSENT;
+      if (st_of(w[q]) != GX_ABSENT) {
+        uint32_t oi = k / d.S, s = k - oi * d.S;
+        atomicOr(&s_mask[oi], 1ull << s);
+        if (st_of(w[q]) != GX_TOMBSTONE) s_live[oi] = 1;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < STORM_TILE / 256; q++) {
+      uint32_t k = t + 256 * q;
+      if (k < ns && st_of(w[q]) != GX_ABSENT && s_live[k / d.S] && w[q] != tomb) {
+        base[k] = tomb;
+        c_wr++;
+      }
+    }
+    for (uint32_t i0 = 0; i0 < on; i0 += blockDim.x) {  // EXPIRE jobs in owner order
+      uint32_t i = i0 + t;
+      bool live = i < on && s_live[i];
+      unsigned long long tot;
+      uint32_t pos = (uint32_t)block_excl_scan64(live ? 1ull : 0ull, s_wave, tot);
+      if (live && jobs + pos < room)
+        d.fifo[(size_t)v * d.Q + ((tail0 + jobs + pos) % d.Q)] =
+            make_job((uint64_t)d.now, s_mask[i], ob + i, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
+      jobs += (uint32_t)tot;
+    }
+    __syncthreads();
+  }
+  bool changed = c_wr != 0;
+  if (__ballot(changed) != 0 && (t & 63) == 0) {
+    mark_change(d);
+    atomicMin(&d.minexp[v], exp_time(d.p, tomb));
+  }
+  c_wr = wave_sum(c_wr);
+  if ((t & 63) == 0) kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
+  if (t == 0) {
+    uint32_t ok = jobs < room ? jobs : room;
+    h->fifo_tail = tail0 + ok;
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
+    ctr_atomic(d, C_EXPSRV, jobs);
+    ctr_atomic(d, C_QDROP, jobs - ok);
+  }
+}
+
+// ========================================================================= phase 3: gossip send ==
+// memberlist kRandomNodes restated as a seeded sampler: k distinct peers != u on u's side.
+GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
+  uint32_t base = 0, m = d.H;
+  if (d.partitioned) {
+    uint32_t half = d.H / 2;
+    if (u < half) {
+      base = 0;
+      m = half;
+    } else {
+      base = half;
+      m = d.H - half;
+    }
+  }
+  if (m < 2) return 0;
+  uint32_t want = d.K < m - 1 ? d.K : m - 1, cnt = 0;
+  for (uint32_t a = 0; cnt < want && a < 64u * d.K; a++) {
+    uint64_t x = rng4(d.p.seed, ST_PEER, (uint64_t)d.round, u, a);
+    uint32_t idx = unif(x, m - 1), self = u - base;
+    uint32_t p = base + (idx >= self ? idx + 1 : idx);
+    bool dup = false;
+    for (uint32_t i = 0; i < cnt; i++) dup |= peers[i] == p;
+    if (!dup) peers[cnt++] = p;
+  }
+  return cnt;
+}
+
+// One thread per host: GetBroadcasts once per sampled peer, in order. Each packet is counted
+// into its receiver's CSR bucket.
+__global__ __launch_bounds__(256) void k_send(Dev d) {
+  Acc a;
+  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < d.H) {
+    uint32_t peers[16];
+    uint32_t np = sample_peers(d, u, peers);
+    uint32_t cap = d.p.packet_cap;
+    for (uint32_t j = 0; j < d.K; j++) d.msg_len[(size_t)u * d.K + j] = 0;
+    for (uint32_t j = 0; j < np; j++) {
+      uint32_t l = get_broadcasts(d, a, u, cap, &d.msg[((size_t)u * d.K + j) * cap]);
+      d.msg_len[(size_t)u * d.K + j] = l;
+      d.msg_dst[(size_t)u * d.K + j] = peers[j];
+      if (l) atomicAdd(&d.in_cnt[peers[j]], 1u);
+      if (l == 0 && d.p.gossip_stop_on_empty) break;
+    }
+  }
+  acc_flush(d, a);
+}
+
+// ====================================================== phase 3b: receiver CSR, sender-ordered ==
+// Exclusive scan of H counts in place into in_cnt[0..H], in_cnt[H] = total. One block of 1024
+// threads, 16 contiguous counts per thread per pass (4 x 16-B loads); in_cnt is padded.
+#define ROUTE_ITEMS 16
+__global__ __launch_bounds__(1024) void k_route_offsets(Dev d) {
+  __shared__ unsigned long long s_wave[16];
+  uint32_t t = threadIdx.x;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < d.H; base += 1024 * ROUTE_ITEMS) {
+    uint32_t i0 = base + t * ROUTE_ITEMS;
+    uint32_t v[ROUTE_ITEMS];
+#pragma unroll
+    for (int q = 0; q < ROUTE_ITEMS / 4; q++) {
+      uint4 x = *reinterpret_cast<const uint4 *>(&d.in_cnt[i0 + 4 * q]);
+      v[4 * q] = i0 + 4 * q < d.H ? x.x : 0;
+      v[4 * q + 1] = i0 + 4 * q + 1 < d.H ? x.y : 0;
+      v[4 * q + 2] = i0 + 4 * q + 2 < d.H ? x.z : 0;
+      v[4 * q + 3] = i0 + 4 * q + 3 < d.H ? x.w : 0;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < ROUTE_ITEMS; q++) sum += v[q];
+    unsigned long long tot;
+    uint32_t pre = (uint32_t)block_excl_scan64(sum, s_wave, tot) + carry;
+#pragma unroll
+    for (int q = 0; q < ROUTE_ITEMS; q++) {
+      uint32_t c = v[q];
+      v[q] = pre;
+      pre += c;
+    }
+#pragma unroll
+    for (int q = 0; q < ROUTE_ITEMS / 4; q++)
+      if (i0 + 4 * q < d.H) *reinterpret_cast<uint4 *>(&d.in_cnt[i0 + 4 * q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    carry += (uint32_t)tot;
+  }
+  __syncthreads();
+  if (t == 0) d.in_cnt[d.H] = carry;
+}
+
+__global__ void k_route_fill(Dev d) {
+  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.H * d.K || d.msg_len[e] == 0) return;
+  uint32_t dst = d.msg_dst[e];
+  uint32_t pos = atomicAdd(&d.in_cur[dst], 1u);
+  d.in_fill[d.in_cnt[dst] + pos] = e;
+}
+
+// Deterministic order: rank of each entry (= sender * K + j) inside its receiver segment.
+__global__ void k_route_rank(Dev d) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.in_cnt[d.H]) return;
+  uint32_t e = d.in_fill[i];
+  uint32_t dst = d.msg_dst[e];
+  uint32_t lo = d.in_cnt[dst], hi = d.in_cnt[dst + 1];
+  uint32_t rank = 0;
+  for (uint32_t x = lo; x < hi; x++) rank += d.in_fill[x] < e;
+  d.in_sorted[lo + rank] = e;
+}
+
+// ============================================================== phase 4: gather-then-merge ==
+// One wave per receiver. Its packets (sender order) are staged record by record in LDS; the first
+// occurrence of each key reads the view slot once, folds every occurrence in arrival order with
+// the AddServiceEntry rule, and writes the slot once. Accepted foreign records are compacted with
+// a wave ballot into the receiver's FIFO (retransmit), in arrival order.
+#define MERGE_TILE 256
+__global__ __launch_bounds__(64) void k_merge(Dev d) {
+  __shared__ uint32_t s_key[MERGE_TILE];
+  __shared__ uint64_t s_val[MERGE_TILE];
+  __shared__ uint64_t s_acc[MERGE_TILE];
+  __shared__ uint8_t s_accf[MERGE_TILE];
+  __shared__ uint32_t s_start[65];
+  __shared__ uint32_t s_ent[64];
+  uint32_t v = blockIdx.x;
+  uint32_t lane = threadIdx.x;
+  uint32_t off = d.in_cnt[v], deg = d.in_cnt[v + 1] - off;
+  if (deg == 0) return;
+  uint32_t cap = d.p.packet_cap;
+  gx_host_state *h = &d.hs[v];
+  uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
+  uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  uint32_t n_retx = 0;
+  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, mexp = ~0ull;
+  uint64_t *row = &d.view[(size_t)v * d.R];
+  for (uint32_t c0 = 0; c0 < deg; c0 += 64) {
+    uint32_t cn = deg - c0 < 64 ? deg - c0 : 64;
+    uint32_t ent = 0, len = 0;
+    if (lane < cn) {
+      ent = d.in_sorted[off + c0 + lane];
+      len = d.msg_len[ent];
+    }
+    uint32_t incl = len;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t y = __shfl_up(incl, o, 64);
+      if ((int)lane >= o) incl += y;
+    }
+    uint32_t total = __shfl(incl, 63, 64);
+    s_start[lane] = incl - len;
+    s_ent[lane] = ent;
+    if (lane == 0) s_start[64] = total;
+    __syncthreads();
+    for (uint32_t t0 = 0; t0 < total; t0 += MERGE_TILE) {
+      uint32_t tn = total - t0 < MERGE_TILE ? total - t0 : MERGE_TILE;
+      for (uint32_t i = lane; i < tn; i += 64) {  // stage this tile's records (arrival order)
+        uint32_t gi = t0 + i;
+        uint32_t lo = 0, hi = cn - 1;  // last message with start <= gi
+        while (lo < hi) {
+          uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_start[mid] <= gi) lo = mid;
+          else hi = mid - 1;
+        }
+        grec g = d.msg[(size_t)s_ent[lo] * cap + (gi - s_start[lo])];
+        s_key[i] = g.r;
+        s_val[i] = g.w;
+        s_accf[i] = 0;
+      }
+      __syncthreads();
+      for (uint32_t i = lane; i < tn; i += 64) {  // fold each key's occurrences in arrival order
+        uint32_t key = s_key[i];
+        bool leader = true;
+        for (uint32_t j = 0; j < i; j++)
+          if (s_key[j] == key) {
+            leader = false;
+            break;
+          }
+        if (!leader) continue;
+        uint64_t w0 = row[key], w = w0;
+        c_rd++;
+        for (uint32_t j = i; j < tn; j++) {
+          if (s_key[j] != key) continue;
+          bool acc, st;
+          w = merge_word(d, w, s_val[j], acc, st);
+          c_stale += st;
+          if (acc) {
+            c_acc++;
+            s_accf[j] = 1;
+            s_acc[j] = w;
+          }
+        }
+        if (w != w0) {
+          row[key] = w;
+          c_wr++;
+          unsigned long long x = exp_time(d.p, w);
+          mexp = x < mexp ? x : mexp;
+        }
+      }
+      c_merge += (lane == 0) ? tn : 0;
+      __syncthreads();
+      for (uint32_t b0 = 0; b0 < tn; b0 += 64) {  // ordered ballot compaction -> retransmit jobs
+        uint32_t i = b0 + lane;
+        bool f = i < tn && s_accf[i] && (s_key[i] / d.S != v);
+        unsigned long long m = __ballot(f);
+        uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (f && n_retx + pos < room)
+          d.fifo[(size_t)v * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
+              make_job(s_acc[i], 0, s_key[i], meta_of(GX_JOB_RETX, 0, 1));
+        n_retx += (uint32_t)__popcll(m);
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  c_merge = wave_sum(c_merge);
+  c_acc = wave_sum(c_acc);
+  c_stale = wave_sum(c_stale);
+  c_rd = wave_sum(c_rd);
+  c_wr = wave_sum(c_wr);
+  mexp = wave_min(mexp);
+  if (lane == 0) {
+    uint32_t ok = n_retx < room ? n_retx : room;
+    h->fifo_tail = tail0 + ok;
+    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 8ull * deg, c_merge);
+    ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
+    ctr_atomic(d, C_GOSSIP_ACC, c_acc);
+    ctr_atomic(d, C_STALE, c_stale);
+    ctr_atomic(d, C_RETX, ok);
+    ctr_atomic(d, C_QDROP, n_retx - ok);
+    if (c_wr) {
+      mark_change(d);
+      atomicMin(&d.minexp[v], mexp);
+    }
+  }
+}
+
+// ============================================================= phase 5: anti-entropy push-pull ==
+// Dense view-pair merge: a <- b and, when `both`, b <- a's pre-exchange words. VEC streams both
+// rows with 16-B loads, 4 slots per thread per 1024-slot tile, and compacts each side's
+// retransmits in key order with one packed block scan per tile.
+template <bool VEC>
+GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
+                 unsigned long long *s_red) {
+  uint64_t *A = &d.view[(size_t)a * d.R];
+  uint64_t *B = &d.view[(size_t)b * d.R];
+  gx_host_state *ha = &d.hs[a], *hb = &d.hs[b];
+  uint32_t ta0 = ha->fifo_tail, ca0 = ta0 - ha->fifo_head;
+  uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
+  uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
+  uint32_t na = 0, nb = 0;
+  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, ma = ~0ull, mb = ~0ull;
+  uint32_t t = threadIdx.x;
+  for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
+    uint64_t wa[4], wb[4], nwa[4], nwb[4];
+    bool fa[4], fb[4];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
+      bool v0 = r0 < d.R, v1 = r0 + 1 < d.R;
+      if (VEC && v0) {
+        ulonglong2 pa = *reinterpret_cast<const ulonglong2 *>(&A[r0]);
+        ulonglong2 pb = *reinterpret_cast<const ulonglong2 *>(&B[r0]);
+        wa[2 * h] = pa.x;
+        wa[2 * h + 1] = pa.y;
+        wb[2 * h] = pb.x;
+        wb[2 * h + 1] = pb.y;
+      } else {
+        wa[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
+        wa[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
+        wb[2 * h] = v0 ? B[r0] : GX_SLOT_ABSENT;
+        wb[2 * h + 1] = v1 ? B[r0 + 1] : GX_SLOT_ABSENT;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+      nwa[k] = wa[k];
+      nwb[k] = wb[k];
+      fa[k] = fb[k] = false;
+      if (st_of(wb[k]) != GX_ABSENT) {  // a.Merge(b): every present record of b
+        bool ac, st;
+        c_merge++;
+        nwa[k] = merge_word(d, wa[k], wb[k], ac, st);
+        c_stale += st;
+        if (ac) {
+          c_acc++;
+          fa[k] = r / d.S != a;
+        }
+      }
+      if (both && st_of(wa[k]) != GX_ABSENT) {  // b.Merge(a's snapshot)
+        bool ac, st;
+        c_merge++;
+        nwb[k] = merge_word(d, wb[k], wa[k], ac, st);
+        c_stale += st;
+        if (ac) {
+          c_acc++;
+          fb[k] = r / d.S != b;
+        }
+      }
+      if (nwa[k] != wa[k]) {
+        c_wr++;
+        unsigned long long x = exp_time(d.p, nwa[k]);
+        ma = x < ma ? x : ma;
+      }
+      if (nwb[k] != wb[k]) {
+        c_wr++;
+        unsigned long long x = exp_time(d.p, nwb[k]);
+        mb = x < mb ? x : mb;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
+      bool cha = nwa[2 * h] != wa[2 * h] || nwa[2 * h + 1] != wa[2 * h + 1];
+      bool chb = nwb[2 * h] != wb[2 * h] || nwb[2 * h + 1] != wb[2 * h + 1];
+      if (VEC) {
+        if (cha) *reinterpret_cast<ulonglong2 *>(&A[r0]) = make_ulonglong2(nwa[2 * h], nwa[2 * h + 1]);
+        if (chb) *reinterpret_cast<ulonglong2 *>(&B[r0]) = make_ulonglong2(nwb[2 * h], nwb[2 * h + 1]);
+      } else {
+        if (nwa[2 * h] != wa[2 * h]) A[r0] = nwa[2 * h];
+        if (nwa[2 * h + 1] != wa[2 * h + 1]) A[r0 + 1] = nwa[2 * h + 1];
+        if (nwb[2 * h] != wb[2 * h]) B[r0] = nwb[2 * h];
+        if (nwb[2 * h + 1] != wb[2 * h + 1]) B[r0 + 1] = nwb[2 * h + 1];
+      }
+    }
+    unsigned long long cnt = (unsigned long long)(fa[0] + fa[1]) | ((unsigned long long)(fa[2] + fa[3]) << 16) |
+                             ((unsigned long long)(fb[0] + fb[1]) << 32) | ((unsigned long long)(fb[2] + fb[3]) << 48);
+    unsigned long long tot;
+    unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
+    uint32_t pa[4], pb[4];
+    pa[0] = na + fld(pre, 0);
+    pa[1] = pa[0] + fa[0];
+    pa[2] = na + fld(tot, 0) + fld(pre, 1);
+    pa[3] = pa[2] + fa[2];
+    pb[0] = nb + fld(pre, 2);
+    pb[1] = pb[0] + fb[0];
+    pb[2] = nb + fld(tot, 2) + fld(pre, 3);
+    pb[3] = pb[2] + fb[2];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+      if (fa[k] && pa[k] < rooma)
+        d.fifo[(size_t)a * d.Q + ((ta0 + pa[k]) % d.Q)] = make_job(nwa[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+      if (fb[k] && pb[k] < roomb)
+        d.fifo[(size_t)b * d.Q + ((tb0 + pb[k]) % d.Q)] = make_job(nwb[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+    }
+    na += fld(tot, 0) + fld(tot, 1);
+    nb += fld(tot, 2) + fld(tot, 3);
+  }
+  ma = block_min(ma, s_red);
+  mb = block_min(mb, s_red);
+  bool changed = c_wr != 0;
+  if (__ballot(changed) != 0 && (t & 63) == 0) mark_change(d);
+  c_wr = wave_sum(c_wr);
+  if ((t & 63) == 0) kbytes(d, GX_K_AE, 8ull * c_wr, 0);
+  block_ctr(d, C_AE_MERGES, c_merge, s_red);
+  block_ctr(d, C_AE_ACC, c_acc, s_red);
+  block_ctr(d, C_STALE, c_stale, s_red);
+  if (t == 0) {
+    if (ma != ~0ull) atomicMin(&d.minexp[a], ma);
+    if (mb != ~0ull) atomicMin(&d.minexp[b], mb);
+    uint32_t oka = na < rooma ? na : rooma, okb = nb < roomb ? nb : roomb;
+    ha->fifo_tail = ta0 + oka;
+    if (both) hb->fifo_tail = tb0 + okb;
+    ctr_atomic(d, C_RETX, oka + (both ? okb : 0));
+    ctr_atomic(d, C_QDROP, (na - oka) + (both ? nb - okb : 0));
+    ctr_atomic(d, C_AESLOTS, (unsigned long long)d.R * (both ? 2 : 1));
+    kbytes(d, GX_K_AE, 16ull * d.R + 32ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
+    if (both) ctr_atomic(d, C_AEX, 1);
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_ae(Dev d, uint64_t key0, uint64_t key1) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  uint32_t t = blockIdx.x, base = 0, m = d.H, q = t;
+  uint64_t key = key0;
+  if (d.partitioned) {
+    uint32_t m0 = d.H / 2, np0 = m0 / 2;
+    if (t < np0) {
+      m = m0;
+    } else {
+      base = m0;
+      m = d.H - m0;
+      q = t - np0;
+      key = key1;
+    }
+  }
+  uint32_t a = base + feistel_perm(key, 2 * q, m);
+  uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
+  ae_pair<VEC>(d, a, b, true, s_wave, s_red);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32_t src) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  ae_pair<VEC>(d, dst, src, false, s_wave, s_red);
+}
+
+// ================================================================ convergence / digests ==
+__global__ void k_converged(Dev d, unsigned long long *bad) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  bool dis = false;
+  if (r < d.R) {
+    uint64_t w0 = d.view[r];
+    for (uint32_t v = 1; v < d.H; v++)
+      if (d.view[(size_t)v * d.R + r] != w0) {
+        dis = true;
+        break;
+      }
+  }
+  unsigned long long c = wave_sum(dis ? 1ull : 0ull);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}
+
+GXD uint64_t feed(uint64_t h, uint64_t x) { return mix64(h ^ x); }
+GXD uint64_t feed_job(uint64_t h, const gx_job &j) {
+  h = feed(h, j.a);
+  h = feed(h, j.b);
+  h = feed(h, (uint64_t)j.c | ((uint64_t)j.meta << 32));
+  return feed(h, (uint64_t)j.wake | ((uint64_t)j.aux << 32));
+}
+__global__ void k_digest(Dev d, uint64_t *out) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= d.H) return;
+  const gx_host_state s = d.hs[v];
+  uint64_t h = 0x243F6A8885A308D3ull;
+  for (uint32_t i = s.fifo_head; i != s.fifo_tail; i++) h = feed_job(h, d.fifo[(size_t)v * d.Q + (i % d.Q)]);
+  h = feed(h, 0xF1F0);
+  for (uint32_t i = s.sleep_head; i != s.sleep_tail; i++) h = feed_job(h, d.sleep[(size_t)v * d.SQ + (i % d.SQ)]);
+  h = feed(h, 0x51EE);
+  h = feed(h, s.dq_len);
+  for (uint32_t i = 0; i < s.dq_len; i++) {
+    grec g = d.dq[(size_t)v * d.DQ + ((s.dq_head + i) & (d.DQ - 1))];
+    h = feed(h, g.w);
+    h = feed(h, g.r);
+  }
+  h = feed(h, 0xA7E4);
+  for (uint32_t a = 0; a < d.A; a++) {
+    if (!((s.arena_used >> a) & 1u)) continue;
+    uint32_t len = d.arena_len[(size_t)v * d.A + a];
+    h = feed(h, a);
+    h = feed(h, len);
+    for (uint32_t i = 0; i < len; i++) {
+      grec g = d.arena[((size_t)v * d.A + a) * d.L + i];
+      h = feed(h, g.w);
+      h = feed(h, g.r);
+    }
+  }
+  h = feed(h, s.flags);
+  h = feed(h, (uint64_t)s.bs_next);
+  h = feed(h, (uint64_t)s.bt_next);
+  h = feed(h, (uint64_t)s.last_bcast_ns);
+  h = feed(h, s.running);
+  out[v] = h;
+}
+
+// ========================================================= single-host ABI kernels (64 lanes) ==
+// Lane 0 runs the scalar reference logic; all lanes join the counter flush.
+__global__ void k_api_add(Dev d, const uint32_t *views, uint32_t fixed_view, const grec *recs, uint32_t n, int src,
+                          uint32_t *acc_out) {
+  Acc a;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < n; i++) acc += add_entry(d, a, views ? views[i] : fixed_view, recs[i], src);
+    *acc_out = acc;
+  }
+  acc_flush(d, a);
+}
+__global__ void k_api_expire(Dev d, uint32_t v, uint32_t o, uint32_t *out) {
+  Acc a;
+  if (threadIdx.x == 0) *out = expire_server(d, a, v, o);
+  acc_flush(d, a);
+}
+__global__ void k_api_send(Dev d, uint32_t v, const grec *list, uint32_t n, uint32_t np) {
+  Acc a;
+  if (threadIdx.x == 0) {
+    int slot = alloc_list(d, a, v);
+    if (slot >= 0) {
+      uint32_t m = n < d.L ? n : d.L;
+      grec *dst = list_ptr(d, v, slot);
+      for (uint32_t i = 0; i < m; i++) dst[i] = list[i];
+      commit_send(d, a, v, slot, m, np);
+    }
+  }
+  acc_flush(d, a);
+}
+__global__ void k_api_bs(Dev d, uint32_t v, const grec *list, uint32_t n) {
+  Acc a;
+  if (threadIdx.x == 0) {
+    uint64_t inc;
+    bs_body_list(d, a, v, list, n, inc);
+  }
+  acc_flush(d, a);
+}
+__global__ void k_api_bt(Dev d, uint32_t v, uint64_t running, const grec *others, const uint32_t *n_others) {
+  Acc a;
+  if (threadIdx.x == 0) {
+    uint32_t n = *n_others;
+    bt_finish(d, a, v, running, others, n < d.L ? n : d.L);
+  }
+  acc_flush(d, a);
+}
+__global__ void k_api_tomb(Dev d, uint32_t v, uint64_t running, uint64_t *out_mask) {
+  Acc a;
+  if (threadIdx.x == 0) *out_mask = tombstone_services(d, a, v, running);
+  acc_flush(d, a);
+}
+__global__ void k_api_getb(Dev d, uint32_t v, uint32_t limit, grec *out, uint32_t *n_out) {
+  Acc a;
+  if (threadIdx.x == 0) *n_out = get_broadcasts(d, a, v, limit, out);
+  acc_flush(d, a);
+}
+__global__ void k_api_is_new(Dev d, uint32_t v, uint64_t w, uint32_t r, uint32_t *out) {
+  if (threadIdx.x == 0) *out = is_new(d, v, w, r);
+}
+__global__ void k_api_set_slot(Dev d, uint32_t v, uint32_t r, uint64_t w) {
+  Acc a;
+  if (threadIdx.x == 0) set_slot(d, a, v, &d.view[(size_t)v * d.R + r], w);
+  acc_flush(d, a);
+}
+__global__ void k_api_mark(Dev d) {
+  if (threadIdx.x == 0) mark_change(d);
+}
