@@ -1,0 +1,33 @@
+"""Round-model golden fixtures (tests/golden/make_golden.py): the CPU oracle must reproduce them
+exactly (CPU), and so must the HIP engine (GPU)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden.make_golden import CASES, run
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def check(lib, name):
+    ref = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    kw, rounds = CASES[name]
+    assert json.loads(str(ref["params"])) == kw and int(ref["rounds"]) == rounds
+    got = run(lib, kw, rounds)
+    assert json.loads(got["stats"]) == json.loads(str(ref["stats"]))
+    assert np.array_equal(got["views"], ref["views"])
+    assert np.array_equal(got["hosts"], ref["hosts"])
+    assert np.array_equal(got["digests"], ref["digests"])
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_oracle_matches_golden(oracle_lib, name):
+    check(oracle_lib, name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_gpu_matches_golden(gx_lib, name):
+    check(gx_lib, name)
