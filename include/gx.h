@@ -130,6 +130,8 @@ typedef struct gx_params {
   int32_t partition_end;
   int32_t storm_round;                /* round at which every host ExpireServer()s the other half, -1 = none */
   int32_t device;                     /* HIP device ordinal (ignored by the oracle) */
+  uint32_t n_shards;                  /* host sharding: 0/1 = this engine owns every host */
+  uint32_t shard_id;                  /* this engine owns hosts [id*H/n, (id+1)*H/n) */
 } gx_params;
 
 /* Per-host bookkeeping (read-back for parity). */
@@ -208,6 +210,32 @@ int gx_enable_timing(gx_engine *e, int on);
 /* ---- whole-round driver (the hot path) ---------------------------------------------------- */
 /* Runs n_rounds rounds of the seeded schedule (DESIGN.md "Round model"). */
 int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
+
+/* ---- sharded rounds ----------------------------------------------------------
+ * A round of a sharded engine is driven phase by phase by an exchange layer (sidecar_amd/dist.py,
+ * torch.distributed: RCCL between GPUs, gloo for the CPU oracle). Exchange buffers are device
+ * memory for the HIP engine and host memory for the oracle; `bytes_per_shard` has n_shards
+ * entries. Wire formats (both little-endian):
+ *   packet: u32 key (= sender * fanout + j), u32 receiver, u32 len, u32 0, then len x {u64 word,
+ *           u32 record key, u32 0}; packets grouped by destination shard, ascending key.
+ *   row:    u32 pair index, u32 host, u64 0, then R = H*S u64 words; rows grouped by destination
+ *           shard, ascending pair index.
+ * gx_run_rounds(e, n) on an unsharded engine equals n x (round_send, round_merge, ae_merge with
+ * nothing received, round_end). */
+int gx_round_send(gx_engine *e);  /* phases 0-3: wake, owner ticks, storm, GetBroadcasts */
+int gx_outbox_bytes(gx_engine *e, uint64_t *bytes_per_shard);
+int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap);
+int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes);
+int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + received packets */
+int gx_ae_bytes(gx_engine *e, uint64_t *bytes_per_shard); /* 0s unless this is a push-pull round */
+int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap);
+int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes); /* phase 5 */
+int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */
+/* Per-record min and max slot word over this engine's views (R entries each; device memory for
+ * the HIP engine), written as (word XOR 2^63) so that signed 64-bit MIN/MAX reductions across
+ * shards order them like the unsigned words. All views agree on record r iff the reduced min
+ * equals the reduced max. */
+int gx_view_minmax(gx_engine *e, uint64_t *min_out, uint64_t *max_out);
 
 /* ---- catalog.ServicesState ---------------------------------------------------------------- */
 /* AddServiceEntry, services_state.go:293-347, applied in array order (views[i] <- svcs[i]). */

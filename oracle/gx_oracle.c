@@ -32,6 +32,9 @@ enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS =
 struct gx_engine {
   gx_params p;
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  uint32_t G, gid, lo, hi; /* shards; this engine owns hosts [lo, hi). Arrays stay H-sized. */
+  uint64_t *rows_in;       /* received push-pull rows (this AE round) */
+  uint32_t n_rows_in;
   int64_t round;
   uint64_t *view;       /* H * R packed slots */
   uint8_t *own_status;  /* H * S local service status (discovery/health) */
@@ -514,7 +517,75 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
   free(sa);
 }
 
-static void ae_phase(gx_engine *e, int64_t now) {
+static uint32_t shard_lo(const gx_engine *e, uint32_t g) { return (uint32_t)(((uint64_t)g * e->H) / e->G); }
+static uint32_t shard_of(const gx_engine *e, uint32_t v) {
+  uint32_t g = 0;
+  while (g + 1 < e->G && shard_lo(e, g + 1) <= v) g++;
+  return g;
+}
+static int is_local(const gx_engine *e, uint32_t v) { return v >= e->lo && v < e->hi; }
+
+/* Phases 0-3 of the current round for this engine's hosts. */
+static void round_send(gx_engine *e) {
+  int64_t now = now_of(e);
+  uint32_t H = e->H, K = e->K, cap = e->p.packet_cap;
+  for (uint32_t v = e->lo; v < e->hi; v++) wake_host(e, v);
+  /* owners: discovery churn, BroadcastServices(+TrackNewServices), BroadcastTombstones */
+  for (uint32_t o = e->lo; o < e->hi; o++) {
+    churn(e, o);
+    gx_host_state *h = &e->hs[o];
+    if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
+    if (!(h->flags & 2u) && h->bt_next <= e->round) bt_tick(e, o, now);
+  }
+  /* SWIM departure storm: NotifyLeave -> ExpireServer for every host of the other half */
+  if (e->p.storm_round >= 0 && e->round == e->p.storm_round) {
+    uint32_t half = H / 2;
+    for (uint32_t v = e->lo; v < e->hi; v++) {
+      uint32_t lo = v < half ? half : 0, hi = v < half ? H : half;
+      for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
+    }
+  }
+  /* gossip send: GetBroadcasts once per selected peer */
+  for (size_t i = 0; i < (size_t)H * K; i++) e->msg_len[i] = 0;
+  for (uint32_t u = e->lo; u < e->hi; u++) {
+    uint32_t peers[64];
+    uint32_t np = sample_peers(e, u, peers);
+    for (uint32_t j = 0; j < np; j++) {
+      uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap]);
+      e->msg_len[(size_t)u * K + j] = l;
+      e->msg_dst[(size_t)u * K + j] = peers[j];
+      if (l == 0 && e->p.gossip_stop_on_empty) break;
+    }
+  }
+}
+
+/* Phase 4: packets to this engine's receivers in sender order -> NotifyMsg -> AddServiceEntry.
+ * Packets from other shards were unpacked into the same H*K message table. */
+static void round_merge(gx_engine *e) {
+  int64_t now = now_of(e);
+  uint32_t H = e->H, K = e->K, cap = e->p.packet_cap;
+  memset(e->in_cnt, 0, sizeof(uint32_t) * (H + 1));
+  for (size_t m = 0; m < (size_t)H * K; m++)
+    if (e->msg_len[m] && is_local(e, e->msg_dst[m])) e->in_cnt[e->msg_dst[m] + 1]++;
+  for (uint32_t v = 0; v < H; v++) e->in_cnt[v + 1] += e->in_cnt[v];
+  uint32_t *cur = (uint32_t *)malloc(sizeof(uint32_t) * H);
+  memcpy(cur, e->in_cnt, sizeof(uint32_t) * H);
+  for (size_t m = 0; m < (size_t)H * K; m++)
+    if (e->msg_len[m] && is_local(e, e->msg_dst[m])) e->in_list[cur[e->msg_dst[m]]++] = (uint32_t)m;
+  free(cur);
+  for (uint32_t v = e->lo; v < e->hi; v++)
+    for (uint32_t i = e->in_cnt[v]; i < e->in_cnt[v + 1]; i++) {
+      uint32_t m = e->in_list[i];
+      for (uint32_t x = 0; x < e->msg_len[m]; x++) add_entry(e, v, e->msg[(size_t)m * cap + x], now, SRC_GOSSIP);
+    }
+}
+
+static int ae_round(const gx_engine *e) {
+  return e->p.ae_period_rounds && (uint64_t)e->round % e->p.ae_period_rounds == e->p.ae_phase;
+}
+
+/* Push-pull pairs of this round in global pair order t: (a, b). Returns the count. */
+static uint32_t ae_pairs(const gx_engine *e, uint32_t *pa, uint32_t *pb) {
   uint32_t groups[2][2];
   int ng;
   if (partitioned(e)) {
@@ -525,72 +596,78 @@ static void ae_phase(gx_engine *e, int64_t now) {
     groups[0][0] = 0; groups[0][1] = e->H;
     ng = 1;
   }
+  uint32_t n = 0;
   for (int g = 0; g < ng; g++) {
     uint32_t base = groups[g][0], m = groups[g][1];
     uint64_t key = rng4(e->p.seed, ST_AE, (uint64_t)e->round, base, 0);
     for (uint32_t t = 0; t + 1 < m; t += 2) {
-      uint32_t a = base + feistel_perm(key, t, m), b = base + feistel_perm(key, t + 1, m);
-      ae_exchange(e, a, b, now);
+      pa[n] = base + feistel_perm(key, t, m);
+      pb[n] = base + feistel_perm(key, t + 1, m);
+      n++;
     }
   }
+  return n;
+}
+
+/* x <- a remote host's row (one direction of a cross-shard push-pull pair). */
+static void ae_merge_row(gx_engine *e, uint32_t x, const uint64_t *row, int count_exchange, int64_t now) {
+  for (uint32_t r = 0; r < e->R; r++) {
+    if (st_of(row[r]) == GX_ABSENT) continue;
+    grec u = {row[r], r, 0};
+    add_entry(e, x, u, now, SRC_AE);
+  }
+  e->st.ae_slots += e->R;
+  if (count_exchange) e->st.ae_exchanges++;
+}
+
+/* Phase 5: pairs with both hosts here merge both ways; cross-shard pairs merge the received
+ * row of the remote member (rows arrive grouped by source shard, ascending pair index). */
+static void ae_phase(gx_engine *e, const uint64_t *rows, uint64_t bytes) {
+  if (!ae_round(e)) return;
+  int64_t now = now_of(e);
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t np = ae_pairs(e, pa, pb);
+  size_t row_bytes = 16 + 8ull * e->R;
+  /* index of each cross pair's row in the received buffer */
+  size_t next = 0;
+  for (uint32_t g = 0; g < e->G; g++) {
+    if (g == e->gid) continue;
+    for (uint32_t t = 0; t < np; t++) {
+      int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
+      uint32_t remote = la ? pb[t] : pa[t];
+      if (la == lb || shard_of(e, remote) != g) continue;
+      const uint8_t *rec = (const uint8_t *)rows + next * row_bytes;
+      if ((next + 1) * row_bytes > bytes) break;
+      uint32_t hdr_t, hdr_h;
+      memcpy(&hdr_t, rec, 4);
+      memcpy(&hdr_h, rec + 4, 4);
+      if (hdr_t == t && hdr_h == remote) {
+        uint64_t *row = (uint64_t *)malloc(8ull * e->R);
+        memcpy(row, rec + 16, 8ull * e->R);
+        ae_merge_row(e, la ? pa[t] : pb[t], row, la, now);
+        free(row);
+      }
+      next++;
+    }
+  }
+  for (uint32_t t = 0; t < np; t++)
+    if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
+  free(pa);
+  free(pb);
+}
+
+static void round_end(gx_engine *e) {
+  e->round++;
+  e->st.round = e->round;
+  for (uint32_t v = e->lo; v < e->hi; v++) wake_host(e, v);
 }
 
 static void run_one_round(gx_engine *e) {
-  int64_t now = now_of(e);
-  uint32_t H = e->H, K = e->K, cap = e->p.packet_cap;
-  for (uint32_t v = 0; v < H; v++) wake_host(e, v);
-  /* owners: discovery churn, BroadcastServices(+TrackNewServices), BroadcastTombstones */
-  for (uint32_t o = 0; o < H; o++) {
-    churn(e, o);
-    gx_host_state *h = &e->hs[o];
-    if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
-    if (!(h->flags & 2u) && h->bt_next <= e->round) bt_tick(e, o, now);
-  }
-  /* SWIM departure storm: NotifyLeave -> ExpireServer for every host of the other half */
-  if (e->p.storm_round >= 0 && e->round == e->p.storm_round) {
-    uint32_t half = H / 2;
-    for (uint32_t v = 0; v < H; v++) {
-      uint32_t lo = v < half ? half : 0, hi = v < half ? H : half;
-      for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
-    }
-  }
-  /* gossip send: GetBroadcasts once per selected peer */
-  for (uint32_t u = 0; u < H; u++) {
-    uint32_t peers[64];
-    uint32_t np = sample_peers(e, u, peers);
-    for (uint32_t j = 0; j < K; j++) {
-      e->msg_len[(size_t)u * K + j] = 0;
-      e->msg_dst[(size_t)u * K + j] = 0xffffffffu;
-    }
-    for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap]);
-      e->msg_len[(size_t)u * K + j] = l;
-      e->msg_dst[(size_t)u * K + j] = peers[j];
-      if (l == 0 && e->p.gossip_stop_on_empty) break;
-    }
-  }
-  /* gossip receive: packets to v in sender order -> NotifyMsg -> AddServiceEntry */
-  memset(e->in_cnt, 0, sizeof(uint32_t) * (H + 1));
-  for (uint32_t u = 0; u < H; u++)
-    for (uint32_t j = 0; j < K; j++)
-      if (e->msg_len[(size_t)u * K + j]) e->in_cnt[e->msg_dst[(size_t)u * K + j] + 1]++;
-  for (uint32_t v = 0; v < H; v++) e->in_cnt[v + 1] += e->in_cnt[v];
-  uint32_t *cur = (uint32_t *)malloc(sizeof(uint32_t) * H);
-  memcpy(cur, e->in_cnt, sizeof(uint32_t) * H);
-  for (uint32_t u = 0; u < H; u++)
-    for (uint32_t j = 0; j < K; j++)
-      if (e->msg_len[(size_t)u * K + j]) e->in_list[cur[e->msg_dst[(size_t)u * K + j]]++] = u * K + j;
-  free(cur);
-  for (uint32_t v = 0; v < H; v++)
-    for (uint32_t i = e->in_cnt[v]; i < e->in_cnt[v + 1]; i++) {
-      uint32_t m = e->in_list[i];
-      for (uint32_t x = 0; x < e->msg_len[m]; x++) add_entry(e, v, e->msg[(size_t)m * cap + x], now, SRC_GOSSIP);
-    }
-  /* anti-entropy push-pull */
-  if (e->p.ae_period_rounds && (uint64_t)e->round % e->p.ae_period_rounds == e->p.ae_phase) ae_phase(e, now);
-  e->round++;
-  e->st.round = e->round;
-  for (uint32_t v = 0; v < H; v++) wake_host(e, v);
+  round_send(e);
+  round_merge(e);
+  ae_phase(e, NULL, 0);
+  round_end(e);
 }
 
 /* ---------------------------------------------------------------------------- ABI ------- */
@@ -645,6 +722,7 @@ static int check_params(const gx_params *p) {
   if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
   if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
+  if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   return GX_OK;
 }
 
@@ -691,6 +769,10 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->A = p->list_slots;
   e->L = p->packet_cap + p->pending_cap;
   e->K = p->fanout;
+  e->G = p->n_shards > 1 ? p->n_shards : 1;
+  e->gid = e->G > 1 ? p->shard_id : 0;
+  e->lo = shard_lo(e, e->gid);
+  e->hi = shard_lo(e, e->gid + 1);
   e->SQ = pow2_at_least(64 > e->K * (p->retransmit_rounds + 1) ? 64 : e->K * (p->retransmit_rounds + 1));
   e->DQ = pow2_at_least(e->L + p->pending_cap + 64);
   size_t H = e->H;
@@ -754,7 +836,7 @@ int gx_enable_timing(gx_engine *e, int on) {
 }
 
 int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
-  if (!e) return GX_EINVAL;
+  if (!e || e->G > 1) return GX_EINVAL;
   for (uint32_t i = 0; i < n_rounds; i++) run_one_round(e);
   return GX_OK;
 }
@@ -946,7 +1028,7 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
 }
 
 int gx_read_views(gx_engine *e, uint32_t lo, uint32_t hi, uint64_t *out) {
-  if (!e || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
+  if (!e || lo > hi || lo < e->lo || hi > e->hi || (hi > lo && !out)) return GX_EINVAL;
   memcpy(out, &e->view[(size_t)lo * e->R], sizeof(uint64_t) * (size_t)(hi - lo) * e->R);
   return GX_OK;
 }
@@ -973,7 +1055,7 @@ int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc) {
   return GX_OK;
 }
 int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out) {
-  if (!e || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
+  if (!e || lo > hi || lo < e->lo || hi > e->hi || (hi > lo && !out)) return GX_EINVAL;
   memcpy(out, &e->hs[lo], sizeof(gx_host_state) * (hi - lo));
   return GX_OK;
 }
@@ -1018,7 +1100,7 @@ static uint64_t feed_job(uint64_t h, const gx_job *j) {
 }
 int gx_host_digests(gx_engine *e, uint64_t *out) {
   if (!e || !out) return GX_EINVAL;
-  for (uint32_t v = 0; v < e->H; v++) {
+  for (uint32_t v = e->lo; v < e->hi; v++) {
     const gx_host_state *s = &e->hs[v];
     uint64_t h = 0x243F6A8885A308D3ull;
     for (uint32_t i = s->fifo_head; i != s->fifo_tail; i++) h = feed_job(h, &e->fifo[(size_t)v * e->Q + (i % e->Q)]);
@@ -1048,7 +1130,128 @@ int gx_host_digests(gx_engine *e, uint64_t *out) {
     h = feed(h, (uint64_t)s->bt_next);
     h = feed(h, (uint64_t)s->last_bcast_ns);
     h = feed(h, s->running);
-    out[v] = h;
+    out[v - e->lo] = h;
+  }
+  return GX_OK;
+}
+
+/* ---------------------------------------------------------------------- sharded rounds -- */
+static size_t slot_bytes(const gx_engine *e) { return 16 + 16ull * e->p.packet_cap; }
+static size_t row_bytes(const gx_engine *e) { return 16 + 8ull * e->R; }
+
+int gx_round_send(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  round_send(e);
+  return GX_OK;
+}
+int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
+  if (!e || !bytes) return GX_EINVAL;
+  for (uint32_t g = 0; g < e->G; g++) bytes[g] = 0;
+  for (size_t m = (size_t)e->lo * e->K; m < (size_t)e->hi * e->K; m++)
+    if (e->msg_len[m] && !is_local(e, e->msg_dst[m])) bytes[shard_of(e, e->msg_dst[m])] += slot_bytes(e);
+  return GX_OK;
+}
+int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  uint8_t *p = (uint8_t *)buf;
+  size_t off = 0, sb = slot_bytes(e);
+  for (uint32_t g = 0; g < e->G; g++)
+    for (size_t m = (size_t)e->lo * e->K; m < (size_t)e->hi * e->K; m++) {
+      if (!e->msg_len[m] || is_local(e, e->msg_dst[m]) || shard_of(e, e->msg_dst[m]) != g) continue;
+      if (off + sb > cap) return GX_EINVAL;
+      uint32_t hdr[4] = {(uint32_t)m, e->msg_dst[m], e->msg_len[m], 0};
+      memset(p + off, 0, sb);
+      memcpy(p + off, hdr, 16);
+      memcpy(p + off + 16, &e->msg[m * e->p.packet_cap], 16ull * e->msg_len[m]);
+      off += sb;
+    }
+  return GX_OK;
+}
+int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
+  if (!e || (bytes && !buf)) return GX_EINVAL;
+  size_t sb = slot_bytes(e);
+  if (bytes % sb) return GX_EINVAL;
+  const uint8_t *p = (const uint8_t *)buf;
+  for (size_t off = 0; off < bytes; off += sb) {
+    uint32_t hdr[4];
+    memcpy(hdr, p + off, 16);
+    uint32_t m = hdr[0], dst = hdr[1], len = hdr[2];
+    if (m >= e->H * e->K || !is_local(e, dst) || len > e->p.packet_cap) return GX_EINVAL;
+    memcpy(&e->msg[(size_t)m * e->p.packet_cap], p + off + 16, 16ull * len);
+    e->msg_len[m] = len;
+    e->msg_dst[m] = dst;
+  }
+  return GX_OK;
+}
+int gx_round_merge(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  round_merge(e);
+  return GX_OK;
+}
+int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
+  if (!e || !bytes) return GX_EINVAL;
+  for (uint32_t g = 0; g < e->G; g++) bytes[g] = 0;
+  if (!ae_round(e) || e->G < 2) return GX_OK;
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t np = ae_pairs(e, pa, pb);
+  for (uint32_t t = 0; t < np; t++) {
+    int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
+    if (la != lb) bytes[shard_of(e, la ? pb[t] : pa[t])] += row_bytes(e);
+  }
+  free(pa);
+  free(pb);
+  return GX_OK;
+}
+int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (!ae_round(e) || e->G < 2) return GX_OK;
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t np = ae_pairs(e, pa, pb);
+  uint8_t *p = (uint8_t *)buf;
+  size_t off = 0, rb = row_bytes(e);
+  int rc = GX_OK;
+  for (uint32_t g = 0; g < e->G && rc == GX_OK; g++)
+    for (uint32_t t = 0; t < np; t++) {
+      int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
+      if (la == lb) continue;
+      uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
+      if (shard_of(e, other) != g) continue;
+      if (off + rb > cap) {
+        rc = GX_EINVAL;
+        break;
+      }
+      uint32_t hdr[4] = {t, mine, 0, 0};
+      memcpy(p + off, hdr, 16);
+      memcpy(p + off + 16, &e->view[(size_t)mine * e->R], 8ull * e->R);
+      off += rb;
+    }
+  free(pa);
+  free(pb);
+  return rc;
+}
+int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
+  if (!e || (bytes && !buf)) return GX_EINVAL;
+  ae_phase(e, (const uint64_t *)buf, bytes);
+  return GX_OK;
+}
+int gx_round_end(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  round_end(e);
+  return GX_OK;
+}
+int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
+  if (!e || !mn || !mx) return GX_EINVAL;
+  for (uint32_t r = 0; r < e->R; r++) {
+    uint64_t a = ~0ull, b = 0;
+    for (uint32_t v = e->lo; v < e->hi; v++) {
+      uint64_t w = e->view[(size_t)v * e->R + r];
+      a = w < a ? w : a;
+      b = w > b ? w : b;
+    }
+    mn[r] = a ^ (1ull << 63);
+    mx[r] = b ^ (1ull << 63);
   }
   return GX_OK;
 }
@@ -1065,7 +1268,7 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
   return GX_OK;
 }
 int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
-  if (!e) return GX_EINVAL;
+  if (!e || e->G > 1) return GX_EINVAL;
   uint64_t bad = 0;
   for (uint32_t r = 0; r < e->R; r++) {
     uint64_t w0 = e->view[r];

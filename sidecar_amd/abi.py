@@ -78,7 +78,8 @@ class GxParams(C.Structure):
         ("pass_increment_ns", C.c_int64), ("tombstone_bump_ns", C.c_int64),
         ("seed", C.c_uint64), ("churn_ppm", C.c_uint32), ("aged_ppm", C.c_uint32),
         ("aged_max_ns", C.c_int64), ("partition_start", C.c_int32), ("partition_end", C.c_int32),
-        ("storm_round", C.c_int32), ("device", C.c_int32),
+        ("storm_round", C.c_int32), ("device", C.c_int32), ("n_shards", C.c_uint32),
+        ("shard_id", C.c_uint32),
     ]
 
 
@@ -119,7 +120,9 @@ ABI_FUNCS = [
     "gx_get_broadcasts", "gx_local_state", "gx_merge_remote_state", "gx_notify_leave",
     "gx_read_views", "gx_write_views", "gx_write_slot", "gx_read_hosts", "gx_read_queue",
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
-    "gx_timing_get", "gx_converged",
+    "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
+    "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
+    "gx_view_minmax",
 ]
 
 
@@ -157,6 +160,11 @@ def _declare(lib):
         "gx_host_digests": ([vp, vp], i32), "gx_stats_get": ([vp, P(GxStats)], i32),
         "gx_timing_get": ([vp, P(GxTiming)], i32),
         "gx_converged": ([vp, P(i32), P(C.c_uint64)], i32),
+        "gx_round_send": ([vp], i32), "gx_outbox_bytes": ([vp, vp], i32),
+        "gx_outbox_pack": ([vp, vp, C.c_uint64], i32), "gx_inbox_unpack": ([vp, vp, C.c_uint64], i32),
+        "gx_round_merge": ([vp], i32), "gx_ae_bytes": ([vp, vp], i32),
+        "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64], i32),
+        "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -232,6 +240,10 @@ class Engine:
         self.params = params
         self.H = params.n_hosts
         self.S = params.n_services
+        self.G = max(1, params.n_shards)
+        gid = params.shard_id if self.G > 1 else 0
+        self.lo = (gid * self.H) // self.G
+        self.hi = ((gid + 1) * self.H) // self.G
         h = C.c_void_p()
         check(self.lib.gx_create(C.byref(params), C.byref(h)), "gx_create")
         self.h = h
@@ -355,8 +367,9 @@ class Engine:
         check(self.lib.gx_notify_leave(self.h, view, node))
 
     # read-back -------------------------------------------------------------------------
-    def read_views(self, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
-        hi = self.H if hi is None else hi
+    def read_views(self, lo: Optional[int] = None, hi: Optional[int] = None) -> np.ndarray:
+        lo = self.lo if lo is None else lo
+        hi = self.hi if hi is None else hi
         out = np.empty((hi - lo, self.H * self.S), dtype=np.uint64)
         check(self.lib.gx_read_views(self.h, lo, hi, out.ctypes.data_as(C.c_void_p)), "gx_read_views")
         return out
@@ -377,8 +390,9 @@ class Engine:
             return None
         return (w >> TS_SHIFT, w & 7)
 
-    def hosts(self, lo=0, hi=None):
-        hi = self.H if hi is None else hi
+    def hosts(self, lo=None, hi=None):
+        lo = self.lo if lo is None else lo
+        hi = self.hi if hi is None else hi
         out = (GxHostState * max(1, hi - lo))()
         check(self.lib.gx_read_hosts(self.h, lo, hi, out))
         return [out[i] for i in range(hi - lo)]
@@ -410,7 +424,7 @@ class Engine:
         return [out[i] for i in range(min(n.value, 1024))]
 
     def digests(self) -> np.ndarray:
-        out = np.empty(self.H, dtype=np.uint64)
+        out = np.empty(self.hi - self.lo, dtype=np.uint64)
         check(self.lib.gx_host_digests(self.h, out.ctypes.data_as(C.c_void_p)), "gx_host_digests")
         return out
 
@@ -423,6 +437,41 @@ class Engine:
         t = GxTiming()
         check(self.lib.gx_timing_get(self.h, C.byref(t)))
         return t.as_dict()
+
+    # sharded rounds (phase API; buffers are addresses: device memory for the HIP engine) -----
+    def round_send(self):
+        check(self.lib.gx_round_send(self.h), "gx_round_send")
+
+    def outbox_bytes(self) -> np.ndarray:
+        out = np.zeros(self.G, dtype=np.uint64)
+        check(self.lib.gx_outbox_bytes(self.h, out.ctypes.data_as(C.c_void_p)), "gx_outbox_bytes")
+        return out
+
+    def outbox_pack(self, ptr: int, cap: int):
+        check(self.lib.gx_outbox_pack(self.h, C.c_void_p(ptr), cap), "gx_outbox_pack")
+
+    def inbox_unpack(self, ptr: int, nbytes: int):
+        check(self.lib.gx_inbox_unpack(self.h, C.c_void_p(ptr), nbytes), "gx_inbox_unpack")
+
+    def round_merge(self):
+        check(self.lib.gx_round_merge(self.h), "gx_round_merge")
+
+    def ae_bytes(self) -> np.ndarray:
+        out = np.zeros(self.G, dtype=np.uint64)
+        check(self.lib.gx_ae_bytes(self.h, out.ctypes.data_as(C.c_void_p)), "gx_ae_bytes")
+        return out
+
+    def ae_pack(self, ptr: int, cap: int):
+        check(self.lib.gx_ae_pack(self.h, C.c_void_p(ptr), cap), "gx_ae_pack")
+
+    def ae_merge(self, ptr: int, nbytes: int):
+        check(self.lib.gx_ae_merge(self.h, C.c_void_p(ptr), nbytes), "gx_ae_merge")
+
+    def round_end(self):
+        check(self.lib.gx_round_end(self.h), "gx_round_end")
+
+    def view_minmax(self, ptr_min: int, ptr_max: int):
+        check(self.lib.gx_view_minmax(self.h, C.c_void_p(ptr_min), C.c_void_p(ptr_max)), "gx_view_minmax")
 
     def converged(self):
         c = C.c_int()

@@ -51,6 +51,9 @@ enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS =
 struct Dev {
   gx_params p;
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  uint32_t lo, Hl, G, gid;  // this engine owns hosts [lo, lo + Hl); per-host arrays are local
+  uint32_t n_remote;        // packets received from other shards this round
+  uint32_t *msg_key;        // [H*K] global sender * K + j of each packet entry
   int64_t round, now;
   int partitioned;
   uint64_t *view;
@@ -170,23 +173,28 @@ GXD void acc_flush(const Dev &d, const Acc &a) {
   if ((threadIdx.x & 63) == 0 && any) mark_change(d);
 }
 
+// Local index of an owned host (global id v in [lo, lo + Hl)).
+GXD uint32_t li(const Dev &d, uint32_t v) { return v - d.lo; }
+GXD uint64_t *vrow(const Dev &d, uint32_t v) { return &d.view[(size_t)li(d, v) * d.R]; }
+GXD gx_host_state *hst(const Dev &d, uint32_t v) { return &d.hs[li(d, v)]; }
+
 GXD void set_slot(const Dev &d, Acc &a, uint32_t v, uint64_t *slot, uint64_t nw) {
   if (*slot != nw) {
     *slot = nw;
     a.changed = true;
-    atomicMin(&d.minexp[v], exp_time(d.p, nw));
+    atomicMin(&d.minexp[li(d, v)], exp_time(d.p, nw));
   }
 }
 
 // ----------------------------------------------------------------------- broadcast FIFO --
 GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
-  if ((j.meta & 0xff) == GX_JOB_SEND) d.hs[v].arena_used &= ~(1u << (j.c & 0xffff));
+  if ((j.meta & 0xff) == GX_JOB_SEND) hst(d, v)->arena_used &= ~(1u << (j.c & 0xffff));
 }
 
 // The unbuffered Broadcasts channel's blocked senders (services_state.go:94) as a FIFO bounded
 // at Q jobs, 2 reserved for the loopers' nil sends.
 GXD bool push_job(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
-  gx_host_state *h = &d.hs[v];
+  gx_host_state *h = hst(d, v);
   uint32_t count = h->fifo_tail - h->fifo_head;
   bool nil = (j.meta & 0xff) <= GX_JOB_NIL_BT;
   uint32_t limit = nil ? d.Q : d.Q - 2;
@@ -195,27 +203,27 @@ GXD bool push_job(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
     free_list(d, v, j);
     return false;
   }
-  d.fifo[(size_t)v * d.Q + (h->fifo_tail % d.Q)] = j;
+  d.fifo[(size_t)li(d, v) * d.Q + (h->fifo_tail % d.Q)] = j;
   h->fifo_tail++;
   return true;
 }
 
 GXD void push_sleep(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
-  gx_host_state *h = &d.hs[v];
+  gx_host_state *h = hst(d, v);
   if (h->sleep_tail - h->sleep_head >= d.SQ) {
     a.c[C_SDROP]++;
     free_list(d, v, j);
     return;
   }
-  d.sleep[(size_t)v * d.SQ + (h->sleep_tail % d.SQ)] = j;
+  d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_tail % d.SQ)] = j;
   h->sleep_tail++;
 }
 
 // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO tail.
 GXD void wake_host(const Dev &d, Acc &a, uint32_t v) {
-  gx_host_state *h = &d.hs[v];
+  gx_host_state *h = hst(d, v);
   while (h->sleep_head != h->sleep_tail) {
-    gx_job j = d.sleep[(size_t)v * d.SQ + (h->sleep_head % d.SQ)];
+    gx_job j = d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_head % d.SQ)];
     if ((int64_t)j.wake > d.round) break;
     h->sleep_head++;
     push_job(d, a, v, j);
@@ -235,22 +243,22 @@ GXD gx_job make_job(uint64_t a, uint64_t b, uint32_t c, uint32_t meta) {
 
 // Lowest free list slot, or -1 (list_drops).
 GXD int alloc_list(const Dev &d, Acc &a, uint32_t v) {
-  uint32_t used = d.hs[v].arena_used;
+  uint32_t used = hst(d, v)->arena_used;
   uint32_t free_bits = ~used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1));
   if (!free_bits) {
     a.c[C_LDROP]++;
     return -1;
   }
   int slot = __builtin_ctz(free_bits);
-  d.hs[v].arena_used = used | (1u << slot);
+  hst(d, v)->arena_used = used | (1u << slot);
   return slot;
 }
 GXD grec *list_ptr(const Dev &d, uint32_t v, uint32_t slot) {
-  return &d.arena[((size_t)v * d.A + slot) * d.L];
+  return &d.arena[((size_t)li(d, v) * d.A + slot) * d.L];
 }
 // SendServices job over an allocated, filled list (services_state.go:579-604).
 GXD void commit_send(const Dev &d, Acc &a, uint32_t v, int slot, uint32_t n, uint32_t npasses) {
-  d.arena_len[(size_t)v * d.A + slot] = n;
+  d.arena_len[(size_t)li(d, v) * d.A + slot] = n;
   a.c[C_SENDJOBS]++;
   push_job(d, a, v, make_job(0, 0, (uint32_t)slot | (n << 16), meta_of(GX_JOB_SEND, 0, npasses)));
 }
@@ -288,12 +296,12 @@ GXD grec job_rec(const Dev &d, uint32_t v, const gx_job &j, uint32_t i, uint32_t
 
 // GetBroadcasts(overhead, limit) + packPacket (services_delegate.go:85-144, :186-223).
 GXD uint32_t get_broadcasts(const Dev &d, Acc &a, uint32_t v, uint32_t limit, grec *packet) {
-  gx_host_state *h = &d.hs[v];
+  gx_host_state *h = hst(d, v);
   uint32_t m = 0;
   uint32_t mask = d.DQ - 1;
-  grec *dq = &d.dq[(size_t)v * d.DQ];
+  grec *dq = &d.dq[(size_t)li(d, v) * d.DQ];
   if (h->fifo_head != h->fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
-    gx_job j = d.fifo[(size_t)v * d.Q + (h->fifo_head % d.Q)];
+    gx_job j = d.fifo[(size_t)li(d, v) * d.Q + (h->fifo_head % d.Q)];
     h->fifo_head++;
     a.c[C_DEQ]++;
     m = job_len(d, j);
@@ -370,7 +378,7 @@ GXD uint64_t merge_word(const Dev &d, uint64_t old, uint64_t u, bool &acc, bool 
 
 GXD bool add_entry(const Dev &d, Acc &a, uint32_t v, grec u, int src) {
   a.c[src == SRC_GOSSIP ? C_GOSSIP_MERGES : src == SRC_AE ? C_AE_MERGES : C_LOCAL_MERGES]++;
-  uint64_t *slot = &d.view[(size_t)v * d.R + u.r];
+  uint64_t *slot = &vrow(d, v)[u.r];
   bool acc, stale;
   uint64_t nw = merge_word(d, *slot, u.w, acc, stale);
   if (stale) {
@@ -411,7 +419,7 @@ GXD uint64_t expiry_word(const Dev &d, uint64_t w, bool &expired, bool &gc) {
 // TombstoneServices(self, list) on the owner's own slots (services_state.go:685-715).
 // Returns the mask of services tombstoned (each contributes the record twice).
 GXD uint64_t tombstone_services(const Dev &d, Acc &a, uint32_t o, uint64_t running) {
-  uint64_t *row = &d.view[(size_t)o * d.R + (size_t)o * d.S];
+  uint64_t *row = &vrow(d, o)[(size_t)o * d.S];
   uint64_t m = 0;
   for (uint32_t s = 0; s < d.S; s++) {
     uint64_t w = row[s];
@@ -425,7 +433,7 @@ GXD uint64_t tombstone_services(const Dev &d, Acc &a, uint32_t o, uint64_t runni
 
 // ExpireServer (services_state.go:150-192) for one (viewer, owner).
 GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
-  uint64_t *row = &d.view[(size_t)v * d.R + (size_t)o * d.S];
+  uint64_t *row = &vrow(d, v)[(size_t)o * d.S];
   uint64_t mask = 0;
   bool live = false;
   for (uint32_t s = 0; s < d.S; s++) {
@@ -443,14 +451,14 @@ GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
 }
 
 GXD bool is_new(const Dev &d, uint32_t o, uint64_t sw, uint32_t r) {
-  uint64_t w = d.view[(size_t)o * d.R + r];
+  uint64_t w = vrow(d, o)[r];
   return st_of(w) == GX_ABSENT || (st_of(sw) != GX_TOMBSTONE && st_of(sw) != st_of(w));
 }
 
 // BroadcastServices looper body (services_state.go:525-574) over fn() = list (n <= 64).
 // Sets inc = bit i for each list element handed to SendServices (0 = a nil was sent).
 GXD void bs_body_list(const Dev &d, Acc &a, uint32_t o, const grec *list, uint32_t n, uint64_t &inc_out) {
-  gx_host_state *h = &d.hs[o];
+  gx_host_state *h = hst(d, o);
   bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > h->last_bcast_ns;  // (:547)
   bool any_new = false;
   uint64_t inc = 0;
@@ -482,7 +490,7 @@ GXD void bs_body_list(const Dev &d, Acc &a, uint32_t o, const grec *list, uint32
 // Second half of the BroadcastTombstones body (services_state.go:613-629), after the view scan
 // left the first L expired records (key order) in `others`.
 GXD void bt_finish(const Dev &d, Acc &a, uint32_t o, uint64_t running, const grec *others, uint32_t n_others) {
-  gx_host_state *h = &d.hs[o];
+  gx_host_state *h = hst(d, o);
   uint64_t own = tombstone_services(d, a, o, running);
   uint32_t n_own = 2u * (uint32_t)__popcll(own);
   if (n_own + n_others > 0) {

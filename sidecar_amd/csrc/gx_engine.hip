@@ -59,6 +59,14 @@ struct gx_engine {
   double ms[GX_K_COUNT];
   uint64_t launches[GX_K_COUNT];
   grec *own_list;
+  // sharded rounds: outbox entry list and push-pull plan (device), rebuilt per round
+  uint32_t *ob_entries;
+  uint32_t n_ob;
+  uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t;
+  int32_t *ae_prow;
+  uint8_t *ae_pcount;
+  uint32_t n_plan, n_pack;
+  int ae_planned_round;
   // small device scratch for single-host ABI calls
   void *api_dev;
   size_t api_dev_bytes;
@@ -78,6 +86,7 @@ static int ensure_api(gx_engine *e, size_t bytes) {
   return GX_OK;
 }
 
+static bool own(const gx_engine *e, uint32_t v) { return v >= e->d.lo && v < e->d.lo + e->d.Hl; }
 static int64_t now_of(const gx_engine *e) { return e->d.p.t0_ns + e->d.round * e->d.p.round_ns; }
 static void set_round_fields(gx_engine *e) {
   e->d.now = now_of(e);
@@ -126,41 +135,69 @@ static int sync_check(gx_engine *e) {
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-static int run_one_round(gx_engine *e) {
+// Phases 0-3 (wake, owners, expiry scan, storm, GetBroadcasts) for this engine's hosts.
+static int round_send_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
+  d.n_remote = 0;
   hipStream_t s = e->stream;
   bool vec = (d.R % 2) == 0;
   {
     LaunchTimer t(e, GX_K_OWNER);
-    k_owner<<<nblk(d.H, 256), 256, 0, s>>>(d, e->own_list);
+    k_owner<<<nblk(d.Hl, 256), 256, 0, s>>>(d, e->own_list);
   }
   {
     LaunchTimer t(e, GX_K_SCAN);
-    if (vec) k_scan<true><<<d.H, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
-    else k_scan<false><<<d.H, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
-    k_bt_finish<<<nblk(d.H, 256), 256, 0, s>>>(d);
+    if (vec) k_scan<true><<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
+    else k_scan<false><<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
+    k_bt_finish<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   }
   if (d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2) {
     LaunchTimer t(e, GX_K_STORM);
-    k_storm<<<d.H, 256, 0, s>>>(d);
+    k_storm<<<d.Hl, 256, 0, s>>>(d);
   }
   {
     LaunchTimer t(e, GX_K_SEND);
-    k_send<<<nblk(d.H, 256), 256, 0, s>>>(d);
+    k_send<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   }
-  size_t ne = (size_t)d.H * d.K;
-  if (ne) {
+  HIPCHK(hipGetLastError());
+  return GX_OK;
+}
+
+// Phase 4: receiver CSR over local + received packets, then gather-then-merge.
+static int round_merge_impl(gx_engine *e) {
+  Dev &d = e->d;
+  set_round_fields(e);
+  hipStream_t s = e->stream;
+  size_t ne = (size_t)d.Hl * d.K + d.n_remote;
+  if (d.K) {
     {
       LaunchTimer t(e, GX_K_ROUTE);
       k_route_offsets<<<1, 1024, 0, s>>>(d);
-      k_route_fill<<<nblk(ne, 256), 256, 0, s>>>(d);
-      k_route_rank<<<nblk(ne, 256), 256, 0, s>>>(d);
+      if (ne) {
+        k_route_fill<<<nblk(ne, 256), 256, 0, s>>>(d);
+        k_route_rank<<<nblk(ne, 256), 256, 0, s>>>(d);
+      }
     }
     LaunchTimer t(e, GX_K_MERGE);
-    k_merge<<<d.H, 64, 0, s>>>(d);
+    k_merge<<<d.Hl, 64, 0, s>>>(d);
   }
-  if (d.p.ae_period_rounds && (uint64_t)d.round % d.p.ae_period_rounds == d.p.ae_phase) {
+  HIPCHK(hipGetLastError());
+  return GX_OK;
+}
+
+static bool ae_round(const gx_engine *e) {
+  const Dev &d = e->d;
+  return d.p.ae_period_rounds && (uint64_t)d.round % d.p.ae_period_rounds == d.p.ae_phase;
+}
+
+// Phase 5 on an unsharded engine: pairs derived on device.
+static int ae_whole_impl(gx_engine *e) {
+  Dev &d = e->d;
+  set_round_fields(e);
+  hipStream_t s = e->stream;
+  bool vec = (d.R % 2) == 0;
+  if (ae_round(e)) {
     uint32_t np;
     uint64_t key0, key1 = 0;
     if (d.partitioned) {
@@ -179,13 +216,20 @@ static int run_one_round(gx_engine *e) {
     }
   }
   HIPCHK(hipGetLastError());
-  d.round++;
   return GX_OK;
+}
+
+static int run_one_round(gx_engine *e) {
+  int rc = round_send_impl(e);
+  if (!rc) rc = round_merge_impl(e);
+  if (!rc) rc = ae_whole_impl(e);
+  if (!rc) e->d.round++;
+  return rc;
 }
 
 static int wake_all(gx_engine *e) {
   set_round_fields(e);
-  k_wake<<<nblk(e->d.H, 256), 256, 0, e->stream>>>(e->d);
+  k_wake<<<nblk(e->d.Hl, 256), 256, 0, e->stream>>>(e->d);
   HIPCHK(hipGetLastError());
   return GX_OK;
 }
@@ -237,6 +281,7 @@ static int check_params(const gx_params *p) {
   if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
   if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
+  if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   return GX_OK;
 }
 
@@ -249,7 +294,8 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
+  void *ptrs[] = {d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
+                  e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
                   d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
   for (void *p : ptrs)
@@ -287,6 +333,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->conv_bad = nullptr;
   e->digest_buf = nullptr;
   e->stream = nullptr;
+  e->ob_entries = nullptr;
+  e->n_ob = 0;
+  e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = nullptr;
+  e->ae_prow = nullptr;
+  e->ae_pcount = nullptr;
+  e->n_plan = e->n_pack = 0;
+  e->ae_planned_round = -1;
   Dev &d = e->d;
   d.p = *p;
   d.H = p->n_hosts;
@@ -296,6 +349,11 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.A = p->list_slots;
   d.L = p->packet_cap + p->pending_cap;
   d.K = p->fanout;
+  d.G = p->n_shards > 1 ? p->n_shards : 1;
+  d.gid = d.G > 1 ? p->shard_id : 0;
+  d.lo = (uint32_t)(((uint64_t)d.gid * d.H) / d.G);
+  d.Hl = (uint32_t)(((uint64_t)(d.gid + 1) * d.H) / d.G) - d.lo;
+  d.n_remote = 0;
   d.SQ = pow2_at_least(64 > d.K * (p->retransmit_rounds + 1) ? 64 : d.K * (p->retransmit_rounds + 1));
   d.DQ = pow2_at_least(d.L + p->pending_cap + 64);
   d.round = 0;
@@ -303,7 +361,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
     delete e;
     return GX_EIO;
   }
-  size_t H = d.H, K = d.K ? d.K : 1;
+  // per-host arrays hold this shard's Hl hosts; the message table also takes the packets received
+  // from other shards (at most (H - Hl) * K), so it is sized H * K.
+  size_t Hg = d.H, H = d.Hl, K = d.K ? d.K : 1;
   ALLOC(d.view, sizeof(uint64_t) * H * d.R);
   ALLOC(d.own_status, H * d.S);
   ALLOC(d.hs, sizeof(gx_host_state) * H);
@@ -312,15 +372,16 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.dq, sizeof(grec) * H * d.DQ);
   ALLOC(d.arena, sizeof(grec) * H * d.A * d.L);
   ALLOC(d.arena_len, sizeof(uint32_t) * H * d.A);
-  ALLOC(d.msg, sizeof(grec) * H * K * p->packet_cap);
-  ALLOC(d.msg_len, sizeof(uint32_t) * H * K);
-  ALLOC(d.msg_dst, sizeof(uint32_t) * H * K);
+  ALLOC(d.msg, sizeof(grec) * Hg * K * p->packet_cap);
+  ALLOC(d.msg_len, sizeof(uint32_t) * Hg * K);
+  ALLOC(d.msg_dst, sizeof(uint32_t) * Hg * K);
+  ALLOC(d.msg_key, sizeof(uint32_t) * Hg * K);
   size_t in_pad = ((H + 1 + 16383) / 16384) * 16384 + 16;  // k_route_offsets reads 16-count rows
   ALLOC(d.in_cnt, sizeof(uint32_t) * in_pad);
   ALLOC(d.minexp, sizeof(unsigned long long) * H);
   ALLOC(d.in_cur, sizeof(uint32_t) * H);
-  ALLOC(d.in_fill, sizeof(uint32_t) * H * K);
-  ALLOC(d.in_sorted, sizeof(uint32_t) * H * K);
+  ALLOC(d.in_fill, sizeof(uint32_t) * Hg * K);
+  ALLOC(d.in_sorted, sizeof(uint32_t) * Hg * K);
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
   ALLOC(d.tick, H);
@@ -328,19 +389,29 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(e->own_list, sizeof(grec) * H * d.S);
   ALLOC(e->conv_bad, sizeof(unsigned long long));
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
+  if (d.G > 1) {
+    ALLOC(e->ob_entries, sizeof(uint32_t) * H * K);
+    size_t np = Hg / 2 + 1;
+    ALLOC(e->ae_pa, sizeof(uint32_t) * np);
+    ALLOC(e->ae_pb, sizeof(uint32_t) * np);
+    ALLOC(e->ae_prow, sizeof(int32_t) * np);
+    ALLOC(e->ae_pcount, np);
+    ALLOC(e->ae_pack_host, sizeof(uint32_t) * np);
+    ALLOC(e->ae_pack_t, sizeof(uint32_t) * np);
+  }
   hipStream_t s = e->stream;
   uint64_t *rec_word = nullptr;
   ALLOC(rec_word, sizeof(uint64_t) * d.R);
   HIPCHK(hipMemsetAsync(d.ctr, 0, sizeof(DevCtr), s));
   HIPCHK(hipMemsetAsync(d.arena_len, 0, sizeof(uint32_t) * H * d.A, s));
-  HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * H * K, s));
+  HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * Hg * K, s));
   HIPCHK(hipMemsetAsync(d.in_cnt, 0, sizeof(uint32_t) * in_pad, s));
   HIPCHK(hipMemsetAsync(d.tick, 0, H, s));
   set_round_fields(e);
   k_init_rec<<<nblk(d.R, 256), 256, 0, s>>>(d, rec_word);
   k_init_views<<<2048, 256, 0, s>>>(d, rec_word);
-  k_init_hosts<<<nblk(d.H, 256), 256, 0, s>>>(d);
-  k_minexp_recompute<<<d.H, 256, 0, s>>>(d, 0);
+  k_init_hosts<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
+  k_minexp_recompute<<<d.Hl, 256, 0, s>>>(d, 0);
   rc = sync_check(e);
   (void)hipFree(rec_word);
   if (rc) {
@@ -372,7 +443,7 @@ int gx_enable_timing(gx_engine *e, int on) {
 }
 
 int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
-  if (!e) return GX_EINVAL;
+  if (!e || e->d.G > 1) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   for (uint32_t i = 0; i < n_rounds; i++) {
     int rc = run_one_round(e);
@@ -422,7 +493,7 @@ static int api_add(gx_engine *e, const uint32_t *views, uint32_t fixed_view, con
   HIPCHK(hipSetDevice(e->device));
   if (views)
     for (uint32_t i = 0; i < n; i++)
-      if (views[i] >= e->d.H) return GX_EINVAL;
+      if (!own(e, views[i])) return GX_EINVAL;
   size_t vbytes = ((sizeof(uint32_t) * (n + 1)) + 255) & ~(size_t)255;
   grec *drec;
   int rc = stage_recs(e, svcs, n, vbytes + 256, &drec);
@@ -447,17 +518,17 @@ int gx_add_service_entries(gx_engine *e, const uint32_t *views, const gx_service
 }
 
 int gx_notify_msg(gx_engine *e, uint32_t host, const gx_service *recs, uint32_t n) {
-  if (!e || host >= e->d.H || (n && !recs)) return GX_EINVAL;
+  if (!e || !own(e, host) || (n && !recs)) return GX_EINVAL;
   return api_add(e, nullptr, host, recs, n, SRC_GOSSIP, nullptr);
 }
 
 int gx_merge_remote_state(gx_engine *e, uint32_t view, const gx_service *svcs, uint32_t n) {
-  if (!e || view >= e->d.H || (n && !svcs)) return GX_EINVAL;
+  if (!e || !own(e, view) || (n && !svcs)) return GX_EINVAL;
   return api_add(e, nullptr, view, svcs, n, SRC_AE, nullptr);
 }
 
 int gx_merge(gx_engine *e, uint32_t dst, uint32_t src) {
-  if (!e || dst >= e->d.H || src >= e->d.H) return GX_EINVAL;
+  if (!e || !own(e, dst) || !own(e, src)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   set_round_fields(e);
   if (e->d.R % 2 == 0) k_merge_views<true><<<1, 256, 0, e->stream>>>(e->d, dst, src);
@@ -466,7 +537,7 @@ int gx_merge(gx_engine *e, uint32_t dst, uint32_t src) {
 }
 
 int gx_tombstone_others(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out) {
-  if (!e || view >= e->d.H || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, view) || (cap && !out)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   int rc = ensure_api(e, 256 + sizeof(grec) * (cap + 1));
   if (rc) return rc;
@@ -491,7 +562,7 @@ int gx_tombstone_others(gx_engine *e, uint32_t view, gx_service *out, uint32_t c
 
 int gx_tombstone_services(gx_engine *e, uint32_t host, const uint16_t *running, uint32_t n_running, gx_service *out,
                           uint32_t cap, uint32_t *n_out) {
-  if (!e || host >= e->d.H || (n_running && !running) || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, host) || (n_running && !running) || (cap && !out)) return GX_EINVAL;
   uint64_t mask = 0;
   for (uint32_t i = 0; i < n_running; i++) {
     if (running[i] >= e->d.S) return GX_EINVAL;
@@ -524,7 +595,7 @@ int gx_tombstone_services(gx_engine *e, uint32_t host, const uint16_t *running, 
 }
 
 int gx_expire_server(gx_engine *e, uint32_t view, uint32_t owner, int *expired) {
-  if (!e || view >= e->d.H || owner >= e->d.H) return GX_EINVAL;
+  if (!e || !own(e, view) || owner >= e->d.H) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   int rc = ensure_api(e, 64);
   if (rc) return rc;
@@ -541,7 +612,7 @@ int gx_expire_server(gx_engine *e, uint32_t view, uint32_t owner, int *expired) 
 int gx_notify_leave(gx_engine *e, uint32_t view, uint32_t node) { return gx_expire_server(e, view, node, nullptr); }
 
 int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32_t n, uint32_t n_passes) {
-  if (!e || host >= e->d.H || (n && !svcs) || n_passes < 1 || n_passes > 255) return GX_EINVAL;
+  if (!e || !own(e, host) || (n && !svcs) || n_passes < 1 || n_passes > 255) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   grec *drec;
   int rc = stage_recs(e, svcs, n, 0, &drec);
@@ -552,7 +623,7 @@ int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32
 }
 
 int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n) {
-  if (!e || host >= e->d.H || (n && !list) || n > 64) return GX_EINVAL;
+  if (!e || !own(e, host) || (n && !list) || n > 64) return GX_EINVAL;
   for (uint32_t i = 0; i < n; i++)
     if (list[i].host != host) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
@@ -565,7 +636,7 @@ int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, u
 }
 
 int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n) {
-  if (!e || host >= e->d.H || (n && !list)) return GX_EINVAL;
+  if (!e || !own(e, host) || (n && !list)) return GX_EINVAL;
   uint64_t mask = 0;
   for (uint32_t i = 0; i < n; i++) {
     if (list[i].host != host || list[i].svc >= e->d.S) return GX_EINVAL;
@@ -585,7 +656,7 @@ int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list,
 
 int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *out) {
   grec g;
-  if (!e || !svc || !out || view >= e->d.H || to_grec(e, svc, &g)) return GX_EINVAL;
+  if (!e || !svc || !out || !own(e, view) || to_grec(e, svc, &g)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   int rc = ensure_api(e, 64);
   if (rc) return rc;
@@ -600,7 +671,7 @@ int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *o
 
 int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *out, uint32_t cap, uint32_t *n_out) {
   if (limit == GX_LIMIT_DEFAULT) limit = e ? e->d.p.packet_cap : 0;
-  if (!e || host >= e->d.H || !n_out || limit > 256 || cap < limit || (limit && !out)) return GX_EINVAL;
+  if (!e || !own(e, host) || !n_out || limit > 256 || cap < limit || (limit && !out)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   int rc = ensure_api(e, 256 + sizeof(grec) * 257);
   if (rc) return rc;
@@ -622,10 +693,12 @@ int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *o
 }
 
 int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out) {
-  if (!e || view >= e->d.H || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, view) || (cap && !out)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
   std::vector<uint64_t> row(e->d.R);
-  HIPCHK(hipMemcpy(row.data(), &e->d.view[(size_t)view * e->d.R], sizeof(uint64_t) * e->d.R, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(row.data(), &e->d.view[(size_t)(view - e->d.lo) * e->d.R], sizeof(uint64_t) * e->d.R,
+                   hipMemcpyDeviceToHost));
   uint32_t n = 0;
   for (uint32_t r = 0; r < e->d.R; r++) {
     if (st_of(row[r]) == GX_ABSENT) continue;
@@ -642,31 +715,31 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
 }
 
 int gx_read_views(gx_engine *e, uint32_t lo, uint32_t hi, uint64_t *out) {
-  if (!e || lo > hi || hi > e->d.H || (hi > lo && !out)) return GX_EINVAL;
+  if (!e || lo > hi || lo < e->d.lo || hi > e->d.lo + e->d.Hl || (hi > lo && !out)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->stream));
   if (hi > lo)
-    HIPCHK(hipMemcpy(out, &e->d.view[(size_t)lo * e->d.R], sizeof(uint64_t) * (size_t)(hi - lo) * e->d.R,
+    HIPCHK(hipMemcpy(out, &e->d.view[(size_t)(lo - e->d.lo) * e->d.R], sizeof(uint64_t) * (size_t)(hi - lo) * e->d.R,
                      hipMemcpyDeviceToHost));
   return GX_OK;
 }
 
 int gx_write_views(gx_engine *e, uint32_t lo, uint32_t hi, const uint64_t *in) {
-  if (!e || lo > hi || hi > e->d.H || (hi > lo && !in)) return GX_EINVAL;
+  if (!e || lo > hi || lo < e->d.lo || hi > e->d.lo + e->d.Hl || (hi > lo && !in)) return GX_EINVAL;
   size_t n = (size_t)(hi - lo) * e->d.R;
   for (size_t i = 0; i < n; i++)
     if (st_of(in[i]) == 7 && in[i] != GX_SLOT_ABSENT) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->stream));
-  if (n) HIPCHK(hipMemcpy(&e->d.view[(size_t)lo * e->d.R], in, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
+  if (n) HIPCHK(hipMemcpy(&e->d.view[(size_t)(lo - e->d.lo) * e->d.R], in, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
   set_round_fields(e);
   k_api_mark<<<1, 64, 0, e->stream>>>(e->d);
-  if (hi > lo) k_minexp_recompute<<<hi - lo, 256, 0, e->stream>>>(e->d, lo);
+  if (hi > lo) k_minexp_recompute<<<hi - lo, 256, 0, e->stream>>>(e->d, lo - e->d.lo);
   return sync_check(e);
 }
 
 int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc) {
-  if (!e || !svc || view >= e->d.H) return GX_EINVAL;
+  if (!e || !svc || !own(e, view)) return GX_EINVAL;
   uint64_t w;
   uint32_t r;
   if (svc->status == GX_ABSENT) {
@@ -686,10 +759,10 @@ int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc) {
 }
 
 int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out) {
-  if (!e || lo > hi || hi > e->d.H || (hi > lo && !out)) return GX_EINVAL;
+  if (!e || lo > hi || lo < e->d.lo || hi > e->d.lo + e->d.Hl || (hi > lo && !out)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->stream));
-  if (hi > lo) HIPCHK(hipMemcpy(out, &e->d.hs[lo], sizeof(gx_host_state) * (hi - lo), hipMemcpyDeviceToHost));
+  if (hi > lo) HIPCHK(hipMemcpy(out, &e->d.hs[lo - e->d.lo], sizeof(gx_host_state) * (hi - lo), hipMemcpyDeviceToHost));
   return GX_OK;
 }
 
@@ -707,53 +780,53 @@ static int read_ring(gx_engine *e, const gx_job *base, uint32_t ring, uint32_t h
 }
 
 int gx_read_queue(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
-  if (!e || host >= e->d.H || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, host) || (cap && !out)) return GX_EINVAL;
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
   if (rc) return rc;
   uint32_t n = h.fifo_tail - h.fifo_head;
-  rc = read_ring(e, &e->d.fifo[(size_t)host * e->d.Q], e->d.Q, h.fifo_head % e->d.Q, n, out, cap);
+  rc = read_ring(e, &e->d.fifo[(size_t)(host - e->d.lo) * e->d.Q], e->d.Q, h.fifo_head % e->d.Q, n, out, cap);
   if (rc) return rc;
   if (n_out) *n_out = n;
   return GX_OK;
 }
 
 int gx_read_sleepers(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
-  if (!e || host >= e->d.H || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, host) || (cap && !out)) return GX_EINVAL;
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
   if (rc) return rc;
   uint32_t n = h.sleep_tail - h.sleep_head;
-  rc = read_ring(e, &e->d.sleep[(size_t)host * e->d.SQ], e->d.SQ, h.sleep_head % e->d.SQ, n, out, cap);
+  rc = read_ring(e, &e->d.sleep[(size_t)(host - e->d.lo) * e->d.SQ], e->d.SQ, h.sleep_head % e->d.SQ, n, out, cap);
   if (rc) return rc;
   if (n_out) *n_out = n;
   return GX_OK;
 }
 
 int gx_read_pending(gx_engine *e, uint32_t host, gx_service *out, uint32_t cap, uint32_t *n_out) {
-  if (!e || host >= e->d.H || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, host) || (cap && !out)) return GX_EINVAL;
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
   if (rc) return rc;
   std::vector<grec> dq(e->d.DQ);
-  HIPCHK(hipMemcpy(dq.data(), &e->d.dq[(size_t)host * e->d.DQ], sizeof(grec) * e->d.DQ, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(dq.data(), &e->d.dq[(size_t)(host - e->d.lo) * e->d.DQ], sizeof(grec) * e->d.DQ, hipMemcpyDeviceToHost));
   for (uint32_t i = 0; i < h.dq_len && i < cap; i++) to_svc(e, &dq[(h.dq_head + i) & (e->d.DQ - 1)], &out[i]);
   if (n_out) *n_out = h.dq_len;
   return GX_OK;
 }
 
 int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, uint32_t cap, uint32_t *n_out) {
-  if (!e || host >= e->d.H || slot >= e->d.A || (cap && !out)) return GX_EINVAL;
+  if (!e || !own(e, host) || slot >= e->d.A || (cap && !out)) return GX_EINVAL;
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
   if (rc) return rc;
   uint32_t n = 0;
   if ((h.arena_used >> slot) & 1u)
-    HIPCHK(hipMemcpy(&n, &e->d.arena_len[(size_t)host * e->d.A + slot], sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&n, &e->d.arena_len[(size_t)(host - e->d.lo) * e->d.A + slot], sizeof(uint32_t), hipMemcpyDeviceToHost));
   uint32_t m = n < cap ? n : cap;
   if (m) {
     std::vector<grec> tmp(m);
-    HIPCHK(hipMemcpy(tmp.data(), &e->d.arena[((size_t)host * e->d.A + slot) * e->d.L], sizeof(grec) * m,
+    HIPCHK(hipMemcpy(tmp.data(), &e->d.arena[((size_t)(host - e->d.lo) * e->d.A + slot) * e->d.L], sizeof(grec) * m,
                      hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < m; i++) to_svc(e, &tmp[i], &out[i]);
   }
@@ -764,8 +837,210 @@ int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, ui
 int gx_host_digests(gx_engine *e, uint64_t *out) {
   if (!e || !out) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  k_digest<<<nblk(e->d.H, 256), 256, 0, e->stream>>>(e->d, e->digest_buf);
-  HIPCHK(hipMemcpyAsync(out, e->digest_buf, sizeof(uint64_t) * e->d.H, hipMemcpyDeviceToHost, e->stream));
+  k_digest<<<nblk(e->d.Hl, 256), 256, 0, e->stream>>>(e->d, e->digest_buf);
+  HIPCHK(hipMemcpyAsync(out, e->digest_buf, sizeof(uint64_t) * e->d.Hl, hipMemcpyDeviceToHost, e->stream));
+  return sync_check(e);
+}
+
+// ------------------------------------------------------------------------- sharded rounds --
+static uint32_t shard_of(const Dev &d, uint32_t v) {
+  uint32_t g = 0;
+  while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= v) g++;
+  return g;
+}
+static size_t slot_bytes(const Dev &d) { return 16 + 16ull * d.p.packet_cap; }
+static size_t row_bytes(const Dev &d) { return 16 + 8ull * d.R; }
+
+int gx_round_send(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = round_send_impl(e);
+  return rc ? rc : sync_check(e);
+}
+
+// Entries of this shard's packets bound for other shards, grouped by destination shard in key
+// order; sizes in bytes per shard.
+int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
+  if (!e || !bytes) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  Dev &d = e->d;
+  for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
+  e->n_ob = 0;
+  if (d.G < 2 || !d.K) return GX_OK;
+  size_t ne = (size_t)d.Hl * d.K;
+  std::vector<uint32_t> len(ne), dst(ne);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(len.data(), d.msg_len, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(dst.data(), d.msg_dst, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
+  std::vector<std::vector<uint32_t>> per(d.G);
+  for (size_t i = 0; i < ne; i++)
+    if (len[i] && !own(e, dst[i])) per[shard_of(d, dst[i])].push_back((uint32_t)i);
+  std::vector<uint32_t> order;
+  for (uint32_t g = 0; g < d.G; g++) {
+    bytes[g] = per[g].size() * slot_bytes(d);
+    order.insert(order.end(), per[g].begin(), per[g].end());
+  }
+  e->n_ob = (uint32_t)order.size();
+  if (e->n_ob) HIPCHK(hipMemcpy(e->ob_entries, order.data(), sizeof(uint32_t) * e->n_ob, hipMemcpyHostToDevice));
+  return GX_OK;
+}
+
+int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (!e->n_ob) return GX_OK;
+  if (cap < e->n_ob * slot_bytes(e->d)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  k_outbox_pack<<<e->n_ob, 64, 0, e->stream>>>(e->d, e->ob_entries, e->n_ob, (uint8_t *)buf);
+  return sync_check(e);
+}
+
+int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
+  if (!e || (bytes && !buf) || bytes % slot_bytes(e->d)) return GX_EINVAL;
+  uint64_t n = bytes / slot_bytes(e->d);
+  if (n > (uint64_t)(e->d.H - e->d.Hl) * e->d.K) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  if (n) k_inbox_unpack<<<(unsigned)n, 64, 0, e->stream>>>(e->d, (const uint8_t *)buf, (uint32_t)n);
+  e->d.n_remote = (uint32_t)n;
+  return sync_check(e);
+}
+
+int gx_round_merge(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = round_merge_impl(e);
+  return rc ? rc : sync_check(e);
+}
+
+// Push-pull plan of this round (host side): global pairs t -> (a, b); local pairs, rows to send
+// (grouped by destination shard, ascending t) and rows to receive (by source shard, ascending t).
+static int ae_plan(gx_engine *e, uint64_t *bytes) {
+  Dev &d = e->d;
+  set_round_fields(e);
+  std::vector<uint32_t> pa, pb;
+  uint32_t groups[2][2];
+  int ng;
+  if (d.partitioned) {
+    groups[0][0] = 0; groups[0][1] = d.H / 2;
+    groups[1][0] = d.H / 2; groups[1][1] = d.H - d.H / 2;
+    ng = 2;
+  } else {
+    groups[0][0] = 0; groups[0][1] = d.H;
+    ng = 1;
+  }
+  for (int gi = 0; gi < ng; gi++) {
+    uint32_t base = groups[gi][0], m = groups[gi][1];
+    uint64_t key = rng4(d.p.seed, ST_AE, (uint64_t)d.round, base, 0);
+    for (uint32_t t = 0; t + 1 < m; t += 2) {
+      pa.push_back(base + feistel_perm(key, t, m));
+      pb.push_back(base + feistel_perm(key, t + 1, m));
+    }
+  }
+  std::vector<uint32_t> plan_a, plan_b, pack_host, pack_t;
+  std::vector<int32_t> plan_row;
+  std::vector<uint8_t> plan_cnt;
+  for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
+  for (uint32_t g = 0; g < d.G; g++) {  // rows to send to shard g (ascending t)
+    if (g == d.gid) continue;
+    for (size_t t = 0; t < pa.size(); t++) {
+      bool la = own(e, pa[t]), lb = own(e, pb[t]);
+      if (la == lb) continue;
+      uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
+      if (shard_of(d, other) != g) continue;
+      pack_host.push_back(mine);
+      pack_t.push_back((uint32_t)t);
+      bytes[g] += row_bytes(d);
+    }
+  }
+  int32_t row = 0;
+  for (uint32_t g = 0; g < d.G; g++) {  // rows received from shard g, same order on both sides
+    if (g == d.gid) continue;
+    for (size_t t = 0; t < pa.size(); t++) {
+      bool la = own(e, pa[t]), lb = own(e, pb[t]);
+      if (la == lb) continue;
+      uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
+      if (shard_of(d, other) != g) continue;
+      plan_a.push_back(mine);
+      plan_b.push_back(other);
+      plan_row.push_back(row++);
+      plan_cnt.push_back(la ? 1 : 0);
+    }
+  }
+  for (size_t t = 0; t < pa.size(); t++)
+    if (own(e, pa[t]) && own(e, pb[t])) {
+      plan_a.push_back(pa[t]);
+      plan_b.push_back(pb[t]);
+      plan_row.push_back(-1);
+      plan_cnt.push_back(0);
+    }
+  e->n_plan = (uint32_t)plan_a.size();
+  e->n_pack = (uint32_t)pack_host.size();
+  if (e->n_plan) {
+    HIPCHK(hipMemcpy(e->ae_pa, plan_a.data(), 4 * e->n_plan, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ae_pb, plan_b.data(), 4 * e->n_plan, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ae_prow, plan_row.data(), 4 * e->n_plan, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ae_pcount, plan_cnt.data(), e->n_plan, hipMemcpyHostToDevice));
+  }
+  if (e->n_pack) {
+    HIPCHK(hipMemcpy(e->ae_pack_host, pack_host.data(), 4 * e->n_pack, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ae_pack_t, pack_t.data(), 4 * e->n_pack, hipMemcpyHostToDevice));
+  }
+  e->ae_planned_round = (int)d.round;
+  return GX_OK;
+}
+
+int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
+  if (!e || !bytes) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  for (uint32_t g = 0; g < e->d.G; g++) bytes[g] = 0;
+  e->n_plan = e->n_pack = 0;
+  e->ae_planned_round = -1;
+  if (e->d.G < 2 || !ae_round(e)) return GX_OK;
+  return ae_plan(e, bytes);
+}
+
+int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (!e->n_pack) return GX_OK;
+  if (e->ae_planned_round != (int)e->d.round || cap < e->n_pack * row_bytes(e->d)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  k_ae_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, (uint8_t *)buf);
+  return sync_check(e);
+}
+
+int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
+  if (!e || (bytes && !buf)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  if (!ae_round(e)) return GX_OK;
+  if (e->d.G < 2) {
+    int rc = ae_whole_impl(e);
+    return rc ? rc : sync_check(e);
+  }
+  if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
+  if (e->n_plan) {
+    set_round_fields(e);
+    LaunchTimer t(e, GX_K_AE);
+    if (e->d.R % 2 == 0)
+      k_ae_plan<true><<<e->n_plan, 256, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_pcount,
+                                                          (const uint8_t *)buf);
+    else
+      k_ae_plan<false><<<e->n_plan, 256, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_pcount,
+                                                           (const uint8_t *)buf);
+  }
+  return sync_check(e);
+}
+
+int gx_round_end(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  e->d.round++;
+  int rc = wake_all(e);
+  return rc ? rc : sync_check(e);
+}
+
+int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
+  if (!e || !mn || !mx) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  k_view_minmax<<<nblk(e->d.R, 256), 256, 0, e->stream>>>(e->d, mn, mx);
   return sync_check(e);
 }
 
@@ -846,7 +1121,7 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
 }
 
 int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
-  if (!e) return GX_EINVAL;
+  if (!e || e->d.G > 1) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipMemsetAsync(e->conv_bad, 0, sizeof(unsigned long long), e->stream));
   {

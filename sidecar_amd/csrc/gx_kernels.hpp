@@ -64,9 +64,9 @@ __global__ void k_init_rec(Dev d, uint64_t *rec_word) {
 }
 
 __global__ void k_init_views(Dev d, const uint64_t *rec_word) {
-  size_t total = (size_t)d.H * d.R;
+  size_t total = (size_t)d.Hl * d.R;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    uint32_t v = (uint32_t)(i / d.R), r = (uint32_t)(i % d.R);
+    uint32_t v = d.lo + (uint32_t)(i / d.R), r = (uint32_t)(i % d.R);
     uint64_t w = GX_SLOT_ABSENT;
     if (d.p.init_mode == GX_INIT_WARM || (d.p.init_mode == GX_INIT_OWN && r / d.S == v)) w = rec_word[r];
     d.view[i] = w;
@@ -74,22 +74,23 @@ __global__ void k_init_views(Dev d, const uint64_t *rec_word) {
 }
 
 __global__ void k_init_hosts(Dev d) {
-  uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= d.H) return;
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= d.Hl) return;
+  uint32_t o = d.lo + idx;
   const gx_params &p = d.p;
   gx_host_state h = {};
   h.bs_next = (int64_t)(rng4(p.seed, ST_PHASE_BS, o, 0, 0) % p.alive_interval_rounds);
   h.bt_next = (int64_t)(rng4(p.seed, ST_PHASE_BT, o, 0, 0) % p.tombstone_interval_rounds);
   h.last_bcast_ns = p.init_mode == GX_INIT_WARM ? p.t0_ns : 0;
   h.running = d.S == 64 ? ~0ull : ((1ull << d.S) - 1);
-  d.hs[o] = h;
-  for (uint32_t s = 0; s < d.S; s++) d.own_status[(size_t)o * d.S + s] = GX_ALIVE;
+  d.hs[idx] = h;
+  for (uint32_t s = 0; s < d.S; s++) d.own_status[(size_t)idx * d.S + s] = GX_ALIVE;
 }
 
 // Exact per-view expiry bound (one block per view): used at create and after raw imports.
-__global__ __launch_bounds__(256) void k_minexp_recompute(Dev d, uint32_t lo) {
+__global__ __launch_bounds__(256) void k_minexp_recompute(Dev d, uint32_t lo_idx) {
   __shared__ unsigned long long s_red[4];
-  uint32_t v = lo + blockIdx.x;
+  uint32_t v = lo_idx + blockIdx.x;  // local index
   const uint64_t *row = &d.view[(size_t)v * d.R];
   unsigned long long m = ~0ull;
   for (uint32_t r = threadIdx.x; r < d.R; r += blockDim.x) {
@@ -102,8 +103,8 @@ __global__ __launch_bounds__(256) void k_minexp_recompute(Dev d, uint32_t lo) {
 
 __global__ void k_wake(Dev d) {
   Acc a;
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v < d.H) wake_host(d, a, v);
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < d.Hl) wake_host(d, a, d.lo + idx);
   acc_flush(d, a);
 }
 
@@ -112,29 +113,30 @@ __global__ void k_wake(Dev d) {
 // TrackNewServices, and flag the BroadcastTombstones tick. Also clears this round's CSR counts.
 __global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
   Acc a;
-  uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o < d.H) {
-    d.in_cnt[o] = 0;
-    d.in_cur[o] = 0;
-    if (o == 0) d.in_cnt[d.H] = 0;
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < d.Hl) {
+    uint32_t o = d.lo + idx;
+    d.in_cnt[idx] = 0;
+    d.in_cur[idx] = 0;
+    if (idx == 0) d.in_cnt[d.Hl] = 0;
     wake_host(d, a, o);
-    gx_host_state *h = &d.hs[o];
+    gx_host_state *h = &d.hs[idx];
     if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
       uint64_t x = rng4(d.p.seed, ST_CHURN, (uint64_t)d.round, o, 0);
       if ((uint32_t)(x & 0xffffffffu) % 1000000u < d.p.churn_ppm) {
         uint32_t s = (uint32_t)((x >> 32) % d.S);
         h->running ^= 1ull << s;
-        if ((h->running >> s) & 1ull) d.own_status[(size_t)o * d.S + s] = GX_ALIVE;
+        if ((h->running >> s) & 1ull) d.own_status[(size_t)idx * d.S + s] = GX_ALIVE;
         a.c[C_CHURN]++;
       }
     }
     if (!(h->flags & 1u) && h->bs_next <= d.round) {
-      grec *list = &own_list[(size_t)o * d.S];  // fn(): running services, restamped now
+      grec *list = &own_list[(size_t)idx * d.S];  // fn(): running services, restamped now
       uint32_t n = 0;
       uint64_t run = h->running;
       for (uint32_t s = 0; s < d.S; s++)
         if ((run >> s) & 1ull) {
-          list[n].w = pack(d.now, d.own_status[(size_t)o * d.S + s]);
+          list[n].w = pack(d.now, d.own_status[(size_t)idx * d.S + s]);
           list[n].r = o * d.S + s;
           list[n].pad = 0;
           n++;
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
           if ((inc >> i) & 1ull) add_entry(d, a, o, list[i], SRC_LOCAL);  // TrackNewServices
       }
     }
-    d.tick[o] = (!(h->flags & 2u) && h->bt_next <= d.round) ? 1 : 0;
+    d.tick[idx] = (!(h->flags & 2u) && h->bt_next <= d.round) ? 1 : 0;
   }
   acc_flush(d, a);
 }
@@ -162,19 +164,19 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
                                                uint32_t *cnt_out, int only_host) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
-  uint32_t o = only_host >= 0 ? (uint32_t)only_host : blockIdx.x;
+  uint32_t oi = only_host >= 0 ? li(d, (uint32_t)only_host) : blockIdx.x;  // local index
   if (only_host < 0) {
-    if (!d.tick[o]) return;
-    if (d.minexp[o] >= (unsigned long long)d.now) {  // nothing can expire in this view
+    if (!d.tick[oi]) return;
+    if (d.minexp[oi] >= (unsigned long long)d.now) {  // nothing can expire in this view
       if (threadIdx.x == 0) {
-        cnt_out[o] = 0;
+        cnt_out[oi] = 0;
         ctr_atomic(d, C_SCANSLOTS, d.R);
       }
       return;
     }
   }
-  uint64_t *row = &d.view[(size_t)o * d.R];
-  grec *list = &list_base[only_host >= 0 ? 0 : (size_t)o * list_stride];
+  uint64_t *row = &d.view[(size_t)oi * d.R];
+  grec *list = &list_base[only_host >= 0 ? 0 : (size_t)oi * list_stride];
   uint32_t n_exp = 0;
   unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, mexp = ~0ull;
   uint32_t t = threadIdx.x;
@@ -240,8 +242,8 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   }
   mexp = block_min(mexp, s_red);
   if (threadIdx.x == 0) {
-    cnt_out[only_host >= 0 ? 0 : o] = n_exp;
-    d.minexp[o] = mexp;  // exact bound after the scan
+    cnt_out[only_host >= 0 ? 0 : oi] = n_exp;
+    d.minexp[oi] = mexp;  // exact bound after the scan
   }
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && (threadIdx.x & 63) == 0) mark_change(d);
@@ -256,10 +258,10 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
 
 __global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
   Acc a;
-  uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o < d.H && d.tick[o]) {
-    uint32_t n = d.scan_cnt[o];
-    bt_finish(d, a, o, d.hs[o].running, &d.scan_list[(size_t)o * d.L], n < d.L ? n : d.L);
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < d.Hl && d.tick[idx]) {
+    uint32_t n = d.scan_cnt[idx];
+    bt_finish(d, a, d.lo + idx, d.hs[idx].running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
   }
   acc_flush(d, a);
 }
@@ -274,10 +276,10 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   __shared__ unsigned long long s_mask[STORM_TILE];
   __shared__ uint32_t s_live[STORM_TILE];
   __shared__ unsigned long long s_wave[4];
-  uint32_t v = blockIdx.x;
+  uint32_t vi = blockIdx.x, v = d.lo + vi;
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
-  gx_host_state *h = &d.hs[v];
+  gx_host_state *h = &d.hs[vi];
   uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
   uint32_t jobs = 0;
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
       s_live[i] = 0;
     }
     __syncthreads();
-    uint64_t *base = &d.view[(size_t)v * d.R + (size_t)ob * d.S];
+    uint64_t *base = &d.view[(size_t)vi * d.R + (size_t)ob * d.S];
     uint64_t w[STORM_TILE / 256];
 #pragma unroll
     for (int q = 0; q < STORM_TILE / 256; q++) {
@@ -319,7 +321,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
       unsigned long long tot;
       uint32_t pos = (uint32_t)block_excl_scan64(live ? 1ull : 0ull, s_wave, tot);
       if (live && jobs + pos < room)
-        d.fifo[(size_t)v * d.Q + ((tail0 + jobs + pos) % d.Q)] =
+        d.fifo[(size_t)vi * d.Q + ((tail0 + jobs + pos) % d.Q)] =
             make_job((uint64_t)d.now, s_mask[i], ob + i, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
       jobs += (uint32_t)tot;
     }
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && (t & 63) == 0) {
     mark_change(d);
-    atomicMin(&d.minexp[v], exp_time(d.p, tomb));
+    atomicMin(&d.minexp[vi], exp_time(d.p, tomb));
   }
   c_wr = wave_sum(c_wr);
   if ((t & 63) == 0) kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
@@ -372,17 +374,21 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 // into its receiver's CSR bucket.
 __global__ __launch_bounds__(256) void k_send(Dev d) {
   Acc a;
-  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < d.H) {
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < d.Hl) {
+    uint32_t u = d.lo + idx;
     uint32_t peers[16];
     uint32_t np = sample_peers(d, u, peers);
     uint32_t cap = d.p.packet_cap;
-    for (uint32_t j = 0; j < d.K; j++) d.msg_len[(size_t)u * d.K + j] = 0;
+    for (uint32_t j = 0; j < d.K; j++) {
+      d.msg_len[(size_t)idx * d.K + j] = 0;
+      d.msg_key[(size_t)idx * d.K + j] = u * d.K + j;
+    }
     for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts(d, a, u, cap, &d.msg[((size_t)u * d.K + j) * cap]);
-      d.msg_len[(size_t)u * d.K + j] = l;
-      d.msg_dst[(size_t)u * d.K + j] = peers[j];
-      if (l) atomicAdd(&d.in_cnt[peers[j]], 1u);
+      uint32_t l = get_broadcasts(d, a, u, cap, &d.msg[((size_t)idx * d.K + j) * cap]);
+      d.msg_len[(size_t)idx * d.K + j] = l;
+      d.msg_dst[(size_t)idx * d.K + j] = peers[j];
+      if (l && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
       if (l == 0 && d.p.gossip_stop_on_empty) break;
     }
   }
@@ -397,16 +403,16 @@ __global__ __launch_bounds__(1024) void k_route_offsets(Dev d) {
   __shared__ unsigned long long s_wave[16];
   uint32_t t = threadIdx.x;
   uint32_t carry = 0;
-  for (uint32_t base = 0; base < d.H; base += 1024 * ROUTE_ITEMS) {
+  for (uint32_t base = 0; base < d.Hl; base += 1024 * ROUTE_ITEMS) {
     uint32_t i0 = base + t * ROUTE_ITEMS;
     uint32_t v[ROUTE_ITEMS];
 #pragma unroll
     for (int q = 0; q < ROUTE_ITEMS / 4; q++) {
       uint4 x = *reinterpret_cast<const uint4 *>(&d.in_cnt[i0 + 4 * q]);
-      v[4 * q] = i0 + 4 * q < d.H ? x.x : 0;
-      v[4 * q + 1] = i0 + 4 * q + 1 < d.H ? x.y : 0;
-      v[4 * q + 2] = i0 + 4 * q + 2 < d.H ? x.z : 0;
-      v[4 * q + 3] = i0 + 4 * q + 3 < d.H ? x.w : 0;
+      v[4 * q] = i0 + 4 * q < d.Hl ? x.x : 0;
+      v[4 * q + 1] = i0 + 4 * q + 1 < d.Hl ? x.y : 0;
+      v[4 * q + 2] = i0 + 4 * q + 2 < d.Hl ? x.z : 0;
+      v[4 * q + 3] = i0 + 4 * q + 3 < d.Hl ? x.w : 0;
     }
     uint32_t sum = 0;
 #pragma unroll
@@ -421,30 +427,34 @@ __global__ __launch_bounds__(1024) void k_route_offsets(Dev d) {
     }
 #pragma unroll
     for (int q = 0; q < ROUTE_ITEMS / 4; q++)
-      if (i0 + 4 * q < d.H) *reinterpret_cast<uint4 *>(&d.in_cnt[i0 + 4 * q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      if (i0 + 4 * q < d.Hl) *reinterpret_cast<uint4 *>(&d.in_cnt[i0 + 4 * q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     carry += (uint32_t)tot;
   }
   __syncthreads();
-  if (t == 0) d.in_cnt[d.H] = carry;
+  if (t == 0) d.in_cnt[d.Hl] = carry;
 }
 
+// Entries: [0, Hl*K) packets of this shard's senders, then n_remote packets from other shards.
 __global__ void k_route_fill(Dev d) {
   uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.H * d.K || d.msg_len[e] == 0) return;
-  uint32_t dst = d.msg_dst[e];
+  if (e >= d.Hl * d.K + d.n_remote || d.msg_len[e] == 0) return;
+  uint32_t dst = d.msg_dst[e] - d.lo;
+  if (dst >= d.Hl) return;  // bound for another shard (outbox)
   uint32_t pos = atomicAdd(&d.in_cur[dst], 1u);
   d.in_fill[d.in_cnt[dst] + pos] = e;
 }
 
 // Deterministic order: rank of each entry (= sender * K + j) inside its receiver segment.
+// Deterministic order: rank of each entry's global key (sender * K + j) inside its receiver segment.
 __global__ void k_route_rank(Dev d) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.in_cnt[d.H]) return;
+  if (i >= d.in_cnt[d.Hl]) return;
   uint32_t e = d.in_fill[i];
-  uint32_t dst = d.msg_dst[e];
+  uint32_t key = d.msg_key[e];
+  uint32_t dst = d.msg_dst[e] - d.lo;
   uint32_t lo = d.in_cnt[dst], hi = d.in_cnt[dst + 1];
   uint32_t rank = 0;
-  for (uint32_t x = lo; x < hi; x++) rank += d.in_fill[x] < e;
+  for (uint32_t x = lo; x < hi; x++) rank += d.msg_key[d.in_fill[x]] < key;
   d.in_sorted[lo + rank] = e;
 }
 
@@ -461,17 +471,17 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   __shared__ uint8_t s_accf[MERGE_TILE];
   __shared__ uint32_t s_start[65];
   __shared__ uint32_t s_ent[64];
-  uint32_t v = blockIdx.x;
+  uint32_t vi = blockIdx.x, v = d.lo + vi;
   uint32_t lane = threadIdx.x;
-  uint32_t off = d.in_cnt[v], deg = d.in_cnt[v + 1] - off;
+  uint32_t off = d.in_cnt[vi], deg = d.in_cnt[vi + 1] - off;
   if (deg == 0) return;
   uint32_t cap = d.p.packet_cap;
-  gx_host_state *h = &d.hs[v];
+  gx_host_state *h = &d.hs[vi];
   uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
   uint32_t n_retx = 0;
   unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, mexp = ~0ull;
-  uint64_t *row = &d.view[(size_t)v * d.R];
+  uint64_t *row = &d.view[(size_t)vi * d.R];
   for (uint32_t c0 = 0; c0 < deg; c0 += 64) {
     uint32_t cn = deg - c0 < 64 ? deg - c0 : 64;
     uint32_t ent = 0, len = 0;
@@ -542,7 +552,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
         unsigned long long m = __ballot(f);
         uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         if (f && n_retx + pos < room)
-          d.fifo[(size_t)v * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
+          d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
               make_job(s_acc[i], 0, s_key[i], meta_of(GX_JOB_RETX, 0, 1));
         n_retx += (uint32_t)__popcll(m);
       }
@@ -567,7 +577,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
     ctr_atomic(d, C_QDROP, n_retx - ok);
     if (c_wr) {
       mark_change(d);
-      atomicMin(&d.minexp[v], mexp);
+      atomicMin(&d.minexp[vi], mexp);
     }
   }
 }
@@ -577,11 +587,13 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
 // rows with 16-B loads, 4 slots per thread per 1024-slot tile, and compacts each side's
 // retransmits in key order with one packed block scan per tile.
 template <bool VEC>
+// `ext` (when both = false): B is another shard's received row of host b (read-only); the pair's
+// exchange is counted where a is the pair's first member (count_ex).
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
-                 unsigned long long *s_red) {
-  uint64_t *A = &d.view[(size_t)a * d.R];
-  uint64_t *B = &d.view[(size_t)b * d.R];
-  gx_host_state *ha = &d.hs[a], *hb = &d.hs[b];
+                 unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false) {
+  uint64_t *A = vrow(d, a);
+  uint64_t *B = ext ? const_cast<uint64_t *>(ext) : vrow(d, b);
+  gx_host_state *ha = hst(d, a), *hb = both ? hst(d, b) : ha;
   uint32_t ta0 = ha->fifo_tail, ca0 = ta0 - ha->fifo_head;
   uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
   uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
@@ -678,9 +690,9 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       if (fa[k] && pa[k] < rooma)
-        d.fifo[(size_t)a * d.Q + ((ta0 + pa[k]) % d.Q)] = make_job(nwa[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+        d.fifo[(size_t)li(d, a) * d.Q + ((ta0 + pa[k]) % d.Q)] = make_job(nwa[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
       if (fb[k] && pb[k] < roomb)
-        d.fifo[(size_t)b * d.Q + ((tb0 + pb[k]) % d.Q)] = make_job(nwb[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+        d.fifo[(size_t)li(d, b) * d.Q + ((tb0 + pb[k]) % d.Q)] = make_job(nwb[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
     }
     na += fld(tot, 0) + fld(tot, 1);
     nb += fld(tot, 2) + fld(tot, 3);
@@ -695,8 +707,8 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   block_ctr(d, C_AE_ACC, c_acc, s_red);
   block_ctr(d, C_STALE, c_stale, s_red);
   if (t == 0) {
-    if (ma != ~0ull) atomicMin(&d.minexp[a], ma);
-    if (mb != ~0ull) atomicMin(&d.minexp[b], mb);
+    if (ma != ~0ull) atomicMin(&d.minexp[li(d, a)], ma);
+    if (both && mb != ~0ull) atomicMin(&d.minexp[li(d, b)], mb);
     uint32_t oka = na < rooma ? na : rooma, okb = nb < roomb ? nb : roomb;
     ha->fifo_tail = ta0 + oka;
     if (both) hb->fifo_tail = tb0 + okb;
@@ -704,7 +716,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     ctr_atomic(d, C_QDROP, (na - oka) + (both ? nb - okb : 0));
     ctr_atomic(d, C_AESLOTS, (unsigned long long)d.R * (both ? 2 : 1));
     kbytes(d, GX_K_AE, 16ull * d.R + 32ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
-    if (both) ctr_atomic(d, C_AEX, 1);
+    if (both || count_ex) ctr_atomic(d, C_AEX, 1);
   }
 }
 
@@ -737,13 +749,107 @@ __global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32
   ae_pair<VEC>(d, dst, src, false, s_wave, s_red);
 }
 
+// Sharded push-pull: plan entry i = (a, b, row): row < 0 -> both members here (a <-> b);
+// row >= 0 -> a is here and b's row is rows_in[row] (16-B header + R words): a <- b only.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_ae_plan(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
+                                                  const uint8_t *pcount, const uint8_t *rows_in) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  uint32_t i = blockIdx.x;
+  if (prow[i] < 0) {
+    ae_pair<VEC>(d, pa[i], pb[i], true, s_wave, s_red);
+  } else {
+    const uint64_t *row = reinterpret_cast<const uint64_t *>(rows_in + (size_t)prow[i] * (16 + 8ull * d.R) + 16);
+    ae_pair<VEC>(d, pa[i], pb[i], false, s_wave, s_red, row, pcount[i] != 0);
+  }
+}
+
+// Gather this shard's rows for its cross-shard push-pull partners (16-B header + row).
+__global__ __launch_bounds__(256) void k_ae_pack(Dev d, const uint32_t *host, const uint32_t *pair_t, uint8_t *out) {
+  uint32_t i = blockIdx.x;
+  uint8_t *dst = out + (size_t)i * (16 + 8ull * d.R);
+  if (threadIdx.x == 0) {
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(dst);
+    hdr[0] = pair_t[i];
+    hdr[1] = host[i];
+    hdr[2] = 0;
+    hdr[3] = 0;
+  }
+  const uint64_t *src = vrow(d, host[i]);
+  uint64_t *o = reinterpret_cast<uint64_t *>(dst + 16);
+  for (uint32_t x = threadIdx.x; x < d.R; x += blockDim.x) o[x] = src[x];
+}
+
+// Outbox: fixed-size slots (16-B header + packet_cap records); slot index per local entry.
+__global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t *out) {
+  uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  uint32_t e = entry[i];
+  size_t sb = 16 + 16ull * d.p.packet_cap;
+  uint8_t *dst = out + (size_t)i * sb;
+  uint32_t len = d.msg_len[e];
+  if (threadIdx.x == 0) {
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(dst);
+    hdr[0] = d.msg_key[e];
+    hdr[1] = d.msg_dst[e];
+    hdr[2] = len;
+    hdr[3] = 0;
+  }
+  grec *recs = reinterpret_cast<grec *>(dst + 16);
+  for (uint32_t x = threadIdx.x; x < d.p.packet_cap; x += blockDim.x) {
+    grec g;
+    if (x < len) {
+      g = d.msg[(size_t)e * d.p.packet_cap + x];
+    } else {
+      g.w = 0;
+      g.r = 0;
+      g.pad = 0;
+    }
+    recs[x] = g;
+  }
+}
+
+// Inbox: received slots -> message entries [Hl*K, Hl*K + n) with receiver counts.
+__global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
+  uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  size_t sb = 16 + 16ull * d.p.packet_cap;
+  const uint8_t *src = in + (size_t)i * sb;
+  const uint32_t *hdr = reinterpret_cast<const uint32_t *>(src);
+  uint32_t key = hdr[0], dst = hdr[1], len = hdr[2];
+  size_t e = (size_t)d.Hl * d.K + i;
+  const grec *recs = reinterpret_cast<const grec *>(src + 16);
+  for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) d.msg[e * d.p.packet_cap + x] = recs[x];
+  if (threadIdx.x == 0) {
+    d.msg_key[e] = key;
+    d.msg_dst[e] = dst;
+    d.msg_len[e] = len;
+    if (len) atomicAdd(&d.in_cnt[dst - d.lo], 1u);
+  }
+}
+
+// Per-record min/max slot word over this shard's views, XOR 2^63 (signed-order reducible).
+__global__ void k_view_minmax(Dev d, uint64_t *mn, uint64_t *mx) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= d.R) return;
+  uint64_t a = ~0ull, b = 0;
+  for (uint32_t v = 0; v < d.Hl; v++) {
+    uint64_t w = d.view[(size_t)v * d.R + r];
+    a = w < a ? w : a;
+    b = w > b ? w : b;
+  }
+  mn[r] = a ^ (1ull << 63);
+  mx[r] = b ^ (1ull << 63);
+}
+
 // ================================================================ convergence / digests ==
 __global__ void k_converged(Dev d, unsigned long long *bad) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   bool dis = false;
   if (r < d.R) {
     uint64_t w0 = d.view[r];
-    for (uint32_t v = 1; v < d.H; v++)
+    for (uint32_t v = 1; v < d.Hl; v++)
       if (d.view[(size_t)v * d.R + r] != w0) {
         dis = true;
         break;
@@ -761,8 +867,8 @@ GXD uint64_t feed_job(uint64_t h, const gx_job &j) {
   return feed(h, (uint64_t)j.wake | ((uint64_t)j.aux << 32));
 }
 __global__ void k_digest(Dev d, uint64_t *out) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= d.H) return;
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;  // local index
+  if (v >= d.Hl) return;
   const gx_host_state s = d.hs[v];
   uint64_t h = 0x243F6A8885A308D3ull;
   for (uint32_t i = s.fifo_head; i != s.fifo_tail; i++) h = feed_job(h, d.fifo[(size_t)v * d.Q + (i % d.Q)]);
@@ -856,7 +962,7 @@ __global__ void k_api_is_new(Dev d, uint32_t v, uint64_t w, uint32_t r, uint32_t
 }
 __global__ void k_api_set_slot(Dev d, uint32_t v, uint32_t r, uint64_t w) {
   Acc a;
-  if (threadIdx.x == 0) set_slot(d, a, v, &d.view[(size_t)v * d.R + r], w);
+  if (threadIdx.x == 0) set_slot(d, a, v, &vrow(d, v)[r], w);
   acc_flush(d, a);
 }
 __global__ void k_api_mark(Dev d) {

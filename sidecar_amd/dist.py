@@ -1,0 +1,168 @@
+"""Host sharding across engines: one round = send phase, packet exchange, merge phase,
+push-pull row exchange, end.
+
+Each engine owns the contiguous host block [g*H/G, (g+1)*H/G). The exchange moves the wire
+formats of include/gx.h between shards:
+  * ``DistShard`` — one process per GPU, ``torch.distributed`` all-to-all (RCCL over xGMI for
+    the HIP engine with backend "nccl"; gloo for the CPU oracle in tests);
+  * ``LocalShards`` — every shard in this process (one GPU or the CPU); the exchange is a
+    device-side concatenation. Used to check the sharded kernels against the unsharded engine.
+Exchange buffers are torch uint8 tensors on the engine's device: the HIP engine reads and
+writes them as device memory.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .abi import Engine, GxParams, default_params
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr() if t.numel() else 0
+
+
+class _Shard:
+    def __init__(self, params: GxParams, lib, device: torch.device):
+        self.e = Engine(params, lib=lib)
+        self.device = device
+
+    def sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def pack(self, sizes: np.ndarray, packer) -> torch.Tensor:
+        buf = torch.empty(int(sizes.sum()), dtype=torch.uint8, device=self.device)
+        packer(_ptr(buf), buf.numel())
+        return buf
+
+
+class LocalShards:
+    """G shards of one cluster driven in one process."""
+
+    def __init__(self, lib, G: int, device="cpu", **kw):
+        self.device = torch.device(device)
+        self.G = G
+        self.shards: List[_Shard] = []
+        for g in range(G):
+            p = default_params(lib, **kw)
+            p.n_shards = G
+            p.shard_id = g
+            if self.device.type == "cuda":
+                p.device = self.device.index or 0
+            self.shards.append(_Shard(p, lib, self.device))
+
+    @property
+    def engines(self) -> List[Engine]:
+        return [s.e for s in self.shards]
+
+    def _exchange(self, sizes_fn, pack_fn, unpack_fn):
+        sizes = [sizes_fn(s.e) for s in self.shards]  # sizes[src][dst]
+        bufs = [s.pack(sz, lambda p, n, e=s.e: pack_fn(e, p, n)) for s, sz in zip(self.shards, sizes)]
+        for s in self.shards:
+            s.sync()
+        for dst, s in enumerate(self.shards):
+            parts = []
+            for src in range(self.G):
+                off = int(sizes[src][:dst].sum())
+                parts.append(bufs[src][off:off + int(sizes[src][dst])])
+            inbox = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=self.device)
+            s.sync()
+            unpack_fn(s.e, _ptr(inbox), inbox.numel())
+
+    def run_rounds(self, n: int):
+        for _ in range(n):
+            for s in self.shards:
+                s.e.round_send()
+            self._exchange(lambda e: e.outbox_bytes(), lambda e, p, c: e.outbox_pack(p, c),
+                           lambda e, p, c: e.inbox_unpack(p, c))
+            for s in self.shards:
+                s.e.round_merge()
+            self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
+                           lambda e, p, c: e.ae_merge(p, c))
+            for s in self.shards:
+                s.e.round_end()
+
+    def stats(self) -> dict:
+        tot = {}
+        for s in self.shards:
+            for k, v in s.e.stats().items():
+                tot[k] = max(tot.get(k, v), v) if k in ("round", "last_change_round") else tot.get(k, 0) + v
+        return tot
+
+    def converged(self):
+        R = self.shards[0].e.H * self.shards[0].e.S
+        mn = torch.empty(R, dtype=torch.int64, device=self.device)
+        mx = torch.empty(R, dtype=torch.int64, device=self.device)
+        gmn = gmx = None
+        for s in self.shards:
+            s.e.view_minmax(_ptr(mn), _ptr(mx))
+            gmn = mn.clone() if gmn is None else torch.minimum(gmn, mn)
+            gmx = mx.clone() if gmx is None else torch.maximum(gmx, mx)
+        bad = int((gmn != gmx).sum().item())
+        return bad == 0, bad
+
+
+class DistShard:
+    """This process's shard; the others are peers in torch.distributed's default group."""
+
+    def __init__(self, lib, rank: int, world: int, device, group=None, **kw):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank, self.world = rank, world
+        self.device = torch.device(device)
+        p = default_params(lib, **kw)
+        p.n_shards = world
+        p.shard_id = rank
+        if self.device.type == "cuda":
+            p.device = self.device.index or 0
+        self.s = _Shard(p, lib, self.device)
+        self.e = self.s.e
+
+    def _exchange(self, sizes: np.ndarray, packer, unpacker):
+        dist = self.dist
+        send_sizes = torch.tensor(sizes.astype(np.int64), device=self.device)
+        recv_sizes = torch.empty_like(send_sizes)
+        dist.all_to_all_single(recv_sizes, send_sizes, group=self.group)
+        rs = [int(x) for x in recv_sizes.tolist()]
+        ss = [int(x) for x in sizes.tolist()]
+        send = self.s.pack(sizes, packer)
+        recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
+        if sum(rs) or sum(ss):
+            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+        self.s.sync()
+        unpacker(_ptr(recv), recv.numel())
+
+    def run_rounds(self, n: int):
+        e = self.e
+        for _ in range(n):
+            e.round_send()
+            self._exchange(e.outbox_bytes(), e.outbox_pack, e.inbox_unpack)
+            e.round_merge()
+            self._exchange(e.ae_bytes(), e.ae_pack, e.ae_merge)
+            e.round_end()
+
+    def stats(self) -> dict:
+        st = self.e.stats()
+        keys = sorted(st)
+        t = torch.tensor([st[k] for k in keys], dtype=torch.int64, device=self.device)
+        mx = t.clone()
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
+        out = dict(zip(keys, t.tolist()))
+        for k in ("round", "last_change_round"):
+            out[k] = int(mx[keys.index(k)].item())
+        return out
+
+    def converged(self):
+        R = self.e.H * self.e.S
+        mn = torch.empty(R, dtype=torch.int64, device=self.device)
+        mx = torch.empty(R, dtype=torch.int64, device=self.device)
+        self.e.view_minmax(_ptr(mn), _ptr(mx))
+        self.dist.all_reduce(mn, op=self.dist.ReduceOp.MIN, group=self.group)
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
+        bad = int((mn != mx).sum().item())
+        return bad == 0, bad

@@ -1,0 +1,36 @@
+"""Host sharding on the HIP engine, G shards in one process on one GPU (device-side exchange of
+the same wire formats RCCL moves between GPUs): bit-identical to the unsharded HIP engine and to
+the CPU oracle."""
+import pytest
+
+from sidecar_amd.abi import Engine, default_params
+from sidecar_amd.dist import LocalShards
+from tests.test_shards_cpu import SCEN, assert_sharded_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("G", [2, 3, 5])
+@pytest.mark.parametrize("name", sorted(SCEN))
+def test_gpu_local_shards_match_whole(gx_lib, oracle_lib, name, G):
+    kw = SCEN[name]
+    whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    orc = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    sh = LocalShards(gx_lib, G, device="cuda:0", **kw)
+    for chunk in (1, 6, 13, 40):
+        whole.run_rounds(chunk)
+        orc.run_rounds(chunk)
+        sh.run_rounds(chunk)
+        assert_sharded_equal(whole, sh, f"{name} G={G} round {whole.round}")
+        assert_sharded_equal(orc, sh, f"{name} G={G} round {whole.round} vs oracle")
+
+
+def test_gpu_shards_cfg2_small(gx_lib):
+    kw = dict(n_hosts=1024, n_services=16, init_mode=2, ae_period_rounds=10, partition_start=0,
+              partition_end=20, storm_round=3, queue_cap=2048, churn_ppm=20000)
+    whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    sh = LocalShards(gx_lib, 4, device="cuda:0", **kw)
+    for chunk in (5, 16):
+        whole.run_rounds(chunk)
+        sh.run_rounds(chunk)
+        assert_sharded_equal(whole, sh, f"cfg2-small round {whole.round}")

@@ -1,0 +1,94 @@
+"""Host sharding on the CPU oracle: a cluster split into G shards (exchange layer in
+sidecar_amd/dist.py) must evolve bit-identically to the unsharded cluster — views, per-host
+bookkeeping, queue digests and the summed counters. Also over torch.distributed gloo with two
+processes (the same protocol the GPUs run over RCCL)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from sidecar_amd.abi import Engine, default_params
+from sidecar_amd.dist import LocalShards
+from tests.parity import host_tuples
+
+SCEN = {
+    "storm": dict(n_hosts=48, n_services=8, init_mode=2, ae_period_rounds=10, partition_start=0,
+                  partition_end=30, storm_round=4, queue_cap=2048),
+    "churn_odd": dict(n_hosts=37, n_services=3, init_mode=1, fanout=4, ae_period_rounds=7, ae_phase=2,
+                      churn_ppm=60000, aged_ppm=40000, queue_cap=64, list_slots=3),
+    "empty": dict(n_hosts=40, n_services=6, init_mode=0, ae_period_rounds=9),
+}
+
+
+def assert_sharded_equal(whole: Engine, shards, what):
+    sw = whole.stats()
+    ss = shards.stats()
+    assert sw == ss, {k: (sw[k], ss[k]) for k in sw if sw[k] != ss[k]}
+    views = np.concatenate([e.read_views() for e in shards.engines])
+    assert np.array_equal(views, whole.read_views()), what
+    hosts = sum((host_tuples(e) for e in shards.engines), [])
+    assert hosts == host_tuples(whole), what
+    dig = np.concatenate([e.digests() for e in shards.engines])
+    assert np.array_equal(dig, whole.digests()), what
+    c, n = shards.converged()
+    assert (c, n) == whole.converged(), what
+
+
+@pytest.mark.parametrize("G", [2, 3, 5])
+@pytest.mark.parametrize("name", sorted(SCEN))
+def test_local_shards_match_whole(oracle_lib, name, G):
+    kw = SCEN[name]
+    whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    sh = LocalShards(oracle_lib, G, **kw)
+    for chunk in (1, 6, 13, 40):
+        whole.run_rounds(chunk)
+        sh.run_rounds(chunk)
+        assert_sharded_equal(whole, sh, f"{name} G={G} round {whole.round}")
+
+
+def _worker(rank, world, port, kw, rounds, q):
+    import torch.distributed as dist
+    from sidecar_amd.dist import DistShard
+    from tests.oracle_lib import load_oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = DistShard(load_oracle(), rank, world, "cpu", **kw)
+    sh.run_rounds(rounds)
+    st = sh.stats()
+    conv = sh.converged()
+    q.put((rank, sh.e.read_views(), host_tuples(sh.e), sh.e.digests(), st, conv))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("name", ["storm", "churn_odd"])
+def test_gloo_world2_matches_whole(oracle_lib, name):
+    kw, rounds, world = SCEN[name], 45, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kw, rounds, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    whole.run_rounds(rounds)
+    assert np.array_equal(np.concatenate([r[1] for r in res]), whole.read_views())
+    assert sum((r[2] for r in res), []) == host_tuples(whole)
+    assert np.array_equal(np.concatenate([r[3] for r in res]), whole.digests())
+    assert res[0][4] == whole.stats()
+    assert res[0][5] == whole.converged()
