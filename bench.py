@@ -8,9 +8,10 @@ rounds (ExpireServer storm), the partition heals, and memberlist push-pull anti-
 
   python bench.py [--gpus N --steps K --warmup W] [--config cfg5|cfg2|cfg3|cfg4] [--no-converge]
 
-Prints ONE JSON line (rank 0). N>1 runs one process per GPU (torch.distributed.run); each GPU
-simulates an independent replica cluster with its own seed (DESIGN.md "Multi-GPU"), so the
-per-GPU work is fixed (weak scaling).
+Prints ONE JSON line (rank 0). N>1 runs one process per GPU (torch.distributed.run): the same
+cluster is sharded by host block over the N GPUs and every round's cross-shard
+packets and push-pull rows move by RCCL all-to-all over xGMI, so the total work is fixed
+(strong scaling). Results are bit-identical to the 1-GPU run.
 """
 import argparse
 import json
@@ -65,27 +66,65 @@ def merges(st):
     return st["gossip_merges"] + st["ae_merges"] + st["local_merges"]
 
 
-def run_converge(lib, cfg, seed, device, max_rounds, check_every):
-    """Fresh engine from round 0: chunks of `check_every` rounds, catalog agreement checked
+class Cluster:
+    """The benchmarked cluster: one engine (N=1) or this rank's shard (N>1, sidecar_amd.dist)."""
+
+    def __init__(self, lib, cfg, seed, rank, world, local_rank, barrier):
+        self.world = world
+        self.barrier = barrier
+        if world == 1:
+            self.e = make_engine(lib, cfg, seed, local_rank)
+            self.shard = None
+        else:
+            from sidecar_amd.dist import DistShard
+            kw = dict(CONFIGS[cfg]["p"])
+            kw["seed"] = seed
+            self.shard = DistShard(lib, rank, world, f"cuda:{local_rank}", **kw)
+            self.e = self.shard.e
+
+    @property
+    def round(self):
+        return self.e.round
+
+    def run_rounds(self, n):
+        if self.shard is None:
+            self.e.run_rounds(n)
+        else:
+            self.shard.run_rounds(n)
+
+    def stats(self):
+        return self.e.stats() if self.shard is None else self.shard.stats()
+
+    def converged(self):
+        return self.e.converged() if self.shard is None else self.shard.converged()
+
+    def close(self):
+        self.e.close()
+
+
+def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every):
+    """Fresh cluster from round 0: chunks of `check_every` rounds, catalog agreement checked
     between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run)."""
-    e = make_engine(lib, cfg, seed, device)
+    c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier)
     wall = 0.0
     conv = None
     try:
-        while e.round < max_rounds:
+        while c.round < max_rounds:
+            barrier()
             t0 = time.perf_counter()
-            e.run_rounds(check_every)
+            c.run_rounds(check_every)
+            barrier()
             wall += time.perf_counter() - t0
-            ok, _ = e.converged()
+            ok, _ = c.converged()
             if ok:
-                lc = e.stats()["last_change_round"]
+                lc = c.stats()["last_change_round"]
                 conv = lc + 1  # the catalog stopped changing after round lc and agrees
                 # wall to convergence: the rounds past the convergence point are excluded pro rata
-                wall = wall * conv / e.round if e.round else wall
+                wall = wall * conv / c.round if c.round else wall
                 break
-        return conv, wall, e.round
+        return conv, wall, c.round
     finally:
-        e.close()
+        c.close()
 
 
 def cpu_baseline(cfg, seconds):
@@ -146,31 +185,28 @@ def main():
 
     from sidecar_amd.abi import load_product
     lib = load_product()
-    seed = args.seed + 7919 * rank
-    e = make_engine(lib, args.config, seed, local_rank)
+    seed = args.seed
+    c = Cluster(lib, args.config, seed, rank, world, local_rank, barrier)
+    e = c.e
     e.enable_timing(True)
     if args.warmup:
-        e.run_rounds(args.warmup)
-    st0, tm0 = e.stats(), e.timing()
+        c.run_rounds(args.warmup)
+    st0, tm0 = c.stats(), e.timing()
     barrier()
     t0 = time.perf_counter()
-    e.run_rounds(args.steps)
+    c.run_rounds(args.steps)
     barrier()
     dt = time.perf_counter() - t0
-    st1, tm1 = e.stats(), e.timing()
-    e.close()
+    st1, tm1 = c.stats(), e.timing()
+    c.close()
 
-    local_merges = merges(st1) - merges(st0)
     split = {k: st1[k] - st0[k] for k in ("gossip_merges", "ae_merges", "local_merges")}
+    tot_merges = merges(st1) - merges(st0)  # whole cluster (summed over shards)
     dt_max = dt
-    tot_merges = local_merges
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt_max = float(t.item())
-        m = torch.tensor([local_merges], dtype=torch.float64, device="cuda")
-        dist.all_reduce(m, op=dist.ReduceOp.SUM)
-        tot_merges = int(m.item())
 
     kern = {}
     for i, k in enumerate(KNAMES):
@@ -199,7 +235,8 @@ def main():
 
     conv = None
     if not args.no_converge:
-        r, w, ran = run_converge(lib, args.config, seed, local_rank, args.converge_max, args.check_every)
+        r, w, ran = run_converge(lib, args.config, seed, rank, world, local_rank, barrier, args.converge_max,
+                                 args.check_every)
         conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
                 "rounds_run": ran, "simulated_s": (r * 0.2) if r else None}
     cpu = None
@@ -211,11 +248,13 @@ def main():
         out = {
             "metric": METRIC, "value": tot_merges / dt_max, "unit": "record-merges/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": dt_max * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": dt_max * 1000.0 / args.steps, "higher_is_better": True,
+            "scaling": "strong",
             "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeded gossip schedule)",
             "config": {"workload": f"{args.config}: " + CONFIGS[args.config]["desc"],
                        "hosts": cfgp["n_hosts"], "services": cfgp["n_services"],
-                       "fanout": cfgp.get("fanout", 3), "parallelism": "replicas" if world > 1 else "single"},
+                       "fanout": cfgp.get("fanout", 3),
+                       "parallelism": f"host-sharded over {world} GPUs (RCCL all-to-all)" if world > 1 else "single GPU"},
             "merges": split, "converge": conv, "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
         }
         print(json.dumps(out), flush=True)

@@ -34,3 +34,35 @@ def test_gpu_shards_cfg2_small(gx_lib):
         whole.run_rounds(chunk)
         sh.run_rounds(chunk)
         assert_sharded_equal(whole, sh, f"cfg2-small round {whole.round}")
+
+
+def test_gpu_distshard_rccl_world1(gx_lib):
+    """DistShard over a real RCCL process group (world size 1: every exchange is empty, but the
+    size all-to-all, the stat reductions and the min/max agreement reduction run on RCCL)."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from sidecar_amd.dist import DistShard
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        kw = SCEN["storm"]
+        sh = DistShard(gx_lib, 0, 1, "cuda:0", **kw)
+        whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+        sh.run_rounds(25)
+        whole.run_rounds(25)
+        assert sh.stats() == whole.stats()
+        assert sh.converged() == whole.converged()
+        import numpy as np
+        assert np.array_equal(sh.e.read_views(), whole.read_views())
+    finally:
+        dist.destroy_process_group()
