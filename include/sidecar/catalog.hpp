@@ -1,0 +1,275 @@
+// sidecar/catalog.hpp — C++ host mirror of Sidecar's catalog API over the gx C-ABI (gx.h).
+//
+// Keeps the reference's method set and argument meaning so callers (and the parity tests in
+// tests/cpp/) read like the reference:
+//   catalog.ServicesState  (catalog/services_state.go:70-80)  -> sidecar::catalog::ServicesState
+//   servicesDelegate       (services_delegate.go:20-27)       -> sidecar::ServicesDelegate
+// Hostnames and service IDs are strings here, interned into the engine's (host, svc) indices by
+// a Cluster. Error behaviour follows the reference: the hot path logs-and-continues (drops are
+// counted by the engine, gx_stats); only misuse of this wrapper (an unknown hostname when the
+// host table is full, a C-ABI error) throws std::runtime_error.
+//
+// Header-only; links against either implementation of gx.h (sidecar_amd/libgx.so, or the CPU
+// oracle in tests).
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../gx.h"
+
+namespace sidecar {
+
+// service.Service fields the merge path reads (service/service.go:32-42). Updated is UTC ns.
+enum Status { ALIVE = GX_ALIVE, TOMBSTONE = GX_TOMBSTONE, UNHEALTHY = GX_UNHEALTHY, UNKNOWN = GX_UNKNOWN,
+              DRAINING = GX_DRAINING };
+
+struct Service {
+  std::string ID;
+  std::string Hostname;
+  int64_t Updated = 0;
+  int Status = ALIVE;
+  bool IsTombstone() const { return Status == TOMBSTONE; }
+  bool operator==(const Service &o) const {
+    return ID == o.ID && Hostname == o.Hostname && Updated == o.Updated && Status == o.Status;
+  }
+};
+
+inline void check(int rc, const char *what) {
+  if (rc != GX_OK) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
+}
+
+// One gx engine plus the string <-> index tables. Each host of the cluster has its own
+// ServicesState view (a real Sidecar node has exactly one).
+class Cluster {
+ public:
+  explicit Cluster(gx_params p) : p_(p) { check(gx_create(&p_, &e_), "gx_create"); }
+  static gx_params Defaults(uint32_t hosts, uint32_t services_per_host) {
+    gx_params p;
+    gx_params_default(&p);
+    p.n_hosts = hosts;
+    p.n_services = services_per_host;
+    return p;
+  }
+  ~Cluster() {
+    if (e_) gx_destroy(e_);
+  }
+  Cluster(const Cluster &) = delete;
+  Cluster &operator=(const Cluster &) = delete;
+
+  gx_engine *engine() const { return e_; }
+  const gx_params &params() const { return p_; }
+  int64_t Now() const {
+    int64_t r = 0;
+    gx_get_round(e_, &r);
+    return p_.t0_ns + r * p_.round_ns;
+  }
+  // Let simulated time pass (the reference reads time.Now(); the engine's clock is rounds).
+  void Advance(int64_t rounds) {
+    int64_t r = 0;
+    check(gx_get_round(e_, &r), "gx_get_round");
+    check(gx_set_round(e_, r + rounds), "gx_set_round");
+  }
+  void RunRounds(uint32_t n) { check(gx_run_rounds(e_, n), "gx_run_rounds"); }
+
+  uint32_t Host(const std::string &name) {
+    auto it = hosts_.find(name);
+    if (it != hosts_.end()) return it->second;
+    if (host_names_.size() >= p_.n_hosts) throw std::runtime_error("host table full: " + name);
+    uint32_t id = (uint32_t)host_names_.size();
+    hosts_[name] = id;
+    host_names_.push_back(name);
+    ids_.emplace_back();
+    id_names_.emplace_back();
+    return id;
+  }
+  uint16_t Id(uint32_t host, const std::string &id) {
+    auto &m = ids_[host];
+    auto it = m.find(id);
+    if (it != m.end()) return it->second;
+    if (id_names_[host].size() >= p_.n_services) throw std::runtime_error("service table full: " + id);
+    uint16_t s = (uint16_t)id_names_[host].size();
+    m[id] = s;
+    id_names_[host].push_back(id);
+    return s;
+  }
+  gx_service Rec(const Service &svc) {
+    uint32_t h = Host(svc.Hostname);
+    gx_service r{};
+    r.updated_ns = svc.Updated;
+    r.host = h;
+    r.svc = Id(h, svc.ID);
+    r.status = (uint8_t)svc.Status;
+    return r;
+  }
+  Service Svc(const gx_service &r) const {
+    Service s;
+    s.Hostname = r.host < host_names_.size() ? host_names_[r.host] : "host-" + std::to_string(r.host);
+    s.ID = (r.host < id_names_.size() && r.svc < id_names_[r.host].size()) ? id_names_[r.host][r.svc]
+                                                                             : "svc-" + std::to_string(r.svc);
+    s.Updated = r.updated_ns;
+    s.Status = r.status;
+    return s;
+  }
+  std::vector<Service> Svcs(const std::vector<gx_service> &rs) const {
+    std::vector<Service> out;
+    for (auto &r : rs) out.push_back(Svc(r));
+    return out;
+  }
+
+ private:
+  gx_params p_;
+  gx_engine *e_ = nullptr;
+  std::map<std::string, uint32_t> hosts_;
+  std::vector<std::string> host_names_;
+  std::vector<std::map<std::string, uint16_t>> ids_;
+  std::vector<std::vector<std::string>> id_names_;
+};
+
+namespace catalog {
+
+// catalog.ServicesState of host `Hostname` (catalog/services_state.go:70-80).
+class ServicesState {
+ public:
+  ServicesState(Cluster &c, const std::string &hostname) : c_(c), Hostname(hostname), self_(c.Host(hostname)) {}
+
+  // AddServiceEntry (services_state.go:293-347)
+  void AddServiceEntry(const Service &svc) {
+    gx_service r = c_.Rec(svc);
+    uint32_t v = self_;
+    check(gx_add_service_entries(c_.engine(), &v, &r, 1, nullptr), "AddServiceEntry");
+  }
+  // Merge (services_state.go:367-373)
+  void Merge(const ServicesState &other) { check(gx_merge(c_.engine(), self_, other.self_), "Merge"); }
+  // ExpireServer (services_state.go:150-192)
+  void ExpireServer(const std::string &hostname) {
+    check(gx_expire_server(c_.engine(), self_, c_.Host(hostname), nullptr), "ExpireServer");
+  }
+  // TombstoneOthersServices (services_state.go:635-683)
+  std::vector<Service> TombstoneOthersServices() {
+    std::vector<gx_service> out(4096);
+    uint32_t n = 0;
+    check(gx_tombstone_others(c_.engine(), self_, out.data(), (uint32_t)out.size(), &n), "TombstoneOthersServices");
+    out.resize(n < out.size() ? n : out.size());
+    return c_.Svcs(out);
+  }
+  // TombstoneServices(hostname, containerList) (services_state.go:685-715), hostname == self
+  std::vector<Service> TombstoneServices(const std::vector<Service> &containerList) {
+    std::vector<uint16_t> running;
+    for (auto &s : containerList) running.push_back(c_.Id(self_, s.ID));
+    std::vector<gx_service> out(256);
+    uint32_t n = 0;
+    check(gx_tombstone_services(c_.engine(), self_, running.data(), (uint32_t)running.size(), out.data(),
+                                (uint32_t)out.size(), &n),
+          "TombstoneServices");
+    out.resize(n < out.size() ? n : out.size());
+    return c_.Svcs(out);
+  }
+  // SendServices(services, looper(runCount)) (services_state.go:579-604)
+  void SendServices(const std::vector<Service> &services, int runCount) {
+    std::vector<gx_service> rs;
+    for (auto &s : services) rs.push_back(c_.Rec(s));
+    check(gx_send_services(c_.engine(), self_, rs.data(), (uint32_t)rs.size(), (uint32_t)runCount), "SendServices");
+  }
+  // One BroadcastServices looper body with fn (services_state.go:525-574)
+  void BroadcastServices(const std::function<std::vector<Service>()> &fn) {
+    std::vector<gx_service> rs;
+    for (auto &s : fn()) rs.push_back(c_.Rec(s));
+    check(gx_broadcast_services(c_.engine(), self_, rs.data(), (uint32_t)rs.size()), "BroadcastServices");
+  }
+  // One BroadcastTombstones looper body with fn (services_state.go:606-633)
+  void BroadcastTombstones(const std::function<std::vector<Service>()> &fn) {
+    std::vector<gx_service> rs;
+    for (auto &s : fn()) rs.push_back(c_.Rec(s));
+    check(gx_broadcast_tombstones(c_.engine(), self_, rs.data(), (uint32_t)rs.size()), "BroadcastTombstones");
+  }
+  // IsNewService (services_state.go:509-521)
+  bool IsNewService(const Service &svc) {
+    gx_service r = c_.Rec(svc);
+    int x = 0;
+    check(gx_is_new_service(c_.engine(), self_, &r, &x), "IsNewService");
+    return x != 0;
+  }
+  // state.Servers[hostname].Services[id], or nothing
+  std::optional<Service> Get(const std::string &hostname, const std::string &id) {
+    for (auto &s : EachService())
+      if (s.Hostname == hostname && s.ID == id) return s;
+    return std::nullopt;
+  }
+  bool HasServer(const std::string &hostname) {
+    for (auto &s : EachService())
+      if (s.Hostname == hostname) return true;
+    return false;
+  }
+  // EachService (services_state.go:726-734), key order
+  std::vector<Service> EachService() {
+    uint32_t n = 0;
+    check(gx_local_state(c_.engine(), self_, nullptr, 0, &n), "LocalState");
+    std::vector<gx_service> out(n ? n : 1);
+    check(gx_local_state(c_.engine(), self_, out.data(), n, &n), "LocalState");
+    out.resize(n);
+    return c_.Svcs(out);
+  }
+  // test hook: svc.Updated = ...; svc.Status = ... on the stored record (no merge rule)
+  void Set(const Service &svc) {
+    gx_service r = c_.Rec(svc);
+    check(gx_write_slot(c_.engine(), self_, &r), "write_slot");
+  }
+  uint32_t index() const { return self_; }
+
+ private:
+  Cluster &c_;
+
+ public:
+  const std::string Hostname;
+
+ private:
+  uint32_t self_;
+};
+
+}  // namespace catalog
+
+// servicesDelegate (services_delegate.go:20-27) of one host.
+class ServicesDelegate {
+ public:
+  ServicesDelegate(Cluster &c, catalog::ServicesState &state) : c_(c), state_(state) {}
+  // NotifyMsg: one decoded packet's records (services_delegate.go:72-83, decode loop :46-56)
+  void NotifyMsg(const std::vector<Service> &msg) {
+    std::vector<gx_service> rs;
+    for (auto &s : msg) rs.push_back(c_.Rec(s));
+    check(gx_notify_msg(c_.engine(), state_.index(), rs.data(), (uint32_t)rs.size()), "NotifyMsg");
+  }
+  // GetBroadcasts with a record budget (services_delegate.go:85-144; packPacket :186-223). An
+  // empty result is the reference's nil.
+  std::vector<Service> GetBroadcasts(uint32_t limit_records = GX_LIMIT_DEFAULT) {
+    std::vector<gx_service> out(256);
+    uint32_t n = 0;
+    check(gx_get_broadcasts(c_.engine(), state_.index(), limit_records, out.data(), (uint32_t)out.size(), &n),
+          "GetBroadcasts");
+    out.resize(n);
+    return c_.Svcs(out);
+  }
+  // LocalState (:146-151)
+  std::vector<Service> LocalState(bool /*join*/) { return state_.EachService(); }
+  // MergeRemoteState (:153-167)
+  void MergeRemoteState(const std::vector<Service> &remote, bool /*join*/) {
+    std::vector<gx_service> rs;
+    for (auto &s : remote) rs.push_back(c_.Rec(s));
+    check(gx_merge_remote_state(c_.engine(), state_.index(), rs.data(), (uint32_t)rs.size()), "MergeRemoteState");
+  }
+  // NotifyLeave (:173-176)
+  void NotifyLeave(const std::string &node) {
+    check(gx_notify_leave(c_.engine(), state_.index(), c_.Host(node)), "NotifyLeave");
+  }
+
+ private:
+  Cluster &c_;
+  catalog::ServicesState &state_;
+};
+
+}  // namespace sidecar

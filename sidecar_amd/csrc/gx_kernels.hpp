@@ -600,9 +600,10 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t na = 0, nb = 0;
   unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
-  for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
-    uint64_t wa[4], wb[4], nwa[4], nwb[4];
-    bool fa[4], fb[4];
+  // Software pipeline: the next 1024-slot tile's loads are in flight while this tile is merged,
+  // written back and (only if something was accepted) compacted.
+  uint64_t qa[4], qb[4];
+  auto load_tile = [&](uint32_t base) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
@@ -610,17 +611,28 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       if (VEC && v0) {
         ulonglong2 pa = *reinterpret_cast<const ulonglong2 *>(&A[r0]);
         ulonglong2 pb = *reinterpret_cast<const ulonglong2 *>(&B[r0]);
-        wa[2 * h] = pa.x;
-        wa[2 * h + 1] = pa.y;
-        wb[2 * h] = pb.x;
-        wb[2 * h + 1] = pb.y;
+        qa[2 * h] = pa.x;
+        qa[2 * h + 1] = pa.y;
+        qb[2 * h] = pb.x;
+        qb[2 * h + 1] = pb.y;
       } else {
-        wa[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
-        wa[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
-        wb[2 * h] = v0 ? B[r0] : GX_SLOT_ABSENT;
-        wb[2 * h + 1] = v1 ? B[r0 + 1] : GX_SLOT_ABSENT;
+        qa[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
+        qa[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
+        qb[2 * h] = v0 ? B[r0] : GX_SLOT_ABSENT;
+        qb[2 * h + 1] = v1 ? B[r0 + 1] : GX_SLOT_ABSENT;
       }
     }
+  };
+  load_tile(0);
+  for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
+    uint64_t wa[4], wb[4], nwa[4], nwb[4];
+    bool fa[4], fb[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      wa[k] = qa[k];
+      wb[k] = qb[k];
+    }
+    if (base + 4 * blockDim.x < d.R) load_tile(base + 4 * blockDim.x);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
@@ -675,6 +687,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     unsigned long long cnt = (unsigned long long)(fa[0] + fa[1]) | ((unsigned long long)(fa[2] + fa[3]) << 16) |
                              ((unsigned long long)(fb[0] + fb[1]) << 32) | ((unsigned long long)(fb[2] + fb[3]) << 48);
+    if (!__syncthreads_or(cnt != 0)) continue;  // nothing accepted in this tile: no retransmits
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
     uint32_t pa[4], pb[4];

@@ -1,0 +1,273 @@
+// Reference KATs restated in C++ against the host mirror (include/sidecar/catalog.hpp), i.e. the
+// same method names as catalog/services_state_test.go and services_delegate_test.go. Linked
+// against either gx.h implementation (CPU oracle for the CPU suite, libgx.so on the GPU).
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "sidecar/catalog.hpp"
+
+using sidecar::Cluster;
+using sidecar::Service;
+using sidecar::ServicesDelegate;
+using sidecar::catalog::ServicesState;
+
+static int failures = 0, checks = 0;
+#define So(cond)                                                                  \
+  do {                                                                            \
+    checks++;                                                                     \
+    if (!(cond)) {                                                                \
+      failures++;                                                                 \
+      std::fprintf(stderr, "%s:%d: %s: FAILED %s\n", __FILE__, __LINE__, cur, #cond); \
+    }                                                                             \
+  } while (0)
+static const char *cur = "";
+
+static const int64_t SEC = 1000000000ll, MIN = 60 * SEC, HOUR = 60 * MIN;
+static const std::string hostname = "shakespeare", anotherHostname = "chaucer", local = "localhost";
+
+static gx_params params() {
+  gx_params p = Cluster::Defaults(8, 8);
+  p.t0_ns = 1700000000ll * SEC;
+  p.retransmit_rounds = 0;  // state.tombstoneRetransmit = 1ns
+  p.queue_cap = 64;
+  return p;
+}
+
+// Test_ServicesStateWithData (services_state_test.go:82-321)
+static void test_services_state_with_data() {
+  {
+    cur = "Merges in a new service (:126-133)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    Service svc{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE};
+    So(!state.HasServer(anotherHostname));
+    state.AddServiceEntry(svc);
+    So(state.HasServer(anotherHostname));
+    So(state.Get(anotherHostname, svc.ID).has_value());
+  }
+  {
+    cur = "Doesn't merge an update that is older than what we have (:135-155)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    Service svc{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE};
+    state.AddServiceEntry(svc);
+    Service stale = svc;
+    stale.Updated = svc.Updated - MIN;
+    state.AddServiceEntry(stale);
+    So(state.Get(anotherHostname, svc.ID)->Updated == svc.Updated);
+  }
+  {
+    cur = "Doesn't merge an update that is past the tombstone lifespan (:157-175)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    int64_t base = c.Now();
+    c.Advance(1);  // the reference re-reads time.Now() inside IsStale
+    Service stale{"deadbeef123", anotherHostname, base - MIN - 3 * HOUR, sidecar::ALIVE};
+    state.AddServiceEntry(stale);
+    So(!state.HasServer(anotherHostname));
+  }
+  {
+    cur = "Retransmits a packet when the state changes (:214-225)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    ServicesDelegate delegate(c, state);
+    Service svc{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE};
+    state.AddServiceEntry(svc);
+    So(delegate.GetBroadcasts().size() == 1);  // catch the retransmit from the initial add
+    c.Advance(1);
+    svc.Status = sidecar::TOMBSTONE;  // svc.Tombstone()
+    svc.Updated = c.Now();
+    state.AddServiceEntry(svc);
+    auto packet = delegate.GetBroadcasts();
+    So(packet.size() == 1 && packet[0] == svc);
+  }
+  {
+    cur = "Doesn't retransmit an add of a new service for this host (:227-243)";
+    Cluster c(params());
+    ServicesState state(c, hostname);
+    ServicesDelegate delegate(c, state);
+    state.AddServiceEntry(Service{"deadbeef123", hostname, c.Now(), sidecar::ALIVE});
+    So(delegate.GetBroadcasts().empty());
+  }
+  {
+    cur = "Sets a service's status to DRAINING (:245-256)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    Service svc{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE};
+    state.AddServiceEntry(svc);
+    c.Advance(1);
+    svc.Status = sidecar::DRAINING;
+    svc.Updated = c.Now();
+    state.AddServiceEntry(svc);
+    So(state.Get(anotherHostname, svc.ID)->Status == sidecar::DRAINING);
+  }
+  {
+    cur = "Doesn't mark a DRAINING service as ALIVE (:258-270)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    Service svc{"deadbeef123", anotherHostname, c.Now(), sidecar::DRAINING};
+    state.AddServiceEntry(svc);
+    c.Advance(1);
+    svc.Status = sidecar::ALIVE;
+    svc.Updated = c.Now();
+    state.AddServiceEntry(svc);
+    So(state.Get(anotherHostname, svc.ID)->Status == sidecar::DRAINING);
+  }
+  {
+    cur = "Merge() merges state we care about from other state structs (:299-308)";
+    Cluster c(params());
+    ServicesState firstState(c, "first"), secondState(c, "second");
+    firstState.AddServiceEntry(Service{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE});
+    secondState.Merge(firstState);
+    So(secondState.EachService() == firstState.EachService());
+  }
+}
+
+// Test_TrackingAndBroadcasting (services_state_test.go:323-570)
+static void test_tracking_and_broadcasting() {
+  gx_params p = params();
+  {
+    cur = "The correct number of messages are sent (:345-353)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    std::vector<Service> services{{"deadbeef123", hostname, c.Now(), sidecar::ALIVE},
+                                  {"deadbeef101", hostname, c.Now(), sidecar::ALIVE}};
+    state.SendServices(services, 5);
+    int n = 0;
+    while (!d.GetBroadcasts().empty()) n++;
+    So(n == 5);
+  }
+  {
+    cur = "New services are serialized into the channel (:368-378)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    std::vector<Service> services{{"deadbeef123", hostname, c.Now(), sidecar::ALIVE},
+                                  {"deadbeef101", hostname, c.Now(), sidecar::ALIVE}};
+    state.BroadcastServices([&] { return services; });
+    So(d.GetBroadcasts() == services);
+  }
+  {
+    cur = "Puts a nil into the broadcasts channel when no services (:380-386)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    state.BroadcastServices([] { return std::vector<Service>{}; });
+    So(d.GetBroadcasts().empty());
+  }
+  {
+    cur = "All of the tombstones are serialized into the channel (:388-400)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    Service junk{"runs", hostname, c.Now(), sidecar::ALIVE};
+    std::vector<Service> services{{"deadbeef123", hostname, c.Now(), sidecar::ALIVE},
+                                  {"deadbeef101", hostname, c.Now(), sidecar::ALIVE}};
+    state.AddServiceEntry(junk);
+    for (auto &s : services) state.AddServiceEntry(s);
+    state.BroadcastTombstones([&] { return services; });
+    auto b = d.GetBroadcasts();
+    So(b.size() == 2);
+    for (auto &x : b) So(x.ID == "runs" && x.Status == sidecar::TOMBSTONE);
+  }
+  {
+    cur = "The timestamp is incremented on each subsequent service broadcast background run (:402-424)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    Service s1{"deadbeef123", hostname, c.Now(), sidecar::TOMBSTONE};
+    state.SendServices({s1}, 2);
+    So(d.GetBroadcasts()[0].Updated == s1.Updated);
+    So(d.GetBroadcasts()[0].Updated == s1.Updated + 50);
+  }
+  {
+    cur = "Alive services have a lifespan and then are tombstoned (:480-492)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    Service s1{"deadbeef123", hostname, c.Now(), sidecar::ALIVE};
+    state.AddServiceEntry(s1);
+    int64_t stamp = s1.Updated - 80 * SEC - 5 * SEC;
+    state.Set(Service{s1.ID, hostname, stamp, sidecar::ALIVE});
+    state.TombstoneOthersServices();
+    auto got = state.Get(hostname, s1.ID);
+    So(got->Status == sidecar::TOMBSTONE && got->Updated == stamp + SEC);
+  }
+  {
+    cur = "Draining services are not tombstoned before their lifespan expires (:509-522)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    Service s1{"deadbeef123", hostname, c.Now(), sidecar::DRAINING};
+    state.AddServiceEntry(s1);
+    int64_t stamp = s1.Updated - 80 * SEC - 5 * SEC;
+    state.Set(Service{s1.ID, hostname, stamp, sidecar::DRAINING});
+    state.TombstoneOthersServices();
+    So(state.Get(hostname, s1.ID)->Status == sidecar::DRAINING);
+  }
+  {
+    cur = "Can detect new services or newly changed services (:552-559)";
+    Cluster c(p);
+    ServicesState state(c, hostname);
+    state.AddServiceEntry(Service{"deadbeef123", hostname, c.Now(), sidecar::UNHEALTHY});
+    So(state.IsNewService(Service{"deadbeef123", hostname, c.Now(), sidecar::ALIVE}));
+    So(!state.IsNewService(Service{"deadbeef123", hostname, c.Now(), sidecar::TOMBSTONE}));
+  }
+}
+
+// Test_ClusterMembershipManagement (services_state_test.go:675-731)
+static void test_cluster_membership() {
+  {
+    cur = "ExpireServer() tombstones all services for a server (:691-714)";
+    Cluster c(params());
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    state.AddServiceEntry(Service{"deadbeef123", hostname, c.Now(), sidecar::ALIVE});
+    state.AddServiceEntry(Service{"deadbeef101", hostname, c.Now(), sidecar::ALIVE});
+    state.ExpireServer(hostname);
+    auto expired = d.GetBroadcasts();
+    So(expired.size() == 2);
+    for (auto &x : expired) So(x.Status == sidecar::TOMBSTONE);
+  }
+  {
+    cur = "does not announce services for hosts with no alive services (:722-729)";
+    Cluster c(params());
+    ServicesState state(c, hostname);
+    ServicesDelegate d(c, state);
+    state.AddServiceEntry(Service{"deadbeef123", hostname, c.Now(), sidecar::TOMBSTONE});
+    state.ExpireServer(hostname);
+    So(state.EachService().size() == 1);
+    So(d.GetBroadcasts().empty());
+  }
+}
+
+// Test_GetBroadcasts (services_delegate_test.go:40-103)
+static void test_get_broadcasts() {
+  Cluster c(params());
+  ServicesState state(c, local);
+  ServicesDelegate delegate(c, state);
+  cur = "Returns nil when there is nothing to send (:41-43)";
+  So(delegate.GetBroadcasts(6).empty());
+  cur = "Returns what's in the channel (:54-63)";
+  std::vector<Service> bCast{{"d419fa7ad1a7", "docker2", 1425431566669648453ll, sidecar::ALIVE},
+                             {"deadbeefabba", "docker2", 1425431566669648453ll, sidecar::ALIVE}};
+  state.SendServices(bCast, 1);
+  So(delegate.GetBroadcasts(6) == bCast);
+  cur = "NotifyMsg merges the packet (:72-83)";
+  c.Advance(1);
+  delegate.NotifyMsg({Service{"feedface", "docker3", c.Now(), sidecar::ALIVE}});
+  So(state.HasServer("docker3"));
+  cur = "NotifyLeave expires the node (:173-176)";
+  delegate.NotifyLeave("docker3");
+  So(state.Get("docker3", "feedface")->Status == sidecar::TOMBSTONE);
+}
+
+int main() {
+  test_services_state_with_data();
+  test_tracking_and_broadcasting();
+  test_cluster_membership();
+  test_get_broadcasts();
+  std::printf("backend=%s checks=%d failures=%d\n", gx_backend(), checks, failures);
+  return failures ? 1 : 0;
+}
