@@ -23,7 +23,7 @@ for name, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
     rows = list(csv.DictReader(open(f"{src}/{name}/run_counter_collection.csv")))
     acc = collections.defaultdict(lambda: [0, 0.0])
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]
         acc[k][0] += 1
         acc[k][1] += float(r["Counter_Value"])
     for k, (n, v) in acc.items():
@@ -37,7 +37,7 @@ for k, v in agg.items():
     if f is not None and w is not None:
         v["hbm_bytes_per_launch"] = int((2 * f + w) * 1024)
     for kk, c in cls.items():
-        if k.startswith(kk + "<") or k == kk:
+        if k == kk:
             summary[c] = v
 json.dump(dict(agg), open(f"{dst}/cfg5_pmc.json", "w"), indent=1, sort_keys=True)
 pmc = {}
@@ -45,6 +45,6 @@ if os.path.exists("profiles/pmc_summary.json"):
     pmc = json.load(open("profiles/pmc_summary.json"))
 pmc["cfg5"] = summary
 pmc["_note"] = ("hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 from separate rocprofv3 --pmc "
-                "passes of bench.py --config cfg5 --steps 12 (profiles/collect.sh)")
+                "passes of bench.py --config cfg5 --steps 100, the same launches as the default bench (profiles/collect.sh)")
 json.dump(pmc, open("profiles/pmc_summary.json", "w"), indent=1, sort_keys=True)
 print(json.dumps(summary, indent=1))

@@ -122,6 +122,8 @@ class DistShard:
         self.s = _Shard(p, lib, self.device)
         self.e = self.s.e
 
+    CHUNK = 256 << 20  # bytes per peer per all-to-all call
+
     def _exchange(self, sizes: np.ndarray, packer, unpacker):
         dist = self.dist
         send_sizes = torch.tensor(sizes.astype(np.int64), device=self.device)
@@ -131,8 +133,25 @@ class DistShard:
         ss = [int(x) for x in sizes.tolist()]
         send = self.s.pack(sizes, packer)
         recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
-        if sum(rs) or sum(ss):
-            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+        # every rank runs the same number of calls: ceil(largest per-peer segment / CHUNK)
+        mx = torch.tensor([max(ss + rs + [0])], dtype=torch.int64, device=self.device)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
+        calls = (int(mx.item()) + self.CHUNK - 1) // self.CHUNK
+        soff = np.concatenate([[0], np.cumsum(ss)])
+        roff = np.concatenate([[0], np.cumsum(rs)])
+        for c in range(calls):
+            lo = c * self.CHUNK
+            s_part = [max(0, min(self.CHUNK, n - lo)) for n in ss]
+            r_part = [max(0, min(self.CHUNK, n - lo)) for n in rs]
+            s_buf = torch.cat([send[int(soff[p]) + lo:int(soff[p]) + lo + s_part[p]] for p in range(self.world)])
+            r_buf = torch.empty(sum(r_part), dtype=torch.uint8, device=self.device)
+            dist.all_to_all_single(r_buf, s_buf, output_split_sizes=r_part, input_split_sizes=s_part,
+                                   group=self.group)
+            o = 0
+            for p in range(self.world):
+                if r_part[p]:
+                    recv[int(roff[p]) + lo:int(roff[p]) + lo + r_part[p]].copy_(r_buf[o:o + r_part[p]])
+                o += r_part[p]
         self.s.sync()
         unpacker(_ptr(recv), recv.numel())
 
