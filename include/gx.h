@@ -132,6 +132,15 @@ typedef struct gx_params {
   int32_t device;                     /* HIP device ordinal (ignored by the oracle) */
   uint32_t n_shards;                  /* host sharding: 0/1 = this engine owns every host */
   uint32_t shard_id;                  /* this engine owns hosts [id*H/n, (id+1)*H/n) */
+  /* Byte-accurate packPacket (services_delegate.go:186-223). limit_bytes = 0 keeps the
+   * record-count budget (packet_cap records per GetBroadcasts call, BASELINE "cap 32
+   * records/msg"). limit_bytes > 0 is memberlist's GetBroadcasts(overhead, limit): messages are
+   * packed while total + len(message) + overhead <= limit, where len(message) is the ffjson
+   * encoding length of the record's Service (gx_message_bytes); packet_cap then only bounds the
+   * packet buffer (a cut it causes is counted in gx_stats.cap_cuts). memberlist passes limit =
+   * UDPBufferSize 1400 - 2 = 1398 and overhead = 2 + 1 = 3. */
+  uint32_t limit_bytes;
+  uint32_t overhead_bytes;
 } gx_params;
 
 /* Per-host bookkeeping (read-back for parity). */
@@ -175,7 +184,9 @@ typedef struct gx_stats {
   int64_t last_change_round; /* last round in which any view slot changed, -1 = none */
   uint64_t scan_slots;       /* view slots streamed by expiry scans */
   uint64_t ae_slots;         /* view slots streamed by anti-entropy merges (both directions) */
-  uint64_t reserved[5];
+  uint64_t bytes_sent;       /* byte-limit mode: sum of len(message) + overhead of sent records */
+  uint64_t cap_cuts;         /* byte-limit mode: packets cut by packet_cap before the byte limit */
+  uint64_t reserved[3];
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */
@@ -229,7 +240,12 @@ int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes);
 int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + received packets */
 int gx_ae_bytes(gx_engine *e, uint64_t *bytes_per_shard); /* 0s unless this is a push-pull round */
 int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap);
-int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes); /* phase 5 */
+int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes);
+/* Optional, between gx_ae_pack and gx_ae_merge: start the push-pull merges of the pairs whose two
+ * hosts are both on this shard, asynchronously on the engine's stream, so they overlap the row
+ * exchange; gx_ae_merge then merges only the pairs with a received row. Pairs are disjoint (every
+ * host is in at most one), so the result is identical either way. */
+int gx_ae_merge_local(gx_engine *e); /* phase 5 */
 int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */
 /* Per-record min and max slot word over this engine's views (R entries each; device memory for
  * the HIP engine), written as (word XOR 2^63) so that signed 64-bit MIN/MAX reductions across
@@ -273,6 +289,22 @@ int gx_notify_msg(gx_engine *e, uint32_t host, const gx_service *recs, uint32_t 
 #define GX_LIMIT_DEFAULT 0xffffffffu
 int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *out, uint32_t cap,
                       uint32_t *n_out);
+/* GetBroadcasts(overhead, limit) with the byte limit of the reference signature: packPacket
+ * keeps the greedy prefix with total + len(message) + overhead <= limit (:194-203); a first
+ * message that does not fit sends nothing and keeps everything pending (:205-221). At most cap
+ * records are returned (pass cap >= packet_cap + 2 * pending_cap for the unbounded reference
+ * result; a cut is counted in gx_stats.cap_cuts). */
+int gx_get_broadcasts_bytes(gx_engine *e, uint32_t host, uint32_t overhead, uint32_t limit,
+                            gx_service *out, uint32_t cap, uint32_t *n_out);
+/* Encoded message length of records: Service.Encode() = ffjson MarshalJSONBuf
+ * (service/service_ffjson.go:370-436) = the record's static bytes (every field except Updated
+ * and Status: ID, Name, Image, Created, Hostname, Ports, ProxyMode and the JSON punctuation,
+ * set with gx_set_static_bytes) + len of time.Time.MarshalJSON(Updated) (quoted RFC3339Nano,
+ * UTC "Z", fraction with trailing zeros trimmed) + len of the decimal Status. */
+#define GX_STATIC_BYTES_DEFAULT 192 /* services_delegate_test.go:16 fixture minus Updated/Status */
+int gx_set_static_bytes(gx_engine *e, uint32_t owner_lo, uint32_t owner_hi,
+                        const uint16_t *bytes /* [(owner_hi - owner_lo) * S] */);
+int gx_message_bytes(gx_engine *e, const gx_service *recs, uint32_t n, uint32_t *out_bytes);
 /* LocalState (:146-151): present records of the view in key order (n_out = total). */
 int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out);
 /* MergeRemoteState (:153-167): a decoded remote state -> Merge. */

@@ -116,6 +116,18 @@ class Cluster {
     s.Status = r.status;
     return s;
   }
+  // Encoded length of every field of svc's Service except Updated and Status (the Go side gets it
+  // from len(svc.Encode()) minus those two); used by the byte-limited GetBroadcasts.
+  void SetStaticBytes(const std::string &hostname, const std::string &id, uint16_t bytes) {
+    uint32_t h = Host(hostname);
+    uint16_t j = Id(h, id);
+    std::vector<uint16_t> row(p_.n_services, (uint16_t)GX_STATIC_BYTES_DEFAULT);
+    auto it = static_.find(h);
+    if (it != static_.end()) row = it->second;
+    row[j] = bytes;
+    static_[h] = row;
+    check(gx_set_static_bytes(e_, h, h + 1, row.data()), "gx_set_static_bytes");
+  }
   std::vector<Service> Svcs(const std::vector<gx_service> &rs) const {
     std::vector<Service> out;
     for (auto &r : rs) out.push_back(Svc(r));
@@ -129,6 +141,7 @@ class Cluster {
   std::vector<std::string> host_names_;
   std::vector<std::map<std::string, uint16_t>> ids_;
   std::vector<std::vector<std::string>> id_names_;
+  std::map<uint32_t, std::vector<uint16_t>> static_;
 };
 
 namespace catalog {
@@ -250,6 +263,18 @@ class ServicesDelegate {
     std::vector<gx_service> out(256);
     uint32_t n = 0;
     check(gx_get_broadcasts(c_.engine(), state_.index(), limit_records, out.data(), (uint32_t)out.size(), &n),
+          "GetBroadcasts");
+    out.resize(n);
+    return c_.Svcs(out);
+  }
+  // GetBroadcasts(overhead, limit) with the reference's byte limit (services_delegate.go:85-144,
+  // packPacket :186-223); nil is an empty result.
+  std::vector<Service> GetBroadcasts(int overhead, int limit) {
+    const gx_params &p = c_.params();
+    std::vector<gx_service> out(p.packet_cap + 2 * p.pending_cap);
+    uint32_t n = 0;
+    check(gx_get_broadcasts_bytes(c_.engine(), state_.index(), (uint32_t)overhead, (uint32_t)limit, out.data(),
+                                  (uint32_t)out.size(), &n),
           "GetBroadcasts");
     out.resize(n);
     return c_.Svcs(out);

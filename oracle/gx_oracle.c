@@ -16,6 +16,7 @@
  */
 #include "../include/gx.h"
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -49,6 +50,8 @@ struct gx_engine {
   uint32_t *msg_dst;    /* H * K */
   uint32_t *in_cnt;     /* H + 1 */
   uint32_t *in_list;    /* H * K  (sender * K + j), grouped by receiver, sender-ascending */
+  uint16_t *sbytes;     /* R  encoded bytes of every Service field but Updated and Status */
+  int64_t ae_local_round; /* round whose shard-local push-pull pairs gx_ae_merge_local merged */
   gx_stats st;
 };
 
@@ -188,9 +191,34 @@ static uint32_t expand(const gx_engine *e, uint32_t v, const gx_job *j, grec *ou
   return n;
 }
 
-/* GetBroadcasts(overhead, limit), services_delegate.go:85-144, with packPacket (:186-223)
- * under a record-count limit. Returns the packet length (0 = nil). */
-static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *packet) {
+/* len(svc.Encode()) for the byte-limited packPacket: ffjson MarshalJSONBuf
+ * (service/service_ffjson.go:370-436) writes every field; all but Updated and Status are fixed per
+ * record key (sbytes). Updated: time.Time.MarshalJSON -> '"' + Format(RFC3339Nano) + '"', which in
+ * UTC is "2006-01-02T15:04:05" + ".999999999" (trailing zeros dropped, and the dot with them when
+ * the fraction is zero) + "Z". Status: FormatBits2 base 10. */
+static uint32_t rfc3339nano_json_len(int64_t ts) {
+  int64_t frac = ((ts % 1000000000ll) + 1000000000ll) % 1000000000ll;
+  uint32_t len = 2 + 19 + 1; /* quotes, date-time, "Z" */
+  if (frac) {
+    char digits[10];
+    snprintf(digits, sizeof digits, "%09lld", (long long)frac);
+    int n = 9;
+    while (n > 0 && digits[n - 1] == '0') n--;
+    len += 1 + (uint32_t)n;
+  }
+  return len;
+}
+static uint32_t message_len(const gx_engine *e, grec g) {
+  char st[8];
+  int n = snprintf(st, sizeof st, "%u", (unsigned)st_of(g.w));
+  return e->sbytes[g.r] + rfc3339nano_json_len(ts_of(g.w)) + (uint32_t)n;
+}
+
+/* GetBroadcasts(overhead, limit), services_delegate.go:85-144, with packPacket (:186-223).
+ * limit = record budget; limit_bytes > 0 adds packPacket's byte limit and per-message overhead.
+ * Returns the packet length (0 = nil). */
+static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *packet, uint32_t limit_bytes,
+                               uint32_t overhead) {
   gx_host_state *h = &e->hs[v];
   grec batch[512];
   uint32_t m = 0;
@@ -233,6 +261,22 @@ static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *p
   h->dq_len += m;
   /* packPacket: greedy prefix within the limit (:186-223) */
   uint32_t l = h->dq_len < limit ? h->dq_len : limit;
+  if (limit_bytes) {
+    uint64_t total = 0;
+    int last_item = -1;
+    for (uint32_t i = 0; i < h->dq_len; i++) { /* for i, message := range broadcasts (:194) */
+      uint32_t len = message_len(e, dq[(h->dq_head + i) & mask]);
+      if (total + len + overhead > limit_bytes) break;
+      if (i == limit) { /* the packet buffer is full before the byte limit */
+        e->st.cap_cuts++;
+        break;
+      }
+      last_item = (int)i;
+      total += len + overhead;
+    }
+    l = (uint32_t)(last_item + 1); /* lastItem < 0: nil, everything stays pending (:205-221) */
+    e->st.bytes_sent += total;
+  }
   for (uint32_t i = 0; i < l; i++) packet[i] = dq[(h->dq_head + i) & mask];
   h->dq_head = (h->dq_head + l) & mask;
   h->dq_len -= l;
@@ -551,7 +595,8 @@ static void round_send(gx_engine *e) {
     uint32_t peers[64];
     uint32_t np = sample_peers(e, u, peers);
     for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap]);
+      uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap], e->p.limit_bytes,
+                                  e->p.overhead_bytes);
       e->msg_len[(size_t)u * K + j] = l;
       e->msg_dst[(size_t)u * K + j] = peers[j];
       if (l == 0 && e->p.gossip_stop_on_empty) break;
@@ -651,8 +696,9 @@ static void ae_phase(gx_engine *e, const uint64_t *rows, uint64_t bytes) {
       next++;
     }
   }
-  for (uint32_t t = 0; t < np; t++)
-    if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
+  if (e->ae_local_round != e->round)
+    for (uint32_t t = 0; t < np; t++)
+      if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
   free(pa);
   free(pb);
 }
@@ -709,6 +755,8 @@ void gx_params_default(gx_params *p) {
   p->partition_end = 0;
   p->storm_round = -1;
   p->device = 0;
+  p->limit_bytes = 0;
+  p->overhead_bytes = 3;
 }
 
 static int check_params(const gx_params *p) {
@@ -722,6 +770,7 @@ static int check_params(const gx_params *p) {
   if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
   if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
+  if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   return GX_OK;
 }
@@ -789,12 +838,16 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->msg_dst = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
   e->in_cnt = (uint32_t *)calloc(H + 1, sizeof(uint32_t));
   e->in_list = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
-  if (!e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
+  e->sbytes = (uint16_t *)malloc(sizeof(uint16_t) * e->R);
+  if (e->sbytes)
+    for (uint32_t r = 0; r < e->R; r++) e->sbytes[r] = GX_STATIC_BYTES_DEFAULT;
+  if (!e->sbytes || !e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
       !e->arena_len || !e->msg || !e->msg_len || !e->msg_dst || !e->in_cnt || !e->in_list) {
     gx_destroy(e);
     return GX_ENOMEM;
   }
   init_state(e);
+  e->ae_local_round = -1;
   *out = e;
   return GX_OK;
 }
@@ -814,6 +867,7 @@ int gx_destroy(gx_engine *e) {
   free(e->msg_dst);
   free(e->in_cnt);
   free(e->in_list);
+  free(e->sbytes);
   free(e);
   return GX_OK;
 }
@@ -1005,9 +1059,39 @@ int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *o
   if (limit == GX_LIMIT_DEFAULT) limit = e ? e->p.packet_cap : 0;
   if (!e || host >= e->H || !n_out || limit > 256 || cap < limit || (limit && !out)) return GX_EINVAL;
   grec pk[256];
-  uint32_t l = get_broadcasts(e, host, limit, pk);
+  uint32_t l = get_broadcasts(e, host, limit, pk, 0, 0);
   for (uint32_t i = 0; i < l; i++) to_svc(e, &pk[i], &out[i]);
   *n_out = l;
+  return GX_OK;
+}
+
+int gx_get_broadcasts_bytes(gx_engine *e, uint32_t host, uint32_t overhead, uint32_t limit, gx_service *out,
+                            uint32_t cap, uint32_t *n_out) {
+  if (!e || host >= e->H || !n_out || (cap && !out) || cap > (1u << 20)) return GX_EINVAL;
+  uint32_t m = cap < e->DQ ? cap : e->DQ;
+  grec *pk = (grec *)malloc(sizeof(grec) * (m ? m : 1));
+  if (!pk) return GX_ENOMEM;
+  uint32_t l = (limit == 0 || cap == 0) ? get_broadcasts(e, host, 0, pk, 0, 0)
+                                        : get_broadcasts(e, host, m, pk, limit, overhead);
+  for (uint32_t i = 0; i < l; i++) to_svc(e, &pk[i], &out[i]);
+  free(pk);
+  *n_out = l;
+  return GX_OK;
+}
+
+int gx_set_static_bytes(gx_engine *e, uint32_t owner_lo, uint32_t owner_hi, const uint16_t *bytes) {
+  if (!e || owner_lo > owner_hi || owner_hi > e->H || (owner_hi > owner_lo && !bytes)) return GX_EINVAL;
+  memcpy(&e->sbytes[(size_t)owner_lo * e->S], bytes, sizeof(uint16_t) * (size_t)(owner_hi - owner_lo) * e->S);
+  return GX_OK;
+}
+
+int gx_message_bytes(gx_engine *e, const gx_service *recs, uint32_t n, uint32_t *out_bytes) {
+  if (!e || (n && (!recs || !out_bytes))) return GX_EINVAL;
+  for (uint32_t i = 0; i < n; i++) {
+    grec g;
+    if (to_grec(e, &recs[i], &g)) return GX_EINVAL;
+    out_bytes[i] = message_len(e, g);
+  }
   return GX_OK;
 }
 
@@ -1234,6 +1318,20 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
 int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
   if (!e || (bytes && !buf)) return GX_EINVAL;
   ae_phase(e, (const uint64_t *)buf, bytes);
+  return GX_OK;
+}
+int gx_ae_merge_local(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  if (!ae_round(e) || e->G < 2 || e->ae_local_round == e->round) return GX_OK;
+  int64_t now = now_of(e);
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t np = ae_pairs(e, pa, pb);
+  for (uint32_t t = 0; t < np; t++)
+    if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
+  free(pa);
+  free(pb);
+  e->ae_local_round = e->round;
   return GX_OK;
 }
 int gx_round_end(gx_engine *e) {

@@ -80,6 +80,8 @@ class GxParams(C.Structure):
         ("aged_max_ns", C.c_int64), ("partition_start", C.c_int32), ("partition_end", C.c_int32),
         ("storm_round", C.c_int32), ("device", C.c_int32), ("n_shards", C.c_uint32),
         ("shard_id", C.c_uint32),
+        ("limit_bytes", C.c_uint32),
+        ("overhead_bytes", C.c_uint32),
     ]
 
 
@@ -97,7 +99,7 @@ class GxStats(C.Structure):
         "pending_drops", "dequeues", "nil_batches", "packets", "records_sent", "expired", "gc",
         "own_tombstones", "expire_server", "send_jobs", "ae_exchanges", "churn_events")] + [
         ("last_change_round", C.c_int64), ("scan_slots", C.c_uint64), ("ae_slots", C.c_uint64),
-        ("reserved", C.c_uint64 * 5)]
+        ("bytes_sent", C.c_uint64), ("cap_cuts", C.c_uint64), ("reserved", C.c_uint64 * 3)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
@@ -122,7 +124,7 @@ ABI_FUNCS = [
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
-    "gx_view_minmax",
+    "gx_view_minmax", "gx_ae_merge_local", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
 ]
 
 
@@ -165,6 +167,10 @@ def _declare(lib):
         "gx_round_merge": ([vp], i32), "gx_ae_bytes": ([vp, vp], i32),
         "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64], i32),
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
+        "gx_ae_merge_local": ([vp], i32),
+        "gx_get_broadcasts_bytes": ([vp, u32, u32, u32, P(GxService), u32, P(u32)], i32),
+        "gx_set_static_bytes": ([vp, u32, u32, P(u16)], i32),
+        "gx_message_bytes": ([vp, P(GxService), u32, P(u32)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -355,6 +361,30 @@ class Engine:
             return None
         return [out[i] for i in range(n.value)]
 
+    def get_broadcasts_bytes(self, host: int, overhead: int, limit: int, cap: Optional[int] = None):
+        """GetBroadcasts(overhead, limit) with the reference's byte limit; None = nil."""
+        cap = 1024 if cap is None else int(cap)
+        out = (GxService * max(1, cap))()
+        n = C.c_uint32()
+        check(self.lib.gx_get_broadcasts_bytes(self.h, host, overhead, limit, out, cap, C.byref(n)),
+              "gx_get_broadcasts_bytes")
+        if n.value == 0:
+            return None
+        return [out[i] for i in range(n.value)]
+
+    def set_static_bytes(self, owner_lo: int, owner_hi: int, nbytes):
+        a = np.ascontiguousarray(np.asarray(nbytes, dtype=np.uint16).reshape(-1))
+        assert a.size == (owner_hi - owner_lo) * self.S
+        check(self.lib.gx_set_static_bytes(self.h, owner_lo, owner_hi,
+                                           a.ctypes.data_as(C.POINTER(C.c_uint16))), "gx_set_static_bytes")
+
+    def message_bytes(self, recs):
+        """len(Service.Encode()) of each record (service/service_ffjson.go:370-436)."""
+        n = len(recs)
+        out = (C.c_uint32 * max(1, n))()
+        check(self.lib.gx_message_bytes(self.h, svc_array(recs), n, out), "gx_message_bytes")
+        return [out[i] for i in range(n)]
+
     def local_state(self, view: int):
         n = C.c_uint32()
         check(self.lib.gx_local_state(self.h, view, None, 0, C.byref(n)))
@@ -466,6 +496,10 @@ class Engine:
 
     def ae_merge(self, ptr: int, nbytes: int):
         check(self.lib.gx_ae_merge(self.h, C.c_void_p(ptr), nbytes), "gx_ae_merge")
+
+    def ae_merge_local(self):
+        """Start this shard's local push-pull pairs (asynchronous; overlaps the row exchange)."""
+        check(self.lib.gx_ae_merge_local(self.h), "gx_ae_merge_local")
 
     def round_end(self):
         check(self.lib.gx_round_end(self.h), "gx_round_end")

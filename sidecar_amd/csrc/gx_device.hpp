@@ -33,7 +33,8 @@ struct grec {
 enum {
   C_GOSSIP_MERGES, C_AE_MERGES, C_LOCAL_MERGES, C_GOSSIP_ACC, C_AE_ACC, C_LOCAL_ACC, C_STALE,
   C_RETX, C_QDROP, C_LDROP, C_SDROP, C_PDROP, C_DEQ, C_NIL, C_PACKETS, C_RECSENT, C_EXPIRED,
-  C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_NCTR
+  C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_BYTESENT,
+  C_CAPCUT, C_NCTR
 };
 
 #define GX_SHARDS 64
@@ -75,6 +76,7 @@ struct Dev {
   grec *scan_list;     // [H][L] first L expired records of this round's scan
   uint32_t *scan_cnt;  // [H]
   uint8_t *tick;       // [H] BroadcastTombstones tick this round
+  uint16_t *sbytes;    // [R] static encoded bytes per record key (every field but Updated/Status)
   DevCtr *ctr;
 };
 
@@ -295,7 +297,31 @@ GXD grec job_rec(const Dev &d, uint32_t v, const gx_job &j, uint32_t i, uint32_t
 }
 
 // GetBroadcasts(overhead, limit) + packPacket (services_delegate.go:85-144, :186-223).
-GXD uint32_t get_broadcasts(const Dev &d, Acc &a, uint32_t v, uint32_t limit, grec *packet) {
+// ---------------------------------------------------------- encoded message length (f-1) --
+// len(Service.Encode()) (service/service_ffjson.go:370-436): the static fields come from the
+// per-record table; "Updated" is time.Time.MarshalJSON = quoted RFC3339Nano in UTC:
+// "YYYY-MM-DDTHH:MM:SS" + ("." + fraction without trailing zeros, omitted when zero) + "Z";
+// "Status" is FormatBits2 decimal.
+GXHD uint32_t json_time_len(int64_t ts) {
+  int64_t f = ts % 1000000000ll;
+  if (f < 0) f += 1000000000ll;
+  if (f == 0) return 22;
+  uint32_t n = 9;
+  while (f % 10 == 0) {
+    f /= 10;
+    n--;
+  }
+  return 23 + n;
+}
+GXHD uint32_t dec_len(uint32_t x) { return x >= 100 ? 3 : x >= 10 ? 2 : 1; }
+GXD uint32_t msg_bytes(const Dev &d, const grec &g) {
+  return d.sbytes[g.r] + json_time_len(ts_of(g.w)) + dec_len((uint32_t)st_of(g.w));
+}
+
+// GetBroadcasts (services_delegate.go:85-144). limit = record budget (the packet buffer);
+// limit_bytes > 0 adds packPacket's byte budget with per-message overhead.
+GXD uint32_t get_broadcasts(const Dev &d, Acc &a, uint32_t v, uint32_t limit, grec *packet,
+                            uint32_t limit_bytes = 0, uint32_t overhead = 0) {
   gx_host_state *h = hst(d, v);
   uint32_t m = 0;
   uint32_t mask = d.DQ - 1;
@@ -337,7 +363,21 @@ GXD uint32_t get_broadcasts(const Dev &d, Acc &a, uint32_t v, uint32_t limit, gr
   } else if (h->dq_len == 0) {  // default: nothing pending (:96-98)
     return 0;
   }
-  uint32_t l = h->dq_len < limit ? h->dq_len : limit;  // packPacket greedy prefix
+  // packPacket (:186-223): the greedy prefix within the limit
+  uint32_t n = h->dq_len < limit ? h->dq_len : limit;
+  uint32_t l = n;
+  if (limit_bytes) {
+    uint64_t total = 0;
+    for (l = 0; l < n; l++) {
+      uint32_t b = msg_bytes(d, dq[(h->dq_head + l) & mask]) + overhead;
+      if (total + b > limit_bytes) break;  // if total+len(message)+overhead > limit (:195)
+      total += b;
+    }
+    if (l == n && n < h->dq_len &&
+        total + msg_bytes(d, dq[(h->dq_head + n) & mask]) + overhead <= limit_bytes)
+      a.c[C_CAPCUT]++;
+    a.c[C_BYTESENT] += (unsigned)total;
+  }
   for (uint32_t i = 0; i < l; i++) packet[i] = dq[(h->dq_head + i) & mask];
   h->dq_head = (h->dq_head + l) & mask;
   h->dq_len -= l;

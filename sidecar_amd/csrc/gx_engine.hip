@@ -65,8 +65,9 @@ struct gx_engine {
   uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t;
   int32_t *ae_prow;
   uint8_t *ae_pcount;
-  uint32_t n_plan, n_pack;
+  uint32_t n_plan, n_pack, n_plan_rows;
   int ae_planned_round;
+  int64_t ae_local_round;
   // small device scratch for single-host ABI calls
   void *api_dev;
   size_t api_dev_bytes;
@@ -268,6 +269,7 @@ void gx_params_default(gx_params *p) {
   p->seed = 0x5EEDull;
   p->aged_max_ns = 100000000000ll;
   p->storm_round = -1;
+  p->overhead_bytes = 3;
 }
 
 static int check_params(const gx_params *p) {
@@ -281,6 +283,7 @@ static int check_params(const gx_params *p) {
   if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
   if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
+  if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   return GX_OK;
 }
@@ -297,7 +300,7 @@ int gx_destroy(gx_engine *e) {
   void *ptrs[] = {d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
-                  d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
+                  d.sbytes, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -338,8 +341,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = nullptr;
   e->ae_prow = nullptr;
   e->ae_pcount = nullptr;
-  e->n_plan = e->n_pack = 0;
+  e->n_plan = e->n_pack = e->n_plan_rows = 0;
   e->ae_planned_round = -1;
+  e->ae_local_round = -1;
   Dev &d = e->d;
   d.p = *p;
   d.H = p->n_hosts;
@@ -385,6 +389,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
   ALLOC(d.tick, H);
+  ALLOC(d.sbytes, sizeof(uint16_t) * d.R);
   ALLOC(d.ctr, sizeof(DevCtr));
   ALLOC(e->own_list, sizeof(grec) * H * d.S);
   ALLOC(e->conv_bad, sizeof(unsigned long long));
@@ -407,6 +412,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * Hg * K, s));
   HIPCHK(hipMemsetAsync(d.in_cnt, 0, sizeof(uint32_t) * in_pad, s));
   HIPCHK(hipMemsetAsync(d.tick, 0, H, s));
+  k_fill_u16<<<256, 256, 0, s>>>(d.sbytes, d.R, (uint16_t)GX_STATIC_BYTES_DEFAULT);
   set_round_fields(e);
   k_init_rec<<<nblk(d.R, 256), 256, 0, s>>>(d, rec_word);
   k_init_views<<<2048, 256, 0, s>>>(d, rec_word);
@@ -669,16 +675,15 @@ int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *o
   return GX_OK;
 }
 
-int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *out, uint32_t cap, uint32_t *n_out) {
-  if (limit == GX_LIMIT_DEFAULT) limit = e ? e->d.p.packet_cap : 0;
-  if (!e || !own(e, host) || !n_out || limit > 256 || cap < limit || (limit && !out)) return GX_EINVAL;
+static int getb_impl(gx_engine *e, uint32_t host, uint32_t limit, uint32_t limit_bytes, uint32_t overhead,
+                     gx_service *out, uint32_t *n_out) {
   HIPCHK(hipSetDevice(e->device));
-  int rc = ensure_api(e, 256 + sizeof(grec) * 257);
+  int rc = ensure_api(e, 256 + sizeof(grec) * (limit + 1));
   if (rc) return rc;
   uint32_t *dn = (uint32_t *)e->api_dev;
   grec *dpk = (grec *)((char *)e->api_dev + 256);
   set_round_fields(e);
-  k_api_getb<<<1, 64, 0, e->stream>>>(e->d, host, limit, dpk, dn);
+  k_api_getb<<<1, 64, 0, e->stream>>>(e->d, host, limit, dpk, dn, limit_bytes, overhead);
   uint32_t n = 0;
   HIPCHK(hipMemcpyAsync(&n, dn, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   rc = sync_check(e);
@@ -690,6 +695,48 @@ int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *o
   }
   *n_out = n;
   return GX_OK;
+}
+
+int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *out, uint32_t cap, uint32_t *n_out) {
+  if (limit == GX_LIMIT_DEFAULT) limit = e ? e->d.p.packet_cap : 0;
+  if (!e || !own(e, host) || !n_out || limit > 256 || cap < limit || (limit && !out)) return GX_EINVAL;
+  return getb_impl(e, host, limit, 0, 0, out, n_out);
+}
+
+int gx_get_broadcasts_bytes(gx_engine *e, uint32_t host, uint32_t overhead, uint32_t limit, gx_service *out,
+                            uint32_t cap, uint32_t *n_out) {
+  if (!e || !own(e, host) || !n_out || (cap && !out) || cap > (1u << 20)) return GX_EINVAL;
+  if (limit == 0 || cap == 0) {  // nothing can fit: the batch still moves to pending
+    return getb_impl(e, host, 0, 0, 0, out, n_out);
+  }
+  return getb_impl(e, host, cap, limit, overhead, out, n_out);
+}
+
+int gx_set_static_bytes(gx_engine *e, uint32_t owner_lo, uint32_t owner_hi, const uint16_t *bytes) {
+  if (!e || owner_lo > owner_hi || owner_hi > e->d.H || (owner_hi > owner_lo && !bytes)) return GX_EINVAL;
+  if (owner_hi == owner_lo) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  size_t n = (size_t)(owner_hi - owner_lo) * e->d.S;
+  HIPCHK(hipMemcpy(&e->d.sbytes[(size_t)owner_lo * e->d.S], bytes, sizeof(uint16_t) * n, hipMemcpyHostToDevice));
+  return GX_OK;
+}
+
+int gx_message_bytes(gx_engine *e, const gx_service *recs, uint32_t n, uint32_t *out_bytes) {
+  if (!e || (n && (!recs || !out_bytes))) return GX_EINVAL;
+  if (!n) return GX_OK;
+  std::vector<grec> g(n);
+  for (uint32_t i = 0; i < n; i++)
+    if (to_grec(e, &recs[i], &g[i])) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, 256 + (sizeof(grec) + sizeof(uint32_t)) * (size_t)n);
+  if (rc) return rc;
+  grec *dg = (grec *)((char *)e->api_dev + 256);
+  uint32_t *dout = (uint32_t *)(dg + n);
+  HIPCHK(hipMemcpyAsync(dg, g.data(), sizeof(grec) * n, hipMemcpyHostToDevice, e->stream));
+  k_api_msg_bytes<<<nblk(n, 256), 256, 0, e->stream>>>(e->d, dg, n, dout);
+  HIPCHK(hipMemcpyAsync(out_bytes, dout, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, e->stream));
+  return sync_check(e);
 }
 
 int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, uint32_t *n_out) {
@@ -973,6 +1020,7 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
       plan_cnt.push_back(0);
     }
   e->n_plan = (uint32_t)plan_a.size();
+  e->n_plan_rows = (uint32_t)row;
   e->n_pack = (uint32_t)pack_host.size();
   if (e->n_plan) {
     HIPCHK(hipMemcpy(e->ae_pa, plan_a.data(), 4 * e->n_plan, hipMemcpyHostToDevice));
@@ -992,7 +1040,7 @@ int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
   if (!e || !bytes) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   for (uint32_t g = 0; g < e->d.G; g++) bytes[g] = 0;
-  e->n_plan = e->n_pack = 0;
+  e->n_plan = e->n_pack = e->n_plan_rows = 0;
   e->ae_planned_round = -1;
   if (e->d.G < 2 || !ae_round(e)) return GX_OK;
   return ae_plan(e, bytes);
@@ -1007,6 +1055,30 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   return sync_check(e);
 }
 
+// Launch the planned pairs [lo, hi) (received-row pairs first, then shard-local pairs).
+static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *buf) {
+  if (hi <= lo) return;
+  set_round_fields(e);
+  LaunchTimer t(e, GX_K_AE);
+  if (e->d.R % 2 == 0)
+    k_ae_plan<true><<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,
+                                                     e->ae_pcount + lo, (const uint8_t *)buf);
+  else
+    k_ae_plan<false><<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,
+                                                      e->ae_pcount + lo, (const uint8_t *)buf);
+}
+
+int gx_ae_merge_local(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  if (!ae_round(e) || e->d.G < 2 || e->ae_local_round == e->d.round) return GX_OK;
+  if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
+  ae_plan_launch(e, e->n_plan_rows, e->n_plan, nullptr);  // asynchronous: overlaps the exchange
+  HIPCHK(hipGetLastError());
+  e->ae_local_round = e->d.round;
+  return GX_OK;
+}
+
 int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
   if (!e || (bytes && !buf)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
@@ -1016,16 +1088,8 @@ int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
     return rc ? rc : sync_check(e);
   }
   if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
-  if (e->n_plan) {
-    set_round_fields(e);
-    LaunchTimer t(e, GX_K_AE);
-    if (e->d.R % 2 == 0)
-      k_ae_plan<true><<<e->n_plan, 256, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_pcount,
-                                                          (const uint8_t *)buf);
-    else
-      k_ae_plan<false><<<e->n_plan, 256, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_pcount,
-                                                           (const uint8_t *)buf);
-  }
+  bool local_done = e->ae_local_round == e->d.round;
+  ae_plan_launch(e, 0, local_done ? e->n_plan_rows : e->n_plan, buf);
   return sync_check(e);
 }
 
@@ -1096,6 +1160,8 @@ int gx_stats_get(gx_engine *e, gx_stats *out) {
   out->send_jobs = c[C_SENDJOBS];
   out->ae_exchanges = c[C_AEX];
   out->churn_events = c[C_CHURN];
+  out->bytes_sent = c[C_BYTESENT];
+  out->cap_cuts = c[C_CAPCUT];
   out->scan_slots = c[C_SCANSLOTS];
   out->ae_slots = c[C_AESLOTS];
   out->last_change_round = (int64_t)lp1 - 1;

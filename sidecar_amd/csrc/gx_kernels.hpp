@@ -385,7 +385,8 @@ __global__ __launch_bounds__(256) void k_send(Dev d) {
       d.msg_key[(size_t)idx * d.K + j] = u * d.K + j;
     }
     for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts(d, a, u, cap, &d.msg[((size_t)idx * d.K + j) * cap]);
+      uint32_t l = get_broadcasts(d, a, u, cap, &d.msg[((size_t)idx * d.K + j) * cap], d.p.limit_bytes,
+                                  d.p.overhead_bytes);
       d.msg_len[(size_t)idx * d.K + j] = l;
       d.msg_dst[(size_t)idx * d.K + j] = peers[j];
       if (l && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
@@ -965,10 +966,18 @@ __global__ void k_api_tomb(Dev d, uint32_t v, uint64_t running, uint64_t *out_ma
   if (threadIdx.x == 0) *out_mask = tombstone_services(d, a, v, running);
   acc_flush(d, a);
 }
-__global__ void k_api_getb(Dev d, uint32_t v, uint32_t limit, grec *out, uint32_t *n_out) {
+__global__ void k_api_getb(Dev d, uint32_t v, uint32_t limit, grec *out, uint32_t *n_out, uint32_t limit_bytes,
+                           uint32_t overhead) {
   Acc a;
-  if (threadIdx.x == 0) *n_out = get_broadcasts(d, a, v, limit, out);
+  if (threadIdx.x == 0) *n_out = get_broadcasts(d, a, v, limit, out, limit_bytes, overhead);
   acc_flush(d, a);
+}
+__global__ void k_api_msg_bytes(Dev d, const grec *recs, uint32_t n, uint32_t *out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = msg_bytes(d, recs[i]);
+}
+__global__ void k_fill_u16(uint16_t *p, size_t n, uint16_t v) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 __global__ void k_api_is_new(Dev d, uint32_t v, uint64_t w, uint32_t r, uint32_t *out) {
   if (threadIdx.x == 0) *out = is_new(d, v, w, r);

@@ -58,9 +58,12 @@ class LocalShards:
     def engines(self) -> List[Engine]:
         return [s.e for s in self.shards]
 
-    def _exchange(self, sizes_fn, pack_fn, unpack_fn):
+    def _exchange(self, sizes_fn, pack_fn, unpack_fn, after_pack=None):
         sizes = [sizes_fn(s.e) for s in self.shards]  # sizes[src][dst]
         bufs = [s.pack(sz, lambda p, n, e=s.e: pack_fn(e, p, n)) for s, sz in zip(self.shards, sizes)]
+        if after_pack is not None:
+            for s in self.shards:
+                after_pack(s.e)
         for s in self.shards:
             s.sync()
         for dst, s in enumerate(self.shards):
@@ -81,7 +84,7 @@ class LocalShards:
             for s in self.shards:
                 s.e.round_merge()
             self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
-                           lambda e, p, c: e.ae_merge(p, c))
+                           lambda e, p, c: e.ae_merge(p, c), after_pack=lambda e: e.ae_merge_local())
             for s in self.shards:
                 s.e.round_end()
 
@@ -124,7 +127,7 @@ class DistShard:
 
     CHUNK = 256 << 20  # bytes per peer per all-to-all call
 
-    def _exchange(self, sizes: np.ndarray, packer, unpacker):
+    def _exchange(self, sizes: np.ndarray, packer, unpacker, after_pack=None):
         dist = self.dist
         send_sizes = torch.tensor(sizes.astype(np.int64), device=self.device)
         recv_sizes = torch.empty_like(send_sizes)
@@ -132,11 +135,16 @@ class DistShard:
         rs = [int(x) for x in recv_sizes.tolist()]
         ss = [int(x) for x in sizes.tolist()]
         send = self.s.pack(sizes, packer)
+        if after_pack is not None:
+            after_pack()  # device work on the engine stream that overlaps the collective
         recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
         # every rank runs the same number of calls: ceil(largest per-peer segment / CHUNK)
         mx = torch.tensor([max(ss + rs + [0])], dtype=torch.int64, device=self.device)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
         calls = (int(mx.item()) + self.CHUNK - 1) // self.CHUNK
+        if calls == 1:
+            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+            calls = 0
         soff = np.concatenate([[0], np.cumsum(ss)])
         roff = np.concatenate([[0], np.cumsum(rs)])
         for c in range(calls):
@@ -161,7 +169,7 @@ class DistShard:
             e.round_send()
             self._exchange(e.outbox_bytes(), e.outbox_pack, e.inbox_unpack)
             e.round_merge()
-            self._exchange(e.ae_bytes(), e.ae_pack, e.ae_merge)
+            self._exchange(e.ae_bytes(), e.ae_pack, e.ae_merge, after_pack=e.ae_merge_local)
             e.round_end()
 
     def stats(self) -> dict:

@@ -263,11 +263,45 @@ static void test_get_broadcasts() {
   So(state.Get("docker3", "feedface")->Status == sidecar::TOMBSTONE);
 }
 
+// Test_GetBroadcasts "Many runs with leftovers" (services_delegate_test.go:88-103) with the
+// reference's byte limits: the fixture messages are 225 / 225 / 214 bytes long.
+static void test_get_broadcasts_bytes() {
+  Cluster c(params());
+  ServicesState state(c, local);
+  ServicesDelegate delegate(c, state);
+  const int64_t t46 = 1425431566669648453ll, t32 = 1425431552630357657ll;
+  // 225 = static + len("\"2015-03-04T01:12:46.669648453Z\"") 32 + len("0") 1
+  c.SetStaticBytes("docker2", "d419fa7ad1a7", 225 - 33);
+  c.SetStaticBytes("docker2", "deadbeefabba", 225 - 33);
+  c.SetStaticBytes("docker1", "1b3295bf300f", 214 - 33);
+  std::vector<Service> bCast{{"d419fa7ad1a7", "docker2", t46, sidecar::ALIVE},
+                             {"deadbeefabba", "docker2", t46, sidecar::ALIVE}};
+  std::vector<Service> bCast2{{"1b3295bf300f", "docker1", t32, sidecar::ALIVE},
+                              {"deadbeefabba", "docker2", t46, sidecar::ALIVE}};
+  cur = "pendingBroadcasts = bCast (nothing fits in 3/100)";
+  state.SendServices(bCast, 1);
+  So(delegate.GetBroadcasts(3, 100).empty());
+  cur = "channel <- bCast2 ++ bCast; 3/100 sends nothing";
+  std::vector<Service> both = bCast2;
+  both.insert(both.end(), bCast.begin(), bCast.end());
+  state.SendServices(both, 1);
+  So(delegate.GetBroadcasts(3, 100).empty());
+  cur = "3/300: one message fits";
+  auto one = delegate.GetBroadcasts(3, 300);
+  So(one.size() == 1 && one[0] == bCast2[0]);
+  So(delegate.GetBroadcasts(3, 100).empty());
+  cur = "3/1398: the other five";
+  auto five = delegate.GetBroadcasts(3, 1398);
+  So(five.size() == 5 && five[0] == bCast2[1] && five[1] == bCast[0] && five[2] == bCast[1]);
+  So(delegate.GetBroadcasts(3, 1398).empty());
+}
+
 int main() {
   test_services_state_with_data();
   test_tracking_and_broadcasting();
   test_cluster_membership();
   test_get_broadcasts();
+  test_get_broadcasts_bytes();
   std::printf("backend=%s checks=%d failures=%d\n", gx_backend(), checks, failures);
   return failures ? 1 : 0;
 }

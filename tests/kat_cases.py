@@ -421,6 +421,142 @@ def kat_getbroadcasts_many_runs(lib):
     assert e.pending(LOCAL) == []
 
 
+# ---- the same delegate tests with packPacket's byte limit computed by the engine
+def go_rfc3339nano(ts):
+    """time.Time.UTC().Format(time.RFC3339Nano) for the parity tests, independent of the engine."""
+    sec, frac = divmod(int(ts), SEC)
+    s = _dt.datetime.fromtimestamp(sec, tz=_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%S")
+    if frac:
+        s += "." + f"{frac:09d}".rstrip("0")
+    return s + "Z"
+
+
+def _fixture_static(doc):
+    """len(doc) minus the bytes of its Updated value (quoted) and its Status digits."""
+    upd = doc.split('"Updated":', 1)[1].split(",", 1)[0]
+    status = doc.rsplit('"Status":', 1)[1].rstrip("}")
+    return len(doc) - len(upd) - len(status)
+
+
+def _delegate_bytes(lib):
+    e = _delegate(lib)
+    tbl = {(DOCKER2, 0): _FIX["d419"], (DOCKER2, 1): _FIX["dead"], (DOCKER1, 0): _FIX["1b32"]}
+    for host in (DOCKER1, DOCKER2):
+        row = [0] * e.S
+        for (h, j), doc in tbl.items():
+            if h == host:
+                row[j] = _fixture_static(doc)
+        e.set_static_bytes(host, host + 1, row)
+    # the engine's len(svc.Encode()) reproduces the fixture lengths 225 / 225 / 214
+    assert e.message_bytes(BCAST + BCAST2[:1]) == [len(_FIX["d419"]), len(_FIX["dead"]), len(_FIX["1b32"])]
+    return e
+
+
+def kat_message_bytes_rfc3339nano(lib):
+    """service_ffjson.go:370-436 — Updated is encoded by time.Time.MarshalJSON (RFC3339Nano, UTC,
+    trailing fractional zeros trimmed); Status in decimal. Static bytes 0 isolate those two."""
+    e = mk(lib)
+    e.set_static_bytes(0, e.H, [0] * (e.H * e.S))
+    ts = [T0, T0 + 1, T0 + 10, T0 + 50, T0 + 100, T0 + 120_000_000, T0 + 999_999_999, T0 + SEC,
+          _T46, _T32, _T46 + 50, _T46 + 4 * 50, 0, 1, 86_399 * SEC + 500_000_000, 2**60 + 12345,
+          T0 - 3 * HOUR - MIN, T0 + 1_000_000]
+    import random as _r
+    rnd = _r.Random(7)
+    ts += [rnd.randrange(0, 2**61) for _ in range(200)]
+    ts += [rnd.randrange(0, 2**50) * 10 ** rnd.randrange(0, 10) % 2**61 for _ in range(200)]
+    st = [ALIVE, TOMBSTONE, UNHEALTHY, UNKNOWN, DRAINING]
+    recs = [(i % e.H, i % e.S, t, st[i % 5]) for i, t in enumerate(ts)]
+    want = [len('"' + go_rfc3339nano(t) + '"') + len(str(s_)) for (_, _, t, s_) in recs]
+    assert e.message_bytes(recs) == want
+
+
+def kat_getbroadcasts_bytes_nothing(lib):
+    """services_delegate_test.go:41-43 — GetBroadcasts(3, 1398) is nil when there is nothing to send."""
+    e = _delegate_bytes(lib)
+    assert e.get_broadcasts_bytes(LOCAL, 3, 1398) is None
+
+
+def kat_getbroadcasts_bytes_pending_only(lib):
+    """services_delegate_test.go:45-52 — returns from the pending list when nothing is new."""
+    e = _delegate_bytes(lib)
+    _set_pending(e, LOCAL, [BCAST[0]])
+    r = e.get_broadcasts_bytes(LOCAL, 3, 1398)
+    assert [tup(x) for x in r] == [BCAST[0]] and e.pending(LOCAL) == []
+
+
+def kat_getbroadcasts_bytes_channel(lib):
+    """services_delegate_test.go:54-63 — returns what's in the channel (2 x 225 B fit in 1398)."""
+    e = _delegate_bytes(lib)
+    e.send_services(LOCAL, BCAST, 1)
+    r = e.get_broadcasts_bytes(LOCAL, 3, 1398)
+    assert [tup(x) for x in r] == BCAST and e.pending(LOCAL) == []
+    assert e.stats()["bytes_sent"] == 2 * (225 + 3)
+
+
+def kat_getbroadcasts_bytes_leftover(lib):
+    """services_delegate_test.go:65-73 — returns what's left when nothing is new."""
+    e = _delegate_bytes(lib)
+    _set_pending(e, LOCAL, BCAST)
+    r = e.get_broadcasts_bytes(LOCAL, 3, 1398)
+    assert [tup(x) for x in r] == BCAST and e.pending(LOCAL) == []
+
+
+def kat_getbroadcasts_bytes_new_and_left(lib):
+    """services_delegate_test.go:75-86 — what's new first, then what's left, when it fits."""
+    e = _delegate_bytes(lib)
+    _set_pending(e, LOCAL, BCAST)
+    e.send_services(LOCAL, BCAST2, 1)
+    r = e.get_broadcasts_bytes(LOCAL, 3, 1398)
+    assert [tup(x) for x in r] == BCAST2 + BCAST and e.pending(LOCAL) == []
+
+
+def kat_getbroadcasts_bytes_many_runs(lib):
+    """services_delegate_test.go:88-103 — GetBroadcasts(3,100) nil, (3,300) one message (214+3),
+    (3,100) nil, (3,1398) the other five: bCast2[1:] ++ bCast ++ bCast... as listed there."""
+    e = _delegate_bytes(lib)
+    _set_pending(e, LOCAL, BCAST)
+    e.send_services(LOCAL, BCAST2 + BCAST, 1)
+    assert e.get_broadcasts_bytes(LOCAL, 3, 100) is None
+    r = e.get_broadcasts_bytes(LOCAL, 3, 300)  # 1 message fits here
+    assert [tup(x) for x in r] == [BCAST2[0]]
+    assert e.get_broadcasts_bytes(LOCAL, 3, 100) is None
+    r = e.get_broadcasts_bytes(LOCAL, 3, 1398)
+    assert len(r) == 5
+    assert [tup(x) for x in r][:3] == BCAST2[1:] + BCAST
+    assert e.pending(LOCAL) == []
+    st = e.stats()
+    assert st["bytes_sent"] == (214 + 3) + 5 * (225 + 3) and st["cap_cuts"] == 0
+
+
+def kat_getbroadcasts_bytes_exact_fit(lib):
+    """packPacket's test is total + len + overhead > limit (services_delegate.go:195): a message
+    ending exactly at the limit fits, one byte less does not."""
+    e = _delegate_bytes(lib)
+    e.send_services(LOCAL, BCAST, 1)
+    assert [tup(x) for x in e.get_broadcasts_bytes(LOCAL, 3, 2 * 228 - 1)] == [BCAST[0]]
+    assert [tup(x) for x in e.get_broadcasts_bytes(LOCAL, 3, 228)] == [BCAST[1]]
+    e.send_services(LOCAL, BCAST, 1)
+    assert e.get_broadcasts_bytes(LOCAL, 3, 227) is None
+    assert [tup(x) for x in e.pending(LOCAL)] == BCAST
+
+
+def kat_getbroadcasts_bytes_pass_length(lib):
+    """Each SendServices pass adds 50 ns (services_state.go:599), which changes the encoded length
+    ("...453Z" -> "...503Z" -> "...553Z" keeps 9 digits; a fraction ending in zeros is shorter)."""
+    e = _delegate_bytes(lib)
+    t = _T46 - 453 + 400  # fraction .6696484 (7 digits), then .66964845 (8), then .6696485 (7)
+    e.send_services(LOCAL, [(DOCKER2, 0, t, ALIVE)], 3)  # retransmit_rounds = 0: passes back to back
+    sent = []
+    for p in range(3):
+        r = e.get_broadcasts_bytes(LOCAL, 0, 1398)
+        assert [tup(x) for x in r] == [(DOCKER2, 0, t + 50 * p, ALIVE)]
+        sent.append(e.stats()["bytes_sent"])
+    lens = [sent[0], sent[1] - sent[0], sent[2] - sent[1]]
+    static = _fixture_static(_FIX["d419"])
+    assert lens == [static + len('"' + go_rfc3339nano(t + 50 * p) + '"') + 1 for p in range(3)]
+    assert lens == [223, 224, 223]
+
+
 # --------------------------------------------------------------- round-model semantic pins
 def kat_order_dependence(lib):
     """SURVEY.md §7 hard part: the merge is not a semilattice. old=(t1,DRAINING):

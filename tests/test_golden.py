@@ -16,7 +16,10 @@ def check(lib, name):
     kw, rounds = CASES[name]
     assert json.loads(str(ref["params"])) == kw and int(ref["rounds"]) == rounds
     got = run(lib, kw, rounds)
-    assert json.loads(got["stats"]) == json.loads(str(ref["stats"]))
+    got_stats, ref_stats = json.loads(got["stats"]), json.loads(str(ref["stats"]))
+    # counters added after the fixtures were made (byte-limit packing) are zero in record mode
+    assert {k: v for k, v in got_stats.items() if k not in ref_stats} == {"bytes_sent": 0, "cap_cuts": 0}
+    assert {k: got_stats[k] for k in ref_stats} == ref_stats
     assert np.array_equal(got["views"], ref["views"])
     assert np.array_equal(got["hosts"], ref["hosts"])
     assert np.array_equal(got["digests"], ref["digests"])

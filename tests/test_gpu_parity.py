@@ -52,6 +52,25 @@ def test_round_model_parity(oracle_lib, gx_lib, name):
     assert g.converged() == o.converged()
 
 
+@pytest.mark.parametrize("limit", [1398, 600, 230])
+def test_byte_limit_parity(oracle_lib, gx_lib, limit):
+    """packPacket under memberlist's byte limit: a random static-length table
+    (ID/Name/Image/Hostname/Ports sizes differ per service) and the round model with churn."""
+    kw = dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, limit_bytes=limit, overhead_bytes=3,
+              ae_period_rounds=10, churn_ppm=50000, aged_ppm=20000, queue_cap=2048)
+    g, o = pair(oracle_lib, gx_lib, **kw)
+    rnd = np.random.default_rng(limit)
+    tbl = rnd.integers(120, 420, size=64 * 8).astype(np.uint16)
+    g.set_static_bytes(0, 64, tbl)
+    o.set_static_bytes(0, 64, tbl)
+    for chunk in (1, 9, 20, 50):
+        g.run_rounds(chunk)
+        o.run_rounds(chunk)
+        assert_same(g, o, f"bytes {limit} round {g.round}")
+    st = g.stats()
+    assert st["bytes_sent"] > 0 and st["cap_cuts"] == 0
+
+
 def test_cfg2_small_parity(oracle_lib, gx_lib):
     """A 1024 x 16 cluster with anti-entropy, churn and expiry-age records."""
     kw = dict(n_hosts=1024, n_services=16, init_mode=INIT_OWN, ae_period_rounds=10, churn_ppm=20000,
