@@ -155,7 +155,8 @@ static int round_send_impl(gx_engine *e) {
   }
   if (d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2) {
     LaunchTimer t(e, GX_K_STORM);
-    k_storm<<<d.Hl, 256, 0, s>>>(d);
+    if (d.S >= 2 && 64 % d.S == 0) k_storm_p2<<<d.Hl, 256, 0, s>>>(d);
+    else k_storm<<<d.Hl, 256, 0, s>>>(d);
   }
   {
     LaunchTimer t(e, GX_K_SEND);
@@ -212,6 +213,8 @@ static int ae_whole_impl(gx_engine *e) {
     }
     if (np) {
       LaunchTimer t(e, GX_K_AE);
+      // PF = 1, default cache policy: deeper prefetch and nt loads measured within noise
+      // (profiles/ae_variants.sh)
       if (vec) k_ae<true><<<np, 256, 0, s>>>(d, key0, key1);
       else k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
     }

@@ -343,6 +343,106 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   }
 }
 
+// Storm for S | 64 (S >= 2): a wave's 128-word chunk holds 128/S whole owners, so the presence
+// masks and liveness come from ballots (no LDS atomics); each owner's first lane emits its
+// EXPIRE job. Rows stream with 16-B loads, the next 1024 words in flight while this tile is
+// folded; one barrier per tile orders the jobs (per-chunk counts, double-buffered).
+GXD uint64_t spread32(uint64_t x) {  // bit i -> bit 2i
+  x &= 0xffffffffull;
+  x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+  x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+  x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+__global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
+  __shared__ uint32_t s_cnt[2][8];
+  uint32_t vi = blockIdx.x, v = d.lo + vi;
+  uint32_t half = d.H / 2;
+  uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
+  gx_host_state *h = &d.hs[vi];
+  uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
+  uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  uint32_t jobs = 0;
+  unsigned long long c_wr = 0;
+  const uint64_t tomb = pack(d.now, GX_TOMBSTONE);
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t LPO = d.S / 2;                      // lanes per owner
+  const uint64_t omask = LPO == 32 ? 0xffffffffull : ((1ull << LPO) - 1);
+  const bool leader = lane % LPO == 0;
+  uint64_t *row = &d.view[(size_t)vi * d.R + (size_t)lo * d.S];
+  const uint32_t nw = (hi - lo) * d.S;
+  ulonglong2 q[2];
+  auto load = [&](uint32_t base) {
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      uint32_t r0 = base + 512 * c + 2 * t;
+      q[c] = r0 < nw ? *reinterpret_cast<const ulonglong2 *>(&row[r0])
+                     : make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+    }
+  };
+  load(0);
+  uint32_t it = 0;
+  for (uint32_t base = 0; base < nw; base += 1024, it ^= 1) {
+    ulonglong2 w[2] = {q[0], q[1]};
+    if (base + 1024 < nw) load(base + 1024);
+    bool lead_live[2];
+    uint64_t pmask[2];
+    uint32_t rank[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      bool p0 = st_of(w[c].x) != GX_ABSENT, p1 = st_of(w[c].y) != GX_ABSENT;
+      bool l0 = p0 && st_of(w[c].x) != GX_TOMBSTONE, l1 = p1 && st_of(w[c].y) != GX_TOMBSTONE;
+      uint64_t b0 = __ballot(p0), b1 = __ballot(p1), bl = __ballot(l0 || l1);
+      uint32_t sh = lane - lane % LPO;  // first lane of this lane's owner
+      bool live = ((bl >> sh) & omask) != 0;
+      pmask[c] = spread32((b0 >> sh) & omask) | (spread32((b1 >> sh) & omask) << 1);
+      uint64_t n0 = (p0 && live) ? tomb : w[c].x, n1 = (p1 && live) ? tomb : w[c].y;
+      bool ch0 = n0 != w[c].x, ch1 = n1 != w[c].y;
+      if (ch0 || ch1) *reinterpret_cast<ulonglong2 *>(&row[base + 512 * c + 2 * t]) = make_ulonglong2(n0, n1);
+      c_wr += ch0 + ch1;
+      lead_live[c] = leader && live;
+      uint64_t bj = __ballot(lead_live[c]);
+      rank[c] = (uint32_t)__popcll(bj & ((1ull << lane) - 1));
+      if (lane == 0) s_cnt[it][4 * c + wv] = (uint32_t)__popcll(bj);
+    }
+    __syncthreads();
+    uint32_t pre[2] = {0, 0}, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      uint32_t x = s_cnt[it][k];
+      if (k < (int)wv) pre[0] += x;
+      if (k < 4 + (int)wv) pre[1] += x;
+      tot += x;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      uint32_t pos = jobs + pre[c] + rank[c];
+      if (lead_live[c] && pos < room) {
+        uint32_t o = lo + (base + 512 * c + 2 * t) / d.S;
+        d.fifo[(size_t)vi * d.Q + ((tail0 + pos) % d.Q)] =
+            make_job((uint64_t)d.now, pmask[c], o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
+      }
+    }
+    jobs += tot;
+  }
+  bool changed = c_wr != 0;
+  if (__ballot(changed) != 0 && lane == 0) {
+    mark_change(d);
+    atomicMin(&d.minexp[vi], exp_time(d.p, tomb));
+  }
+  c_wr = wave_sum(c_wr);
+  if (lane == 0) kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
+  if (t == 0) {
+    uint32_t ok = jobs < room ? jobs : room;
+    h->fifo_tail = tail0 + ok;
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
+    ctr_atomic(d, C_EXPSRV, jobs);
+    ctr_atomic(d, C_QDROP, jobs - ok);
+  }
+}
+
 // ========================================================================= phase 3: gossip send ==
 // memberlist kRandomNodes restated as a seeded sampler: k distinct peers != u on u's side.
 GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
@@ -587,9 +687,20 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
 // Dense view-pair merge: a <- b and, when `both`, b <- a's pre-exchange words. VEC streams both
 // rows with 16-B loads, 4 slots per thread per 1024-slot tile, and compacts each side's
 // retransmits in key order with one packed block scan per tile.
-template <bool VEC>
+template <bool NT>
+GXD ulonglong2 ld16(const uint64_t *p) {
+  if (NT) {
+    typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+    v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(p));
+    return make_ulonglong2(x.x, x.y);
+  }
+  return *reinterpret_cast<const ulonglong2 *>(p);
+}
+
 // `ext` (when both = false): B is another shard's received row of host b (read-only); the pair's
-// exchange is counted where a is the pair's first member (count_ex).
+// exchange is counted where a is the pair's first member (count_ex). PF = tiles whose loads are in
+// flight while one is merged (software pipeline depth); NT = non-temporal loads (read-once rows).
+template <bool VEC, int PF = 1, bool NT = false>
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
                  unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false) {
   uint64_t *A = vrow(d, a);
@@ -601,39 +712,33 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t na = 0, nb = 0;
   unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
-  // Software pipeline: the next 1024-slot tile's loads are in flight while this tile is merged,
-  // written back and (only if something was accepted) compacted.
-  uint64_t qa[4], qb[4];
-  auto load_tile = [&](uint32_t base) {
+  const uint32_t TILE = 4 * blockDim.x;
+  // Software pipeline: the next PF 1024-slot tiles' loads are in flight while this tile is
+  // merged, written back and (only if something was accepted) compacted.
+  uint64_t qa[PF][4], qb[PF][4];
+  auto load_tile = [&](uint32_t base, uint64_t *xa, uint64_t *xb) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
       bool v0 = r0 < d.R, v1 = r0 + 1 < d.R;
       if (VEC && v0) {
-        ulonglong2 pa = *reinterpret_cast<const ulonglong2 *>(&A[r0]);
-        ulonglong2 pb = *reinterpret_cast<const ulonglong2 *>(&B[r0]);
-        qa[2 * h] = pa.x;
-        qa[2 * h + 1] = pa.y;
-        qb[2 * h] = pb.x;
-        qb[2 * h + 1] = pb.y;
+        ulonglong2 pa = ld16<NT>(&A[r0]);
+        ulonglong2 pb = ld16<NT>(&B[r0]);
+        xa[2 * h] = pa.x;
+        xa[2 * h + 1] = pa.y;
+        xb[2 * h] = pb.x;
+        xb[2 * h + 1] = pb.y;
       } else {
-        qa[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
-        qa[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
-        qb[2 * h] = v0 ? B[r0] : GX_SLOT_ABSENT;
-        qb[2 * h + 1] = v1 ? B[r0 + 1] : GX_SLOT_ABSENT;
+        xa[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
+        xa[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
+        xb[2 * h] = v0 ? B[r0] : GX_SLOT_ABSENT;
+        xb[2 * h + 1] = v1 ? B[r0 + 1] : GX_SLOT_ABSENT;
       }
     }
   };
-  load_tile(0);
-  for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
-    uint64_t wa[4], wb[4], nwa[4], nwb[4];
+  auto merge_tile = [&](uint32_t base, const uint64_t *wa, const uint64_t *wb) {
+    uint64_t nwa[4], nwb[4];
     bool fa[4], fb[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      wa[k] = qa[k];
-      wb[k] = qb[k];
-    }
-    if (base + 4 * blockDim.x < d.R) load_tile(base + 4 * blockDim.x);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
@@ -688,7 +793,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     unsigned long long cnt = (unsigned long long)(fa[0] + fa[1]) | ((unsigned long long)(fa[2] + fa[3]) << 16) |
                              ((unsigned long long)(fb[0] + fb[1]) << 32) | ((unsigned long long)(fb[2] + fb[3]) << 48);
-    if (!__syncthreads_or(cnt != 0)) continue;  // nothing accepted in this tile: no retransmits
+    if (!__syncthreads_or(cnt != 0)) return;  // nothing accepted in this tile: no retransmits
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
     uint32_t pa[4], pb[4];
@@ -710,6 +815,25 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     na += fld(tot, 0) + fld(tot, 1);
     nb += fld(tot, 2) + fld(tot, 3);
+  };
+#pragma unroll
+  for (int s = 0; s < PF; s++)
+    if (s * TILE < d.R) load_tile(s * TILE, qa[s], qb[s]);
+  for (uint32_t base = 0; base < d.R; base += PF * TILE) {
+#pragma unroll
+    for (int s = 0; s < PF; s++) {
+      uint32_t bs = base + s * TILE;
+      if (bs < d.R) {
+        uint64_t wa[4], wb[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          wa[k] = qa[s][k];
+          wb[k] = qb[s][k];
+        }
+        if (bs + PF * TILE < d.R) load_tile(bs + PF * TILE, qa[s], qb[s]);
+        merge_tile(bs, wa, wb);
+      }
+    }
   }
   ma = block_min(ma, s_red);
   mb = block_min(mb, s_red);
@@ -734,7 +858,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   }
 }
 
-template <bool VEC>
+template <bool VEC, int PF = 1, bool NT = false>
 __global__ __launch_bounds__(256) void k_ae(Dev d, uint64_t key0, uint64_t key1) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
@@ -753,7 +877,7 @@ __global__ __launch_bounds__(256) void k_ae(Dev d, uint64_t key0, uint64_t key1)
   }
   uint32_t a = base + feistel_perm(key, 2 * q, m);
   uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
-  ae_pair<VEC>(d, a, b, true, s_wave, s_red);
+  ae_pair<VEC, PF, NT>(d, a, b, true, s_wave, s_red);
 }
 
 template <bool VEC>

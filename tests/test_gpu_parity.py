@@ -31,6 +31,15 @@ SCENARIOS = {
                                gossip_stop_on_empty=0, fanout=4),
     "tiny_h2": dict(n_hosts=2, n_services=2, init_mode=INIT_OWN, ae_period_rounds=3),
     "h1": dict(n_hosts=1, n_services=4, init_mode=INIT_EMPTY),
+    # ExpireServer storm at every S class: ballot kernel (S | 64) and the generic LDS kernel
+    "storm_s2": dict(n_hosts=130, n_services=2, init_mode=INIT_WARM, partition_start=0, partition_end=12,
+                     storm_round=3, queue_cap=512, churn_ppm=50000),
+    "storm_s3": dict(n_hosts=90, n_services=3, init_mode=INIT_WARM, partition_start=0, partition_end=12,
+                     storm_round=2, queue_cap=256, ae_period_rounds=5),
+    "storm_s64": dict(n_hosts=70, n_services=64, init_mode=INIT_WARM, partition_start=0, partition_end=12,
+                      storm_round=4, queue_cap=64, churn_ppm=100000),
+    "storm_s16_qfull": dict(n_hosts=300, n_services=16, init_mode=INIT_WARM, partition_start=0,
+                            partition_end=12, storm_round=1, queue_cap=40),
     "high_fanout": dict(n_hosts=20, n_services=4, init_mode=INIT_OWN, fanout=16, packet_cap=8),
 }
 
