@@ -72,7 +72,7 @@ struct Dev {
   uint32_t *in_cnt;    // [H+1] receiver counts, then exclusive offsets
   uint32_t *in_cur;    // [H] fill cursors
   uint32_t *in_fill;   // [H*K] entries in arrival order (atomic fill)
-  uint32_t *in_sorted; // [H*K] entries sender-ordered per receiver
+  uint2 *in_sorted;    // [H*K] (entry, length) sender-ordered per receiver
   grec *scan_list;     // [H][L] first L expired records of this round's scan
   uint32_t *scan_cnt;  // [H]
   uint8_t *tick;       // [H] BroadcastTombstones tick this round
@@ -273,28 +273,6 @@ GXD uint32_t job_len(const Dev &d, const gx_job &j) {
   return 0;
 }
 
-// Record i of pass `pass` of a job: Updated + pass * 50ns (services_state.go:588-599).
-GXD grec job_rec(const Dev &d, uint32_t v, const gx_job &j, uint32_t i, uint32_t &bit_cursor) {
-  uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff;
-  uint64_t dw = ((uint64_t)pass * (uint64_t)d.p.pass_increment_ns) << GX_TS_SHIFT;
-  grec g;
-  g.pad = 0;
-  if (kind == GX_JOB_RETX) {
-    g.w = j.a;
-    g.r = j.c;
-  } else if (kind == GX_JOB_SEND) {
-    grec s = list_ptr(d, v, j.c & 0xffff)[i];
-    g.w = s.w + dw;
-    g.r = s.r;
-  } else {  // EXPIRE: i-th set bit of the mask, walked with a cursor
-    uint64_t m = j.b >> bit_cursor;
-    uint32_t s = bit_cursor + (uint32_t)__builtin_ctzll(m);
-    bit_cursor = s + 1;
-    g.w = pack((int64_t)j.a, GX_TOMBSTONE) + dw;
-    g.r = j.c * d.S + s;
-  }
-  return g;
-}
 
 // GetBroadcasts(overhead, limit) + packPacket (services_delegate.go:85-144, :186-223).
 // ---------------------------------------------------------- encoded message length (f-1) --
@@ -318,77 +296,172 @@ GXD uint32_t msg_bytes(const Dev &d, const grec &g) {
   return d.sbytes[g.r] + json_time_len(ts_of(g.w)) + dec_len((uint32_t)st_of(g.w));
 }
 
-// GetBroadcasts (services_delegate.go:85-144). limit = record budget (the packet buffer);
-// limit_bytes > 0 adds packPacket's byte budget with per-message overhead.
-GXD uint32_t get_broadcasts(const Dev &d, Acc &a, uint32_t v, uint32_t limit, grec *packet,
-                            uint32_t limit_bytes = 0, uint32_t overhead = 0) {
-  gx_host_state *h = hst(d, v);
-  uint32_t m = 0;
-  uint32_t mask = d.DQ - 1;
+// Position of the n-th (0-based) set bit of m (n < popcount(m)).
+GXD uint32_t nth_set_bit(uint64_t m, uint32_t n) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    uint64_t low = m & ((1ull << w) - 1);
+    uint32_t c = (uint32_t)__popcll(low);
+    if (n >= c) {
+      n -= c;
+      m >>= w;
+      pos += w;
+    } else {
+      m = low;
+    }
+  }
+  return pos;
+}
+// Inclusive scan over the T lanes of a team (tl = lane within the team).
+template <int T>
+GXD uint32_t team_incl_scan(uint32_t x, uint32_t tl) {
+#pragma unroll
+  for (int o = 1; o < T; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, T);
+    if ((int)tl >= o) x += y;
+  }
+  return x;
+}
+
+// The FIFO pushes of one host, on its register copy `hs` (the whole wave holds the same copy;
+// lane 0 stores).
+GXD void free_list_r(gx_host_state &hs, const gx_job &j) {
+  if ((j.meta & 0xff) == GX_JOB_SEND) hs.arena_used &= ~(1u << (j.c & 0xffff));
+}
+GXD void push_job_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const gx_job &j, bool lane0) {
+  uint32_t count = hs.fifo_tail - hs.fifo_head;
+  bool nil = (j.meta & 0xff) <= GX_JOB_NIL_BT;
+  if (count >= (nil ? d.Q : d.Q - 2)) {
+    if (lane0) a.c[C_QDROP]++;
+    free_list_r(hs, j);
+    return;
+  }
+  if (lane0) d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_tail % d.Q)] = j;
+  hs.fifo_tail++;
+}
+GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const gx_job &j, bool lane0) {
+  if (hs.sleep_tail - hs.sleep_head >= d.SQ) {
+    if (lane0) a.c[C_SDROP]++;
+    free_list_r(hs, j);
+    return;
+  }
+  if (lane0) d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail % d.SQ)] = j;
+  hs.sleep_tail++;
+}
+
+// GetBroadcasts (services_delegate.go:85-144) with packPacket (:186-223) by a team of T lanes
+// per host: the control state is the team-uniform register copy `hs`, the records move
+// lane-parallel. broadcast = batch ++ pendingBroadcasts is read as a virtual sequence (batch
+// record i from the job, then the pending ring); only the batch records that stay pending are
+// written to the ring. limit = record budget (the packet buffer); limit_bytes > 0 adds the byte
+// budget + overhead. Every lane of the team calls it; ring writes are fenced before the next call.
+template <int T>
+GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, uint32_t limit,
+                                 grec *packet, uint32_t limit_bytes, uint32_t overhead) {
+  const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
+  const bool lane0 = tl == 0;
+  const uint32_t mask = d.DQ - 1;
   grec *dq = &d.dq[(size_t)li(d, v) * d.DQ];
-  if (h->fifo_head != h->fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
-    gx_job j = d.fifo[(size_t)li(d, v) * d.Q + (h->fifo_head % d.Q)];
-    h->fifo_head++;
-    a.c[C_DEQ]++;
+  gx_job j = make_job(0, 0, 0, 0);
+  uint32_t m = 0;
+  if (hs.fifo_head != hs.fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
+    j = d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_head % d.Q)];
+    hs.fifo_head++;
+    if (lane0) a.c[C_DEQ]++;
     m = job_len(d, j);
-    // broadcast = batch ++ pendingBroadcasts (:104-106): push the batch to the deque front
-    uint32_t head = (h->dq_head - m) & mask;
-    uint32_t cur = 0;
-    for (uint32_t i = 0; i < m; i++) dq[(head + i) & mask] = job_rec(d, v, j, i, cur);
-    h->dq_head = head;
-    h->dq_len += m;
     uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff, np = (j.meta >> 16) & 0xff;
     if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
-      a.c[C_NIL]++;
-      h->flags &= ~1u;
-      h->bs_next = d.round + d.p.alive_interval_rounds;
+      if (lane0) a.c[C_NIL]++;
+      hs.flags &= ~1u;
+      hs.bs_next = d.round + d.p.alive_interval_rounds;
     } else if (kind == GX_JOB_NIL_BT) {  // ... BroadcastTombstones (:628)
-      a.c[C_NIL]++;
-      h->flags &= ~2u;
-      h->bt_next = d.round + d.p.tombstone_interval_rounds;
+      if (lane0) a.c[C_NIL]++;
+      hs.flags &= ~2u;
+      hs.bt_next = d.round + d.p.tombstone_interval_rounds;
     } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
-      if (pass + 1 < np) {
-        j.meta = meta_of((int)kind, pass + 1, np);
+      if (pass + 1 < np) {  // the looper re-arms (services_state.go:585-601)
+        gx_job nj = j;
+        nj.meta = meta_of((int)kind, pass + 1, np);
         if (d.p.retransmit_rounds == 0) {
-          j.wake = (uint32_t)d.round;
-          push_job(d, a, v, j);
+          nj.wake = (uint32_t)d.round;
+          push_job_r(d, a, v, hs, nj, lane0);
         } else {
-          j.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
-          push_sleep(d, a, v, j);
+          nj.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
+          push_sleep_r(d, a, v, hs, nj, lane0);
         }
       } else {
-        free_list(d, v, j);
+        free_list_r(hs, j);  // the list is read below; nothing reallocates it in this call
       }
     }
-  } else if (h->dq_len == 0) {  // default: nothing pending (:96-98)
+  } else if (hs.dq_len == 0) {  // default: nothing pending (:96-98)
     return 0;
   }
+  const uint32_t head = hs.dq_head, n = m + hs.dq_len;
+  const uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff;
+  const uint64_t dw = ((uint64_t)pass * (uint64_t)d.p.pass_increment_ns) << GX_TS_SHIFT;
+  auto item = [&](uint32_t i) -> grec {  // element i of batch ++ pendingBroadcasts
+    grec g;
+    g.pad = 0;
+    if (i >= m) return dq[(head + (i - m)) & mask];
+    if (kind == GX_JOB_RETX) {
+      g.w = j.a;
+      g.r = j.c;
+    } else if (kind == GX_JOB_SEND) {  // Updated + pass * 50ns (services_state.go:588-599)
+      grec s = list_ptr(d, v, j.c & 0xffff)[i];
+      g.w = s.w + dw;
+      g.r = s.r;
+    } else {  // EXPIRE: the i-th tombstoned service of the owner
+      g.w = pack((int64_t)j.a, GX_TOMBSTONE) + dw;
+      g.r = j.c * d.S + nth_set_bit(j.b, i);
+    }
+    return g;
+  };
   // packPacket (:186-223): the greedy prefix within the limit
-  uint32_t n = h->dq_len < limit ? h->dq_len : limit;
-  uint32_t l = n;
+  const uint32_t nmax = n < limit ? n : limit;
+  uint32_t l = nmax;
   if (limit_bytes) {
     uint64_t total = 0;
-    for (l = 0; l < n; l++) {
-      uint32_t b = msg_bytes(d, dq[(h->dq_head + l) & mask]) + overhead;
-      if (total + b > limit_bytes) break;  // if total+len(message)+overhead > limit (:195)
-      total += b;
+    l = 0;
+    const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1);
+    for (uint32_t c0 = 0; c0 < nmax; c0 += T) {
+      uint32_t i = c0 + tl;
+      uint32_t b = i < nmax ? msg_bytes(d, item(i)) + overhead : 0;
+      uint32_t incl = team_incl_scan<T>(b, tl);
+      bool fits = i < nmax && total + incl <= limit_bytes;  // total+len(message)+overhead > limit (:195)
+      // prefix sums rise, so the fitting lanes are a prefix of the team
+      uint32_t k = (uint32_t)__popcll((__ballot(fits) >> (tw * T)) & tmask);
+      if (k) total += __shfl(incl, (int)k - 1, T);
+      l += k;
+      uint32_t chunk = nmax - c0 < T ? nmax - c0 : T;
+      if (k < chunk) break;
     }
-    if (l == n && n < h->dq_len &&
-        total + msg_bytes(d, dq[(h->dq_head + n) & mask]) + overhead <= limit_bytes)
-      a.c[C_CAPCUT]++;
-    a.c[C_BYTESENT] += (unsigned)total;
+    if (lane0) {
+      if (l == nmax && nmax < n && total + msg_bytes(d, item(nmax)) + overhead <= limit_bytes) a.c[C_CAPCUT]++;
+      a.c[C_BYTESENT] += (unsigned)total;
+    }
   }
-  for (uint32_t i = 0; i < l; i++) packet[i] = dq[(h->dq_head + i) & mask];
-  h->dq_head = (h->dq_head + l) & mask;
-  h->dq_len -= l;
-  if (h->dq_len > d.p.pending_cap) {  // pendingBroadcasts = leftover[:MAX_PENDING_LENGTH]
-    a.c[C_PDROP] += h->dq_len - d.p.pending_cap;
-    h->dq_len = d.p.pending_cap;
+  for (uint32_t i = tl; i < l; i += T) packet[i] = item(i);
+  // leftover = broadcast[l:]; batch records that stay pending go in front of the old head
+  uint32_t nh;
+  if (l < m) {
+    uint32_t k = m - l;
+    nh = (head - k) & mask;
+    for (uint32_t i = tl; i < k; i += T) dq[(nh + i) & mask] = item(l + i);
+  } else {
+    nh = (head + (l - m)) & mask;
   }
-  if (l) {
+  hs.dq_head = nh;
+  hs.dq_len = n - l;
+  if (hs.dq_len > d.p.pending_cap) {  // pendingBroadcasts = leftover[:MAX_PENDING_LENGTH]
+    if (lane0) a.c[C_PDROP] += hs.dq_len - d.p.pending_cap;
+    hs.dq_len = d.p.pending_cap;
+  }
+  if (l && lane0) {
     a.c[C_PACKETS]++;
     a.c[C_RECSENT] += l;
   }
+  __threadfence_block();  // ring and FIFO stores are visible to the wave's next call
   return l;
 }
 

@@ -160,7 +160,8 @@ static int round_send_impl(gx_engine *e) {
   }
   {
     LaunchTimer t(e, GX_K_SEND);
-    k_send<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
+    // 4 lanes per host: measured best of 1/4/8/16/64 (profiles/send_team.sh)
+    k_send<4><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -182,7 +183,8 @@ static int round_merge_impl(gx_engine *e) {
       }
     }
     LaunchTimer t(e, GX_K_MERGE);
-    k_merge<<<d.Hl, 64, 0, s>>>(d);
+    if (d.R < (1u << 26)) k_merge<true><<<d.Hl, 64, 0, s>>>(d);  // 32-bit sort keys
+    else k_merge<false><<<d.Hl, 64, 0, s>>>(d);
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -388,7 +390,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.minexp, sizeof(unsigned long long) * H);
   ALLOC(d.in_cur, sizeof(uint32_t) * H);
   ALLOC(d.in_fill, sizeof(uint32_t) * Hg * K);
-  ALLOC(d.in_sorted, sizeof(uint32_t) * Hg * K);
+  ALLOC(d.in_sorted, sizeof(uint2) * Hg * K);
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
   ALLOC(d.tick, H);

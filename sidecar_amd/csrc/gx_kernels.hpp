@@ -470,28 +470,34 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
   return cnt;
 }
 
-// One thread per host: GetBroadcasts once per sampled peer, in order. Each packet is counted
-// into its receiver's CSR bucket.
+// A team of T lanes per host: GetBroadcasts once per sampled peer, in order
+// (get_broadcasts_team). Each packet is counted into its receiver's CSR bucket.
+template <int T>
 __global__ __launch_bounds__(256) void k_send(Dev d) {
   Acc a;
-  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T, lane = threadIdx.x & (T - 1);
   if (idx < d.Hl) {
     uint32_t u = d.lo + idx;
     uint32_t peers[16];
     uint32_t np = sample_peers(d, u, peers);
     uint32_t cap = d.p.packet_cap;
-    for (uint32_t j = 0; j < d.K; j++) {
+    for (uint32_t j = lane; j < d.K; j += T) {
       d.msg_len[(size_t)idx * d.K + j] = 0;
       d.msg_key[(size_t)idx * d.K + j] = u * d.K + j;
     }
+    gx_host_state *h = &d.hs[idx];
+    gx_host_state hs = *h;
     for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts(d, a, u, cap, &d.msg[((size_t)idx * d.K + j) * cap], d.p.limit_bytes,
-                                  d.p.overhead_bytes);
-      d.msg_len[(size_t)idx * d.K + j] = l;
-      d.msg_dst[(size_t)idx * d.K + j] = peers[j];
-      if (l && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
+      uint32_t l = get_broadcasts_team<T>(d, a, u, hs, cap, &d.msg[((size_t)idx * d.K + j) * cap], d.p.limit_bytes,
+                                       d.p.overhead_bytes);
+      if (lane == 0) {
+        d.msg_len[(size_t)idx * d.K + j] = l;
+        d.msg_dst[(size_t)idx * d.K + j] = peers[j];
+        if (l && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
+      }
       if (l == 0 && d.p.gossip_stop_on_empty) break;
     }
+    if (lane == 0) *h = hs;
   }
   acc_flush(d, a);
 }
@@ -556,108 +562,132 @@ __global__ void k_route_rank(Dev d) {
   uint32_t lo = d.in_cnt[dst], hi = d.in_cnt[dst + 1];
   uint32_t rank = 0;
   for (uint32_t x = lo; x < hi; x++) rank += d.msg_key[d.in_fill[x]] < key;
-  d.in_sorted[lo + rank] = e;
+  d.in_sorted[lo + rank] = make_uint2(e, d.msg_len[e]);
 }
 
 // ============================================================== phase 4: gather-then-merge ==
-// One wave per receiver. Its packets (sender order) are staged record by record in LDS; the first
-// occurrence of each key reads the view slot once, folds every occurrence in arrival order with
-// the AddServiceEntry rule, and writes the slot once. Accepted foreign records are compacted with
-// a wave ballot into the receiver's FIFO (retransmit), in arrival order.
-#define MERGE_TILE 256
+// One wave per receiver, one inbound record per lane per 64-record tile (its packets in sender
+// order). The tile's view slots are prefetched as soon as the keys are known; duplicate keys are
+// grouped by an in-register bitonic sort of (key, arrival lane), and each group folds its
+// occurrences in arrival order with the AddServiceEntry rule (one wave-uniform step per
+// occurrence of the longest group, usually 1). The group's first lane writes the slot once.
+// Accepted foreign records are compacted with a wave ballot into the receiver's FIFO
+// (retransmit), in arrival order.
+template <bool K32>
+GXD uint64_t bitonic64(uint64_t x, uint32_t lane) {  // ascending across the 64 lanes
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      uint64_t o;
+      if (K32) o = (uint32_t)__shfl_xor((uint32_t)x, (int)j, 64);
+      else o = __shfl_xor(x, (int)j, 64);
+      bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+      x = keep_min ? (o < x ? o : x) : (o > x ? o : x);
+    }
+  }
+  return x;
+}
+
+template <bool K32>
 __global__ __launch_bounds__(64) void k_merge(Dev d) {
-  __shared__ uint32_t s_key[MERGE_TILE];
-  __shared__ uint64_t s_val[MERGE_TILE];
-  __shared__ uint64_t s_acc[MERGE_TILE];
-  __shared__ uint8_t s_accf[MERGE_TILE];
   __shared__ uint32_t s_start[65];
   __shared__ uint32_t s_ent[64];
-  uint32_t vi = blockIdx.x, v = d.lo + vi;
-  uint32_t lane = threadIdx.x;
-  uint32_t off = d.in_cnt[vi], deg = d.in_cnt[vi + 1] - off;
+  __shared__ uint8_t s_accf[64];
+  __shared__ uint64_t s_accw[64];
+  const uint32_t vi = blockIdx.x, v = d.lo + vi;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t off = d.in_cnt[vi], deg = d.in_cnt[vi + 1] - off;
   if (deg == 0) return;
-  uint32_t cap = d.p.packet_cap;
+  const uint32_t cap = d.p.packet_cap;
   gx_host_state *h = &d.hs[vi];
-  uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
-  uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  const uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
+  const uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
   uint32_t n_retx = 0;
   unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, mexp = ~0ull;
   uint64_t *row = &d.view[(size_t)vi * d.R];
+  const uint32_t INV = K32 ? 0x3ffffffu : 0xffffffffu;  // sorts after every real key
   for (uint32_t c0 = 0; c0 < deg; c0 += 64) {
     uint32_t cn = deg - c0 < 64 ? deg - c0 : 64;
-    uint32_t ent = 0, len = 0;
-    if (lane < cn) {
-      ent = d.in_sorted[off + c0 + lane];
-      len = d.msg_len[ent];
-    }
-    uint32_t incl = len;
+    uint2 el = lane < cn ? d.in_sorted[off + c0 + lane] : make_uint2(0, 0);  // (entry, length)
+    uint32_t incl = el.y;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       uint32_t y = __shfl_up(incl, o, 64);
       if ((int)lane >= o) incl += y;
     }
     uint32_t total = __shfl(incl, 63, 64);
-    s_start[lane] = incl - len;
-    s_ent[lane] = ent;
-    if (lane == 0) s_start[64] = total;
+    s_start[lane] = incl - el.y;
+    s_ent[lane] = el.x;
     __syncthreads();
-    for (uint32_t t0 = 0; t0 < total; t0 += MERGE_TILE) {
-      uint32_t tn = total - t0 < MERGE_TILE ? total - t0 : MERGE_TILE;
-      for (uint32_t i = lane; i < tn; i += 64) {  // stage this tile's records (arrival order)
-        uint32_t gi = t0 + i;
-        uint32_t lo = 0, hi = cn - 1;  // last message with start <= gi
+    for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+      uint32_t i = t0 + lane;
+      bool valid = i < total;
+      uint32_t key = INV;
+      uint64_t val = 0, w0 = 0;
+      if (valid) {
+        uint32_t lo = 0, hi = cn - 1;  // last packet with start <= i
         while (lo < hi) {
           uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_start[mid] <= gi) lo = mid;
+          if (s_start[mid] <= i) lo = mid;
           else hi = mid - 1;
         }
-        grec g = d.msg[(size_t)s_ent[lo] * cap + (gi - s_start[lo])];
-        s_key[i] = g.r;
-        s_val[i] = g.w;
-        s_accf[i] = 0;
+        grec g = d.msg[(size_t)s_ent[lo] * cap + (i - s_start[lo])];
+        key = g.r;
+        val = g.w;
+        w0 = row[key];  // prefetch: in flight during the sort
       }
-      __syncthreads();
-      for (uint32_t i = lane; i < tn; i += 64) {  // fold each key's occurrences in arrival order
-        uint32_t key = s_key[i];
-        bool leader = true;
-        for (uint32_t j = 0; j < i; j++)
-          if (s_key[j] == key) {
-            leader = false;
-            break;
-          }
-        if (!leader) continue;
-        uint64_t w0 = row[key], w = w0;
+      c_merge += valid;
+      uint64_t sk = K32 ? (uint64_t)((key << 6) | lane) : (((uint64_t)key << 6) | lane);
+      sk = bitonic64<K32>(sk, lane);
+      const uint32_t src = (uint32_t)(sk & 63), skey = (uint32_t)(sk >> 6);
+      const bool vs = skey != INV;
+      const uint64_t sval = __shfl(val, (int)src, 64), sw0 = __shfl(w0, (int)src, 64);
+      uint32_t pkey = __shfl_up(skey, 1, 64);
+      const bool head = vs && (lane == 0 || pkey != skey);
+      const uint64_t heads = __ballot(head);
+      const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+      const uint32_t gs = 63 - (uint32_t)__clzll((heads & le) | 1ull);  // first lane of this group
+      const uint32_t kpos = lane - gs;
+      const uint64_t after = heads & ~le;
+      const uint32_t nvs = (uint32_t)__popcll(__ballot(vs));
+      const uint32_t glen = (after ? (uint32_t)__ffsll((long long)after) - 1 : nvs) - lane;  // heads only
+      uint32_t kmax = vs ? kpos : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        uint32_t y = __shfl_xor(kmax, o, 64);
+        kmax = y > kmax ? y : kmax;
+      }
+      uint64_t wg = sw0, wme = 0;
+      bool acc = false, stl = false;
+      for (uint32_t kk = 0; kk <= kmax; kk++) {  // occurrence kk of every group, arrival order
+        uint64_t wcur = __shfl(wg, (int)gs, 64);
+        if (vs && kpos == kk) wme = merge_word(d, wcur, sval, acc, stl);
+        uint64_t wn = __shfl(wme, (int)((gs + kk) & 63), 64);
+        if (head && kk < glen) wg = wn;
+      }
+      c_stale += stl;
+      c_acc += acc;
+      if (head) {
         c_rd++;
-        for (uint32_t j = i; j < tn; j++) {
-          if (s_key[j] != key) continue;
-          bool acc, st;
-          w = merge_word(d, w, s_val[j], acc, st);
-          c_stale += st;
-          if (acc) {
-            c_acc++;
-            s_accf[j] = 1;
-            s_acc[j] = w;
-          }
-        }
-        if (w != w0) {
-          row[key] = w;
+        if (wg != sw0) {
+          row[skey] = wg;
           c_wr++;
-          unsigned long long x = exp_time(d.p, w);
+          unsigned long long x = exp_time(d.p, wg);
           mexp = x < mexp ? x : mexp;
         }
       }
-      c_merge += (lane == 0) ? tn : 0;
+      s_accf[src] = vs && acc && (skey / d.S != v);
+      s_accw[src] = wme;
+      __threadfence_block();  // slot stores land before a later tile reads the same keys
       __syncthreads();
-      for (uint32_t b0 = 0; b0 < tn; b0 += 64) {  // ordered ballot compaction -> retransmit jobs
-        uint32_t i = b0 + lane;
-        bool f = i < tn && s_accf[i] && (s_key[i] / d.S != v);
-        unsigned long long m = __ballot(f);
-        uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (f && n_retx + pos < room)
-          d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
-              make_job(s_acc[i], 0, s_key[i], meta_of(GX_JOB_RETX, 0, 1));
-        n_retx += (uint32_t)__popcll(m);
-      }
-      __threadfence_block();
+      bool f = s_accf[lane];  // ordered ballot compaction -> retransmit jobs (arrival order)
+      unsigned long long m = __ballot(f);
+      uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (f && n_retx + pos < room)
+        d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
+            make_job(s_accw[lane], 0, key, meta_of(GX_JOB_RETX, 0, 1));
+      n_retx += (uint32_t)__popcll(m);
       __syncthreads();
     }
   }
@@ -1093,7 +1123,12 @@ __global__ void k_api_tomb(Dev d, uint32_t v, uint64_t running, uint64_t *out_ma
 __global__ void k_api_getb(Dev d, uint32_t v, uint32_t limit, grec *out, uint32_t *n_out, uint32_t limit_bytes,
                            uint32_t overhead) {
   Acc a;
-  if (threadIdx.x == 0) *n_out = get_broadcasts(d, a, v, limit, out, limit_bytes, overhead);
+  gx_host_state hs = *hst(d, v);
+  uint32_t l = get_broadcasts_team<64>(d, a, v, hs, limit, out, limit_bytes, overhead);
+  if (threadIdx.x == 0) {
+    *hst(d, v) = hs;
+    *n_out = l;
+  }
   acc_flush(d, a);
 }
 __global__ void k_api_msg_bytes(Dev d, const grec *recs, uint32_t n, uint32_t *out) {
