@@ -229,8 +229,12 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
  * entries. Wire formats (both little-endian):
  *   packet: u32 key (= sender * fanout + j), u32 receiver, u32 len, u32 0, then len x {u64 word,
  *           u32 record key, u32 0}; packets grouped by destination shard, ascending key.
- *   row:    u32 pair index, u32 host, u64 0, then R = H*S u64 words; rows grouped by destination
- *           shard, ascending pair index.
+ *   digest: u32 pair index, u32 host, u32 n_blocks, u32 0, then n_blocks x {u64 d0, u64 d1}: the
+ *           host's round-start row in blocks of GX_DIGEST_SLOTS slots (GX digest below); one
+ *           message per cross-shard push-pull pair, grouped by destination shard, ascending pair.
+ *   delta:  u32 pair index, u32 host, u32 n_sent, u32 0, then n_sent x GX_DIGEST_SLOTS u64 words:
+ *           the row's blocks whose digests differ from the partner's, ascending (the last block
+ *           of a row zero-padded); grouped like the digests.
  * gx_run_rounds(e, n) on an unsharded engine equals n x (round_send, round_merge, ae_merge with
  * nothing received, round_end). */
 int gx_round_send(gx_engine *e);  /* phases 0-3: wake, owner ticks, storm, GetBroadcasts */
@@ -238,12 +242,24 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes_per_shard);
 int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap);
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes);
 int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + received packets */
-int gx_ae_bytes(gx_engine *e, uint64_t *bytes_per_shard); /* 0s unless this is a push-pull round */
+/* Push-pull across shards exchanges block digests first and then only the blocks that differ
+ * (Dynamo-style anti-entropy). Views and every counter equal those of a full-row exchange: a
+ * block whose digests match merges the host's own copy, which is the same record set. Per AE
+ * round: gx_ae_bytes -> gx_ae_pack (digests) -> [gx_ae_merge_local] -> exchange ->
+ * gx_ae_delta_bytes (received digests) -> gx_ae_delta_pack -> exchange -> gx_ae_merge.
+ * Digest of block b = slots [b*512, min(R, (b+1)*512)) of a row, i = slot index in the row,
+ * w = slot word, mix(z) = SplitMix64 (z += 0x9E3779B97F4A7C15, then its two xor-shift-multiply
+ * steps and the final xor-shift), sums mod 2^64:
+ *   d0 = sum_i mix(w ^ (i * 0xD6E8FEB86659FD93)),  d1 = sum_i mix(w + i * 0xC2B2AE3D27D4EB4F + 0x165667B19E3779F9) */
+#define GX_DIGEST_SLOTS 512
+int gx_ae_bytes(gx_engine *e, uint64_t *bytes_per_shard); /* digest messages; 0s unless a push-pull round */
 int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap);
-int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes);
+int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *bytes_per_shard);
+int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap);
+int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes); /* the received delta blocks */
 /* Optional, between gx_ae_pack and gx_ae_merge: start the push-pull merges of the pairs whose two
- * hosts are both on this shard, asynchronously on the engine's stream, so they overlap the row
- * exchange; gx_ae_merge then merges only the pairs with a received row. Pairs are disjoint (every
+ * hosts are both on this shard, asynchronously on the engine's stream, so they overlap the
+ * exchanges; gx_ae_merge then merges only the cross-shard pairs. Pairs are disjoint (every
  * host is in at most one), so the result is identical either way. */
 int gx_ae_merge_local(gx_engine *e); /* phase 5 */
 int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */

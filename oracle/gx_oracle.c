@@ -34,8 +34,16 @@ struct gx_engine {
   gx_params p;
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
   uint32_t G, gid, lo, hi; /* shards; this engine owns hosts [lo, hi). Arrays stay H-sized. */
-  uint64_t *rows_in;       /* received push-pull rows (this AE round) */
-  uint32_t n_rows_in;
+  /* cross-shard push-pull pairs of this AE round, in (partner shard, pair index) order, which is
+   * the order of the digest and delta messages in both directions */
+  uint32_t x_n, nblk;
+  uint32_t *x_t, *x_mine;
+  uint8_t *x_first;     /* this side holds the pair's first member (counts the exchange) */
+  uint64_t *x_dig;      /* [x_n][nblk][2] own digests */
+  uint8_t *x_diff;      /* [x_n][nblk] 1 = the partner's digest differs */
+  uint32_t *x_cnt;
+  uint64_t x_total;
+  int64_t x_round, x_delta_round;
   int64_t round;
   uint64_t *view;       /* H * R packed slots */
   uint8_t *own_status;  /* H * S local service status (discovery/health) */
@@ -665,42 +673,54 @@ static void ae_merge_row(gx_engine *e, uint32_t x, const uint64_t *row, int coun
   if (count_exchange) e->st.ae_exchanges++;
 }
 
-/* Phase 5: pairs with both hosts here merge both ways; cross-shard pairs merge the received
- * row of the remote member (rows arrive grouped by source shard, ascending pair index). */
-static void ae_phase(gx_engine *e, const uint64_t *rows, uint64_t bytes) {
-  if (!ae_round(e)) return;
+/* Phase 5, pairs with both hosts here: both merge the other's round-start row. */
+static void ae_phase_local(gx_engine *e) {
+  if (!ae_round(e) || e->ae_local_round == e->round) return;
   int64_t now = now_of(e);
   uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
   uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
   uint32_t np = ae_pairs(e, pa, pb);
-  size_t row_bytes = 16 + 8ull * e->R;
-  /* index of each cross pair's row in the received buffer */
-  size_t next = 0;
+  for (uint32_t t = 0; t < np; t++)
+    if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
+  free(pa);
+  free(pb);
+  e->ae_local_round = e->round;
+}
+
+/* Block digest of gx.h: slots [b*512, min(R, (b+1)*512)) of a row. */
+static void block_digest(const gx_engine *e, const uint64_t *row, uint32_t b, uint64_t *d0, uint64_t *d1) {
+  uint64_t s0 = 0, s1 = 0;
+  uint32_t lo = b * GX_DIGEST_SLOTS, hi = lo + GX_DIGEST_SLOTS < e->R ? lo + GX_DIGEST_SLOTS : e->R;
+  for (uint32_t i = lo; i < hi; i++) {
+    s0 += mix64(row[i] ^ ((uint64_t)i * 0xD6E8FEB86659FD93ull));
+    s1 += mix64(row[i] + (uint64_t)i * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+  }
+  *d0 = s0;
+  *d1 = s1;
+}
+
+/* The cross-shard pairs of this round, in message order. */
+static void ae_cross_build(gx_engine *e) {
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t np = ae_pairs(e, pa, pb);
+  e->x_n = 0;
   for (uint32_t g = 0; g < e->G; g++) {
     if (g == e->gid) continue;
     for (uint32_t t = 0; t < np; t++) {
       int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
-      uint32_t remote = la ? pb[t] : pa[t];
-      if (la == lb || shard_of(e, remote) != g) continue;
-      const uint8_t *rec = (const uint8_t *)rows + next * row_bytes;
-      if ((next + 1) * row_bytes > bytes) break;
-      uint32_t hdr_t, hdr_h;
-      memcpy(&hdr_t, rec, 4);
-      memcpy(&hdr_h, rec + 4, 4);
-      if (hdr_t == t && hdr_h == remote) {
-        uint64_t *row = (uint64_t *)malloc(8ull * e->R);
-        memcpy(row, rec + 16, 8ull * e->R);
-        ae_merge_row(e, la ? pa[t] : pb[t], row, la, now);
-        free(row);
-      }
-      next++;
+      if (la == lb) continue;
+      uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
+      if (shard_of(e, other) != g) continue;
+      e->x_t[e->x_n] = t;
+      e->x_mine[e->x_n] = mine;
+      e->x_first[e->x_n] = (uint8_t)la;
+      e->x_n++;
     }
   }
-  if (e->ae_local_round != e->round)
-    for (uint32_t t = 0; t < np; t++)
-      if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
   free(pa);
   free(pb);
+  e->x_round = e->round;
 }
 
 static void round_end(gx_engine *e) {
@@ -712,7 +732,7 @@ static void round_end(gx_engine *e) {
 static void run_one_round(gx_engine *e) {
   round_send(e);
   round_merge(e);
-  ae_phase(e, NULL, 0);
+  ae_phase_local(e);
   round_end(e);
 }
 
@@ -839,6 +859,21 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->in_cnt = (uint32_t *)calloc(H + 1, sizeof(uint32_t));
   e->in_list = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
   e->sbytes = (uint16_t *)malloc(sizeof(uint16_t) * e->R);
+  e->nblk = (e->R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
+  e->x_round = e->x_delta_round = -1;
+  if (e->G > 1) {
+    size_t hl = e->hi - e->lo;
+    e->x_t = (uint32_t *)calloc(hl, sizeof(uint32_t));
+    e->x_mine = (uint32_t *)calloc(hl, sizeof(uint32_t));
+    e->x_first = (uint8_t *)calloc(hl, 1);
+    e->x_dig = (uint64_t *)calloc(hl * e->nblk * 2, sizeof(uint64_t));
+    e->x_diff = (uint8_t *)calloc(hl * e->nblk, 1);
+    e->x_cnt = (uint32_t *)calloc(hl, sizeof(uint32_t));
+    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_dig || !e->x_diff || !e->x_cnt) {
+      gx_destroy(e);
+      return GX_ENOMEM;
+    }
+  }
   if (e->sbytes)
     for (uint32_t r = 0; r < e->R; r++) e->sbytes[r] = GX_STATIC_BYTES_DEFAULT;
   if (!e->sbytes || !e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
@@ -868,6 +903,12 @@ int gx_destroy(gx_engine *e) {
   free(e->in_cnt);
   free(e->in_list);
   free(e->sbytes);
+  free(e->x_t);
+  free(e->x_mine);
+  free(e->x_first);
+  free(e->x_dig);
+  free(e->x_diff);
+  free(e->x_cnt);
   free(e);
   return GX_OK;
 }
@@ -1221,7 +1262,6 @@ int gx_host_digests(gx_engine *e, uint64_t *out) {
 
 /* ---------------------------------------------------------------------- sharded rounds -- */
 static size_t slot_bytes(const gx_engine *e) { return 16 + 16ull * e->p.packet_cap; }
-static size_t row_bytes(const gx_engine *e) { return 16 + 8ull * e->R; }
 
 int gx_round_send(gx_engine *e) {
   if (!e) return GX_EINVAL;
@@ -1272,66 +1312,139 @@ int gx_round_merge(gx_engine *e) {
   round_merge(e);
   return GX_OK;
 }
+static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk; }
+
 int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
   if (!e || !bytes) return GX_EINVAL;
   for (uint32_t g = 0; g < e->G; g++) bytes[g] = 0;
+  e->x_round = e->x_delta_round = -1;
+  e->x_n = 0;
   if (!ae_round(e) || e->G < 2) return GX_OK;
+  ae_cross_build(e);
+  /* message k goes to the partner's shard; messages are grouped by that shard */
   uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
   uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
-  uint32_t np = ae_pairs(e, pa, pb);
-  for (uint32_t t = 0; t < np; t++) {
-    int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
-    if (la != lb) bytes[shard_of(e, la ? pb[t] : pa[t])] += row_bytes(e);
+  ae_pairs(e, pa, pb);
+  for (uint32_t k = 0; k < e->x_n; k++) {
+    uint32_t t = e->x_t[k], other = e->x_first[k] ? pb[t] : pa[t];
+    bytes[shard_of(e, other)] += dig_bytes(e);
   }
   free(pa);
   free(pb);
   return GX_OK;
 }
+
 int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!e || (cap && !buf)) return GX_EINVAL;
-  if (!ae_round(e) || e->G < 2) return GX_OK;
+  if (!ae_round(e) || e->G < 2 || !e->x_n) return GX_OK;
+  if (e->x_round != e->round || cap < e->x_n * dig_bytes(e)) return GX_EINVAL;
+  uint8_t *p = (uint8_t *)buf;
+  for (uint32_t k = 0; k < e->x_n; k++) {
+    uint8_t *m = p + (size_t)k * dig_bytes(e);
+    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->nblk, 0};
+    memcpy(m, hdr, 16);
+    const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
+    for (uint32_t b = 0; b < e->nblk; b++) {
+      uint64_t *dg = &e->x_dig[((size_t)k * e->nblk + b) * 2];
+      block_digest(e, row, b, &dg[0], &dg[1]);
+      memcpy(m + 16 + 16ull * b, dg, 16);
+    }
+  }
+  return GX_OK;
+}
+
+int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *out) {
+  if (!e || !out || (bytes && !digests)) return GX_EINVAL;
+  for (uint32_t g = 0; g < e->G; g++) out[g] = 0;
+  e->x_delta_round = -1;
+  e->x_total = 0;
+  if (!ae_round(e) || e->G < 2) return bytes ? GX_EINVAL : GX_OK;
+  if (e->x_round != e->round || bytes != e->x_n * dig_bytes(e)) return GX_EINVAL;
   uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
   uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
-  uint32_t np = ae_pairs(e, pa, pb);
-  uint8_t *p = (uint8_t *)buf;
-  size_t off = 0, rb = row_bytes(e);
+  ae_pairs(e, pa, pb);
   int rc = GX_OK;
-  for (uint32_t g = 0; g < e->G && rc == GX_OK; g++)
-    for (uint32_t t = 0; t < np; t++) {
-      int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
-      if (la == lb) continue;
-      uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
-      if (shard_of(e, other) != g) continue;
-      if (off + rb > cap) {
-        rc = GX_EINVAL;
-        break;
-      }
-      uint32_t hdr[4] = {t, mine, 0, 0};
-      memcpy(p + off, hdr, 16);
-      memcpy(p + off + 16, &e->view[(size_t)mine * e->R], 8ull * e->R);
-      off += rb;
+  for (uint32_t k = 0; k < e->x_n; k++) {
+    const uint8_t *m = (const uint8_t *)digests + (size_t)k * dig_bytes(e);
+    uint32_t hdr[4];
+    memcpy(hdr, m, 16);
+    if (hdr[0] != e->x_t[k] || hdr[2] != e->nblk) rc = GX_EINVAL;
+    uint32_t n = 0;
+    for (uint32_t b = 0; b < e->nblk; b++) {
+      uint64_t theirs[2];
+      memcpy(theirs, m + 16 + 16ull * b, 16);
+      const uint64_t *mine = &e->x_dig[((size_t)k * e->nblk + b) * 2];
+      uint8_t differ = theirs[0] != mine[0] || theirs[1] != mine[1];
+      e->x_diff[(size_t)k * e->nblk + b] = differ;
+      n += differ;
     }
+    e->x_cnt[k] = n;
+    uint64_t sz = 16 + (uint64_t)n * 8 * GX_DIGEST_SLOTS;
+    uint32_t t = e->x_t[k], other = e->x_first[k] ? pb[t] : pa[t];
+    out[shard_of(e, other)] += sz;
+    e->x_total += sz;
+  }
   free(pa);
   free(pb);
+  if (rc == GX_OK) e->x_delta_round = e->round;
   return rc;
 }
+
+int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (!ae_round(e) || e->G < 2 || !e->x_n) return GX_OK;
+  if (e->x_delta_round != e->round || cap < e->x_total) return GX_EINVAL;
+  uint8_t *p = (uint8_t *)buf;
+  for (uint32_t k = 0; k < e->x_n; k++) {
+    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->x_cnt[k], 0};
+    memcpy(p, hdr, 16);
+    p += 16;
+    const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
+    for (uint32_t b = 0; b < e->nblk; b++) {
+      if (!e->x_diff[(size_t)k * e->nblk + b]) continue;
+      uint64_t blk[GX_DIGEST_SLOTS] = {0};
+      for (uint32_t i = 0; i < GX_DIGEST_SLOTS && b * GX_DIGEST_SLOTS + i < e->R; i++) blk[i] = row[b * GX_DIGEST_SLOTS + i];
+      memcpy(p, blk, sizeof blk);
+      p += sizeof blk;
+    }
+  }
+  return GX_OK;
+}
+
+/* Cross-shard pairs merge the partner's row rebuilt from the delta: sent blocks from the message,
+ * the other blocks from this host's own row (their digests matched); then the local pairs. */
 int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
   if (!e || (bytes && !buf)) return GX_EINVAL;
-  ae_phase(e, (const uint64_t *)buf, bytes);
+  if (!ae_round(e)) return GX_OK;
+  if (e->G > 1 && e->x_n) {
+    if (e->x_delta_round != e->round || bytes != e->x_total) return GX_EINVAL;
+    int64_t now = now_of(e);
+    uint64_t *row = (uint64_t *)malloc(8ull * e->R);
+    const uint8_t *p = (const uint8_t *)buf;
+    for (uint32_t k = 0; k < e->x_n; k++) {
+      uint32_t hdr[4];
+      memcpy(hdr, p, 16);
+      p += 16;
+      const uint64_t *own = &e->view[(size_t)e->x_mine[k] * e->R];
+      for (uint32_t b = 0; b < e->nblk; b++) {
+        uint32_t lo = b * GX_DIGEST_SLOTS, n = lo + GX_DIGEST_SLOTS < e->R ? GX_DIGEST_SLOTS : e->R - lo;
+        if (e->x_diff[(size_t)k * e->nblk + b]) {
+          memcpy(&row[lo], p, 8ull * n);
+          p += 8 * GX_DIGEST_SLOTS;
+        } else {
+          memcpy(&row[lo], &own[lo], 8ull * n);
+        }
+      }
+      ae_merge_row(e, e->x_mine[k], row, e->x_first[k], now);
+    }
+    free(row);
+  }
+  ae_phase_local(e);
   return GX_OK;
 }
 int gx_ae_merge_local(gx_engine *e) {
   if (!e) return GX_EINVAL;
-  if (!ae_round(e) || e->G < 2 || e->ae_local_round == e->round) return GX_OK;
-  int64_t now = now_of(e);
-  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
-  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
-  uint32_t np = ae_pairs(e, pa, pb);
-  for (uint32_t t = 0; t < np; t++)
-    if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
-  free(pa);
-  free(pb);
-  e->ae_local_round = e->round;
+  if (e->G > 1) ae_phase_local(e);
   return GX_OK;
 }
 int gx_round_end(gx_engine *e) {

@@ -124,7 +124,7 @@ ABI_FUNCS = [
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
-    "gx_view_minmax", "gx_ae_merge_local", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
+    "gx_view_minmax", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
 ]
 
 
@@ -168,6 +168,8 @@ def _declare(lib):
         "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64], i32),
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
         "gx_ae_merge_local": ([vp], i32),
+        "gx_ae_delta_bytes": ([vp, vp, C.c_uint64, vp], i32),
+        "gx_ae_delta_pack": ([vp, vp, C.c_uint64], i32),
         "gx_get_broadcasts_bytes": ([vp, u32, u32, u32, P(GxService), u32, P(u32)], i32),
         "gx_set_static_bytes": ([vp, u32, u32, P(u16)], i32),
         "gx_message_bytes": ([vp, P(GxService), u32, P(u32)], i32),
@@ -493,6 +495,16 @@ class Engine:
 
     def ae_pack(self, ptr: int, cap: int):
         check(self.lib.gx_ae_pack(self.h, C.c_void_p(ptr), cap), "gx_ae_pack")
+
+    def ae_delta_bytes(self, ptr: int, nbytes: int) -> np.ndarray:
+        """Compare the received push-pull digests with this shard's; delta sizes per shard."""
+        out = np.zeros(self.G, dtype=np.uint64)
+        check(self.lib.gx_ae_delta_bytes(self.h, C.c_void_p(ptr), nbytes, out.ctypes.data_as(C.c_void_p)),
+              "gx_ae_delta_bytes")
+        return out
+
+    def ae_delta_pack(self, ptr: int, cap: int):
+        check(self.lib.gx_ae_delta_pack(self.h, C.c_void_p(ptr), cap), "gx_ae_delta_pack")
 
     def ae_merge(self, ptr: int, nbytes: int):
         check(self.lib.gx_ae_merge(self.h, C.c_void_p(ptr), nbytes), "gx_ae_merge")

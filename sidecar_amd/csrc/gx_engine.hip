@@ -66,6 +66,17 @@ struct gx_engine {
   int32_t *ae_prow;
   uint8_t *ae_pcount;
   uint32_t n_plan, n_pack, n_plan_rows;
+  // push-pull digests / delta (per cross pair k, in pack order = receive order)
+  uint32_t nblk, nmw;
+  ulonglong2 *ae_dig;  // [Hl][nblk] own digests
+  uint32_t *ae_mask;   // [Hl][nmw] differing blocks
+  uint32_t *ae_cnt;    // [Hl] differing block count
+  uint64_t *ae_off;    // [Hl] delta message offsets
+  uint32_t *ae_err;
+  std::vector<uint32_t> pack_gstart;  // pack index range per destination shard
+  std::vector<uint64_t> delta_off_h;
+  uint64_t delta_total;
+  int ae_delta_round;
   int ae_planned_round;
   int64_t ae_local_round;
   // small device scratch for single-host ABI calls
@@ -302,7 +313,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
@@ -346,6 +357,11 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = nullptr;
   e->ae_prow = nullptr;
   e->ae_pcount = nullptr;
+  e->ae_dig = nullptr;
+  e->ae_mask = e->ae_cnt = e->ae_err = nullptr;
+  e->ae_off = nullptr;
+  e->ae_delta_round = -1;
+  e->delta_total = 0;
   e->n_plan = e->n_pack = e->n_plan_rows = 0;
   e->ae_planned_round = -1;
   e->ae_local_round = -1;
@@ -408,6 +424,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->ae_pcount, np);
     ALLOC(e->ae_pack_host, sizeof(uint32_t) * np);
     ALLOC(e->ae_pack_t, sizeof(uint32_t) * np);
+    e->nblk = (d.R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
+    e->nmw = (e->nblk + 31) / 32;
+    ALLOC(e->ae_dig, sizeof(ulonglong2) * H * e->nblk);
+    ALLOC(e->ae_mask, sizeof(uint32_t) * H * e->nmw);
+    ALLOC(e->ae_cnt, sizeof(uint32_t) * H);
+    ALLOC(e->ae_off, sizeof(uint64_t) * H);
+    ALLOC(e->ae_err, sizeof(uint32_t));
   }
   hipStream_t s = e->stream;
   uint64_t *rec_word = nullptr;
@@ -901,7 +924,7 @@ static uint32_t shard_of(const Dev &d, uint32_t v) {
   return g;
 }
 static size_t slot_bytes(const Dev &d) { return 16 + 16ull * d.p.packet_cap; }
-static size_t row_bytes(const Dev &d) { return 16 + 8ull * d.R; }
+static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk; }
 
 int gx_round_send(gx_engine *e) {
   if (!e) return GX_EINVAL;
@@ -991,7 +1014,9 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
   std::vector<int32_t> plan_row;
   std::vector<uint8_t> plan_cnt;
   for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
-  for (uint32_t g = 0; g < d.G; g++) {  // rows to send to shard g (ascending t)
+  e->pack_gstart.assign(d.G + 1, 0);
+  for (uint32_t g = 0; g < d.G; g++) {  // digests (then deltas) to send to shard g (ascending t)
+    e->pack_gstart[g] = (uint32_t)pack_host.size();
     if (g == d.gid) continue;
     for (size_t t = 0; t < pa.size(); t++) {
       bool la = own(e, pa[t]), lb = own(e, pb[t]);
@@ -1000,11 +1025,14 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
       if (shard_of(d, other) != g) continue;
       pack_host.push_back(mine);
       pack_t.push_back((uint32_t)t);
-      bytes[g] += row_bytes(d);
+      bytes[g] += dig_bytes(e);
     }
   }
+  e->pack_gstart[d.G] = (uint32_t)pack_host.size();
+  // messages received from shard g come in the same (shard, ascending t) order as the ones sent,
+  // so cross pair k has the same index in both directions
   int32_t row = 0;
-  for (uint32_t g = 0; g < d.G; g++) {  // rows received from shard g, same order on both sides
+  for (uint32_t g = 0; g < d.G; g++) {
     if (g == d.gid) continue;
     for (size_t t = 0; t < pa.size(); t++) {
       bool la = own(e, pa[t]), lb = own(e, pb[t]);
@@ -1054,9 +1082,61 @@ int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
 int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!e || (cap && !buf)) return GX_EINVAL;
   if (!e->n_pack) return GX_OK;
-  if (e->ae_planned_round != (int)e->d.round || cap < e->n_pack * row_bytes(e->d)) return GX_EINVAL;
+  if (e->ae_planned_round != (int)e->d.round || cap < e->n_pack * dig_bytes(e)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  k_ae_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, (uint8_t *)buf);
+  if (e->d.R % 2 == 0)
+    k_ae_digest<true><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, (uint8_t *)buf,
+                                                         e->ae_dig, e->nblk);
+  else
+    k_ae_digest<false><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, (uint8_t *)buf,
+                                                          e->ae_dig, e->nblk);
+  return sync_check(e);
+}
+
+int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *out) {
+  if (!e || !out || (bytes && !digests)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  Dev &d = e->d;
+  for (uint32_t g = 0; g < d.G; g++) out[g] = 0;
+  e->ae_delta_round = -1;
+  e->delta_total = 0;
+  if (d.G < 2 || !ae_round(e)) return bytes ? GX_EINVAL : GX_OK;
+  if (e->ae_planned_round != (int)d.round || bytes != e->n_pack * dig_bytes(e)) return GX_EINVAL;
+  std::vector<uint32_t> cnt(e->n_pack);
+  if (e->n_pack) {
+    HIPCHK(hipMemsetAsync(e->ae_err, 0, sizeof(uint32_t), e->stream));
+    k_ae_mask<<<e->n_pack, 256, 0, e->stream>>>((const uint8_t *)digests, e->ae_dig, e->ae_pack_t, e->nblk, e->nmw,
+                                                 e->ae_mask, e->ae_cnt, e->ae_err);
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, e->ae_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(cnt.data(), e->ae_cnt, sizeof(uint32_t) * e->n_pack, hipMemcpyDeviceToHost, e->stream));
+    int rc = sync_check(e);
+    if (rc) return rc;
+    if (err) return GX_EINVAL;  // digests of another pair or another row size
+  }
+  e->delta_off_h.resize(e->n_pack);
+  uint64_t o = 0;
+  for (uint32_t g = 0; g < d.G; g++)
+    for (uint32_t k = e->pack_gstart[g]; k < e->pack_gstart[g + 1]; k++) {
+      e->delta_off_h[k] = o;
+      uint64_t sz = 16 + (uint64_t)cnt[k] * 8 * GX_DIGEST_SLOTS;
+      out[g] += sz;
+      o += sz;
+    }
+  e->delta_total = o;
+  if (e->n_pack)
+    HIPCHK(hipMemcpy(e->ae_off, e->delta_off_h.data(), sizeof(uint64_t) * e->n_pack, hipMemcpyHostToDevice));
+  e->ae_delta_round = (int)d.round;
+  return GX_OK;
+}
+
+int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (!e->n_pack) return GX_OK;
+  if (e->ae_delta_round != (int)e->d.round || cap < e->delta_total) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  k_ae_delta_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
+                                                     e->ae_off, e->nmw, (uint8_t *)buf);
   return sync_check(e);
 }
 
@@ -1067,10 +1147,12 @@ static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *b
   LaunchTimer t(e, GX_K_AE);
   if (e->d.R % 2 == 0)
     k_ae_plan<true><<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,
-                                                     e->ae_pcount + lo, (const uint8_t *)buf);
+                                                     e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off,
+                                                     e->ae_mask, e->nmw);
   else
     k_ae_plan<false><<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,
-                                                      e->ae_pcount + lo, (const uint8_t *)buf);
+                                                      e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off,
+                                                      e->ae_mask, e->nmw);
 }
 
 int gx_ae_merge_local(gx_engine *e) {
@@ -1093,6 +1175,7 @@ int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
     return rc ? rc : sync_check(e);
   }
   if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
+  if (e->n_plan_rows && (e->ae_delta_round != (int)e->d.round || bytes != e->delta_total)) return GX_EINVAL;
   bool local_done = e->ae_local_round == e->d.round;
   ae_plan_launch(e, 0, local_done ? e->n_plan_rows : e->n_plan, buf);
   return sync_check(e);

@@ -727,12 +727,15 @@ GXD ulonglong2 ld16(const uint64_t *p) {
   return *reinterpret_cast<const ulonglong2 *>(p);
 }
 
-// `ext` (when both = false): B is another shard's received row of host b (read-only); the pair's
-// exchange is counted where a is the pair's first member (count_ex). PF = tiles whose loads are in
-// flight while one is merged (software pipeline depth); NT = non-temporal loads (read-once rows).
+// `ext` (when both = false): B is host b's row from another shard (read-only); the pair's
+// exchange is counted where a is the pair's first member (count_ex). With `emask`, ext holds only
+// the 512-slot blocks whose bit is set (ascending); every other block of B is A's own block (the
+// digests matched), which merges with the counts of the identical remote block and no change.
+// PF = tiles whose loads are in flight while one is merged; NT = non-temporal loads.
 template <bool VEC, int PF = 1, bool NT = false>
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
-                 unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false) {
+                 unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false,
+                 const uint32_t *emask = nullptr) {
   uint64_t *A = vrow(d, a);
   uint64_t *B = ext ? const_cast<uint64_t *>(ext) : vrow(d, b);
   gx_host_state *ha = hst(d, a), *hb = both ? hst(d, b) : ha;
@@ -746,14 +749,22 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   // Software pipeline: the next PF 1024-slot tiles' loads are in flight while this tile is
   // merged, written back and (only if something was accepted) compacted.
   uint64_t qa[PF][4], qb[PF][4];
+  uint32_t erank = 0;  // set mask bits below the next block to load
   auto load_tile = [&](uint32_t base, uint64_t *xa, uint64_t *xb) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
       bool v0 = r0 < d.R, v1 = r0 + 1 < d.R;
+      const uint64_t *Bp = B + r0;  // B[r0], B[r0 + 1]
+      if (emask && base + GX_DIGEST_SLOTS * h < d.R) {
+        uint32_t blk = (base >> 9) + h;
+        bool sent = (emask[blk >> 5] >> (blk & 31)) & 1u;
+        Bp = sent ? ext + (size_t)erank * GX_DIGEST_SLOTS + (r0 - blk * GX_DIGEST_SLOTS) : A + r0;
+        erank += sent;
+      }
       if (VEC && v0) {
         ulonglong2 pa = ld16<NT>(&A[r0]);
-        ulonglong2 pb = ld16<NT>(&B[r0]);
+        ulonglong2 pb = ld16<NT>(Bp);
         xa[2 * h] = pa.x;
         xa[2 * h + 1] = pa.y;
         xb[2 * h] = pb.x;
@@ -761,8 +772,8 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       } else {
         xa[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
         xa[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
-        xb[2 * h] = v0 ? B[r0] : GX_SLOT_ABSENT;
-        xb[2 * h + 1] = v1 ? B[r0 + 1] : GX_SLOT_ABSENT;
+        xb[2 * h] = v0 ? Bp[0] : GX_SLOT_ABSENT;
+        xb[2 * h + 1] = v1 ? Bp[1] : GX_SLOT_ABSENT;
       }
     }
   };
@@ -917,36 +928,128 @@ __global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32
   ae_pair<VEC>(d, dst, src, false, s_wave, s_red);
 }
 
-// Sharded push-pull: plan entry i = (a, b, row): row < 0 -> both members here (a <-> b);
-// row >= 0 -> a is here and b's row is rows_in[row] (16-B header + R words): a <- b only.
+// Sharded push-pull: plan entry i = (a, b, k): k < 0 -> both members here (a <-> b); k >= 0 ->
+// a is here and b's differing blocks are delta message k of `in` (at off[k], mask k): a <- b only.
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_plan(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
-                                                  const uint8_t *pcount, const uint8_t *rows_in) {
+                                                  const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
+                                                  const uint32_t *mask, uint32_t nmw) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
   uint32_t i = blockIdx.x;
-  if (prow[i] < 0) {
+  int32_t k = prow[i];
+  if (k < 0) {
     ae_pair<VEC>(d, pa[i], pb[i], true, s_wave, s_red);
   } else {
-    const uint64_t *row = reinterpret_cast<const uint64_t *>(rows_in + (size_t)prow[i] * (16 + 8ull * d.R) + 16);
-    ae_pair<VEC>(d, pa[i], pb[i], false, s_wave, s_red, row, pcount[i] != 0);
+    const uint64_t *blocks = reinterpret_cast<const uint64_t *>(in + off[k] + 16);
+    ae_pair<VEC>(d, pa[i], pb[i], false, s_wave, s_red, blocks, pcount[i] != 0, mask + (size_t)k * nmw);
   }
 }
 
-// Gather this shard's rows for its cross-shard push-pull partners (16-B header + row).
-__global__ __launch_bounds__(256) void k_ae_pack(Dev d, const uint32_t *host, const uint32_t *pair_t, uint8_t *out) {
-  uint32_t i = blockIdx.x;
-  uint8_t *dst = out + (size_t)i * (16 + 8ull * d.R);
+// Push-pull digests of this shard's cross-pair rows (gx.h "digest"): one block per pair, one wave
+// per 512-slot block at a time. Also kept in `own` for the comparison.
+GXD uint64_t dig_mix(uint64_t z) { return mix64(z); }
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, const uint32_t *pair_t, uint8_t *out,
+                                                    ulonglong2 *own, uint32_t nblk) {
+  const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint8_t *msg = out + (size_t)k * (16 + 16ull * nblk);
   if (threadIdx.x == 0) {
-    uint32_t *hdr = reinterpret_cast<uint32_t *>(dst);
-    hdr[0] = pair_t[i];
-    hdr[1] = host[i];
-    hdr[2] = 0;
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
+    hdr[0] = pair_t[k];
+    hdr[1] = host[k];
+    hdr[2] = nblk;
     hdr[3] = 0;
   }
-  const uint64_t *src = vrow(d, host[i]);
-  uint64_t *o = reinterpret_cast<uint64_t *>(dst + 16);
-  for (uint32_t x = threadIdx.x; x < d.R; x += blockDim.x) o[x] = src[x];
+  const uint64_t *row = vrow(d, host[k]);
+  for (uint32_t b = wv; b < nblk; b += 4) {
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t i = b * GX_DIGEST_SLOTS + 2 * (64 * q + lane);
+      uint64_t w0 = 0, w1 = 0;
+      bool v0 = i < d.R, v1 = i + 1 < d.R;
+      if (VEC && v0) {
+        ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(&row[i]);
+        w0 = x.x;
+        w1 = x.y;
+      } else {
+        if (v0) w0 = row[i];
+        if (v1) w1 = row[i + 1];
+      }
+      if (v0) {
+        s0 += dig_mix(w0 ^ ((uint64_t)i * 0xD6E8FEB86659FD93ull));
+        s1 += dig_mix(w0 + (uint64_t)i * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+      }
+      if (v1) {
+        s0 += dig_mix(w1 ^ ((uint64_t)(i + 1) * 0xD6E8FEB86659FD93ull));
+        s1 += dig_mix(w1 + (uint64_t)(i + 1) * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+      }
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+      ulonglong2 dg = make_ulonglong2(s0, s1);
+      own[(size_t)k * nblk + b] = dg;
+      *reinterpret_cast<ulonglong2 *>(msg + 16 + 16ull * b) = dg;
+    }
+  }
+}
+
+// Compare own digests with the partner's (message k of `in`): mask bit b = block b differs.
+__global__ __launch_bounds__(256) void k_ae_mask(const uint8_t *in, const ulonglong2 *own, const uint32_t *pair_t,
+                                                  uint32_t nblk, uint32_t nmw, uint32_t *mask, uint32_t *cnt,
+                                                  uint32_t *err) {
+  __shared__ uint32_t s_n[4];
+  const uint32_t k = blockIdx.x;
+  const uint8_t *msg = in + (size_t)k * (16 + 16ull * nblk);
+  const uint32_t *hdr = reinterpret_cast<const uint32_t *>(msg);
+  if (threadIdx.x == 0 && (hdr[0] != pair_t[k] || hdr[2] != nblk)) atomicOr(err, 1u);
+  uint32_t n = 0;
+  for (uint32_t w = threadIdx.x; w < nmw; w += blockDim.x) {
+    uint32_t bits = 0;
+    for (uint32_t j = 0; j < 32; j++) {
+      uint32_t b = w * 32 + j;
+      if (b >= nblk) break;
+      ulonglong2 x = own[(size_t)k * nblk + b];
+      ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(msg + 16 + 16ull * b);
+      if (x.x != y.x || x.y != y.y) bits |= 1u << j;
+    }
+    mask[(size_t)k * nmw + w] = bits;
+    n += __popc(bits);
+  }
+  n = (uint32_t)wave_sum(n);
+  if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[k] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+}
+
+// The differing blocks of each cross-pair row (gx.h "delta"), message k at off[k].
+__global__ __launch_bounds__(256) void k_ae_delta_pack(Dev d, const uint32_t *host, const uint32_t *pair_t,
+                                                        const uint32_t *mask, const uint32_t *cnt, const uint64_t *off,
+                                                        uint32_t nmw, uint8_t *out) {
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  uint8_t *msg = out + off[k];
+  if (t == 0) {
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
+    hdr[0] = pair_t[k];
+    hdr[1] = host[k];
+    hdr[2] = cnt[k];
+    hdr[3] = 0;
+  }
+  const uint64_t *row = vrow(d, host[k]);
+  uint32_t j = 0;
+  for (uint32_t w = 0; w < nmw; w++) {
+    uint32_t bits = mask[(size_t)k * nmw + w];
+    while (bits) {
+      uint32_t blk = w * 32 + (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      uint32_t i = blk * GX_DIGEST_SLOTS + 2 * t;  // 256 threads x 2 words = one block
+      uint64_t w0 = i < d.R ? row[i] : 0, w1 = i + 1 < d.R ? row[i + 1] : 0;
+      *reinterpret_cast<ulonglong2 *>(msg + 16 + (size_t)j * 8 * GX_DIGEST_SLOTS + 16ull * t) = make_ulonglong2(w0, w1);
+      j++;
+    }
+  }
 }
 
 // Outbox: fixed-size slots (16-B header + packet_cap records); slot index per local entry.

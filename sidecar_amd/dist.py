@@ -1,5 +1,5 @@
 """Host sharding across engines: one round = send phase, packet exchange, merge phase,
-push-pull row exchange, end.
+push-pull digest exchange, push-pull delta exchange, end.
 
 Each engine owns the contiguous host block [g*H/G, (g+1)*H/G). The exchange moves the wire
 formats of include/gx.h between shards:
@@ -22,6 +22,25 @@ from .abi import Engine, GxParams, default_params
 
 def _ptr(t: torch.Tensor) -> int:
     return t.data_ptr() if t.numel() else 0
+
+
+class WireBytes:
+    """Bytes each exchange moved between shards (this process's shards, sent side)."""
+
+    def __init__(self, R: int):
+        self.R = R
+        self.packets = self.ae_digest = self.ae_delta = self.ae_full_rows = 0
+
+    def add_ae(self, digest_sizes, delta_sizes):
+        dig = int(np.asarray(digest_sizes).sum())
+        nblk = (self.R + 511) // 512
+        self.ae_digest += dig
+        self.ae_delta += int(np.asarray(delta_sizes).sum())
+        self.ae_full_rows += dig // (16 + 16 * nblk) * (16 + 8 * self.R)  # the same pairs as full rows
+
+    def as_dict(self):
+        return {"packets": self.packets, "ae_digest": self.ae_digest, "ae_delta": self.ae_delta,
+                "ae_full_rows_equivalent": self.ae_full_rows}
 
 
 class _Shard:
@@ -53,38 +72,58 @@ class LocalShards:
             if self.device.type == "cuda":
                 p.device = self.device.index or 0
             self.shards.append(_Shard(p, lib, self.device))
+        self.wire = WireBytes(self.shards[0].e.H * self.shards[0].e.S)
+        self.trace_ae = False  # keep each push-pull round's digest and delta inboxes (host copies)
+        self.ae_trace = []
 
     @property
     def engines(self) -> List[Engine]:
         return [s.e for s in self.shards]
 
-    def _exchange(self, sizes_fn, pack_fn, unpack_fn, after_pack=None):
+    def _exchange(self, sizes_fn, pack_fn, after_pack=None) -> List[torch.Tensor]:
+        """Every shard packs per destination; returns each shard's inbox (sources ascending)."""
         sizes = [sizes_fn(s.e) for s in self.shards]  # sizes[src][dst]
+        self.last_sizes = sizes
         bufs = [s.pack(sz, lambda p, n, e=s.e: pack_fn(e, p, n)) for s, sz in zip(self.shards, sizes)]
         if after_pack is not None:
             for s in self.shards:
                 after_pack(s.e)
         for s in self.shards:
             s.sync()
-        for dst, s in enumerate(self.shards):
+        inboxes = []
+        for dst in range(self.G):
             parts = []
             for src in range(self.G):
                 off = int(sizes[src][:dst].sum())
                 parts.append(bufs[src][off:off + int(sizes[src][dst])])
-            inbox = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=self.device)
+            inboxes.append(torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=self.device))
+        for s in self.shards:
             s.sync()
-            unpack_fn(s.e, _ptr(inbox), inbox.numel())
+        return inboxes
 
     def run_rounds(self, n: int):
         for _ in range(n):
             for s in self.shards:
                 s.e.round_send()
-            self._exchange(lambda e: e.outbox_bytes(), lambda e, p, c: e.outbox_pack(p, c),
-                           lambda e, p, c: e.inbox_unpack(p, c))
+            inb = self._exchange(lambda e: e.outbox_bytes(), lambda e, p, c: e.outbox_pack(p, c))
+            self.wire.packets += int(sum(int(x.sum()) for x in self.last_sizes))
+            for s, x in zip(self.shards, inb):
+                s.e.inbox_unpack(_ptr(x), x.numel())
             for s in self.shards:
                 s.e.round_merge()
-            self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
-                           lambda e, p, c: e.ae_merge(p, c), after_pack=lambda e: e.ae_merge_local())
+            # push-pull: digests, then the blocks that differ (shard-local pairs overlap both)
+            dig = self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
+                                 after_pack=lambda e: e.ae_merge_local())
+            dig_sizes = self.last_sizes
+            delta_sizes = {id(s.e): s.e.ae_delta_bytes(_ptr(x), x.numel()) for s, x in zip(self.shards, dig)}
+            delta = self._exchange(lambda e: delta_sizes[id(e)], lambda e, p, c: e.ae_delta_pack(p, c))
+            for a, b in zip(dig_sizes, self.last_sizes):
+                self.wire.add_ae(a, b)
+            if self.trace_ae and any(x.numel() for x in dig):
+                self.ae_trace.append(([x.cpu().numpy().tobytes() for x in dig],
+                                      [x.cpu().numpy().tobytes() for x in delta]))
+            for s, x in zip(self.shards, delta):
+                s.e.ae_merge(_ptr(x), x.numel())
             for s in self.shards:
                 s.e.round_end()
 
@@ -124,10 +163,12 @@ class DistShard:
             p.device = self.device.index or 0
         self.s = _Shard(p, lib, self.device)
         self.e = self.s.e
+        self.wire = WireBytes(self.e.H * self.e.S)
 
     CHUNK = 256 << 20  # bytes per peer per all-to-all call
 
-    def _exchange(self, sizes: np.ndarray, packer, unpacker, after_pack=None):
+    def _exchange(self, sizes: np.ndarray, packer, after_pack=None) -> torch.Tensor:
+        """all-to-all of this shard's per-destination messages; returns the inbox (sources ascending)."""
         dist = self.dist
         send_sizes = torch.tensor(sizes.astype(np.int64), device=self.device)
         recv_sizes = torch.empty_like(send_sizes)
@@ -161,15 +202,24 @@ class DistShard:
                     recv[int(roff[p]) + lo:int(roff[p]) + lo + r_part[p]].copy_(r_buf[o:o + r_part[p]])
                 o += r_part[p]
         self.s.sync()
-        unpacker(_ptr(recv), recv.numel())
+        return recv
 
     def run_rounds(self, n: int):
         e = self.e
         for _ in range(n):
             e.round_send()
-            self._exchange(e.outbox_bytes(), e.outbox_pack, e.inbox_unpack)
+            ob = e.outbox_bytes()
+            self.wire.packets += int(ob.sum())
+            x = self._exchange(ob, e.outbox_pack)
+            e.inbox_unpack(_ptr(x), x.numel())
             e.round_merge()
-            self._exchange(e.ae_bytes(), e.ae_pack, e.ae_merge, after_pack=e.ae_merge_local)
+            # push-pull: digests, then only the blocks that differ (local pairs overlap both)
+            dsz = e.ae_bytes()
+            dig = self._exchange(dsz, e.ae_pack, after_pack=e.ae_merge_local)
+            sizes = e.ae_delta_bytes(_ptr(dig), dig.numel())
+            self.wire.add_ae(dsz, sizes)
+            delta = self._exchange(sizes, e.ae_delta_pack)
+            e.ae_merge(_ptr(delta), delta.numel())
             e.round_end()
 
     def stats(self) -> dict:

@@ -36,6 +36,27 @@ def test_gpu_shards_cfg2_small(gx_lib):
         assert_sharded_equal(whole, sh, f"cfg2-small round {whole.round}")
 
 
+def test_gpu_push_pull_wire_identical_to_oracle(gx_lib, oracle_lib):
+    """The HIP engine's digest and delta messages (gx.h wire formats) equal the oracle's byte for
+    byte, round after round, so either implementation can sit on either end of an exchange."""
+    kw = dict(n_hosts=160, n_services=16, init_mode=2, ae_period_rounds=4, partition_start=0,
+              partition_end=10, storm_round=2, churn_ppm=40000, queue_cap=4096)
+    g = LocalShards(gx_lib, 3, device="cuda:0", **kw)
+    o = LocalShards(oracle_lib, 3, **kw)
+    g.trace_ae = o.trace_ae = True
+    g.run_rounds(30)
+    o.run_rounds(30)
+    assert len(g.ae_trace) == len(o.ae_trace) > 0
+    for i, ((gd, gx), (od, ox)) in enumerate(zip(g.ae_trace, o.ae_trace)):
+        assert gd == od, f"digest inbox, push-pull round {i}"
+        assert gx == ox, f"delta inbox, push-pull round {i}"
+    assert g.wire.as_dict() == o.wire.as_dict()
+    w = g.wire.as_dict()
+    assert w["ae_delta"] < w["ae_full_rows_equivalent"]
+    assert g.stats() == o.stats()
+    assert all((a.read_views() == b.read_views()).all() for a, b in zip(g.engines, o.engines))
+
+
 def test_gpu_distshard_rccl_world1(gx_lib):
     """DistShard over a real RCCL process group (world size 1: every exchange is empty, but the
     size all-to-all, the stat reductions and the min/max agreement reduction run on RCCL)."""
