@@ -9,9 +9,10 @@ rounds (ExpireServer storm), the partition heals, and memberlist push-pull anti-
   python bench.py [--gpus N --steps K --warmup W] [--config cfg5|cfg2|cfg3|cfg4] [--no-converge]
 
 Prints ONE JSON line (rank 0). N>1 runs one process per GPU (torch.distributed.run): the same
-cluster is sharded by host block over the N GPUs and every round's cross-shard
-packets and push-pull rows move by RCCL all-to-all over xGMI, so the total work is fixed
-(strong scaling). Results are bit-identical to the 1-GPU run.
+cluster is sharded by host block over the N GPUs. Every round's cross-shard packets,
+and on push-pull rounds the row digests and the differing row blocks, move by RCCL all-to-all over
+xGMI, so the total work is fixed (strong scaling); `exchange` reports the bytes moved. Results are
+bit-identical to the 1-GPU run.
 """
 import argparse
 import json
@@ -69,7 +70,7 @@ def merges(st):
 class Cluster:
     """The benchmarked cluster: one engine (N=1) or this rank's shard (N>1, sidecar_amd.dist)."""
 
-    def __init__(self, lib, cfg, seed, rank, world, local_rank, barrier):
+    def __init__(self, lib, cfg, seed, rank, world, local_rank, barrier, device=None):
         self.world = world
         self.barrier = barrier
         if world == 1:
@@ -79,7 +80,7 @@ class Cluster:
             from sidecar_amd.dist import DistShard
             kw = dict(CONFIGS[cfg]["p"])
             kw["seed"] = seed
-            self.shard = DistShard(lib, rank, world, f"cuda:{local_rank}", **kw)
+            self.shard = DistShard(lib, rank, world, device or f"cuda:{local_rank}", **kw)
             self.e = self.shard.e
 
     @property
@@ -98,14 +99,25 @@ class Cluster:
     def converged(self):
         return self.e.converged() if self.shard is None else self.shard.converged()
 
+    def exchange_bytes(self):
+        """Bytes moved between GPUs by the whole job (summed over ranks); None at N = 1."""
+        if self.shard is None:
+            return None
+        w = self.shard.wire.as_dict()
+        keys = sorted(w)
+        import torch
+        t = torch.tensor([w[k] for k in keys], dtype=torch.int64, device=self.shard.device)
+        self.shard.dist.all_reduce(t, op=self.shard.dist.ReduceOp.SUM, group=self.shard.group)
+        return dict(zip(keys, [int(x) for x in t.tolist()]))
+
     def close(self):
         self.e.close()
 
 
-def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every):
+def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
     """Fresh cluster from round 0: chunks of `check_every` rounds, catalog agreement checked
     between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run)."""
-    c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier)
+    c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier, device)
     wall = 0.0
     conv = None
     try:
@@ -192,12 +204,15 @@ def main():
     if args.warmup:
         c.run_rounds(args.warmup)
     st0, tm0 = c.stats(), e.timing()
+    x0 = c.exchange_bytes()
     barrier()
     t0 = time.perf_counter()
     c.run_rounds(args.steps)
     barrier()
     dt = time.perf_counter() - t0
     st1, tm1 = c.stats(), e.timing()
+    x1 = c.exchange_bytes()
+    xfer = {k: x1[k] - x0[k] for k in x1} if x1 else None
     c.close()
 
     split = {k: st1[k] - st0[k] for k in ("gossip_merges", "ae_merges", "local_merges")}
@@ -256,6 +271,7 @@ def main():
                        "fanout": cfgp.get("fanout", 3),
                        "parallelism": f"host-sharded over {world} GPUs (RCCL all-to-all)" if world > 1 else "single GPU"},
             "merges": split, "converge": conv, "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+            "exchange": xfer,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
