@@ -43,6 +43,7 @@ extern "C" {
 #define GX_ENOMEM (-12)
 #define GX_EINVAL (-22)
 #define GX_ENOSYS (-38)
+#define GX_ENOENT (-2)
 
 /* service.Service.Status values, service/service.go:17-23. GX_ABSENT marks an empty slot. */
 #define GX_ALIVE 0
@@ -186,7 +187,9 @@ typedef struct gx_stats {
   uint64_t ae_slots;         /* view slots streamed by anti-entropy merges (both directions) */
   uint64_t bytes_sent;       /* byte-limit mode: sum of len(message) + overhead of sent records */
   uint64_t cap_cuts;         /* byte-limit mode: packets cut by packet_cap before the byte limit */
-  uint64_t reserved[3];
+  uint64_t change_events;    /* ServiceChanged calls (services_state.go:195-199), all views */
+  uint64_t listener_drops;   /* ChangeEvents a full listener channel did not take (:230-236) */
+  uint64_t reserved[1];
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */
@@ -327,6 +330,42 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
 int gx_merge_remote_state(gx_engine *e, uint32_t view, const gx_service *svcs, uint32_t n);
 /* NotifyLeave (:173-176) -> ExpireServer(node). */
 int gx_notify_leave(gx_engine *e, uint32_t view, uint32_t node);
+
+/* ---- change bookkeeping and listeners --------------------------------------
+ * Every ServiceChanged (services_state.go:195-199) of a view sets its Server's LastUpdated and
+ * LastChanged and the view's state.LastChanged to the changed record's Updated, and notifies the
+ * view's listeners. A newer record that keeps its status sets only LastUpdated (:321-323). The
+ * call sites are AddServiceEntry (insert, previous status UNKNOWN; status change), the lifespan
+ * expiry of TombstoneOthersServices (Updated + 1 s), TombstoneServices and ExpireServer (now).
+ * "Last" is processing order: arrival order for gossip packets, key order for push-pull,
+ * Merge and expiry scans, owner then service order for ExpireServer storms.
+ * Initial catalogs (GX_INIT_OWN/WARM) count as inserted in key order, without events. */
+typedef struct gx_server_times {
+  int64_t last_updated_ns; /* Server.LastUpdated; 0 = time.Unix(0, 0) (NewServer, :57-66) */
+  int64_t last_changed_ns; /* Server.LastChanged */
+} gx_server_times;
+typedef struct gx_change_event { /* catalog.ChangeEvent (services_state.go:38-43) */
+  gx_service service;            /* the record after the change */
+  int64_t time_ns;               /* Time = state.LastChanged at the notification */
+  uint32_t previous_status;      /* PreviousStatus; GX_UNKNOWN for a new record */
+  uint32_t pad;
+} gx_change_event;
+#define GX_MAX_LISTENERS 64
+#define GX_LISTENER_MAX_CAPACITY 65536
+/* Server times of owners [owner_lo, owner_hi) in `view`; meaningful while the server exists
+ * (the view holds a record of it). */
+int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t owner_lo, uint32_t owner_hi,
+                         gx_server_times *out);
+int gx_read_last_changed(gx_engine *e, uint32_t view_lo, uint32_t view_hi, int64_t *out);
+/* AddListener (:253-268): listener `id` of `view` with a channel buffered for `capacity` events.
+ * Capacity 0 is refused like an unbuffered channel (GX_EINVAL); re-adding an id replaces it.
+ * Events reach it with the channel's non-blocking send: a full channel drops the event
+ * (listener_drops), :230-236. */
+int gx_add_listener(gx_engine *e, uint32_t view, uint32_t id, uint32_t capacity);
+int gx_remove_listener(gx_engine *e, uint32_t view, uint32_t id); /* :272-284; GX_ENOENT */
+/* Receive the listener's buffered events, oldest first (at most cap; n_out = received). */
+int gx_listener_drain(gx_engine *e, uint32_t view, uint32_t id, gx_change_event *out, uint32_t cap,
+                      uint32_t *n_out);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */
 int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);

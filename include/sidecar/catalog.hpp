@@ -13,6 +13,7 @@
 // oracle in tests).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -38,6 +39,19 @@ struct Service {
   bool operator==(const Service &o) const {
     return ID == o.ID && Hostname == o.Hostname && Updated == o.Updated && Status == o.Status;
   }
+};
+
+// catalog.ChangeEvent (services_state.go:38-43)
+struct ChangeEvent {
+  Service Svc;
+  int PreviousStatus = UNKNOWN;
+  int64_t Time = 0;
+};
+
+// Server.LastUpdated / LastChanged (services_state.go:49-54); 0 = time.Unix(0, 0)
+struct ServerTimes {
+  int64_t LastUpdated = 0;
+  int64_t LastChanged = 0;
 };
 
 inline void check(int rc, const char *what) {
@@ -208,6 +222,46 @@ class ServicesState {
     check(gx_is_new_service(c_.engine(), self_, &r, &x), "IsNewService");
     return x != 0;
   }
+  // state.LastChanged
+  int64_t LastChanged() const {
+    int64_t t = 0;
+    check(gx_read_last_changed(c_.engine(), self_, self_ + 1, &t), "LastChanged");
+    return t;
+  }
+  // state.Servers[hostname].LastUpdated / LastChanged
+  ServerTimes Times(const std::string &hostname) {
+    gx_server_times t{};
+    uint32_t o = c_.Host(hostname);
+    check(gx_read_server_times(c_.engine(), self_, o, o + 1, &t), "ServerTimes");
+    return {t.last_updated_ns, t.last_changed_ns};
+  }
+  // AddListener (:253-268): false when refused (an unbuffered channel, capacity 0)
+  bool AddListener(const std::string &name, uint32_t capacity) {
+    return gx_add_listener(c_.engine(), self_, ListenerId(name), capacity) == GX_OK;
+  }
+  // RemoveListener (:272-284): false = "no listener found with the name"
+  bool RemoveListener(const std::string &name) {
+    return gx_remove_listener(c_.engine(), self_, ListenerId(name)) == GX_OK;
+  }
+  // Receive everything buffered on a listener's channel, oldest first.
+  std::vector<ChangeEvent> Receive(const std::string &name) {
+    std::vector<gx_change_event> buf(GX_LISTENER_MAX_CAPACITY < 4096 ? GX_LISTENER_MAX_CAPACITY : 4096);
+    std::vector<ChangeEvent> out;
+    for (;;) {
+      uint32_t n = 0;
+      check(gx_listener_drain(c_.engine(), self_, ListenerId(name), buf.data(), (uint32_t)buf.size(), &n),
+            "listener_drain");
+      for (uint32_t i = 0; i < n; i++) out.push_back({c_.Svc(buf[i].service), (int)buf[i].previous_status, buf[i].time_ns});
+      if (n < buf.size()) return out;
+    }
+  }
+  // EachServiceSorted (catalog/view.go:14-26): by Updated; ties in key order (Go's sort.Sort
+  // leaves them unspecified).
+  std::vector<Service> EachServiceSorted() {
+    auto v = EachService();
+    std::stable_sort(v.begin(), v.end(), [](const Service &a, const Service &b) { return a.Updated < b.Updated; });
+    return v;
+  }
   // state.Servers[hostname].Services[id], or nothing
   std::optional<Service> Get(const std::string &hostname, const std::string &id) {
     for (auto &s : EachService())
@@ -234,9 +288,17 @@ class ServicesState {
     check(gx_write_slot(c_.engine(), self_, &r), "write_slot");
   }
   uint32_t index() const { return self_; }
+  uint32_t ListenerId(const std::string &name) {
+    auto it = listener_ids_.find(name);
+    if (it != listener_ids_.end()) return it->second;
+    uint32_t id = (uint32_t)listener_ids_.size();
+    listener_ids_[name] = id;
+    return id;
+  }
 
  private:
   Cluster &c_;
+  std::map<std::string, uint32_t> listener_ids_;
 
  public:
   const std::string Hostname;

@@ -59,6 +59,12 @@ struct gx_engine {
   uint32_t *in_cnt;     /* H + 1 */
   uint32_t *in_list;    /* H * K  (sender * K + j), grouped by receiver, sender-ascending */
   uint16_t *sbytes;     /* R  encoded bytes of every Service field but Updated and Status */
+  gx_server_times *srvt; /* H * H  Server.LastUpdated / LastChanged per (view, owner) */
+  int64_t *vlc;          /* H  state.LastChanged per view */
+  struct olistener {
+    uint32_t used, view, id, cap, head, count;
+    gx_change_event *ring;
+  } lst[GX_MAX_LISTENERS];
   int64_t ae_local_round; /* round whose shard-local push-pull pairs gx_ae_merge_local merged */
   gx_stats st;
 };
@@ -300,6 +306,38 @@ static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *p
   return l;
 }
 
+/* ------------------------------------------------------ change bookkeeping -- */
+/* NotifyListeners (services_state.go:218-240): a non-blocking send to every listener. */
+static void notify_listeners(gx_engine *e, uint32_t v, uint32_t r, uint64_t nw, int prev) {
+  for (int i = 0; i < GX_MAX_LISTENERS; i++) {
+    struct olistener *l = &e->lst[i];
+    if (!l->used || l->view != v) continue;
+    if (l->count >= l->cap) { /* select { case ch <- event: default: warn } */
+      e->st.listener_drops++;
+      continue;
+    }
+    gx_change_event *ev = &l->ring[(l->head + l->count) % l->cap];
+    memset(ev, 0, sizeof *ev);
+    ev->service.updated_ns = ts_of(nw);
+    ev->service.host = r / e->S;
+    ev->service.svc = (uint16_t)(r % e->S);
+    ev->service.status = (uint8_t)st_of(nw);
+    ev->time_ns = e->vlc[v];
+    ev->previous_status = (uint32_t)prev;
+    l->count++;
+  }
+}
+/* ServiceChanged (:195-199) = serverChanged (:204-215) + NotifyListeners. */
+static void service_changed(gx_engine *e, uint32_t v, uint32_t r, uint64_t nw, int prev) {
+  int64_t ts = ts_of(nw);
+  gx_server_times *t = &e->srvt[(size_t)v * e->H + r / e->S];
+  t->last_updated_ns = ts;
+  t->last_changed_ns = ts;
+  e->vlc[v] = ts;
+  e->st.change_events++;
+  notify_listeners(e, v, r, nw, prev);
+}
+
 /* ---------------------------------------------------------------------- catalog semantics -- */
 /* AddServiceEntry, catalog/services_state.go:293-347 (+ IsStale service/service.go:68-72,
  * Invalidates :64-66, retransmit :377-392). */
@@ -324,6 +362,12 @@ static int add_entry(gx_engine *e, uint32_t v, grec u, int64_t now, int src) {
     return 0; /* equal or older: keep the first arrival */
   }
   set_slot(e, slot, nw);
+  if (st_of(old) == GX_ABSENT) {
+    service_changed(e, v, u.r, nw, GX_UNKNOWN); /* ServiceChanged(&newSvc, UNKNOWN, ...) (:319) */
+  } else {
+    e->srvt[(size_t)v * e->H + u.r / e->S].last_updated_ns = ts; /* server.LastUpdated (:323) */
+    if (st_of(old) != st_of(nw)) service_changed(e, v, u.r, nw, st_of(old)); /* (:338-340) */
+  }
   if (src == SRC_GOSSIP) e->st.gossip_accepts++;
   else if (src == SRC_AE) e->st.ae_accepts++;
   else e->st.local_accepts++;
@@ -355,6 +399,7 @@ static uint32_t scan_view(gx_engine *e, uint32_t v, int64_t now, grec *out, uint
       if (ts < now - life) { /* (:655-679): TOMBSTONE at Updated + 1s */
         uint64_t nw = pack(ts + e->p.tombstone_bump_ns, GX_TOMBSTONE);
         set_slot(e, &row[r], nw);
+        service_changed(e, v, r, nw, st); /* (:673-676) */
         e->st.expired++;
         if (n < cap) {
           out[n].w = nw;
@@ -379,6 +424,7 @@ static uint32_t tombstone_services(gx_engine *e, uint32_t o, uint64_t running, i
     if (st_of(w) == GX_ABSENT || ((running >> s) & 1ull) || st_of(w) == GX_TOMBSTONE) continue;
     uint64_t nw = pack(now, GX_TOMBSTONE); /* svc.Tombstone(): Updated = now (service.go:91-94) */
     set_slot(e, &row[r], nw);
+    service_changed(e, o, r, nw, st_of(w)); /* (:703-705) */
     e->st.own_tombstones++;
     for (int k = 0; k < 2; k++) { /* appended twice (:707-710) */
       if (n < cap) {
@@ -405,7 +451,11 @@ static int expire_server(gx_engine *e, uint32_t v, uint32_t o, int64_t now) {
   }
   if (!live) return 0; /* no server / no services / no live services (:154-170) */
   for (uint32_t s = 0; s < e->S; s++)
-    if ((mask >> s) & 1ull) set_slot(e, &row[s], pack(now, GX_TOMBSTONE)); /* (:176-181) */
+    if ((mask >> s) & 1ull) { /* Tombstone() + ServiceChanged for every record (:176-181) */
+      int prev = st_of(row[s]);
+      set_slot(e, &row[s], pack(now, GX_TOMBSTONE));
+      service_changed(e, v, o * e->S + s, row[s], prev);
+    }
   e->st.expire_server++;
   gx_job j = {(uint64_t)now, mask, o, meta_of(GX_JOB_EXPIRE, 0, e->p.tombstone_count), 0, 0};
   push_job(e, v, &j); /* SendServices(tombstones, TOMBSTONE_COUNT) (:188-191) */
@@ -810,6 +860,18 @@ static void init_state(gx_engine *e) {
       for (uint32_t v = 0; v < H; v++) e->view[(size_t)v * R + r] = w;
     }
   }
+  /* initial records count as inserted in key order (no events): LastUpdated = LastChanged = the
+   * owner's last record, state.LastChanged = the view's last record */
+  memset(e->srvt, 0, sizeof(gx_server_times) * (size_t)H * H);
+  memset(e->vlc, 0, sizeof(int64_t) * H);
+  for (uint32_t v = 0; v < H && p->init_mode != GX_INIT_EMPTY; v++)
+    for (uint32_t r = 0; r < R; r++) {
+      uint64_t w = e->view[(size_t)v * R + r];
+      if (st_of(w) == GX_ABSENT) continue;
+      e->srvt[(size_t)v * H + r / S].last_updated_ns = ts_of(w);
+      e->srvt[(size_t)v * H + r / S].last_changed_ns = ts_of(w);
+      e->vlc[v] = ts_of(w);
+    }
   memset(e->own_status, GX_ALIVE, (size_t)H * S);
   for (uint32_t o = 0; o < H; o++) {
     gx_host_state *h = &e->hs[o];
@@ -859,6 +921,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->in_cnt = (uint32_t *)calloc(H + 1, sizeof(uint32_t));
   e->in_list = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
   e->sbytes = (uint16_t *)malloc(sizeof(uint16_t) * e->R);
+  e->srvt = (gx_server_times *)malloc(sizeof(gx_server_times) * H * H);
+  e->vlc = (int64_t *)malloc(sizeof(int64_t) * H);
   e->nblk = (e->R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
   e->x_round = e->x_delta_round = -1;
   if (e->G > 1) {
@@ -876,7 +940,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   }
   if (e->sbytes)
     for (uint32_t r = 0; r < e->R; r++) e->sbytes[r] = GX_STATIC_BYTES_DEFAULT;
-  if (!e->sbytes || !e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
+  if (!e->sbytes || !e->srvt || !e->vlc || !e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
       !e->arena_len || !e->msg || !e->msg_len || !e->msg_dst || !e->in_cnt || !e->in_list) {
     gx_destroy(e);
     return GX_ENOMEM;
@@ -903,6 +967,9 @@ int gx_destroy(gx_engine *e) {
   free(e->in_cnt);
   free(e->in_list);
   free(e->sbytes);
+  free(e->srvt);
+  free(e->vlc);
+  for (int i = 0; i < GX_MAX_LISTENERS; i++) free(e->lst[i].ring);
   free(e->x_t);
   free(e->x_mine);
   free(e->x_first);
@@ -1149,6 +1216,60 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
     n++;
   }
   if (n_out) *n_out = n;
+  return GX_OK;
+}
+
+int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, gx_server_times *out) {
+  if (!e || view >= e->H || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
+  memcpy(out, &e->srvt[(size_t)view * e->H + lo], sizeof(gx_server_times) * (hi - lo));
+  return GX_OK;
+}
+int gx_read_last_changed(gx_engine *e, uint32_t lo, uint32_t hi, int64_t *out) {
+  if (!e || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
+  memcpy(out, &e->vlc[lo], sizeof(int64_t) * (hi - lo));
+  return GX_OK;
+}
+static struct olistener *find_listener(gx_engine *e, uint32_t view, uint32_t id) {
+  for (int i = 0; i < GX_MAX_LISTENERS; i++)
+    if (e->lst[i].used && e->lst[i].view == view && e->lst[i].id == id) return &e->lst[i];
+  return NULL;
+}
+int gx_add_listener(gx_engine *e, uint32_t view, uint32_t id, uint32_t capacity) {
+  if (!e || view >= e->H || capacity < 1 || capacity > GX_LISTENER_MAX_CAPACITY) return GX_EINVAL;
+  struct olistener *l = find_listener(e, view, id);
+  if (!l)
+    for (int i = 0; i < GX_MAX_LISTENERS && !l; i++)
+      if (!e->lst[i].used) l = &e->lst[i];
+  if (!l) return GX_ENOMEM;
+  gx_change_event *ring = (gx_change_event *)calloc(capacity, sizeof(gx_change_event));
+  if (!ring) return GX_ENOMEM;
+  free(l->ring);
+  l->used = 1;
+  l->view = view;
+  l->id = id;
+  l->cap = capacity;
+  l->head = l->count = 0;
+  l->ring = ring;
+  return GX_OK;
+}
+int gx_remove_listener(gx_engine *e, uint32_t view, uint32_t id) {
+  if (!e) return GX_EINVAL;
+  struct olistener *l = find_listener(e, view, id);
+  if (!l) return GX_ENOENT;
+  free(l->ring);
+  memset(l, 0, sizeof *l);
+  return GX_OK;
+}
+int gx_listener_drain(gx_engine *e, uint32_t view, uint32_t id, gx_change_event *out, uint32_t cap,
+                      uint32_t *n_out) {
+  if (!e || !n_out || (cap && !out)) return GX_EINVAL;
+  struct olistener *l = find_listener(e, view, id);
+  if (!l) return GX_ENOENT;
+  uint32_t n = l->count < cap ? l->count : cap;
+  for (uint32_t i = 0; i < n; i++) out[i] = l->ring[(l->head + i) % l->cap];
+  l->head = (l->head + n) % l->cap;
+  l->count -= n;
+  *n_out = n;
   return GX_OK;
 }
 

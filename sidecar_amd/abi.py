@@ -19,6 +19,7 @@ GX_OK = 0
 GX_EIO = -5
 GX_ENOMEM = -12
 GX_EINVAL = -22
+GX_ENOENT = -2
 GX_ENOSYS = -38
 
 ALIVE, TOMBSTONE, UNHEALTHY, UNKNOWN, DRAINING, ABSENT = 0, 1, 2, 3, 4, 7
@@ -85,6 +86,19 @@ class GxParams(C.Structure):
     ]
 
 
+class GxServerTimes(C.Structure):
+    _fields_ = [("last_updated_ns", C.c_int64), ("last_changed_ns", C.c_int64)]
+
+
+class GxChangeEvent(C.Structure):
+    _fields_ = [("service", GxService), ("time_ns", C.c_int64), ("previous_status", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+    def tup(self):
+        return (self.service.host, self.service.svc, self.service.updated_ns, self.service.status,
+                self.previous_status, self.time_ns)
+
+
 class GxHostState(C.Structure):
     _fields_ = [("fifo_head", C.c_uint32), ("fifo_tail", C.c_uint32), ("sleep_head", C.c_uint32),
                 ("sleep_tail", C.c_uint32), ("dq_head", C.c_uint32), ("dq_len", C.c_uint32),
@@ -99,7 +113,8 @@ class GxStats(C.Structure):
         "pending_drops", "dequeues", "nil_batches", "packets", "records_sent", "expired", "gc",
         "own_tombstones", "expire_server", "send_jobs", "ae_exchanges", "churn_events")] + [
         ("last_change_round", C.c_int64), ("scan_slots", C.c_uint64), ("ae_slots", C.c_uint64),
-        ("bytes_sent", C.c_uint64), ("cap_cuts", C.c_uint64), ("reserved", C.c_uint64 * 3)]
+        ("bytes_sent", C.c_uint64), ("cap_cuts", C.c_uint64), ("change_events", C.c_uint64),
+        ("listener_drops", C.c_uint64), ("reserved", C.c_uint64 * 1)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
@@ -124,7 +139,8 @@ ABI_FUNCS = [
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
-    "gx_view_minmax", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
+    "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
+    "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
 ]
 
 
@@ -168,6 +184,11 @@ def _declare(lib):
         "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64], i32),
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
         "gx_ae_merge_local": ([vp], i32),
+        "gx_read_server_times": ([vp, u32, u32, u32, vp], i32),
+        "gx_read_last_changed": ([vp, u32, u32, vp], i32),
+        "gx_add_listener": ([vp, u32, u32, u32], i32),
+        "gx_remove_listener": ([vp, u32, u32], i32),
+        "gx_listener_drain": ([vp, u32, u32, P(GxChangeEvent), u32, P(u32)], i32),
         "gx_ae_delta_bytes": ([vp, vp, C.c_uint64, vp], i32),
         "gx_ae_delta_pack": ([vp, vp, C.c_uint64], i32),
         "gx_get_broadcasts_bytes": ([vp, u32, u32, u32, P(GxService), u32, P(u32)], i32),
@@ -454,6 +475,35 @@ class Engine:
         n = C.c_uint32()
         check(self.lib.gx_read_list(self.h, host, slot, out, 1024, C.byref(n)))
         return [out[i] for i in range(min(n.value, 1024))]
+
+    def server_times(self, view: int, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
+        """Server.LastUpdated / LastChanged of owners [lo, hi) in `view`: int64 [n, 2]."""
+        hi = self.H if hi is None else hi
+        out = np.empty((hi - lo, 2), dtype=np.int64)
+        check(self.lib.gx_read_server_times(self.h, view, lo, hi, out.ctypes.data_as(C.c_void_p)),
+              "gx_read_server_times")
+        return out
+
+    def last_changed(self, lo: Optional[int] = None, hi: Optional[int] = None) -> np.ndarray:
+        """state.LastChanged of views [lo, hi)."""
+        lo = self.lo if lo is None else lo
+        hi = self.hi if hi is None else hi
+        out = np.empty(hi - lo, dtype=np.int64)
+        check(self.lib.gx_read_last_changed(self.h, lo, hi, out.ctypes.data_as(C.c_void_p)),
+              "gx_read_last_changed")
+        return out
+
+    def add_listener(self, view: int, lid: int, capacity: int):
+        check(self.lib.gx_add_listener(self.h, view, lid, capacity), "gx_add_listener")
+
+    def remove_listener(self, view: int, lid: int) -> int:
+        return self.lib.gx_remove_listener(self.h, view, lid)
+
+    def drain_listener(self, view: int, lid: int, cap: int = 4096):
+        out = (GxChangeEvent * max(1, cap))()
+        n = C.c_uint32()
+        check(self.lib.gx_listener_drain(self.h, view, lid, out, cap, C.byref(n)), "gx_listener_drain")
+        return [out[i] for i in range(n.value)]
 
     def digests(self) -> np.ndarray:
         out = np.empty(self.hi - self.lo, dtype=np.uint64)

@@ -34,7 +34,7 @@ enum {
   C_GOSSIP_MERGES, C_AE_MERGES, C_LOCAL_MERGES, C_GOSSIP_ACC, C_AE_ACC, C_LOCAL_ACC, C_STALE,
   C_RETX, C_QDROP, C_LDROP, C_SDROP, C_PDROP, C_DEQ, C_NIL, C_PACKETS, C_RECSENT, C_EXPIRED,
   C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_BYTESENT,
-  C_CAPCUT, C_NCTR
+  C_CAPCUT, C_CHG, C_NCTR
 };
 
 #define GX_SHARDS 64
@@ -77,6 +77,12 @@ struct Dev {
   uint32_t *scan_cnt;  // [H]
   uint8_t *tick;       // [H] BroadcastTombstones tick this round
   uint16_t *sbytes;    // [R] static encoded bytes per record key (every field but Updated/Status)
+  gx_server_times *srvt;  // [Hl][H] Server.LastUpdated / LastChanged per (view, owner)
+  int64_t *vlc;           // [Hl] state.LastChanged
+  int32_t *ev_slot;       // [Hl] event log of a listening view, -1 = no listener
+  gx_change_event *ev_log;  // [n_logs][ev_cap] ChangeEvents in processing order
+  uint32_t *ev_cnt;       // [n_logs] events since the last delivery (may exceed ev_cap)
+  uint32_t ev_cap;
   DevCtr *ctr;
 };
 
@@ -186,6 +192,36 @@ GXD void set_slot(const Dev &d, Acc &a, uint32_t v, uint64_t *slot, uint64_t nw)
     a.changed = true;
     atomicMin(&d.minexp[li(d, v)], exp_time(d.p, nw));
   }
+}
+
+// --------------------------------------------------- change bookkeeping --
+GXD gx_server_times *srv_times(const Dev &d, uint32_t v, uint32_t o) {
+  return &d.srvt[(size_t)li(d, v) * d.H + o];
+}
+// ChangeEvent at position pos of view v's log (listening views only).
+GXD void ev_put(const Dev &d, int32_t k, uint32_t pos, uint32_t r, uint64_t nw, int prev) {
+  if (pos >= d.ev_cap) return;
+  gx_change_event ev;
+  ev.service.updated_ns = ts_of(nw);
+  ev.service.host = r / d.S;
+  ev.service.svc = (uint16_t)(r % d.S);
+  ev.service.status = (uint8_t)st_of(nw);
+  ev.service.flags = 0;
+  ev.time_ns = ts_of(nw);
+  ev.previous_status = (uint32_t)prev;
+  ev.pad = 0;
+  d.ev_log[(size_t)k * d.ev_cap + pos] = ev;
+}
+// ServiceChanged (services_state.go:195-199) from a path that owns view v alone (one thread).
+GXD void svc_changed(const Dev &d, Acc &a, uint32_t v, uint32_t r, uint64_t nw, int prev) {
+  int64_t ts = ts_of(nw);
+  gx_server_times *t = srv_times(d, v, r / d.S);
+  t->last_updated_ns = ts;
+  t->last_changed_ns = ts;
+  d.vlc[li(d, v)] = ts;
+  a.c[C_CHG]++;
+  int32_t k = d.ev_slot[li(d, v)];
+  if (k >= 0) ev_put(d, k, d.ev_cnt[k]++, r, nw, prev);
 }
 
 // ----------------------------------------------------------------------- broadcast FIFO --
@@ -499,7 +535,14 @@ GXD bool add_entry(const Dev &d, Acc &a, uint32_t v, grec u, int src) {
     return false;
   }
   if (!acc) return false;
+  uint64_t old = *slot;
   set_slot(d, a, v, slot, nw);
+  if (st_of(old) == GX_ABSENT) {
+    svc_changed(d, a, v, u.r, nw, GX_UNKNOWN);  // ServiceChanged(&newSvc, UNKNOWN, ...) (:319)
+  } else {
+    srv_times(d, v, u.r / d.S)->last_updated_ns = ts_of(nw);  // server.LastUpdated (:323)
+    if (st_of(old) != st_of(nw)) svc_changed(d, a, v, u.r, nw, st_of(old));  // (:338-340)
+  }
   a.c[src == SRC_GOSSIP ? C_GOSSIP_ACC : src == SRC_AE ? C_AE_ACC : C_LOCAL_ACC]++;
   if (u.r / d.S != v) {  // retransmit foreign records only (services_state.go:377-392)
     if (push_job(d, a, v, make_job(nw, 0, u.r, meta_of(GX_JOB_RETX, 0, 1)))) a.c[C_RETX]++;
@@ -538,6 +581,7 @@ GXD uint64_t tombstone_services(const Dev &d, Acc &a, uint32_t o, uint64_t runni
     uint64_t w = row[s];
     if (st_of(w) == GX_ABSENT || ((running >> s) & 1ull) || st_of(w) == GX_TOMBSTONE) continue;
     set_slot(d, a, o, &row[s], pack(d.now, GX_TOMBSTONE));  // svc.Tombstone() (service.go:91-94)
+    svc_changed(d, a, o, o * d.S + s, row[s], st_of(w));     // (:703-705)
     m |= 1ull << s;
   }
   a.c[C_OWNTOMB] += (unsigned)__popcll(m);
@@ -557,7 +601,11 @@ GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
   }
   if (!live) return false;  // no server / no services / no live services (:154-170)
   for (uint32_t s = 0; s < d.S; s++)
-    if ((mask >> s) & 1ull) set_slot(d, a, v, &row[s], pack(d.now, GX_TOMBSTONE));
+    if ((mask >> s) & 1ull) {  // Tombstone() + ServiceChanged for every record (:176-181)
+      int prev = st_of(row[s]);
+      set_slot(d, a, v, &row[s], pack(d.now, GX_TOMBSTONE));
+      svc_changed(d, a, v, o * d.S + s, row[s], prev);
+    }
   a.c[C_EXPSRV]++;
   push_job(d, a, v, make_job((uint64_t)d.now, mask, o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count)));
   return true;

@@ -24,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <deque>
 #include <vector>
 
 
@@ -79,6 +80,14 @@ struct gx_engine {
   int ae_delta_round;
   int ae_planned_round;
   int64_t ae_local_round;
+  // listeners: host-side channels fed from the per-view device event logs
+  struct Listener {
+    uint32_t view, id, cap;
+    std::deque<gx_change_event> ring;
+  };
+  std::vector<Listener> listeners;
+  std::vector<uint32_t> log_views;  // view of each device event log
+  uint64_t listener_drops;
   // small device scratch for single-host ABI calls
   void *api_dev;
   size_t api_dev_bytes;
@@ -139,10 +148,38 @@ static int drain_timing(gx_engine *e) {
   return GX_OK;
 }
 
+// Deliver the device event logs into the listeners' channels (non-blocking sends: a full
+// channel drops the event, services_state.go:230-236) and reset the logs. Channels are drained
+// only between ABI calls, so each listener receives a prefix of its view's events.
+static int deliver_events(gx_engine *e) {
+  size_t nlog = e->log_views.size();
+  if (!nlog) return GX_OK;
+  std::vector<uint32_t> cnt(nlog);
+  HIPCHK(hipMemcpy(cnt.data(), e->d.ev_cnt, sizeof(uint32_t) * nlog, hipMemcpyDeviceToHost));
+  bool any = false;
+  for (uint32_t c : cnt) any |= c != 0;
+  if (!any) return GX_OK;
+  for (size_t k = 0; k < nlog; k++) {
+    if (!cnt[k]) continue;
+    uint32_t n = cnt[k] < e->d.ev_cap ? cnt[k] : e->d.ev_cap;
+    std::vector<gx_change_event> ev(n);
+    HIPCHK(hipMemcpy(ev.data(), &e->d.ev_log[k * e->d.ev_cap], sizeof(gx_change_event) * n, hipMemcpyDeviceToHost));
+    for (auto &l : e->listeners) {
+      if (l.view != e->log_views[k]) continue;
+      uint32_t room = l.cap - (uint32_t)l.ring.size();
+      uint32_t take = cnt[k] < room ? cnt[k] : room;  // take <= n: ev_cap >= every capacity
+      for (uint32_t i = 0; i < take; i++) l.ring.push_back(ev[i]);
+      e->listener_drops += cnt[k] - take;
+    }
+  }
+  HIPCHK(hipMemset(e->d.ev_cnt, 0, sizeof(uint32_t) * nlog));
+  return GX_OK;
+}
+
 static int sync_check(gx_engine *e) {
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipGetLastError());
-  return GX_OK;
+  return e->log_views.empty() ? GX_OK : deliver_events(e);
 }
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
@@ -316,7 +353,7 @@ int gx_destroy(gx_engine *e) {
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
-                  d.sbytes, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
+                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -411,6 +448,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
   ALLOC(d.tick, H);
   ALLOC(d.sbytes, sizeof(uint16_t) * d.R);
+  ALLOC(d.srvt, sizeof(gx_server_times) * H * Hg);
+  ALLOC(d.vlc, sizeof(int64_t) * H);
+  ALLOC(d.ev_slot, sizeof(int32_t) * H);
   ALLOC(d.ctr, sizeof(DevCtr));
   ALLOC(e->own_list, sizeof(grec) * H * d.S);
   ALLOC(e->conv_bad, sizeof(unsigned long long));
@@ -440,10 +480,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
   HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * Hg * K, s));
   HIPCHK(hipMemsetAsync(d.in_cnt, 0, sizeof(uint32_t) * in_pad, s));
   HIPCHK(hipMemsetAsync(d.tick, 0, H, s));
+  HIPCHK(hipMemsetAsync(d.ev_slot, 0xff, sizeof(int32_t) * H, s));  // -1: no listener
   k_fill_u16<<<256, 256, 0, s>>>(d.sbytes, d.R, (uint16_t)GX_STATIC_BYTES_DEFAULT);
   set_round_fields(e);
   k_init_rec<<<nblk(d.R, 256), 256, 0, s>>>(d, rec_word);
   k_init_views<<<2048, 256, 0, s>>>(d, rec_word);
+  k_init_times<<<2048, 256, 0, s>>>(d, rec_word);
   k_init_hosts<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   k_minexp_recompute<<<d.Hl, 256, 0, s>>>(d, 0);
   rc = sync_check(e);
@@ -787,6 +829,105 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
   }
   if (n_out) *n_out = n;
   return GX_OK;
+}
+
+int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, gx_server_times *out) {
+  if (!e || !own(e, view) || lo > hi || hi > e->d.H || (hi > lo && !out)) return GX_EINVAL;
+  if (hi == lo) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(out, &e->d.srvt[(size_t)(view - e->d.lo) * e->d.H + lo], sizeof(gx_server_times) * (hi - lo),
+                   hipMemcpyDeviceToHost));
+  return GX_OK;
+}
+
+int gx_read_last_changed(gx_engine *e, uint32_t lo, uint32_t hi, int64_t *out) {
+  if (!e || lo > hi || (hi > lo && (!out || !own(e, lo) || !own(e, hi - 1)))) return GX_EINVAL;
+  if (hi == lo) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(out, &e->d.vlc[lo - e->d.lo], sizeof(int64_t) * (hi - lo), hipMemcpyDeviceToHost));
+  return GX_OK;
+}
+
+// Device event logs: one per listening view, sized for the largest channel capacity.
+static int rebuild_logs(gx_engine *e) {
+  Dev &d = e->d;
+  std::vector<uint32_t> views;
+  uint32_t cap = 0;
+  for (auto &l : e->listeners) {
+    bool seen = false;
+    for (uint32_t v : views) seen |= v == l.view;
+    if (!seen) views.push_back(l.view);
+    cap = l.cap > cap ? l.cap : cap;
+  }
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (d.ev_log) (void)hipFree(d.ev_log);
+  if (d.ev_cnt) (void)hipFree(d.ev_cnt);
+  d.ev_log = nullptr;
+  d.ev_cnt = nullptr;
+  d.ev_cap = 0;
+  HIPCHK(hipMemset(d.ev_slot, 0xff, sizeof(int32_t) * d.Hl));
+  e->log_views = views;
+  if (views.empty()) return GX_OK;
+  if (hipMalloc((void **)&d.ev_log, sizeof(gx_change_event) * cap * views.size()) != hipSuccess ||
+      hipMalloc((void **)&d.ev_cnt, sizeof(uint32_t) * views.size()) != hipSuccess) {
+    (void)hipGetLastError();
+    e->listeners.clear();
+    e->log_views.clear();
+    return GX_ENOMEM;
+  }
+  d.ev_cap = cap;
+  HIPCHK(hipMemset(d.ev_cnt, 0, sizeof(uint32_t) * views.size()));
+  for (size_t k = 0; k < views.size(); k++) {
+    int32_t slot = (int32_t)k;
+    HIPCHK(hipMemcpy(&d.ev_slot[views[k] - d.lo], &slot, sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  return GX_OK;
+}
+
+int gx_add_listener(gx_engine *e, uint32_t view, uint32_t id, uint32_t capacity) {
+  if (!e || !own(e, view) || capacity < 1 || capacity > GX_LISTENER_MAX_CAPACITY) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  bool found = false;
+  for (auto &l : e->listeners)
+    if (l.view == view && l.id == id) {
+      l.cap = capacity;
+      l.ring.clear();
+      found = true;
+    }
+  if (!found) {
+    if (e->listeners.size() >= GX_MAX_LISTENERS) return GX_ENOMEM;
+    e->listeners.push_back({view, id, capacity, {}});
+  }
+  return rebuild_logs(e);
+}
+
+int gx_remove_listener(gx_engine *e, uint32_t view, uint32_t id) {
+  if (!e) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  for (size_t i = 0; i < e->listeners.size(); i++)
+    if (e->listeners[i].view == view && e->listeners[i].id == id) {
+      e->listeners.erase(e->listeners.begin() + (long)i);
+      return rebuild_logs(e);
+    }
+  return GX_ENOENT;
+}
+
+int gx_listener_drain(gx_engine *e, uint32_t view, uint32_t id, gx_change_event *out, uint32_t cap,
+                      uint32_t *n_out) {
+  if (!e || !n_out || (cap && !out)) return GX_EINVAL;
+  for (auto &l : e->listeners)
+    if (l.view == view && l.id == id) {
+      uint32_t n = (uint32_t)l.ring.size() < cap ? (uint32_t)l.ring.size() : cap;
+      for (uint32_t i = 0; i < n; i++) {
+        out[i] = l.ring.front();
+        l.ring.pop_front();
+      }
+      *n_out = n;
+      return GX_OK;
+    }
+  return GX_ENOENT;
 }
 
 int gx_read_views(gx_engine *e, uint32_t lo, uint32_t hi, uint64_t *out) {
@@ -1248,6 +1389,8 @@ int gx_stats_get(gx_engine *e, gx_stats *out) {
   out->send_jobs = c[C_SENDJOBS];
   out->ae_exchanges = c[C_AEX];
   out->churn_events = c[C_CHURN];
+  out->change_events = c[C_CHG];
+  out->listener_drops = e->listener_drops;
   out->bytes_sent = c[C_BYTESENT];
   out->cap_cuts = c[C_CAPCUT];
   out->scan_slots = c[C_SCANSLOTS];

@@ -73,6 +73,43 @@ __global__ void k_init_views(Dev d, const uint64_t *rec_word) {
   }
 }
 
+// Initial catalogs count as inserted in key order: LastUpdated = LastChanged = the owner's last
+// record, state.LastChanged = the view's last record (no events).
+__global__ void k_init_times(Dev d, const uint64_t *rec_word) {
+  size_t total = (size_t)d.Hl * d.H;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t vi = (uint32_t)(i / d.H), o = (uint32_t)(i % d.H), v = d.lo + vi;
+    gx_server_times t = {0, 0};
+    if (d.p.init_mode == GX_INIT_WARM || (d.p.init_mode == GX_INIT_OWN && o == v)) {
+      int64_t ts = ts_of(rec_word[(size_t)o * d.S + d.S - 1]);
+      t.last_updated_ns = ts;
+      t.last_changed_ns = ts;
+    }
+    d.srvt[i] = t;
+    if (o == 0) {
+      int64_t lc = 0;
+      if (d.p.init_mode == GX_INIT_WARM) lc = ts_of(rec_word[d.R - 1]);
+      else if (d.p.init_mode == GX_INIT_OWN) lc = ts_of(rec_word[(size_t)v * d.S + d.S - 1]);
+      d.vlc[vi] = lc;
+    }
+  }
+}
+
+// One tile's server times in key order: s_lu[i] / s_lc[i] = 1 + the last key of owner o0 + i
+// with an accepted / a status-changing record this tile (0 = none); the slot already holds the
+// stored word.
+GXD void tile_owner_times(const Dev &d, uint32_t x, const uint64_t *row, uint32_t o0, uint32_t n,
+                          const uint32_t *s_lu, const uint32_t *s_lc) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    uint32_t ku = s_lu[i], kc = s_lc[i];
+    if (!ku && !kc) continue;
+    gx_server_times *t = srv_times(d, x, o0 + i);
+    if (ku) t->last_updated_ns = ts_of(row[ku - 1]);
+    if (kc) t->last_changed_ns = ts_of(row[kc - 1]);
+  }
+}
+#define TILE_OWNERS 1026  // owners a 1024-slot tile can touch (S = 1, plus both ends)
+
 __global__ void k_init_hosts(Dev d) {
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= d.Hl) return;
@@ -164,6 +201,8 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
                                                uint32_t *cnt_out, int only_host) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
+  __shared__ uint32_t s_lu[TILE_OWNERS];
+  __shared__ uint32_t s_last;
   uint32_t oi = only_host >= 0 ? li(d, (uint32_t)only_host) : blockIdx.x;  // local index
   if (only_host < 0) {
     if (!d.tick[oi]) return;
@@ -177,6 +216,9 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   }
   uint64_t *row = &d.view[(size_t)oi * d.R];
   grec *list = &list_base[only_host >= 0 ? 0 : (size_t)oi * list_stride];
+  const int32_t evk = d.ev_slot[oi];
+  const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
+  uint32_t last_key = 0;  // 1 + the last expired key (state.LastChanged)
   uint32_t n_exp = 0;
   unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, mexp = ~0ull;
   uint32_t t = threadIdx.x;
@@ -238,13 +280,34 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
         list[pos[k]] = g;
       }
     }
-    n_exp += fld(tot, 0) + fld(tot, 1);
+    uint32_t tn = (uint32_t)(fld(tot, 0) + fld(tot, 1));
+    if (tn) {  // ServiceChanged per expiry (:673-676): server times, state.LastChanged, events
+      uint32_t o0 = base / d.S, oe = ((base + 4 * blockDim.x < d.R ? base + 4 * blockDim.x : d.R) - 1) / d.S;
+      for (uint32_t i = t; i <= oe - o0; i += blockDim.x) s_lu[i] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (!ex[k]) continue;
+        uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+        atomicMax(&s_lu[r / d.S - o0], r + 1);
+        if (pos[k] == n_exp + tn - 1) s_last = r + 1;
+        if (evk >= 0) ev_put(d, evk, ev0 + pos[k], r, nw[k], st_of(w[k]));
+      }
+      __syncthreads();
+      tile_owner_times(d, oi + d.lo, row, o0, oe - o0 + 1, s_lu, s_lu);
+      last_key = s_last;
+      __syncthreads();
+    }
+    n_exp += tn;
   }
   mexp = block_min(mexp, s_red);
   if (threadIdx.x == 0) {
     cnt_out[only_host >= 0 ? 0 : oi] = n_exp;
     d.minexp[oi] = mexp;  // exact bound after the scan
+    if (last_key) d.vlc[oi] = ts_of(row[last_key - 1]);
+    if (evk >= 0) d.ev_cnt[evk] = ev0 + n_exp;
   }
+  block_ctr(d, C_CHG, c_exp, s_red);
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && (threadIdx.x & 63) == 0) mark_change(d);
   c_wr = wave_sum(c_wr);
@@ -275,6 +338,7 @@ __global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
 __global__ __launch_bounds__(256) void k_storm(Dev d) {
   __shared__ unsigned long long s_mask[STORM_TILE];
   __shared__ uint32_t s_live[STORM_TILE];
+  __shared__ uint32_t s_ebase[STORM_TILE];
   __shared__ unsigned long long s_wave[4];
   uint32_t vi = blockIdx.x, v = d.lo + vi;
   uint32_t half = d.H / 2;
@@ -282,9 +346,11 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   gx_host_state *h = &d.hs[vi];
   uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
-  uint32_t jobs = 0;
-  unsigned long long c_wr = 0;
+  uint32_t jobs = 0, n_ev = 0;
+  unsigned long long c_wr = 0, c_chg = 0;
   uint64_t tomb = pack(d.now, GX_TOMBSTONE);
+  const int32_t evk = d.ev_slot[vi];
+  const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
   uint32_t OT = STORM_TILE / d.S;
   uint32_t t = threadIdx.x;
   for (uint32_t ob = lo; ob < hi; ob += OT) {
@@ -318,14 +384,36 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
     for (uint32_t i0 = 0; i0 < on; i0 += blockDim.x) {  // EXPIRE jobs in owner order
       uint32_t i = i0 + t;
       bool live = i < on && s_live[i];
+      uint32_t ec = live ? (uint32_t)__popcll(s_mask[i]) : 0u;  // ServiceChanged per record
       unsigned long long tot;
-      uint32_t pos = (uint32_t)block_excl_scan64(live ? 1ull : 0ull, s_wave, tot);
+      unsigned long long pre = block_excl_scan64((live ? 1ull : 0ull) | ((unsigned long long)ec << 16), s_wave, tot);
+      uint32_t pos = (uint32_t)fld(pre, 0);
       if (live && jobs + pos < room)
         d.fifo[(size_t)vi * d.Q + ((tail0 + jobs + pos) % d.Q)] =
             make_job((uint64_t)d.now, s_mask[i], ob + i, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
-      jobs += (uint32_t)tot;
+      if (live) {
+        gx_server_times *st = srv_times(d, v, ob + i);
+        st->last_updated_ns = d.now;
+        st->last_changed_ns = d.now;
+        s_ebase[i] = ev0 + n_ev + (uint32_t)fld(pre, 1);
+      }
+      c_chg += ec;
+      jobs += (uint32_t)fld(tot, 0);
+      n_ev += (uint32_t)fld(tot, 1);
     }
     __syncthreads();
+    if (evk >= 0) {  // events: owner order, then service order
+#pragma unroll
+      for (int q = 0; q < STORM_TILE / 256; q++) {
+        uint32_t k = t + 256 * q;
+        if (k >= ns || st_of(w[q]) == GX_ABSENT) continue;
+        uint32_t oi = k / d.S, sv = k - oi * d.S;
+        if (!s_live[oi]) continue;
+        uint32_t pos = s_ebase[oi] + (uint32_t)__popcll(s_mask[oi] & ((1ull << sv) - 1));
+        ev_put(d, evk, pos, ob * d.S + k, tomb, st_of(w[q]));
+      }
+      __syncthreads();
+    }
   }
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && (t & 63) == 0) {
@@ -333,10 +421,16 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
     atomicMin(&d.minexp[vi], exp_time(d.p, tomb));
   }
   c_wr = wave_sum(c_wr);
-  if ((t & 63) == 0) kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
+  c_chg = wave_sum(c_chg);
+  if ((t & 63) == 0) {
+    kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
+    ctr_atomic(d, C_CHG, c_chg);
+  }
   if (t == 0) {
     uint32_t ok = jobs < room ? jobs : room;
     h->fifo_tail = tail0 + ok;
+    if (jobs) d.vlc[vi] = d.now;
+    if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
     ctr_atomic(d, C_EXPSRV, jobs);
     ctr_atomic(d, C_QDROP, jobs - ok);
@@ -358,15 +452,18 @@ GXD uint64_t spread32(uint64_t x) {  // bit i -> bit 2i
 }
 __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   __shared__ uint32_t s_cnt[2][8];
+  __shared__ uint32_t s_ecnt[2][8];
   uint32_t vi = blockIdx.x, v = d.lo + vi;
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
   uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
-  uint32_t jobs = 0;
-  unsigned long long c_wr = 0;
+  uint32_t jobs = 0, n_ev = 0;
+  unsigned long long c_wr = 0, c_chg = 0;
   const uint64_t tomb = pack(d.now, GX_TOMBSTONE);
+  const int32_t evk = d.ev_slot[vi];
+  const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t LPO = d.S / 2;                      // lanes per owner
   const uint64_t omask = LPO == 32 ? 0xffffffffull : ((1ull << LPO) - 1);
@@ -387,9 +484,9 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   for (uint32_t base = 0; base < nw; base += 1024, it ^= 1) {
     ulonglong2 w[2] = {q[0], q[1]};
     if (base + 1024 < nw) load(base + 1024);
-    bool lead_live[2];
+    bool lead_live[2], live_c[2];
     uint64_t pmask[2];
-    uint32_t rank[2];
+    uint32_t rank[2], erank[2], sh_c[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
       bool p0 = st_of(w[c].x) != GX_ABSENT, p1 = st_of(w[c].y) != GX_ABSENT;
@@ -400,12 +497,31 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       pmask[c] = spread32((b0 >> sh) & omask) | (spread32((b1 >> sh) & omask) << 1);
       uint64_t n0 = (p0 && live) ? tomb : w[c].x, n1 = (p1 && live) ? tomb : w[c].y;
       bool ch0 = n0 != w[c].x, ch1 = n1 != w[c].y;
+      live_c[c] = live;
+      sh_c[c] = sh;
+      c_chg += live ? (unsigned)(p0 + p1) : 0u;  // ServiceChanged per record of a live owner
       if (ch0 || ch1) *reinterpret_cast<ulonglong2 *>(&row[base + 512 * c + 2 * t]) = make_ulonglong2(n0, n1);
       c_wr += ch0 + ch1;
       lead_live[c] = leader && live;
       uint64_t bj = __ballot(lead_live[c]);
       rank[c] = (uint32_t)__popcll(bj & ((1ull << lane) - 1));
       if (lane == 0) s_cnt[it][4 * c + wv] = (uint32_t)__popcll(bj);
+      if (lead_live[c]) {  // serverChanged (:204-215) for a live owner
+        gx_server_times *st = srv_times(d, v, lo + (base + 512 * c + 2 * t) / d.S);
+        st->last_updated_ns = d.now;
+        st->last_changed_ns = d.now;
+      }
+      if (evk >= 0) {  // events: owner order, then service order
+        uint32_t ec = lead_live[c] ? (uint32_t)__popcll(pmask[c]) : 0u;
+        uint32_t inc = ec;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          uint32_t y = __shfl_up(inc, o, 64);
+          if ((int)lane >= o) inc += y;
+        }
+        erank[c] = inc - ec;
+        if (lane == 63) s_ecnt[it][4 * c + wv] = inc;
+      }
     }
     __syncthreads();
     uint32_t pre[2] = {0, 0}, tot = 0;
@@ -426,6 +542,28 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       }
     }
     jobs += tot;
+    if (evk >= 0) {
+      uint32_t epre[2] = {0, 0}, etot = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        uint32_t x = s_ecnt[it][k];
+        if (k < (int)wv) epre[0] += x;
+        if (k < 4 + (int)wv) epre[1] += x;
+        etot += x;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        uint32_t ob = __shfl(erank[c], (int)sh_c[c], 64);  // the owner's first event
+        uint32_t r0 = base + 512 * c + 2 * t, key0 = lo * d.S + r0;
+        uint32_t s0 = r0 % d.S;
+        uint64_t below = pmask[c] & ((1ull << s0) - 1);
+        uint32_t e0 = ev0 + n_ev + epre[c] + ob + (uint32_t)__popcll(below);
+        bool p0 = st_of(w[c].x) != GX_ABSENT, p1 = st_of(w[c].y) != GX_ABSENT;
+        if (live_c[c] && p0) ev_put(d, evk, e0, key0, tomb, st_of(w[c].x));
+        if (live_c[c] && p1) ev_put(d, evk, e0 + p0, key0 + 1, tomb, st_of(w[c].y));
+      }
+      n_ev += etot;
+    }
   }
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && lane == 0) {
@@ -433,10 +571,16 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
     atomicMin(&d.minexp[vi], exp_time(d.p, tomb));
   }
   c_wr = wave_sum(c_wr);
-  if (lane == 0) kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
+  c_chg = wave_sum(c_chg);
+  if (lane == 0) {
+    kbytes(d, GX_K_STORM, 8ull * c_wr, 0);
+    ctr_atomic(d, C_CHG, c_chg);
+  }
   if (t == 0) {
     uint32_t ok = jobs < room ? jobs : room;
     h->fifo_tail = tail0 + ok;
+    if (jobs) d.vlc[vi] = d.now;
+    if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
     ctr_atomic(d, C_EXPSRV, jobs);
     ctr_atomic(d, C_QDROP, jobs - ok);
@@ -594,6 +738,8 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   __shared__ uint32_t s_start[65];
   __shared__ uint32_t s_ent[64];
   __shared__ uint8_t s_accf[64];
+  __shared__ uint8_t s_chg[64];
+  __shared__ uint8_t s_prev[64];
   __shared__ uint64_t s_accw[64];
   const uint32_t vi = blockIdx.x, v = d.lo + vi;
   const uint32_t lane = threadIdx.x;
@@ -603,10 +749,14 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   gx_host_state *h = &d.hs[vi];
   const uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   const uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
-  uint32_t n_retx = 0;
-  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, mexp = ~0ull;
+  uint32_t n_retx = 0, n_ev = 0;
+  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, c_chg = 0, mexp = ~0ull;
   uint64_t *row = &d.view[(size_t)vi * d.R];
   const uint32_t INV = K32 ? 0x3ffffffu : 0xffffffffu;  // sorts after every real key
+  const int32_t evk = d.ev_slot[vi];
+  const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
+  int64_t vlc_ts = 0;
+  bool vlc_set = false;
   for (uint32_t c0 = 0; c0 < deg; c0 += 64) {
     uint32_t cn = deg - c0 < 64 ? deg - c0 : 64;
     uint2 el = lane < cn ? d.in_sorted[off + c0 + lane] : make_uint2(0, 0);  // (entry, length)
@@ -658,11 +808,14 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
         uint32_t y = __shfl_xor(kmax, o, 64);
         kmax = y > kmax ? y : kmax;
       }
-      uint64_t wg = sw0, wme = 0;
+      uint64_t wg = sw0, wme = 0, wprev = GX_SLOT_ABSENT;
       bool acc = false, stl = false;
       for (uint32_t kk = 0; kk <= kmax; kk++) {  // occurrence kk of every group, arrival order
         uint64_t wcur = __shfl(wg, (int)gs, 64);
-        if (vs && kpos == kk) wme = merge_word(d, wcur, sval, acc, stl);
+        if (vs && kpos == kk) {
+          wprev = wcur;
+          wme = merge_word(d, wcur, sval, acc, stl);
+        }
         uint64_t wn = __shfl(wme, (int)((gs + kk) & 63), 64);
         if (head && kk < glen) wg = wn;
       }
@@ -677,10 +830,52 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
           mexp = x < mexp ? x : mexp;
         }
       }
+      // ServiceChanged: an insert, or a stored status that differs (:317-340)
+      const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
+      c_chg += chg;
       s_accf[src] = vs && acc && (skey / d.S != v);
+      s_chg[src] = chg;
+      s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
       s_accw[src] = wme;
+      // per owner (contiguous in key order): its last accepted and last status-changing
+      // occurrence in arrival order (segmented max of arrival lane + 1)
+      const uint32_t own = vs ? skey / d.S : 0xffffffffu;
+      uint32_t mu = acc ? src + 1 : 0, mc = chg ? src + 1 : 0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t yu = __shfl_down(mu, o, 64), yc = __shfl_down(mc, o, 64), yo = __shfl_down(own, o, 64);
+        if (lane + o < 64 && yo == own) {
+          mu = yu > mu ? yu : mu;
+          mc = yc > mc ? yc : mc;
+        }
+      }
+      uint32_t pown = __shfl_up(own, 1, 64);
+      const bool ohead = vs && (lane == 0 || pown != own);
+      uint32_t mcmax = mc;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        uint32_t y = __shfl_xor(mcmax, o, 64);
+        mcmax = y > mcmax ? y : mcmax;
+      }
       __threadfence_block();  // slot stores land before a later tile reads the same keys
       __syncthreads();
+      if (ohead && (mu || mc)) {
+        gx_server_times *st = srv_times(d, v, own);
+        if (mu) st->last_updated_ns = ts_of(s_accw[mu - 1]);  // server.LastUpdated (:323)
+        if (mc) st->last_changed_ns = ts_of(s_accw[mc - 1]);  // serverChanged (:204-215)
+      }
+      if (mcmax) {
+        vlc_ts = ts_of(s_accw[mcmax - 1]);  // state.LastChanged
+        vlc_set = true;
+      }
+      if (evk >= 0) {  // ChangeEvents in arrival order
+        bool fe = s_chg[lane] != 0;
+        unsigned long long me = __ballot(fe);
+        if (fe)
+          ev_put(d, evk, ev0 + n_ev + (uint32_t)__popcll(me & ((1ull << lane) - 1ull)), key, s_accw[lane],
+                 s_prev[lane]);
+        n_ev += (uint32_t)__popcll(me);
+      }
       bool f = s_accf[lane];  // ordered ballot compaction -> retransmit jobs (arrival order)
       unsigned long long m = __ballot(f);
       uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
@@ -696,10 +891,14 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   c_stale = wave_sum(c_stale);
   c_rd = wave_sum(c_rd);
   c_wr = wave_sum(c_wr);
+  c_chg = wave_sum(c_chg);
   mexp = wave_min(mexp);
   if (lane == 0) {
     uint32_t ok = n_retx < room ? n_retx : room;
     h->fifo_tail = tail0 + ok;
+    if (vlc_set) d.vlc[vi] = vlc_ts;
+    if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
+    ctr_atomic(d, C_CHG, c_chg);
     kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 8ull * deg, c_merge);
     ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
     ctr_atomic(d, C_GOSSIP_ACC, c_acc);
@@ -743,9 +942,16 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
   uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
   uint32_t na = 0, nb = 0;
-  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, ma = ~0ull, mb = ~0ull;
+  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0, ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
   const uint32_t TILE = 4 * blockDim.x;
+  // change bookkeeping: per-owner last accept / status change of each tile, the
+  // last status change of the pass (state.LastChanged), events for listening views; key order
+  __shared__ uint32_t s_lu[TILE_OWNERS], s_lc[TILE_OWNERS];
+  __shared__ uint32_t s_last[2];
+  const int32_t evka = d.ev_slot[li(d, a)], evkb = both ? d.ev_slot[li(d, b)] : -1;
+  const uint32_t ev0a = evka >= 0 ? d.ev_cnt[evka] : 0, ev0b = evkb >= 0 ? d.ev_cnt[evkb] : 0;
+  uint32_t nev_a = 0, nev_b = 0, last_a = 0, last_b = 0;
   // Software pipeline: the next PF 1024-slot tiles' loads are in flight while this tile is
   // merged, written back and (only if something was accepted) compacted.
   uint64_t qa[PF][4], qb[PF][4];
@@ -779,13 +985,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   };
   auto merge_tile = [&](uint32_t base, const uint64_t *wa, const uint64_t *wb) {
     uint64_t nwa[4], nwb[4];
-    bool fa[4], fb[4];
+    bool fa[4], fb[4], xa[4], xb[4], ca[4], cb[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       nwa[k] = wa[k];
       nwb[k] = wb[k];
-      fa[k] = fb[k] = false;
+      fa[k] = fb[k] = xa[k] = xb[k] = false;
       if (st_of(wb[k]) != GX_ABSENT) {  // a.Merge(b): every present record of b
         bool ac, st;
         c_merge++;
@@ -794,6 +1000,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         if (ac) {
           c_acc++;
           fa[k] = r / d.S != a;
+          xa[k] = true;
         }
       }
       if (both && st_of(wa[k]) != GX_ABSENT) {  // b.Merge(a's snapshot)
@@ -804,8 +1011,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         if (ac) {
           c_acc++;
           fb[k] = r / d.S != b;
+          xb[k] = true;
         }
       }
+      // ServiceChanged: an insert, or a stored status that differs (:317-340)
+      ca[k] = xa[k] && (st_of(wa[k]) == GX_ABSENT || st_of(wa[k]) != st_of(nwa[k]));
+      cb[k] = xb[k] && (st_of(wb[k]) == GX_ABSENT || st_of(wb[k]) != st_of(nwb[k]));
+      c_chg += ca[k] + cb[k];
       if (nwa[k] != wa[k]) {
         c_wr++;
         unsigned long long x = exp_time(d.p, nwa[k]);
@@ -834,7 +1046,49 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     unsigned long long cnt = (unsigned long long)(fa[0] + fa[1]) | ((unsigned long long)(fa[2] + fa[3]) << 16) |
                              ((unsigned long long)(fb[0] + fb[1]) << 32) | ((unsigned long long)(fb[2] + fb[3]) << 48);
-    if (!__syncthreads_or(cnt != 0)) return;  // nothing accepted in this tile: no retransmits
+    bool anyx = xa[0] | xa[1] | xa[2] | xa[3] | xb[0] | xb[1] | xb[2] | xb[3];
+    if (!__syncthreads_or(anyx)) return;  // nothing accepted in this tile: no retransmits, no changes
+    {  // server times (both sides) and ChangeEvents, key order
+      uint32_t o0 = base / d.S, oe = ((base + TILE < d.R ? base + TILE : d.R) - 1) / d.S, no = oe - o0 + 1;
+      unsigned long long ec = (unsigned long long)(ca[0] + ca[1]) | ((unsigned long long)(ca[2] + ca[3]) << 16) |
+                              ((unsigned long long)(cb[0] + cb[1]) << 32) | ((unsigned long long)(cb[2] + cb[3]) << 48);
+      unsigned long long etot;
+      unsigned long long epre = block_excl_scan64(ec, s_wave, etot);
+      uint32_t pe[4] = {fld(epre, 0), fld(epre, 0) + ca[0], fld(etot, 0) + fld(epre, 1), 0};
+      pe[3] = pe[2] + ca[2];
+      uint32_t qe[4] = {fld(epre, 2), fld(epre, 2) + cb[0], fld(etot, 2) + fld(epre, 3), 0};
+      qe[3] = qe[2] + cb[2];
+      uint32_t ta = fld(etot, 0) + fld(etot, 1), tb = fld(etot, 2) + fld(etot, 3);
+      for (int side = 0; side < (both ? 2 : 1); side++) {
+        const bool *xf = side ? xb : xa, *cf = side ? cb : ca;
+        const uint64_t *wo = side ? wb : wa, *wn = side ? nwb : nwa;
+        const uint32_t *pp = side ? qe : pe;
+        const uint32_t tn = side ? tb : ta;
+        const int32_t evk = side ? evkb : evka;
+        const uint32_t evb = side ? ev0b + nev_b : ev0a + nev_a;
+        uint32_t x = side ? b : a;
+        for (uint32_t i = t; i < no; i += blockDim.x) s_lu[i] = s_lc[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+          if (xf[k]) atomicMax(&s_lu[r / d.S - o0], r + 1);
+          if (cf[k]) {
+            atomicMax(&s_lc[r / d.S - o0], r + 1);
+            if (pp[k] == tn - 1) s_last[side] = r + 1;
+            if (evk >= 0)
+              ev_put(d, evk, evb + pp[k], r, wn[k], st_of(wo[k]) == GX_ABSENT ? GX_UNKNOWN : st_of(wo[k]));
+          }
+        }
+        __syncthreads();
+        tile_owner_times(d, x, side ? B : A, o0, no, s_lu, s_lc);
+        __syncthreads();
+      }
+      if (ta) last_a = s_last[0];
+      if (tb) last_b = s_last[1];
+      nev_a += ta;
+      nev_b += tb;
+    }
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
     uint32_t pa[4], pb[4];
@@ -878,6 +1132,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   }
   ma = block_min(ma, s_red);
   mb = block_min(mb, s_red);
+  block_ctr(d, C_CHG, c_chg, s_red);
+  if (t == 0) {
+    if (last_a) d.vlc[li(d, a)] = ts_of(A[last_a - 1]);
+    if (both && last_b) d.vlc[li(d, b)] = ts_of(B[last_b - 1]);
+    if (evka >= 0) d.ev_cnt[evka] = ev0a + nev_a;
+    if (evkb >= 0) d.ev_cnt[evkb] = ev0b + nev_b;
+  }
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && (t & 63) == 0) mark_change(d);
   c_wr = wave_sum(c_wr);

@@ -296,12 +296,47 @@ static void test_get_broadcasts_bytes() {
   So(delegate.GetBroadcasts(3, 1398).empty());
 }
 
+// Server times, state.LastChanged and listeners (services_state_test.go:177-212, :572-626)
+static void test_change_bookkeeping() {
+  Cluster c(params());
+  ServicesState state(c, local);
+  const int64_t t0 = c.Now();
+  Service svc{"deadbeef123", "chaucer", t0, sidecar::ALIVE};
+  cur = "NewServer / NewServicesState start at Unix(0)";
+  So(state.LastChanged() == 0 && state.Times("chaucer").LastUpdated == 0);
+  cur = "AddListener refuses an unbuffered channel";
+  So(!state.AddListener("bad", 0));
+  So(state.AddListener("listener1", 1) && state.AddListener("listener2", 8));
+  cur = "a new service moves LastChanged; the listeners hear it";
+  state.AddServiceEntry(svc);
+  So(state.LastChanged() == t0 && state.Times("chaucer").LastChanged == t0);
+  cur = "a newer record with the same status moves only LastUpdated";
+  svc.Updated = t0 + 5;
+  state.AddServiceEntry(svc);
+  So(state.Times("chaucer").LastUpdated == t0 + 5 && state.LastChanged() == t0);
+  cur = "a status change moves LastChanged and is an event (previous status ALIVE)";
+  svc.Updated = t0 + 9;
+  svc.Status = sidecar::TOMBSTONE;
+  state.AddServiceEntry(svc);
+  So(state.LastChanged() == t0 + 9);
+  auto e1 = state.Receive("listener1"), e2 = state.Receive("listener2");
+  So(e1.size() == 1 && e1[0].PreviousStatus == sidecar::UNKNOWN);  // channel of 1: the second was dropped
+  So(e2.size() == 2 && e2[1].PreviousStatus == sidecar::ALIVE && e2[1].Svc == svc && e2[1].Time == t0 + 9);
+  cur = "RemoveListener reports a missing one";
+  So(state.RemoveListener("listener1") && !state.RemoveListener("listener1"));
+  cur = "EachServiceSorted orders by Updated";
+  state.AddServiceEntry(Service{"older", "chaucer", t0 - 100, sidecar::ALIVE});
+  auto sorted = state.EachServiceSorted();
+  So(sorted.size() == 2 && sorted[0].ID == "older");
+}
+
 int main() {
   test_services_state_with_data();
   test_tracking_and_broadcasting();
   test_cluster_membership();
   test_get_broadcasts();
   test_get_broadcasts_bytes();
+  test_change_bookkeeping();
   std::printf("backend=%s checks=%d failures=%d\n", gx_backend(), checks, failures);
   return failures ? 1 : 0;
 }

@@ -321,6 +321,162 @@ def kat_is_stale(lib):
     assert e2.add_service_entry(LOCAL, (CH, 0, now - HOUR, ALIVE)) == 1
 
 
+# ------------------------------------------- change bookkeeping and listeners
+def _times(e, view, owner):
+    lu, lc = e.server_times(view, owner, owner + 1)[0]
+    return int(lu), int(lc)
+
+
+def kat_new_server_times_epoch(lib):
+    """services_state_test.go:53-61, :74-77 — NewServer and NewServicesState start LastUpdated and
+    LastChanged at time.Unix(0, 0)."""
+    e = mk(lib)
+    assert _times(e, LOCAL, CH) == (0, 0)
+    assert int(e.last_changed(LOCAL, LOCAL + 1)[0]) == 0
+
+
+def kat_last_updated_newer_record(lib):
+    """services_state_test.go:177-183 — a newer record sets the server's LastUpdated to its Updated."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    nd = T0 + 5 * 24 * HOUR  # svc.Updated.AddDate(0, 0, 5)
+    e.add_service_entry(LOCAL, (CH, 0, nd, ALIVE))
+    assert _times(e, LOCAL, CH)[0] == nd
+
+
+def kat_last_changed_on_new(lib):
+    """services_state_test.go:185-194 — a new service moves state.LastChanged and the server's."""
+    e = mk(lib)
+    before = int(e.last_changed(LOCAL, LOCAL + 1)[0])
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    assert int(e.last_changed(LOCAL, LOCAL + 1)[0]) > before
+    assert _times(e, LOCAL, CH)[1] > before
+    assert _times(e, LOCAL, CH) == (T0, T0)
+
+
+def kat_last_changed_on_status_change(lib):
+    """services_state_test.go:196-203 — a status change (svc.Tombstone()) moves state.LastChanged."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    before = int(e.last_changed(LOCAL, LOCAL + 1)[0])
+    e.set_round(1)
+    e.add_service_entry(LOCAL, (CH, 0, e.now(), TOMBSTONE))
+    assert int(e.last_changed(LOCAL, LOCAL + 1)[0]) > before
+
+
+def kat_last_changed_skips_same_status(lib):
+    """services_state_test.go:205-212 — a newer record with the same status leaves
+    state.LastChanged (and the server's LastChanged) alone; LastUpdated still moves."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    before = int(e.last_changed(LOCAL, LOCAL + 1)[0])
+    e.set_round(1)
+    e.add_service_entry(LOCAL, (CH, 0, e.now(), ALIVE))
+    assert int(e.last_changed(LOCAL, LOCAL + 1)[0]) == before
+    assert _times(e, LOCAL, CH) == (e.now(), T0)
+
+
+def kat_last_changed_draining_sticky(lib):
+    """services_state.go:329-340 — a newer ALIVE over DRAINING is stored as DRAINING: no status
+    change, so only LastUpdated moves."""
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (CH, 0, T0, DRAINING))
+    e.set_round(1)
+    e.add_service_entry(LOCAL, (CH, 0, e.now(), ALIVE))
+    assert _times(e, LOCAL, CH) == (e.now(), T0)
+    assert e.stats()["change_events"] == 1
+
+
+def kat_last_changed_when_tombstoned(lib):
+    """services_state_test.go:426-435 — BroadcastTombstones tombstoning a service that stopped
+    running moves state.LastChanged and the server's LastChanged."""
+    e = mk(lib)
+    e.add_service_entry(SH, (SH, 5, T0, ALIVE))  # "runs": not in the container list
+    before = int(e.last_changed(SH, SH + 1)[0])
+    e.set_round(1)
+    out = e.tombstone_services(SH, running=[])
+    assert len(out) == 2
+    assert int(e.last_changed(SH, SH + 1)[0]) > before and _times(e, SH, SH)[1] > before
+    assert _times(e, SH, SH) == (e.now(), e.now())
+
+
+def kat_last_changed_on_expiry(lib):
+    """services_state_test.go:480-492, :494-507 — lifespan expiry tombstones at Updated + 1 s and
+    moves the server's LastChanged (to that time)."""
+    e, s1, s2 = _tb(lib)
+    e.add_service_entry(SH, s1)
+    e.add_service_entry(SH, (SH, 1, T0, DRAINING))
+    stamp = T0 - ALIVE_LIFESPAN - 5 * SEC
+    e.write_slot(SH, (SH, 0, stamp, ALIVE))
+    e.write_slot(SH, (SH, 1, T0 - DRAINING_LIFESPAN - 5 * SEC, DRAINING))
+    e.tombstone_others(SH)
+    # key order: service 1's expiry is the later change
+    t1 = T0 - DRAINING_LIFESPAN - 5 * SEC + SEC
+    assert _times(e, SH, SH) == (t1, t1)
+    assert int(e.last_changed(SH, SH + 1)[0]) == t1
+
+
+def kat_expire_server_times(lib):
+    """services_state.go:176-181 — ExpireServer tombstones every record at now and ServiceChanged
+    runs for each, including existing tombstones."""
+    e = mk(lib)
+    e.add_service_entries([LOCAL] * 3, [(CH, 0, T0, ALIVE), (CH, 1, T0, TOMBSTONE), (CH, 2, T0, DRAINING)])
+    n0 = e.stats()["change_events"]
+    e.set_round(3)
+    assert e.expire_server(LOCAL, CH) == 1
+    assert e.stats()["change_events"] - n0 == 3
+    assert _times(e, LOCAL, CH) == (e.now(), e.now())
+
+
+def kat_listener_receives_changes(lib):
+    """services_state_test.go:609-626 — a major state change notifies every listener; the event
+    carries the record, the previous status (UNKNOWN for a new one) and state.LastChanged."""
+    e = mk(lib)
+    e.add_listener(LOCAL, 1, 4)
+    e.add_listener(LOCAL, 2, 4)
+    e.add_service_entry(LOCAL, (LOCAL, 0, T0, ALIVE))
+    e.add_service_entry(LOCAL, (LOCAL, 0, T0 + SEC, ALIVE))  # newer, same status: no event
+    e.add_service_entry(LOCAL, (LOCAL, 0, T0 + 2 * SEC, TOMBSTONE))
+    for lid in (1, 2):
+        ev = [x.tup() for x in e.drain_listener(LOCAL, lid)]
+        assert ev == [(LOCAL, 0, T0, ALIVE, UNKNOWN, T0),
+                      (LOCAL, 0, T0 + 2 * SEC, TOMBSTONE, ALIVE, T0 + 2 * SEC)]
+    assert e.drain_listener(LOCAL, 1) == []
+
+
+def kat_listener_full_channel_drops(lib):
+    """services_state.go:230-236 — a full channel does not block: the event is dropped for that
+    listener only."""
+    e = mk(lib)
+    e.add_listener(LOCAL, 1, 1)
+    e.add_listener(LOCAL, 2, 3)
+    e.add_service_entries([LOCAL] * 3, [(CH, s, T0, ALIVE) for s in range(3)])
+    assert [x.service.svc for x in e.drain_listener(LOCAL, 1)] == [0]
+    assert [x.service.svc for x in e.drain_listener(LOCAL, 2)] == [0, 1, 2]
+    assert e.stats()["listener_drops"] == 2
+
+
+def kat_listener_add_remove(lib):
+    """services_state_test.go:581-605 — AddListener refuses an unbuffered channel; RemoveListener
+    removes by name and reports a missing one."""
+    from sidecar_amd.abi import GX_EINVAL, GX_ENOENT
+    e = mk(lib)
+    assert lib.gx_add_listener(e.h, LOCAL, 9, 0) == GX_EINVAL
+    e.add_listener(LOCAL, 1, 2)
+    assert e.remove_listener(LOCAL, 1) == 0
+    assert e.remove_listener(LOCAL, 1) == GX_ENOENT
+    e.add_service_entry(LOCAL, (CH, 0, T0, ALIVE))
+    assert e.stats()["listener_drops"] == 0
+
+
+def kat_listener_other_views_silent(lib):
+    """Listeners are per ServicesState: a change in another view does not reach them."""
+    e = mk(lib)
+    e.add_listener(LOCAL, 1, 8)
+    e.add_service_entry(SH, (CH, 0, T0, ALIVE))
+    assert e.drain_listener(LOCAL, 1) == [] and e.stats()["change_events"] == 1
+
+
 # ---------------------------------------------------------------------- services_delegate_test.go
 # Fixture records (services_delegate_test.go:15-20): byte lengths drive packPacket.
 _FIX = {

@@ -6,10 +6,19 @@ def host_tuples(e):
     return [tuple(getattr(h, f) for f, _ in h._fields_) for h in e.hosts()]
 
 
+def server_times(e, max_views=512):
+    """Server.LastUpdated/LastChanged of every owner, for up to max_views of the engine's views
+    (evenly spaced), plus state.LastChanged of all of them."""
+    n = e.hi - e.lo
+    pick = range(e.lo, e.hi) if n <= max_views else np.linspace(e.lo, e.hi - 1, max_views).astype(int)
+    return np.stack([e.server_times(int(v)) for v in pick]), e.last_changed()
+
+
 def snapshot(e, views=True):
     s = {"hosts": host_tuples(e), "digests": e.digests(), "stats": e.stats()}
     if views:
         s["views"] = e.read_views()
+        s["times"], s["last_changed"] = server_times(e)
     return s
 
 
@@ -23,6 +32,12 @@ def assert_same(a, b, what=""):
     if not np.array_equal(sa["digests"], sb["digests"]):
         bad = np.nonzero(sa["digests"] != sb["digests"])[0]
         raise AssertionError(f"{what}: queue digests differ for hosts {bad[:10].tolist()}")
+    if not np.array_equal(sa["last_changed"], sb["last_changed"]):
+        bad = np.nonzero(sa["last_changed"] != sb["last_changed"])[0]
+        raise AssertionError(f"{what}: state.LastChanged differs for views {bad[:10].tolist()}")
+    if not np.array_equal(sa["times"], sb["times"]):
+        diff = np.argwhere(sa["times"] != sb["times"])
+        raise AssertionError(f"{what}: {len(diff)} server times differ, first (view#, owner, field) {diff[:5].tolist()}")
 
 
 def _dict_diff(a, b):

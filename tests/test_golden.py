@@ -17,8 +17,11 @@ def check(lib, name):
     assert json.loads(str(ref["params"])) == kw and int(ref["rounds"]) == rounds
     got = run(lib, kw, rounds)
     got_stats, ref_stats = json.loads(got["stats"]), json.loads(str(ref["stats"]))
-    # counters added after the fixtures were made (byte-limit packing) are zero in record mode
-    assert {k: v for k, v in got_stats.items() if k not in ref_stats} == {"bytes_sent": 0, "cap_cuts": 0}
+    # counters added after the fixtures were made: byte-limit packing (zero in record mode),
+    # listener drops (no listeners) and ServiceChanged calls (not in the fixtures)
+    extra = {k: v for k, v in got_stats.items() if k not in ref_stats}
+    assert set(extra) == {"bytes_sent", "cap_cuts", "change_events", "listener_drops"}
+    assert extra["bytes_sent"] == extra["cap_cuts"] == extra["listener_drops"] == 0
     assert {k: got_stats[k] for k in ref_stats} == ref_stats
     assert np.array_equal(got["views"], ref["views"])
     assert np.array_equal(got["hosts"], ref["hosts"])

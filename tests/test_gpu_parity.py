@@ -61,6 +61,35 @@ def test_round_model_parity(oracle_lib, gx_lib, name):
     assert g.converged() == o.converged()
 
 
+LISTEN = {  # scenario -> [(view, listener id, capacity)]
+    "cfg1_storm": [(0, 1, 4), (0, 2, 4096), (40, 1, 300), (63, 7, 1)],
+    "cfg1_churn_aged": [(3, 1, 64), (17, 2, 4096)],
+    "storm_s3": [(5, 1, 2048), (60, 1, 17)],
+    "odd_sizes": [(0, 1, 100), (36, 1, 4096)],
+}
+
+
+@pytest.mark.parametrize("name", sorted(LISTEN))
+def test_change_events_parity(oracle_lib, gx_lib, name):
+    """ChangeEvents reach listeners in the same order, with the same drops, on both engines
+    (SURVEY §8f-4); server times and state.LastChanged are compared by assert_same."""
+    g, o = pair(oracle_lib, gx_lib, **SCENARIOS[name])
+    for v, lid, cap in LISTEN[name]:
+        g.add_listener(v, lid, cap)
+        o.add_listener(v, lid, cap)
+    n_ev = 0
+    for chunk in (1, 3, 7, 20, 40):
+        g.run_rounds(chunk)
+        o.run_rounds(chunk)
+        assert_same(g, o, f"{name} round {g.round}")
+        for v, lid, cap in LISTEN[name]:
+            ge = [x.tup() for x in g.drain_listener(v, lid, cap // 2 + 1)]  # leave some buffered
+            oe = [x.tup() for x in o.drain_listener(v, lid, cap // 2 + 1)]
+            assert ge == oe, f"{name} view {v} listener {lid} round {g.round}"
+            n_ev += len(ge)
+    assert n_ev > 0 and g.stats()["change_events"] > 0
+
+
 @pytest.mark.parametrize("limit", [1398, 600, 230])
 def test_byte_limit_parity(oracle_lib, gx_lib, limit):
     """packPacket under memberlist's byte limit: a random static-length table

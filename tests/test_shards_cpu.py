@@ -39,6 +39,11 @@ def assert_sharded_equal(whole: Engine, shards, what):
     assert np.array_equal(dig, whole.digests()), what
     c, n = shards.converged()
     assert (c, n) == whole.converged(), what
+    lc = np.concatenate([e.last_changed() for e in shards.engines])
+    assert np.array_equal(lc, whole.last_changed()), what
+    for e in shards.engines:
+        for v in (e.lo, (e.lo + e.hi) // 2, e.hi - 1):
+            assert np.array_equal(e.server_times(v), whole.server_times(v)), (what, v)
 
 
 @pytest.mark.parametrize("G", [2, 3, 5])
