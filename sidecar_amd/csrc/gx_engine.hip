@@ -197,14 +197,16 @@ static int round_send_impl(gx_engine *e) {
   }
   {
     LaunchTimer t(e, GX_K_SCAN);
-    if (vec) k_scan<true><<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
-    else k_scan<false><<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
+    const bool ev = !e->log_views.empty();
+    (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
+        <<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
     k_bt_finish<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   }
   if (d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2) {
     LaunchTimer t(e, GX_K_STORM);
-    if (d.S >= 2 && 64 % d.S == 0) k_storm_p2<<<d.Hl, 256, 0, s>>>(d);
-    else k_storm<<<d.Hl, 256, 0, s>>>(d);
+    const bool ev = !e->log_views.empty();
+    if (d.S >= 2 && 64 % d.S == 0) (ev ? k_storm_p2<true> : k_storm_p2<false>)<<<d.Hl, 256, 0, s>>>(d);
+    else (ev ? k_storm<true> : k_storm<false>)<<<d.Hl, 256, 0, s>>>(d);
   }
   {
     LaunchTimer t(e, GX_K_SEND);
@@ -231,8 +233,9 @@ static int round_merge_impl(gx_engine *e) {
       }
     }
     LaunchTimer t(e, GX_K_MERGE);
-    if (d.R < (1u << 26)) k_merge<true><<<d.Hl, 64, 0, s>>>(d);  // 32-bit sort keys
-    else k_merge<false><<<d.Hl, 64, 0, s>>>(d);
+    const bool ev = !e->log_views.empty();
+    if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<d.Hl, 64, 0, s>>>(d);  // 32-bit keys
+    else (ev ? k_merge<false, true> : k_merge<false, false>)<<<d.Hl, 64, 0, s>>>(d);
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -265,8 +268,12 @@ static int ae_whole_impl(gx_engine *e) {
       LaunchTimer t(e, GX_K_AE);
       // PF = 1, default cache policy: deeper prefetch and nt loads measured within noise
       // (profiles/ae_variants.sh)
-      if (vec) k_ae<true><<<np, 256, 0, s>>>(d, key0, key1);
-      else k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
+      // the ChangeEvent variant only while some view has a listener
+      const bool ev = !e->log_views.empty();
+      if (vec && !ev) k_ae<true><<<np, 256, 0, s>>>(d, key0, key1);
+      else if (vec) k_ae_ev<true><<<np, 256, 0, s>>>(d, key0, key1);
+      else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
+      else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);
     }
   }
   HIPCHK(hipGetLastError());
@@ -607,8 +614,11 @@ int gx_merge(gx_engine *e, uint32_t dst, uint32_t src) {
   if (!e || !own(e, dst) || !own(e, src)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   set_round_fields(e);
-  if (e->d.R % 2 == 0) k_merge_views<true><<<1, 256, 0, e->stream>>>(e->d, dst, src);
-  else k_merge_views<false><<<1, 256, 0, e->stream>>>(e->d, dst, src);
+  const bool ev = !e->log_views.empty();
+  if (e->d.R % 2 == 0 && !ev) k_merge_views<true, false><<<1, 256, 0, e->stream>>>(e->d, dst, src);
+  else if (e->d.R % 2 == 0) k_merge_views<true, true><<<1, 256, 0, e->stream>>>(e->d, dst, src);
+  else if (!ev) k_merge_views<false, false><<<1, 256, 0, e->stream>>>(e->d, dst, src);
+  else k_merge_views<false, true><<<1, 256, 0, e->stream>>>(e->d, dst, src);
   return sync_check(e);
 }
 
@@ -620,8 +630,8 @@ int gx_tombstone_others(gx_engine *e, uint32_t view, gx_service *out, uint32_t c
   uint32_t *dcnt = (uint32_t *)e->api_dev;
   grec *dlist = (grec *)((char *)e->api_dev + 256);
   set_round_fields(e);
-  if (e->d.R % 2 == 0) k_scan<true><<<1, 256, 0, e->stream>>>(e->d, dlist, 0, cap, dcnt, (int)view);
-  else k_scan<false><<<1, 256, 0, e->stream>>>(e->d, dlist, 0, cap, dcnt, (int)view);
+  (e->d.R % 2 == 0 ? k_scan<true, true> : k_scan<false, true>)<<<1, 256, 0, e->stream>>>(e->d, dlist, 0, cap, dcnt,
+                                                                                        (int)view);
   uint32_t n = 0;
   HIPCHK(hipMemcpyAsync(&n, dcnt, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   rc = sync_check(e);
@@ -724,8 +734,8 @@ int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list,
   uint32_t *dcnt = (uint32_t *)e->api_dev;
   grec *dlist = (grec *)((char *)e->api_dev + 256);
   set_round_fields(e);
-  if (e->d.R % 2 == 0) k_scan<true><<<1, 256, 0, e->stream>>>(e->d, dlist, 0, e->d.L, dcnt, (int)host);
-  else k_scan<false><<<1, 256, 0, e->stream>>>(e->d, dlist, 0, e->d.L, dcnt, (int)host);
+  (e->d.R % 2 == 0 ? k_scan<true, true> : k_scan<false, true>)<<<1, 256, 0, e->stream>>>(e->d, dlist, 0, e->d.L, dcnt,
+                                                                                        (int)host);
   k_api_bt<<<1, 64, 0, e->stream>>>(e->d, host, mask, dlist, dcnt);
   return sync_check(e);
 }
@@ -1286,14 +1296,16 @@ static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *b
   if (hi <= lo) return;
   set_round_fields(e);
   LaunchTimer t(e, GX_K_AE);
-  if (e->d.R % 2 == 0)
-    k_ae_plan<true><<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,
-                                                     e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off,
-                                                     e->ae_mask, e->nmw);
-  else
-    k_ae_plan<false><<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,
-                                                      e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off,
-                                                      e->ae_mask, e->nmw);
+#define GX_AE_PLAN(V, E)                                                                                     \
+  (E ? k_ae_plan_ev<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,             \
+                                                  e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off, e->ae_mask, \
+                                                  e->nmw)
+  const bool ev = !e->log_views.empty();
+  if (e->d.R % 2 == 0 && !ev) GX_AE_PLAN(true, false);
+  else if (e->d.R % 2 == 0) GX_AE_PLAN(true, true);
+  else if (!ev) GX_AE_PLAN(false, false);
+  else GX_AE_PLAN(false, true);
+#undef GX_AE_PLAN
 }
 
 int gx_ae_merge_local(gx_engine *e) {

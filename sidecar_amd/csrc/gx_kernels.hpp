@@ -196,7 +196,7 @@ __global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
 // slot has ts + lifespan < now), so its scan is skipped: identical results, no HBM traffic.
 // Otherwise the row is streamed with 16-B loads (4 slots per thread per 1024-slot tile), the
 // lifespans applied, and the first list_cap tombstones compacted in key order (packed block scan).
-template <bool VEC>
+template <bool VEC, bool EV>
 __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t list_stride, uint32_t list_cap,
                                                uint32_t *cnt_out, int only_host) {
   __shared__ unsigned long long s_wave[4];
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
         uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
         atomicMax(&s_lu[r / d.S - o0], r + 1);
         if (pos[k] == n_exp + tn - 1) s_last = r + 1;
-        if (evk >= 0) ev_put(d, evk, ev0 + pos[k], r, nw[k], st_of(w[k]));
+        if (EV && evk >= 0) ev_put(d, evk, ev0 + pos[k], r, nw[k], st_of(w[k]));
       }
       __syncthreads();
       tile_owner_times(d, oi + d.lo, row, o0, oe - o0 + 1, s_lu, s_lu);
@@ -335,6 +335,7 @@ __global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
 // owner's presence mask and liveness in LDS, tombstone the live owners' present slots, and
 // compact the EXPIRE jobs in owner order.
 #define STORM_TILE 1024
+template <bool EV>
 __global__ __launch_bounds__(256) void k_storm(Dev d) {
   __shared__ unsigned long long s_mask[STORM_TILE];
   __shared__ uint32_t s_live[STORM_TILE];
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
       n_ev += (uint32_t)fld(tot, 1);
     }
     __syncthreads();
-    if (evk >= 0) {  // events: owner order, then service order
+    if (EV && evk >= 0) {  // events: owner order, then service order
 #pragma unroll
       for (int q = 0; q < STORM_TILE / 256; q++) {
         uint32_t k = t + 256 * q;
@@ -450,6 +451,7 @@ GXD uint64_t spread32(uint64_t x) {  // bit i -> bit 2i
   x = (x | (x << 1)) & 0x5555555555555555ull;
   return x;
 }
+template <bool EV>
 __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   __shared__ uint32_t s_cnt[2][8];
   __shared__ uint32_t s_ecnt[2][8];
@@ -511,7 +513,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
         st->last_updated_ns = d.now;
         st->last_changed_ns = d.now;
       }
-      if (evk >= 0) {  // events: owner order, then service order
+      if (EV && evk >= 0) {  // events: owner order, then service order
         uint32_t ec = lead_live[c] ? (uint32_t)__popcll(pmask[c]) : 0u;
         uint32_t inc = ec;
 #pragma unroll
@@ -542,7 +544,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       }
     }
     jobs += tot;
-    if (evk >= 0) {
+    if (EV && evk >= 0) {
       uint32_t epre[2] = {0, 0}, etot = 0;
 #pragma unroll
       for (int k = 0; k < 8; k++) {
@@ -733,7 +735,7 @@ GXD uint64_t bitonic64(uint64_t x, uint32_t lane) {  // ascending across the 64 
   return x;
 }
 
-template <bool K32>
+template <bool K32, bool EV>
 __global__ __launch_bounds__(64) void k_merge(Dev d) {
   __shared__ uint32_t s_start[65];
   __shared__ uint32_t s_ent[64];
@@ -834,8 +836,10 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
       const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
       c_chg += chg;
       s_accf[src] = vs && acc && (skey / d.S != v);
-      s_chg[src] = chg;
-      s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
+      if (EV) {
+        s_chg[src] = chg;
+        s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
+      }
       s_accw[src] = wme;
       // per owner (contiguous in key order): its last accepted and last status-changing
       // occurrence in arrival order (segmented max of arrival lane + 1)
@@ -863,12 +867,13 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
         gx_server_times *st = srv_times(d, v, own);
         if (mu) st->last_updated_ns = ts_of(s_accw[mu - 1]);  // server.LastUpdated (:323)
         if (mc) st->last_changed_ns = ts_of(s_accw[mc - 1]);  // serverChanged (:204-215)
+        c_wr += (mu != 0) + (mc != 0);                        // counted as written words
       }
       if (mcmax) {
         vlc_ts = ts_of(s_accw[mcmax - 1]);  // state.LastChanged
         vlc_set = true;
       }
-      if (evk >= 0) {  // ChangeEvents in arrival order
+      if (EV && evk >= 0) {  // ChangeEvents in arrival order
         bool fe = s_chg[lane] != 0;
         unsigned long long me = __ballot(fe);
         if (fe)
@@ -926,12 +931,99 @@ GXD ulonglong2 ld16(const uint64_t *p) {
   return *reinterpret_cast<const ulonglong2 *>(p);
 }
 
+// Server times of one push-pull side for S dividing 128 (S >= 2, 16-B mapping): a wave's
+// 128-slot chunk holds whole owners, S/2 lanes each, so the last accepted / status-changing
+// key of every owner comes from a max over its lane group (no LDS, no barrier). f = accepted
+// bits 0-3 | changed bits 4-7 of this thread's slots; lk = this thread's running last changed
+// key + 1 (state.LastChanged, reduced at the end of the pass).
+GXD void side_times_shfl(const Dev &d, uint32_t x, uint32_t base, uint32_t f, const uint64_t *nw, uint32_t &lk,
+                         uint32_t &words_written) {
+  const uint32_t t = threadIdx.x, lane = t & 63, lpo = d.S / 2;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t r0 = base + 512 * h + 2 * t;
+    const uint32_t fa0 = (f >> (2 * h)) & 1u, fa1 = (f >> (2 * h + 1)) & 1u;
+    const uint32_t fc0 = (f >> (4 + 2 * h)) & 1u, fc1 = (f >> (4 + 2 * h + 1)) & 1u;
+    if (!__ballot(fa0 | fa1)) continue;  // changes only come with accepts
+    uint32_t ku = fa1 ? r0 + 2 : (fa0 ? r0 + 1 : 0u), kc = fc1 ? r0 + 2 : (fc0 ? r0 + 1 : 0u);
+    int64_t tu = ts_of(fa1 ? nw[2 * h + 1] : nw[2 * h]), tc = ts_of(fc1 ? nw[2 * h + 1] : nw[2 * h]);
+    for (uint32_t o = 1; o < lpo; o <<= 1) {
+      uint32_t yk = __shfl_xor(ku, (int)o, 64), yc = __shfl_xor(kc, (int)o, 64);
+      int64_t yu = __shfl_xor(tu, (int)o, 64), yt = __shfl_xor(tc, (int)o, 64);
+      if (yk > ku) {
+        ku = yk;
+        tu = yu;
+      }
+      if (yc > kc) {
+        kc = yc;
+        tc = yt;
+      }
+    }
+    if (lane % lpo == 0 && (ku | kc)) {
+      gx_server_times *st = srv_times(d, x, r0 / d.S);
+      if (ku) st->last_updated_ns = tu;
+      if (kc) st->last_changed_ns = tc;
+      words_written += (ku != 0) + (kc != 0);
+    }
+    lk = kc > lk ? kc : lk;
+  }
+}
+
+// Server times and ChangeEvents of one push-pull tile, key order: fl bit
+// 8*side + k = slot k accepted, bit 8*side + 4 + k = its status changed; os = old statuses
+// (3 bits per slot). The stored words are read back from the rows. s_last[side] keeps 1 + the
+// last changed key of the pass (tiles come in key order, so a running max). EV: also the
+// ChangeEvents of listening views; returns the tile's changed counts (side a | side b << 16).
+template <bool VEC, bool EV>
+GXD uint32_t ae_book(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t base, uint32_t fl, uint32_t os,
+                     const uint64_t *A, const uint64_t *B, uint32_t *s_lu, uint32_t *s_lc, uint32_t *s_last,
+                     unsigned long long *s_wave, int32_t evka, int32_t evkb, uint32_t evba, uint32_t evbb) {
+  const uint32_t t = threadIdx.x, TILE = 4 * blockDim.x;
+  const uint32_t o0 = base / d.S, no = ((base + TILE < d.R ? base + TILE : d.R) - 1) / d.S - o0 + 1;
+  unsigned long long epre = 0, etot = 0;
+  if (EV) {
+    const unsigned long long ec = (unsigned long long)__popc(fl & 0x30u) |
+                                  ((unsigned long long)__popc(fl & 0xC0u) << 16) |
+                                  ((unsigned long long)__popc(fl & 0x3000u) << 32) |
+                                  ((unsigned long long)__popc(fl & 0xC000u) << 48);
+    epre = block_excl_scan64(ec, s_wave, etot);
+  }
+  for (int side = 0; side < (both ? 2 : 1); side++) {
+    const uint64_t *X = side ? B : A;
+    for (uint32_t i = t; i < no; i += blockDim.x) s_lu[i] = s_lc[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+      if ((fl >> (8 * side + k)) & 1u) atomicMax(&s_lu[r / d.S - o0], r + 1);
+      if ((fl >> (8 * side + 4 + k)) & 1u) {
+        atomicMax(&s_lc[r / d.S - o0], r + 1);
+        atomicMax(&s_last[side], r + 1);
+        if (EV) {
+          const int32_t evk = side ? evkb : evka;
+          if (evk >= 0) {
+            const int h = k >> 1;
+            const uint32_t pos = fld(epre, 2 * side + h) + (h ? fld(etot, 2 * side) : 0u) +
+                                 ((k & 1) ? ((fl >> (8 * side + 4 + k - 1)) & 1u) : 0u);
+            const int prev = (int)((os >> (3 * (4 * side + k))) & 7u);
+            ev_put(d, evk, (side ? evbb : evba) + pos, r, X[r], prev == GX_ABSENT ? GX_UNKNOWN : prev);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    tile_owner_times(d, side ? b : a, X, o0, no, s_lu, s_lc);
+    __syncthreads();
+  }
+  return EV ? (fld(etot, 0) + fld(etot, 1)) | ((fld(etot, 2) + fld(etot, 3)) << 16) : 0u;
+}
+
 // `ext` (when both = false): B is host b's row from another shard (read-only); the pair's
 // exchange is counted where a is the pair's first member (count_ex). With `emask`, ext holds only
 // the 512-slot blocks whose bit is set (ascending); every other block of B is A's own block (the
 // digests matched), which merges with the counts of the identical remote block and no change.
 // PF = tiles whose loads are in flight while one is merged; NT = non-temporal loads.
-template <bool VEC, int PF = 1, bool NT = false>
+template <bool VEC, int PF = 1, bool NT = false, bool EV = false>
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
                  unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false,
                  const uint32_t *emask = nullptr) {
@@ -942,16 +1034,23 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
   uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
   uint32_t na = 0, nb = 0;
-  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0, ma = ~0ull, mb = ~0ull;
+  uint32_t c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0;  // per thread: < 2^32
+  unsigned long long ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
   const uint32_t TILE = 4 * blockDim.x;
   // change bookkeeping: per-owner last accept / status change of each tile, the
   // last status change of the pass (state.LastChanged), events for listening views; key order
   __shared__ uint32_t s_lu[TILE_OWNERS], s_lc[TILE_OWNERS];
   __shared__ uint32_t s_last[2];
-  const int32_t evka = d.ev_slot[li(d, a)], evkb = both ? d.ev_slot[li(d, b)] : -1;
-  const uint32_t ev0a = evka >= 0 ? d.ev_cnt[evka] : 0, ev0b = evkb >= 0 ? d.ev_cnt[evkb] : 0;
-  uint32_t nev_a = 0, nev_b = 0, last_a = 0, last_b = 0;
+  if (t < 2) s_last[t] = 0;  // read after the pass's barriers
+  const int32_t evka = __builtin_amdgcn_readfirstlane(d.ev_slot[li(d, a)]);
+  const int32_t evkb = __builtin_amdgcn_readfirstlane(both ? d.ev_slot[li(d, b)] : -1);
+  const uint32_t ev0a = __builtin_amdgcn_readfirstlane(evka >= 0 ? d.ev_cnt[evka] : 0);
+  const uint32_t ev0b = __builtin_amdgcn_readfirstlane(evkb >= 0 ? d.ev_cnt[evkb] : 0);
+  uint32_t nev_a = 0, nev_b = 0;
+  // S | 128 without events: server times by lane-group shuffles (side_times_shfl)
+  const bool shfl_times = !EV && VEC && d.S >= 2 && (128u % d.S) == 0;
+  uint32_t lk_a = 0, lk_b = 0;
   // Software pipeline: the next PF 1024-slot tiles' loads are in flight while this tile is
   // merged, written back and (only if something was accepted) compacted.
   uint64_t qa[PF][4], qb[PF][4];
@@ -985,13 +1084,14 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   };
   auto merge_tile = [&](uint32_t base, const uint64_t *wa, const uint64_t *wb) {
     uint64_t nwa[4], nwb[4];
-    bool fa[4], fb[4], xa[4], xb[4], ca[4], cb[4];
+    bool fa[4], fb[4];
+    uint32_t accb = 0;  // bit k: side a accepted slot k, bit 8 + k: side b
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       nwa[k] = wa[k];
       nwb[k] = wb[k];
-      fa[k] = fb[k] = xa[k] = xb[k] = false;
+      fa[k] = fb[k] = false;
       if (st_of(wb[k]) != GX_ABSENT) {  // a.Merge(b): every present record of b
         bool ac, st;
         c_merge++;
@@ -1000,7 +1100,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         if (ac) {
           c_acc++;
           fa[k] = r / d.S != a;
-          xa[k] = true;
+          accb |= 1u << k;
         }
       }
       if (both && st_of(wa[k]) != GX_ABSENT) {  // b.Merge(a's snapshot)
@@ -1011,13 +1111,10 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         if (ac) {
           c_acc++;
           fb[k] = r / d.S != b;
-          xb[k] = true;
+          accb |= 1u << (8 + k);
         }
       }
-      // ServiceChanged: an insert, or a stored status that differs (:317-340)
-      ca[k] = xa[k] && (st_of(wa[k]) == GX_ABSENT || st_of(wa[k]) != st_of(nwa[k]));
-      cb[k] = xb[k] && (st_of(wb[k]) == GX_ABSENT || st_of(wb[k]) != st_of(nwb[k]));
-      c_chg += ca[k] + cb[k];
+
       if (nwa[k] != wa[k]) {
         c_wr++;
         unsigned long long x = exp_time(d.p, nwa[k]);
@@ -1046,48 +1143,29 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     unsigned long long cnt = (unsigned long long)(fa[0] + fa[1]) | ((unsigned long long)(fa[2] + fa[3]) << 16) |
                              ((unsigned long long)(fb[0] + fb[1]) << 32) | ((unsigned long long)(fb[2] + fb[3]) << 48);
-    bool anyx = xa[0] | xa[1] | xa[2] | xa[3] | xb[0] | xb[1] | xb[2] | xb[3];
-    if (!__syncthreads_or(anyx)) return;  // nothing accepted in this tile: no retransmits, no changes
-    {  // server times (both sides) and ChangeEvents, key order
-      uint32_t o0 = base / d.S, oe = ((base + TILE < d.R ? base + TILE : d.R) - 1) / d.S, no = oe - o0 + 1;
-      unsigned long long ec = (unsigned long long)(ca[0] + ca[1]) | ((unsigned long long)(ca[2] + ca[3]) << 16) |
-                              ((unsigned long long)(cb[0] + cb[1]) << 32) | ((unsigned long long)(cb[2] + cb[3]) << 48);
-      unsigned long long etot;
-      unsigned long long epre = block_excl_scan64(ec, s_wave, etot);
-      uint32_t pe[4] = {fld(epre, 0), fld(epre, 0) + ca[0], fld(etot, 0) + fld(epre, 1), 0};
-      pe[3] = pe[2] + ca[2];
-      uint32_t qe[4] = {fld(epre, 2), fld(epre, 2) + cb[0], fld(etot, 2) + fld(epre, 3), 0};
-      qe[3] = qe[2] + cb[2];
-      uint32_t ta = fld(etot, 0) + fld(etot, 1), tb = fld(etot, 2) + fld(etot, 3);
-      for (int side = 0; side < (both ? 2 : 1); side++) {
-        const bool *xf = side ? xb : xa, *cf = side ? cb : ca;
-        const uint64_t *wo = side ? wb : wa, *wn = side ? nwb : nwa;
-        const uint32_t *pp = side ? qe : pe;
-        const uint32_t tn = side ? tb : ta;
-        const int32_t evk = side ? evkb : evka;
-        const uint32_t evb = side ? ev0b + nev_b : ev0a + nev_a;
-        uint32_t x = side ? b : a;
-        for (uint32_t i = t; i < no; i += blockDim.x) s_lu[i] = s_lc[i] = 0;
-        __syncthreads();
+    // change flags and old statuses, packed so that they are all the bookkeeping below keeps
+    // fl bit 8*side + k: accepted, bit 8*side + 4 + k: status changed (ServiceChanged: an insert,
+    // or a stored status that differs, :317-340); os: old statuses (events only)
+    uint32_t fl = 0, os = 0;
+    const bool wave_acc = __ballot(accb != 0) != 0;
+    if (wave_acc) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
-          if (xf[k]) atomicMax(&s_lu[r / d.S - o0], r + 1);
-          if (cf[k]) {
-            atomicMax(&s_lc[r / d.S - o0], r + 1);
-            if (pp[k] == tn - 1) s_last[side] = r + 1;
-            if (evk >= 0)
-              ev_put(d, evk, evb + pp[k], r, wn[k], st_of(wo[k]) == GX_ABSENT ? GX_UNKNOWN : st_of(wo[k]));
-          }
-        }
-        __syncthreads();
-        tile_owner_times(d, x, side ? B : A, o0, no, s_lu, s_lc);
-        __syncthreads();
+      for (int k = 0; k < 4; k++) {
+        bool ca = ((accb >> k) & 1u) && (st_of(wa[k]) == GX_ABSENT || st_of(wa[k]) != st_of(nwa[k]));
+        bool cb = ((accb >> (8 + k)) & 1u) && (st_of(wb[k]) == GX_ABSENT || st_of(wb[k]) != st_of(nwb[k]));
+        fl |= (accb & (0x101u << k)) | ((uint32_t)ca << (4 + k)) | ((uint32_t)cb << (12 + k));
+        c_chg += ca + cb;
+        if (EV) os |= ((uint32_t)st_of(wa[k]) << (3 * k)) | ((uint32_t)st_of(wb[k]) << (3 * (4 + k)));
       }
-      if (ta) last_a = s_last[0];
-      if (tb) last_b = s_last[1];
-      nev_a += ta;
-      nev_b += tb;
+    }
+    if (shfl_times) {
+      if (wave_acc) {  // this wave accepted something
+        side_times_shfl(d, a, base, fl & 0xffu, nwa, lk_a, c_wr);  // server times count as written words
+        if (both) side_times_shfl(d, b, base, (fl >> 8) & 0xffu, nwb, lk_b, c_wr);
+      }
+      if (!__syncthreads_or(cnt != 0)) return;  // no foreign record accepted: no retransmits
+    } else if (!__syncthreads_or(fl != 0)) {
+      return;  // nothing accepted in this tile: no retransmits, no changes
     }
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
@@ -1110,6 +1188,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     na += fld(tot, 0) + fld(tot, 1);
     nb += fld(tot, 2) + fld(tot, 3);
+    // server times (both sides) and ChangeEvents, key order (out of line: rare, register-heavy)
+    if (!shfl_times) {
+      uint32_t done = ae_book<VEC, EV>(d, a, b, both, base, fl, os, A, B, s_lu, s_lc, s_last, s_wave, evka, evkb,
+                                       ev0a + nev_a, ev0b + nev_b);
+      nev_a += done & 0xffffu;
+      nev_b += done >> 16;
+    }
   };
 #pragma unroll
   for (int s = 0; s < PF; s++)
@@ -1133,16 +1218,28 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   ma = block_min(ma, s_red);
   mb = block_min(mb, s_red);
   block_ctr(d, C_CHG, c_chg, s_red);
+  if (shfl_times) {  // the pass's last changed key per side (it is in the row now)
+    for (int o = 32; o > 0; o >>= 1) {
+      uint32_t ya = __shfl_xor(lk_a, o, 64), yb = __shfl_xor(lk_b, o, 64);
+      lk_a = ya > lk_a ? ya : lk_a;
+      lk_b = yb > lk_b ? yb : lk_b;
+    }
+    if ((t & 63) == 0) {
+      if (lk_a) atomicMax(&s_last[0], lk_a);
+      if (lk_b) atomicMax(&s_last[1], lk_b);
+    }
+    __syncthreads();
+  }
   if (t == 0) {
-    if (last_a) d.vlc[li(d, a)] = ts_of(A[last_a - 1]);
-    if (both && last_b) d.vlc[li(d, b)] = ts_of(B[last_b - 1]);
+    if (s_last[0]) d.vlc[li(d, a)] = ts_of(A[s_last[0] - 1]);
+    if (both && s_last[1]) d.vlc[li(d, b)] = ts_of(B[s_last[1] - 1]);
     if (evka >= 0) d.ev_cnt[evka] = ev0a + nev_a;
     if (evkb >= 0) d.ev_cnt[evkb] = ev0b + nev_b;
   }
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && (t & 63) == 0) mark_change(d);
-  c_wr = wave_sum(c_wr);
-  if ((t & 63) == 0) kbytes(d, GX_K_AE, 8ull * c_wr, 0);
+  unsigned long long cw = wave_sum((unsigned long long)c_wr);
+  if ((t & 63) == 0) kbytes(d, GX_K_AE, 8ull * cw, 0);
   block_ctr(d, C_AE_MERGES, c_merge, s_red);
   block_ctr(d, C_AE_ACC, c_acc, s_red);
   block_ctr(d, C_STALE, c_stale, s_red);
@@ -1160,8 +1257,8 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   }
 }
 
-template <bool VEC, int PF = 1, bool NT = false>
-__global__ __launch_bounds__(256) void k_ae(Dev d, uint64_t key0, uint64_t key1) {
+template <bool VEC, bool EV, int PF, bool NT>
+GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
   uint32_t t = blockIdx.x, base = 0, m = d.H, q = t;
@@ -1179,20 +1276,32 @@ __global__ __launch_bounds__(256) void k_ae(Dev d, uint64_t key0, uint64_t key1)
   }
   uint32_t a = base + feistel_perm(key, 2 * q, m);
   uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
-  ae_pair<VEC, PF, NT>(d, a, b, true, s_wave, s_red);
+  ae_pair<VEC, PF, NT, EV>(d, a, b, true, s_wave, s_red);
 }
 
+// The push-pull kernel, without ChangeEvents (no listener anywhere): kept within 128 VGPRs so
+// that 4 waves per SIMD stay resident; with events (listeners present) a separate entry point.
+template <bool VEC, int PF = 1, bool NT = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae(Dev d, uint64_t key0,
+                                                                                   uint64_t key1) {
+  ae_round_pair<VEC, false, PF, NT>(d, key0, key1);
+}
 template <bool VEC>
+__global__ __launch_bounds__(256) void k_ae_ev(Dev d, uint64_t key0, uint64_t key1) {
+  ae_round_pair<VEC, true, 1, false>(d, key0, key1);
+}
+
+template <bool VEC, bool EV>
 __global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32_t src) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
-  ae_pair<VEC>(d, dst, src, false, s_wave, s_red);
+  ae_pair<VEC, 1, false, EV>(d, dst, src, false, s_wave, s_red);
 }
 
 // Sharded push-pull: plan entry i = (a, b, k): k < 0 -> both members here (a <-> b); k >= 0 ->
 // a is here and b's differing blocks are delta message k of `in` (at off[k], mask k): a <- b only.
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_ae_plan(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
+template <bool VEC, bool EV>
+GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
                                                   const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
                                                   const uint32_t *mask, uint32_t nmw) {
   __shared__ unsigned long long s_wave[4];
@@ -1200,11 +1309,23 @@ __global__ __launch_bounds__(256) void k_ae_plan(Dev d, const uint32_t *pa, cons
   uint32_t i = blockIdx.x;
   int32_t k = prow[i];
   if (k < 0) {
-    ae_pair<VEC>(d, pa[i], pb[i], true, s_wave, s_red);
+    ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], true, s_wave, s_red);
   } else {
     const uint64_t *blocks = reinterpret_cast<const uint64_t *>(in + off[k] + 16);
-    ae_pair<VEC>(d, pa[i], pb[i], false, s_wave, s_red, blocks, pcount[i] != 0, mask + (size_t)k * nmw);
+    ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, blocks, pcount[i] != 0, mask + (size_t)k * nmw);
   }
+}
+template <bool VEC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae_plan(
+    Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow, const uint8_t *pcount, const uint8_t *in,
+    const uint64_t *off, const uint32_t *mask, uint32_t nmw) {
+  ae_plan_pair<VEC, false>(d, pa, pb, prow, pcount, in, off, mask, nmw);
+}
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_ae_plan_ev(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
+                                                     const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
+                                                     const uint32_t *mask, uint32_t nmw) {
+  ae_plan_pair<VEC, true>(d, pa, pb, prow, pcount, in, off, mask, nmw);
 }
 
 // Push-pull digests of this shard's cross-pair rows (gx.h "digest"): one block per pair, one wave
