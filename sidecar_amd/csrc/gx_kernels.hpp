@@ -52,6 +52,17 @@ GXD unsigned long long block_min(unsigned long long x, unsigned long long *s_red
   return m;
 }
 
+GXD unsigned long long block_sum(unsigned long long x, unsigned long long *s_red) {
+  x = wave_sum(x);
+  uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if (lane == 0) s_red[w] = x;
+  __syncthreads();
+  unsigned long long m = 0;
+  for (uint32_t i = 0; i < nw; i++) m += s_red[i];
+  __syncthreads();
+  return m;
+}
+
 // =================================================================================== init ==
 __global__ void k_init_rec(Dev d, uint64_t *rec_word) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1035,6 +1046,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
   uint32_t na = 0, nb = 0;
   uint32_t c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0;  // per thread: < 2^32
+  uint32_t c_qa = 0, c_qb = 0;  // retransmits counted after both FIFOs filled up (all dropped)
   unsigned long long ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
   const uint32_t TILE = 4 * blockDim.x;
@@ -1163,6 +1175,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         side_times_shfl(d, a, base, fl & 0xffu, nwa, lk_a, c_wr);  // server times count as written words
         if (both) side_times_shfl(d, b, base, (fl >> 8) & 0xffu, nwb, lk_b, c_wr);
       }
+      // Both FIFOs full (block-uniform): every further retransmit is dropped, so its position no
+      // longer matters; count it per thread and reduce once after the pass (no scan, no barrier).
+      if (na >= rooma && (!both || nb >= roomb)) {
+        c_qa += fld(cnt, 0) + fld(cnt, 1);
+        c_qb += fld(cnt, 2) + fld(cnt, 3);
+        return;
+      }
       if (!__syncthreads_or(cnt != 0)) return;  // no foreign record accepted: no retransmits
     } else if (!__syncthreads_or(fl != 0)) {
       return;  // nothing accepted in this tile: no retransmits, no changes
@@ -1217,6 +1236,11 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   }
   ma = block_min(ma, s_red);
   mb = block_min(mb, s_red);
+  if (shfl_times) {
+    unsigned long long q = block_sum((unsigned long long)c_qa | ((unsigned long long)c_qb << 32), s_red);
+    na += (uint32_t)q;
+    nb += (uint32_t)(q >> 32);
+  }
   block_ctr(d, C_CHG, c_chg, s_red);
   if (shfl_times) {  // the pass's last changed key per side (it is in the row now)
     for (int o = 32; o > 0; o >>= 1) {
