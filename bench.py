@@ -139,29 +139,43 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
         c.close()
 
 
-def cpu_baseline(cfg, seconds):
-    """The CPU oracle (single thread) on a bounded sample of the same scenario, scaled down in H
-    so it runs ~`seconds` of CPU work. Returns the cpu_baseline object."""
+def _oracle_rate(lib, cfg, h_sample, warmup, steps):
+    """Merges/s of the oracle over rounds [warmup, warmup + steps) of cfg's schedule at H = h_sample
+    (the GPU bench's own round window, so both see the same storm / push-pull / gossip mix)."""
     from sidecar_amd.abi import Engine, default_params
-    from tests.oracle_lib import load_oracle
-    orc = load_oracle()
     p = dict(CONFIGS[cfg]["p"])
-    h_sample = min(p["n_hosts"], 2048)
-    p["n_hosts"] = h_sample
-    pr = default_params(orc, **p)
-    e = Engine(pr, lib=orc)
-    t0 = time.perf_counter()
+    p["n_hosts"] = min(p["n_hosts"], h_sample)
+    e = Engine(default_params(lib, **p), lib=lib)
+    if warmup:
+        e.run_rounds(warmup)
     st0 = e.stats()
-    while time.perf_counter() - t0 < seconds:
-        e.run_rounds(10)
+    t0 = time.perf_counter()
+    e.run_rounds(steps)
     dt = time.perf_counter() - t0
-    st = e.stats()
-    m = merges(st) - merges(st0)
+    m = merges(e.stats()) - merges(st0)
     e.close()
-    return {"value": m / dt, "unit": "record-merges/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/gx_oracle.c single-threaded, same {cfg} schedule at H={h_sample} "
-                      f"(S={p['n_services']}), rounds 0..{st['round']} in {dt:.1f}s; "
-                      f"Go reference unavailable (no Go toolchain on the box)"}
+    return m / dt, dt, p
+
+
+def cpu_baseline(cfg, warmup, steps, h_mt=8192, h_single=2048):
+    """The CPU oracle on a bounded sample of the same workload: the bench's round window of cfg's
+    schedule with H scaled down (about 10 s each). The multi-threaded build (per-host phase loops
+    on every core this process may use, OpenMP) is the reported baseline; the serial build (the
+    reference's one merge goroutine per node, services_state.go:129-135) is reported beside it."""
+    import ctypes
+    from tests.oracle_lib import load_oracle
+    omp = load_oracle(omp=True)
+    omp.gx_oracle_threads.restype = ctypes.c_int
+    threads = int(omp.gx_oracle_threads())
+    v_mt, dt_mt, p = _oracle_rate(omp, cfg, h_mt, warmup, steps)
+    v_1, dt_1, p1 = _oracle_rate(load_oracle(), cfg, h_single, warmup, steps)
+    win = f"rounds [{warmup}, {warmup + steps})"
+    return {"value": v_mt, "unit": "record-merges/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/gx_oracle.c built with OpenMP ({threads} threads over hosts), same {cfg} "
+                      f"schedule at H={p['n_hosts']} (S={p['n_services']}), {win} in {dt_mt:.1f}s; "
+                      f"Go reference unavailable (no Go toolchain on the box)",
+            "single_thread": {"value": v_1, "cores": 1,
+                              "sample": f"serial oracle at H={p1['n_hosts']}, {win} in {dt_1:.1f}s"}}
 
 
 def main():
@@ -175,7 +189,7 @@ def main():
     ap.add_argument("--converge-max", type=int, default=3000)
     ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-hosts", type=int, default=8192, help="H of the multi-threaded CPU sample")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     args = ap.parse_args()
 
@@ -256,7 +270,7 @@ def main():
                 "rounds_run": ran, "simulated_s": (r * 0.2) if r else None}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, args.cpu_seconds)
+        cpu = cpu_baseline(args.config, args.warmup, args.steps, h_mt=args.cpu_hosts)
 
     if rank == 0:
         cfgp = CONFIGS[args.config]["p"]

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stddef.h>
 
 typedef struct grec {
   uint64_t w; /* packed (ts << 3) | status */
@@ -103,6 +104,61 @@ static inline void set_slot(gx_engine *e, uint64_t *slot, uint64_t nw) {
     *slot = nw;
     e->st.last_change_round = e->round;
   }
+}
+
+/* ------------------------------------------------------------- per-host parallel loops ---- */
+/* Every phase of a round touches only the state of the host it runs for (its view row, FIFO,
+ * sleep ring, pending deque, lists, server times), so a phase is a loop over hosts whose
+ * iterations commute. for_hosts runs fn(e, i, ctx) for i in [0, n). Built with GX_ORACLE_OMP
+ * (liboracle_gx_omp.so, the multi-threaded CPU baseline of bench.py) it runs the iterations on
+ * OpenMP threads, each with a private copy of the engine header whose counters are summed
+ * afterwards; listeners keep it serial (their channels live in the header). The serial build is
+ * the checker; tests/test_oracle_omp.py checks that both builds agree bit for bit. */
+typedef void (*host_fn)(gx_engine *e, uint32_t i, void *ctx);
+#ifdef GX_ORACLE_OMP
+#include <omp.h>
+static int any_listener(const gx_engine *e) {
+  for (int i = 0; i < GX_MAX_LISTENERS; i++)
+    if (e->lst[i].used) return 1;
+  return 0;
+}
+static void stats_merge(gx_stats *dst, const gx_stats *src) {
+  uint64_t *d = (uint64_t *)dst;
+  const uint64_t *s = (const uint64_t *)src;
+  const size_t n = sizeof(gx_stats) / sizeof(uint64_t);
+  const size_t i_round = offsetof(gx_stats, round) / sizeof(uint64_t);
+  const size_t i_lcr = offsetof(gx_stats, last_change_round) / sizeof(uint64_t);
+  for (size_t i = 0; i < n; i++)
+    if (i != i_round && i != i_lcr) d[i] += s[i];
+  if (src->last_change_round > dst->last_change_round) dst->last_change_round = src->last_change_round;
+}
+#endif
+/* Threads the phase loops use (oracle-only symbol, not part of gx.h): bench.py reports it as
+ * cpu_baseline.cores. */
+int gx_oracle_threads(void) {
+#ifdef GX_ORACLE_OMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+static void for_hosts(gx_engine *e, uint32_t n, host_fn fn, void *ctx) {
+#ifdef GX_ORACLE_OMP
+  if (n > 1 && !any_listener(e)) {
+#pragma omp parallel
+    {
+      gx_engine loc = *e;
+      memset(&loc.st, 0, sizeof loc.st);
+      loc.st.last_change_round = e->st.last_change_round;
+#pragma omp for schedule(dynamic, 4)
+      for (uint32_t i = 0; i < n; i++) fn(&loc, i, ctx);
+#pragma omp critical
+      stats_merge(&e->st, &loc.st);
+    }
+    return;
+  }
+#endif
+  for (uint32_t i = 0; i < n; i++) fn(e, i, ctx);
 }
 
 /* ------------------------------------------------------------------------ broadcast FIFO -- */
@@ -627,46 +683,65 @@ static uint32_t shard_of(const gx_engine *e, uint32_t v) {
 }
 static int is_local(const gx_engine *e, uint32_t v) { return v >= e->lo && v < e->hi; }
 
-/* Phases 0-3 of the current round for this engine's hosts. */
+/* Phases 0-3 of the current round for this engine's hosts. Each phase is a loop over hosts
+ * (for_hosts); a host's iteration touches only that host's state. */
+static void ph_wake(gx_engine *e, uint32_t i, void *ctx) {
+  (void)ctx;
+  wake_host(e, e->lo + i);
+}
+/* owners: discovery churn, BroadcastServices(+TrackNewServices), BroadcastTombstones */
+static void ph_owner(gx_engine *e, uint32_t i, void *ctx) {
+  int64_t now = *(const int64_t *)ctx;
+  uint32_t o = e->lo + i;
+  churn(e, o);
+  gx_host_state *h = &e->hs[o];
+  if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
+  if (!(h->flags & 2u) && h->bt_next <= e->round) bt_tick(e, o, now);
+}
+/* SWIM departure storm: NotifyLeave -> ExpireServer for every host of the other half */
+static void ph_storm(gx_engine *e, uint32_t i, void *ctx) {
+  int64_t now = *(const int64_t *)ctx;
+  uint32_t v = e->lo + i, half = e->H / 2;
+  uint32_t lo = v < half ? half : 0, hi = v < half ? e->H : half;
+  for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
+}
+/* gossip send: GetBroadcasts once per selected peer */
+static void ph_send(gx_engine *e, uint32_t i, void *ctx) {
+  (void)ctx;
+  uint32_t u = e->lo + i, K = e->K, cap = e->p.packet_cap;
+  uint32_t peers[64];
+  uint32_t np = sample_peers(e, u, peers);
+  for (uint32_t j = 0; j < np; j++) {
+    uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap], e->p.limit_bytes,
+                                e->p.overhead_bytes);
+    e->msg_len[(size_t)u * K + j] = l;
+    e->msg_dst[(size_t)u * K + j] = peers[j];
+    if (l == 0 && e->p.gossip_stop_on_empty) break;
+  }
+}
 static void round_send(gx_engine *e) {
   int64_t now = now_of(e);
-  uint32_t H = e->H, K = e->K, cap = e->p.packet_cap;
-  for (uint32_t v = e->lo; v < e->hi; v++) wake_host(e, v);
-  /* owners: discovery churn, BroadcastServices(+TrackNewServices), BroadcastTombstones */
-  for (uint32_t o = e->lo; o < e->hi; o++) {
-    churn(e, o);
-    gx_host_state *h = &e->hs[o];
-    if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
-    if (!(h->flags & 2u) && h->bt_next <= e->round) bt_tick(e, o, now);
-  }
-  /* SWIM departure storm: NotifyLeave -> ExpireServer for every host of the other half */
-  if (e->p.storm_round >= 0 && e->round == e->p.storm_round) {
-    uint32_t half = H / 2;
-    for (uint32_t v = e->lo; v < e->hi; v++) {
-      uint32_t lo = v < half ? half : 0, hi = v < half ? H : half;
-      for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
-    }
-  }
-  /* gossip send: GetBroadcasts once per selected peer */
-  for (size_t i = 0; i < (size_t)H * K; i++) e->msg_len[i] = 0;
-  for (uint32_t u = e->lo; u < e->hi; u++) {
-    uint32_t peers[64];
-    uint32_t np = sample_peers(e, u, peers);
-    for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap], e->p.limit_bytes,
-                                  e->p.overhead_bytes);
-      e->msg_len[(size_t)u * K + j] = l;
-      e->msg_dst[(size_t)u * K + j] = peers[j];
-      if (l == 0 && e->p.gossip_stop_on_empty) break;
-    }
-  }
+  uint32_t n = e->hi - e->lo;
+  for_hosts(e, n, ph_wake, NULL);
+  for_hosts(e, n, ph_owner, &now);
+  if (e->p.storm_round >= 0 && e->round == e->p.storm_round) for_hosts(e, n, ph_storm, &now);
+  for (size_t i = 0; i < (size_t)e->H * e->K; i++) e->msg_len[i] = 0;
+  for_hosts(e, n, ph_send, NULL);
 }
 
 /* Phase 4: packets to this engine's receivers in sender order -> NotifyMsg -> AddServiceEntry.
  * Packets from other shards were unpacked into the same H*K message table. */
+static void ph_receive(gx_engine *e, uint32_t i, void *ctx) {
+  int64_t now = *(const int64_t *)ctx;
+  uint32_t v = e->lo + i, cap = e->p.packet_cap;
+  for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) {
+    uint32_t m = e->in_list[x];
+    for (uint32_t y = 0; y < e->msg_len[m]; y++) add_entry(e, v, e->msg[(size_t)m * cap + y], now, SRC_GOSSIP);
+  }
+}
 static void round_merge(gx_engine *e) {
   int64_t now = now_of(e);
-  uint32_t H = e->H, K = e->K, cap = e->p.packet_cap;
+  uint32_t H = e->H, K = e->K;
   memset(e->in_cnt, 0, sizeof(uint32_t) * (H + 1));
   for (size_t m = 0; m < (size_t)H * K; m++)
     if (e->msg_len[m] && is_local(e, e->msg_dst[m])) e->in_cnt[e->msg_dst[m] + 1]++;
@@ -676,11 +751,7 @@ static void round_merge(gx_engine *e) {
   for (size_t m = 0; m < (size_t)H * K; m++)
     if (e->msg_len[m] && is_local(e, e->msg_dst[m])) e->in_list[cur[e->msg_dst[m]]++] = (uint32_t)m;
   free(cur);
-  for (uint32_t v = e->lo; v < e->hi; v++)
-    for (uint32_t i = e->in_cnt[v]; i < e->in_cnt[v + 1]; i++) {
-      uint32_t m = e->in_list[i];
-      for (uint32_t x = 0; x < e->msg_len[m]; x++) add_entry(e, v, e->msg[(size_t)m * cap + x], now, SRC_GOSSIP);
-    }
+  for_hosts(e, e->hi - e->lo, ph_receive, &now);
 }
 
 static int ae_round(const gx_engine *e) {
@@ -723,15 +794,23 @@ static void ae_merge_row(gx_engine *e, uint32_t x, const uint64_t *row, int coun
   if (count_exchange) e->st.ae_exchanges++;
 }
 
+struct ae_ctx {
+  const uint32_t *pa, *pb;
+  int64_t now;
+};
+static void ph_ae_pair(gx_engine *e, uint32_t t, void *ctx) {
+  const struct ae_ctx *c = (const struct ae_ctx *)ctx;
+  if (is_local(e, c->pa[t]) && is_local(e, c->pb[t])) ae_exchange(e, c->pa[t], c->pb[t], c->now);
+}
 /* Phase 5, pairs with both hosts here: both merge the other's round-start row. */
 static void ae_phase_local(gx_engine *e) {
   if (!ae_round(e) || e->ae_local_round == e->round) return;
   int64_t now = now_of(e);
   uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
   uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  struct ae_ctx c = {pa, pb, now};
   uint32_t np = ae_pairs(e, pa, pb);
-  for (uint32_t t = 0; t < np; t++)
-    if (is_local(e, pa[t]) && is_local(e, pb[t])) ae_exchange(e, pa[t], pb[t], now);
+  for_hosts(e, np, ph_ae_pair, &c); /* pairs are disjoint: every host is in at most one */
   free(pa);
   free(pb);
   e->ae_local_round = e->round;

@@ -443,7 +443,8 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
     h->fifo_tail = tail0 + ok;
     if (jobs) d.vlc[vi] = d.now;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
-    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
+    // + 16 B of server times (LastUpdated, LastChanged) per live owner
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok + 16ull * jobs, (unsigned long long)(hi - lo) * d.S);
     ctr_atomic(d, C_EXPSRV, jobs);
     ctr_atomic(d, C_QDROP, jobs - ok);
   }
@@ -483,8 +484,9 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   const bool leader = lane % LPO == 0;
   uint64_t *row = &d.view[(size_t)vi * d.R + (size_t)lo * d.S];
   const uint32_t nw = (hi - lo) * d.S;
-  ulonglong2 q[2];
-  auto load = [&](uint32_t base) {
+  // two 1024-word tiles in flight while one is processed (q0: even tiles, q1: odd tiles)
+  ulonglong2 q0[2], q1[2];
+  auto load = [&](uint32_t base, ulonglong2 *q) {
 #pragma unroll
     for (int c = 0; c < 2; c++) {
       uint32_t r0 = base + 512 * c + 2 * t;
@@ -492,11 +494,9 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
                      : make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
     }
   };
-  load(0);
-  uint32_t it = 0;
-  for (uint32_t base = 0; base < nw; base += 1024, it ^= 1) {
-    ulonglong2 w[2] = {q[0], q[1]};
-    if (base + 1024 < nw) load(base + 1024);
+  load(0, q0);
+  if (1024 < nw) load(1024, q1);
+  auto tile = [&](uint32_t base, uint32_t it, const ulonglong2 *w) {
     bool lead_live[2], live_c[2];
     uint64_t pmask[2];
     uint32_t rank[2], erank[2], sh_c[2];
@@ -577,6 +577,18 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       }
       n_ev += etot;
     }
+  };
+  for (uint32_t base = 0; base < nw; base += 2048) {
+    {
+      ulonglong2 w[2] = {q0[0], q0[1]};
+      if (base + 2048 < nw) load(base + 2048, q0);
+      tile(base, 0, w);
+    }
+    if (base + 1024 < nw) {
+      ulonglong2 w[2] = {q1[0], q1[1]};
+      if (base + 3072 < nw) load(base + 3072, q1);
+      tile(base + 1024, 1, w);
+    }
   }
   bool changed = c_wr != 0;
   if (__ballot(changed) != 0 && lane == 0) {
@@ -594,7 +606,8 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
     h->fifo_tail = tail0 + ok;
     if (jobs) d.vlc[vi] = d.now;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
-    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok, (unsigned long long)(hi - lo) * d.S);
+    // + 16 B of server times (LastUpdated, LastChanged) per live owner
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok + 16ull * jobs, (unsigned long long)(hi - lo) * d.S);
     ctr_atomic(d, C_EXPSRV, jobs);
     ctr_atomic(d, C_QDROP, jobs - ok);
   }
