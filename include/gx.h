@@ -201,7 +201,9 @@ typedef struct gx_stats {
 #define GX_K_MERGE 5
 #define GX_K_AE 6
 #define GX_K_CONVERGE 7
-#define GX_K_COUNT 8
+#define GX_K_ENCODE 8 /* LocalState JSON encoder (gx_local_state_json) */
+#define GX_K_DECODE 9 /* Decode JSON parser (gx_decode_state_json, gx_merge_remote_state_json) */
+#define GX_K_COUNT 10
 typedef struct gx_timing {
   double ms[GX_K_COUNT];
   uint64_t launches[GX_K_COUNT];
@@ -366,6 +368,74 @@ int gx_remove_listener(gx_engine *e, uint32_t view, uint32_t id); /* :272-284; G
 /* Receive the listener's buffered events, oldest first (at most cap; n_out = received). */
 int gx_listener_drain(gx_engine *e, uint32_t view, uint32_t id, gx_change_event *out, uint32_t cap,
                       uint32_t *n_out);
+
+/* ---- full-state JSON codec ------------------------------------------------
+ * The wire format of memberlist push-pull: LocalState() = state.Encode() (services_delegate.go:
+ * 146-151, services_state.go:117-125) and MergeRemoteState(buf) = catalog.Decode(buf) + Merge
+ * (services_delegate.go:153-167, services_state.go:367-373, 774-782). The JSON is ffjson's
+ * ServicesState/Server/Service marshal (catalog/services_state_ffjson.go:771-803, 334-375;
+ * service/service_ffjson.go:370-436) with the Servers and Services maps falling back to
+ * encoding/json (sorted keys, HTML-escaped strings, no trailing newline).
+ *
+ * Names. The record model carries indices, so the codec needs the strings once:
+ *   hosts[host_off[o] .. host_off[o+1])  raw hostname of host o (Servers key, Server.Name,
+ *                                         Service.Hostname, state.Hostname of view o)
+ *   ids[id_off[r] .. id_off[r+1])        raw Service.ID of record r = host * S + svc
+ *   pre/post of record r                 its encoded Service JSON around the Updated value:
+ *       pre  = {"ID":..,"Name":..,"Image":..,"Created":..,"Hostname":..,"Ports":..,"Updated":
+ *       post = ,"ProxyMode":..,"Status":
+ *     exactly the bytes of Service.MarshalJSON after encoding/json's compaction (HTML-escaped);
+ *     the record's JSON is pre + time.MarshalJSON(Updated) + post + decimal Status + "}".
+ * gx_set_names also sets every record's static message bytes (gx_set_static_bytes) to
+ * len(pre) + len(post) + 1, so packPacket lengths and the codec agree.
+ * Times are formatted in UTC ("Z"): the reference formats time.Unix(0, 0) in the local zone,
+ * which is UTC in Sidecar's containers.
+ *
+ * Decoding accepts RFC 8259 JSON whose types match the Go structs (ffjson would fail otherwise:
+ * nothing is merged and GX_EINVAL is returned, the reference's "Failed to MergeRemoteState" log
+ * and return, services_delegate.go:158-162). Object keys match fields ASCII-case-insensitively,
+ * the last duplicate field wins, unknown fields are skipped. Deviations, all rejected with
+ * GX_EINVAL because the reference result is undefined or depends on Go map order: a null server
+ * or service (the reference panics in Merge), a repeated key inside the Servers map or one
+ * Services map, two records with the same (Hostname, ID), nesting deeper than GX_JSON_MAX_DEPTH.
+ * Records whose Hostname/ID are not in the names table are skipped and counted (`unknown`; the
+ * reference would create them, the engine's key space is fixed). Status outside 0..6 or Updated
+ * at or after 2^61 ns are skipped and counted (`invalid`). Updated before 1970 merges as
+ * time 0, which IsStale drops exactly like the original time. The decoded records are merged in
+ * key order (the model's Merge order), as anti-entropy merges. */
+#define GX_JSON_MAX_DEPTH 16
+typedef struct gx_names {
+  const char *cluster_name;
+  uint64_t cluster_name_len;
+  const char *hosts;
+  const uint64_t *host_off; /* [H + 1] */
+  const char *ids;
+  const uint64_t *id_off;   /* [R + 1] */
+  const char *pre;
+  const uint64_t *pre_off;  /* [R + 1] */
+  const char *post;
+  const uint64_t *post_off; /* [R + 1] */
+} gx_names;
+typedef struct gx_decode_stats {
+  uint64_t bytes;    /* input length */
+  uint64_t tokens;   /* JSON tokens (brackets, ':', ',', strings, scalars) */
+  uint32_t services; /* Service objects under the winning Servers / Services members */
+  uint32_t records;  /* records decoded (merged, for the merge call) */
+  uint32_t unknown;  /* Hostname/ID not in the names table */
+  uint32_t invalid;  /* Status outside 0..6 or Updated >= 2^61 ns */
+  int64_t error_at;  /* byte offset of the first error found, -1 = none (diagnostic only) */
+} gx_decode_stats;
+int gx_set_names(gx_engine *e, const gx_names *names);
+/* LocalState(): the view's ServicesState JSON. n_out = its length; with cap < n_out nothing is
+ * written (call again with a larger buffer). GX_ENOENT if no names were set. */
+int gx_local_state_json(gx_engine *e, uint32_t view, char *out, uint64_t cap, uint64_t *n_out);
+/* catalog.Decode(): the records of a ServicesState JSON in document order (n_out = total, at
+ * most cap written), without merging. */
+int gx_decode_state_json(gx_engine *e, const char *buf, uint64_t len, gx_service *out, uint32_t cap,
+                         uint32_t *n_out, gx_decode_stats *ds);
+/* MergeRemoteState(buf): Decode + Merge into `view`. */
+int gx_merge_remote_state_json(gx_engine *e, uint32_t view, const char *buf, uint64_t len,
+                               gx_decode_stats *ds);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */
 int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);

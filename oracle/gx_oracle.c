@@ -67,8 +67,10 @@ struct gx_engine {
     gx_change_event *ring;
   } lst[GX_MAX_LISTENERS];
   int64_t ae_local_round; /* round whose shard-local push-pull pairs gx_ae_merge_local merged */
+  struct onames *names;   /* full-state JSON codec names (gx_oracle_json.c), NULL until set */
   gx_stats st;
 };
+static void free_names(gx_engine *e);
 
 /* ---------------------------------------------------------------- helpers / schedule RNG -- */
 static inline uint64_t mix64(uint64_t z) {
@@ -1055,6 +1057,7 @@ int gx_destroy(gx_engine *e) {
   free(e->x_dig);
   free(e->x_diff);
   free(e->x_cnt);
+  free_names(e);
   free(e);
   return GX_OK;
 }
@@ -1693,3 +1696,6 @@ int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   if (n_disagree) *n_disagree = bad;
   return GX_OK;
 }
+
+/* Full-state JSON codec: LocalState / MergeRemoteState wire format. */
+#include "gx_oracle_json.c"

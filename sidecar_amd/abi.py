@@ -30,7 +30,7 @@ JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE = 0, 1, 2, 3, 4
 INIT_EMPTY, INIT_OWN, INIT_WARM = 0, 1, 2
 LIMIT_DEFAULT = 0xFFFFFFFF
 
-K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge"]
+K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode"]
 
 
 class GxService(C.Structure):
@@ -121,12 +121,27 @@ class GxStats(C.Structure):
 
 
 class GxTiming(C.Structure):
-    _fields_ = [("ms", C.c_double * 8), ("launches", C.c_uint64 * 8), ("bytes", C.c_uint64 * 8),
-                ("units", C.c_uint64 * 8)]
+    _fields_ = [("ms", C.c_double * 10), ("launches", C.c_uint64 * 10), ("bytes", C.c_uint64 * 10),
+                ("units", C.c_uint64 * 10)]
 
     def as_dict(self):
         return {K_NAMES[i]: {"ms": self.ms[i], "launches": self.launches[i],
-                             "bytes": self.bytes[i], "units": self.units[i]} for i in range(8)}
+                             "bytes": self.bytes[i], "units": self.units[i]} for i in range(10)}
+
+
+class GxNames(C.Structure):
+    _fields_ = [("cluster_name", C.c_char_p), ("cluster_name_len", C.c_uint64),
+                ("hosts", C.c_char_p), ("host_off", C.c_void_p), ("ids", C.c_char_p), ("id_off", C.c_void_p),
+                ("pre", C.c_char_p), ("pre_off", C.c_void_p), ("post", C.c_char_p), ("post_off", C.c_void_p)]
+
+
+class GxDecodeStats(C.Structure):
+    _fields_ = [("bytes", C.c_uint64), ("tokens", C.c_uint64), ("services", C.c_uint32),
+                ("records", C.c_uint32), ("unknown", C.c_uint32), ("invalid", C.c_uint32),
+                ("error_at", C.c_int64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 ABI_FUNCS = [
@@ -141,6 +156,7 @@ ABI_FUNCS = [
     "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
     "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
+    "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
 ]
 
 
@@ -194,6 +210,10 @@ def _declare(lib):
         "gx_get_broadcasts_bytes": ([vp, u32, u32, u32, P(GxService), u32, P(u32)], i32),
         "gx_set_static_bytes": ([vp, u32, u32, P(u16)], i32),
         "gx_message_bytes": ([vp, P(GxService), u32, P(u32)], i32),
+        "gx_set_names": ([vp, P(GxNames)], i32),
+        "gx_local_state_json": ([vp, u32, vp, C.c_uint64, P(C.c_uint64)], i32),
+        "gx_decode_state_json": ([vp, vp, C.c_uint64, P(GxService), u32, P(u32), P(GxDecodeStats)], i32),
+        "gx_merge_remote_state_json": ([vp, u32, vp, C.c_uint64, P(GxDecodeStats)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -415,6 +435,41 @@ class Engine:
         out = (GxService * cap)()
         check(self.lib.gx_local_state(self.h, view, out, cap, C.byref(n)))
         return [out[i] for i in range(n.value)]
+
+    # full-state JSON codec ------------------------------------------------
+    def set_names(self, names) -> None:
+        """gx_set_names from a sidecar_amd.codec.Names."""
+        hosts, hoff = names._blob(names.hosts)
+        ids, ioff = names._blob(names.ids)
+        pre, poff = names._blob(names.pre)
+        post, qoff = names._blob(names.post)
+        self._names_keep = (hosts, hoff, ids, ioff, pre, poff, post, qoff, names.cluster_name)
+        nm = GxNames(names.cluster_name, len(names.cluster_name), hosts, hoff.ctypes.data, ids, ioff.ctypes.data,
+                     pre, poff.ctypes.data, post, qoff.ctypes.data)
+        check(self.lib.gx_set_names(self.h, C.byref(nm)), "gx_set_names")
+
+    def local_state_json(self, view: int) -> bytes:
+        """LocalState(): the view's ServicesState JSON (services_delegate.go:146-151)."""
+        n = C.c_uint64()
+        check(self.lib.gx_local_state_json(self.h, view, None, 0, C.byref(n)), "gx_local_state_json")
+        buf = C.create_string_buffer(max(1, n.value))
+        check(self.lib.gx_local_state_json(self.h, view, buf, n.value, C.byref(n)), "gx_local_state_json")
+        return buf.raw[:n.value]
+
+    def decode_state_json(self, data: bytes, cap: Optional[int] = None):
+        """catalog.Decode(): (rc, records in document order, decode stats)."""
+        cap = (len(data) // 64 + 16) if cap is None else cap
+        out = (GxService * max(1, cap))()
+        n = C.c_uint32()
+        ds = GxDecodeStats()
+        rc = self.lib.gx_decode_state_json(self.h, data, len(data), out, cap, C.byref(n), C.byref(ds))
+        return rc, [out[i].tup() for i in range(min(n.value, cap))], ds.as_dict()
+
+    def merge_remote_state_json(self, view: int, data: bytes):
+        """MergeRemoteState(buf): (rc, decode stats)."""
+        ds = GxDecodeStats()
+        rc = self.lib.gx_merge_remote_state_json(self.h, view, data, len(data), C.byref(ds))
+        return rc, ds.as_dict()
 
     def notify_leave(self, view: int, node: int):
         check(self.lib.gx_notify_leave(self.h, view, node))

@@ -44,6 +44,7 @@ static uint32_t pow2_at_least(uint32_t x) {
 }
 
 #include "gx_kernels.hpp"
+#include "gx_codec.hpp"
 
 // ================================================================================ host ==
 struct TimedLaunch {
@@ -59,6 +60,8 @@ struct gx_engine {
   std::vector<TimedLaunch> pending_ev;
   double ms[GX_K_COUNT];
   uint64_t launches[GX_K_COUNT];
+  uint64_t host_bytes[GX_K_COUNT], host_units[GX_K_COUNT];  // codec classes (gx_codec_host.hpp)
+  struct CodecState *codec;
   grec *own_list;
   // sharded rounds: outbox entry list and push-pull plan (device), rebuilt per round
   uint32_t *ob_entries;
@@ -94,6 +97,8 @@ struct gx_engine {
   unsigned long long *conv_bad;
   uint64_t *digest_buf;
 };
+
+static void codec_free(gx_engine *e);  // gx_codec_host.hpp
 
 static int ensure_api(gx_engine *e, size_t bytes) {
   if (bytes <= e->api_dev_bytes) return GX_OK;
@@ -363,6 +368,7 @@ int gx_destroy(gx_engine *e) {
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  codec_free(e);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return GX_OK;
@@ -390,6 +396,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->timing = 0;
   memset(e->ms, 0, sizeof(e->ms));
   memset(e->launches, 0, sizeof(e->launches));
+  memset(e->host_bytes, 0, sizeof(e->host_bytes));
+  memset(e->host_units, 0, sizeof(e->host_units));
+  e->codec = nullptr;
   e->own_list = nullptr;
   e->api_dev = nullptr;
   e->api_dev_bytes = 0;
@@ -1423,8 +1432,8 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
   for (int i = 0; i < GX_K_COUNT; i++) {
     out->ms[i] = e->ms[i];
     out->launches[i] = e->launches[i];
-    out->bytes[i] = bytes[i];
-    out->units[i] = units[i];
+    out->bytes[i] = i < 8 ? bytes[i] : e->host_bytes[i];  // codec classes: accounted on the host
+    out->units[i] = i < 8 ? units[i] : e->host_units[i];
   }
   return GX_OK;
 }
@@ -1447,3 +1456,7 @@ int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
 }
 
 }  // extern "C"
+
+// full-state JSON codec: gx_set_names, gx_local_state_json, gx_decode_state_json,
+// gx_merge_remote_state_json
+#include "gx_codec_host.hpp"
