@@ -16,16 +16,20 @@ between it and the Status value.
 from __future__ import annotations
 
 import datetime as _dt
+import re
 from typing import Iterable, Optional, Sequence, Tuple
 
 import numpy as np
 
 _HEX = "0123456789abcdef"
+_PLAIN = re.compile(rb"[\x20-\x21\x23-\x25\x27-\x3b\x3d\x3f-\x5b\x5d-\x7e]*")
 
 
 def go_json_string(s) -> bytes:
     """encoding/json encodeState.string(s, escapeHTML=true), Go 1.13."""
     b = s.encode() if isinstance(s, str) else bytes(s)
+    if _PLAIN.fullmatch(b):  # nothing to escape
+        return b'"' + b + b'"'
     out = bytearray(b'"')
     i = 0
     n = len(b)
@@ -167,17 +171,17 @@ def synthetic_names(H: int, S: int, seed: int = 1, cluster: str = "default") -> 
     rng = np.random.default_rng(seed)
     hosts = [f"ip-10-{(o >> 16) & 255}-{(o >> 8) & 255}-{o & 255}.cluster.local" for o in range(H)]
     created0 = 1_424_891_086_000_000_000  # 2015-02-25T19:04:46Z
+    hx = rng.integers(0, 2**48, size=H * S)
+    cr = rng.integers(0, 86_400, size=H * S)
     ids, pre, post = [], [], []
     images = ["nginx:latest", "redis:5", "gossip/api:1.4.2", "0415448f2cc2"]
     for o in range(H):
         for j in range(S):
-            hx = rng.integers(0, 2**48)
-            sid = f"{int(hx):012x}"
-            name = f"/svc-{o}-{j}"
-            img = images[(o + j) % len(images)]
-            created = created0 + int(rng.integers(0, 86_400)) * 1_000_000_000
+            r = o * S + j
+            sid = f"{int(hx[r]):012x}"
             ports = [("tcp", 10000 + j, 8000 + j, f"10.{(o >> 8) & 255}.{o & 255}.{j}")]
-            a, b = service_fragments(sid, name, img, created, hosts[o], ports, "http")
+            a, b = service_fragments(sid, f"/svc-{o}-{j}", images[(o + j) % len(images)],
+                                     created0 + int(cr[r]) * 1_000_000_000, hosts[o], ports, "http")
             ids.append(sid)
             pre.append(a)
             post.append(b)

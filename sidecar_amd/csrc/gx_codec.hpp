@@ -308,96 +308,107 @@ __global__ __launch_bounds__(256) void k_enc_len(Dev d, Names nm, uint32_t vi, u
   }
 }
 
-// one wave per server position k: writes the server at out + HEAD + off[k]; the separator comma
-// after every server but the last one (off[k] + len[k] == total)
+// One wave per server. The server's bytes are assembled in a per-wave LDS buffer: the static
+// fragments (ID key, pre, post) of each entry are copied by the 64 lanes together (coalesced
+// reads); each entry's lane then formats its Updated time and Status in place; lane 0 writes the
+// footer. The buffer starts at the output address mod 4, so the wave stores it with aligned
+// dword stores (bytes only at the two ends). A server larger than the buffer is written by the
+// same steps straight to the output.
+#define ENC_LDS 12288
+GXD void put_bytes(char *dst, const char *src, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) dst[i] = src[i];
+}
 __global__ __launch_bounds__(256) void k_enc_write(Dev d, Names nm, uint32_t vi, const uint32_t *srv_len,
                                                    const uint32_t *srv_off, char *out) {
-  const uint32_t lane = threadIdx.x & 63, k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ __attribute__((aligned(16))) char lds[4][ENC_LDS + 16];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = blockIdx.x * 4 + wv;
   if (k >= d.H || srv_len[k] == 0) return;
   const uint32_t o = nm.host_order[k];
-  const uint64_t *row = d.view + (size_t)vi * d.R;
-  char *p = out + LLEN(L_HEAD) + srv_off[k];
-  const bool last = srv_off[k] + srv_len[k] == srv_off[d.H];
-  const char *eh = nm.ehost + nm.ehost_off[o];
-  const uint32_t ehn = (uint32_t)(nm.ehost_off[o + 1] - nm.ehost_off[o]);
-  // this lane's service (ID order)
-  uint32_t r = 0, len = 0;
-  uint64_t w = GX_SLOT_ABSENT;
+  const uint64_t gpos = LLEN(L_HEAD) + (uint64_t)srv_off[k];  // server's first byte in the output
+  const uint32_t slen = srv_len[k] - ((srv_off[k] + srv_len[k] == srv_off[d.H]) ? 1u : 0u);  // + separator
+  const bool in_lds = slen + 4 <= ENC_LDS;
+  char *base = in_lds ? lds[wv] + (gpos & 3) : out + gpos;
+  // this lane's entry (ID order)
+  uint32_t r = 0, len = 0, kn = 0, pn = 0, qn = 0;
+  uint64_t w = GX_SLOT_ABSENT, eo = 0, po = 0, qo = 0;
   bool present = false;
   if (lane < d.S) {
     r = o * d.S + nm.svc_order[(size_t)o * d.S + lane];
-    w = row[r];
+    w = d.view[(size_t)vi * d.R + r];
     present = st_of(w) != GX_ABSENT;
-    if (present) len = entry_len(nm, r, w) + 1;  // + comma
+    if (present) {
+      eo = nm.eid_off[r];
+      kn = (uint32_t)(nm.eid_off[r + 1] - eo);
+      po = nm.pre_off[r];
+      pn = (uint32_t)(nm.pre_off[r + 1] - po);
+      qo = nm.post_off[r];
+      qn = (uint32_t)(nm.post_off[r + 1] - qo);
+      len = kn + 1 + pn + time_len(ts_of(w)) + qn + 3;  // key : pre time post status } ,
+    }
   }
   uint32_t inc = len;
   for (int s = 1; s < 64; s <<= 1) {
     uint32_t y = __shfl_up(inc, s, 64);
     if ((int)lane >= s) inc += y;
   }
-  const uint32_t tot = __shfl(inc, 63, 64);  // entries + one comma each
-  wcopy(p, eh, ehn, lane);
-  p += ehn;
-  wcopy(p, L_NAME, LLEN(L_NAME), lane);
-  p += LLEN(L_NAME);
-  wcopy(p, eh, ehn, lane);
-  p += ehn;
-  wcopy(p, L_SVCS, LLEN(L_SVCS), lane);
-  p += LLEN(L_SVCS);
-  char *ent = p;
-  uint64_t pm = __ballot(present);
+  const uint32_t tot = __shfl(inc, 63, 64);
+  const char *eh = nm.ehost + nm.ehost_off[o];
+  const uint32_t ehn = (uint32_t)(nm.ehost_off[o + 1] - nm.ehost_off[o]);
+  wcopy(base, eh, ehn, lane);
+  wcopy(base + ehn, L_NAME, LLEN(L_NAME), lane);
+  wcopy(base + ehn + LLEN(L_NAME), eh, ehn, lane);
+  wcopy(base + 2 * ehn + LLEN(L_NAME), L_SVCS, LLEN(L_SVCS), lane);
+  char *ent = base + 2 * ehn + LLEN(L_NAME) + LLEN(L_SVCS);
+  // static fragments, entry by entry, all lanes copying
+  const uint64_t pall = __ballot(present);
+  uint64_t pm = pall;
   while (pm) {
     const int j = __ffsll((unsigned long long)pm) - 1;
     pm &= pm - 1;
-    const uint32_t rj = __shfl(r, j, 64);
-    const uint64_t wj = __shfl(w, j, 64);
     char *q = ent + (__shfl(inc, j, 64) - __shfl(len, j, 64));
-    const uint32_t kn = (uint32_t)(nm.eid_off[rj + 1] - nm.eid_off[rj]);
-    wcopy(q, nm.eid + nm.eid_off[rj], kn, lane);
-    q += kn;
-    if (lane == 0) *q = ':';
-    q += 1;
-    const uint32_t pn = (uint32_t)(nm.pre_off[rj + 1] - nm.pre_off[rj]);
-    wcopy(q, nm.pre + nm.pre_off[rj], pn, lane);
-    q += pn;
-    char tb[32];
-    const uint32_t tn = fmt_time(ts_of(wj), tb);
-    if (lane < tn) {
-#pragma unroll
-      for (uint32_t i = 0; i < 32; i++)
-        if (i == lane) q[i] = tb[i];
-    }
-    q += tn;
-    const uint32_t qn = (uint32_t)(nm.post_off[rj + 1] - nm.post_off[rj]);
-    wcopy(q, nm.post + nm.post_off[rj], qn, lane);
-    q += qn;
-    if (lane == 0) {
-      q[0] = (char)('0' + st_of(wj));
-      q[1] = '}';
-      q[2] = ',';  // the last entry's comma is overwritten by the footer below
-    }
+    const uint32_t jk = __shfl(kn, j, 64), jp = __shfl(pn, j, 64), jq = __shfl(qn, j, 64);
+    const uint32_t jt = time_len(ts_of(__shfl(w, j, 64)));
+    wcopy(q, nm.eid + __shfl(eo, j, 64), jk, lane);
+    wcopy(q + jk + 1, nm.pre + __shfl(po, j, 64), jp, lane);
+    wcopy(q + jk + 1 + jp + jt, nm.post + __shfl(qo, j, 64), jq, lane);
   }
-  p = ent + (tot ? tot - 1 : 0);
-  const gx_server_times st = d.srvt[(size_t)vi * d.H + o];
-  wcopy(p, L_LU, LLEN(L_LU), lane);
-  p += LLEN(L_LU);
-  char tb[32];
-  uint32_t tn = fmt_time(st.last_updated_ns, tb);
-#pragma unroll
-  for (uint32_t i = 0; i < 32; i++)
-    if (i == lane && i < tn) p[i] = tb[i];
-  p += tn;
-  wcopy(p, L_LC, LLEN(L_LC), lane);
-  p += LLEN(L_LC);
-  tn = fmt_time(st.last_changed_ns, tb);
-#pragma unroll
-  for (uint32_t i = 0; i < 32; i++)
-    if (i == lane && i < tn) p[i] = tb[i];
-  p += tn;
+  if (present) {  // this lane's own entry: ':', Updated, Status, '}', ','
+    char *q = ent + (inc - len);
+    q[kn] = ':';
+    q += kn + 1 + pn;
+    q += fmt_time(ts_of(w), q) + qn;
+    q[0] = (char)('0' + st_of(w));
+    q[1] = '}';
+    if (pall >> (lane + 1)) q[2] = ',';  // not the last entry; the footer follows the last one
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (lane == 0) {
-    p[0] = '}';
-    if (!last) p[1] = ',';
+    char *f = ent + (tot ? tot - 1 : 0);
+    const gx_server_times st = d.srvt[(size_t)vi * d.H + o];
+    put_bytes(f, L_LU, LLEN(L_LU));
+    f += LLEN(L_LU);
+    f += fmt_time(st.last_updated_ns, f);
+    put_bytes(f, L_LC, LLEN(L_LC));
+    f += LLEN(L_LC);
+    f += fmt_time(st.last_changed_ns, f);
+    f[0] = '}';
+    if (srv_off[k] + srv_len[k] != srv_off[d.H]) f[1] = ',';
   }
+  if (!in_lds) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // LDS -> HBM: bytes up to the first 4-aligned output address, dwords, then the tail bytes
+  const uint32_t head = (uint32_t)((4 - (gpos & 3)) & 3) < slen ? (uint32_t)((4 - (gpos & 3)) & 3) : slen;
+  const uint32_t ndw = (slen - head) / 4, tail = slen - head - 4 * ndw;
+  char *g = out + gpos;
+  if (lane < head) g[lane] = base[lane];
+  const uint32_t *ls = reinterpret_cast<const uint32_t *>(base + head);
+  uint32_t *gd = reinterpret_cast<uint32_t *>(g + head);
+  for (uint32_t i = lane; i < ndw; i += 64) gd[i] = ls[i];
+  if (lane < tail) g[head + 4 * ndw + lane] = base[head + 4 * ndw + lane];
 }
 
 // header and tail of the state object (one wave)
@@ -408,11 +419,8 @@ __global__ void k_enc_frame(Dev d, Names nm, uint32_t vi, const uint32_t *srv_of
   char *p = out + LLEN(L_HEAD) + (sb ? sb - 1 : 0);
   wcopy(p, L_TLC, LLEN(L_TLC), lane);
   p += LLEN(L_TLC);
-  char tb[32];
-  uint32_t tn = fmt_time(d.vlc[vi], tb);
-#pragma unroll
-  for (uint32_t i = 0; i < 32; i++)
-    if (i == lane && i < tn) p[i] = tb[i];
+  uint32_t tn = time_len(d.vlc[vi]);
+  if (lane == 0) fmt_time(d.vlc[vi], p);
   p += tn;
   wcopy(p, L_CN, LLEN(L_CN), lane);
   p += LLEN(L_CN);
@@ -445,7 +453,7 @@ struct Dec {
   LO16 *clo;         // [nc + 1] last open per level inside the chunk, then exclusive max prefix
   // per token (SoA)
   uint32_t *tpos, *tpar, *tmt, *taux;
-  uint8_t *tkind, *tlev, *tflag, *tck;
+  uint8_t *tkind, *tflag, *tck;
   // services and records
   uint32_t *sflag;   // [T + 1] 1 = winning Service object (then: exclusive prefix = list index)
   uint32_t *slist;   // [n_svc] service open tokens, document order
@@ -482,28 +490,64 @@ GXD int lex(int s, uint8_t c, bool &tok) {
   return ST_SCL;
 }
 
-__global__ __launch_bounds__(256) void k_dec_fsm(Dec x) {
-  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+// The byte-walking kernels stage their block's chunks in LDS first: 128 threads x 256 B, read
+// from HBM with coalesced dword loads; chunk t sits at dword t * 65 (padded: the 128 walkers read
+// 128 different banks). A walker reads a dword and steps through its 4 bytes.
+#define GXC_BT 128
+#define GXC_PAD 65
+GXD void stage_chunks(const Dec &x, uint32_t *sb) {
+  const uint32_t c0 = blockIdx.x * GXC_BT;
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(x.s) + (size_t)c0 * (GXC_CH / 4);
+  const uint32_t ndw = (uint32_t)min((size_t)GXC_BT * (GXC_CH / 4), ((size_t)x.n + 3) / 4 - (size_t)c0 * (GXC_CH / 4));
+  for (uint32_t i = threadIdx.x; i < ndw; i += GXC_BT) sb[(i >> 6) * GXC_PAD + (i & 63)] = src[i];
+  __syncthreads();
+}
+#define WALK_BEGIN(a, b)                                            \
+  for (uint32_t i0 = (a); i0 < (b); i0 += 4) {                      \
+    const uint32_t dw = sb[threadIdx.x * GXC_PAD + ((i0 - (a)) >> 2)]; \
+    for (uint32_t q = 0; q < 4 && i0 + q < (b); q++) {              \
+      const uint32_t i = i0 + q;                                    \
+      const uint8_t ch = (uint8_t)(dw >> (8 * q));
+#define WALK_END \
+  }              \
+  }
+
+// lexer transition table of one byte for the 4 states: byte 8*s = next state (bits 0-1), token
+// starts (bit 2), opens a container (bit 3), closes one (bit 4)
+GXD uint32_t lex_entry(uint32_t ch) {
+  uint32_t w = 0;
+  for (int s = 0; s < 4; s++) {
+    bool tok;
+    const bool was_out = s == ST_OUT || s == ST_SCL;
+    const uint32_t ns = (uint32_t)lex(s, (uint8_t)ch, tok);
+    const uint32_t op = was_out && (ch == '{' || ch == '['), cl = was_out && (ch == '}' || ch == ']');
+    w |= (ns | (uint32_t)tok << 2 | op << 3 | cl << 4) << (8 * s);
+  }
+  return w;
+}
+__global__ __launch_bounds__(GXC_BT) void k_dec_fsm(Dec x) {
+  __shared__ uint32_t sb[GXC_BT * GXC_PAD];
+  __shared__ uint32_t ltab[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += GXC_BT) ltab[i] = lex_entry(i);
+  stage_chunks(x, sb);
+  const uint32_t c = blockIdx.x * GXC_BT + threadIdx.x;
   if (c >= x.nc) return;
   const uint32_t a = c * GXC_CH, b = min(a + GXC_CH, x.n);
-  int st[4] = {0, 1, 2, 3};
+  uint32_t st[4] = {0, 1, 2, 3};
   uint32_t tk[4] = {0, 0, 0, 0};
   int32_t dp[4] = {0, 0, 0, 0}, mn[4] = {0, 0, 0, 0};
-  for (uint32_t i = a; i < b; i++) {
-    const uint8_t ch = x.s[i];
+  WALK_BEGIN(a, b)
+  const uint32_t W = ltab[ch];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const bool was_out = st[k] == ST_OUT || st[k] == ST_SCL;
-      bool tok;
-      st[k] = lex(st[k], ch, tok);
-      tk[k] += tok;
-      if (was_out && (ch == '{' || ch == '[')) dp[k]++;
-      if (was_out && (ch == '}' || ch == ']')) {
-        dp[k]--;
-        mn[k] = min(mn[k], dp[k]);
-      }
-    }
+  for (int k = 0; k < 4; k++) {
+    const uint32_t e = (W >> (8 * st[k])) & 0x1Fu;
+    st[k] = e & 3u;
+    tk[k] += (e >> 2) & 1u;
+    dp[k] += (int32_t)((e >> 3) & 1u) - (int32_t)((e >> 4) & 1u);
+    mn[k] = min(mn[k], dp[k]);
   }
+  (void)i;
+  WALK_END
   uint8_t m = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -522,8 +566,12 @@ __global__ __launch_bounds__(256) void k_dec_sel(Dec x) {
   x.ctd[c] = TD{x.ctok[s * x.nc + c], x.cdd[s * x.nc + c]};
 }
 // depth never below zero; per chunk, the last open bracket (global token index + 1) per level
-__global__ __launch_bounds__(256) void k_dec_levels(Dec x) {
-  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(GXC_BT) void k_dec_levels(Dec x) {
+  __shared__ uint32_t sb[GXC_BT * GXC_PAD];
+  __shared__ uint32_t ltab[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += GXC_BT) ltab[i] = lex_entry(i);
+  stage_chunks(x, sb);
+  const uint32_t c = blockIdx.x * GXC_BT + threadIdx.x;
   if (c >= x.nc) return;
   const int s0 = x.cmap[c] & 3;
   const TD td = x.ctd[c];
@@ -533,30 +581,32 @@ __global__ __launch_bounds__(256) void k_dec_levels(Dec x) {
   int s = s0;
   int32_t depth = td.depth;
   uint32_t ti = td.tok;
-  for (uint32_t i = a; i < b; i++) {
-    const uint8_t ch = x.s[i];
-    const bool was_out = s == ST_OUT || s == ST_SCL;
-    bool tok;
-    s = lex(s, ch, tok);
-    if (was_out && (ch == '{' || ch == '[')) {
-      if (depth >= GXC_MAXD) dec_err(x, i);
-      else {
+  WALK_BEGIN(a, b)
+  const uint32_t e = (ltab[ch] >> (8 * s)) & 0x1Fu;
+  s = (int)(e & 3u);
+  if (e & 8u) {
+    if (depth >= GXC_MAXD) dec_err(x, i);
+    else {
 #pragma unroll
-        for (int L = 0; L < GXC_MAXD; L++)
-          if (L == depth) lo.v[L] = ti + 1;
-      }
-      depth++;
+      for (int L = 0; L < GXC_MAXD; L++)
+        if (L == depth) lo.v[L] = ti + 1;
     }
-    if (was_out && (ch == '}' || ch == ']')) depth--;
-    ti += tok;
+    depth++;
   }
+  if (e & 16u) depth--;
+  ti += (e >> 2) & 1u;
+  WALK_END
   x.clo[c] = lo;
 }
 // tokens (SoA): position, kind, level, parent container, bracket match
-__global__ __launch_bounds__(256) void k_dec_emit(Dec x) {
-  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(GXC_BT) void k_dec_emit(Dec x) {
+  __shared__ uint32_t sb[GXC_BT * GXC_PAD];
+  __shared__ uint32_t sl[GXC_BT][GXC_MAXD + 1];
+  __shared__ uint32_t ltab[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += GXC_BT) ltab[i] = lex_entry(i);
+  stage_chunks(x, sb);
+  const uint32_t c = blockIdx.x * GXC_BT + threadIdx.x;
   if (c >= x.nc) return;
-  __shared__ uint32_t sl[256][GXC_MAXD + 1];
   uint32_t *lo = sl[threadIdx.x];
   const LO16 pre = x.clo[c];
   for (int L = 0; L < GXC_MAXD; L++) lo[L] = pre.v[L];
@@ -564,42 +614,37 @@ __global__ __launch_bounds__(256) void k_dec_emit(Dec x) {
   int s = x.cmap[c] & 3;
   int32_t depth = x.ctd[c].depth;
   uint32_t ti = x.ctd[c].tok;
-  for (uint32_t i = a; i < b; i++) {
-    const uint8_t ch = x.s[i];
-    bool tok;
-    const bool was_out = s == ST_OUT || s == ST_SCL;
-    s = lex(s, ch, tok);
-    if (!tok) continue;
-    if (ti >= x.T) break;  // cannot happen for a consistent scan; keeps writes in bounds
-    uint8_t kind = ch == '"' ? T_STR : (is_struct(ch) ? ch : T_SCL);
-    uint32_t par = GXC_NONE, mt = GXC_NONE;
-    int32_t lev = depth;
-    (void)was_out;
-    if (kind == T_OBJ || kind == T_ARR) {
-      if (depth > 0 && depth <= GXC_MAXD) par = lo[depth - 1] - 1;
-      if (depth < GXC_MAXD) lo[depth] = ti + 1;
-      depth++;
-    } else if (kind == T_OBJE || kind == T_ARRE) {
-      depth--;
-      lev = depth;
-      if (depth >= 0 && depth < GXC_MAXD) {
-        mt = lo[depth] - 1;
-        if (depth > 0) par = lo[depth - 1] - 1;
-        if (mt != GXC_NONE) x.tmt[mt] = ti;
-      }
-      x.tmt[ti] = mt;
-    } else if (depth > 0 && depth <= GXC_MAXD) {
-      par = lo[depth - 1] - 1;
-    }
-    x.tpos[ti] = i;
-    x.tkind[ti] = kind;
-    x.tlev[ti] = (uint8_t)(lev < 0 ? 255 : (lev > 255 ? 255 : lev));
-    x.tpar[ti] = par;
-    x.tflag[ti] = 0;
-    x.tck[ti] = K_ANY;
-    x.taux[ti] = 0;
-    ti++;
+  bool stop = false;
+  WALK_BEGIN(a, b)
+  const uint32_t e = (ltab[ch] >> (8 * s)) & 0x1Fu;
+  s = (int)(e & 3u);
+  if (!(e & 4u) || stop) continue;
+  if (ti >= x.T) {  // cannot happen for a consistent scan; keeps writes in bounds
+    stop = true;
+    continue;
   }
+  uint8_t kind = ch == '"' ? T_STR : (is_struct(ch) ? ch : T_SCL);
+  uint32_t par = GXC_NONE, mt = GXC_NONE;
+  if (kind == T_OBJ || kind == T_ARR) {
+    if (depth > 0 && depth <= GXC_MAXD) par = lo[depth - 1] - 1;
+    if (depth < GXC_MAXD) lo[depth] = ti + 1;
+    depth++;
+  } else if (kind == T_OBJE || kind == T_ARRE) {
+    depth--;
+    if (depth >= 0 && depth < GXC_MAXD) {
+      mt = lo[depth] - 1;
+      if (depth > 0) par = lo[depth - 1] - 1;
+      if (mt != GXC_NONE) x.tmt[mt] = ti;
+    }
+    x.tmt[ti] = mt;
+  } else if (depth > 0 && depth <= GXC_MAXD) {
+    par = lo[depth - 1] - 1;
+  }
+  x.tpos[ti] = i;  // tflag, tck, taux are preset by the host (memset)
+  x.tkind[ti] = kind;
+  x.tpar[ti] = par;
+  ti++;
+  WALK_END
 }
 
 GXD int hexv(uint8_t c) {
@@ -875,10 +920,93 @@ GXD bool unq_equal_raw(const Dec &x, uint32_t tok, const char *raw, uint32_t rn)
   }
 }
 
+// Keys of at most 11 raw bytes without escapes (every field name) are packed, ASCII-uppercased,
+// into two words and compared against packed constants; escaped keys take the unquoting path.
+struct KP {
+  uint64_t a, b;
+  uint32_t len;  // 0xFE = escaped (slow path), 0xFD = longer than any field name
+};
+GXD KP key_pack(const Dec &x, uint32_t tok) {
+  const uint32_t p = x.tpos[tok] + 1;
+  KP k{0, 0, 0};
+  for (uint32_t i = 0; i < 12; i++) {
+    if (p + i >= x.n) {
+      k.len = 0xFD;
+      return k;
+    }
+    uint32_t c = x.s[p + i];
+    if (c == '"') {
+      k.len = i;
+      return k;
+    }
+    if (c == '\\') {
+      k.len = 0xFE;
+      return k;
+    }
+    if (c >= 'a' && c <= 'z') c -= 32;
+    if (i < 8) k.a |= (uint64_t)c << (8 * i);
+    else k.b |= (uint64_t)c << (8 * (i - 8));
+  }
+  k.len = 0xFD;
+  return k;
+}
+GXHD constexpr uint32_t cx_len(const char *s) {
+  uint32_t n = 0;
+  while (s[n]) n++;
+  return n;
+}
+GXHD constexpr uint64_t cx_pack(const char *s, uint32_t from) {
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < 8 && s[from + i]; i++) {
+    uint32_t c = (uint8_t)s[from + i];
+    if (c >= 'a' && c <= 'z') c -= 32;
+    v |= (uint64_t)c << (8 * i);
+  }
+  return v;
+}
+#define KEQ(k, name) ((k).len == cx_len(name) && (k).a == cx_pack(name, 0) && (k).b == (cx_len(name) > 8 ? cx_pack(name, 8) : 0ull))
+
 // fields (field ids per container kind)
 enum { F_NONE, F_SERVERS, F_LASTCHANGED, F_CLUSTERNAME, F_HOSTNAME, F_NAME, F_SERVICES, F_LASTUPDATED, F_ID,
        F_IMAGE, F_PROXYMODE, F_CREATED, F_UPDATED, F_PORTS, F_STATUS, F_TYPE, F_IP, F_PORT, F_SERVICEPORT };
+GXD int field_of_slow(const Dec &x, uint32_t key, int ck);
 GXD int field_of(const Dec &x, uint32_t key, int ck) {
+  const KP k = key_pack(x, key);
+  if (k.len == 0xFE) return field_of_slow(x, key, ck);
+  switch (ck) {
+    case K_TOP:
+      if (KEQ(k, "Servers")) return F_SERVERS;
+      if (KEQ(k, "LastChanged")) return F_LASTCHANGED;
+      if (KEQ(k, "ClusterName")) return F_CLUSTERNAME;
+      if (KEQ(k, "Hostname")) return F_HOSTNAME;
+      return F_NONE;
+    case K_SERVER:
+      if (KEQ(k, "Name")) return F_NAME;
+      if (KEQ(k, "Services")) return F_SERVICES;
+      if (KEQ(k, "LastUpdated")) return F_LASTUPDATED;
+      if (KEQ(k, "LastChanged")) return F_LASTCHANGED;
+      return F_NONE;
+    case K_SERVICE:
+      if (KEQ(k, "ID")) return F_ID;
+      if (KEQ(k, "Name")) return F_NAME;
+      if (KEQ(k, "Image")) return F_IMAGE;
+      if (KEQ(k, "Created")) return F_CREATED;
+      if (KEQ(k, "Hostname")) return F_HOSTNAME;
+      if (KEQ(k, "Ports")) return F_PORTS;
+      if (KEQ(k, "Updated")) return F_UPDATED;
+      if (KEQ(k, "ProxyMode")) return F_PROXYMODE;
+      if (KEQ(k, "Status")) return F_STATUS;
+      return F_NONE;
+    case K_PORT:
+      if (KEQ(k, "Type")) return F_TYPE;
+      if (KEQ(k, "Port")) return F_PORT;
+      if (KEQ(k, "ServicePort")) return F_SERVICEPORT;
+      if (KEQ(k, "IP")) return F_IP;
+      return F_NONE;
+  }
+  return F_NONE;
+}
+GXD int field_of_slow(const Dec &x, uint32_t key, int ck) {
   switch (ck) {
     case K_TOP:
       if (key_is(x, key, "Servers")) return F_SERVERS;

@@ -39,7 +39,41 @@ struct Bump {
   }
 };
 
+// Device -> pageable host copy through two pinned staging chunks: the DMA of chunk i+1 overlaps
+// the host memcpy of chunk i (a plain pageable hipMemcpy runs at a few GB/s).
+#define PIN_CHUNK (8u << 20)
+struct Pinned {
+  char *p[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
+static int d2h_staged(gx_engine *e, Pinned &pn, char *dst, const char *src, size_t n) {
+  for (int i = 0; i < 2; i++) {
+    if (!pn.p[i]) {
+      HIPCHK(hipHostMalloc((void **)&pn.p[i], PIN_CHUNK, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&pn.ev[i], hipEventDisableTiming));
+    }
+  }
+  const size_t nch = (n + PIN_CHUNK - 1) / PIN_CHUNK;
+  for (size_t c = 0; c < nch && c < 2; c++) {
+    const size_t len = std::min<size_t>(PIN_CHUNK, n - c * PIN_CHUNK);
+    HIPCHK(hipMemcpyAsync(pn.p[c & 1], src + c * PIN_CHUNK, len, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipEventRecord(pn.ev[c & 1], e->stream));
+  }
+  for (size_t c = 0; c < nch; c++) {
+    const size_t len = std::min<size_t>(PIN_CHUNK, n - c * PIN_CHUNK);
+    HIPCHK(hipEventSynchronize(pn.ev[c & 1]));
+    memcpy(dst + c * PIN_CHUNK, pn.p[c & 1], len);
+    if (c + 2 < nch) {
+      const size_t l2 = std::min<size_t>(PIN_CHUNK, n - (c + 2) * PIN_CHUNK);
+      HIPCHK(hipMemcpyAsync(pn.p[c & 1], src + (c + 2) * PIN_CHUNK, l2, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipEventRecord(pn.ev[c & 1], e->stream));
+    }
+  }
+  return GX_OK;
+}
+
 struct CodecState {
+  Pinned pin2;                   // staging for LocalState copies to the caller
   gxc::Names nm;                 // device pointers
   std::vector<void *> owned;     // device allocations of the names tables
   std::vector<uint32_t> ehost_len;
@@ -47,7 +81,6 @@ struct CodecState {
   DevBuf out;                    // encoder output
   DevBuf enc;                    // encoder server lengths / offsets + scan scratch
   DevBuf in, ph1, ph2, ph3;      // decoder input and phase buffers
-  DevBuf pin;                    // pinned host staging (not used for small inputs)
 };
 
 static void codec_free(gx_engine *e) {
@@ -57,6 +90,10 @@ static void codec_free(gx_engine *e) {
   if (c->seen) (void)hipFree(c->seen);
   for (DevBuf *b : {&c->out, &c->enc, &c->in, &c->ph1, &c->ph2, &c->ph3})
     if (b->p) (void)hipFree(b->p);
+  for (int i = 0; i < 2; i++) {
+    if (c->pin2.p[i]) (void)hipHostFree(c->pin2.p[i]);
+    if (c->pin2.ev[i]) (void)hipEventDestroy(c->pin2.ev[i]);
+  }
   delete c;
   e->codec = nullptr;
 }
@@ -185,7 +222,8 @@ static int enc_impl(gx_engine *e, uint32_t view, char *out, uint64_t cap, uint64
     gxc::k_enc_frame<<<1, 64, 0, e->stream>>>(d, c->nm, vi, off, (char *)dout);
     gxc::k_enc_write<<<nblk(d.H, 4), 256, 0, e->stream>>>(d, c->nm, vi, len, off, (char *)dout);
   }
-  HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, e->stream));
+  rc = d2h_staged(e, c->pin2, out, (const char *)dout, total);
+  if (rc) return rc;
   rc = sync_check(e);
   if (rc) return rc;
   // algorithmic bytes: the view row and server times read, every output byte written and (but
@@ -244,7 +282,7 @@ static int dec_impl(gx_engine *e, const char *buf, uint64_t len, gx_decode_stats
   HIPCHK(hipMemsetAsync(x.err, 0xFF, sizeof(unsigned long long), e->stream));
   HIPCHK(hipMemsetAsync(x.win_top, 0, sizeof(uint32_t), e->stream));
   HIPCHK(hipMemsetAsync(x.cnt, 0, sizeof(uint32_t) * 4, e->stream));
-  gxc::k_dec_fsm<<<nblk(nc, 256), 256, 0, e->stream>>>(x);
+  gxc::k_dec_fsm<<<nblk(nc, GXC_BT), GXC_BT, 0, e->stream>>>(x);
   HIPCHK(hipMemcpyAsync(x.cmap + nc, &idmap, 1, hipMemcpyHostToDevice, e->stream));
   rc = mscan<gxc::MMap, 16>(e, x.cmap, nc + 1, B1, soff);
   if (rc) return rc;
@@ -252,7 +290,7 @@ static int dec_impl(gx_engine *e, const char *buf, uint64_t len, gx_decode_stats
   HIPCHK(hipMemcpyAsync(x.ctd + nc, &td0, sizeof(td0), hipMemcpyHostToDevice, e->stream));
   rc = mscan<gxc::MTD, 8>(e, x.ctd, nc + 1, B1, soff);
   if (rc) return rc;
-  gxc::k_dec_levels<<<nblk(nc, 256), 256, 0, e->stream>>>(x);
+  gxc::k_dec_levels<<<nblk(nc, GXC_BT), GXC_BT, 0, e->stream>>>(x);
   HIPCHK(hipMemcpyAsync(x.clo + nc, &lo0, sizeof(lo0), hipMemcpyHostToDevice, e->stream));
   rc = mscan<gxc::MLO, 1>(e, x.clo, nc + 1, B1, soff);
   if (rc) return rc;
@@ -277,7 +315,7 @@ static int dec_impl(gx_engine *e, const char *buf, uint64_t len, gx_decode_stats
   while (dsz < T / 2) dsz <<= 1;
   x.dmask = dsz - 1;
   const size_t sc2 = mscan_scratch<gxc::MAdd32, 16>(T + 1);
-  const size_t b2 = 12 * 256 + (size_t)(T + 1) * (5 * 4 + 4) + (size_t)dsz * 4 + sc2;
+  const size_t b2 = 12 * 256 + (size_t)(T + 1) * (5 * 4 + 3) + (size_t)dsz * 4 + sc2;
   void *p2;
   rc = dbuf(c->ph2, b2, &p2);
   if (rc) return rc;
@@ -289,14 +327,16 @@ static int dec_impl(gx_engine *e, const char *buf, uint64_t len, gx_decode_stats
   x.taux = bq.take<uint32_t>(B2, T + 1);
   x.sflag = bq.take<uint32_t>(B2, T + 1);
   x.tkind = bq.take<uint8_t>(B2, T + 1);
-  x.tlev = bq.take<uint8_t>(B2, T + 1);
   x.tflag = bq.take<uint8_t>(B2, T + 1);
   x.tck = bq.take<uint8_t>(B2, T + 1);
   x.dset = bq.take<uint32_t>(B2, dsz);
   size_t soff2 = bq.off;
   HIPCHK(hipMemsetAsync(x.tmt, 0xFF, sizeof(uint32_t) * (T + 1), e->stream));
+  HIPCHK(hipMemsetAsync(x.taux, 0, sizeof(uint32_t) * (T + 1), e->stream));
+  HIPCHK(hipMemsetAsync(x.tflag, 0, T + 1, e->stream));
+  HIPCHK(hipMemsetAsync(x.tck, gxc::K_ANY, T + 1, e->stream));
   HIPCHK(hipMemsetAsync(x.dset, 0, sizeof(uint32_t) * dsz, e->stream));
-  gxc::k_dec_emit<<<nblk(nc, 256), 256, 0, e->stream>>>(x);
+  gxc::k_dec_emit<<<nblk(nc, GXC_BT), GXC_BT, 0, e->stream>>>(x);
   gxc::k_dec_check<<<nblk(T, 256), 256, 0, e->stream>>>(x);
   gxc::k_dec_kind<<<nblk(T, 256), 256, 0, e->stream>>>(x);
   gxc::k_dec_member<<<nblk(T, 256), 256, 0, e->stream>>>(x);

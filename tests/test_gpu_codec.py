@@ -105,3 +105,39 @@ def test_gpu_codec_1024x16(oracle_lib, gx_lib):
     doc = o.local_state_json(900)
     assert g.merge_remote_state_json(5, doc)[0] == o.merge_remote_state_json(5, doc)[0] == 0
     assert_same(g, o, "1024x16 merge")
+
+
+def test_gpu_decode_fuzz_equals_oracle(oracle_lib, gx_lib):
+    """Seeded byte mutations (flip, insert, delete, duplicate a span) of valid states: the GPU parser
+    accepts exactly what the oracle accepts and decodes the same records."""
+    import random
+    kw = SCEN["h12_s4_own"]
+    g, o = pair(oracle_lib, gx_lib, kw, 19)
+    rng = random.Random(2024)
+    alphabet = b'{}[]:,"\\ u0123456789abcdefnulltrue-.eE+Z\n\t'
+    base = [o.local_state_json(v) for v in range(kw["n_hosts"])]
+    n_ok = 0
+    for i in range(300):
+        doc = bytearray(rng.choice(base))
+        for _ in range(rng.randint(1, 3)):
+            p = rng.randrange(len(doc))
+            m = rng.randrange(4)
+            if m == 0:
+                doc[p] = rng.choice(alphabet)
+            elif m == 1:
+                doc.insert(p, rng.choice(alphabet))
+            elif m == 2:
+                del doc[p]
+            else:
+                q = min(len(doc), p + rng.randint(1, 40))
+                doc[p:p] = doc[p:q]
+        rg, recg, dsg = g.decode_state_json(bytes(doc))
+        ro, reco, dso = o.decode_state_json(bytes(doc))
+        assert rg == ro, (i, bytes(doc), dsg, dso)
+        if ro == 0:
+            n_ok += 1
+            assert recg == reco, i
+            dsg.pop("error_at")
+            dso.pop("error_at")
+            assert dsg == dso, i
+    assert 0 < n_ok < 300
