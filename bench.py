@@ -52,7 +52,7 @@ CONFIGS = {
                                                                 queue_cap=4096, init_mode=0)),
 }
 
-KNAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode"]
+KNAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode", "fd"]
 
 
 def make_engine(lib, cfg, seed, device):

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 1
+#define GX_ABI_VERSION 2
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -142,6 +142,25 @@ typedef struct gx_params {
    * UDPBufferSize 1400 - 2 = 1398 and overhead = 2 + 1 = 3. */
   uint32_t limit_bytes;
   uint32_t overhead_bytes;
+  /* memberlist failure detection (see "memberlist" below).
+   * fd_enable = 0 keeps the scripted model: partitions restrict peer sampling to a side and
+   * storm_round scripts NotifyLeave. fd_enable = 1 runs memberlist's SWIM detector on every host:
+   * partitions and departures drop packets, and NotifyLeave -> ExpireServer follows the
+   * detector's dead declarations. Defaults are DefaultLANConfig (main.go:243); the fields
+   * memberlist derives from the cluster size are filled by gx_fd_defaults(). */
+  uint32_t fd_enable;
+  uint32_t fd_probe_rounds;        /* ProbeInterval 1 s = 5 rounds */
+  uint32_t fd_indirect_checks;     /* IndirectChecks 3 */
+  uint32_t fd_retransmit_limit;    /* RetransmitMult 4 * ceil(log10(n + 1)), 1..GX_FD_MAX_TX */
+  uint32_t fd_msg_cap;             /* memberlist messages per gossip packet, 1..64 */
+  uint32_t fd_msg_bytes;           /* byte mode: encoded length of one memberlist message */
+  uint32_t fd_gossip_dead_rounds;  /* GossipToTheDeadTime 30 s = 150 rounds */
+  uint32_t fd_suspicion_k;         /* SuspicionMult - 2 confirmations (0 when n - 2 < k), <= 7 */
+  uint32_t fd_suspicion_rounds[8]; /* suspicion timeout after c confirmations, c = 0..k */
+  /* Host departures (crash): from depart_round on, a seeded depart_ppm fraction of the hosts
+   * stops every activity and drops every packet sent to it (both models). -1 = none. */
+  int32_t depart_round;
+  uint32_t depart_ppm;
 } gx_params;
 
 /* Per-host bookkeeping (read-back for parity). */
@@ -189,6 +208,16 @@ typedef struct gx_stats {
   uint64_t cap_cuts;         /* byte-limit mode: packets cut by packet_cap before the byte limit */
   uint64_t change_events;    /* ServiceChanged calls (services_state.go:195-199), all views */
   uint64_t listener_drops;   /* ChangeEvents a full listener channel did not take (:230-236) */
+  uint64_t lost_packets;     /* packets sent to a departed or partitioned-off peer (records lost) */
+  uint64_t fd_probes;        /* probeNode calls */
+  uint64_t fd_probe_failures;/* probes without a direct or indirect ack -> suspectNode */
+  uint64_t fd_suspicions;    /* suspicion timers started (alive -> suspect) */
+  uint64_t fd_confirmations; /* independent suspicion confirmations (Lifeguard) */
+  uint64_t fd_deaths;        /* deadNode accepted: NotifyLeave calls */
+  uint64_t fd_refutes;       /* refute(): a host raised its own incarnation */
+  uint64_t fd_alive_updates; /* aliveNode accepted about another host */
+  uint64_t fd_msgs_sent;     /* memberlist broadcasts put into gossip packets */
+  uint64_t fd_msgs_received; /* memberlist broadcasts handled by receivers */
   uint64_t reserved[1];
 } gx_stats;
 
@@ -203,7 +232,8 @@ typedef struct gx_stats {
 #define GX_K_CONVERGE 7
 #define GX_K_ENCODE 8 /* LocalState JSON encoder (gx_local_state_json) */
 #define GX_K_DECODE 9 /* Decode JSON parser (gx_decode_state_json, gx_merge_remote_state_json) */
-#define GX_K_COUNT 10
+#define GX_K_FD 10    /* memberlist failure detection: timers + probes, messages in and out */
+#define GX_K_COUNT 11
 typedef struct gx_timing {
   double ms[GX_K_COUNT];
   uint64_t launches[GX_K_COUNT];
@@ -436,6 +466,81 @@ int gx_decode_state_json(gx_engine *e, const char *buf, uint64_t len, gx_service
 /* MergeRemoteState(buf): Decode + Merge into `view`. */
 int gx_merge_remote_state_json(gx_engine *e, uint32_t view, const char *buf, uint64_t len,
                                gx_decode_stats *ds);
+
+/* ---- memberlist failure detection -------------------------------------------
+ * memberlist is a dependency absent from the reference tree: github.com/NinesStack/memberlist
+ * v0.0.0-20170522194404-cfac2b5cf519 (go.mod:6), a fork of hashicorp/memberlist. Sidecar uses
+ * DefaultLANConfig (main.go:243-261) and reacts only to NotifyLeave -> go ExpireServer(node)
+ * (services_delegate.go:173-176); NotifyJoin/NotifyUpdate only log (:169-171, :178-180). The
+ * engine restates memberlist's published SWIM + Lifeguard algorithm (state.go probe/probeNode,
+ * aliveNode/suspectNode/deadNode/refute, suspicion.go, queue.go TransmitLimitedQueue,
+ * util.go kRandomNodes/retransmitLimit/suspicionTimeout) per simulated host; the resolutions
+ * the round model makes are listed in DESIGN.md §3b. Parity against the fork is unpinned (no
+ * reference test exercises it); the oracle and the GPU engine agree bit for bit.
+ *
+ * Each host keeps a member list over all H hosts (gx_member per (host, node)) and a broadcast
+ * queue of memberlist messages: at most one queued message per node (a newer one invalidates
+ * it), sent fewest-transmits first and newest first among equal counts, each sent
+ * fd_retransmit_limit times. Host ids are 16-bit here: fd_enable requires n_hosts <= 65534 and
+ * an unsharded engine. */
+#define GX_M_ALIVE 0
+#define GX_M_SUSPECT 1
+#define GX_M_DEAD 2
+#define GX_FD_NONE 0xffffu
+#define GX_FD_MAX_TX 32
+#define GX_FD_NO_DEADLINE 0x7fffffff
+typedef struct gx_member {    /* memberlist nodeState of `node` in one host's list */
+  uint32_t incarnation;
+  uint32_t msg_incarnation;   /* the queued message about the node (when tx > 0) */
+  int32_t change_round;       /* StateChange (suspicion start for SUSPECT) */
+  int32_t deadline;           /* suspicion timer: fires at the first round >= deadline */
+  uint8_t state;              /* GX_M_* */
+  uint8_t n_conf;             /* independent confirmations of the suspicion */
+  uint8_t tx;                 /* queued message: transmits + 1; 0 = none queued */
+  uint8_t msg_kind;           /* GX_M_* kind of the queued message (alive / suspect / dead) */
+  uint16_t msg_from;          /* From of the queued suspect / dead message */
+  uint16_t susp_from[3];      /* suspicion: the accuser, then the confirmers (n_conf of them) */
+  uint16_t q_prev, q_next;    /* queue links, GX_FD_NONE = end */
+} gx_member;
+typedef struct gx_fd_host {
+  uint32_t probe_pass;        /* probe-list shuffles so far (resetNodes) */
+  uint32_t probe_index;       /* probeIndex into the pass's permutation */
+  int32_t wrap_round;         /* round of the last resetNodes; dead nodes older than
+                                 GossipToTheDeadTime at that round are reaped */
+  int32_t min_deadline;       /* earliest suspicion deadline of the host (exact lower bound) */
+  uint32_t q_len;             /* queued memberlist messages */
+  uint32_t departed;          /* 1 from depart_round on if this host crashed */
+  uint16_t q_head[GX_FD_MAX_TX]; /* per transmit count: the newest queued node */
+} gx_fd_host;
+typedef struct gx_fd_msg {    /* alive / suspect / dead message (memberlist net.go) */
+  uint32_t incarnation;
+  uint16_t node;
+  uint16_t from;              /* suspect / dead: the accuser; alive: the node itself */
+  uint8_t kind;               /* GX_M_* */
+  uint8_t pad[3];
+} gx_fd_msg;
+/* Derived memberlist parameters for n = p->n_hosts (util.go, suspicion.go):
+ *   fd_retransmit_limit = RetransmitMult(4) * ceil(log10(n + 1))
+ *   min = SuspicionMult(4) * max(1, log10(max(1, n))) * ProbeInterval (ms precision),
+ *   max = SuspicionMaxTimeoutMult(6) * min; k = SuspicionMult - 2, 0 if n - 2 < k
+ *   timeout(c) = max(min, max - (max - min) * log(c + 1) / log(k + 1)), floored to ms
+ *   (c = 0: max, or min when k < 1), stored in rounds rounded up. */
+int gx_fd_defaults(gx_params *p);
+int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t node_lo, uint32_t node_hi, gx_member *out);
+int gx_fd_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_fd_host *out);
+/* The host's queued memberlist messages in send order, with their transmit counts. */
+int gx_fd_read_queue(gx_engine *e, uint32_t host, gx_fd_msg *out, uint8_t *transmits, uint32_t cap,
+                     uint32_t *n_out);
+/* memberlist packet handlers on one host, in order: aliveNode / suspectNode / deadNode
+ * (state.go); a dead declaration calls NotifyLeave -> ExpireServer on the host's catalog view. */
+int gx_fd_notify(gx_engine *e, uint32_t host, const gx_fd_msg *msgs, uint32_t n);
+/* TransmitLimitedQueue.GetBroadcasts of one host with a budget of `limit` messages. */
+int gx_fd_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_fd_msg *out, uint32_t *n_out);
+/* One probe() of the host at the current round: target selection over the shuffled list, direct
+ * and IndirectChecks probes, suspectNode on failure. target = GX_FD_NONE if nothing to probe. */
+int gx_fd_probe(gx_engine *e, uint32_t host, uint32_t *target, int *acked);
+/* Suspicion timers of the host due at the current round -> deadNode, in node order. */
+int gx_fd_timers(gx_engine *e, uint32_t host);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */
 int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stddef.h>
+#include <math.h>
 
 typedef struct grec {
   uint64_t w; /* packed (ts << 3) | status */
@@ -68,6 +69,13 @@ struct gx_engine {
   } lst[GX_MAX_LISTENERS];
   int64_t ae_local_round; /* round whose shard-local push-pull pairs gx_ae_merge_local merged */
   struct onames *names;   /* full-state JSON codec names (gx_oracle_json.c), NULL until set */
+  /* memberlist failure detection (gx_oracle_fd.c), allocated when fd_enable */
+  gx_member *mem;         /* H * H  member list of every host */
+  gx_fd_host *fdh;        /* H */
+  gx_fd_msg *fdm;         /* H * K * fd_msg_cap  memberlist messages of this round's packets */
+  uint32_t *fd_len;       /* H * K */
+  uint32_t *fd_peers;     /* H * K  gossip targets (memberlist's choice) */
+  uint32_t *fd_np;        /* H */
   gx_stats st;
 };
 static void free_names(gx_engine *e);
@@ -685,16 +693,20 @@ static uint32_t shard_of(const gx_engine *e, uint32_t v) {
 }
 static int is_local(const gx_engine *e, uint32_t v) { return v >= e->lo && v < e->hi; }
 
+/* memberlist failure detection, host departures */
+#include "gx_oracle_fd.c"
+
 /* Phases 0-3 of the current round for this engine's hosts. Each phase is a loop over hosts
  * (for_hosts); a host's iteration touches only that host's state. */
 static void ph_wake(gx_engine *e, uint32_t i, void *ctx) {
   (void)ctx;
-  wake_host(e, e->lo + i);
+  if (!departed(e, e->lo + i)) wake_host(e, e->lo + i);
 }
 /* owners: discovery churn, BroadcastServices(+TrackNewServices), BroadcastTombstones */
 static void ph_owner(gx_engine *e, uint32_t i, void *ctx) {
   int64_t now = *(const int64_t *)ctx;
   uint32_t o = e->lo + i;
+  if (departed(e, o)) return; /* a crashed host runs no loopers */
   churn(e, o);
   gx_host_state *h = &e->hs[o];
   if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
@@ -704,21 +716,43 @@ static void ph_owner(gx_engine *e, uint32_t i, void *ctx) {
 static void ph_storm(gx_engine *e, uint32_t i, void *ctx) {
   int64_t now = *(const int64_t *)ctx;
   uint32_t v = e->lo + i, half = e->H / 2;
+  if (departed(e, v)) return;
   uint32_t lo = v < half ? half : 0, hi = v < half ? e->H : half;
   for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
 }
 /* gossip send: GetBroadcasts once per selected peer */
+/* With the failure detector, the targets are memberlist's (ph_fd_send took their memberlist
+ * messages first; getBroadcasts gives the delegate the bytes left, and stops the round when a
+ * packet would be empty). A packet to an unreachable peer is lost after GetBroadcasts took its
+ * records. */
 static void ph_send(gx_engine *e, uint32_t i, void *ctx) {
   (void)ctx;
   uint32_t u = e->lo + i, K = e->K, cap = e->p.packet_cap;
+  if (departed(e, u)) return;
   uint32_t peers[64];
-  uint32_t np = sample_peers(e, u, peers);
+  const int fd = e->p.fd_enable != 0;
+  uint32_t np = fd ? e->fd_np[u] : sample_peers(e, u, peers);
   for (uint32_t j = 0; j < np; j++) {
-    uint32_t l = get_broadcasts(e, u, cap, &e->msg[((size_t)u * K + j) * cap], e->p.limit_bytes,
-                                e->p.overhead_bytes);
-    e->msg_len[(size_t)u * K + j] = l;
-    e->msg_dst[(size_t)u * K + j] = peers[j];
-    if (l == 0 && e->p.gossip_stop_on_empty) break;
+    size_t x = (size_t)u * K + j;
+    uint32_t peer = fd ? e->fd_peers[x] : peers[j], nf = fd ? e->fd_len[x] : 0, l;
+    if (fd && e->p.limit_bytes) {
+      uint32_t used = nf * (e->p.fd_msg_bytes + 2);
+      uint32_t avail = e->p.limit_bytes > used ? e->p.limit_bytes - used : 0;
+      l = avail > e->p.overhead_bytes
+              ? get_broadcasts(e, u, cap, &e->msg[x * cap], avail, e->p.overhead_bytes)
+              : 0;
+    } else {
+      l = get_broadcasts(e, u, cap, &e->msg[x * cap], e->p.limit_bytes, e->p.overhead_bytes);
+    }
+    e->msg_len[x] = l;
+    e->msg_dst[x] = peer;
+    int stop = l == 0 && nf == 0 && e->p.gossip_stop_on_empty;
+    if ((l || nf) && !reach(e, u, peer)) {
+      e->st.lost_packets++;
+      e->msg_len[x] = 0;
+      if (fd) e->fd_len[x] = 0;
+    }
+    if (stop) break;
   }
 }
 static void round_send(gx_engine *e) {
@@ -727,8 +761,14 @@ static void round_send(gx_engine *e) {
   for_hosts(e, n, ph_wake, NULL);
   for_hosts(e, n, ph_owner, &now);
   if (e->p.storm_round >= 0 && e->round == e->p.storm_round) for_hosts(e, n, ph_storm, &now);
+  if (e->p.fd_enable) for_hosts(e, n, ph_fd_tick, &now);
   for (size_t i = 0; i < (size_t)e->H * e->K; i++) e->msg_len[i] = 0;
+  if (e->p.fd_enable) for_hosts(e, n, ph_fd_send, NULL);
   for_hosts(e, n, ph_send, NULL);
+}
+
+static int pkt_live(const gx_engine *e, size_t m) {
+  return e->msg_len[m] || (e->p.fd_enable && e->fd_len[m]);
 }
 
 /* Phase 4: packets to this engine's receivers in sender order -> NotifyMsg -> AddServiceEntry.
@@ -746,14 +786,15 @@ static void round_merge(gx_engine *e) {
   uint32_t H = e->H, K = e->K;
   memset(e->in_cnt, 0, sizeof(uint32_t) * (H + 1));
   for (size_t m = 0; m < (size_t)H * K; m++)
-    if (e->msg_len[m] && is_local(e, e->msg_dst[m])) e->in_cnt[e->msg_dst[m] + 1]++;
+    if (pkt_live(e, m) && is_local(e, e->msg_dst[m])) e->in_cnt[e->msg_dst[m] + 1]++;
   for (uint32_t v = 0; v < H; v++) e->in_cnt[v + 1] += e->in_cnt[v];
   uint32_t *cur = (uint32_t *)malloc(sizeof(uint32_t) * H);
   memcpy(cur, e->in_cnt, sizeof(uint32_t) * H);
   for (size_t m = 0; m < (size_t)H * K; m++)
-    if (e->msg_len[m] && is_local(e, e->msg_dst[m])) e->in_list[cur[e->msg_dst[m]]++] = (uint32_t)m;
+    if (pkt_live(e, m) && is_local(e, e->msg_dst[m])) e->in_list[cur[e->msg_dst[m]]++] = (uint32_t)m;
   free(cur);
   for_hosts(e, e->hi - e->lo, ph_receive, &now);
+  if (e->p.fd_enable) for_hosts(e, e->hi - e->lo, ph_fd_receive, &now);
 }
 
 static int ae_round(const gx_engine *e) {
@@ -764,7 +805,7 @@ static int ae_round(const gx_engine *e) {
 static uint32_t ae_pairs(const gx_engine *e, uint32_t *pa, uint32_t *pb) {
   uint32_t groups[2][2];
   int ng;
-  if (partitioned(e)) {
+  if (partitioned(e) && !e->p.fd_enable) {
     groups[0][0] = 0; groups[0][1] = e->H / 2;
     groups[1][0] = e->H / 2; groups[1][1] = e->H - e->H / 2;
     ng = 2;
@@ -800,9 +841,18 @@ struct ae_ctx {
   const uint32_t *pa, *pb;
   int64_t now;
 };
+/* A push-pull pair runs unless a member crashed; with the failure detector it also needs the
+ * network path and the initiator (the pair's first host) to see the partner ALIVE (memberlist
+ * pushPull picks among alive nodes). */
+static int ae_pair_ok(const gx_engine *e, uint32_t a, uint32_t b) {
+  if (departed(e, a) || departed(e, b)) return 0;
+  if (e->p.fd_enable) return reach(e, a, b) && MEM(e, a, b)->state == GX_M_ALIVE;
+  return 1;
+}
 static void ph_ae_pair(gx_engine *e, uint32_t t, void *ctx) {
   const struct ae_ctx *c = (const struct ae_ctx *)ctx;
-  if (is_local(e, c->pa[t]) && is_local(e, c->pb[t])) ae_exchange(e, c->pa[t], c->pb[t], c->now);
+  if (is_local(e, c->pa[t]) && is_local(e, c->pb[t]) && ae_pair_ok(e, c->pa[t], c->pb[t]))
+    ae_exchange(e, c->pa[t], c->pb[t], c->now);
 }
 /* Phase 5, pairs with both hosts here: both merge the other's round-start row. */
 static void ae_phase_local(gx_engine *e) {
@@ -857,7 +907,8 @@ static void ae_cross_build(gx_engine *e) {
 static void round_end(gx_engine *e) {
   e->round++;
   e->st.round = e->round;
-  for (uint32_t v = e->lo; v < e->hi; v++) wake_host(e, v);
+  for (uint32_t v = e->lo; v < e->hi; v++)
+    if (!departed(e, v)) wake_host(e, v);
 }
 
 static void run_one_round(gx_engine *e) {
@@ -908,6 +959,15 @@ void gx_params_default(gx_params *p) {
   p->device = 0;
   p->limit_bytes = 0;
   p->overhead_bytes = 3;
+  p->fd_enable = 0;
+  p->fd_probe_rounds = 5;
+  p->fd_indirect_checks = 3;
+  p->fd_msg_cap = 16;
+  p->fd_msg_bytes = 64;
+  p->fd_gossip_dead_rounds = 150;
+  p->depart_round = -1;
+  p->depart_ppm = 0;
+  gx_fd_defaults(p);
 }
 
 static int check_params(const gx_params *p) {
@@ -923,6 +983,16 @@ static int check_params(const gx_params *p) {
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
+  if (p->depart_ppm > 1000000u) return GX_EINVAL;
+  /* departures and the failure detector run on an unsharded engine */
+  if (p->depart_round >= 0 && p->depart_ppm && p->n_shards > 1) return GX_EINVAL;
+  if (p->fd_enable) {
+    if (p->n_hosts > 65534 || p->n_shards > 1 || p->fanout > 16) return GX_EINVAL;
+    if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
+    if (p->fd_retransmit_limit < 1 || p->fd_retransmit_limit > GX_FD_MAX_TX || p->fd_suspicion_k > 2) return GX_EINVAL;
+    for (uint32_t c = 0; c <= p->fd_suspicion_k; c++)
+      if (p->fd_suspicion_rounds[c] > (1u << 30)) return GX_EINVAL;
+  }
   return GX_OK;
 }
 
@@ -965,6 +1035,7 @@ static void init_state(gx_engine *e) {
   memset(&e->st, 0, sizeof(e->st));
   e->st.last_change_round = -1;
   e->round = 0;
+  fd_init(e);
 }
 
 int gx_create(const gx_params *p, gx_engine **out) {
@@ -1019,6 +1090,19 @@ int gx_create(const gx_params *p, gx_engine **out) {
       return GX_ENOMEM;
     }
   }
+  if (p->fd_enable) {
+    size_t k = e->K ? e->K : 1;
+    e->mem = (gx_member *)malloc(sizeof(gx_member) * H * H);
+    e->fdh = (gx_fd_host *)calloc(H, sizeof(gx_fd_host));
+    e->fdm = (gx_fd_msg *)calloc(H * k * p->fd_msg_cap, sizeof(gx_fd_msg));
+    e->fd_len = (uint32_t *)calloc(H * k, sizeof(uint32_t));
+    e->fd_peers = (uint32_t *)calloc(H * k, sizeof(uint32_t));
+    e->fd_np = (uint32_t *)calloc(H, sizeof(uint32_t));
+    if (!e->mem || !e->fdh || !e->fdm || !e->fd_len || !e->fd_peers || !e->fd_np) {
+      gx_destroy(e);
+      return GX_ENOMEM;
+    }
+  }
   if (e->sbytes)
     for (uint32_t r = 0; r < e->R; r++) e->sbytes[r] = GX_STATIC_BYTES_DEFAULT;
   if (!e->sbytes || !e->srvt || !e->vlc || !e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
@@ -1057,6 +1141,12 @@ int gx_destroy(gx_engine *e) {
   free(e->x_dig);
   free(e->x_diff);
   free(e->x_cnt);
+  free(e->mem);
+  free(e->fdh);
+  free(e->fdm);
+  free(e->fd_len);
+  free(e->fd_peers);
+  free(e->fd_np);
   free_names(e);
   free(e);
   return GX_OK;
@@ -1660,6 +1750,7 @@ int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
   for (uint32_t r = 0; r < e->R; r++) {
     uint64_t a = ~0ull, b = 0;
     for (uint32_t v = e->lo; v < e->hi; v++) {
+      if (departed(e, v)) continue;
       uint64_t w = e->view[(size_t)v * e->R + r];
       a = w < a ? w : a;
       b = w > b ? w : b;
@@ -1683,11 +1774,14 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
 }
 int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   if (!e || e->G > 1) return GX_EINVAL;
+  /* the live views must agree; a crashed host's view is frozen and left out */
   uint64_t bad = 0;
-  for (uint32_t r = 0; r < e->R; r++) {
-    uint64_t w0 = e->view[r];
-    for (uint32_t v = 1; v < e->H; v++)
-      if (e->view[(size_t)v * e->R + r] != w0) {
+  uint32_t v0 = 0;
+  while (v0 < e->H && departed(e, v0)) v0++;
+  for (uint32_t r = 0; r < e->R && v0 < e->H; r++) {
+    uint64_t w0 = e->view[(size_t)v0 * e->R + r];
+    for (uint32_t v = v0 + 1; v < e->H; v++)
+      if (!departed(e, v) && e->view[(size_t)v * e->R + r] != w0) {
         bad++;
         break;
       }

@@ -30,7 +30,7 @@ JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE = 0, 1, 2, 3, 4
 INIT_EMPTY, INIT_OWN, INIT_WARM = 0, 1, 2
 LIMIT_DEFAULT = 0xFFFFFFFF
 
-K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode"]
+K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode", "fd"]
 
 
 class GxService(C.Structure):
@@ -83,7 +83,14 @@ class GxParams(C.Structure):
         ("shard_id", C.c_uint32),
         ("limit_bytes", C.c_uint32),
         ("overhead_bytes", C.c_uint32),
+        ("fd_enable", C.c_uint32), ("fd_probe_rounds", C.c_uint32), ("fd_indirect_checks", C.c_uint32),
+        ("fd_retransmit_limit", C.c_uint32), ("fd_msg_cap", C.c_uint32), ("fd_msg_bytes", C.c_uint32),
+        ("fd_gossip_dead_rounds", C.c_uint32), ("fd_suspicion_k", C.c_uint32),
+        ("fd_suspicion_rounds", C.c_uint32 * 8), ("depart_round", C.c_int32), ("depart_ppm", C.c_uint32),
     ]
+
+    # fields memberlist derives from the cluster size (gx_fd_defaults)
+    FD_DERIVED = ("fd_retransmit_limit", "fd_suspicion_k", "fd_suspicion_rounds")
 
 
 class GxServerTimes(C.Structure):
@@ -114,19 +121,52 @@ class GxStats(C.Structure):
         "own_tombstones", "expire_server", "send_jobs", "ae_exchanges", "churn_events")] + [
         ("last_change_round", C.c_int64), ("scan_slots", C.c_uint64), ("ae_slots", C.c_uint64),
         ("bytes_sent", C.c_uint64), ("cap_cuts", C.c_uint64), ("change_events", C.c_uint64),
-        ("listener_drops", C.c_uint64), ("reserved", C.c_uint64 * 1)]
+        ("listener_drops", C.c_uint64)] + [(n, C.c_uint64) for n in (
+        "lost_packets", "fd_probes", "fd_probe_failures", "fd_suspicions", "fd_confirmations",
+        "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received")] + [
+        ("reserved", C.c_uint64 * 1)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
 
 
+M_ALIVE, M_SUSPECT, M_DEAD = 0, 1, 2
+FD_NONE = 0xFFFF
+FD_NO_DEADLINE = 0x7FFFFFFF
+
+
+class GxMember(C.Structure):
+    _fields_ = [("incarnation", C.c_uint32), ("msg_incarnation", C.c_uint32), ("change_round", C.c_int32),
+                ("deadline", C.c_int32), ("state", C.c_uint8), ("n_conf", C.c_uint8), ("tx", C.c_uint8),
+                ("msg_kind", C.c_uint8), ("msg_from", C.c_uint16), ("susp_from", C.c_uint16 * 3),
+                ("q_prev", C.c_uint16), ("q_next", C.c_uint16)]
+
+
+class GxFdHost(C.Structure):
+    _fields_ = [("probe_pass", C.c_uint32), ("probe_index", C.c_uint32), ("wrap_round", C.c_int32),
+                ("min_deadline", C.c_int32), ("q_len", C.c_uint32), ("departed", C.c_uint32),
+                ("q_head", C.c_uint16 * 32)]
+
+
+class GxFdMsg(C.Structure):
+    _fields_ = [("incarnation", C.c_uint32), ("node", C.c_uint16), ("from_", C.c_uint16), ("kind", C.c_uint8),
+                ("pad", C.c_uint8 * 3)]
+
+    def tup(self):
+        return (self.kind, self.node, self.incarnation, self.from_)
+
+
+def fd_msg(kind, node, inc, frm=None) -> GxFdMsg:
+    return GxFdMsg(int(inc), int(node), int(node if frm is None else frm), int(kind))
+
+
 class GxTiming(C.Structure):
-    _fields_ = [("ms", C.c_double * 10), ("launches", C.c_uint64 * 10), ("bytes", C.c_uint64 * 10),
-                ("units", C.c_uint64 * 10)]
+    _fields_ = [("ms", C.c_double * 11), ("launches", C.c_uint64 * 11), ("bytes", C.c_uint64 * 11),
+                ("units", C.c_uint64 * 11)]
 
     def as_dict(self):
         return {K_NAMES[i]: {"ms": self.ms[i], "launches": self.launches[i],
-                             "bytes": self.bytes[i], "units": self.units[i]} for i in range(10)}
+                             "bytes": self.bytes[i], "units": self.units[i]} for i in range(len(K_NAMES))}
 
 
 class GxNames(C.Structure):
@@ -157,6 +197,8 @@ ABI_FUNCS = [
     "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
+    "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
+    "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers",
 ]
 
 
@@ -214,6 +256,14 @@ def _declare(lib):
         "gx_local_state_json": ([vp, u32, vp, C.c_uint64, P(C.c_uint64)], i32),
         "gx_decode_state_json": ([vp, vp, C.c_uint64, P(GxService), u32, P(u32), P(GxDecodeStats)], i32),
         "gx_merge_remote_state_json": ([vp, u32, vp, C.c_uint64, P(GxDecodeStats)], i32),
+        "gx_fd_defaults": ([P(GxParams)], i32),
+        "gx_fd_read_members": ([vp, u32, u32, u32, P(GxMember)], i32),
+        "gx_fd_read_hosts": ([vp, u32, u32, P(GxFdHost)], i32),
+        "gx_fd_read_queue": ([vp, u32, P(GxFdMsg), P(C.c_uint8), u32, P(u32)], i32),
+        "gx_fd_notify": ([vp, u32, P(GxFdMsg), u32], i32),
+        "gx_fd_get_broadcasts": ([vp, u32, u32, P(GxFdMsg), P(u32)], i32),
+        "gx_fd_probe": ([vp, u32, P(u32), P(i32)], i32),
+        "gx_fd_timers": ([vp, u32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -254,11 +304,16 @@ def check(rc: int, what: str = ""):
 
 def default_params(lib=None, **kw) -> GxParams:
     p = GxParams()
-    (lib or load_product()).gx_params_default(C.byref(p))
+    lib = lib or load_product()
+    lib.gx_params_default(C.byref(p))
     for k, v in kw.items():
         if not hasattr(p, k):
             raise KeyError(k)
+        if k == "fd_suspicion_rounds":
+            v = (C.c_uint32 * 8)(*v)
         setattr(p, k, v)
+    if not any(k in kw for k in GxParams.FD_DERIVED):
+        check(lib.gx_fd_defaults(C.byref(p)), "gx_fd_defaults")  # memberlist's size-derived values
     return p
 
 
@@ -623,6 +678,49 @@ class Engine:
 
     def view_minmax(self, ptr_min: int, ptr_max: int):
         check(self.lib.gx_view_minmax(self.h, C.c_void_p(ptr_min), C.c_void_p(ptr_max)), "gx_view_minmax")
+
+    # memberlist failure detection ---------------------------------------------
+    def fd_members(self, host: int, lo: int = 0, hi: Optional[int] = None) -> bytes:
+        hi = self.H if hi is None else hi
+        out = (GxMember * max(1, hi - lo))()
+        check(self.lib.gx_fd_read_members(self.h, host, lo, hi, out), "gx_fd_read_members")
+        return bytes(out)[:C.sizeof(GxMember) * (hi - lo)]
+
+    def fd_member(self, host: int, node: int) -> GxMember:
+        m = GxMember()
+        check(self.lib.gx_fd_read_members(self.h, host, node, node + 1, C.byref(m)), "gx_fd_read_members")
+        return m
+
+    def fd_hosts(self, lo: int = 0, hi: Optional[int] = None):
+        hi = self.H if hi is None else hi
+        out = (GxFdHost * max(1, hi - lo))()
+        check(self.lib.gx_fd_read_hosts(self.h, lo, hi, out), "gx_fd_read_hosts")
+        return [out[i] for i in range(hi - lo)]
+
+    def fd_queue(self, host: int, cap: int = 65536):
+        out = (GxFdMsg * cap)()
+        tx = (C.c_uint8 * cap)()
+        n = C.c_uint32()
+        check(self.lib.gx_fd_read_queue(self.h, host, out, tx, cap, C.byref(n)), "gx_fd_read_queue")
+        return [(out[i].tup(), tx[i]) for i in range(min(n.value, cap))]
+
+    def fd_notify(self, host: int, msgs: Sequence):
+        arr = (GxFdMsg * max(1, len(msgs)))(*[m if isinstance(m, GxFdMsg) else fd_msg(*m) for m in msgs])
+        check(self.lib.gx_fd_notify(self.h, host, arr, len(msgs)), "gx_fd_notify")
+
+    def fd_get_broadcasts(self, host: int, limit: int):
+        out = (GxFdMsg * max(1, limit))()
+        n = C.c_uint32()
+        check(self.lib.gx_fd_get_broadcasts(self.h, host, limit, out, C.byref(n)), "gx_fd_get_broadcasts")
+        return [out[i].tup() for i in range(n.value)]
+
+    def fd_probe(self, host: int):
+        t, ack = C.c_uint32(), C.c_int()
+        check(self.lib.gx_fd_probe(self.h, host, C.byref(t), C.byref(ack)), "gx_fd_probe")
+        return (None if t.value == FD_NONE else t.value), bool(ack.value)
+
+    def fd_timers(self, host: int):
+        check(self.lib.gx_fd_timers(self.h, host), "gx_fd_timers")
 
     def converged(self):
         c = C.c_int()

@@ -36,10 +36,16 @@ enum {
   C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_BYTESENT,
   C_CAPCUT, C_CHG, C_NCTR
 };
+// Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
+enum {
+  C_LOST = C_NCTR, C_FD_PROBES, C_FD_PROBE_FAIL, C_FD_SUSPECT, C_FD_CONFIRM, C_FD_DEATH, C_FD_REFUTE,
+  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_NCTR_ALL
+};
+#define GX_NCTR_SLOTS 48
 
 #define GX_SHARDS 64
 struct DevCtr {
-  unsigned long long c[GX_SHARDS][32];              // counter shards (shard = block % 64)
+  unsigned long long c[GX_SHARDS][GX_NCTR_SLOTS];   // counter shards (shard = block % 64)
   unsigned long long last_change_p1[GX_SHARDS][8];  // last round with a slot change + 1
   unsigned long long bytes[GX_SHARDS][8];           // algorithmic HBM bytes per kernel class
   unsigned long long units[GX_SHARDS][8];           // slots / records per kernel class
@@ -47,7 +53,7 @@ struct DevCtr {
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5, ST_INIT_AGE = 6,
-       ST_AE = 7 };
+       ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11 };
 
 struct Dev {
   gx_params p;
@@ -84,6 +90,17 @@ struct Dev {
   uint32_t *ev_cnt;       // [n_logs] events since the last delivery (may exceed ev_cap)
   uint32_t ev_cap;
   DevCtr *ctr;
+  // memberlist failure detection (gx_fd.hpp), allocated when p.fd_enable; requires an unsharded
+  // engine, so member rows are indexed by host id
+  gx_member *mem;      // [H][H] member list of every host (the deadline field lives in fd_dl)
+  int32_t *fd_dl;      // [H][H] suspicion deadlines, scanned by k_fd_tick
+  gx_fd_host *fdh;     // [H]
+  gx_fd_msg *fdm;      // [H*K][fd_msg_cap] memberlist messages of this round's packets
+  uint32_t *fd_len;    // [H*K]
+  uint32_t *fd_peers;  // [H*K] gossip targets (memberlist's kRandomNodes)
+  uint32_t *fd_np;     // [H]
+  int pair_split;      // push-pull pairs stay inside partition halves (scripted model)
+  int departures;      // p.depart_round >= 0 && p.depart_ppm
 };
 
 // ------------------------------------------------------------------- schedule RNG (seeded) --
@@ -138,6 +155,13 @@ GXHD unsigned long long exp_time(const gx_params &p, uint64_t w) {
   return (unsigned long long)(ts_of(w) + life);
 }
 
+// Host departures (crash) and network reachability a -> b. With the failure
+// detector the partition is a network property; the scripted model samples within a side.
+GXHD bool departed_at(const gx_params &p, int64_t round, uint32_t u) {
+  if (p.depart_round < 0 || round < p.depart_round || !p.depart_ppm) return false;
+  return (uint32_t)(rng4(p.seed, ST_DEPART, u, 0, 0) % 1000000ull) < p.depart_ppm;
+}
+
 // ------------------------------------------------------------------------------ counters --
 GXD uint32_t shard_id() { return blockIdx.x & (GX_SHARDS - 1); }
 
@@ -183,6 +207,11 @@ GXD void acc_flush(const Dev &d, const Acc &a) {
 
 // Local index of an owned host (global id v in [lo, lo + Hl)).
 GXD uint32_t li(const Dev &d, uint32_t v) { return v - d.lo; }
+GXD bool departed(const Dev &d, uint32_t u) { return d.departures && departed_at(d.p, d.round, u); }
+GXD bool reach(const Dev &d, uint32_t a, uint32_t b) {
+  if (departed(d, a) || departed(d, b)) return false;
+  return !(d.partitioned && ((a < d.H / 2) != (b < d.H / 2)));
+}
 GXD uint64_t *vrow(const Dev &d, uint32_t v) { return &d.view[(size_t)li(d, v) * d.R]; }
 GXD gx_host_state *hst(const Dev &d, uint32_t v) { return &d.hs[li(d, v)]; }
 

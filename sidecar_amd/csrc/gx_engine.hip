@@ -20,6 +20,7 @@
 // No MFMA: the work is int64 compare/select over HBM-resident views (memory-bound).
 #include <hip/hip_runtime.h>
 
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -44,6 +45,7 @@ static uint32_t pow2_at_least(uint32_t x) {
 }
 
 #include "gx_kernels.hpp"
+#include "gx_fd.hpp"
 #include "gx_codec.hpp"
 
 // ================================================================================ host ==
@@ -117,6 +119,7 @@ static int64_t now_of(const gx_engine *e) { return e->d.p.t0_ns + e->d.round * e
 static void set_round_fields(gx_engine *e) {
   e->d.now = now_of(e);
   e->d.partitioned = e->d.round >= e->d.p.partition_start && e->d.round < e->d.p.partition_end;
+  e->d.pair_split = e->d.partitioned && !e->d.p.fd_enable;
 }
 
 struct LaunchTimer {
@@ -207,6 +210,10 @@ static int round_send_impl(gx_engine *e) {
         <<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
     k_bt_finish<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   }
+  if (d.p.fd_enable) {  // suspicion timers -> deadNode -> NotifyLeave; probe ticks
+    LaunchTimer t(e, GX_K_FD);
+    k_fd_tick<<<d.H, 64, 0, s>>>(d);
+  }
   if (d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2) {
     LaunchTimer t(e, GX_K_STORM);
     const bool ev = !e->log_views.empty();
@@ -215,8 +222,10 @@ static int round_send_impl(gx_engine *e) {
   }
   {
     LaunchTimer t(e, GX_K_SEND);
+    if (d.p.fd_enable) k_fd_send<<<nblk(d.H, 64), 64, 0, s>>>(d);  // memberlist's targets + messages
     // 4 lanes per host: measured best of 1/4/8/16/64 (profiles/send_team.sh)
-    k_send<4><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
+    if (d.p.fd_enable || d.departures) k_send<4, true><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
+    else k_send<4, false><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -242,6 +251,10 @@ static int round_merge_impl(gx_engine *e) {
     if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<d.Hl, 64, 0, s>>>(d);  // 32-bit keys
     else (ev ? k_merge<false, true> : k_merge<false, false>)<<<d.Hl, 64, 0, s>>>(d);
   }
+  if (d.p.fd_enable && d.K) {  // the packets' memberlist messages, after the catalog merge
+    LaunchTimer t(e, GX_K_FD);
+    k_fd_recv<<<nblk(d.H, 64), 64, 0, s>>>(d);
+  }
   HIPCHK(hipGetLastError());
   return GX_OK;
 }
@@ -260,7 +273,7 @@ static int ae_whole_impl(gx_engine *e) {
   if (ae_round(e)) {
     uint32_t np;
     uint64_t key0, key1 = 0;
-    if (d.partitioned) {
+    if (d.pair_split) {
       uint32_t m0 = d.H / 2, m1 = d.H - m0;
       np = m0 / 2 + m1 / 2;
       key0 = rng4(d.p.seed, ST_AE, (uint64_t)d.round, 0, 0);
@@ -335,6 +348,43 @@ void gx_params_default(gx_params *p) {
   p->aged_max_ns = 100000000000ll;
   p->storm_round = -1;
   p->overhead_bytes = 3;
+  p->fd_probe_rounds = 5;
+  p->fd_indirect_checks = 3;
+  p->fd_msg_cap = 16;
+  p->fd_msg_bytes = 64;
+  p->fd_gossip_dead_rounds = 150;
+  p->depart_round = -1;
+  gx_fd_defaults(p);
+}
+
+// memberlist's size-derived parameters: util.go retransmitLimit / suspicionTimeout,
+// suspicion.go remainingSuspicionTime (include/gx.h).
+int gx_fd_defaults(gx_params *p) {
+  if (!p || p->n_hosts < 1 || p->fd_probe_rounds < 1 || p->round_ns <= 0) return GX_EINVAL;
+  const int suspicion_mult = 4, max_mult = 6, retransmit_mult = 4;
+  const double n = (double)p->n_hosts;
+  uint32_t limit = (uint32_t)(retransmit_mult * (int)ceil(log10(n + 1.0)));
+  p->fd_retransmit_limit = limit > GX_FD_MAX_TX ? GX_FD_MAX_TX : limit;
+  const double node_scale = fmax(1.0, log10(fmax(1.0, n)));
+  const int64_t interval = (int64_t)p->fd_probe_rounds * p->round_ns;
+  const int64_t tmin = (int64_t)suspicion_mult * (int64_t)(node_scale * 1000.0) * interval / 1000;
+  const int64_t tmax = (int64_t)max_mult * tmin;
+  int k = suspicion_mult - 2;
+  if ((int)p->n_hosts - 2 < k) k = 0;
+  p->fd_suspicion_k = (uint32_t)k;
+  for (int c = 0; c < 8; c++) {
+    int64_t t = tmin;
+    if (c == 0) {
+      t = k < 1 ? tmin : tmax;
+    } else if (c <= k) {
+      const double frac = log((double)c + 1.0) / log((double)k + 1.0);
+      const double raw = (double)tmax / 1e9 - frac * ((double)tmax / 1e9 - (double)tmin / 1e9);
+      t = (int64_t)floor(1000.0 * raw) * 1000000ll;
+      if (t < tmin) t = tmin;
+    }
+    p->fd_suspicion_rounds[c] = (uint32_t)((t + p->round_ns - 1) / p->round_ns);
+  }
+  return GX_OK;
 }
 
 static int check_params(const gx_params *p) {
@@ -350,6 +400,16 @@ static int check_params(const gx_params *p) {
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
+  if (p->depart_ppm > 1000000u) return GX_EINVAL;
+  // departures and the failure detector run on an unsharded engine
+  if (p->depart_round >= 0 && p->depart_ppm && p->n_shards > 1) return GX_EINVAL;
+  if (p->fd_enable) {
+    if (p->n_hosts > 65534 || p->n_shards > 1 || p->fanout > 16) return GX_EINVAL;
+    if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
+    if (p->fd_retransmit_limit < 1 || p->fd_retransmit_limit > GX_FD_MAX_TX || p->fd_suspicion_k > 2) return GX_EINVAL;
+    for (uint32_t c = 0; c <= p->fd_suspicion_k; c++)
+      if (p->fd_suspicion_rounds[c] > (1u << 30)) return GX_EINVAL;
+  }
   return GX_OK;
 }
 
@@ -365,7 +425,8 @@ int gx_destroy(gx_engine *e) {
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
-                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf};
+                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf,
+                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
@@ -469,6 +530,16 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.ev_slot, sizeof(int32_t) * H);
   ALLOC(d.ctr, sizeof(DevCtr));
   ALLOC(e->own_list, sizeof(grec) * H * d.S);
+  d.departures = p->depart_round >= 0 && p->depart_ppm;
+  if (p->fd_enable) {  // unsharded: H == Hl
+    ALLOC(d.mem, sizeof(gx_member) * Hg * Hg);
+    ALLOC(d.fd_dl, sizeof(int32_t) * Hg * Hg);
+    ALLOC(d.fdh, sizeof(gx_fd_host) * Hg);
+    ALLOC(d.fdm, sizeof(gx_fd_msg) * Hg * K * p->fd_msg_cap);
+    ALLOC(d.fd_len, sizeof(uint32_t) * Hg * K);
+    ALLOC(d.fd_peers, sizeof(uint32_t) * Hg * K);
+    ALLOC(d.fd_np, sizeof(uint32_t) * Hg);
+  }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
   if (d.G > 1) {
@@ -503,6 +574,10 @@ int gx_create(const gx_params *p, gx_engine **out) {
   k_init_views<<<2048, 256, 0, s>>>(d, rec_word);
   k_init_times<<<2048, 256, 0, s>>>(d, rec_word);
   k_init_hosts<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
+  if (p->fd_enable) {
+    k_fd_init<<<2048, 256, 0, s>>>(d);
+    HIPCHK(hipMemsetAsync(d.fd_len, 0, sizeof(uint32_t) * Hg * K, s));
+  }
   k_minexp_recompute<<<d.Hl, 256, 0, s>>>(d, 0);
   rc = sync_check(e);
   (void)hipFree(rec_word);
@@ -1365,11 +1440,11 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
   int rc = sync_check(e);
   if (rc) return rc;
   const DevCtr &x = tmp[0];
-  for (int i = 0; i < 32; i++) c[i] = 0;
+  for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] = 0;
   for (int i = 0; i < 8; i++) bytes[i] = units[i] = 0;
   *last_p1 = 0;
   for (int s = 0; s < GX_SHARDS; s++) {
-    for (int i = 0; i < 32; i++) c[i] += x.c[s][i];
+    for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] += x.c[s][i];
     for (int i = 0; i < 8; i++) {
       bytes[i] += x.bytes[s][i];
       units[i] += x.units[s][i];
@@ -1382,10 +1457,20 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
 int gx_stats_get(gx_engine *e, gx_stats *out) {
   if (!e || !out) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  unsigned long long c[32], lp1, bytes[8], units[8];
+  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[8], units[8];
   int rc = read_ctr(e, c, &lp1, bytes, units);
   if (rc) return rc;
   memset(out, 0, sizeof(*out));
+  out->lost_packets = c[C_LOST];
+  out->fd_probes = c[C_FD_PROBES];
+  out->fd_probe_failures = c[C_FD_PROBE_FAIL];
+  out->fd_suspicions = c[C_FD_SUSPECT];
+  out->fd_confirmations = c[C_FD_CONFIRM];
+  out->fd_deaths = c[C_FD_DEATH];
+  out->fd_refutes = c[C_FD_REFUTE];
+  out->fd_alive_updates = c[C_FD_ALIVE];
+  out->fd_msgs_sent = c[C_FD_SENT];
+  out->fd_msgs_received = c[C_FD_RECV];
   out->round = e->d.round;
   out->gossip_merges = c[C_GOSSIP_MERGES];
   out->ae_merges = c[C_AE_MERGES];
@@ -1425,7 +1510,7 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
   HIPCHK(hipSetDevice(e->device));
   int rc = drain_timing(e);
   if (rc) return rc;
-  unsigned long long c[32], lp1, bytes[8], units[8];
+  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[8], units[8];
   rc = read_ctr(e, c, &lp1, bytes, units);
   if (rc) return rc;
   memset(out, 0, sizeof(*out));
@@ -1436,6 +1521,128 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
     out->units[i] = i < 8 ? units[i] : e->host_units[i];
   }
   return GX_OK;
+}
+
+// ------------------------------------------------------- memberlist failure detection ----
+static bool fd_ok(const gx_engine *e, uint32_t host) { return e && e->d.p.fd_enable && host < e->d.H; }
+
+int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t lo, uint32_t hi, gx_member *out) {
+  if (!fd_ok(e, host) || lo > hi || hi > e->d.H || (!out && hi > lo)) return GX_EINVAL;
+  if (hi == lo) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  const Dev &d = e->d;
+  std::vector<int32_t> dl(hi - lo);
+  HIPCHK(hipMemcpyAsync(out, &d.mem[(size_t)host * d.H + lo], sizeof(gx_member) * (hi - lo), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipMemcpyAsync(dl.data(), &d.fd_dl[(size_t)host * d.H + lo], sizeof(int32_t) * (hi - lo),
+                        hipMemcpyDeviceToHost, e->stream));
+  int rc = sync_check(e);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < hi - lo; i++) out[i].deadline = dl[i];
+  return GX_OK;
+}
+
+int gx_fd_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_fd_host *out) {
+  if (!e || !e->d.p.fd_enable || lo > hi || hi > e->d.H || (!out && hi > lo)) return GX_EINVAL;
+  if (hi == lo) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipMemcpyAsync(out, &e->d.fdh[lo], sizeof(gx_fd_host) * (hi - lo), hipMemcpyDeviceToHost, e->stream));
+  int rc = sync_check(e);
+  if (rc) return rc;
+  for (uint32_t v = lo; v < hi; v++) out[v - lo].departed = departed_at(e->d.p, e->d.round, v) ? 1u : 0u;
+  return GX_OK;
+}
+
+int gx_fd_read_queue(gx_engine *e, uint32_t host, gx_fd_msg *out, uint8_t *transmits, uint32_t cap,
+                     uint32_t *n_out) {
+  if (!fd_ok(e, host) || !n_out) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  const Dev &d = e->d;
+  std::vector<gx_member> row(d.H);
+  gx_fd_host h;
+  HIPCHK(hipMemcpyAsync(row.data(), &d.mem[(size_t)host * d.H], sizeof(gx_member) * d.H, hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipMemcpyAsync(&h, &d.fdh[host], sizeof(gx_fd_host), hipMemcpyDeviceToHost, e->stream));
+  int rc = sync_check(e);
+  if (rc) return rc;
+  uint32_t n = 0;
+  for (uint32_t b = 0; b < d.p.fd_retransmit_limit; b++)
+    for (uint32_t m = h.q_head[b]; m != GX_FD_NONE && n <= d.H; m = row[m].q_next) {
+      if (n < cap) {
+        if (out) {
+          gx_fd_msg g = {};
+          g.incarnation = row[m].msg_incarnation;
+          g.node = (uint16_t)m;
+          g.from = row[m].msg_from;
+          g.kind = row[m].msg_kind;
+          out[n] = g;
+        }
+        if (transmits) transmits[n] = (uint8_t)b;
+      }
+      n++;
+    }
+  *n_out = n;
+  return GX_OK;
+}
+
+int gx_fd_notify(gx_engine *e, uint32_t host, const gx_fd_msg *msgs, uint32_t n) {
+  if (!fd_ok(e, host) || (!msgs && n)) return GX_EINVAL;
+  for (uint32_t i = 0; i < n; i++)
+    if (msgs[i].node >= e->d.H || msgs[i].kind > GX_M_DEAD) return GX_EINVAL;
+  if (!n) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, sizeof(gx_fd_msg) * n);
+  if (rc) return rc;
+  set_round_fields(e);
+  HIPCHK(hipMemcpyAsync(e->api_dev, msgs, sizeof(gx_fd_msg) * n, hipMemcpyHostToDevice, e->stream));
+  k_fd_api_notify<<<1, 64, 0, e->stream>>>(e->d, host, (const gx_fd_msg *)e->api_dev, n);
+  return sync_check(e);
+}
+
+int gx_fd_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_fd_msg *out, uint32_t *n_out) {
+  if (!fd_ok(e, host) || !n_out || limit > 64 || (!out && limit)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, 64 + sizeof(gx_fd_msg) * 64);
+  if (rc) return rc;
+  set_round_fields(e);
+  uint32_t *dn = (uint32_t *)e->api_dev;
+  gx_fd_msg *dm = (gx_fd_msg *)((char *)e->api_dev + 64);
+  k_fd_api_getb<<<1, 64, 0, e->stream>>>(e->d, host, limit, dm, dn);
+  uint32_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, dn, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  rc = sync_check(e);
+  if (rc) return rc;
+  if (n) {
+    HIPCHK(hipMemcpyAsync(out, dm, sizeof(gx_fd_msg) * n, hipMemcpyDeviceToHost, e->stream));
+    rc = sync_check(e);
+    if (rc) return rc;
+  }
+  *n_out = n;
+  return GX_OK;
+}
+
+int gx_fd_probe(gx_engine *e, uint32_t host, uint32_t *target, int *acked) {
+  if (!fd_ok(e, host)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, 64);
+  if (rc) return rc;
+  set_round_fields(e);
+  k_fd_api_probe<<<1, 64, 0, e->stream>>>(e->d, host, (uint32_t *)e->api_dev);
+  uint32_t x[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(x, e->api_dev, sizeof(x), hipMemcpyDeviceToHost, e->stream));
+  rc = sync_check(e);
+  if (rc) return rc;
+  if (target) *target = x[0];
+  if (acked) *acked = (int)x[1];
+  return GX_OK;
+}
+
+int gx_fd_timers(gx_engine *e, uint32_t host) {
+  if (!fd_ok(e, host)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  set_round_fields(e);
+  k_fd_api_timers<<<1, 64, 0, e->stream>>>(e->d, host);
+  return sync_check(e);
 }
 
 int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {

@@ -1,0 +1,439 @@
+// gx_fd.hpp — memberlist failure detection on the device.
+//
+// memberlist (github.com/NinesStack/memberlist v0.0.0-20170522194404-cfac2b5cf519, reference
+// go.mod:6; a fork of hashicorp/memberlist, absent from the reference tree) runs SWIM + Lifeguard
+// on every Sidecar node; Sidecar only reacts to NotifyLeave -> go ExpireServer(node)
+// (services_delegate.go:173-176). Per simulated host the engine keeps memberlist's member list
+// (gx_member per (host, node), suspicion deadlines in fd_dl for coalesced timer scans) and its
+// TransmitLimitedQueue as per-transmit-count stacks linked through the member rows.
+//
+// Kernels (one host per thread or wave; the work is pointer-chasing integer logic, latency-
+// bound, not bandwidth-bound):
+//   k_fd_tick   one wave per host: suspicion timers due -> deadNode (NotifyLeave ->
+//               ExpireServer), the due deadlines found by a coalesced scan of the host's fd_dl
+//               row (only when its exact lower bound min_deadline has passed); then probe() on
+//               the host's probe tick (lane 0)
+//   k_fd_send   one thread per host: kRandomNodes gossip targets, then the memberlist messages
+//               of every packet (TransmitLimitedQueue.GetBroadcasts)
+//   k_fd_recv   one thread per receiver, after the catalog merge: the packets' memberlist
+//               messages in sender order -> aliveNode / suspectNode / deadNode
+// Handlers follow the restatement in oracle/gx_oracle_fd.c (the CPU checker) rule for rule.
+
+struct FdAcc {
+  unsigned c[C_NCTR_ALL - C_NCTR];
+  GXD FdAcc() {
+#pragma unroll
+    for (int i = 0; i < C_NCTR_ALL - C_NCTR; i++) c[i] = 0;
+  }
+  GXD void inc(int k, unsigned v = 1) { c[k - C_NCTR] += v; }
+};
+GXD void fd_flush(const Dev &d, const FdAcc &f) {
+  for (int i = 0; i < C_NCTR_ALL - C_NCTR; i++) {
+    unsigned long long x = wave_sum((unsigned long long)f.c[i]);
+    if ((threadIdx.x & 63) == 0) ctr_atomic(d, C_NCTR + i, x);
+  }
+}
+
+GXD gx_member *memp(const Dev &d, uint32_t v, uint32_t m) { return &d.mem[(size_t)v * d.H + m]; }
+GXD int32_t *dlp(const Dev &d, uint32_t v, uint32_t m) { return &d.fd_dl[(size_t)v * d.H + m]; }
+
+// Reaped at the host's last resetNodes: dead for more than GossipToTheDeadTime.
+GXD bool fd_reaped(const Dev &d, uint32_t v, const gx_member *x) {
+  return x->state == GX_M_DEAD &&
+         (int64_t)d.fdh[v].wrap_round - (int64_t)x->change_round > (int64_t)d.p.fd_gossip_dead_rounds;
+}
+
+// ----------------------------------------------------------------- TransmitLimitedQueue --
+GXD void q_unlink(const Dev &d, uint32_t v, uint32_t m) {
+  gx_member *x = memp(d, v, m);
+  gx_fd_host *h = &d.fdh[v];
+  const uint16_t pv = x->q_prev, nx = x->q_next;
+  if (pv != GX_FD_NONE) memp(d, v, pv)->q_next = nx;
+  else h->q_head[x->tx - 1] = nx;
+  if (nx != GX_FD_NONE) memp(d, v, nx)->q_prev = pv;
+  x->q_prev = x->q_next = GX_FD_NONE;
+  x->tx = 0;
+  h->q_len--;
+}
+GXD void q_push(const Dev &d, uint32_t v, uint32_t m, uint32_t b) {  // newest of bucket b
+  gx_member *x = memp(d, v, m);
+  gx_fd_host *h = &d.fdh[v];
+  const uint16_t top = h->q_head[b];
+  x->q_prev = GX_FD_NONE;
+  x->q_next = top;
+  if (top != GX_FD_NONE) memp(d, v, top)->q_prev = (uint16_t)m;
+  h->q_head[b] = (uint16_t)m;
+  x->tx = (uint8_t)(b + 1);
+  h->q_len++;
+}
+// encodeAndBroadcast -> QueueBroadcast: invalidates the queued message about m.
+GXD void fd_broadcast(const Dev &d, uint32_t v, uint32_t m, int kind, uint32_t inc, uint32_t from) {
+  gx_member *x = memp(d, v, m);
+  if (x->tx) q_unlink(d, v, m);
+  x->msg_kind = (uint8_t)kind;
+  x->msg_incarnation = inc;
+  x->msg_from = (uint16_t)from;
+  q_push(d, v, m, 0);
+}
+// TransmitLimitedQueue.GetBroadcasts with a message budget (<= 64).
+GXD uint32_t fd_get_broadcasts(const Dev &d, FdAcc &f, uint32_t v, uint32_t limit, gx_fd_msg *out) {
+  uint16_t taken[64];
+  uint8_t from_b[64];
+  uint32_t n = 0;
+  const uint32_t L = d.p.fd_retransmit_limit;
+  if (limit > 64) limit = 64;
+  for (uint32_t b = 0; b < L && n < limit; b++)
+    for (uint32_t m = d.fdh[v].q_head[b]; m != GX_FD_NONE && n < limit; m = memp(d, v, m)->q_next) {
+      taken[n] = (uint16_t)m;
+      from_b[n] = (uint8_t)b;
+      n++;
+    }
+  for (uint32_t i = 0; i < n; i++) {
+    const gx_member *x = memp(d, v, taken[i]);
+    gx_fd_msg g;
+    g.incarnation = x->msg_incarnation;
+    g.node = taken[i];
+    g.from = x->msg_from;
+    g.kind = x->msg_kind;
+    g.pad[0] = g.pad[1] = g.pad[2] = 0;
+    out[i] = g;
+    q_unlink(d, v, taken[i]);
+  }
+  for (uint32_t i = n; i-- > 0;)
+    if ((uint32_t)from_b[i] + 1 < L) q_push(d, v, taken[i], from_b[i] + 1u);
+  f.inc(C_FD_SENT, n);
+  return n;
+}
+
+// --------------------------------------------------------------------- message handlers --
+GXD void fd_set_deadline(const Dev &d, uint32_t v, uint32_t m, int64_t dl) {
+  if (dl > GX_FD_NO_DEADLINE - 1) dl = GX_FD_NO_DEADLINE - 1;
+  *dlp(d, v, m) = (int32_t)dl;
+  if ((int32_t)dl < d.fdh[v].min_deadline) d.fdh[v].min_deadline = (int32_t)dl;
+}
+GXD void fd_refute(const Dev &d, FdAcc &f, uint32_t v, uint32_t accused) {
+  gx_member *me = memp(d, v, v);
+  uint32_t inc = me->incarnation + 1;
+  if (accused >= inc) inc = accused + 1;
+  me->incarnation = inc;
+  fd_broadcast(d, v, v, GX_M_ALIVE, inc, v);
+  f.inc(C_FD_REFUTE);
+}
+// deadNode; NotifyLeave -> ExpireServer (services_delegate.go:173-176).
+GXD void fd_dead_node(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+  const uint32_t m = g.node;
+  gx_member *x = memp(d, v, m);
+  if (fd_reaped(d, v, x)) return;
+  if (g.incarnation < x->incarnation) return;
+  *dlp(d, v, m) = GX_FD_NO_DEADLINE;  // delete(m.nodeTimers, d.Node)
+  if (x->state == GX_M_DEAD) return;
+  if (m == v) {
+    fd_refute(d, f, v, g.incarnation);
+    return;
+  }
+  fd_broadcast(d, v, m, GX_M_DEAD, g.incarnation, g.from);
+  x->incarnation = g.incarnation;
+  x->state = GX_M_DEAD;
+  x->change_round = (int32_t)d.round;
+  f.inc(C_FD_DEATH);
+  expire_server(d, a, v, m);
+}
+GXD bool fd_confirm(const Dev &d, FdAcc &f, uint32_t v, uint32_t m, gx_member *x, uint32_t from) {
+  if (x->n_conf >= d.p.fd_suspicion_k) return false;
+  for (uint32_t i = 0; i <= x->n_conf; i++)
+    if (x->susp_from[i] == from) return false;
+  x->susp_from[1 + x->n_conf] = (uint16_t)from;
+  x->n_conf++;
+  *dlp(d, v, m) = GX_FD_NO_DEADLINE;
+  fd_set_deadline(d, v, m, (int64_t)x->change_round + d.p.fd_suspicion_rounds[x->n_conf]);
+  f.inc(C_FD_CONFIRM);
+  return true;
+}
+GXD void fd_suspect_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+  const uint32_t m = g.node;
+  gx_member *x = memp(d, v, m);
+  if (fd_reaped(d, v, x)) return;
+  if (g.incarnation < x->incarnation) return;
+  if (x->state == GX_M_SUSPECT) {
+    if (fd_confirm(d, f, v, m, x, g.from)) fd_broadcast(d, v, m, GX_M_SUSPECT, g.incarnation, g.from);
+    return;
+  }
+  if (x->state != GX_M_ALIVE) return;
+  if (m == v) {
+    fd_refute(d, f, v, g.incarnation);
+    return;
+  }
+  fd_broadcast(d, v, m, GX_M_SUSPECT, g.incarnation, g.from);
+  x->incarnation = g.incarnation;
+  x->state = GX_M_SUSPECT;
+  x->change_round = (int32_t)d.round;
+  x->n_conf = 0;
+  x->susp_from[0] = (uint16_t)g.from;
+  x->susp_from[1] = x->susp_from[2] = GX_FD_NONE;
+  fd_set_deadline(d, v, m, d.round + (int64_t)d.p.fd_suspicion_rounds[0]);
+  f.inc(C_FD_SUSPECT);
+}
+GXD void fd_alive_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+  const uint32_t m = g.node;
+  gx_member *x = memp(d, v, m);
+  if (fd_reaped(d, v, x)) {  // unknown node: re-added as dead, incarnation 0
+    x->state = GX_M_DEAD;
+    x->incarnation = 0;
+    x->change_round = INT32_MIN;
+  }
+  if (m == v) {
+    if (g.incarnation <= x->incarnation) return;
+    uint32_t inc = x->incarnation + 1;
+    if (g.incarnation >= inc) inc = g.incarnation + 1;
+    x->incarnation = inc;
+    fd_broadcast(d, v, v, GX_M_ALIVE, inc, v);
+    f.inc(C_FD_REFUTE);
+    return;
+  }
+  if (g.incarnation <= x->incarnation) return;
+  *dlp(d, v, m) = GX_FD_NO_DEADLINE;
+  fd_broadcast(d, v, m, GX_M_ALIVE, g.incarnation, g.from);
+  x->incarnation = g.incarnation;
+  if (x->state != GX_M_ALIVE) {
+    x->state = GX_M_ALIVE;
+    x->change_round = (int32_t)d.round;
+  }
+  x->n_conf = 0;
+  f.inc(C_FD_ALIVE);
+}
+GXD void fd_handle(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+  if (g.node >= d.H) return;
+  if (g.kind == GX_M_ALIVE) fd_alive_node(d, f, v, g);
+  else if (g.kind == GX_M_SUSPECT) fd_suspect_node(d, f, v, g);
+  else if (g.kind == GX_M_DEAD) fd_dead_node(d, a, f, v, g);
+  f.inc(C_FD_RECV);
+}
+
+// ---------------------------------------------------------------------------- probes ------
+// probe() + probeNode(): returns the target (GX_FD_NONE if none), *ack its outcome.
+GXD uint32_t fd_probe_host(const Dev &d, FdAcc &f, uint32_t v, bool *ack_out) {
+  gx_fd_host *h = &d.fdh[v];
+  const uint32_t H = d.H;
+  uint32_t t = GX_FD_NONE, num_check = 0;
+  *ack_out = false;
+  while (num_check < H) {
+    if (h->probe_index >= H) {  // resetNodes: reap, reshuffle
+      h->probe_pass++;
+      h->probe_index = 0;
+      h->wrap_round = (int32_t)d.round;
+      num_check++;
+      continue;
+    }
+    uint32_t c = feistel_perm(rng4(d.p.seed, ST_FD_PERM, v, h->probe_pass, 0), h->probe_index, H);
+    h->probe_index++;
+    if (c == v || memp(d, v, c)->state == GX_M_DEAD) {
+      num_check++;
+      continue;
+    }
+    t = c;
+    break;
+  }
+  if (t == GX_FD_NONE) return t;
+  f.inc(C_FD_PROBES);
+  bool ack = reach(d, v, t);
+  if (!ack) {  // IndirectChecks relays: kRandomNodes over alive nodes other than us and the target
+    uint32_t relays[16], nr = 0;
+    const uint32_t want = d.p.fd_indirect_checks;
+    for (uint32_t a = 0; nr < want && a < 3u * H; a++) {
+      uint32_t r = unif(rng4(d.p.seed, ST_FD_RELAY, (uint64_t)d.round, v, a), H);
+      if (r == v || r == t || memp(d, v, r)->state != GX_M_ALIVE) continue;
+      bool dup = false;
+      for (uint32_t i = 0; i < nr; i++) dup |= relays[i] == r;
+      if (!dup) relays[nr++] = r;
+    }
+    for (uint32_t i = 0; i < nr; i++)
+      if (reach(d, v, relays[i]) && reach(d, relays[i], t)) ack = true;
+  }
+  if (!ack) {
+    f.inc(C_FD_PROBE_FAIL);
+    gx_fd_msg s;
+    s.incarnation = memp(d, v, t)->incarnation;
+    s.node = (uint16_t)t;
+    s.from = (uint16_t)v;
+    s.kind = GX_M_SUSPECT;
+    fd_suspect_node(d, f, v, s);
+  }
+  *ack_out = ack;
+  return t;
+}
+GXD bool fd_probe_tick(const Dev &d, uint32_t v) {
+  const uint32_t P = d.p.fd_probe_rounds;
+  return (uint64_t)d.round % P == rng4(d.p.seed, ST_FD_PHASE, v, 0, 0) % P;
+}
+
+// Suspicion timers of host v due this round, one wave: coalesced scan of the fd_dl row, lane 0
+// declares the due nodes dead in node order; the new exact min_deadline is the wave minimum of
+// the rest.
+GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (d.fdh[v].min_deadline > d.round) return;  // uniform
+  int32_t mn = GX_FD_NO_DEADLINE;
+  for (uint32_t base = 0; base < d.H; base += 64) {
+    const uint32_t m = base + lane;
+    const int32_t dl = m < d.H ? *dlp(d, v, m) : GX_FD_NO_DEADLINE;
+    const bool due = dl <= d.round;
+    if (!due) mn = dl < mn ? dl : mn;
+    unsigned long long due_mask = __ballot(due);
+    if (lane == 0)
+      while (due_mask) {
+        const uint32_t k = (uint32_t)__ffsll((long long)due_mask) - 1;
+        due_mask &= due_mask - 1;
+        gx_fd_msg g;
+        g.incarnation = memp(d, v, base + k)->incarnation;
+        g.node = (uint16_t)(base + k);
+        g.from = (uint16_t)v;
+        g.kind = GX_M_DEAD;
+        fd_dead_node(d, a, f, v, g);
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int32_t y = __shfl_xor(mn, o, 64);
+    mn = y < mn ? y : mn;
+  }
+  if (lane == 0) d.fdh[v].min_deadline = mn;
+}
+
+// gossip(): kRandomNodes(GossipNodes) skipping us and nodes dead beyond GossipToTheDeadTime.
+GXD uint32_t fd_sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
+  const uint32_t H = d.H;
+  uint32_t cnt = 0;
+  if (H < 2) return 0;
+  for (uint32_t a = 0; cnt < d.K && a < 3u * H; a++) {
+    uint32_t p = unif(rng4(d.p.seed, ST_PEER, (uint64_t)d.round, u, a), H);
+    if (p == u) continue;
+    const gx_member *x = memp(d, u, p);
+    if (x->state == GX_M_DEAD && d.round - (int64_t)x->change_round > (int64_t)d.p.fd_gossip_dead_rounds) continue;
+    bool dup = false;
+    for (uint32_t i = 0; i < cnt; i++) dup |= peers[i] == p;
+    if (!dup) peers[cnt++] = p;
+  }
+  return cnt;
+}
+GXD uint32_t fd_budget(const Dev &d) {
+  uint32_t b = d.p.fd_msg_cap;
+  if (d.p.limit_bytes) {
+    uint32_t x = d.p.limit_bytes / (d.p.fd_msg_bytes + 2);
+    b = x < b ? x : b;
+  }
+  return b;
+}
+
+// ---------------------------------------------------------------------------- kernels -----
+__global__ void k_fd_init(Dev d) {
+  const size_t n = (size_t)d.H * d.H;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    gx_member x;
+    x.incarnation = 0;
+    x.msg_incarnation = 0;
+    x.change_round = 0;
+    x.deadline = GX_FD_NO_DEADLINE;
+    x.state = GX_M_ALIVE;
+    x.n_conf = 0;
+    x.tx = 0;
+    x.msg_kind = 0;
+    x.msg_from = GX_FD_NONE;
+    x.susp_from[0] = x.susp_from[1] = x.susp_from[2] = GX_FD_NONE;
+    x.q_prev = x.q_next = GX_FD_NONE;
+    d.mem[i] = x;
+    d.fd_dl[i] = GX_FD_NO_DEADLINE;
+  }
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < d.H; v += (size_t)gridDim.x * blockDim.x) {
+    gx_fd_host h;
+    h.probe_pass = 0;
+    h.probe_index = 0;
+    h.wrap_round = INT32_MIN;
+    h.min_deadline = GX_FD_NO_DEADLINE;
+    h.q_len = 0;
+    h.departed = 0;
+    for (int b = 0; b < GX_FD_MAX_TX; b++) h.q_head[b] = GX_FD_NONE;
+    d.fdh[v] = h;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_fd_tick(Dev d) {
+  Acc a;
+  FdAcc f;
+  const uint32_t v = blockIdx.x;
+  if (!departed(d, v)) {
+    fd_timers_wave(d, a, f, v);
+    if (threadIdx.x == 0 && fd_probe_tick(d, v)) {
+      bool ack;
+      fd_probe_host(d, f, v, &ack);
+    }
+  }
+  acc_flush(d, a);
+  fd_flush(d, f);
+}
+
+__global__ __launch_bounds__(64) void k_fd_send(Dev d) {
+  FdAcc f;
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < d.H) {
+    const uint32_t K = d.K, cap = d.p.fd_msg_cap;
+    for (uint32_t j = 0; j < K; j++) d.fd_len[(size_t)u * K + j] = 0;
+    uint32_t np = 0;
+    if (!departed(d, u)) {
+      uint32_t peers[16];
+      np = fd_sample_peers(d, u, peers);
+      const uint32_t budget = fd_budget(d);
+      for (uint32_t j = 0; j < np; j++) {
+        d.fd_peers[(size_t)u * K + j] = peers[j];
+        d.fd_len[(size_t)u * K + j] = fd_get_broadcasts(d, f, u, budget, &d.fdm[((size_t)u * K + j) * cap]);
+      }
+    }
+    d.fd_np[u] = np;
+  }
+  fd_flush(d, f);
+}
+
+__global__ __launch_bounds__(64) void k_fd_recv(Dev d) {
+  Acc a;
+  FdAcc f;
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < d.H && !departed(d, v)) {
+    const uint32_t cap = d.p.fd_msg_cap;
+    for (uint32_t x = d.in_cnt[v]; x < d.in_cnt[v + 1]; x++) {
+      const uint32_t e = d.in_sorted[x].x, n = d.fd_len[e];
+      for (uint32_t y = 0; y < n; y++) fd_handle(d, a, f, v, d.fdm[(size_t)e * cap + y]);
+    }
+  }
+  acc_flush(d, a);
+  fd_flush(d, f);
+}
+
+// Single-host ABI kernels (one wave; lane 0 runs the handler logic).
+__global__ __launch_bounds__(64) void k_fd_api_notify(Dev d, uint32_t v, const gx_fd_msg *msgs, uint32_t n) {
+  Acc a;
+  FdAcc f;
+  if (threadIdx.x == 0)
+    for (uint32_t i = 0; i < n; i++) fd_handle(d, a, f, v, msgs[i]);
+  acc_flush(d, a);
+  fd_flush(d, f);
+}
+__global__ __launch_bounds__(64) void k_fd_api_getb(Dev d, uint32_t v, uint32_t limit, gx_fd_msg *out, uint32_t *n_out) {
+  FdAcc f;
+  if (threadIdx.x == 0) *n_out = fd_get_broadcasts(d, f, v, limit, out);
+  fd_flush(d, f);
+}
+__global__ __launch_bounds__(64) void k_fd_api_probe(Dev d, uint32_t v, uint32_t *out) {
+  FdAcc f;
+  if (threadIdx.x == 0) {
+    bool ack;
+    out[0] = fd_probe_host(d, f, v, &ack);
+    out[1] = ack;
+  }
+  fd_flush(d, f);
+}
+__global__ __launch_bounds__(64) void k_fd_api_timers(Dev d, uint32_t v) {
+  Acc a;
+  FdAcc f;
+  fd_timers_wave(d, a, f, v);
+  acc_flush(d, a);
+  fd_flush(d, f);
+}

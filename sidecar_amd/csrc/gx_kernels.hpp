@@ -167,6 +167,10 @@ __global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
     d.in_cnt[idx] = 0;
     d.in_cur[idx] = 0;
     if (idx == 0) d.in_cnt[d.Hl] = 0;
+    if (departed(d, o)) {  // a crashed host runs no loopers
+      d.tick[idx] = 0;
+      goto done;
+    }
     wake_host(d, a, o);
     gx_host_state *h = &d.hs[idx];
     if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
@@ -199,6 +203,7 @@ __global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
     }
     d.tick[idx] = (!(h->flags & 2u) && h->bt_next <= d.round) ? 1 : 0;
   }
+done:
   acc_flush(d, a);
 }
 
@@ -353,6 +358,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   __shared__ uint32_t s_ebase[STORM_TILE];
   __shared__ unsigned long long s_wave[4];
   uint32_t vi = blockIdx.x, v = d.lo + vi;
+  if (departed(d, v)) return;  // uniform per block
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
@@ -468,6 +474,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   __shared__ uint32_t s_cnt[2][8];
   __shared__ uint32_t s_ecnt[2][8];
   uint32_t vi = blockIdx.x, v = d.lo + vi;
+  if (departed(d, v)) return;  // uniform per block
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
@@ -642,34 +649,59 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 
 // A team of T lanes per host: GetBroadcasts once per sampled peer, in order
 // (get_broadcasts_team). Each packet is counted into its receiver's CSR bucket.
-template <int T>
+// X (failure detector or departures): the targets are memberlist's (k_fd_send took their
+// memberlist messages first and, in byte mode, the delegate gets the bytes left; the round stops
+// at a packet that would be empty), and a packet to an unreachable peer is lost after
+// GetBroadcasts took its records.
+template <int T, bool X>
 __global__ __launch_bounds__(256) void k_send(Dev d) {
   Acc a;
   uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T, lane = threadIdx.x & (T - 1);
+  unsigned lost = 0;
   if (idx < d.Hl) {
     uint32_t u = d.lo + idx;
-    uint32_t peers[16];
-    uint32_t np = sample_peers(d, u, peers);
     uint32_t cap = d.p.packet_cap;
     for (uint32_t j = lane; j < d.K; j += T) {
       d.msg_len[(size_t)idx * d.K + j] = 0;
       d.msg_key[(size_t)idx * d.K + j] = u * d.K + j;
     }
-    gx_host_state *h = &d.hs[idx];
-    gx_host_state hs = *h;
-    for (uint32_t j = 0; j < np; j++) {
-      uint32_t l = get_broadcasts_team<T>(d, a, u, hs, cap, &d.msg[((size_t)idx * d.K + j) * cap], d.p.limit_bytes,
-                                       d.p.overhead_bytes);
-      if (lane == 0) {
-        d.msg_len[(size_t)idx * d.K + j] = l;
-        d.msg_dst[(size_t)idx * d.K + j] = peers[j];
-        if (l && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
+    if (!X || !departed(d, u)) {
+      const bool fd = X && d.p.fd_enable;
+      uint32_t peers[16];
+      uint32_t np;
+      if (fd) {
+        np = d.fd_np[idx];
+        for (uint32_t j = 0; j < np; j++) peers[j] = d.fd_peers[(size_t)idx * d.K + j];
+      } else {
+        np = sample_peers(d, u, peers);
       }
-      if (l == 0 && d.p.gossip_stop_on_empty) break;
+      gx_host_state *h = &d.hs[idx];
+      gx_host_state hs = *h;
+      for (uint32_t j = 0; j < np; j++) {
+        const size_t x = (size_t)idx * d.K + j;
+        uint32_t nf = fd ? d.fd_len[x] : 0, lim = d.p.limit_bytes, l = 0;
+        bool call = true;
+        if (fd && lim) {
+          uint32_t used = nf * (d.p.fd_msg_bytes + 2);
+          lim = lim > used ? lim - used : 0;
+          call = lim > d.p.overhead_bytes;
+        }
+        if (call) l = get_broadcasts_team<T>(d, a, u, hs, cap, &d.msg[x * cap], lim, d.p.overhead_bytes);
+        if (lane == 0) {
+          bool live = l || nf, ok = !X || reach(d, u, peers[j]);
+          d.msg_len[x] = ok ? l : 0;
+          if (fd && !ok) d.fd_len[x] = 0;
+          lost += live && !ok;
+          d.msg_dst[x] = peers[j];
+          if (live && ok && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
+        }
+        if (l == 0 && nf == 0 && d.p.gossip_stop_on_empty) break;
+      }
+      if (lane == 0) *h = hs;
     }
-    if (lane == 0) *h = hs;
   }
   acc_flush(d, a);
+  if (X && lost) ctr_atomic(d, C_LOST, lost);
 }
 
 // ====================================================== phase 3b: receiver CSR, sender-ordered ==
@@ -714,7 +746,8 @@ __global__ __launch_bounds__(1024) void k_route_offsets(Dev d) {
 // Entries: [0, Hl*K) packets of this shard's senders, then n_remote packets from other shards.
 __global__ void k_route_fill(Dev d) {
   uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.Hl * d.K + d.n_remote || d.msg_len[e] == 0) return;
+  if (e >= d.Hl * d.K + d.n_remote) return;
+  if (d.msg_len[e] == 0 && !(d.p.fd_enable && d.fd_len[e])) return;  // memberlist-only packets count
   uint32_t dst = d.msg_dst[e] - d.lo;
   if (dst >= d.Hl) return;  // bound for another shard (outbox)
   uint32_t pos = atomicAdd(&d.in_cur[dst], 1u);
@@ -1300,7 +1333,7 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
   __shared__ unsigned long long s_red[4];
   uint32_t t = blockIdx.x, base = 0, m = d.H, q = t;
   uint64_t key = key0;
-  if (d.partitioned) {
+  if (d.pair_split) {
     uint32_t m0 = d.H / 2, np0 = m0 / 2;
     if (t < np0) {
       m = m0;
@@ -1313,6 +1346,13 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
   }
   uint32_t a = base + feistel_perm(key, 2 * q, m);
   uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
+  // a crashed member skips the pair; with the failure detector the network path is needed and
+  // the initiator (a) must see b ALIVE (memberlist pushPull picks among alive nodes)
+  if (d.departures || d.p.fd_enable) {
+    bool ok = !departed(d, a) && !departed(d, b);
+    if (ok && d.p.fd_enable) ok = reach(d, a, b) && d.mem[(size_t)a * d.H + b].state == GX_M_ALIVE;
+    if (!ok) return;
+  }
   ae_pair<VEC, PF, NT, EV>(d, a, b, true, s_wave, s_red);
 }
 
@@ -1525,6 +1565,7 @@ __global__ void k_view_minmax(Dev d, uint64_t *mn, uint64_t *mx) {
   if (r >= d.R) return;
   uint64_t a = ~0ull, b = 0;
   for (uint32_t v = 0; v < d.Hl; v++) {
+    if (departed(d, d.lo + v)) continue;  // a crashed host's view is frozen and left out
     uint64_t w = d.view[(size_t)v * d.R + r];
     a = w < a ? w : a;
     b = w > b ? w : b;
@@ -1537,10 +1578,12 @@ __global__ void k_view_minmax(Dev d, uint64_t *mn, uint64_t *mx) {
 __global__ void k_converged(Dev d, unsigned long long *bad) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   bool dis = false;
-  if (r < d.R) {
-    uint64_t w0 = d.view[r];
-    for (uint32_t v = 1; v < d.Hl; v++)
-      if (d.view[(size_t)v * d.R + r] != w0) {
+  if (r < d.R) {  // the live views must agree; crashed hosts' views are left out
+    uint32_t v0 = 0;
+    while (v0 < d.Hl && departed(d, d.lo + v0)) v0++;
+    uint64_t w0 = v0 < d.Hl ? d.view[(size_t)v0 * d.R + r] : 0;
+    for (uint32_t v = v0 + 1; v < d.Hl; v++)
+      if (!departed(d, d.lo + v) && d.view[(size_t)v * d.R + r] != w0) {
         dis = true;
         break;
       }

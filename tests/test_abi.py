@@ -25,7 +25,7 @@ def test_libgx_exports_every_symbol():
     lib = load_library(LIBGX_PATH)
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.gx_abi_version() == 1
+    assert lib.gx_abi_version() == 2
     assert lib.gx_backend().decode() == "hip-gfx950"
 
 
@@ -42,4 +42,34 @@ def test_params_default_identical(oracle_lib):
     a = default_params(oracle_lib)
     b = default_params(load_library(LIBGX_PATH))
     for f, _ in a._fields_:
-        assert getattr(a, f) == getattr(b, f), f
+        x, y = getattr(a, f), getattr(b, f)
+        if hasattr(x, "_length_"):  # ctypes array
+            x, y = list(x), list(y)
+        assert x == y, f
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 9, 10, 63, 64, 99, 100, 999, 1000, 4096, 16384, 32768, 65534])
+def test_fd_defaults_identical(oracle_lib, n):
+    """memberlist's size-derived parameters (retransmitLimit, Lifeguard suspicion timeouts) agree
+    between the product and the oracle, and follow util.go / suspicion.go."""
+    import ctypes as C
+    import math
+    from sidecar_amd.abi import GxParams
+    if not os.path.exists(LIBGX_PATH):
+        pytest.skip("libgx not built")
+    got = []
+    for lib in (oracle_lib, load_library(LIBGX_PATH)):
+        p = GxParams()
+        lib.gx_params_default(C.byref(p))
+        p.n_hosts = n
+        assert lib.gx_fd_defaults(C.byref(p)) == 0
+        got.append((p.fd_retransmit_limit, p.fd_suspicion_k, list(p.fd_suspicion_rounds)))
+    assert got[0] == got[1]
+    limit, k, rounds = got[0]
+    assert limit == min(32, 4 * math.ceil(math.log10(n + 1)))
+    assert k == (0 if n - 2 < 2 else 2)
+    tmin_ms = 4 * int(max(1.0, math.log10(max(1, n))) * 1000) * 1000 // 1000  # ProbeInterval 1 s
+    assert rounds[0] == math.ceil((tmin_ms if k < 1 else 6 * tmin_ms) / 200)
+    if k:
+        assert rounds[k] == math.ceil(tmin_ms / 200)  # k confirmations: the minimum
+        assert rounds[0] >= rounds[1] >= rounds[2]
