@@ -47,6 +47,20 @@ CONFIGS = {
     "cfg4": dict(desc="8192 hosts x 64 services, push-pull full-state merge every 10 rounds",
                  p=dict(n_hosts=8192, n_services=64, fanout=3, queue_cap=4096, init_mode=1,
                         ae_period_rounds=10)),
+    # cfg 5 driven by memberlist's failure detector instead of the scripted storm:
+    # the partition drops packets, SWIM probes suspect the other half, Lifeguard timers decide
+    # (for a 10 s partition at this size they do not expire: refutations win after the heal)
+    "cfg5fd": dict(desc="cfg5 with memberlist failure detection: 32768 hosts x 16 services, 2-way network "
+                        "partition rounds [0,50), SWIM probes + Lifeguard suspicion, NotifyLeave -> "
+                        "ExpireServer, push-pull every 10 rounds",
+                   p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
+                          queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                          partition_end=50, ae_period_rounds=10, fd_enable=1)),
+    # host crashes detected by the failure detector: 2% of 16384 hosts crash at round 5
+    "fd_depart": dict(desc="16384 hosts x 16 services, 2% of hosts crash at round 5, memberlist failure "
+                           "detection (SWIM + Lifeguard) -> NotifyLeave -> ExpireServer, push-pull every 10 rounds",
+                      p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2,
+                             ae_period_rounds=10, fd_enable=1, depart_round=5, depart_ppm=20000)),
     # small plumbing case (configs[0]); also the CPU-baseline scale model
     "cfg1": dict(desc="64 hosts x 8 services, fanout 3", p=dict(n_hosts=64, n_services=8, fanout=3,
                                                                 queue_cap=4096, init_mode=0)),
@@ -97,7 +111,14 @@ class Cluster:
         return self.e.stats() if self.shard is None else self.shard.stats()
 
     def converged(self):
-        return self.e.converged() if self.shard is None else self.shard.converged()
+        if self.shard is not None:
+            return self.shard.converged()
+        ok, n = self.e.converged()
+        if ok and self.e.params.fd_enable:
+            # with the failure detector, converged also means every live host sees the truth:
+            # crashed hosts dead, live hosts alive (no pending suspicion, no false death)
+            ok, n = self.e.fd_converged()
+        return ok, n
 
     def exchange_bytes(self):
         """Bytes moved between GPUs by the whole job (summed over ranks); None at N = 1."""
@@ -131,6 +152,8 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
             if ok:
                 lc = c.stats()["last_change_round"]
                 conv = lc + 1  # the catalog stopped changing after round lc and agrees
+                if CONFIGS[cfg]["p"].get("fd_enable"):
+                    conv = max(conv, c.round)  # membership agreement is known at check granularity
                 # wall to convergence: the rounds past the convergence point are excluded pro rata
                 wall = wall * conv / c.round if c.round else wall
                 break
@@ -157,7 +180,7 @@ def _oracle_rate(lib, cfg, h_sample, warmup, steps):
     return m / dt, dt, p
 
 
-def cpu_baseline(cfg, warmup, steps, h_mt=8192, h_single=2048):
+def cpu_baseline(cfg, warmup, steps, h_mt=16384, h_single=4096):
     """The CPU oracle on a bounded sample of the same workload: the bench's round window of cfg's
     schedule with H scaled down (about 10 s each). The multi-threaded build (per-host phase loops
     on every core this process may use, OpenMP) is the reported baseline; the serial build (the
@@ -189,7 +212,7 @@ def main():
     ap.add_argument("--converge-max", type=int, default=3000)
     ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-hosts", type=int, default=8192, help="H of the multi-threaded CPU sample")
+    ap.add_argument("--cpu-hosts", type=int, default=16384, help="H of the multi-threaded CPU sample")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     args = ap.parse_args()
 
@@ -287,6 +310,9 @@ def main():
             "merges": split, "converge": conv, "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
             "exchange": xfer,
         }
+        if cfgp.get("fd_enable") or cfgp.get("depart_ppm"):
+            out["failure_detection"] = {k: st1[k] - st0[k] for k in st1 if k.startswith("fd_") or k in (
+                "lost_packets", "expire_server")}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

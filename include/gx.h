@@ -541,6 +541,9 @@ int gx_fd_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_fd_msg 
 int gx_fd_probe(gx_engine *e, uint32_t host, uint32_t *target, int *acked);
 /* Suspicion timers of the host due at the current round -> deadNode, in node order. */
 int gx_fd_timers(gx_engine *e, uint32_t host);
+/* Membership agreement with the truth: n_disagree = nodes that some live host sees otherwise
+ * than they are (a crashed node not DEAD, a live node not ALIVE); converged iff 0. */
+int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */
 int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);

@@ -470,3 +470,18 @@ int gx_fd_timers(gx_engine *e, uint32_t host) {
   fd_timers_host(e, host, now_of(e));
   return GX_OK;
 }
+int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
+  if (!e || !e->p.fd_enable) return GX_EINVAL;
+  uint64_t bad = 0;
+  for (uint32_t m = 0; m < e->H; m++) {
+    int want = departed(e, m) ? GX_M_DEAD : GX_M_ALIVE;
+    for (uint32_t v = 0; v < e->H; v++)
+      if (!departed(e, v) && MEM(e, v, m)->state != want) {
+        bad++;
+        break;
+      }
+  }
+  if (converged) *converged = bad == 0;
+  if (n_disagree) *n_disagree = bad;
+  return GX_OK;
+}

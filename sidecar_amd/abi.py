@@ -198,7 +198,7 @@ ABI_FUNCS = [
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
     "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
-    "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers",
+    "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers", "gx_fd_converged",
 ]
 
 
@@ -264,6 +264,7 @@ def _declare(lib):
         "gx_fd_get_broadcasts": ([vp, u32, u32, P(GxFdMsg), P(u32)], i32),
         "gx_fd_probe": ([vp, u32, P(u32), P(i32)], i32),
         "gx_fd_timers": ([vp, u32], i32),
+        "gx_fd_converged": ([vp, P(i32), P(C.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -721,6 +722,12 @@ class Engine:
 
     def fd_timers(self, host: int):
         check(self.lib.gx_fd_timers(self.h, host), "gx_fd_timers")
+
+    def fd_converged(self):
+        c = C.c_int()
+        n = C.c_uint64()
+        check(self.lib.gx_fd_converged(self.h, C.byref(c), C.byref(n)), "gx_fd_converged")
+        return bool(c.value), n.value
 
     def converged(self):
         c = C.c_int()

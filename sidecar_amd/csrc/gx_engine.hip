@@ -1645,6 +1645,21 @@ int gx_fd_timers(gx_engine *e, uint32_t host) {
   return sync_check(e);
 }
 
+int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
+  if (!e || !e->d.p.fd_enable) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  set_round_fields(e);
+  HIPCHK(hipMemsetAsync(e->conv_bad, 0, sizeof(unsigned long long), e->stream));
+  k_fd_converged<<<nblk(e->d.H, 256), 256, 0, e->stream>>>(e->d, e->conv_bad);
+  unsigned long long bad = 0;
+  HIPCHK(hipMemcpyAsync(&bad, e->conv_bad, sizeof(bad), hipMemcpyDeviceToHost, e->stream));
+  int rc = sync_check(e);
+  if (rc) return rc;
+  if (converged) *converged = bad == 0;
+  if (n_disagree) *n_disagree = bad;
+  return GX_OK;
+}
+
 int gx_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   if (!e || e->d.G > 1) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));

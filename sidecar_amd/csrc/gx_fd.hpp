@@ -437,3 +437,17 @@ __global__ __launch_bounds__(64) void k_fd_api_timers(Dev d, uint32_t v) {
   acc_flush(d, a);
   fd_flush(d, f);
 }
+
+// Membership agreement with the truth (gx_fd_converged): one thread per node m reads column m of
+// the member lists (adjacent threads, adjacent nodes: coalesced rows).
+__global__ void k_fd_converged(Dev d, unsigned long long *bad) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  bool dis = false;
+  if (m < d.H) {
+    const uint8_t want = departed(d, m) ? GX_M_DEAD : GX_M_ALIVE;
+    for (uint32_t v = 0; v < d.H && !dis; v++)
+      dis = !departed(d, v) && memp(d, v, m)->state != want;
+  }
+  unsigned long long c = wave_sum(dis ? 1ull : 0ull);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}

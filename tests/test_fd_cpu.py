@@ -38,7 +38,7 @@ def test_departures_detected_and_expired(oracle_lib):
     st = e.stats()
     assert st["fd_deaths"] == len(live) * len(gone)
     assert st["lost_packets"] > 0 and st["fd_refutes"] == 0
-    assert e.converged() == (True, 0)
+    assert e.converged() == (True, 0) and e.fd_converged() == (True, 0)
 
 
 def test_no_failures_no_suspicions(oracle_lib):
@@ -65,6 +65,7 @@ def test_long_partition_splits_membership(oracle_lib):
     st = e.stats()
     assert st["fd_deaths"] == 2 * half * (H - half)
     assert not e.converged()[0]
+    assert e.fd_converged() == (False, H)  # every node is dead to the other half
 
 
 def test_short_partition_recovers(oracle_lib):

@@ -32,6 +32,8 @@ def compare(gx_lib, oracle_lib, kw, rounds, chunks=(1, 6, 33, 60)):
         if kw.get("fd_enable"):
             assert_same_fd(g, o, f"round {g.round}")
     assert g.converged() == o.converged()
+    if kw.get("fd_enable"):
+        assert g.fd_converged() == o.fd_converged()
     g.close()
     o.close()
 
