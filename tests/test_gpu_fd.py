@@ -84,3 +84,25 @@ def test_gpu_fd_api_fuzz(gx_lib, oracle_lib):
         if step % 50 == 49:
             assert_same(g, o, f"step {step}")
             assert_same_fd(g, o, f"step {step}")
+
+
+def test_gpu_fd_with_listeners(gx_lib, oracle_lib):
+    """ChangeEvents of NotifyLeave -> ExpireServer reach buffered listeners identically (the
+    event-logging kernel variants run while a listener exists)."""
+    kw = dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, fd_enable=1, depart_round=3, depart_ppm=100_000,
+              ae_period_rounds=10, queue_cap=4096)
+    g = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    o = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    for e in (g, o):
+        e.add_listener(0, 1, 16)
+        e.add_listener(17, 2, 4096)
+    for n in (40, 60, 80):
+        g.run_rounds(n)
+        o.run_rounds(n)
+        for view, lid in ((0, 1), (17, 2)):
+            a = [x.tup() for x in g.drain_listener(view, lid)]
+            b = [x.tup() for x in o.drain_listener(view, lid)]
+            assert a == b, f"round {g.round}: listener {lid} of view {view} differs"
+        assert_same(g, o, f"round {g.round}")
+        assert_same_fd(g, o, f"round {g.round}")
+    assert g.stats()["listener_drops"] > 0  # the 16-event channel overflowed during the deaths
