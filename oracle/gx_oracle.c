@@ -890,7 +890,7 @@ static void ae_cross_build(gx_engine *e) {
     if (g == e->gid) continue;
     for (uint32_t t = 0; t < np; t++) {
       int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
-      if (la == lb) continue;
+      if (la == lb || !ae_pair_ok(e, pa[t], pb[t])) continue;
       uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
       if (shard_of(e, other) != g) continue;
       e->x_t[e->x_n] = t;
@@ -984,8 +984,7 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
-  /* departures and the failure detector run on an unsharded engine */
-  if (p->depart_round >= 0 && p->depart_ppm && p->n_shards > 1) return GX_EINVAL;
+  /* the failure detector runs on an unsharded engine */
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->n_shards > 1 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1156,7 +1155,8 @@ int gx_set_round(gx_engine *e, int64_t round) {
   if (!e || round < e->round) return GX_EINVAL;
   e->round = round;
   e->st.round = round;
-  for (uint32_t v = 0; v < e->H; v++) wake_host(e, v);
+  for (uint32_t v = 0; v < e->H; v++)
+    if (!departed(e, v)) wake_host(e, v); /* a crashed host stays frozen */
   return GX_OK;
 }
 int gx_get_round(gx_engine *e, int64_t *round) {

@@ -401,8 +401,7 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
-  // departures and the failure detector run on an unsharded engine
-  if (p->depart_round >= 0 && p->depart_ppm && p->n_shards > 1) return GX_EINVAL;
+  // the failure detector runs on an unsharded engine
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->n_shards > 1 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1245,6 +1244,11 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
       pb.push_back(base + feistel_perm(key, t + 1, m));
     }
   }
+  // a pair with a crashed member does not run (both shards skip it alike; pair indices unchanged)
+  std::vector<uint8_t> runs(pa.size(), 1);
+  if (d.departures)
+    for (size_t t = 0; t < pa.size(); t++)
+      runs[t] = !departed_at(d.p, d.round, pa[t]) && !departed_at(d.p, d.round, pb[t]);
   std::vector<uint32_t> plan_a, plan_b, pack_host, pack_t;
   std::vector<int32_t> plan_row;
   std::vector<uint8_t> plan_cnt;
@@ -1255,7 +1259,7 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
     if (g == d.gid) continue;
     for (size_t t = 0; t < pa.size(); t++) {
       bool la = own(e, pa[t]), lb = own(e, pb[t]);
-      if (la == lb) continue;
+      if (la == lb || !runs[t]) continue;
       uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
       if (shard_of(d, other) != g) continue;
       pack_host.push_back(mine);
@@ -1271,7 +1275,7 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
     if (g == d.gid) continue;
     for (size_t t = 0; t < pa.size(); t++) {
       bool la = own(e, pa[t]), lb = own(e, pb[t]);
-      if (la == lb) continue;
+      if (la == lb || !runs[t]) continue;
       uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
       if (shard_of(d, other) != g) continue;
       plan_a.push_back(mine);
@@ -1281,7 +1285,7 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
     }
   }
   for (size_t t = 0; t < pa.size(); t++)
-    if (own(e, pa[t]) && own(e, pb[t])) {
+    if (own(e, pa[t]) && own(e, pb[t]) && runs[t]) {
       plan_a.push_back(pa[t]);
       plan_b.push_back(pb[t]);
       plan_row.push_back(-1);

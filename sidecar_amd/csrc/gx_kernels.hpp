@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_minexp_recompute(Dev d, uint32_t lo_idx
 __global__ void k_wake(Dev d) {
   Acc a;
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < d.Hl) wake_host(d, a, d.lo + idx);
+  if (idx < d.Hl && !departed(d, d.lo + idx)) wake_host(d, a, d.lo + idx);  // a crashed host stays frozen
   acc_flush(d, a);
 }
 

@@ -84,8 +84,6 @@ def test_fd_param_checks(oracle_lib):
         kw = dict(base, **bad)
         with pytest.raises(GxError, match=f"rc={GX_EINVAL}"):
             Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
-    with pytest.raises(GxError, match=f"rc={GX_EINVAL}"):  # departures need an unsharded engine
-        Engine(default_params(oracle_lib, n_hosts=64, depart_round=3, depart_ppm=10, n_shards=2), lib=oracle_lib)
     e = Engine(default_params(oracle_lib, n_hosts=16), lib=oracle_lib)  # fd off: no fd state
     with pytest.raises(GxError):
         e.fd_members(0)

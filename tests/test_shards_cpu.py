@@ -24,6 +24,9 @@ SCEN = {
                     partition_end=12, storm_round=3, churn_ppm=30000, queue_cap=4096),
     "blocks_ragged": dict(n_hosts=70, n_services=11, init_mode=1, ae_period_rounds=4, ae_phase=1,
                           churn_ppm=80000, aged_ppm=50000, queue_cap=1024),
+    # host crashes: lost packets across shards, push-pull pairs with a crashed member skipped
+    "departures": dict(n_hosts=60, n_services=8, init_mode=2, ae_period_rounds=5, partition_start=0,
+                       partition_end=12, storm_round=3, depart_round=4, depart_ppm=150000, queue_cap=2048),
 }
 
 
