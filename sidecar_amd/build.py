@@ -1,4 +1,5 @@
 """Builds the HIP engine in-tree: sidecar_amd/libgx.so for gfx950 (hipcc, no JIT cache)."""
+import glob
 import os
 import subprocess
 import sys
@@ -6,9 +7,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = [os.path.join(HERE, "csrc", "gx_engine.hip")]
-DEPS = SRC + [os.path.join(HERE, "csrc", "gx_device.hpp"), os.path.join(HERE, "csrc", "gx_kernels.hpp"),
-              os.path.join(HERE, "csrc", "gx_codec.hpp"), os.path.join(HERE, "csrc", "gx_codec_host.hpp"),
-              os.path.join(ROOT, "include", "gx.h")]
+DEPS = SRC + sorted(glob.glob(os.path.join(HERE, "csrc", "*.hpp"))) + [os.path.join(ROOT, "include", "gx.h")]
 OUT = os.path.join(HERE, "libgx.so")
 ARCH = os.environ.get("GX_OFFLOAD_ARCH", "gfx950")
 
