@@ -75,3 +75,55 @@ def test_cfg5_properties_and_determinism(gx_lib):
     assert ok, bad
     mn, mx = _minmax(e)
     assert np.array_equal(mn, mx)
+
+
+CFG4 = dict(n_hosts=8192, n_services=64, fanout=3, queue_cap=4096, init_mode=1, ae_period_rounds=10)
+FD_DEPART = dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2, ae_period_rounds=10,
+                 fd_enable=1, depart_round=5, depart_ppm=20000)
+
+
+def _omp_oracle():
+    # the OpenMP build of the oracle: bit-identical to the serial checker (tests/test_oracle_omp.py,
+    # tests/test_fd_cpu.py), fast enough for the full-size push-pull rounds
+    from tests.oracle_lib import load_oracle
+    return load_oracle(omp=True)
+
+
+def _slabs_equal(g, o, step):
+    for lo in range(0, g.H, step):
+        hi = min(g.H, lo + step)
+        assert np.array_equal(g.read_views(lo, hi), o.read_views(lo, hi)), lo
+
+
+def test_cfg4_full_parity(gx_lib):
+    """cfg 4 (8192 x 64, push-pull full-state merges every 10 rounds) against the oracle, bit for
+    bit, over two push-pull rounds (rounds 0 and 10): 8.6e9 record-merges."""
+    orc = _omp_oracle()
+    g = Engine(default_params(gx_lib, **CFG4), lib=gx_lib)
+    o = Engine(default_params(orc, **CFG4), lib=orc)
+    g.run_rounds(11)
+    o.run_rounds(11)
+    assert g.stats() == o.stats()
+    assert g.stats()["ae_exchanges"] == 2 * (8192 // 2)
+    assert np.array_equal(g.digests(), o.digests())
+    _slabs_equal(g, o, 1024)
+
+
+def test_fd_depart_full_parity(gx_lib):
+    """The failure detector at cfg 3's size (16384 x 16, 2% of hosts crash at round 5) against the
+    oracle, bit for bit, for 25 rounds: catalog views, counters, queue digests, every host's probe
+    and queue state, and the member lists of 64 hosts."""
+    from tests.fd_parity import assert_same_fd  # noqa: F401  (full tables are 8.6 GB: sampled below)
+    orc = _omp_oracle()
+    g = Engine(default_params(gx_lib, **FD_DEPART), lib=gx_lib)
+    o = Engine(default_params(orc, **FD_DEPART), lib=orc)
+    g.run_rounds(25)
+    o.run_rounds(25)
+    sg, so = g.stats(), o.stats()
+    assert sg == so
+    assert sg["fd_probe_failures"] > 0 and sg["fd_suspicions"] > 0
+    assert np.array_equal(g.digests(), o.digests())
+    assert [bytes(h) for h in g.fd_hosts()] == [bytes(h) for h in o.fd_hosts()]
+    for v in np.linspace(0, 16383, 64).astype(int):
+        assert g.fd_members(int(v)) == o.fd_members(int(v)), v
+    _slabs_equal(g, o, 4096)
