@@ -262,11 +262,17 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
  * torch.distributed: RCCL between GPUs, gloo for the CPU oracle). Exchange buffers are device
  * memory for the HIP engine and host memory for the oracle; `bytes_per_shard` has n_shards
  * entries. Wire formats (both little-endian):
- *   packet: u32 key (= sender * fanout + j), u32 receiver, u32 len, u32 0, then len x {u64 word,
- *           u32 record key, u32 0}; packets grouped by destination shard, ascending key.
- *   digest: u32 pair index, u32 host, u32 n_blocks, u32 0, then n_blocks x {u64 d0, u64 d1}: the
+ *   packet: u32 key (= sender * fanout + j), u32 receiver, u32 len, u32 n_fd, then packet_cap x
+ *           {u64 word, u32 record key, u32 0} (the first len used); with fd_enable then fd_msg_cap x
+ *           {u32 incarnation, u32 node | from << 16, u32 kind, u32 0} (the first n_fd used, the
+ *           packet's memberlist messages); fixed-size slots grouped by destination shard, ascending
+ *           key.
+ *   digest: u32 pair index, u32 host, u32 n_blocks, u32 runs, then n_blocks x {u64 d0, u64 d1}: the
  *           host's round-start row in blocks of GX_DIGEST_SLOTS slots (GX digest below); one
  *           message per cross-shard push-pull pair, grouped by destination shard, ascending pair.
+ *           `runs` (fd_enable only, else 0): 1 if the sender holds the pair's initiator (first
+ *           host) and the pair runs (path up, partner ALIVE in the initiator's list); the other
+ *           side follows it, and a pair that does not run ships no blocks.
  *   delta:  u32 pair index, u32 host, u32 n_sent, u32 0, then n_sent x GX_DIGEST_SLOTS u64 words:
  *           the row's blocks whose digests differ from the partner's, ascending (the last block
  *           of a row zero-padded); grouped like the digests.
@@ -481,8 +487,8 @@ int gx_merge_remote_state_json(gx_engine *e, uint32_t view, const char *buf, uin
  * Each host keeps a member list over all H hosts (gx_member per (host, node)) and a broadcast
  * queue of memberlist messages: at most one queued message per node (a newer one invalidates
  * it), sent fewest-transmits first and newest first among equal counts, each sent
- * fd_retransmit_limit times. Host ids are 16-bit here: fd_enable requires n_hosts <= 65534 and
- * an unsharded engine. */
+ * fd_retransmit_limit times. Host ids are 16-bit here: fd_enable requires n_hosts <= 65534. On a
+ * sharded engine the per-host calls below take this shard's hosts. */
 #define GX_M_ALIVE 0
 #define GX_M_SUSPECT 1
 #define GX_M_DEAD 2
@@ -541,8 +547,9 @@ int gx_fd_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_fd_msg 
 int gx_fd_probe(gx_engine *e, uint32_t host, uint32_t *target, int *acked);
 /* Suspicion timers of the host due at the current round -> deadNode, in node order. */
 int gx_fd_timers(gx_engine *e, uint32_t host);
-/* Membership agreement with the truth: n_disagree = nodes that some live host sees otherwise
- * than they are (a crashed node not DEAD, a live node not ALIVE); converged iff 0. */
+/* Membership agreement with the truth: n_disagree = nodes that some live host of this engine sees
+ * otherwise than they are (a crashed node not DEAD, a live node not ALIVE); converged iff 0 (on
+ * every shard). */
 int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */

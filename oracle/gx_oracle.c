@@ -41,6 +41,7 @@ struct gx_engine {
   uint32_t x_n, nblk;
   uint32_t *x_t, *x_mine;
   uint8_t *x_first;     /* this side holds the pair's first member (counts the exchange) */
+  uint8_t *x_run;       /* the pair runs (failure detector: the initiator's decision, digest word 3) */
   uint64_t *x_dig;      /* [x_n][nblk][2] own digests */
   uint8_t *x_diff;      /* [x_n][nblk] 1 = the partner's digest differs */
   uint32_t *x_cnt;
@@ -763,7 +764,10 @@ static void round_send(gx_engine *e) {
   if (e->p.storm_round >= 0 && e->round == e->p.storm_round) for_hosts(e, n, ph_storm, &now);
   if (e->p.fd_enable) for_hosts(e, n, ph_fd_tick, &now);
   for (size_t i = 0; i < (size_t)e->H * e->K; i++) e->msg_len[i] = 0;
-  if (e->p.fd_enable) for_hosts(e, n, ph_fd_send, NULL);
+  if (e->p.fd_enable) {
+    memset(e->fd_len, 0, sizeof(uint32_t) * (size_t)e->H * (e->K ? e->K : 1));
+    for_hosts(e, n, ph_fd_send, NULL);
+  }
   for_hosts(e, n, ph_send, NULL);
 }
 
@@ -824,6 +828,24 @@ static uint32_t ae_pairs(const gx_engine *e, uint32_t *pa, uint32_t *pb) {
     }
   }
   return n;
+}
+
+/* Pair t of this round's push-pull matching (the t-th pair ae_pairs lists). */
+static void ae_pair_at(const gx_engine *e, uint32_t t, uint32_t *a, uint32_t *b) {
+  uint32_t base = 0, m = e->H, q = t;
+  if (partitioned(e) && !e->p.fd_enable) {
+    uint32_t m0 = e->H / 2, np0 = m0 / 2;
+    if (t < np0) {
+      m = m0;
+    } else {
+      base = m0;
+      m = e->H - m0;
+      q = t - np0;
+    }
+  }
+  uint64_t key = rng4(e->p.seed, ST_AE, (uint64_t)e->round, base, 0);
+  *a = base + feistel_perm(key, 2 * q, m);
+  *b = base + feistel_perm(key, 2 * q + 1, m);
 }
 
 /* x <- a remote host's row (one direction of a cross-shard push-pull pair). */
@@ -890,7 +912,7 @@ static void ae_cross_build(gx_engine *e) {
     if (g == e->gid) continue;
     for (uint32_t t = 0; t < np; t++) {
       int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
-      if (la == lb || !ae_pair_ok(e, pa[t], pb[t])) continue;
+      if (la == lb || departed(e, pa[t]) || departed(e, pb[t])) continue;  /* fd decision: digest flag */
       uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
       if (shard_of(e, other) != g) continue;
       e->x_t[e->x_n] = t;
@@ -984,9 +1006,8 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
-  /* the failure detector runs on an unsharded engine */
   if (p->fd_enable) {
-    if (p->n_hosts > 65534 || p->n_shards > 1 || p->fanout > 16) return GX_EINVAL;
+    if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
     if (p->fd_retransmit_limit < 1 || p->fd_retransmit_limit > GX_FD_MAX_TX || p->fd_suspicion_k > 2) return GX_EINVAL;
     for (uint32_t c = 0; c <= p->fd_suspicion_k; c++)
@@ -1081,10 +1102,11 @@ int gx_create(const gx_params *p, gx_engine **out) {
     e->x_t = (uint32_t *)calloc(hl, sizeof(uint32_t));
     e->x_mine = (uint32_t *)calloc(hl, sizeof(uint32_t));
     e->x_first = (uint8_t *)calloc(hl, 1);
+    e->x_run = (uint8_t *)calloc(hl, 1);
     e->x_dig = (uint64_t *)calloc(hl * e->nblk * 2, sizeof(uint64_t));
     e->x_diff = (uint8_t *)calloc(hl * e->nblk, 1);
     e->x_cnt = (uint32_t *)calloc(hl, sizeof(uint32_t));
-    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_dig || !e->x_diff || !e->x_cnt) {
+    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_run || !e->x_dig || !e->x_diff || !e->x_cnt) {
       gx_destroy(e);
       return GX_ENOMEM;
     }
@@ -1137,6 +1159,7 @@ int gx_destroy(gx_engine *e) {
   free(e->x_t);
   free(e->x_mine);
   free(e->x_first);
+  free(e->x_run);
   free(e->x_dig);
   free(e->x_diff);
   free(e->x_cnt);
@@ -1554,7 +1577,12 @@ int gx_host_digests(gx_engine *e, uint64_t *out) {
 }
 
 /* ---------------------------------------------------------------------- sharded rounds -- */
-static size_t slot_bytes(const gx_engine *e) { return 16 + 16ull * e->p.packet_cap; }
+/* packet slot (gx.h wire format): header, packet_cap records, then fd_msg_cap memberlist messages
+ * of 16 B {u32 incarnation, u16 node | u16 from << 16, u32 kind, u32 0} with the failure detector */
+static size_t slot_bytes(const gx_engine *e) {
+  return 16 + 16ull * e->p.packet_cap + (e->p.fd_enable ? 16ull * e->p.fd_msg_cap : 0);
+}
+static uint32_t fd_len_of(const gx_engine *e, size_t m) { return e->p.fd_enable ? e->fd_len[m] : 0; }
 
 int gx_round_send(gx_engine *e) {
   if (!e) return GX_EINVAL;
@@ -1565,7 +1593,7 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   if (!e || !bytes) return GX_EINVAL;
   for (uint32_t g = 0; g < e->G; g++) bytes[g] = 0;
   for (size_t m = (size_t)e->lo * e->K; m < (size_t)e->hi * e->K; m++)
-    if (e->msg_len[m] && !is_local(e, e->msg_dst[m])) bytes[shard_of(e, e->msg_dst[m])] += slot_bytes(e);
+    if ((e->msg_len[m] || fd_len_of(e, m)) && !is_local(e, e->msg_dst[m])) bytes[shard_of(e, e->msg_dst[m])] += slot_bytes(e);
   return GX_OK;
 }
 int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
@@ -1574,12 +1602,18 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   size_t off = 0, sb = slot_bytes(e);
   for (uint32_t g = 0; g < e->G; g++)
     for (size_t m = (size_t)e->lo * e->K; m < (size_t)e->hi * e->K; m++) {
-      if (!e->msg_len[m] || is_local(e, e->msg_dst[m]) || shard_of(e, e->msg_dst[m]) != g) continue;
+      if ((!e->msg_len[m] && !fd_len_of(e, m)) || is_local(e, e->msg_dst[m]) || shard_of(e, e->msg_dst[m]) != g) continue;
       if (off + sb > cap) return GX_EINVAL;
-      uint32_t hdr[4] = {(uint32_t)m, e->msg_dst[m], e->msg_len[m], 0};
+      uint32_t nfd = fd_len_of(e, m);
+      uint32_t hdr[4] = {(uint32_t)m, e->msg_dst[m], e->msg_len[m], nfd};
       memset(p + off, 0, sb);
       memcpy(p + off, hdr, 16);
       memcpy(p + off + 16, &e->msg[m * e->p.packet_cap], 16ull * e->msg_len[m]);
+      for (uint32_t y = 0; y < nfd; y++) {
+        const gx_fd_msg *g = &e->fdm[m * e->p.fd_msg_cap + y];
+        uint32_t w[4] = {g->incarnation, (uint32_t)g->node | ((uint32_t)g->from << 16), g->kind, 0};
+        memcpy(p + off + 16 + 16ull * e->p.packet_cap + 16ull * y, w, 16);
+      }
       off += sb;
     }
   return GX_OK;
@@ -1592,11 +1626,18 @@ int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
   for (size_t off = 0; off < bytes; off += sb) {
     uint32_t hdr[4];
     memcpy(hdr, p + off, 16);
-    uint32_t m = hdr[0], dst = hdr[1], len = hdr[2];
-    if (m >= e->H * e->K || !is_local(e, dst) || len > e->p.packet_cap) return GX_EINVAL;
+    uint32_t m = hdr[0], dst = hdr[1], len = hdr[2], nfd = e->p.fd_enable ? hdr[3] : 0;
+    if (m >= e->H * e->K || !is_local(e, dst) || len > e->p.packet_cap || nfd > e->p.fd_msg_cap) return GX_EINVAL;
     memcpy(&e->msg[(size_t)m * e->p.packet_cap], p + off + 16, 16ull * len);
     e->msg_len[m] = len;
     e->msg_dst[m] = dst;
+    for (uint32_t y = 0; y < nfd; y++) {
+      uint32_t w[4];
+      memcpy(w, p + off + 16 + 16ull * e->p.packet_cap + 16ull * y, 16);
+      gx_fd_msg g = {w[0], (uint16_t)(w[1] & 0xffffu), (uint16_t)(w[1] >> 16), (uint8_t)w[2], {0, 0, 0}};
+      e->fdm[(size_t)m * e->p.fd_msg_cap + y] = g;
+    }
+    if (e->p.fd_enable) e->fd_len[m] = nfd;
   }
   return GX_OK;
 }
@@ -1606,6 +1647,14 @@ int gx_round_merge(gx_engine *e) {
   return GX_OK;
 }
 static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk; }
+/* Failure detector: the initiator (this side's host `mine`, cross pair k) runs the pair when the
+ * path exists and it sees the partner alive (memberlist pushPull picks among alive nodes). */
+static int ae_initiator_runs(const gx_engine *e, uint32_t mine, uint32_t k) {
+  uint32_t pa_t, pb_t;
+  ae_pair_at(e, e->x_t[k], &pa_t, &pb_t);
+  uint32_t other = mine == pa_t ? pb_t : pa_t;
+  return reach(e, mine, other) && MEM(e, mine, other)->state == GX_M_ALIVE;
+}
 
 int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
   if (!e || !bytes) return GX_EINVAL;
@@ -1634,7 +1683,9 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   uint8_t *p = (uint8_t *)buf;
   for (uint32_t k = 0; k < e->x_n; k++) {
     uint8_t *m = p + (size_t)k * dig_bytes(e);
-    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->nblk, 0};
+    /* word 3: with the failure detector, the initiator's decision that the pair runs */
+    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->nblk,
+                       (uint32_t)(e->p.fd_enable && e->x_first[k] && ae_initiator_runs(e, e->x_mine[k], k))};
     memcpy(m, hdr, 16);
     const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
     for (uint32_t b = 0; b < e->nblk; b++) {
@@ -1662,12 +1713,14 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
     uint32_t hdr[4];
     memcpy(hdr, m, 16);
     if (hdr[0] != e->x_t[k] || hdr[2] != e->nblk) rc = GX_EINVAL;
+    e->x_run[k] = (uint8_t)(!e->p.fd_enable ||
+                            (e->x_first[k] ? ae_initiator_runs(e, e->x_mine[k], k) : (hdr[3] & 1u) != 0));
     uint32_t n = 0;
     for (uint32_t b = 0; b < e->nblk; b++) {
       uint64_t theirs[2];
       memcpy(theirs, m + 16 + 16ull * b, 16);
       const uint64_t *mine = &e->x_dig[((size_t)k * e->nblk + b) * 2];
-      uint8_t differ = theirs[0] != mine[0] || theirs[1] != mine[1];
+      uint8_t differ = e->x_run[k] && (theirs[0] != mine[0] || theirs[1] != mine[1]);
       e->x_diff[(size_t)k * e->nblk + b] = differ;
       n += differ;
     }
@@ -1718,6 +1771,7 @@ int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
       uint32_t hdr[4];
       memcpy(hdr, p, 16);
       p += 16;
+      if (!e->x_run[k]) continue; /* the pair does not run: its delta holds no blocks */
       const uint64_t *own = &e->view[(size_t)e->x_mine[k] * e->R];
       for (uint32_t b = 0; b < e->nblk; b++) {
         uint32_t lo = b * GX_DIGEST_SLOTS, n = lo + GX_DIGEST_SLOTS < e->R ? GX_DIGEST_SLOTS : e->R - lo;

@@ -410,7 +410,7 @@ static void fd_init(gx_engine *e) {
 }
 
 /* ------------------------------------------------------------------------------ ABI ------ */
-static int fd_host_ok(const gx_engine *e, uint32_t host) { return e && e->p.fd_enable && host < e->H; }
+static int fd_host_ok(const gx_engine *e, uint32_t host) { return e && e->p.fd_enable && host < e->H && is_local(e, host); }
 
 int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t lo, uint32_t hi, gx_member *out) {
   if (!fd_host_ok(e, host) || lo > hi || hi > e->H || (!out && hi > lo)) return GX_EINVAL;
@@ -418,7 +418,8 @@ int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t lo, uint32_t hi, gx
   return GX_OK;
 }
 int gx_fd_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_fd_host *out) {
-  if (!e || !e->p.fd_enable || lo > hi || hi > e->H || (!out && hi > lo)) return GX_EINVAL;
+  if (!e || !e->p.fd_enable || lo > hi || (hi > lo && (!is_local(e, lo) || !is_local(e, hi - 1))) || (!out && hi > lo))
+    return GX_EINVAL;
   for (uint32_t v = lo; v < hi; v++) {
     out[v - lo] = e->fdh[v];
     out[v - lo].departed = (uint32_t)departed(e, v);
@@ -475,7 +476,7 @@ int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   uint64_t bad = 0;
   for (uint32_t m = 0; m < e->H; m++) {
     int want = departed(e, m) ? GX_M_DEAD : GX_M_ALIVE;
-    for (uint32_t v = 0; v < e->H; v++)
+    for (uint32_t v = e->lo; v < e->hi; v++) /* this engine's hosts */
       if (!departed(e, v) && MEM(e, v, m)->state != want) {
         bad++;
         break;

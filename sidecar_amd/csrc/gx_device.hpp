@@ -90,15 +90,15 @@ struct Dev {
   uint32_t *ev_cnt;       // [n_logs] events since the last delivery (may exceed ev_cap)
   uint32_t ev_cap;
   DevCtr *ctr;
-  // memberlist failure detection (gx_fd.hpp), allocated when p.fd_enable; requires an unsharded
-  // engine, so member rows are indexed by host id
-  gx_member *mem;      // [H][H] member list of every host (the deadline field lives in fd_dl)
-  int32_t *fd_dl;      // [H][H] suspicion deadlines, scanned by k_fd_tick
-  gx_fd_host *fdh;     // [H]
+  // memberlist failure detection (gx_fd.hpp), allocated when p.fd_enable; per-host arrays hold
+  // this shard's Hl hosts (memp / dlp / fdhp), the message table also the received packets
+  gx_member *mem;      // [Hl][H] member list of every host (the deadline field lives in fd_dl)
+  int32_t *fd_dl;      // [Hl][H] suspicion deadlines, scanned by k_fd_tick
+  gx_fd_host *fdh;     // [Hl]
   gx_fd_msg *fdm;      // [H*K][fd_msg_cap] memberlist messages of this round's packets
   uint32_t *fd_len;    // [H*K]
-  uint32_t *fd_peers;  // [H*K] gossip targets (memberlist's kRandomNodes)
-  uint32_t *fd_np;     // [H]
+  uint32_t *fd_peers;  // [Hl*K] gossip targets (memberlist's kRandomNodes)
+  uint32_t *fd_np;     // [Hl]
   int pair_split;      // push-pull pairs stay inside partition halves (scripted model)
   int departures;      // p.depart_round >= 0 && p.depart_ppm
 };
@@ -208,6 +208,10 @@ GXD void acc_flush(const Dev &d, const Acc &a) {
 // Local index of an owned host (global id v in [lo, lo + Hl)).
 GXD uint32_t li(const Dev &d, uint32_t v) { return v - d.lo; }
 GXD bool departed(const Dev &d, uint32_t u) { return d.departures && departed_at(d.p, d.round, u); }
+// memberlist state of this engine's host v (rows are shard-local, like the views)
+GXD gx_member *memp(const Dev &d, uint32_t v, uint32_t m) { return &d.mem[(size_t)li(d, v) * d.H + m]; }
+GXD int32_t *dlp(const Dev &d, uint32_t v, uint32_t m) { return &d.fd_dl[(size_t)li(d, v) * d.H + m]; }
+GXD gx_fd_host *fdhp(const Dev &d, uint32_t v) { return &d.fdh[li(d, v)]; }
 GXD bool reach(const Dev &d, uint32_t a, uint32_t b) {
   if (departed(d, a) || departed(d, b)) return false;
   return !(d.partitioned && ((a < d.H / 2) != (b < d.H / 2)));

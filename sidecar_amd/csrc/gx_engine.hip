@@ -68,7 +68,8 @@ struct gx_engine {
   // sharded rounds: outbox entry list and push-pull plan (device), rebuilt per round
   uint32_t *ob_entries;
   uint32_t n_ob;
-  uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t;
+  uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t, *ae_pack_other;
+  uint8_t *ae_pack_first, *ae_skip;  // this side is the pair's initiator; the pair does not run
   int32_t *ae_prow;
   uint8_t *ae_pcount;
   uint32_t n_plan, n_pack, n_plan_rows;
@@ -212,7 +213,7 @@ static int round_send_impl(gx_engine *e) {
   }
   if (d.p.fd_enable) {  // suspicion timers -> deadNode -> NotifyLeave; probe ticks
     LaunchTimer t(e, GX_K_FD);
-    k_fd_tick<<<d.H, 64, 0, s>>>(d);
+    k_fd_tick<<<d.Hl, 64, 0, s>>>(d);
   }
   if (d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2) {
     LaunchTimer t(e, GX_K_STORM);
@@ -222,7 +223,7 @@ static int round_send_impl(gx_engine *e) {
   }
   {
     LaunchTimer t(e, GX_K_SEND);
-    if (d.p.fd_enable) k_fd_send<<<nblk(d.H, 64), 64, 0, s>>>(d);  // memberlist's targets + messages
+    if (d.p.fd_enable) k_fd_send<<<nblk(d.Hl, 64), 64, 0, s>>>(d);  // memberlist's targets + messages
     // 4 lanes per host: measured best of 1/4/8/16/64 (profiles/send_team.sh)
     if (d.p.fd_enable || d.departures) k_send<4, true><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
     else k_send<4, false><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
@@ -253,7 +254,7 @@ static int round_merge_impl(gx_engine *e) {
   }
   if (d.p.fd_enable && d.K) {  // the packets' memberlist messages, after the catalog merge
     LaunchTimer t(e, GX_K_FD);
-    k_fd_recv<<<nblk(d.H, 64), 64, 0, s>>>(d);
+    k_fd_recv<<<nblk(d.Hl, 64), 64, 0, s>>>(d);
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -401,9 +402,8 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
-  // the failure detector runs on an unsharded engine
   if (p->fd_enable) {
-    if (p->n_hosts > 65534 || p->n_shards > 1 || p->fanout > 16) return GX_EINVAL;
+    if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
     if (p->fd_retransmit_limit < 1 || p->fd_retransmit_limit > GX_FD_MAX_TX || p->fd_suspicion_k > 2) return GX_EINVAL;
     for (uint32_t c = 0; c <= p->fd_suspicion_k; c++)
@@ -421,7 +421,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf,
@@ -467,7 +467,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->stream = nullptr;
   e->ob_entries = nullptr;
   e->n_ob = 0;
-  e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = nullptr;
+  e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = e->ae_pack_other = nullptr;
+  e->ae_pack_first = e->ae_skip = nullptr;
   e->ae_prow = nullptr;
   e->ae_pcount = nullptr;
   e->ae_dig = nullptr;
@@ -530,14 +531,14 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.ctr, sizeof(DevCtr));
   ALLOC(e->own_list, sizeof(grec) * H * d.S);
   d.departures = p->depart_round >= 0 && p->depart_ppm;
-  if (p->fd_enable) {  // unsharded: H == Hl
-    ALLOC(d.mem, sizeof(gx_member) * Hg * Hg);
-    ALLOC(d.fd_dl, sizeof(int32_t) * Hg * Hg);
-    ALLOC(d.fdh, sizeof(gx_fd_host) * Hg);
+  if (p->fd_enable) {  // member rows of this shard's hosts
+    ALLOC(d.mem, sizeof(gx_member) * H * Hg);
+    ALLOC(d.fd_dl, sizeof(int32_t) * H * Hg);
+    ALLOC(d.fdh, sizeof(gx_fd_host) * H);
     ALLOC(d.fdm, sizeof(gx_fd_msg) * Hg * K * p->fd_msg_cap);
     ALLOC(d.fd_len, sizeof(uint32_t) * Hg * K);
-    ALLOC(d.fd_peers, sizeof(uint32_t) * Hg * K);
-    ALLOC(d.fd_np, sizeof(uint32_t) * Hg);
+    ALLOC(d.fd_peers, sizeof(uint32_t) * H * K);
+    ALLOC(d.fd_np, sizeof(uint32_t) * H);
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
@@ -550,6 +551,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->ae_pcount, np);
     ALLOC(e->ae_pack_host, sizeof(uint32_t) * np);
     ALLOC(e->ae_pack_t, sizeof(uint32_t) * np);
+    ALLOC(e->ae_pack_other, sizeof(uint32_t) * np);
+    ALLOC(e->ae_pack_first, np);
+    ALLOC(e->ae_skip, np);
     e->nblk = (d.R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
     e->nmw = (e->nblk + 31) / 32;
     ALLOC(e->ae_dig, sizeof(ulonglong2) * H * e->nblk);
@@ -1157,7 +1161,11 @@ static uint32_t shard_of(const Dev &d, uint32_t v) {
   while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= v) g++;
   return g;
 }
-static size_t slot_bytes(const Dev &d) { return 16 + 16ull * d.p.packet_cap; }
+// packet slot (gx.h wire format): header, packet_cap records, then fd_msg_cap memberlist messages
+// when the failure detector is on
+static size_t slot_bytes(const Dev &d) {
+  return 16 + 16ull * d.p.packet_cap + (d.p.fd_enable ? 16ull * d.p.fd_msg_cap : 0);
+}
 static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk; }
 
 int gx_round_send(gx_engine *e) {
@@ -1177,13 +1185,14 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   e->n_ob = 0;
   if (d.G < 2 || !d.K) return GX_OK;
   size_t ne = (size_t)d.Hl * d.K;
-  std::vector<uint32_t> len(ne), dst(ne);
+  std::vector<uint32_t> len(ne), dst(ne), nfd(ne, 0);
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(len.data(), d.msg_len, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(dst.data(), d.msg_dst, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
+  if (d.p.fd_enable) HIPCHK(hipMemcpy(nfd.data(), d.fd_len, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
   std::vector<std::vector<uint32_t>> per(d.G);
   for (size_t i = 0; i < ne; i++)
-    if (len[i] && !own(e, dst[i])) per[shard_of(d, dst[i])].push_back((uint32_t)i);
+    if ((len[i] || nfd[i]) && !own(e, dst[i])) per[shard_of(d, dst[i])].push_back((uint32_t)i);
   std::vector<uint32_t> order;
   for (uint32_t g = 0; g < d.G; g++) {
     bytes[g] = per[g].size() * slot_bytes(d);
@@ -1228,7 +1237,7 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
   std::vector<uint32_t> pa, pb;
   uint32_t groups[2][2];
   int ng;
-  if (d.partitioned) {
+  if (d.pair_split) {
     groups[0][0] = 0; groups[0][1] = d.H / 2;
     groups[1][0] = d.H / 2; groups[1][1] = d.H - d.H / 2;
     ng = 2;
@@ -1249,7 +1258,8 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
   if (d.departures)
     for (size_t t = 0; t < pa.size(); t++)
       runs[t] = !departed_at(d.p, d.round, pa[t]) && !departed_at(d.p, d.round, pb[t]);
-  std::vector<uint32_t> plan_a, plan_b, pack_host, pack_t;
+  std::vector<uint32_t> plan_a, plan_b, pack_host, pack_t, pack_other;
+  std::vector<uint8_t> pack_first;
   std::vector<int32_t> plan_row;
   std::vector<uint8_t> plan_cnt;
   for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
@@ -1264,6 +1274,8 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
       if (shard_of(d, other) != g) continue;
       pack_host.push_back(mine);
       pack_t.push_back((uint32_t)t);
+      pack_other.push_back(other);
+      pack_first.push_back(la ? 1 : 0);
       bytes[g] += dig_bytes(e);
     }
   }
@@ -1303,6 +1315,9 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
   if (e->n_pack) {
     HIPCHK(hipMemcpy(e->ae_pack_host, pack_host.data(), 4 * e->n_pack, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(e->ae_pack_t, pack_t.data(), 4 * e->n_pack, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ae_pack_other, pack_other.data(), 4 * e->n_pack, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->ae_pack_first, pack_first.data(), e->n_pack, hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(e->ae_skip, 0, e->n_pack, e->stream));
   }
   e->ae_planned_round = (int)d.round;
   return GX_OK;
@@ -1324,10 +1339,12 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (e->ae_planned_round != (int)e->d.round || cap < e->n_pack * dig_bytes(e)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   if (e->d.R % 2 == 0)
-    k_ae_digest<true><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, (uint8_t *)buf,
+    k_ae_digest<true><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other,
+                                                         e->ae_pack_first, (uint8_t *)buf,
                                                          e->ae_dig, e->nblk);
   else
-    k_ae_digest<false><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, (uint8_t *)buf,
+    k_ae_digest<false><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other,
+                                                          e->ae_pack_first, (uint8_t *)buf,
                                                           e->ae_dig, e->nblk);
   return sync_check(e);
 }
@@ -1344,8 +1361,9 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
   std::vector<uint32_t> cnt(e->n_pack);
   if (e->n_pack) {
     HIPCHK(hipMemsetAsync(e->ae_err, 0, sizeof(uint32_t), e->stream));
-    k_ae_mask<<<e->n_pack, 256, 0, e->stream>>>((const uint8_t *)digests, e->ae_dig, e->ae_pack_t, e->nblk, e->nmw,
-                                                 e->ae_mask, e->ae_cnt, e->ae_err);
+    k_ae_mask<<<e->n_pack, 256, 0, e->stream>>>(e->d, (const uint8_t *)digests, e->ae_dig, e->ae_pack_t,
+                                                 e->ae_pack_host, e->ae_pack_other, e->ae_pack_first, e->nblk,
+                                                 e->nmw, e->ae_mask, e->ae_cnt, e->ae_err, e->ae_skip);
     uint32_t err = 0;
     HIPCHK(hipMemcpyAsync(&err, e->ae_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(cnt.data(), e->ae_cnt, sizeof(uint32_t) * e->n_pack, hipMemcpyDeviceToHost, e->stream));
@@ -1387,7 +1405,7 @@ static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *b
 #define GX_AE_PLAN(V, E)                                                                                     \
   (E ? k_ae_plan_ev<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,             \
                                                   e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off, e->ae_mask, \
-                                                  e->nmw)
+                                                  e->nmw, e->ae_skip)
   const bool ev = !e->log_views.empty();
   if (e->d.R % 2 == 0 && !ev) GX_AE_PLAN(true, false);
   else if (e->d.R % 2 == 0) GX_AE_PLAN(true, true);
@@ -1528,7 +1546,7 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
 }
 
 // ------------------------------------------------------- memberlist failure detection ----
-static bool fd_ok(const gx_engine *e, uint32_t host) { return e && e->d.p.fd_enable && host < e->d.H; }
+static bool fd_ok(const gx_engine *e, uint32_t host) { return e && e->d.p.fd_enable && own(e, host); }
 
 int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t lo, uint32_t hi, gx_member *out) {
   if (!fd_ok(e, host) || lo > hi || hi > e->d.H || (!out && hi > lo)) return GX_EINVAL;
@@ -1536,9 +1554,9 @@ int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t lo, uint32_t hi, gx
   HIPCHK(hipSetDevice(e->device));
   const Dev &d = e->d;
   std::vector<int32_t> dl(hi - lo);
-  HIPCHK(hipMemcpyAsync(out, &d.mem[(size_t)host * d.H + lo], sizeof(gx_member) * (hi - lo), hipMemcpyDeviceToHost,
-                        e->stream));
-  HIPCHK(hipMemcpyAsync(dl.data(), &d.fd_dl[(size_t)host * d.H + lo], sizeof(int32_t) * (hi - lo),
+  HIPCHK(hipMemcpyAsync(out, &d.mem[(size_t)(host - d.lo) * d.H + lo], sizeof(gx_member) * (hi - lo),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(dl.data(), &d.fd_dl[(size_t)(host - d.lo) * d.H + lo], sizeof(int32_t) * (hi - lo),
                         hipMemcpyDeviceToHost, e->stream));
   int rc = sync_check(e);
   if (rc) return rc;
@@ -1547,10 +1565,12 @@ int gx_fd_read_members(gx_engine *e, uint32_t host, uint32_t lo, uint32_t hi, gx
 }
 
 int gx_fd_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_fd_host *out) {
-  if (!e || !e->d.p.fd_enable || lo > hi || hi > e->d.H || (!out && hi > lo)) return GX_EINVAL;
+  if (!e || !e->d.p.fd_enable || lo > hi || (hi > lo && (!own(e, lo) || !own(e, hi - 1))) || (!out && hi > lo))
+    return GX_EINVAL;
   if (hi == lo) return GX_OK;
   HIPCHK(hipSetDevice(e->device));
-  HIPCHK(hipMemcpyAsync(out, &e->d.fdh[lo], sizeof(gx_fd_host) * (hi - lo), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(out, &e->d.fdh[lo - e->d.lo], sizeof(gx_fd_host) * (hi - lo), hipMemcpyDeviceToHost,
+                        e->stream));
   int rc = sync_check(e);
   if (rc) return rc;
   for (uint32_t v = lo; v < hi; v++) out[v - lo].departed = departed_at(e->d.p, e->d.round, v) ? 1u : 0u;
@@ -1564,9 +1584,9 @@ int gx_fd_read_queue(gx_engine *e, uint32_t host, gx_fd_msg *out, uint8_t *trans
   const Dev &d = e->d;
   std::vector<gx_member> row(d.H);
   gx_fd_host h;
-  HIPCHK(hipMemcpyAsync(row.data(), &d.mem[(size_t)host * d.H], sizeof(gx_member) * d.H, hipMemcpyDeviceToHost,
-                        e->stream));
-  HIPCHK(hipMemcpyAsync(&h, &d.fdh[host], sizeof(gx_fd_host), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(row.data(), &d.mem[(size_t)(host - d.lo) * d.H], sizeof(gx_member) * d.H,
+                        hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&h, &d.fdh[host - d.lo], sizeof(gx_fd_host), hipMemcpyDeviceToHost, e->stream));
   int rc = sync_check(e);
   if (rc) return rc;
   uint32_t n = 0;

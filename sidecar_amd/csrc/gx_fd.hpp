@@ -34,19 +34,17 @@ GXD void fd_flush(const Dev &d, const FdAcc &f) {
   }
 }
 
-GXD gx_member *memp(const Dev &d, uint32_t v, uint32_t m) { return &d.mem[(size_t)v * d.H + m]; }
-GXD int32_t *dlp(const Dev &d, uint32_t v, uint32_t m) { return &d.fd_dl[(size_t)v * d.H + m]; }
 
 // Reaped at the host's last resetNodes: dead for more than GossipToTheDeadTime.
 GXD bool fd_reaped(const Dev &d, uint32_t v, const gx_member *x) {
   return x->state == GX_M_DEAD &&
-         (int64_t)d.fdh[v].wrap_round - (int64_t)x->change_round > (int64_t)d.p.fd_gossip_dead_rounds;
+         (int64_t)fdhp(d, v)->wrap_round - (int64_t)x->change_round > (int64_t)d.p.fd_gossip_dead_rounds;
 }
 
 // ----------------------------------------------------------------- TransmitLimitedQueue --
 GXD void q_unlink(const Dev &d, uint32_t v, uint32_t m) {
   gx_member *x = memp(d, v, m);
-  gx_fd_host *h = &d.fdh[v];
+  gx_fd_host *h = fdhp(d, v);
   const uint16_t pv = x->q_prev, nx = x->q_next;
   if (pv != GX_FD_NONE) memp(d, v, pv)->q_next = nx;
   else h->q_head[x->tx - 1] = nx;
@@ -57,7 +55,7 @@ GXD void q_unlink(const Dev &d, uint32_t v, uint32_t m) {
 }
 GXD void q_push(const Dev &d, uint32_t v, uint32_t m, uint32_t b) {  // newest of bucket b
   gx_member *x = memp(d, v, m);
-  gx_fd_host *h = &d.fdh[v];
+  gx_fd_host *h = fdhp(d, v);
   const uint16_t top = h->q_head[b];
   x->q_prev = GX_FD_NONE;
   x->q_next = top;
@@ -83,7 +81,7 @@ GXD uint32_t fd_get_broadcasts(const Dev &d, FdAcc &f, uint32_t v, uint32_t limi
   const uint32_t L = d.p.fd_retransmit_limit;
   if (limit > 64) limit = 64;
   for (uint32_t b = 0; b < L && n < limit; b++)
-    for (uint32_t m = d.fdh[v].q_head[b]; m != GX_FD_NONE && n < limit; m = memp(d, v, m)->q_next) {
+    for (uint32_t m = fdhp(d, v)->q_head[b]; m != GX_FD_NONE && n < limit; m = memp(d, v, m)->q_next) {
       taken[n] = (uint16_t)m;
       from_b[n] = (uint8_t)b;
       n++;
@@ -109,7 +107,7 @@ GXD uint32_t fd_get_broadcasts(const Dev &d, FdAcc &f, uint32_t v, uint32_t limi
 GXD void fd_set_deadline(const Dev &d, uint32_t v, uint32_t m, int64_t dl) {
   if (dl > GX_FD_NO_DEADLINE - 1) dl = GX_FD_NO_DEADLINE - 1;
   *dlp(d, v, m) = (int32_t)dl;
-  if ((int32_t)dl < d.fdh[v].min_deadline) d.fdh[v].min_deadline = (int32_t)dl;
+  if ((int32_t)dl < fdhp(d, v)->min_deadline) fdhp(d, v)->min_deadline = (int32_t)dl;
 }
 GXD void fd_refute(const Dev &d, FdAcc &f, uint32_t v, uint32_t accused) {
   gx_member *me = memp(d, v, v);
@@ -212,7 +210,7 @@ GXD void fd_handle(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_msg &
 // ---------------------------------------------------------------------------- probes ------
 // probe() + probeNode(): returns the target (GX_FD_NONE if none), *ack its outcome.
 GXD uint32_t fd_probe_host(const Dev &d, FdAcc &f, uint32_t v, bool *ack_out) {
-  gx_fd_host *h = &d.fdh[v];
+  gx_fd_host *h = fdhp(d, v);
   const uint32_t H = d.H;
   uint32_t t = GX_FD_NONE, num_check = 0;
   *ack_out = false;
@@ -271,7 +269,7 @@ GXD bool fd_probe_tick(const Dev &d, uint32_t v) {
 // the rest.
 GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
-  if (d.fdh[v].min_deadline > d.round) return;  // uniform
+  if (fdhp(d, v)->min_deadline > d.round) return;  // uniform
   int32_t mn = GX_FD_NO_DEADLINE;
   for (uint32_t base = 0; base < d.H; base += 64) {
     const uint32_t m = base + lane;
@@ -296,7 +294,7 @@ GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
     int32_t y = __shfl_xor(mn, o, 64);
     mn = y < mn ? y : mn;
   }
-  if (lane == 0) d.fdh[v].min_deadline = mn;
+  if (lane == 0) fdhp(d, v)->min_deadline = mn;
 }
 
 // gossip(): kRandomNodes(GossipNodes) skipping us and nodes dead beyond GossipToTheDeadTime.
@@ -326,7 +324,7 @@ GXD uint32_t fd_budget(const Dev &d) {
 
 // ---------------------------------------------------------------------------- kernels -----
 __global__ void k_fd_init(Dev d) {
-  const size_t n = (size_t)d.H * d.H;
+  const size_t n = (size_t)d.Hl * d.H;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     gx_member x;
     x.incarnation = 0;
@@ -343,7 +341,7 @@ __global__ void k_fd_init(Dev d) {
     d.mem[i] = x;
     d.fd_dl[i] = GX_FD_NO_DEADLINE;
   }
-  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < d.H; v += (size_t)gridDim.x * blockDim.x) {
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < d.Hl; v += (size_t)gridDim.x * blockDim.x) {
     gx_fd_host h;
     h.probe_pass = 0;
     h.probe_index = 0;
@@ -356,10 +354,10 @@ __global__ void k_fd_init(Dev d) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_fd_tick(Dev d) {
+__global__ __launch_bounds__(64) void k_fd_tick(Dev d) {  // one wave per host of this engine
   Acc a;
   FdAcc f;
-  const uint32_t v = blockIdx.x;
+  const uint32_t v = d.lo + blockIdx.x;
   if (!departed(d, v)) {
     fd_timers_wave(d, a, f, v);
     if (threadIdx.x == 0 && fd_probe_tick(d, v)) {
@@ -371,34 +369,34 @@ __global__ __launch_bounds__(64) void k_fd_tick(Dev d) {
   fd_flush(d, f);
 }
 
-__global__ __launch_bounds__(64) void k_fd_send(Dev d) {
+__global__ __launch_bounds__(64) void k_fd_send(Dev d) {  // one thread per host of this engine
   FdAcc f;
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < d.H) {
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x, u = d.lo + idx;
+  if (idx < d.Hl) {
     const uint32_t K = d.K, cap = d.p.fd_msg_cap;
-    for (uint32_t j = 0; j < K; j++) d.fd_len[(size_t)u * K + j] = 0;
+    for (uint32_t j = 0; j < K; j++) d.fd_len[(size_t)idx * K + j] = 0;
     uint32_t np = 0;
     if (!departed(d, u)) {
       uint32_t peers[16];
       np = fd_sample_peers(d, u, peers);
       const uint32_t budget = fd_budget(d);
       for (uint32_t j = 0; j < np; j++) {
-        d.fd_peers[(size_t)u * K + j] = peers[j];
-        d.fd_len[(size_t)u * K + j] = fd_get_broadcasts(d, f, u, budget, &d.fdm[((size_t)u * K + j) * cap]);
+        d.fd_peers[(size_t)idx * K + j] = peers[j];
+        d.fd_len[(size_t)idx * K + j] = fd_get_broadcasts(d, f, u, budget, &d.fdm[((size_t)idx * K + j) * cap]);
       }
     }
-    d.fd_np[u] = np;
+    d.fd_np[idx] = np;
   }
   fd_flush(d, f);
 }
 
-__global__ __launch_bounds__(64) void k_fd_recv(Dev d) {
+__global__ __launch_bounds__(64) void k_fd_recv(Dev d) {  // one thread per receiver of this engine
   Acc a;
   FdAcc f;
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v < d.H && !departed(d, v)) {
+  const uint32_t vi = blockIdx.x * blockDim.x + threadIdx.x, v = d.lo + vi;
+  if (vi < d.Hl && !departed(d, v)) {
     const uint32_t cap = d.p.fd_msg_cap;
-    for (uint32_t x = d.in_cnt[v]; x < d.in_cnt[v + 1]; x++) {
+    for (uint32_t x = d.in_cnt[vi]; x < d.in_cnt[vi + 1]; x++) {
       const uint32_t e = d.in_sorted[x].x, n = d.fd_len[e];
       for (uint32_t y = 0; y < n; y++) fd_handle(d, a, f, v, d.fdm[(size_t)e * cap + y]);
     }
@@ -443,9 +441,9 @@ __global__ __launch_bounds__(64) void k_fd_api_timers(Dev d, uint32_t v) {
 __global__ void k_fd_converged(Dev d, unsigned long long *bad) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   bool dis = false;
-  if (m < d.H) {
+  if (m < d.H) {  // over this engine's live hosts
     const uint8_t want = departed(d, m) ? GX_M_DEAD : GX_M_ALIVE;
-    for (uint32_t v = 0; v < d.H && !dis; v++)
+    for (uint32_t v = d.lo; v < d.lo + d.Hl && !dis; v++)
       dis = !departed(d, v) && memp(d, v, m)->state != want;
   }
   unsigned long long c = wave_sum(dis ? 1ull : 0ull);

@@ -1350,7 +1350,7 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
   // the initiator (a) must see b ALIVE (memberlist pushPull picks among alive nodes)
   if (d.departures || d.p.fd_enable) {
     bool ok = !departed(d, a) && !departed(d, b);
-    if (ok && d.p.fd_enable) ok = reach(d, a, b) && d.mem[(size_t)a * d.H + b].state == GX_M_ALIVE;
+    if (ok && d.p.fd_enable) ok = reach(d, a, b) && memp(d, a, b)->state == GX_M_ALIVE;
     if (!ok) return;
   }
   ae_pair<VEC, PF, NT, EV>(d, a, b, true, s_wave, s_red);
@@ -1380,11 +1380,14 @@ __global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32
 template <bool VEC, bool EV>
 GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
                                                   const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
-                                                  const uint32_t *mask, uint32_t nmw) {
+                                                  const uint32_t *mask, uint32_t nmw, const uint8_t *skip) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
   uint32_t i = blockIdx.x;
   int32_t k = prow[i];
+  if (k < 0 && d.p.fd_enable && !(reach(d, pa[i], pb[i]) && memp(d, pa[i], pb[i])->state == GX_M_ALIVE))
+    return;  // memberlist pushPull: the initiator (pa) needs the path and sees the partner alive
+  if (k >= 0 && skip[k]) return;  // the same decision for a cross-shard pair (digest flag)
   if (k < 0) {
     ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], true, s_wave, s_red);
   } else {
@@ -1395,21 +1398,27 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
 template <bool VEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae_plan(
     Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow, const uint8_t *pcount, const uint8_t *in,
-    const uint64_t *off, const uint32_t *mask, uint32_t nmw) {
-  ae_plan_pair<VEC, false>(d, pa, pb, prow, pcount, in, off, mask, nmw);
+    const uint64_t *off, const uint32_t *mask, uint32_t nmw, const uint8_t *skip) {
+  ae_plan_pair<VEC, false>(d, pa, pb, prow, pcount, in, off, mask, nmw, skip);
 }
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_plan_ev(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
                                                      const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
-                                                     const uint32_t *mask, uint32_t nmw) {
-  ae_plan_pair<VEC, true>(d, pa, pb, prow, pcount, in, off, mask, nmw);
+                                                     const uint32_t *mask, uint32_t nmw, const uint8_t *skip) {
+  ae_plan_pair<VEC, true>(d, pa, pb, prow, pcount, in, off, mask, nmw, skip);
 }
 
 // Push-pull digests of this shard's cross-pair rows (gx.h "digest"): one block per pair, one wave
 // per 512-slot block at a time. Also kept in `own` for the comparison.
 GXD uint64_t dig_mix(uint64_t z) { return mix64(z); }
+// With the failure detector the initiator's side decides whether the pair runs (it needs the
+// path and sees the partner alive, memberlist pushPull) and says so in header word 3.
+GXD bool ae_initiator_runs(const Dev &d, uint32_t mine, uint32_t other) {
+  return reach(d, mine, other) && memp(d, mine, other)->state == GX_M_ALIVE;
+}
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, const uint32_t *pair_t, uint8_t *out,
+__global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, const uint32_t *pair_t,
+                                                    const uint32_t *other, const uint8_t *first, uint8_t *out,
                                                     ulonglong2 *own, uint32_t nblk) {
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint8_t *msg = out + (size_t)k * (16 + 16ull * nblk);
@@ -1418,7 +1427,7 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
     hdr[0] = pair_t[k];
     hdr[1] = host[k];
     hdr[2] = nblk;
-    hdr[3] = 0;
+    hdr[3] = d.p.fd_enable && first[k] && ae_initiator_runs(d, host[k], other[k]) ? 1u : 0u;
   }
   const uint64_t *row = vrow(d, host[k]);
   for (uint32_t b = wv; b < nblk; b += 4) {
@@ -1456,14 +1465,18 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
 }
 
 // Compare own digests with the partner's (message k of `in`): mask bit b = block b differs.
-__global__ __launch_bounds__(256) void k_ae_mask(const uint8_t *in, const ulonglong2 *own, const uint32_t *pair_t,
-                                                  uint32_t nblk, uint32_t nmw, uint32_t *mask, uint32_t *cnt,
-                                                  uint32_t *err) {
+// A pair that does not run (failure detector: the initiator's decision) ships no blocks.
+__global__ __launch_bounds__(256) void k_ae_mask(Dev d, const uint8_t *in, const ulonglong2 *own,
+                                                  const uint32_t *pair_t, const uint32_t *host, const uint32_t *other,
+                                                  const uint8_t *first, uint32_t nblk, uint32_t nmw, uint32_t *mask,
+                                                  uint32_t *cnt, uint32_t *err, uint8_t *skip) {
   __shared__ uint32_t s_n[4];
   const uint32_t k = blockIdx.x;
   const uint8_t *msg = in + (size_t)k * (16 + 16ull * nblk);
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(msg);
   if (threadIdx.x == 0 && (hdr[0] != pair_t[k] || hdr[2] != nblk)) atomicOr(err, 1u);
+  const bool runs = !d.p.fd_enable || (first[k] ? ae_initiator_runs(d, host[k], other[k]) : (hdr[3] & 1u) != 0);
+  if (threadIdx.x == 0) skip[k] = runs ? 0 : 1;
   uint32_t n = 0;
   for (uint32_t w = threadIdx.x; w < nmw; w += blockDim.x) {
     uint32_t bits = 0;
@@ -1472,7 +1485,7 @@ __global__ __launch_bounds__(256) void k_ae_mask(const uint8_t *in, const ulongl
       if (b >= nblk) break;
       ulonglong2 x = own[(size_t)k * nblk + b];
       ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(msg + 16 + 16ull * b);
-      if (x.x != y.x || x.y != y.y) bits |= 1u << j;
+      if (runs && (x.x != y.x || x.y != y.y)) bits |= 1u << j;
     }
     mask[(size_t)k * nmw + w] = bits;
     n += __popc(bits);
@@ -1516,15 +1529,25 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
   uint32_t i = blockIdx.x;
   if (i >= n) return;
   uint32_t e = entry[i];
-  size_t sb = 16 + 16ull * d.p.packet_cap;
+  const uint32_t fcap = d.p.fd_enable ? d.p.fd_msg_cap : 0;
+  size_t sb = 16 + 16ull * d.p.packet_cap + 16ull * fcap;
   uint8_t *dst = out + (size_t)i * sb;
-  uint32_t len = d.msg_len[e];
+  uint32_t len = d.msg_len[e], nfd = fcap ? d.fd_len[e] : 0;
   if (threadIdx.x == 0) {
     uint32_t *hdr = reinterpret_cast<uint32_t *>(dst);
     hdr[0] = d.msg_key[e];
     hdr[1] = d.msg_dst[e];
     hdr[2] = len;
-    hdr[3] = 0;
+    hdr[3] = nfd;
+  }
+  uint4 *fm = reinterpret_cast<uint4 *>(dst + 16 + 16ull * d.p.packet_cap);  // memberlist messages
+  for (uint32_t x = threadIdx.x; x < fcap; x += blockDim.x) {
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (x < nfd) {
+      const gx_fd_msg g = d.fdm[(size_t)e * fcap + x];
+      w = make_uint4(g.incarnation, (uint32_t)g.node | ((uint32_t)g.from << 16), g.kind, 0);
+    }
+    fm[x] = w;
   }
   grec *recs = reinterpret_cast<grec *>(dst + 16);
   for (uint32_t x = threadIdx.x; x < d.p.packet_cap; x += blockDim.x) {
@@ -1544,18 +1567,31 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
 __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   uint32_t i = blockIdx.x;
   if (i >= n) return;
-  size_t sb = 16 + 16ull * d.p.packet_cap;
+  const uint32_t fcap = d.p.fd_enable ? d.p.fd_msg_cap : 0;
+  size_t sb = 16 + 16ull * d.p.packet_cap + 16ull * fcap;
   const uint8_t *src = in + (size_t)i * sb;
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(src);
-  uint32_t key = hdr[0], dst = hdr[1], len = hdr[2];
+  uint32_t key = hdr[0], dst = hdr[1], len = hdr[2], nfd = fcap ? hdr[3] : 0;
   size_t e = (size_t)d.Hl * d.K + i;
   const grec *recs = reinterpret_cast<const grec *>(src + 16);
   for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) d.msg[e * d.p.packet_cap + x] = recs[x];
+  const uint4 *fm = reinterpret_cast<const uint4 *>(src + 16 + 16ull * d.p.packet_cap);
+  for (uint32_t x = threadIdx.x; x < nfd; x += blockDim.x) {
+    const uint4 w = fm[x];
+    gx_fd_msg g;
+    g.incarnation = w.x;
+    g.node = (uint16_t)(w.y & 0xffffu);
+    g.from = (uint16_t)(w.y >> 16);
+    g.kind = (uint8_t)w.z;
+    g.pad[0] = g.pad[1] = g.pad[2] = 0;
+    d.fdm[e * fcap + x] = g;
+  }
   if (threadIdx.x == 0) {
     d.msg_key[e] = key;
     d.msg_dst[e] = dst;
     d.msg_len[e] = len;
-    if (len) atomicAdd(&d.in_cnt[dst - d.lo], 1u);
+    if (fcap) d.fd_len[e] = nfd;
+    if (len || nfd) atomicAdd(&d.in_cnt[dst - d.lo], 1u);
   }
 }
 

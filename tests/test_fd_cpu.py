@@ -79,7 +79,7 @@ def test_short_partition_recovers(oracle_lib):
 
 def test_fd_param_checks(oracle_lib):
     base = dict(n_hosts=64, n_services=8, fd_enable=1)
-    for bad in (dict(n_shards=2), dict(n_hosts=65535), dict(fd_msg_cap=0), dict(fd_msg_cap=65),
+    for bad in (dict(n_hosts=65535), dict(fd_msg_cap=0), dict(fd_msg_cap=65),
                 dict(fd_suspicion_k=3), dict(fd_retransmit_limit=0), dict(fd_retransmit_limit=33)):
         kw = dict(base, **bad)
         with pytest.raises(GxError, match=f"rc={GX_EINVAL}"):

@@ -27,6 +27,12 @@ SCEN = {
     # host crashes: lost packets across shards, push-pull pairs with a crashed member skipped
     "departures": dict(n_hosts=60, n_services=8, init_mode=2, ae_period_rounds=5, partition_start=0,
                        partition_end=12, storm_round=3, depart_round=4, depart_ppm=150000, queue_cap=2048),
+    # memberlist failure detection across shards: memberlist messages ride in the packet slots,
+    # the push-pull initiator's decision travels in the digest header
+    "fd": dict(n_hosts=64, n_services=8, init_mode=2, ae_period_rounds=5, partition_start=0,
+               partition_end=45, depart_round=3, depart_ppm=100000, fd_enable=1, queue_cap=4096),
+    "fd_bytes": dict(n_hosts=50, n_services=6, init_mode=1, ae_period_rounds=4, churn_ppm=30000, depart_round=10,
+                     depart_ppm=100000, fd_enable=1, limit_bytes=1398, packet_cap=48, queue_cap=2048),
 }
 
 
@@ -47,6 +53,13 @@ def assert_sharded_equal(whole: Engine, shards, what):
     for e in shards.engines:
         for v in (e.lo, (e.lo + e.hi) // 2, e.hi - 1):
             assert np.array_equal(e.server_times(v), whole.server_times(v)), (what, v)
+    if whole.params.fd_enable:  # every host's member list, probe/queue state and queue
+        for e in shards.engines:
+            assert [bytes(h) for h in e.fd_hosts(e.lo, e.hi)] == [bytes(h) for h in whole.fd_hosts(e.lo, e.hi)], what
+            for v in range(e.lo, e.hi):
+                assert e.fd_members(v) == whole.fd_members(v), (what, v)
+                assert e.fd_queue(v) == whole.fd_queue(v), (what, v)
+        assert all(e.fd_converged()[0] for e in shards.engines) == whole.fd_converged()[0], what
 
 
 @pytest.mark.parametrize("G", [2, 3, 5])
