@@ -61,6 +61,11 @@ CONFIGS = {
                            "detection (SWIM + Lifeguard) -> NotifyLeave -> ExpireServer, push-pull every 10 rounds",
                       p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2,
                              ae_period_rounds=10, fd_enable=1, depart_round=5, depart_ppm=20000)),
+    # plumbing case of the failure detector (CPU rehearsal of the sharded path)
+    "cfg1fd": dict(desc="64 hosts x 8 services, fanout 3, 10% of hosts crash at round 5, memberlist failure "
+                        "detection, push-pull every 10 rounds",
+                   p=dict(n_hosts=64, n_services=8, fanout=3, queue_cap=4096, init_mode=2, ae_period_rounds=10,
+                          fd_enable=1, depart_round=5, depart_ppm=100000)),
     # small plumbing case (configs[0]); also the CPU-baseline scale model
     "cfg1": dict(desc="64 hosts x 8 services, fanout 3", p=dict(n_hosts=64, n_services=8, fanout=3,
                                                                 queue_cap=4096, init_mode=0)),

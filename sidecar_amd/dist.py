@@ -144,6 +144,8 @@ class LocalShards:
             gmn = mn.clone() if gmn is None else torch.minimum(gmn, mn)
             gmx = mx.clone() if gmx is None else torch.maximum(gmx, mx)
         bad = int((gmn != gmx).sum().item())
+        if bad == 0 and self.shards[0].e.params.fd_enable:  # membership agrees with the truth too
+            bad = sum(s.e.fd_converged()[1] for s in self.shards)
         return bad == 0, bad
 
 
@@ -242,4 +244,8 @@ class DistShard:
         self.dist.all_reduce(mn, op=self.dist.ReduceOp.MIN, group=self.group)
         self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
         bad = int((mn != mx).sum().item())
+        if self.e.params.fd_enable:  # membership agrees with the truth on every shard too
+            t = torch.tensor([bad + self.e.fd_converged()[1]], dtype=torch.int64, device=self.device)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+            bad = int(t.item())
         return bad == 0, bad
