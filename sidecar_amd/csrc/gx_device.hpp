@@ -100,6 +100,8 @@ struct Dev {
   uint32_t *fd_peers;  // [Hl*K] gossip targets (memberlist's kRandomNodes)
   uint32_t *fd_np;     // [Hl]
   int pair_split;      // push-pull pairs stay inside partition halves (scripted model)
+  uint64_t divS;       // r / S as a 64x32 multiply-high (Lemire: M = (2^64 - 1) / S + 1), S > 1
+  uint32_t logS;       // log2(S) when S is a power of two
   int departures;      // p.depart_round >= 0 && p.depart_ppm
 };
 
@@ -207,6 +209,10 @@ GXD void acc_flush(const Dev &d, const Acc &a) {
 
 // Local index of an owned host (global id v in [lo, lo + Hl)).
 GXD uint32_t li(const Dev &d, uint32_t v) { return v - d.lo; }
+// Owner of record key r (r / S) without a runtime 32-bit division; exact for every 32-bit r.
+GXD uint32_t owner_of(const Dev &d, uint32_t r) { return d.S == 1 ? r : (uint32_t)__umul64hi(d.divS, (uint64_t)r); }
+// r belongs to owner o (r / S == o) as one range compare
+GXD bool owned_by(const Dev &d, uint32_t r, uint32_t o) { return r - o * d.S < d.S; }
 GXD bool departed(const Dev &d, uint32_t u) { return d.departures && departed_at(d.p, d.round, u); }
 // memberlist state of this engine's host v (rows are shard-local, like the views)
 GXD gx_member *memp(const Dev &d, uint32_t v, uint32_t m) { return &d.mem[(size_t)li(d, v) * d.H + m]; }
@@ -248,7 +254,7 @@ GXD void ev_put(const Dev &d, int32_t k, uint32_t pos, uint32_t r, uint64_t nw, 
 // ServiceChanged (services_state.go:195-199) from a path that owns view v alone (one thread).
 GXD void svc_changed(const Dev &d, Acc &a, uint32_t v, uint32_t r, uint64_t nw, int prev) {
   int64_t ts = ts_of(nw);
-  gx_server_times *t = srv_times(d, v, r / d.S);
+  gx_server_times *t = srv_times(d, v, owner_of(d, r));
   t->last_updated_ns = ts;
   t->last_changed_ns = ts;
   d.vlc[li(d, v)] = ts;

@@ -488,6 +488,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.A = p->list_slots;
   d.L = p->packet_cap + p->pending_cap;
   d.K = p->fanout;
+  d.divS = d.S > 1 ? ~0ull / d.S + 1 : 0;
+  d.logS = 0;
+  while ((1u << d.logS) < d.S) d.logS++;  // used where S divides 64 (a power of two)
   d.G = p->n_shards > 1 ? p->n_shards : 1;
   d.gid = d.G > 1 ? p->shard_id : 0;
   d.lo = (uint32_t)(((uint64_t)d.gid * d.H) / d.G);

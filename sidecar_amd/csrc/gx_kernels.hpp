@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t LPO = d.S / 2;                      // lanes per owner
   const uint64_t omask = LPO == 32 ? 0xffffffffull : ((1ull << LPO) - 1);
-  const bool leader = lane % LPO == 0;
+  const bool leader = (lane & (LPO - 1)) == 0;
   uint64_t *row = &d.view[(size_t)vi * d.R + (size_t)lo * d.S];
   const uint32_t nw = (hi - lo) * d.S;
   // two 1024-word tiles in flight while one is processed (q0: even tiles, q1: odd tiles)
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       bool p0 = st_of(w[c].x) != GX_ABSENT, p1 = st_of(w[c].y) != GX_ABSENT;
       bool l0 = p0 && st_of(w[c].x) != GX_TOMBSTONE, l1 = p1 && st_of(w[c].y) != GX_TOMBSTONE;
       uint64_t b0 = __ballot(p0), b1 = __ballot(p1), bl = __ballot(l0 || l1);
-      uint32_t sh = lane - lane % LPO;  // first lane of this lane's owner
+      uint32_t sh = lane & ~(LPO - 1);  // first lane of this lane's owner (S | 64: LPO a power of 2)
       bool live = ((bl >> sh) & omask) != 0;
       pmask[c] = spread32((b0 >> sh) & omask) | (spread32((b1 >> sh) & omask) << 1);
       uint64_t n0 = (p0 && live) ? tomb : w[c].x, n1 = (p1 && live) ? tomb : w[c].y;
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       rank[c] = (uint32_t)__popcll(bj & ((1ull << lane) - 1));
       if (lane == 0) s_cnt[it][4 * c + wv] = (uint32_t)__popcll(bj);
       if (lead_live[c]) {  // serverChanged (:204-215) for a live owner
-        gx_server_times *st = srv_times(d, v, lo + (base + 512 * c + 2 * t) / d.S);
+        gx_server_times *st = srv_times(d, v, lo + ((base + 512 * c + 2 * t) >> d.logS));
         st->last_updated_ns = d.now;
         st->last_changed_ns = d.now;
       }
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
     for (int c = 0; c < 2; c++) {
       uint32_t pos = jobs + pre[c] + rank[c];
       if (lead_live[c] && pos < room) {
-        uint32_t o = lo + (base + 512 * c + 2 * t) / d.S;
+        uint32_t o = lo + ((base + 512 * c + 2 * t) >> d.logS);
         d.fifo[(size_t)vi * d.Q + ((tail0 + pos) % d.Q)] =
             make_job((uint64_t)d.now, pmask[c], o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
       }
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       for (int c = 0; c < 2; c++) {
         uint32_t ob = __shfl(erank[c], (int)sh_c[c], 64);  // the owner's first event
         uint32_t r0 = base + 512 * c + 2 * t, key0 = lo * d.S + r0;
-        uint32_t s0 = r0 % d.S;
+        uint32_t s0 = r0 & (d.S - 1);
         uint64_t below = pmask[c] & ((1ull << s0) - 1);
         uint32_t e0 = ev0 + n_ev + epre[c] + ob + (uint32_t)__popcll(below);
         bool p0 = st_of(w[c].x) != GX_ABSENT, p1 = st_of(w[c].y) != GX_ABSENT;
@@ -892,7 +892,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
       // ServiceChanged: an insert, or a stored status that differs (:317-340)
       const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
       c_chg += chg;
-      s_accf[src] = vs && acc && (skey / d.S != v);
+      s_accf[src] = vs && acc && !owned_by(d, skey, v);
       if (EV) {
         s_chg[src] = chg;
         s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
       s_accw[src] = wme;
       // per owner (contiguous in key order): its last accepted and last status-changing
       // occurrence in arrival order (segmented max of arrival lane + 1)
-      const uint32_t own = vs ? skey / d.S : 0xffffffffu;
+      const uint32_t own = vs ? owner_of(d, skey) : 0xffffffffu;
       uint32_t mu = acc ? src + 1 : 0, mc = chg ? src + 1 : 0;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -1017,7 +1017,7 @@ GXD void side_times_shfl(const Dev &d, uint32_t x, uint32_t base, uint32_t f, co
       }
     }
     if (lane % lpo == 0 && (ku | kc)) {
-      gx_server_times *st = srv_times(d, x, r0 / d.S);
+      gx_server_times *st = srv_times(d, x, owner_of(d, r0));
       if (ku) st->last_updated_ns = tu;
       if (kc) st->last_changed_ns = tc;
       words_written += (ku != 0) + (kc != 0);
@@ -1052,9 +1052,9 @@ GXD uint32_t ae_book(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t b
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
-      if ((fl >> (8 * side + k)) & 1u) atomicMax(&s_lu[r / d.S - o0], r + 1);
+      if ((fl >> (8 * side + k)) & 1u) atomicMax(&s_lu[owner_of(d, r) - o0], r + 1);
       if ((fl >> (8 * side + 4 + k)) & 1u) {
-        atomicMax(&s_lc[r / d.S - o0], r + 1);
+        atomicMax(&s_lc[owner_of(d, r) - o0], r + 1);
         atomicMax(&s_last[side], r + 1);
         if (EV) {
           const int32_t evk = side ? evkb : evka;
@@ -1157,7 +1157,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         c_stale += st;
         if (ac) {
           c_acc++;
-          fa[k] = r / d.S != a;
+          fa[k] = !owned_by(d, r, a);
           accb |= 1u << k;
         }
       }
@@ -1168,7 +1168,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         c_stale += st;
         if (ac) {
           c_acc++;
-          fb[k] = r / d.S != b;
+          fb[k] = !owned_by(d, r, b);
           accb |= 1u << (8 + k);
         }
       }
