@@ -1001,27 +1001,23 @@ GXD void side_times_shfl(const Dev &d, uint32_t x, uint32_t base, uint32_t f, co
     const uint32_t r0 = base + 512 * h + 2 * t;
     const uint32_t fa0 = (f >> (2 * h)) & 1u, fa1 = (f >> (2 * h + 1)) & 1u;
     const uint32_t fc0 = (f >> (4 + 2 * h)) & 1u, fc1 = (f >> (4 + 2 * h + 1)) & 1u;
-    if (!__ballot(fa0 | fa1)) continue;  // changes only come with accepts
-    uint32_t ku = fa1 ? r0 + 2 : (fa0 ? r0 + 1 : 0u), kc = fc1 ? r0 + 2 : (fc0 ? r0 + 1 : 0u);
-    int64_t tu = ts_of(fa1 ? nw[2 * h + 1] : nw[2 * h]), tc = ts_of(fc1 ? nw[2 * h + 1] : nw[2 * h]);
-    for (uint32_t o = 1; o < lpo; o <<= 1) {
-      uint32_t yk = __shfl_xor(ku, (int)o, 64), yc = __shfl_xor(kc, (int)o, 64);
-      int64_t yu = __shfl_xor(tu, (int)o, 64), yt = __shfl_xor(tc, (int)o, 64);
-      if (yk > ku) {
-        ku = yk;
-        tu = yu;
-      }
-      if (yc > kc) {
-        kc = yc;
-        tc = yt;
-      }
-    }
-    if (lane % lpo == 0 && (ku | kc)) {
+    const uint64_t bu_all = __ballot(fa0 | fa1);
+    if (!bu_all) continue;  // changes only come with accepts
+    // An owner's slots sit in its lane group in key order, so its last accepted (changed) slot is
+    // in the group's highest lane with that flag: two ballots and one shuffle per field.
+    const uint32_t g0 = lane & ~(lpo - 1);
+    const uint64_t gmask = (lpo == 32 ? 0xffffffffull : ((1ull << lpo) - 1ull)) << g0;
+    const uint64_t bu = bu_all & gmask, bc = __ballot(fc0 | fc1) & gmask;
+    const int64_t tu = ts_of(fa1 ? nw[2 * h + 1] : nw[2 * h]), tc = ts_of(fc1 ? nw[2 * h + 1] : nw[2 * h]);
+    const int lu = bu ? 63 - __clzll((long long)bu) : (int)lane, lc = bc ? 63 - __clzll((long long)bc) : (int)lane;
+    const int64_t gu = __shfl(tu, lu, 64), gc = __shfl(tc, lc, 64);
+    if (lane == g0 && (bu | bc)) {
       gx_server_times *st = srv_times(d, x, owner_of(d, r0));
-      if (ku) st->last_updated_ns = tu;
-      if (kc) st->last_changed_ns = tc;
-      words_written += (ku != 0) + (kc != 0);
+      if (bu) st->last_updated_ns = gu;
+      if (bc) st->last_changed_ns = gc;
+      words_written += (bu != 0) + (bc != 0);
     }
+    const uint32_t kc = fc1 ? r0 + 2 : (fc0 ? r0 + 1 : 0u);  // state.LastChanged: max over all lanes later
     lk = kc > lk ? kc : lk;
   }
 }
