@@ -161,6 +161,10 @@ typedef struct gx_params {
    * stops every activity and drops every packet sent to it (both models). -1 = none. */
   int32_t depart_round;
   uint32_t depart_ppm;
+  /* fd_enable: push-pull also merges memberlist state (state.go mergeState): each side merges the
+   * other's round-start member list, alive -> aliveNode, suspect or dead -> suspectNode{From: us}.
+   * 1 = memberlist's behaviour (default), 0 = catalog only. */
+  uint32_t fd_push_pull_state;
 } gx_params;
 
 /* Per-host bookkeeping (read-back for parity). */
@@ -218,7 +222,7 @@ typedef struct gx_stats {
   uint64_t fd_alive_updates; /* aliveNode accepted about another host */
   uint64_t fd_msgs_sent;     /* memberlist broadcasts put into gossip packets */
   uint64_t fd_msgs_received; /* memberlist broadcasts handled by receivers */
-  uint64_t reserved[1];
+  uint64_t fd_state_merges;  /* remote node states merged by push-pull (mergeState) */
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */
@@ -267,7 +271,9 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
  *           {u32 incarnation, u32 node | from << 16, u32 kind, u32 0} (the first n_fd used, the
  *           packet's memberlist messages); fixed-size slots grouped by destination shard, ascending
  *           key.
- *   digest: u32 pair index, u32 host, u32 n_blocks, u32 runs, then n_blocks x {u64 d0, u64 d1}: the
+ *   digest: u32 pair index, u32 host, u32 n_blocks, u32 runs, then n_blocks x {u64 d0, u64 d1}, then
+ *           with fd_enable and fd_push_pull_state H x u64 (the host's round-start member list:
+ *           incarnation << 32 | state, 0xff = not in the list): the
  *           host's round-start row in blocks of GX_DIGEST_SLOTS slots (GX digest below); one
  *           message per cross-shard push-pull pair, grouped by destination shard, ascending pair.
  *           `runs` (fd_enable only, else 0): 1 if the sender holds the pair's initiator (first
@@ -547,6 +553,10 @@ int gx_fd_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_fd_msg 
 int gx_fd_probe(gx_engine *e, uint32_t host, uint32_t *target, int *acked);
 /* Suspicion timers of the host due at the current round -> deadNode, in node order. */
 int gx_fd_timers(gx_engine *e, uint32_t host);
+/* pushPull's membership half (state.go mergeState) on one host: `remote` is a member list as
+ * pushPull sends it, H x u64 (incarnation << 32 | state, 0xff = not in the list); alive ->
+ * aliveNode, suspect or dead -> suspectNode{From: host}, in node order. */
+int gx_fd_merge_state(gx_engine *e, uint32_t host, const uint64_t *remote);
 /* Membership agreement with the truth: n_disagree = nodes that some live host of this engine sees
  * otherwise than they are (a crashed node not DEAD, a live node not ALIVE); converged iff 0 (on
  * every shard). */

@@ -42,6 +42,7 @@ struct gx_engine {
   uint32_t *x_t, *x_mine;
   uint8_t *x_first;     /* this side holds the pair's first member (counts the exchange) */
   uint8_t *x_run;       /* the pair runs (failure detector: the initiator's decision, digest word 3) */
+  uint64_t *x_rsnap;    /* [x_n][H] the partner's round-start member list (push-pull membership) */
   uint64_t *x_dig;      /* [x_n][nblk][2] own digests */
   uint8_t *x_diff;      /* [x_n][nblk] 1 = the partner's digest differs */
   uint32_t *x_cnt;
@@ -667,6 +668,10 @@ static uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
   return x;
 }
 
+/* gx_oracle_fd.c: memberlist push-pull membership merge */
+static void fd_snapshot_row(const gx_engine *e, uint32_t v, uint64_t *out);
+static void fd_merge_state(gx_engine *e, uint32_t v, const uint64_t *remote);
+
 static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
   uint64_t *sa = (uint64_t *)malloc(sizeof(uint64_t) * e->R);
   memcpy(sa, &e->view[(size_t)a * e->R], sizeof(uint64_t) * e->R);
@@ -684,6 +689,15 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
   e->st.ae_exchanges++;
   e->st.ae_slots += 2ull * e->R;
   free(sa);
+  if (e->p.fd_enable && e->p.fd_push_pull_state) { /* pushPull's membership half */
+    uint64_t *ma = (uint64_t *)malloc(8ull * e->H), *mb = (uint64_t *)malloc(8ull * e->H);
+    fd_snapshot_row(e, a, ma);
+    fd_snapshot_row(e, b, mb);
+    fd_merge_state(e, a, mb);
+    fd_merge_state(e, b, ma);
+    free(ma);
+    free(mb);
+  }
 }
 
 static uint32_t shard_lo(const gx_engine *e, uint32_t g) { return (uint32_t)(((uint64_t)g * e->H) / e->G); }
@@ -989,6 +1003,7 @@ void gx_params_default(gx_params *p) {
   p->fd_gossip_dead_rounds = 150;
   p->depart_round = -1;
   p->depart_ppm = 0;
+  p->fd_push_pull_state = 1;
   gx_fd_defaults(p);
 }
 
@@ -1103,10 +1118,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
     e->x_mine = (uint32_t *)calloc(hl, sizeof(uint32_t));
     e->x_first = (uint8_t *)calloc(hl, 1);
     e->x_run = (uint8_t *)calloc(hl, 1);
+    if (p->fd_enable && p->fd_push_pull_state) e->x_rsnap = (uint64_t *)calloc(hl * H, sizeof(uint64_t));
     e->x_dig = (uint64_t *)calloc(hl * e->nblk * 2, sizeof(uint64_t));
     e->x_diff = (uint8_t *)calloc(hl * e->nblk, 1);
     e->x_cnt = (uint32_t *)calloc(hl, sizeof(uint32_t));
-    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_run || !e->x_dig || !e->x_diff || !e->x_cnt) {
+    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_run || !e->x_dig || !e->x_diff || !e->x_cnt ||
+        (p->fd_enable && p->fd_push_pull_state && !e->x_rsnap)) {
       gx_destroy(e);
       return GX_ENOMEM;
     }
@@ -1160,6 +1177,7 @@ int gx_destroy(gx_engine *e) {
   free(e->x_mine);
   free(e->x_first);
   free(e->x_run);
+  free(e->x_rsnap);
   free(e->x_dig);
   free(e->x_diff);
   free(e->x_cnt);
@@ -1646,7 +1664,8 @@ int gx_round_merge(gx_engine *e) {
   round_merge(e);
   return GX_OK;
 }
-static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk; }
+static int pp_state(const gx_engine *e) { return e->p.fd_enable && e->p.fd_push_pull_state; }
+static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk + (pp_state(e) ? 8ull * e->H : 0); }
 /* Failure detector: the initiator (this side's host `mine`, cross pair k) runs the pair when the
  * path exists and it sees the partner alive (memberlist pushPull picks among alive nodes). */
 static int ae_initiator_runs(const gx_engine *e, uint32_t mine, uint32_t k) {
@@ -1693,6 +1712,13 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
       block_digest(e, row, b, &dg[0], &dg[1]);
       memcpy(m + 16 + 16ull * b, dg, 16);
     }
+    if (pp_state(e)) { /* the member list pushPull sends, as of now (round start of the phase) */
+      uint64_t *snap = (uint64_t *)(m + 16 + 16ull * e->nblk);
+      for (uint32_t x = 0; x < e->H; x++) {
+        uint64_t w = fd_snap_word(e, e->x_mine[k], x);
+        memcpy(&snap[x], &w, 8);
+      }
+    }
   }
   return GX_OK;
 }
@@ -1715,6 +1741,7 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
     if (hdr[0] != e->x_t[k] || hdr[2] != e->nblk) rc = GX_EINVAL;
     e->x_run[k] = (uint8_t)(!e->p.fd_enable ||
                             (e->x_first[k] ? ae_initiator_runs(e, e->x_mine[k], k) : (hdr[3] & 1u) != 0));
+    if (pp_state(e)) memcpy(&e->x_rsnap[(size_t)k * e->H], m + 16 + 16ull * e->nblk, 8ull * e->H);
     uint32_t n = 0;
     for (uint32_t b = 0; b < e->nblk; b++) {
       uint64_t theirs[2];
@@ -1785,6 +1812,9 @@ int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
       ae_merge_row(e, e->x_mine[k], row, e->x_first[k], now);
     }
     free(row);
+    if (pp_state(e)) /* pushPull's membership half: the partner's round-start list */
+      for (uint32_t k = 0; k < e->x_n; k++)
+        if (e->x_run[k]) fd_merge_state(e, e->x_mine[k], &e->x_rsnap[(size_t)k * e->H]);
   }
   ae_phase_local(e);
   return GX_OK;

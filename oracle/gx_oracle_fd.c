@@ -255,6 +255,36 @@ static void fd_handle(gx_engine *e, uint32_t v, const gx_fd_msg *g, int64_t now)
   e->st.fd_msgs_received++;
 }
 
+/* ------------------------------------------------- push-pull membership (mergeState) ------ */
+/* A host's member list as pushPull sends it (round-start snapshot): incarnation << 32 | state per
+ * node, FD_SNAP_ABSENT for a reaped node (no longer in its list). */
+#define FD_SNAP_ABSENT 0xffull
+static uint64_t fd_snap_word(const gx_engine *e, uint32_t v, uint32_t m) {
+  const gx_member *x = MEM(e, v, m);
+  if (fd_reaped(e, v, x)) return FD_SNAP_ABSENT;
+  return ((uint64_t)x->incarnation << 32) | x->state;
+}
+static void fd_snapshot_row(const gx_engine *e, uint32_t v, uint64_t *out) {
+  for (uint32_t m = 0; m < e->H; m++) out[m] = fd_snap_word(e, v, m);
+}
+/* state.go mergeState, node order: alive -> aliveNode; suspect or dead -> suspectNode{From: us}
+ * ("we prefer to suspect that node instead of declaring it dead instantly"). */
+static void fd_merge_state(gx_engine *e, uint32_t v, const uint64_t *remote) {
+  for (uint32_t m = 0; m < e->H; m++) {
+    uint64_t w = remote[m];
+    if ((w & 0xffu) == FD_SNAP_ABSENT) continue;
+    gx_fd_msg g = {(uint32_t)(w >> 32), (uint16_t)m, (uint16_t)m, GX_M_ALIVE, {0, 0, 0}};
+    e->st.fd_state_merges++;
+    if ((w & 0xffu) == GX_M_ALIVE) {
+      fd_alive_node(e, v, &g);
+    } else {
+      g.kind = GX_M_SUSPECT;
+      g.from = (uint16_t)v;
+      fd_suspect_node(e, v, &g);
+    }
+  }
+}
+
 /* ------------------------------------------------------------------ timers and probes ----- */
 /* Suspicion timers due this round, in node order: deadNode{incarnation, node, From: self}. */
 static void fd_timers_host(gx_engine *e, uint32_t v, int64_t now) {
@@ -484,5 +514,10 @@ int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   }
   if (converged) *converged = bad == 0;
   if (n_disagree) *n_disagree = bad;
+  return GX_OK;
+}
+int gx_fd_merge_state(gx_engine *e, uint32_t host, const uint64_t *remote) {
+  if (!fd_host_ok(e, host) || !remote) return GX_EINVAL;
+  fd_merge_state(e, host, remote);
   return GX_OK;
 }

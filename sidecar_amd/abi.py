@@ -87,6 +87,7 @@ class GxParams(C.Structure):
         ("fd_retransmit_limit", C.c_uint32), ("fd_msg_cap", C.c_uint32), ("fd_msg_bytes", C.c_uint32),
         ("fd_gossip_dead_rounds", C.c_uint32), ("fd_suspicion_k", C.c_uint32),
         ("fd_suspicion_rounds", C.c_uint32 * 8), ("depart_round", C.c_int32), ("depart_ppm", C.c_uint32),
+        ("fd_push_pull_state", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)
@@ -123,8 +124,8 @@ class GxStats(C.Structure):
         ("bytes_sent", C.c_uint64), ("cap_cuts", C.c_uint64), ("change_events", C.c_uint64),
         ("listener_drops", C.c_uint64)] + [(n, C.c_uint64) for n in (
         "lost_packets", "fd_probes", "fd_probe_failures", "fd_suspicions", "fd_confirmations",
-        "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received")] + [
-        ("reserved", C.c_uint64 * 1)]
+        "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received",
+        "fd_state_merges")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
@@ -198,7 +199,7 @@ ABI_FUNCS = [
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
     "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
-    "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers", "gx_fd_converged",
+    "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers", "gx_fd_converged", "gx_fd_merge_state",
 ]
 
 
@@ -265,6 +266,7 @@ def _declare(lib):
         "gx_fd_probe": ([vp, u32, P(u32), P(i32)], i32),
         "gx_fd_timers": ([vp, u32], i32),
         "gx_fd_converged": ([vp, P(i32), P(C.c_uint64)], i32),
+        "gx_fd_merge_state": ([vp, u32, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -722,6 +724,12 @@ class Engine:
 
     def fd_timers(self, host: int):
         check(self.lib.gx_fd_timers(self.h, host), "gx_fd_timers")
+
+    def fd_merge_state(self, host: int, remote: Sequence):
+        """pushPull's mergeState on `host`; remote[m] = (state, incarnation) or None (not listed)."""
+        arr = np.array([0xFF if x is None else (int(x[1]) << 32) | int(x[0]) for x in remote], dtype=np.uint64)
+        assert arr.size == self.H
+        check(self.lib.gx_fd_merge_state(self.h, host, arr.ctypes.data), "gx_fd_merge_state")
 
     def fd_converged(self):
         c = C.c_int()

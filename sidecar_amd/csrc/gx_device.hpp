@@ -39,7 +39,7 @@ enum {
 // Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
 enum {
   C_LOST = C_NCTR, C_FD_PROBES, C_FD_PROBE_FAIL, C_FD_SUSPECT, C_FD_CONFIRM, C_FD_DEATH, C_FD_REFUTE,
-  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_NCTR_ALL
+  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_NCTR_ALL
 };
 #define GX_NCTR_SLOTS 48
 
@@ -99,6 +99,7 @@ struct Dev {
   uint32_t *fd_len;    // [H*K]
   uint32_t *fd_peers;  // [Hl*K] gossip targets (memberlist's kRandomNodes)
   uint32_t *fd_np;     // [Hl]
+  uint64_t *fd_snap;   // [Hl][H] round-start member lists of push-pull (incarnation << 32 | state)
   int pair_split;      // push-pull pairs stay inside partition halves (scripted model)
   uint64_t divS;       // r / S as a 64x32 multiply-high (Lemire: M = (2^64 - 1) / S + 1), S > 1
   uint32_t logS;       // log2(S) when S is a power of two

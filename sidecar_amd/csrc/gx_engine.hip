@@ -70,6 +70,7 @@ struct gx_engine {
   uint32_t n_ob;
   uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t, *ae_pack_other;
   uint8_t *ae_pack_first, *ae_skip;  // this side is the pair's initiator; the pair does not run
+  uint64_t *fd_rsnap;                // [pairs][H] partner member lists received with the digests
   int32_t *ae_prow;
   uint8_t *ae_pcount;
   uint32_t n_plan, n_pack, n_plan_rows;
@@ -116,6 +117,8 @@ static int ensure_api(gx_engine *e, size_t bytes) {
 }
 
 static bool own(const gx_engine *e, uint32_t v) { return v >= e->d.lo && v < e->d.lo + e->d.Hl; }
+// push-pull also merges memberlist state (mergeState)
+static bool pp_state(const Dev &d) { return d.p.fd_enable && d.p.fd_push_pull_state; }
 static int64_t now_of(const gx_engine *e) { return e->d.p.t0_ns + e->d.round * e->d.p.round_ns; }
 static void set_round_fields(gx_engine *e) {
   e->d.now = now_of(e);
@@ -294,6 +297,11 @@ static int ae_whole_impl(gx_engine *e) {
       else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
       else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);
     }
+    if (np && pp_state(d)) {  // pushPull's membership half (mergeState), from round-start lists
+      LaunchTimer t(e, GX_K_FD);
+      k_fd_snap<<<2048, 256, 0, s>>>(d);
+      k_fd_pushpull<<<2 * np, 64, 0, s>>>(d, key0, key1);
+    }
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -355,6 +363,7 @@ void gx_params_default(gx_params *p) {
   p->fd_msg_bytes = 64;
   p->fd_gossip_dead_rounds = 150;
   p->depart_round = -1;
+  p->fd_push_pull_state = 1;
   gx_fd_defaults(p);
 }
 
@@ -421,11 +430,11 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf,
-                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np};
+                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
@@ -469,6 +478,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->n_ob = 0;
   e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = e->ae_pack_other = nullptr;
   e->ae_pack_first = e->ae_skip = nullptr;
+  e->fd_rsnap = nullptr;
   e->ae_prow = nullptr;
   e->ae_pcount = nullptr;
   e->ae_dig = nullptr;
@@ -542,6 +552,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(d.fd_len, sizeof(uint32_t) * Hg * K);
     ALLOC(d.fd_peers, sizeof(uint32_t) * H * K);
     ALLOC(d.fd_np, sizeof(uint32_t) * H);
+    if (p->fd_push_pull_state) ALLOC(d.fd_snap, sizeof(uint64_t) * H * Hg);
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
@@ -557,6 +568,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->ae_pack_other, sizeof(uint32_t) * np);
     ALLOC(e->ae_pack_first, np);
     ALLOC(e->ae_skip, np);
+    if (p->fd_enable && p->fd_push_pull_state) ALLOC(e->fd_rsnap, sizeof(uint64_t) * np * Hg);
     e->nblk = (d.R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
     e->nmw = (e->nblk + 31) / 32;
     ALLOC(e->ae_dig, sizeof(ulonglong2) * H * e->nblk);
@@ -1169,7 +1181,7 @@ static uint32_t shard_of(const Dev &d, uint32_t v) {
 static size_t slot_bytes(const Dev &d) {
   return 16 + 16ull * d.p.packet_cap + (d.p.fd_enable ? 16ull * d.p.fd_msg_cap : 0);
 }
-static size_t dig_bytes(const gx_engine *e) { return 16 + 16ull * e->nblk; }
+static size_t dig_bytes(const gx_engine *e) { return dig_stride(e->d, e->nblk); }
 
 int gx_round_send(gx_engine *e) {
   if (!e) return GX_EINVAL;
@@ -1322,6 +1334,7 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
     HIPCHK(hipMemcpy(e->ae_pack_first, pack_first.data(), e->n_pack, hipMemcpyHostToDevice));
     HIPCHK(hipMemsetAsync(e->ae_skip, 0, e->n_pack, e->stream));
   }
+  if (pp_state(d)) k_fd_snap<<<2048, 256, 0, e->stream>>>(d);  // round-start member lists (pushPull)
   e->ae_planned_round = (int)d.round;
   return GX_OK;
 }
@@ -1367,6 +1380,9 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
     k_ae_mask<<<e->n_pack, 256, 0, e->stream>>>(e->d, (const uint8_t *)digests, e->ae_dig, e->ae_pack_t,
                                                  e->ae_pack_host, e->ae_pack_other, e->ae_pack_first, e->nblk,
                                                  e->nmw, e->ae_mask, e->ae_cnt, e->ae_err, e->ae_skip);
+    if (pp_state(d))  // the partners' member lists ride with their digests
+      k_fd_rsnap<<<1024, 256, 0, e->stream>>>(d, (const uint8_t *)digests, dig_bytes(e), e->nblk, e->n_pack,
+                                               e->fd_rsnap);
     uint32_t err = 0;
     HIPCHK(hipMemcpyAsync(&err, e->ae_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(cnt.data(), e->ae_cnt, sizeof(uint32_t) * e->n_pack, hipMemcpyDeviceToHost, e->stream));
@@ -1440,6 +1456,11 @@ int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
   if (e->n_plan_rows && (e->ae_delta_round != (int)e->d.round || bytes != e->delta_total)) return GX_EINVAL;
   bool local_done = e->ae_local_round == e->d.round;
   ae_plan_launch(e, 0, local_done ? e->n_plan_rows : e->n_plan, buf);
+  if (pp_state(e->d) && e->n_plan) {  // pushPull's membership half, every planned pair
+    LaunchTimer t(e, GX_K_FD);
+    k_fd_pushpull_plan<<<2 * e->n_plan, 64, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_skip,
+                                                             e->fd_rsnap);
+  }
   return sync_check(e);
 }
 
@@ -1496,6 +1517,7 @@ int gx_stats_get(gx_engine *e, gx_stats *out) {
   out->fd_alive_updates = c[C_FD_ALIVE];
   out->fd_msgs_sent = c[C_FD_SENT];
   out->fd_msgs_received = c[C_FD_RECV];
+  out->fd_state_merges = c[C_FD_STATE_MERGE];
   out->round = e->d.round;
   out->gossip_merges = c[C_GOSSIP_MERGES];
   out->ae_merges = c[C_AE_MERGES];
@@ -1669,6 +1691,17 @@ int gx_fd_timers(gx_engine *e, uint32_t host) {
   HIPCHK(hipSetDevice(e->device));
   set_round_fields(e);
   k_fd_api_timers<<<1, 64, 0, e->stream>>>(e->d, host);
+  return sync_check(e);
+}
+
+int gx_fd_merge_state(gx_engine *e, uint32_t host, const uint64_t *remote) {
+  if (!fd_ok(e, host) || !remote) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, sizeof(uint64_t) * e->d.H);
+  if (rc) return rc;
+  set_round_fields(e);
+  HIPCHK(hipMemcpyAsync(e->api_dev, remote, sizeof(uint64_t) * e->d.H, hipMemcpyHostToDevice, e->stream));
+  k_fd_api_merge_state<<<1, 64, 0, e->stream>>>(e->d, host, (const uint64_t *)e->api_dev);
   return sync_check(e);
 }
 

@@ -322,6 +322,64 @@ GXD uint32_t fd_budget(const Dev &d) {
   return b;
 }
 
+// ------------------------------------------------- push-pull membership (mergeState) ------
+// The member list pushPull sends: incarnation << 32 | state per node, FD_SNAP_ABSENT if reaped.
+#define FD_SNAP_ABSENT 0xffull
+GXD uint64_t fd_snap_word(const Dev &d, uint32_t v, uint32_t m) {
+  const gx_member *x = memp(d, v, m);
+  if (fd_reaped(d, v, x)) return FD_SNAP_ABSENT;
+  return ((uint64_t)x->incarnation << 32) | x->state;
+}
+// state.go mergeState into host v, node order: alive -> aliveNode, suspect or dead ->
+// suspectNode{From: v}. One wave: the lanes test 64 nodes at a time for an effect (a superset of
+// the nodes whose handler changes anything; a node's test reads only that node's row, which the
+// handlers of other nodes do not change), lane 0 runs the handlers of the flagged nodes in order.
+GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t *remote) {
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned present_n = 0;
+  for (uint32_t base = 0; base < d.H; base += 64) {
+    const uint32_t m = base + lane;
+    const uint64_t w = m < d.H ? remote[m] : FD_SNAP_ABSENT;
+    const bool present = (w & 0xffu) != FD_SNAP_ABSENT;
+    bool flag = false;
+    if (present) {
+      present_n++;
+      const gx_member *x = memp(d, v, m);
+      const bool reaped = fd_reaped(d, v, x);
+      const uint32_t inc = (uint32_t)(w >> 32);
+      if ((w & 0xffu) == GX_M_ALIVE) {
+        flag = reaped || inc > x->incarnation;
+      } else {
+        bool confirm = x->state == GX_M_SUSPECT && x->n_conf < d.p.fd_suspicion_k;
+        for (uint32_t i = 0; i < 3 && confirm; i++)
+          if (i <= x->n_conf && x->susp_from[i] == v) confirm = false;
+        flag = !reaped && inc >= x->incarnation && (x->state == GX_M_ALIVE || confirm);
+      }
+    }
+    unsigned long long fm = __ballot(flag);
+    if (lane == 0)
+      while (fm) {
+        const uint32_t k = (uint32_t)__ffsll((long long)fm) - 1;
+        fm &= fm - 1;
+        const uint64_t x = remote[base + k];
+        gx_fd_msg g;
+        g.incarnation = (uint32_t)(x >> 32);
+        g.node = (uint16_t)(base + k);
+        g.pad[0] = g.pad[1] = g.pad[2] = 0;
+        if ((x & 0xffu) == GX_M_ALIVE) {
+          g.from = (uint16_t)(base + k);
+          g.kind = GX_M_ALIVE;
+          fd_alive_node(d, f, v, g);
+        } else {
+          g.from = (uint16_t)v;
+          g.kind = GX_M_SUSPECT;
+          fd_suspect_node(d, f, v, g);
+        }
+      }
+  }
+  f.inc(C_FD_STATE_MERGE, present_n);
+}
+
 // ---------------------------------------------------------------------------- kernels -----
 __global__ void k_fd_init(Dev d) {
   const size_t n = (size_t)d.Hl * d.H;
@@ -405,6 +463,63 @@ __global__ __launch_bounds__(64) void k_fd_recv(Dev d) {  // one thread per rece
   fd_flush(d, f);
 }
 
+// Round-start member lists of this engine's hosts (push-pull), one thread per (host, node).
+__global__ void k_fd_snap(Dev d) {
+  const size_t n = (size_t)d.Hl * d.H;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    d.fd_snap[i] = fd_snap_word(d, d.lo + (uint32_t)(i / d.H), (uint32_t)(i % d.H));
+}
+GXD const uint64_t *snap_row(const Dev &d, uint32_t v) { return &d.fd_snap[(size_t)li(d, v) * d.H]; }
+// pushPull runs when both are up, the path exists and the initiator a sees b alive at round start
+GXD bool pp_runs(const Dev &d, uint32_t a, uint32_t b) {
+  return !departed(d, a) && !departed(d, b) && reach(d, a, b) && (snap_row(d, a)[b] & 0xffu) == GX_M_ALIVE;
+}
+// Unsharded push-pull round: pair t as k_ae derives it; wave 2t merges b's list into a, 2t+1 a's into b.
+__global__ __launch_bounds__(64) void k_fd_pushpull(Dev d, uint64_t key0, uint64_t key1) {
+  FdAcc f;
+  const uint32_t t = blockIdx.x >> 1, side = blockIdx.x & 1;
+  uint32_t base = 0, m = d.H, q = t;
+  uint64_t key = key0;
+  if (d.pair_split) {
+    uint32_t m0 = d.H / 2, np0 = m0 / 2;
+    if (t < np0) {
+      m = m0;
+    } else {
+      base = m0;
+      m = d.H - m0;
+      q = t - np0;
+      key = key1;
+    }
+  }
+  const uint32_t a = base + feistel_perm(key, 2 * q, m), b = base + feistel_perm(key, 2 * q + 1, m);
+  if (pp_runs(d, a, b)) fd_merge_state_wave(d, f, side ? b : a, snap_row(d, side ? a : b));
+  fd_flush(d, f);
+}
+// Sharded push-pull round over the plan (ae_plan): a local pair merges both ways from the local
+// lists; a cross pair merges the partner's list received with the digests (rsnap row k) into this
+// side's host unless the pair does not run.
+__global__ __launch_bounds__(64) void k_fd_pushpull_plan(Dev d, const uint32_t *pa, const uint32_t *pb,
+                                                          const int32_t *prow, const uint8_t *skip,
+                                                          const uint64_t *rsnap) {
+  FdAcc f;
+  const uint32_t i = blockIdx.x >> 1, side = blockIdx.x & 1;
+  const int32_t k = prow[i];
+  if (k < 0) {
+    if (pp_runs(d, pa[i], pb[i])) fd_merge_state_wave(d, f, side ? pb[i] : pa[i], snap_row(d, side ? pa[i] : pb[i]));
+  } else if (side == 0 && !skip[k]) {
+    fd_merge_state_wave(d, f, pa[i], &rsnap[(size_t)k * d.H]);
+  }
+  fd_flush(d, f);
+}
+// The partner lists of this round's cross pairs, out of the digest inbox (message k).
+__global__ void k_fd_rsnap(Dev d, const uint8_t *in, size_t dig_bytes, uint32_t nblk, uint32_t n, uint64_t *rsnap) {
+  const size_t tot = (size_t)n * d.H;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t k = i / d.H, x = i % d.H;
+    rsnap[i] = *reinterpret_cast<const uint64_t *>(in + k * dig_bytes + 16 + 16ull * nblk + 8 * x);
+  }
+}
+
 // Single-host ABI kernels (one wave; lane 0 runs the handler logic).
 __global__ __launch_bounds__(64) void k_fd_api_notify(Dev d, uint32_t v, const gx_fd_msg *msgs, uint32_t n) {
   Acc a;
@@ -448,4 +563,9 @@ __global__ void k_fd_converged(Dev d, unsigned long long *bad) {
   }
   unsigned long long c = wave_sum(dis ? 1ull : 0ull);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}
+__global__ __launch_bounds__(64) void k_fd_api_merge_state(Dev d, uint32_t v, const uint64_t *remote) {
+  FdAcc f;
+  fd_merge_state_wave(d, f, v, remote);
+  fd_flush(d, f);
 }

@@ -1412,12 +1412,21 @@ GXD uint64_t dig_mix(uint64_t z) { return mix64(z); }
 GXD bool ae_initiator_runs(const Dev &d, uint32_t mine, uint32_t other) {
   return reach(d, mine, other) && memp(d, mine, other)->state == GX_M_ALIVE;
 }
+// digest message size (gx.h): + the host's round-start member list with push-pull membership
+GXHD size_t dig_stride(const Dev &d, uint32_t nblk) {
+  return 16 + 16ull * nblk + (d.p.fd_enable && d.p.fd_push_pull_state ? 8ull * d.H : 0);
+}
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, const uint32_t *pair_t,
                                                     const uint32_t *other, const uint8_t *first, uint8_t *out,
                                                     ulonglong2 *own, uint32_t nblk) {
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint8_t *msg = out + (size_t)k * (16 + 16ull * nblk);
+  uint8_t *msg = out + (size_t)k * dig_stride(d, nblk);
+  if (d.p.fd_enable && d.p.fd_push_pull_state) {  // the member list, snapshot of this AE round (k_fd_snap)
+    const uint64_t *snap = &d.fd_snap[(size_t)li(d, host[k]) * d.H];
+    uint64_t *dst = reinterpret_cast<uint64_t *>(msg + 16 + 16ull * nblk);
+    for (uint32_t x = threadIdx.x; x < d.H; x += blockDim.x) dst[x] = snap[x];
+  }
   if (threadIdx.x == 0) {
     uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
     hdr[0] = pair_t[k];
@@ -1468,7 +1477,7 @@ __global__ __launch_bounds__(256) void k_ae_mask(Dev d, const uint8_t *in, const
                                                   uint32_t *cnt, uint32_t *err, uint8_t *skip) {
   __shared__ uint32_t s_n[4];
   const uint32_t k = blockIdx.x;
-  const uint8_t *msg = in + (size_t)k * (16 + 16ull * nblk);
+  const uint8_t *msg = in + (size_t)k * dig_stride(d, nblk);
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(msg);
   if (threadIdx.x == 0 && (hdr[0] != pair_t[k] || hdr[2] != nblk)) atomicOr(err, 1u);
   const bool runs = !d.p.fd_enable || (first[k] ? ae_initiator_runs(d, host[k], other[k]) : (hdr[3] & 1u) != 0);

@@ -252,7 +252,30 @@ def kat_probe_skips_dead_and_reaps(lib):
     assert member(e, ME, A) == (M_ALIVE, 1)
 
 
-ALL = [kat_suspect_node, kat_suspect_double, kat_suspect_old, kat_suspect_refute,
+def kat_merge_state(lib):
+    """TestMemberList_MergeState: pushPull's mergeState applies a remote member list — a newer
+    alive incarnation updates, a dead node is only suspected (From: us), an equal incarnation
+    changes nothing, unlisted nodes are untouched; a list that calls us dead makes us refute."""
+    e = mk(lib)
+    e.fd_notify(ME, [(M_ALIVE, A, 1, A), (M_ALIVE, B, 1, B), (M_ALIVE, C, 1, C)])
+    remote = [None] * H
+    remote[A] = (M_ALIVE, 2)
+    remote[B] = (M_DEAD, 1)
+    remote[C] = (M_ALIVE, 1)
+    remote[D] = (M_ALIVE, 2)
+    e.fd_merge_state(ME, remote)
+    assert member(e, ME, A) == (M_ALIVE, 2)
+    m = e.fd_member(ME, B)
+    assert (m.state, m.incarnation, m.susp_from[0]) == (M_SUSPECT, 1, ME)
+    assert member(e, ME, C) == (M_ALIVE, 1) and member(e, ME, D) == (M_ALIVE, 2)
+    assert member(e, ME, 5) == (M_ALIVE, 0)
+    st = e.stats()
+    assert (st["fd_state_merges"], st["fd_suspicions"], st["fd_alive_updates"]) == (4, 1, 3 + 2)
+    e.fd_merge_state(ME, [None] * ME + [(M_DEAD, 0)] + [None] * (H - ME - 1))
+    assert member(e, ME, ME) == (M_ALIVE, 1) and e.stats()["fd_refutes"] == 1
+
+
+ALL = [kat_suspect_node, kat_merge_state, kat_suspect_double, kat_suspect_old, kat_suspect_refute,
        kat_suspicion_confirmations, kat_confirm_past_deadline, kat_dead_node, kat_dead_clears_suspicion,
        kat_alive_replay_after_dead, kat_alive_clears_suspect, kat_queue_order_and_limit,
        kat_probe_departed, kat_probe_partition_indirect, kat_probe_skips_dead_and_reaps]
