@@ -47,8 +47,8 @@ enum {
 struct DevCtr {
   unsigned long long c[GX_SHARDS][GX_NCTR_SLOTS];   // counter shards (shard = block % 64)
   unsigned long long last_change_p1[GX_SHARDS][8];  // last round with a slot change + 1
-  unsigned long long bytes[GX_SHARDS][8];           // algorithmic HBM bytes per kernel class
-  unsigned long long units[GX_SHARDS][8];           // slots / records per kernel class
+  unsigned long long bytes[GX_SHARDS][16];          // algorithmic HBM bytes per kernel class
+  unsigned long long units[GX_SHARDS][16];          // slots / records per kernel class
 };
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };

@@ -1487,11 +1487,11 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
   if (rc) return rc;
   const DevCtr &x = tmp[0];
   for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] = 0;
-  for (int i = 0; i < 8; i++) bytes[i] = units[i] = 0;
+  for (int i = 0; i < 16; i++) bytes[i] = units[i] = 0;
   *last_p1 = 0;
   for (int s = 0; s < GX_SHARDS; s++) {
     for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] += x.c[s][i];
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < 16; i++) {
       bytes[i] += x.bytes[s][i];
       units[i] += x.units[s][i];
     }
@@ -1503,7 +1503,7 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
 int gx_stats_get(gx_engine *e, gx_stats *out) {
   if (!e || !out) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[8], units[8];
+  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[16], units[16];
   int rc = read_ctr(e, c, &lp1, bytes, units);
   if (rc) return rc;
   memset(out, 0, sizeof(*out));
@@ -1557,15 +1557,16 @@ int gx_timing_get(gx_engine *e, gx_timing *out) {
   HIPCHK(hipSetDevice(e->device));
   int rc = drain_timing(e);
   if (rc) return rc;
-  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[8], units[8];
+  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[16], units[16];
   rc = read_ctr(e, c, &lp1, bytes, units);
   if (rc) return rc;
   memset(out, 0, sizeof(*out));
   for (int i = 0; i < GX_K_COUNT; i++) {
     out->ms[i] = e->ms[i];
     out->launches[i] = e->launches[i];
-    out->bytes[i] = i < 8 ? bytes[i] : e->host_bytes[i];  // codec classes: accounted on the host
-    out->units[i] = i < 8 ? units[i] : e->host_units[i];
+    const bool host = i == GX_K_ENCODE || i == GX_K_DECODE;  // codec classes: accounted on the host
+    out->bytes[i] = host ? e->host_bytes[i] : bytes[i];
+    out->units[i] = host ? e->host_units[i] : units[i];
   }
   return GX_OK;
 }

@@ -270,6 +270,7 @@ GXD bool fd_probe_tick(const Dev &d, uint32_t v) {
 GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
   if (fdhp(d, v)->min_deadline > d.round) return;  // uniform
+  if (lane == 0) kbytes(d, GX_K_FD, 4ull * d.H, d.H);  // the deadline row
   int32_t mn = GX_FD_NO_DEADLINE;
   for (uint32_t base = 0; base < d.H; base += 64) {
     const uint32_t m = base + lane;
@@ -378,6 +379,7 @@ GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t 
       }
   }
   f.inc(C_FD_STATE_MERGE, present_n);
+  if (lane == 0) kbytes(d, GX_K_FD, 24ull * d.H, d.H);  // remote word + the node's row fields, per node
 }
 
 // ---------------------------------------------------------------------------- kernels -----
@@ -468,6 +470,7 @@ __global__ void k_fd_snap(Dev d) {
   const size_t n = (size_t)d.Hl * d.H;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     d.fd_snap[i] = fd_snap_word(d, d.lo + (uint32_t)(i / d.H), (uint32_t)(i % d.H));
+  if (blockIdx.x == 0 && threadIdx.x == 0) kbytes(d, GX_K_FD, 20ull * n, n);  // 12 B of row read, 8 B written
 }
 GXD const uint64_t *snap_row(const Dev &d, uint32_t v) { return &d.fd_snap[(size_t)li(d, v) * d.H]; }
 // pushPull runs when both are up, the path exists and the initiator a sees b alive at round start
