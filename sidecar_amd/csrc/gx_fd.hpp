@@ -337,24 +337,39 @@ GXD uint64_t fd_snap_word(const Dev &d, uint32_t v, uint32_t m) {
 // handlers of other nodes do not change), lane 0 runs the handlers of the flagged nodes in order.
 GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t *remote) {
   const uint32_t lane = threadIdx.x & 63;
+  const int64_t wrap = fdhp(d, v)->wrap_round, dead_rounds = d.p.fd_gossip_dead_rounds;
   unsigned present_n = 0;
-  for (uint32_t base = 0; base < d.H; base += 64) {
+  // the next chunk's remote words and row fields are loaded while this chunk is tested and handled
+  // (the handlers touch only flagged nodes' rows and queue links, never the fields tested here)
+  auto load = [&](uint32_t base, uint64_t &w, uint4 &lo, uint4 &hi) {
     const uint32_t m = base + lane;
-    const uint64_t w = m < d.H ? remote[m] : FD_SNAP_ABSENT;
+    w = m < d.H ? remote[m] : FD_SNAP_ABSENT;
+    if (m < d.H && (w & 0xffu) != FD_SNAP_ABSENT) {
+      const uint4 *x = reinterpret_cast<const uint4 *>(memp(d, v, m));
+      lo = x[0];  // incarnation, msg_incarnation, change_round, deadline
+      hi = x[1];  // state, n_conf, tx, msg_kind | msg_from, susp_from[0] | susp_from[1], susp_from[2] | q_prev, q_next
+    }
+  };
+  uint64_t w = 0, wn = 0;
+  uint4 lo = make_uint4(0, 0, 0, 0), hi = lo, lon = lo, hin = lo;
+  load(0, w, lo, hi);
+  for (uint32_t base = 0; base < d.H; base += 64) {
+    if (base + 64 < d.H) load(base + 64, wn, lon, hin);
     const bool present = (w & 0xffu) != FD_SNAP_ABSENT;
     bool flag = false;
     if (present) {
       present_n++;
-      const gx_member *x = memp(d, v, m);
-      const bool reaped = fd_reaped(d, v, x);
+      const uint32_t inc_l = lo.x, state = hi.x & 0xffu, n_conf = (hi.x >> 8) & 0xffu;
+      const bool reaped = state == GX_M_DEAD && wrap - (int64_t)(int32_t)lo.z > dead_rounds;
       const uint32_t inc = (uint32_t)(w >> 32);
       if ((w & 0xffu) == GX_M_ALIVE) {
-        flag = reaped || inc > x->incarnation;
+        flag = reaped || inc > inc_l;
       } else {
-        bool confirm = x->state == GX_M_SUSPECT && x->n_conf < d.p.fd_suspicion_k;
+        const uint32_t from[3] = {hi.y >> 16, hi.z & 0xffffu, hi.z >> 16};
+        bool confirm = state == GX_M_SUSPECT && n_conf < d.p.fd_suspicion_k;
         for (uint32_t i = 0; i < 3 && confirm; i++)
-          if (i <= x->n_conf && x->susp_from[i] == v) confirm = false;
-        flag = !reaped && inc >= x->incarnation && (x->state == GX_M_ALIVE || confirm);
+          if (i <= n_conf && from[i] == v) confirm = false;
+        flag = !reaped && inc >= inc_l && (state == GX_M_ALIVE || confirm);
       }
     }
     unsigned long long fm = __ballot(flag);
@@ -377,6 +392,9 @@ GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t 
           fd_suspect_node(d, f, v, g);
         }
       }
+    w = wn;
+    lo = lon;
+    hi = hin;
   }
   f.inc(C_FD_STATE_MERGE, present_n);
   if (lane == 0) kbytes(d, GX_K_FD, 24ull * d.H, d.H);  // remote word + the node's row fields, per node
