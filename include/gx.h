@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 2
+#define GX_ABI_VERSION 3
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -279,9 +279,24 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
  *           `runs` (fd_enable only, else 0): 1 if the sender holds the pair's initiator (first
  *           host) and the pair runs (path up, partner ALIVE in the initiator's list); the other
  *           side follows it, and a pair that does not run ships no blocks.
- *   delta:  u32 pair index, u32 host, u32 n_sent, u32 0, then n_sent x GX_DIGEST_SLOTS u64 words:
- *           the row's blocks whose digests differ from the partner's, ascending (the last block
- *           of a row zero-padded); grouped like the digests.
+ *   lead:   u32 pair index, u32 host, u32 n_lead, u32 0, then n_lead encoded blocks (below): the
+ *           row's blocks whose digests differ from the partner's and that this side leads,
+ *           ascending. The side whose block has fewer literals leads it (the count rides in the
+ *           digest); on a tie the pair's first host. A lead block encodes the sender's own words
+ *           (own bits = the padding past the row's end). Grouped like the digests.
+ *   return: per destination shard a table of u64 message sizes (one per pair, in message order),
+ *           then the messages: u32 pair index, u32 host, u32 n_ret, u32 0, then n_ret u32 literal
+ *           counts (padded with a 0 to an even number), then n_ret encoded blocks: for each block
+ *           the partner leads, ascending, this side's words for the partner's merge. Slot i is an
+ *           own slot (the partner merges its own word instead) when merging this side's word y
+ *           into the partner's word x has exactly the effect of merging x into x: both absent, or
+ *           both present, y not stored, and IsStale(y) == IsStale(x).
+ *   encoded block: u64 own[8], u64 neu[8] (bit i of the 512-bit masks = slot i of the block),
+ *           then one u64 word per neu bit. Slot i is the receiver's own word if own bit i is set,
+ *           else literal number popcount(neu bits 0..i) - 1. neu bit i is set iff slot i is not an
+ *           own slot and i = 0, slot i-1 is an own slot, or word(i) != word(i-1).
+ * The follower merges the partner's lead blocks; the leader merges the follower's return blocks,
+ * so a block's words cross the link once, run-length coded, plus the partner's winning words.
  * gx_run_rounds(e, n) on an unsharded engine equals n x (round_send, round_merge, ae_merge with
  * nothing received, round_end). */
 int gx_round_send(gx_engine *e);  /* phases 0-3: wake, owner ticks, storm, GetBroadcasts */
@@ -290,20 +305,26 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap);
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes);
 int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + received packets */
 /* Push-pull across shards exchanges block digests first and then only the blocks that differ
- * (Dynamo-style anti-entropy). Views and every counter equal those of a full-row exchange: a
- * block whose digests match merges the host's own copy, which is the same record set. Per AE
- * round: gx_ae_bytes -> gx_ae_pack (digests) -> [gx_ae_merge_local] -> exchange ->
- * gx_ae_delta_bytes (received digests) -> gx_ae_delta_pack -> exchange -> gx_ae_merge.
+ * (Dynamo-style anti-entropy), each once: its leader ships it run-length coded, the follower
+ * merges it and returns only the words that change the leader's merge. Views and every counter
+ * equal those of a full-row exchange: a block whose digests match merges the host's own copy,
+ * which is the same record set. Per AE round: gx_ae_bytes -> gx_ae_pack (digests) ->
+ * [gx_ae_merge_local] -> exchange -> gx_ae_delta_bytes (received digests) -> gx_ae_delta_pack
+ * (lead blocks) -> exchange -> gx_ae_return_bytes (received lead blocks) -> gx_ae_return_pack ->
+ * exchange -> gx_ae_merge (both inboxes).
  * Digest of block b = slots [b*512, min(R, (b+1)*512)) of a row, i = slot index in the row,
  * w = slot word, mix(z) = SplitMix64 (z += 0x9E3779B97F4A7C15, then its two xor-shift-multiply
- * steps and the final xor-shift), sums mod 2^64:
- *   d0 = sum_i mix(w ^ (i * 0xD6E8FEB86659FD93)),  d1 = sum_i mix(w + i * 0xC2B2AE3D27D4EB4F + 0x165667B19E3779F9) */
+ * steps and the final xor-shift), sums mod 2^64, L = literal count of the block's lead encoding:
+ *   d0 = sum_i mix(w ^ (i * 0xD6E8FEB86659FD93)),
+ *   d1 = (sum_i mix(w + i * 0xC2B2AE3D27D4EB4F + 0x165667B19E3779F9) mod 2^54) | L << 54 */
 #define GX_DIGEST_SLOTS 512
 int gx_ae_bytes(gx_engine *e, uint64_t *bytes_per_shard); /* digest messages; 0s unless a push-pull round */
 int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap);
 int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *bytes_per_shard);
-int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap);
-int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes); /* the received delta blocks */
+int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap); /* lead blocks */
+int gx_ae_return_bytes(gx_engine *e, const void *lead, uint64_t lead_bytes, uint64_t *bytes_per_shard);
+int gx_ae_return_pack(gx_engine *e, const void *lead, uint64_t lead_bytes, void *buf, uint64_t cap);
+int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void *ret, uint64_t ret_bytes);
 /* Optional, between gx_ae_pack and gx_ae_merge: start the push-pull merges of the pairs whose two
  * hosts are both on this shard, asynchronously on the engine's stream, so they overlap the
  * exchanges; gx_ae_merge then merges only the cross-shard pairs. Pairs are disjoint (every

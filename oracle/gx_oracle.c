@@ -29,6 +29,7 @@ typedef struct grec {
 } grec;
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
+enum { X_SAME = 0, X_LEAD = 1, X_FOLLOW = 2 }; /* a cross pair's row block in the push-pull delta */
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5,
        ST_INIT_AGE = 6, ST_AE = 7 };
 
@@ -44,10 +45,12 @@ struct gx_engine {
   uint8_t *x_run;       /* the pair runs (failure detector: the initiator's decision, digest word 3) */
   uint64_t *x_rsnap;    /* [x_n][H] the partner's round-start member list (push-pull membership) */
   uint64_t *x_dig;      /* [x_n][nblk][2] own digests */
-  uint8_t *x_diff;      /* [x_n][nblk] 1 = the partner's digest differs */
-  uint32_t *x_cnt;
-  uint64_t x_total;
-  int64_t x_round, x_delta_round;
+  uint8_t *x_blk;       /* [x_n][nblk] 0 = digests match, X_LEAD = this side leads, X_FOLLOW */
+  uint16_t *x_lt;       /* [x_n][nblk] literal count of the partner's block (its digest) */
+  uint32_t *x_nlead, *x_nfol;
+  uint64_t *x_rsz;      /* [x_n] return message sizes */
+  uint64_t x_total, x_lin, x_rtotal;
+  int64_t x_round, x_delta_round, x_ret_round;
   int64_t round;
   uint64_t *view;       /* H * R packed slots */
   uint8_t *own_status;  /* H * S local service status (discovery/health) */
@@ -904,7 +907,51 @@ static void ae_phase_local(gx_engine *e) {
   e->ae_local_round = e->round;
 }
 
-/* Block digest of gx.h: slots [b*512, min(R, (b+1)*512)) of a row. */
+/* Encoded block of gx.h: own[8], neu[8] (512-bit masks), then the literal words. w = the block's
+ * words, own = own flags; returns the literal count and, with out, writes 128 + 8 * count bytes. */
+static uint32_t enc_block(const uint64_t *w, const uint8_t *own, uint8_t *out) {
+  uint64_t om[8] = {0}, nm[8] = {0};
+  uint32_t L = 0;
+  for (uint32_t i = 0; i < GX_DIGEST_SLOTS; i++) {
+    if (own[i]) {
+      om[i >> 6] |= 1ull << (i & 63);
+      continue;
+    }
+    if (i == 0 || own[i - 1] || w[i] != w[i - 1]) {
+      nm[i >> 6] |= 1ull << (i & 63);
+      if (out) memcpy(out + 128 + 8ull * L, &w[i], 8);
+      L++;
+    }
+  }
+  if (out) {
+    memcpy(out, om, 64);
+    memcpy(out + 64, nm, 64);
+  }
+  return L;
+}
+/* Decode an encoded block: slot i = own[i] if its own bit is set, else its literal. */
+static void dec_block(const uint8_t *in, const uint64_t *own, uint64_t *w) {
+  uint64_t om[8], nm[8];
+  memcpy(om, in, 64);
+  memcpy(nm, in + 64, 64);
+  int64_t rank = -1;
+  for (uint32_t i = 0; i < GX_DIGEST_SLOTS; i++) {
+    if ((nm[i >> 6] >> (i & 63)) & 1) rank++;
+    if ((om[i >> 6] >> (i & 63)) & 1) w[i] = own[i];
+    else memcpy(&w[i], in + 128 + 8 * rank, 8);
+  }
+}
+/* Block b of a row, zero-padded, with own flags on the padding (the lead encoding). */
+static uint32_t row_block(const gx_engine *e, const uint64_t *row, uint32_t b, uint64_t *w, uint8_t *pad) {
+  uint32_t lo = b * GX_DIGEST_SLOTS, n = lo + GX_DIGEST_SLOTS < e->R ? GX_DIGEST_SLOTS : e->R - lo;
+  for (uint32_t i = 0; i < GX_DIGEST_SLOTS; i++) {
+    w[i] = i < n ? row[lo + i] : 0;
+    pad[i] = i >= n;
+  }
+  return n;
+}
+
+/* Block digest of gx.h: slots [b*512, min(R, (b+1)*512)) of a row, the lead literal count on top. */
 static void block_digest(const gx_engine *e, const uint64_t *row, uint32_t b, uint64_t *d0, uint64_t *d1) {
   uint64_t s0 = 0, s1 = 0;
   uint32_t lo = b * GX_DIGEST_SLOTS, hi = lo + GX_DIGEST_SLOTS < e->R ? lo + GX_DIGEST_SLOTS : e->R;
@@ -912,8 +959,11 @@ static void block_digest(const gx_engine *e, const uint64_t *row, uint32_t b, ui
     s0 += mix64(row[i] ^ ((uint64_t)i * 0xD6E8FEB86659FD93ull));
     s1 += mix64(row[i] + (uint64_t)i * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
   }
+  uint64_t w[GX_DIGEST_SLOTS];
+  uint8_t pad[GX_DIGEST_SLOTS];
+  row_block(e, row, b, w, pad);
   *d0 = s0;
-  *d1 = s1;
+  *d1 = (s1 & ((1ull << 54) - 1)) | (uint64_t)enc_block(w, pad, NULL) << 54;
 }
 
 /* The cross-shard pairs of this round, in message order. */
@@ -1111,7 +1161,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->srvt = (gx_server_times *)malloc(sizeof(gx_server_times) * H * H);
   e->vlc = (int64_t *)malloc(sizeof(int64_t) * H);
   e->nblk = (e->R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
-  e->x_round = e->x_delta_round = -1;
+  e->x_round = e->x_delta_round = e->x_ret_round = -1;
   if (e->G > 1) {
     size_t hl = e->hi - e->lo;
     e->x_t = (uint32_t *)calloc(hl, sizeof(uint32_t));
@@ -1120,9 +1170,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
     e->x_run = (uint8_t *)calloc(hl, 1);
     if (p->fd_enable && p->fd_push_pull_state) e->x_rsnap = (uint64_t *)calloc(hl * H, sizeof(uint64_t));
     e->x_dig = (uint64_t *)calloc(hl * e->nblk * 2, sizeof(uint64_t));
-    e->x_diff = (uint8_t *)calloc(hl * e->nblk, 1);
-    e->x_cnt = (uint32_t *)calloc(hl, sizeof(uint32_t));
-    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_run || !e->x_dig || !e->x_diff || !e->x_cnt ||
+    e->x_blk = (uint8_t *)calloc(hl * e->nblk, 1);
+    e->x_lt = (uint16_t *)calloc(hl * e->nblk, sizeof(uint16_t));
+    e->x_nlead = (uint32_t *)calloc(hl, sizeof(uint32_t));
+    e->x_nfol = (uint32_t *)calloc(hl, sizeof(uint32_t));
+    e->x_rsz = (uint64_t *)calloc(hl, sizeof(uint64_t));
+    if (!e->x_t || !e->x_mine || !e->x_first || !e->x_run || !e->x_dig || !e->x_blk || !e->x_lt ||
+        !e->x_nlead || !e->x_nfol || !e->x_rsz ||
         (p->fd_enable && p->fd_push_pull_state && !e->x_rsnap)) {
       gx_destroy(e);
       return GX_ENOMEM;
@@ -1179,8 +1233,11 @@ int gx_destroy(gx_engine *e) {
   free(e->x_run);
   free(e->x_rsnap);
   free(e->x_dig);
-  free(e->x_diff);
-  free(e->x_cnt);
+  free(e->x_blk);
+  free(e->x_lt);
+  free(e->x_nlead);
+  free(e->x_nfol);
+  free(e->x_rsz);
   free(e->mem);
   free(e->fdh);
   free(e->fdm);
@@ -1678,7 +1735,7 @@ static int ae_initiator_runs(const gx_engine *e, uint32_t mine, uint32_t k) {
 int gx_ae_bytes(gx_engine *e, uint64_t *bytes) {
   if (!e || !bytes) return GX_EINVAL;
   for (uint32_t g = 0; g < e->G; g++) bytes[g] = 0;
-  e->x_round = e->x_delta_round = -1;
+  e->x_round = e->x_delta_round = e->x_ret_round = -1;
   e->x_n = 0;
   if (!ae_round(e) || e->G < 2) return GX_OK;
   ae_cross_build(e);
@@ -1723,11 +1780,19 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   return GX_OK;
 }
 
+static uint64_t enc_bytes(uint32_t lits) { return 128 + 8ull * lits; }
+static uint64_t pair_dest(const gx_engine *e, uint32_t k, const uint32_t *pa, const uint32_t *pb) {
+  uint32_t t = e->x_t[k];
+  return shard_of(e, e->x_first[k] ? pb[t] : pa[t]);
+}
+
+/* Received digests -> which blocks differ and who leads each (the fewer literals; ties: the
+ * pair's first host). Sizes of this side's lead messages per shard. */
 int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *out) {
   if (!e || !out || (bytes && !digests)) return GX_EINVAL;
   for (uint32_t g = 0; g < e->G; g++) out[g] = 0;
-  e->x_delta_round = -1;
-  e->x_total = 0;
+  e->x_delta_round = e->x_ret_round = -1;
+  e->x_total = e->x_lin = 0;
   if (!ae_round(e) || e->G < 2) return bytes ? GX_EINVAL : GX_OK;
   if (e->x_round != e->round || bytes != e->x_n * dig_bytes(e)) return GX_EINVAL;
   uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
@@ -1742,20 +1807,29 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
     e->x_run[k] = (uint8_t)(!e->p.fd_enable ||
                             (e->x_first[k] ? ae_initiator_runs(e, e->x_mine[k], k) : (hdr[3] & 1u) != 0));
     if (pp_state(e)) memcpy(&e->x_rsnap[(size_t)k * e->H], m + 16 + 16ull * e->nblk, 8ull * e->H);
-    uint32_t n = 0;
+    uint64_t sz = 16, in = 16;
+    e->x_nlead[k] = e->x_nfol[k] = 0;
     for (uint32_t b = 0; b < e->nblk; b++) {
       uint64_t theirs[2];
       memcpy(theirs, m + 16 + 16ull * b, 16);
       const uint64_t *mine = &e->x_dig[((size_t)k * e->nblk + b) * 2];
-      uint8_t differ = e->x_run[k] && (theirs[0] != mine[0] || theirs[1] != mine[1]);
-      e->x_diff[(size_t)k * e->nblk + b] = differ;
-      n += differ;
+      uint32_t lm = (uint32_t)(mine[1] >> 54), lt = (uint32_t)(theirs[1] >> 54);
+      uint8_t kind = X_SAME;
+      if (e->x_run[k] && (theirs[0] != mine[0] || theirs[1] != mine[1]))
+        kind = lm < lt || (lm == lt && e->x_first[k]) ? X_LEAD : X_FOLLOW;
+      e->x_blk[(size_t)k * e->nblk + b] = kind;
+      e->x_lt[(size_t)k * e->nblk + b] = (uint16_t)lt;
+      if (kind == X_LEAD) {
+        e->x_nlead[k]++;
+        sz += enc_bytes(lm);
+      } else if (kind == X_FOLLOW) {
+        e->x_nfol[k]++;
+        in += enc_bytes(lt);
+      }
     }
-    e->x_cnt[k] = n;
-    uint64_t sz = 16 + (uint64_t)n * 8 * GX_DIGEST_SLOTS;
-    uint32_t t = e->x_t[k], other = e->x_first[k] ? pb[t] : pa[t];
-    out[shard_of(e, other)] += sz;
+    out[pair_dest(e, k, pa, pb)] += sz;
     e->x_total += sz;
+    e->x_lin += in;
   }
   free(pa);
   free(pb);
@@ -1768,50 +1842,199 @@ int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!ae_round(e) || e->G < 2 || !e->x_n) return GX_OK;
   if (e->x_delta_round != e->round || cap < e->x_total) return GX_EINVAL;
   uint8_t *p = (uint8_t *)buf;
+  uint64_t w[GX_DIGEST_SLOTS];
+  uint8_t pad[GX_DIGEST_SLOTS];
   for (uint32_t k = 0; k < e->x_n; k++) {
-    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->x_cnt[k], 0};
+    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->x_nlead[k], 0};
     memcpy(p, hdr, 16);
     p += 16;
     const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
     for (uint32_t b = 0; b < e->nblk; b++) {
-      if (!e->x_diff[(size_t)k * e->nblk + b]) continue;
-      uint64_t blk[GX_DIGEST_SLOTS] = {0};
-      for (uint32_t i = 0; i < GX_DIGEST_SLOTS && b * GX_DIGEST_SLOTS + i < e->R; i++) blk[i] = row[b * GX_DIGEST_SLOTS + i];
-      memcpy(p, blk, sizeof blk);
-      p += sizeof blk;
+      if (e->x_blk[(size_t)k * e->nblk + b] != X_LEAD) continue;
+      row_block(e, row, b, w, pad);
+      p += enc_bytes(enc_block(w, pad, p));
     }
   }
   return GX_OK;
 }
 
-/* Cross-shard pairs merge the partner's row rebuilt from the delta: sent blocks from the message,
- * the other blocks from this host's own row (their digests matched); then the local pairs. */
-int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
-  if (!e || (bytes && !buf)) return GX_EINVAL;
+/* Same effect on the partner's merge as its own word (gx.h "return"): x = the partner's word,
+ * y = this side's. */
+static int ret_own(const gx_engine *e, uint64_t x, uint64_t y) {
+  int xa = st_of(x) == GX_ABSENT, ya = st_of(y) == GX_ABSENT;
+  if (xa || ya) return xa && ya;
+  int64_t thr = now_of(e) - e->p.tombstone_lifespan_ns - e->p.stale_fudge_ns;
+  int sx = ts_of(x) < thr, sy = ts_of(y) < thr;
+  if (sy) return sx;
+  return !sx && ts_of(y) <= ts_of(x);
+}
+/* The return blocks of pair k: the partner's lead blocks (message at `m`) against this side's
+ * row. Writes the message when out != NULL; returns its size. */
+static uint64_t ret_message(gx_engine *e, uint32_t k, const uint8_t *m, uint8_t *out) {
+  const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
+  uint32_t nf = e->x_nfol[k], j = 0;
+  uint64_t sz = 16 + 4ull * (nf + (nf & 1));
+  if (out) {
+    uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], nf, 0};
+    memcpy(out, hdr, 16);
+    memset(out + 16, 0, 4ull * (nf + (nf & 1)));
+  }
+  const uint8_t *in = m + 16;
+  uint64_t x[GX_DIGEST_SLOTS], y[GX_DIGEST_SLOTS];
+  uint8_t own[GX_DIGEST_SLOTS];
+  for (uint32_t b = 0; b < e->nblk; b++) {
+    if (e->x_blk[(size_t)k * e->nblk + b] != X_FOLLOW) continue;
+    uint32_t n = row_block(e, row, b, y, own);
+    dec_block(in, y, x);
+    in += enc_bytes(e->x_lt[(size_t)k * e->nblk + b]);
+    for (uint32_t i = 0; i < n; i++) own[i] = (uint8_t)ret_own(e, x[i], y[i]);
+    uint32_t L = enc_block(y, own, out ? out + sz : NULL);
+    if (out) memcpy(out + 16 + 4ull * j, &L, 4);
+    j++;
+    sz += enc_bytes(L);
+  }
+  return sz;
+}
+/* Received lead blocks: message k of the lead inbox starts at the returned offsets. */
+static int lead_offsets(const gx_engine *e, const void *lead, uint64_t bytes, uint64_t *off) {
+  if (e->x_delta_round != e->round || bytes != e->x_lin || (bytes && !lead)) return GX_EINVAL;
+  uint64_t o = 0;
+  for (uint32_t k = 0; k < e->x_n; k++) {
+    uint32_t hdr[4];
+    memcpy(hdr, (const uint8_t *)lead + o, 16);
+    if (hdr[0] != e->x_t[k] || hdr[2] != e->x_nfol[k]) return GX_EINVAL;
+    off[k] = o;
+    o += 16;
+    for (uint32_t b = 0; b < e->nblk; b++)
+      if (e->x_blk[(size_t)k * e->nblk + b] == X_FOLLOW) o += enc_bytes(e->x_lt[(size_t)k * e->nblk + b]);
+  }
+  return GX_OK;
+}
+
+int gx_ae_return_bytes(gx_engine *e, const void *lead, uint64_t lead_bytes, uint64_t *out) {
+  if (!e || !out) return GX_EINVAL;
+  for (uint32_t g = 0; g < e->G; g++) out[g] = 0;
+  e->x_ret_round = -1;
+  e->x_rtotal = 0;
+  if (!ae_round(e) || e->G < 2 || !e->x_n) return lead_bytes ? GX_EINVAL : GX_OK;
+  uint64_t *off = (uint64_t *)malloc(8ull * e->x_n);
+  int rc = lead_offsets(e, lead, lead_bytes, off);
+  if (rc == GX_OK) {
+    uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+    uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+    ae_pairs(e, pa, pb);
+    for (uint32_t k = 0; k < e->x_n; k++) {
+      e->x_rsz[k] = ret_message(e, k, (const uint8_t *)lead + off[k], NULL);
+      out[pair_dest(e, k, pa, pb)] += 8 + e->x_rsz[k];  /* size table entry + message */
+      e->x_rtotal += 8 + e->x_rsz[k];
+    }
+    free(pa);
+    free(pb);
+    e->x_ret_round = e->round;
+  }
+  free(off);
+  return rc;
+}
+
+int gx_ae_return_pack(gx_engine *e, const void *lead, uint64_t lead_bytes, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (!ae_round(e) || e->G < 2 || !e->x_n) return GX_OK;
+  if (e->x_ret_round != e->round || cap < e->x_rtotal) return GX_EINVAL;
+  uint64_t *off = (uint64_t *)malloc(8ull * e->x_n);
+  int rc = lead_offsets(e, lead, lead_bytes, off);
+  if (rc == GX_OK) {
+    uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+    uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+    ae_pairs(e, pa, pb);
+    uint8_t *p = (uint8_t *)buf;
+    for (uint32_t k0 = 0; k0 < e->x_n;) { /* one segment per destination shard: sizes, messages */
+      uint32_t k1 = k0;
+      while (k1 < e->x_n && pair_dest(e, k1, pa, pb) == pair_dest(e, k0, pa, pb)) k1++;
+      for (uint32_t k = k0; k < k1; k++) memcpy(p + 8ull * (k - k0), &e->x_rsz[k], 8);
+      p += 8ull * (k1 - k0);
+      for (uint32_t k = k0; k < k1; k++) p += ret_message(e, k, (const uint8_t *)lead + off[k], p);
+      k0 = k1;
+    }
+    free(pa);
+    free(pb);
+  }
+  free(off);
+  return rc;
+}
+
+/* Cross-shard pairs merge the partner's row rebuilt from the exchange: blocks whose digests
+ * matched from this host's own row, blocks the partner led from its lead blocks, blocks this side
+ * led from the partner's return blocks; then the local pairs. */
+int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void *ret, uint64_t ret_bytes) {
+  if (!e || (lead_bytes && !lead) || (ret_bytes && !ret)) return GX_EINVAL;
   if (!ae_round(e)) return GX_OK;
   if (e->G > 1 && e->x_n) {
-    if (e->x_delta_round != e->round || bytes != e->x_total) return GX_EINVAL;
+    uint64_t *loff = (uint64_t *)malloc(8ull * e->x_n), *roff = (uint64_t *)malloc(8ull * e->x_n);
+    int rc = lead_offsets(e, lead, lead_bytes, loff);
+    /* return inbox: segments in source-shard order, each a size table and the messages */
+    uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+    uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+    ae_pairs(e, pa, pb);
+    uint64_t o = 0;
+    for (uint32_t k0 = 0; rc == GX_OK && k0 < e->x_n;) {
+      uint32_t k1 = k0;
+      while (k1 < e->x_n && pair_dest(e, k1, pa, pb) == pair_dest(e, k0, pa, pb)) k1++;
+      uint64_t mo = o + 8ull * (k1 - k0);
+      for (uint32_t k = k0; k < k1 && rc == GX_OK; k++) {
+        uint64_t sz;
+        if (o + 8ull * (k - k0) + 8 > ret_bytes) { rc = GX_EINVAL; break; }
+        memcpy(&sz, (const uint8_t *)ret + o + 8ull * (k - k0), 8);
+        roff[k] = mo;
+        uint32_t hdr[4];
+        if (mo + 16 > ret_bytes) { rc = GX_EINVAL; break; }
+        memcpy(hdr, (const uint8_t *)ret + mo, 16);
+        if (hdr[0] != e->x_t[k] || hdr[2] != e->x_nlead[k]) rc = GX_EINVAL;
+        mo += sz;
+      }
+      o = mo;
+      k0 = k1;
+    }
+    if (rc == GX_OK && o != ret_bytes) rc = GX_EINVAL;
+    free(pa);
+    free(pb);
+    if (rc != GX_OK) {
+      free(loff);
+      free(roff);
+      return rc;
+    }
     int64_t now = now_of(e);
     uint64_t *row = (uint64_t *)malloc(8ull * e->R);
-    const uint8_t *p = (const uint8_t *)buf;
+    uint64_t ownw[GX_DIGEST_SLOTS], w[GX_DIGEST_SLOTS];
+    uint8_t pad[GX_DIGEST_SLOTS];
     for (uint32_t k = 0; k < e->x_n; k++) {
-      uint32_t hdr[4];
-      memcpy(hdr, p, 16);
-      p += 16;
-      if (!e->x_run[k]) continue; /* the pair does not run: its delta holds no blocks */
+      if (!e->x_run[k]) continue; /* the pair does not run: no blocks either way */
       const uint64_t *own = &e->view[(size_t)e->x_mine[k] * e->R];
+      const uint8_t *lp = (const uint8_t *)lead + loff[k] + 16;
+      const uint8_t *rm = (const uint8_t *)ret + roff[k];
+      uint32_t nl = e->x_nlead[k], j = 0;
+      const uint8_t *rp = rm + 16 + 4ull * (nl + (nl & 1));
       for (uint32_t b = 0; b < e->nblk; b++) {
-        uint32_t lo = b * GX_DIGEST_SLOTS, n = lo + GX_DIGEST_SLOTS < e->R ? GX_DIGEST_SLOTS : e->R - lo;
-        if (e->x_diff[(size_t)k * e->nblk + b]) {
-          memcpy(&row[lo], p, 8ull * n);
-          p += 8 * GX_DIGEST_SLOTS;
+        uint32_t lo = b * GX_DIGEST_SLOTS, n = row_block(e, own, b, ownw, pad);
+        uint8_t kind = e->x_blk[(size_t)k * e->nblk + b];
+        if (kind == X_FOLLOW) {
+          dec_block(lp, ownw, w);
+          lp += enc_bytes(e->x_lt[(size_t)k * e->nblk + b]);
+        } else if (kind == X_LEAD) {
+          uint32_t L;
+          memcpy(&L, rm + 16 + 4ull * j, 4);
+          j++;
+          dec_block(rp, ownw, w);
+          rp += enc_bytes(L);
         } else {
-          memcpy(&row[lo], &own[lo], 8ull * n);
+          memcpy(w, ownw, sizeof w);
         }
+        memcpy(&row[lo], w, 8ull * n);
       }
       ae_merge_row(e, e->x_mine[k], row, e->x_first[k], now);
     }
     free(row);
+    free(loff);
+    free(roff);
     if (pp_state(e)) /* pushPull's membership half: the partner's round-start list */
       for (uint32_t k = 0; k < e->x_n; k++)
         if (e->x_run[k]) fd_merge_state(e, e->x_mine[k], &e->x_rsnap[(size_t)k * e->H]);

@@ -196,7 +196,7 @@ ABI_FUNCS = [
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
     "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
-    "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
+    "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
     "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
     "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers", "gx_fd_converged", "gx_fd_merge_state",
@@ -240,7 +240,7 @@ def _declare(lib):
         "gx_round_send": ([vp], i32), "gx_outbox_bytes": ([vp, vp], i32),
         "gx_outbox_pack": ([vp, vp, C.c_uint64], i32), "gx_inbox_unpack": ([vp, vp, C.c_uint64], i32),
         "gx_round_merge": ([vp], i32), "gx_ae_bytes": ([vp, vp], i32),
-        "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64], i32),
+        "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64, vp, C.c_uint64], i32),
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
         "gx_ae_merge_local": ([vp], i32),
         "gx_read_server_times": ([vp, u32, u32, u32, vp], i32),
@@ -250,6 +250,8 @@ def _declare(lib):
         "gx_listener_drain": ([vp, u32, u32, P(GxChangeEvent), u32, P(u32)], i32),
         "gx_ae_delta_bytes": ([vp, vp, C.c_uint64, vp], i32),
         "gx_ae_delta_pack": ([vp, vp, C.c_uint64], i32),
+        "gx_ae_return_bytes": ([vp, vp, C.c_uint64, vp], i32),
+        "gx_ae_return_pack": ([vp, vp, C.c_uint64, vp, C.c_uint64], i32),
         "gx_get_broadcasts_bytes": ([vp, u32, u32, u32, P(GxService), u32, P(u32)], i32),
         "gx_set_static_bytes": ([vp, u32, u32, P(u16)], i32),
         "gx_message_bytes": ([vp, P(GxService), u32, P(u32)], i32),
@@ -660,7 +662,7 @@ class Engine:
         check(self.lib.gx_ae_pack(self.h, C.c_void_p(ptr), cap), "gx_ae_pack")
 
     def ae_delta_bytes(self, ptr: int, nbytes: int) -> np.ndarray:
-        """Compare the received push-pull digests with this shard's; delta sizes per shard."""
+        """Compare the received push-pull digests with this shard's; lead-message sizes per shard."""
         out = np.zeros(self.G, dtype=np.uint64)
         check(self.lib.gx_ae_delta_bytes(self.h, C.c_void_p(ptr), nbytes, out.ctypes.data_as(C.c_void_p)),
               "gx_ae_delta_bytes")
@@ -669,8 +671,25 @@ class Engine:
     def ae_delta_pack(self, ptr: int, cap: int):
         check(self.lib.gx_ae_delta_pack(self.h, C.c_void_p(ptr), cap), "gx_ae_delta_pack")
 
-    def ae_merge(self, ptr: int, nbytes: int):
-        check(self.lib.gx_ae_merge(self.h, C.c_void_p(ptr), nbytes), "gx_ae_merge")
+    def ae_return_bytes(self, ptr: int, nbytes: int) -> np.ndarray:
+        """Received lead blocks -> sizes of the return messages per shard."""
+        out = np.zeros(self.G, dtype=np.uint64)
+        check(self.lib.gx_ae_return_bytes(self.h, C.c_void_p(ptr), nbytes, out.ctypes.data_as(C.c_void_p)),
+              "gx_ae_return_bytes")
+        return out
+
+    def ae_return_pack(self, lead_ptr: int, lead_bytes: int, ptr: int, cap: int):
+        check(self.lib.gx_ae_return_pack(self.h, C.c_void_p(lead_ptr), lead_bytes, C.c_void_p(ptr), cap),
+              "gx_ae_return_pack")
+
+    def ae_merge(self, lead_ptr: int = 0, lead_bytes: int = 0, ret_ptr: int = 0, ret_bytes: int = 0):
+        check(self.lib.gx_ae_merge(self.h, C.c_void_p(lead_ptr), lead_bytes, C.c_void_p(ret_ptr), ret_bytes),
+              "gx_ae_merge")
+
+    def is_ae_round(self) -> bool:
+        """This round is a push-pull round (every shard agrees: the schedule is global)."""
+        p = self.params
+        return bool(p.ae_period_rounds) and self.round % p.ae_period_rounds == p.ae_phase
 
     def ae_merge_local(self):
         """Start this shard's local push-pull pairs (asynchronous; overlaps the row exchange)."""

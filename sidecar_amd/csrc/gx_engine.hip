@@ -77,14 +77,19 @@ struct gx_engine {
   // push-pull digests / delta (per cross pair k, in pack order = receive order)
   uint32_t nblk, nmw;
   ulonglong2 *ae_dig;  // [Hl][nblk] own digests
-  uint32_t *ae_mask;   // [Hl][nmw] differing blocks
-  uint32_t *ae_cnt;    // [Hl] differing block count
-  uint64_t *ae_off;    // [Hl] delta message offsets
+  uint32_t *ae_mask;   // [Hl][nmw] differing blocks this side leads
+  uint32_t *ae_fmask;  // [Hl][nmw] differing blocks the partner leads
+  uint16_t *ae_lt;     // [Hl][nblk] the partner's literal counts (its digests)
+  uint32_t *ae_cnt;    // [Hl] blocks this side leads
+  uint32_t *ae_nfol;   // [Hl] blocks the partner leads
+  uint64_t *ae_sz;     // [4][Hl] lead message size, partner's lead size, return size, scratch
+  uint64_t *ae_off;    // [4][Hl] lead offsets, lead inbox offsets, return offsets, return table entries
+  uint64_t *ae_rioff;  // [Hl] return inbox offsets
   uint32_t *ae_err;
   std::vector<uint32_t> pack_gstart;  // pack index range per destination shard
   std::vector<uint64_t> delta_off_h;
-  uint64_t delta_total;
-  int ae_delta_round;
+  uint64_t delta_total, lead_in_total, ret_total;
+  int ae_delta_round, ae_ret_round;
   int ae_planned_round;
   int64_t ae_local_round;
   // listeners: host-side channels fed from the per-view device event logs
@@ -430,7 +435,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_cnt, e->ae_off, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf,
@@ -482,10 +487,11 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ae_prow = nullptr;
   e->ae_pcount = nullptr;
   e->ae_dig = nullptr;
-  e->ae_mask = e->ae_cnt = e->ae_err = nullptr;
-  e->ae_off = nullptr;
-  e->ae_delta_round = -1;
-  e->delta_total = 0;
+  e->ae_mask = e->ae_fmask = e->ae_cnt = e->ae_nfol = e->ae_err = nullptr;
+  e->ae_lt = nullptr;
+  e->ae_sz = e->ae_off = e->ae_rioff = nullptr;
+  e->ae_delta_round = e->ae_ret_round = -1;
+  e->delta_total = e->lead_in_total = e->ret_total = 0;
   e->n_plan = e->n_pack = e->n_plan_rows = 0;
   e->ae_planned_round = -1;
   e->ae_local_round = -1;
@@ -573,8 +579,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
     e->nmw = (e->nblk + 31) / 32;
     ALLOC(e->ae_dig, sizeof(ulonglong2) * H * e->nblk);
     ALLOC(e->ae_mask, sizeof(uint32_t) * H * e->nmw);
+    ALLOC(e->ae_fmask, sizeof(uint32_t) * H * e->nmw);
+    ALLOC(e->ae_lt, sizeof(uint16_t) * H * e->nblk);
     ALLOC(e->ae_cnt, sizeof(uint32_t) * H);
-    ALLOC(e->ae_off, sizeof(uint64_t) * H);
+    ALLOC(e->ae_nfol, sizeof(uint32_t) * H);
+    ALLOC(e->ae_sz, sizeof(uint64_t) * 4 * H);
+    ALLOC(e->ae_off, sizeof(uint64_t) * 4 * H);
+    ALLOC(e->ae_rioff, sizeof(uint64_t) * H);
     ALLOC(e->ae_err, sizeof(uint32_t));
   }
   hipStream_t s = e->stream;
@@ -1365,43 +1376,47 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   return sync_check(e);
 }
 
+// Received digests -> differing blocks and who leads each; lead message sizes per shard, and the
+// offsets of this side's lead messages and of the partner's in the lead inbox.
 int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *out) {
   if (!e || !out || (bytes && !digests)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   Dev &d = e->d;
   for (uint32_t g = 0; g < d.G; g++) out[g] = 0;
-  e->ae_delta_round = -1;
-  e->delta_total = 0;
+  e->ae_delta_round = e->ae_ret_round = -1;
+  e->delta_total = e->lead_in_total = 0;
   if (d.G < 2 || !ae_round(e)) return bytes ? GX_EINVAL : GX_OK;
   if (e->ae_planned_round != (int)d.round || bytes != e->n_pack * dig_bytes(e)) return GX_EINVAL;
-  std::vector<uint32_t> cnt(e->n_pack);
-  if (e->n_pack) {
+  const uint32_t np = e->n_pack;
+  std::vector<uint64_t> sz(2 * (size_t)np);
+  if (np) {
     HIPCHK(hipMemsetAsync(e->ae_err, 0, sizeof(uint32_t), e->stream));
-    k_ae_mask<<<e->n_pack, 256, 0, e->stream>>>(e->d, (const uint8_t *)digests, e->ae_dig, e->ae_pack_t,
-                                                 e->ae_pack_host, e->ae_pack_other, e->ae_pack_first, e->nblk,
-                                                 e->nmw, e->ae_mask, e->ae_cnt, e->ae_err, e->ae_skip);
+    k_ae_mask<<<np, 256, 0, e->stream>>>(d, (const uint8_t *)digests, e->ae_dig, e->ae_pack_t, e->ae_pack_host,
+                                         e->ae_pack_other, e->ae_pack_first, e->nblk, e->nmw, e->ae_mask,
+                                         e->ae_fmask, e->ae_lt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_sz + np,
+                                         e->ae_err, e->ae_skip);
     if (pp_state(d))  // the partners' member lists ride with their digests
-      k_fd_rsnap<<<1024, 256, 0, e->stream>>>(d, (const uint8_t *)digests, dig_bytes(e), e->nblk, e->n_pack,
-                                               e->fd_rsnap);
+      k_fd_rsnap<<<1024, 256, 0, e->stream>>>(d, (const uint8_t *)digests, dig_bytes(e), e->nblk, np, e->fd_rsnap);
     uint32_t err = 0;
     HIPCHK(hipMemcpyAsync(&err, e->ae_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(cnt.data(), e->ae_cnt, sizeof(uint32_t) * e->n_pack, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(sz.data(), e->ae_sz, sizeof(uint64_t) * 2 * np, hipMemcpyDeviceToHost, e->stream));
     int rc = sync_check(e);
     if (rc) return rc;
     if (err) return GX_EINVAL;  // digests of another pair or another row size
   }
-  e->delta_off_h.resize(e->n_pack);
-  uint64_t o = 0;
+  e->delta_off_h.assign(2 * (size_t)np, 0);
+  uint64_t o = 0, oi = 0;
   for (uint32_t g = 0; g < d.G; g++)
     for (uint32_t k = e->pack_gstart[g]; k < e->pack_gstart[g + 1]; k++) {
       e->delta_off_h[k] = o;
-      uint64_t sz = 16 + (uint64_t)cnt[k] * 8 * GX_DIGEST_SLOTS;
-      out[g] += sz;
-      o += sz;
+      e->delta_off_h[np + k] = oi;
+      out[g] += sz[k];
+      o += sz[k];
+      oi += sz[np + k];
     }
   e->delta_total = o;
-  if (e->n_pack)
-    HIPCHK(hipMemcpy(e->ae_off, e->delta_off_h.data(), sizeof(uint64_t) * e->n_pack, hipMemcpyHostToDevice));
+  e->lead_in_total = oi;
+  if (np) HIPCHK(hipMemcpy(e->ae_off, e->delta_off_h.data(), sizeof(uint64_t) * 2 * np, hipMemcpyHostToDevice));
   e->ae_delta_round = (int)d.round;
   return GX_OK;
 }
@@ -1411,20 +1426,82 @@ int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!e->n_pack) return GX_OK;
   if (e->ae_delta_round != (int)e->d.round || cap < e->delta_total) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  k_ae_delta_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
-                                                     e->ae_off, e->nmw, (uint8_t *)buf);
+  k_ae_lead_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
+                                                    e->ae_off, e->nmw, (uint8_t *)buf);
+  return sync_check(e);
+}
+
+// Received lead blocks -> return message sizes: per destination shard a u64 size table, then the
+// messages (gx.h "return").
+int gx_ae_return_bytes(gx_engine *e, const void *lead, uint64_t lead_bytes, uint64_t *out) {
+  if (!e || !out || (lead_bytes && !lead)) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  Dev &d = e->d;
+  for (uint32_t g = 0; g < d.G; g++) out[g] = 0;
+  e->ae_ret_round = -1;
+  e->ret_total = 0;
+  const uint32_t np = e->n_pack;
+  if (d.G < 2 || !ae_round(e) || !np) return lead_bytes ? GX_EINVAL : GX_OK;
+  if (e->ae_delta_round != (int)d.round || lead_bytes != e->lead_in_total) return GX_EINVAL;
+  k_ae_ret<true><<<np, 256, 0, e->stream>>>(d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
+                                            (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
+                                            e->ae_sz + 2 * np, nullptr, nullptr, nullptr);
+  std::vector<uint64_t> rsz(np);
+  HIPCHK(hipMemcpyAsync(rsz.data(), e->ae_sz + 2 * np, sizeof(uint64_t) * np, hipMemcpyDeviceToHost, e->stream));
+  int rc = sync_check(e);
+  if (rc) return rc;
+  std::vector<uint64_t> off(2 * (size_t)np);  // message offsets, size-table entry offsets
+  uint64_t o = 0;
+  for (uint32_t g = 0; g < d.G; g++) {
+    uint32_t k0 = e->pack_gstart[g], k1 = e->pack_gstart[g + 1];
+    uint64_t seg = o;
+    o += 8ull * (k1 - k0);
+    for (uint32_t k = k0; k < k1; k++) {
+      off[np + k] = seg + 8ull * (k - k0);
+      off[k] = o;
+      o += rsz[k];
+    }
+    out[g] = o - seg;
+  }
+  e->ret_total = o;
+  HIPCHK(hipMemcpy(e->ae_off + 2 * np, off.data(), sizeof(uint64_t) * 2 * np, hipMemcpyHostToDevice));
+  e->ae_ret_round = (int)d.round;
+  return GX_OK;
+}
+
+int gx_ae_return_pack(gx_engine *e, const void *lead, uint64_t lead_bytes, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf) || (lead_bytes && !lead)) return GX_EINVAL;
+  const uint32_t np = e->n_pack;
+  if (!np) return GX_OK;
+  if (e->ae_ret_round != (int)e->d.round || cap < e->ret_total || lead_bytes != e->lead_in_total) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  k_ae_ret<false><<<np, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
+                                             (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
+                                             e->ae_sz + 2 * np, e->ae_off + 2 * np, e->ae_off + 3 * np,
+                                             (uint8_t *)buf);
   return sync_check(e);
 }
 
 // Launch the planned pairs [lo, hi) (received-row pairs first, then shard-local pairs).
-static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *buf) {
+static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *lead, const void *ret) {
   if (hi <= lo) return;
   set_round_fields(e);
   LaunchTimer t(e, GX_K_AE);
+  const uint32_t np = e->n_pack;
+  AeIn in;
+  in.lead = (const uint8_t *)lead;
+  in.ret = (const uint8_t *)ret;
+  in.ioff = e->ae_off + np;
+  in.rioff = e->ae_rioff;
+  in.lmask = e->ae_mask;
+  in.fmask = e->ae_fmask;
+  in.lt = e->ae_lt;
+  in.nlead = e->ae_cnt;
+  in.nmw = e->nmw;
+  in.nblk = e->nblk;
 #define GX_AE_PLAN(V, E)                                                                                     \
-  (E ? k_ae_plan_ev<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo,             \
-                                                  e->ae_pcount + lo, (const uint8_t *)buf, e->ae_off, e->ae_mask, \
-                                                  e->nmw, e->ae_skip)
+  (E ? k_ae_plan_ev<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, \
+                                                                        e->ae_prow + lo, e->ae_pcount + lo, in, e->ae_skip)
   const bool ev = !e->log_views.empty();
   if (e->d.R % 2 == 0 && !ev) GX_AE_PLAN(true, false);
   else if (e->d.R % 2 == 0) GX_AE_PLAN(true, true);
@@ -1438,14 +1515,14 @@ int gx_ae_merge_local(gx_engine *e) {
   HIPCHK(hipSetDevice(e->device));
   if (!ae_round(e) || e->d.G < 2 || e->ae_local_round == e->d.round) return GX_OK;
   if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
-  ae_plan_launch(e, e->n_plan_rows, e->n_plan, nullptr);  // asynchronous: overlaps the exchange
+  ae_plan_launch(e, e->n_plan_rows, e->n_plan, nullptr, nullptr);  // asynchronous: overlaps the exchange
   HIPCHK(hipGetLastError());
   e->ae_local_round = e->d.round;
   return GX_OK;
 }
 
-int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
-  if (!e || (bytes && !buf)) return GX_EINVAL;
+int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void *ret, uint64_t ret_bytes) {
+  if (!e || (lead_bytes && !lead) || (ret_bytes && !ret)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   if (!ae_round(e)) return GX_OK;
   if (e->d.G < 2) {
@@ -1453,9 +1530,29 @@ int gx_ae_merge(gx_engine *e, const void *buf, uint64_t bytes) {
     return rc ? rc : sync_check(e);
   }
   if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
-  if (e->n_plan_rows && (e->ae_delta_round != (int)e->d.round || bytes != e->delta_total)) return GX_EINVAL;
+  const uint32_t np = e->n_pack;
+  if (np) {
+    if (e->ae_ret_round != (int)e->d.round || lead_bytes != e->lead_in_total) return GX_EINVAL;
+    // the return inbox: per source shard a size table, then that shard's messages
+    std::vector<uint64_t> rio(np), tab;
+    uint64_t o = 0;
+    for (uint32_t g = 0; g < e->d.G; g++) {
+      uint32_t k0 = e->pack_gstart[g], k1 = e->pack_gstart[g + 1];
+      if (k1 == k0) continue;
+      if (o + 8ull * (k1 - k0) > ret_bytes) return GX_EINVAL;
+      tab.resize(k1 - k0);
+      HIPCHK(hipMemcpy(tab.data(), (const uint8_t *)ret + o, 8ull * (k1 - k0), hipMemcpyDeviceToHost));
+      o += 8ull * (k1 - k0);
+      for (uint32_t k = k0; k < k1; k++) {
+        rio[k] = o;
+        o += tab[k - k0];
+      }
+    }
+    if (o != ret_bytes) return GX_EINVAL;
+    HIPCHK(hipMemcpy(e->ae_rioff, rio.data(), sizeof(uint64_t) * np, hipMemcpyHostToDevice));
+  }
   bool local_done = e->ae_local_round == e->d.round;
-  ae_plan_launch(e, 0, local_done ? e->n_plan_rows : e->n_plan, buf);
+  ae_plan_launch(e, 0, local_done ? e->n_plan_rows : e->n_plan, lead, ret);
   if (pp_state(e->d) && e->n_plan) {  // pushPull's membership half, every planned pair
     LaunchTimer t(e, GX_K_FD);
     k_fd_pushpull_plan<<<2 * e->n_plan, 64, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_skip,

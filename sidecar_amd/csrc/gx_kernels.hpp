@@ -1072,16 +1072,38 @@ GXD uint32_t ae_book(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t b
 }
 
 // `ext` (when both = false): B is host b's row from another shard (read-only); the pair's
-// exchange is counted where a is the pair's first member (count_ex). With `emask`, ext holds only
-// the 512-slot blocks whose bit is set (ascending); every other block of B is A's own block (the
-// digests matched), which merges with the counts of the identical remote block and no change.
+// exchange is counted where a is the pair's first member (count_ex). With `xs` (cross-shard pair,
+// gx.h "lead"/"return"), B is rebuilt block by block: a block the partner leads is decoded from
+// its lead block, a block this side leads from the partner's return block (own slots = A's
+// word), and every other block is A's own block (the digests matched), which merges with the
+// counts of the identical remote block and no change.
 // PF = tiles whose loads are in flight while one is merged; NT = non-temporal loads.
+struct XSrc {
+  const uint8_t *lead;   // the partner's lead blocks (message + 16)
+  const uint8_t *ret;    // the partner's return blocks (after the count table)
+  const uint32_t *rcnt;  // literal counts of the return blocks
+  const uint32_t *lmask, *fmask;  // blocks this side leads / follows
+  const uint16_t *lt;    // literal counts of the partner's blocks (its digests)
+};
+// Slots s, s + 1 (s even) of an encoded block (gx.h): own slots keep w[], the others take their
+// literal (popcount rank in the neu mask).
+GXD void dec_pair(const uint64_t *enc, uint32_t s, bool v0, bool v1, uint64_t *w) {
+  const uint32_t wi = s >> 6;
+  const uint64_t om = enc[wi], nm = enc[8 + wi];
+  int32_t pre = -1;
+  for (uint32_t i = 0; i < wi; i++) pre += __popcll(enc[8 + i]);
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    const uint32_t b = (s + e) & 63;
+    if ((e ? v1 : v0) && !((om >> b) & 1ull)) w[e] = enc[16 + pre + __popcll(nm & ((2ull << b) - 1ull))];
+  }
+}
 template <bool VEC, int PF = 1, bool NT = false, bool EV = false>
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
                  unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false,
-                 const uint32_t *emask = nullptr) {
+                 const XSrc *xs = nullptr) {
   uint64_t *A = vrow(d, a);
-  uint64_t *B = ext ? const_cast<uint64_t *>(ext) : vrow(d, b);
+  uint64_t *B = xs ? A : ext ? const_cast<uint64_t *>(ext) : vrow(d, b);
   gx_host_state *ha = hst(d, a), *hb = both ? hst(d, b) : ha;
   uint32_t ta0 = ha->fifo_tail, ca0 = ta0 - ha->fifo_head;
   uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
@@ -1108,18 +1130,24 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   // Software pipeline: the next PF 1024-slot tiles' loads are in flight while this tile is
   // merged, written back and (only if something was accepted) compacted.
   uint64_t qa[PF][4], qb[PF][4];
-  uint32_t erank = 0;  // set mask bits below the next block to load
+  uint64_t xo_f = 0, xo_r = 0;  // byte offsets of the next lead / return block (block-uniform)
+  uint32_t xj = 0;
   auto load_tile = [&](uint32_t base, uint64_t *xa, uint64_t *xb) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
       bool v0 = r0 < d.R, v1 = r0 + 1 < d.R;
       const uint64_t *Bp = B + r0;  // B[r0], B[r0 + 1]
-      if (emask && base + GX_DIGEST_SLOTS * h < d.R) {
-        uint32_t blk = (base >> 9) + h;
-        bool sent = (emask[blk >> 5] >> (blk & 31)) & 1u;
-        Bp = sent ? ext + (size_t)erank * GX_DIGEST_SLOTS + (r0 - blk * GX_DIGEST_SLOTS) : A + r0;
-        erank += sent;
+      const uint64_t *enc = nullptr;
+      uint32_t blk = (base >> 9) + h;
+      if (xs && base + GX_DIGEST_SLOTS * h < d.R) {
+        if ((xs->fmask[blk >> 5] >> (blk & 31)) & 1u) {
+          enc = reinterpret_cast<const uint64_t *>(xs->lead + xo_f);
+          xo_f += 128 + 8ull * xs->lt[blk];
+        } else if ((xs->lmask[blk >> 5] >> (blk & 31)) & 1u) {
+          enc = reinterpret_cast<const uint64_t *>(xs->ret + xo_r);
+          xo_r += 128 + 8ull * xs->rcnt[xj++];
+        }
       }
       if (VEC && v0) {
         ulonglong2 pa = ld16<NT>(&A[r0]);
@@ -1134,6 +1162,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         xb[2 * h] = v0 ? Bp[0] : GX_SLOT_ABSENT;
         xb[2 * h + 1] = v1 ? Bp[1] : GX_SLOT_ABSENT;
       }
+      if (enc) dec_pair(enc, r0 - blk * GX_DIGEST_SLOTS, v0, v1, &xb[2 * h]);
     }
   };
   auto merge_tile = [&](uint32_t base, const uint64_t *wa, const uint64_t *wb) {
@@ -1372,11 +1401,18 @@ __global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32
 }
 
 // Sharded push-pull: plan entry i = (a, b, k): k < 0 -> both members here (a <-> b); k >= 0 ->
-// a is here and b's differing blocks are delta message k of `in` (at off[k], mask k): a <- b only.
+// a is here and b is cross pair k, its row rebuilt from the lead and return inboxes: a <- b only.
+struct AeIn {
+  const uint8_t *lead, *ret;         // the two inboxes
+  const uint64_t *ioff, *rioff;      // [k] message offsets in them
+  const uint32_t *lmask, *fmask;     // [k][nmw]
+  const uint16_t *lt;                // [k][nblk]
+  const uint32_t *nlead;             // [k]
+  uint32_t nmw, nblk;
+};
 template <bool VEC, bool EV>
 GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
-                                                  const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
-                                                  const uint32_t *mask, uint32_t nmw, const uint8_t *skip) {
+                      const uint8_t *pcount, const AeIn &in, const uint8_t *skip) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
   uint32_t i = blockIdx.x;
@@ -1387,21 +1423,28 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
   if (k < 0) {
     ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], true, s_wave, s_red);
   } else {
-    const uint64_t *blocks = reinterpret_cast<const uint64_t *>(in + off[k] + 16);
-    ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, blocks, pcount[i] != 0, mask + (size_t)k * nmw);
+    const uint32_t nl = in.nlead[k];
+    const uint8_t *rm = in.ret + in.rioff[k];
+    XSrc xs;
+    xs.lead = in.lead + in.ioff[k] + 16;
+    xs.rcnt = reinterpret_cast<const uint32_t *>(rm + 16);
+    xs.ret = rm + 16 + 4ull * (nl + (nl & 1u));
+    xs.lmask = in.lmask + (size_t)k * in.nmw;
+    xs.fmask = in.fmask + (size_t)k * in.nmw;
+    xs.lt = in.lt + (size_t)k * in.nblk;
+    ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, nullptr, pcount[i] != 0, &xs);
   }
 }
 template <bool VEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae_plan(
-    Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow, const uint8_t *pcount, const uint8_t *in,
-    const uint64_t *off, const uint32_t *mask, uint32_t nmw, const uint8_t *skip) {
-  ae_plan_pair<VEC, false>(d, pa, pb, prow, pcount, in, off, mask, nmw, skip);
+    Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow, const uint8_t *pcount, AeIn in,
+    const uint8_t *skip) {
+  ae_plan_pair<VEC, false>(d, pa, pb, prow, pcount, in, skip);
 }
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_plan_ev(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
-                                                     const uint8_t *pcount, const uint8_t *in, const uint64_t *off,
-                                                     const uint32_t *mask, uint32_t nmw, const uint8_t *skip) {
-  ae_plan_pair<VEC, true>(d, pa, pb, prow, pcount, in, off, mask, nmw, skip);
+                                                     const uint8_t *pcount, AeIn in, const uint8_t *skip) {
+  ae_plan_pair<VEC, true>(d, pa, pb, prow, pcount, in, skip);
 }
 
 // Push-pull digests of this shard's cross-pair rows (gx.h "digest"): one block per pair, one wave
@@ -1436,7 +1479,8 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
   }
   const uint64_t *row = vrow(d, host[k]);
   for (uint32_t b = wv; b < nblk; b += 4) {
-    uint64_t s0 = 0, s1 = 0;
+    uint64_t s0 = 0, s1 = 0, carry = 0;
+    uint32_t lits = 0;  // literal count of the block's lead encoding (neighbour rule, gx.h)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       uint32_t i = b * GX_DIGEST_SLOTS + 2 * (64 * q + lane);
@@ -1458,75 +1502,241 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
         s0 += dig_mix(w1 ^ ((uint64_t)(i + 1) * 0xD6E8FEB86659FD93ull));
         s1 += dig_mix(w1 + (uint64_t)(i + 1) * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
       }
+      uint64_t pw = __shfl_up(w1, 1, 64);  // the slot before 2 * (64q + lane)
+      if (lane == 0) pw = carry;
+      lits += (v0 && ((q == 0 && lane == 0) || w0 != pw)) + (v1 && w1 != w0);
+      carry = __shfl(w1, 63, 64);
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
+    lits = (uint32_t)wave_sum((unsigned long long)lits);
     if (lane == 0) {
-      ulonglong2 dg = make_ulonglong2(s0, s1);
+      ulonglong2 dg = make_ulonglong2(s0, (s1 & ((1ull << 54) - 1)) | (uint64_t)lits << 54);
       own[(size_t)k * nblk + b] = dg;
       *reinterpret_cast<ulonglong2 *>(msg + 16 + 16ull * b) = dg;
     }
   }
 }
 
-// Compare own digests with the partner's (message k of `in`): mask bit b = block b differs.
-// A pair that does not run (failure detector: the initiator's decision) ships no blocks.
+// Compare own digests with the partner's (message k of `in`): the blocks that differ, and who
+// leads each (fewer literals; ties: the pair's first host). Per pair: lead and follow counts, the
+// size of this side's lead message and of the partner's. A pair that does not run (failure
+// detector: the initiator's decision) ships no blocks.
 __global__ __launch_bounds__(256) void k_ae_mask(Dev d, const uint8_t *in, const ulonglong2 *own,
                                                   const uint32_t *pair_t, const uint32_t *host, const uint32_t *other,
-                                                  const uint8_t *first, uint32_t nblk, uint32_t nmw, uint32_t *mask,
-                                                  uint32_t *cnt, uint32_t *err, uint8_t *skip) {
-  __shared__ uint32_t s_n[4];
+                                                  const uint8_t *first, uint32_t nblk, uint32_t nmw, uint32_t *lmask,
+                                                  uint32_t *fmask, uint16_t *lt, uint32_t *nlead, uint32_t *nfol,
+                                                  uint64_t *lsz, uint64_t *isz, uint32_t *err, uint8_t *skip) {
+  __shared__ unsigned long long s_n[4][3];
   const uint32_t k = blockIdx.x;
   const uint8_t *msg = in + (size_t)k * dig_stride(d, nblk);
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(msg);
   if (threadIdx.x == 0 && (hdr[0] != pair_t[k] || hdr[2] != nblk)) atomicOr(err, 1u);
   const bool runs = !d.p.fd_enable || (first[k] ? ae_initiator_runs(d, host[k], other[k]) : (hdr[3] & 1u) != 0);
   if (threadIdx.x == 0) skip[k] = runs ? 0 : 1;
-  uint32_t n = 0;
+  unsigned long long n = 0, bl = 0, bi = 0;  // n: lead count | follow count << 32
   for (uint32_t w = threadIdx.x; w < nmw; w += blockDim.x) {
-    uint32_t bits = 0;
+    uint32_t lb = 0, fb = 0;
     for (uint32_t j = 0; j < 32; j++) {
       uint32_t b = w * 32 + j;
       if (b >= nblk) break;
       ulonglong2 x = own[(size_t)k * nblk + b];
       ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(msg + 16 + 16ull * b);
-      if (runs && (x.x != y.x || x.y != y.y)) bits |= 1u << j;
+      uint32_t lm = (uint32_t)(x.y >> 54), ly = (uint32_t)(y.y >> 54);
+      lt[(size_t)k * nblk + b] = (uint16_t)ly;
+      if (runs && (x.x != y.x || x.y != y.y)) {
+        if (lm < ly || (lm == ly && first[k])) {
+          lb |= 1u << j;
+          bl += 128 + 8ull * lm;
+        } else {
+          fb |= 1u << j;
+          bi += 128 + 8ull * ly;
+        }
+      }
     }
-    mask[(size_t)k * nmw + w] = bits;
-    n += __popc(bits);
+    lmask[(size_t)k * nmw + w] = lb;
+    fmask[(size_t)k * nmw + w] = fb;
+    n += __popc(lb) | ((unsigned long long)__popc(fb) << 32);
   }
-  n = (uint32_t)wave_sum(n);
-  if ((threadIdx.x & 63) == 0) s_n[threadIdx.x >> 6] = n;
+  n = wave_sum(n);
+  bl = wave_sum(bl);
+  bi = wave_sum(bi);
+  const uint32_t wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_n[wv][0] = n;
+    s_n[wv][1] = bl;
+    s_n[wv][2] = bi;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) cnt[k] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+  if (threadIdx.x == 0) {
+    unsigned long long tn = 0, tl = 0, ti = 0;
+    for (int q = 0; q < 4; q++) {
+      tn += s_n[q][0];
+      tl += s_n[q][1];
+      ti += s_n[q][2];
+    }
+    nlead[k] = (uint32_t)tn;
+    nfol[k] = (uint32_t)(tn >> 32);
+    lsz[k] = 16 + tl;
+    isz[k] = 16 + ti;
+  }
 }
 
-// The differing blocks of each cross-pair row (gx.h "delta"), message k at off[k].
-__global__ __launch_bounds__(256) void k_ae_delta_pack(Dev d, const uint32_t *host, const uint32_t *pair_t,
-                                                        const uint32_t *mask, const uint32_t *cnt, const uint64_t *off,
-                                                        uint32_t nmw, uint8_t *out) {
-  const uint32_t k = blockIdx.x, t = threadIdx.x;
+// Own flags of the padding past the row's end in mask word q of a block with n slots.
+GXD uint64_t pad_mask(uint32_t n, uint32_t q) {
+  return n >= 64 * (q + 1) ? 0ull : n <= 64 * q ? ~0ull : ~0ull << (n - 64 * q);
+}
+// Block-wide encoding of one block (gx.h "encoded block"): thread t holds slots t and t + 256
+// (words w[], own flags own[], new-literal flags nw[]); writes the masks and the literals at enc.
+GXD void enc_store(uint64_t *enc, const uint64_t *w, const bool *ownf, const bool *nw, unsigned long long *s_om,
+                   unsigned long long *s_nm) {
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (nw[h]) {
+      const uint32_t wi = 4 * h + wv;
+      uint32_t rank = __popcll(s_nm[wi] & ((1ull << lane) - 1ull));
+      for (uint32_t q = 0; q < wi; q++) rank += __popcll(s_nm[q]);
+      enc[16 + rank] = w[h];
+    }
+  }
+  if (t < 8) {
+    enc[t] = s_om[t];
+    enc[8 + t] = s_nm[t];
+  }
+}
+
+// Lead messages (gx.h "lead"): the blocks this side leads, run-length coded, at off[k].
+__global__ __launch_bounds__(256) void k_ae_lead_pack(Dev d, const uint32_t *host, const uint32_t *pair_t,
+                                                       const uint32_t *lmask, const uint32_t *nlead,
+                                                       const uint64_t *off, uint32_t nmw, uint8_t *out) {
+  __shared__ unsigned long long s_om[8], s_nm[8];
+  const uint32_t k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   uint8_t *msg = out + off[k];
   if (t == 0) {
     uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
     hdr[0] = pair_t[k];
     hdr[1] = host[k];
-    hdr[2] = cnt[k];
+    hdr[2] = nlead[k];
     hdr[3] = 0;
   }
   const uint64_t *row = vrow(d, host[k]);
-  uint32_t j = 0;
-  for (uint32_t w = 0; w < nmw; w++) {
-    uint32_t bits = mask[(size_t)k * nmw + w];
+  uint64_t o = 16;
+  for (uint32_t mw = 0; mw < nmw; mw++) {
+    uint32_t bits = lmask[(size_t)k * nmw + mw];
     while (bits) {
-      uint32_t blk = w * 32 + (uint32_t)__builtin_ctz(bits);
+      const uint32_t blk = mw * 32 + (uint32_t)__builtin_ctz(bits);
       bits &= bits - 1;
-      uint32_t i = blk * GX_DIGEST_SLOTS + 2 * t;  // 256 threads x 2 words = one block
-      uint64_t w0 = i < d.R ? row[i] : 0, w1 = i + 1 < d.R ? row[i + 1] : 0;
-      *reinterpret_cast<ulonglong2 *>(msg + 16 + (size_t)j * 8 * GX_DIGEST_SLOTS + 16ull * t) = make_ulonglong2(w0, w1);
-      j++;
+      const uint32_t lo = blk * GX_DIGEST_SLOTS, n = lo + GX_DIGEST_SLOTS <= d.R ? GX_DIGEST_SLOTS : d.R - lo;
+      uint64_t w[2];
+      bool ownf[2], nw[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t s = 256 * h + t;
+        const bool v = s < n;
+        w[h] = v ? row[lo + s] : 0;
+        const uint64_t p = v && s > 0 ? row[lo + s - 1] : 0;
+        ownf[h] = !v;
+        nw[h] = v && (s == 0 || w[h] != p);
+        const unsigned long long m = __ballot(nw[h]);
+        if (lane == 0) {
+          s_nm[4 * h + wv] = m;
+          s_om[4 * h + wv] = pad_mask(n, 4 * h + wv);
+        }
+      }
+      __syncthreads();
+      enc_store(reinterpret_cast<uint64_t *>(msg + o), w, ownf, nw, s_om, s_nm);
+      uint32_t L = 0;
+      for (int q = 0; q < 8; q++) L += __popcll(s_nm[q]);
+      o += 128 + 8ull * L;
+      __syncthreads();
     }
   }
+}
+
+// Return messages (gx.h "return"): for every block the partner leads, this side's words for the
+// partner's merge; own slots where merging them would act exactly like the partner's own word.
+// COUNT: sizes only (rsz[k]); else the messages at roff[k] and their size-table entries.
+GXD bool ret_own(const Dev &d, uint64_t x, uint64_t y) {
+  const bool xa = st_of(x) == GX_ABSENT, ya = st_of(y) == GX_ABSENT;
+  if (xa || ya) return xa && ya;
+  const int64_t thr = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+  const bool sx = ts_of(x) < thr, sy = ts_of(y) < thr;
+  if (sy) return sx;
+  return !sx && ts_of(y) <= ts_of(x);
+}
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_ae_ret(Dev d, const uint32_t *host, const uint32_t *pair_t,
+                                                 const uint32_t *fmask, const uint32_t *nfol, const uint16_t *lt,
+                                                 const uint8_t *lead, const uint64_t *ioff, uint32_t nblk,
+                                                 uint32_t nmw, uint64_t *rsz, const uint64_t *roff,
+                                                 const uint64_t *rtab, uint8_t *out) {
+  __shared__ unsigned long long s_om[8], s_nm[8], s_xm[8];
+  const uint32_t k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nf = nfol[k];
+  const uint8_t *lm = lead + ioff[k];
+  uint8_t *msg = COUNT ? nullptr : out + roff[k];
+  if (!COUNT && t == 0) {
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
+    hdr[0] = pair_t[k];
+    hdr[1] = host[k];
+    hdr[2] = nf;
+    hdr[3] = 0;
+    if (nf & 1u) hdr[4 + nf] = 0;
+    *reinterpret_cast<uint64_t *>(out + rtab[k]) = rsz[k];
+  }
+  const uint64_t *row = vrow(d, host[k]);
+  uint64_t li = 16, o = 16 + 4ull * (nf + (nf & 1u));
+  uint32_t j = 0;
+  for (uint32_t mw = 0; mw < nmw; mw++) {
+    uint32_t bits = fmask[(size_t)k * nmw + mw];
+    while (bits) {
+      const uint32_t blk = mw * 32 + (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      const uint32_t lo = blk * GX_DIGEST_SLOTS, n = lo + GX_DIGEST_SLOTS <= d.R ? GX_DIGEST_SLOTS : d.R - lo;
+      const uint64_t *xe = reinterpret_cast<const uint64_t *>(lm + li);  // the partner's lead block
+      li += 128 + 8ull * lt[(size_t)k * nblk + blk];
+      if (t < 8) s_xm[t] = xe[8 + t];
+      __syncthreads();
+      uint64_t y[2];
+      bool ownf[2], nw[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t s = 256 * h + t, wi = 4 * h + wv;
+        const bool v = s < n;
+        y[h] = v ? row[lo + s] : 0;
+        ownf[h] = true;
+        if (v) {
+          uint32_t rank = __popcll(s_xm[wi] & ((2ull << lane) - 1ull)) - 1;
+          for (uint32_t q = 0; q < wi; q++) rank += __popcll(s_xm[q]);
+          ownf[h] = ret_own(d, xe[16 + rank], y[h]);
+        }
+        const unsigned long long m = __ballot(ownf[h]);
+        if (lane == 0) s_om[wi] = m;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t s = 256 * h + t;
+        const bool op = s == 0 || ((s_om[(s - 1) >> 6] >> ((s - 1) & 63)) & 1ull);
+        const uint64_t yp = s > 0 && s - 1 < n ? row[lo + s - 1] : 0;
+        nw[h] = !ownf[h] && (op || y[h] != yp);
+        const unsigned long long m = __ballot(nw[h]);
+        if (lane == 0) s_nm[4 * h + wv] = m;
+      }
+      __syncthreads();
+      uint32_t L = 0;
+      for (int q = 0; q < 8; q++) L += __popcll(s_nm[q]);
+      if (!COUNT) {
+        enc_store(reinterpret_cast<uint64_t *>(msg + o), y, ownf, nw, s_om, s_nm);
+        if (t == 0) reinterpret_cast<uint32_t *>(msg + 16)[j] = L;
+      }
+      o += 128 + 8ull * L;
+      j++;
+      __syncthreads();
+    }
+  }
+  if (COUNT && t == 0) rsz[k] = o;
 }
 
 // Outbox: fixed-size slots (16-B header + packet_cap records); slot index per local entry.

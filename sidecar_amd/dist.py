@@ -27,20 +27,26 @@ def _ptr(t: torch.Tensor) -> int:
 class WireBytes:
     """Bytes each exchange moved between shards (this process's shards, sent side)."""
 
-    def __init__(self, R: int):
-        self.R = R
-        self.packets = self.ae_digest = self.ae_delta = self.ae_full_rows = 0
+    def __init__(self, e: Engine):
+        p = e.params
+        self.R = e.H * e.S
+        # one digest message per cross-shard pair (gx.h "digest")
+        self.dig_msg = 16 + 16 * ((self.R + 511) // 512) + (8 * e.H if p.fd_enable and p.fd_push_pull_state else 0)
+        self.packets = self.ae_digest = self.ae_delta = self.ae_lead = self.ae_return = self.ae_full_rows = 0
 
-    def add_ae(self, digest_sizes, delta_sizes):
+    def add_ae(self, digest_sizes, lead_sizes, return_sizes):
         dig = int(np.asarray(digest_sizes).sum())
-        nblk = (self.R + 511) // 512
+        n_msgs = dig // self.dig_msg
         self.ae_digest += dig
-        self.ae_delta += int(np.asarray(delta_sizes).sum())
-        self.ae_full_rows += dig // (16 + 16 * nblk) * (16 + 8 * self.R)  # the same pairs as full rows
+        lead, ret = int(np.asarray(lead_sizes).sum()), int(np.asarray(return_sizes).sum())
+        self.ae_lead += lead
+        self.ae_return += ret
+        self.ae_delta += lead + ret
+        self.ae_full_rows += n_msgs * (16 + 8 * self.R)  # the same pairs' full rows
 
     def as_dict(self):
         return {"packets": self.packets, "ae_digest": self.ae_digest, "ae_delta": self.ae_delta,
-                "ae_full_rows_equivalent": self.ae_full_rows}
+                "ae_lead": self.ae_lead, "ae_return": self.ae_return, "ae_full_rows_equivalent": self.ae_full_rows}
 
 
 class _Shard:
@@ -72,7 +78,7 @@ class LocalShards:
             if self.device.type == "cuda":
                 p.device = self.device.index or 0
             self.shards.append(_Shard(p, lib, self.device))
-        self.wire = WireBytes(self.shards[0].e.H * self.shards[0].e.S)
+        self.wire = WireBytes(self.shards[0].e)
         self.trace_ae = False  # keep each push-pull round's digest and delta inboxes (host copies)
         self.ae_trace = []
 
@@ -111,19 +117,27 @@ class LocalShards:
                 s.e.inbox_unpack(_ptr(x), x.numel())
             for s in self.shards:
                 s.e.round_merge()
-            # push-pull: digests, then the blocks that differ (shard-local pairs overlap both)
-            dig = self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
-                                 after_pack=lambda e: e.ae_merge_local())
-            dig_sizes = self.last_sizes
-            delta_sizes = {id(s.e): s.e.ae_delta_bytes(_ptr(x), x.numel()) for s, x in zip(self.shards, dig)}
-            delta = self._exchange(lambda e: delta_sizes[id(e)], lambda e, p, c: e.ae_delta_pack(p, c))
-            for a, b in zip(dig_sizes, self.last_sizes):
-                self.wire.add_ae(a, b)
-            if self.trace_ae and any(x.numel() for x in dig):
-                self.ae_trace.append(([x.cpu().numpy().tobytes() for x in dig],
-                                      [x.cpu().numpy().tobytes() for x in delta]))
-            for s, x in zip(self.shards, delta):
-                s.e.ae_merge(_ptr(x), x.numel())
+            # push-pull: digests, the blocks each side leads, the partners' return blocks (gx.h);
+            # shard-local pairs overlap the exchanges. Every shard agrees on the AE rounds.
+            if self.shards[0].e.is_ae_round():
+                dig = self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
+                                     after_pack=lambda e: e.ae_merge_local())
+                dig_sizes = self.last_sizes
+                lead_sizes = {id(s.e): s.e.ae_delta_bytes(_ptr(x), x.numel()) for s, x in zip(self.shards, dig)}
+                lead = self._exchange(lambda e: lead_sizes[id(e)], lambda e, p, c: e.ae_delta_pack(p, c))
+                lead_sz = self.last_sizes
+                ret_sizes = {id(s.e): s.e.ae_return_bytes(_ptr(x), x.numel()) for s, x in zip(self.shards, lead)}
+                lead_of = {id(s.e): x for s, x in zip(self.shards, lead)}
+                ret = self._exchange(lambda e: ret_sizes[id(e)],
+                                     lambda e, p, c: e.ae_return_pack(_ptr(lead_of[id(e)]), lead_of[id(e)].numel(), p, c))
+                for a, b, c in zip(dig_sizes, lead_sz, self.last_sizes):
+                    self.wire.add_ae(a, b, c)
+                if self.trace_ae and any(x.numel() for x in dig):
+                    self.ae_trace.append(([x.cpu().numpy().tobytes() for x in dig],
+                                          [x.cpu().numpy().tobytes() for x in lead],
+                                          [x.cpu().numpy().tobytes() for x in ret]))
+                for s, x, y in zip(self.shards, lead, ret):
+                    s.e.ae_merge(_ptr(x), x.numel(), _ptr(y), y.numel())
             for s in self.shards:
                 s.e.round_end()
 
@@ -165,7 +179,7 @@ class DistShard:
             p.device = self.device.index or 0
         self.s = _Shard(p, lib, self.device)
         self.e = self.s.e
-        self.wire = WireBytes(self.e.H * self.e.S)
+        self.wire = WireBytes(self.e)
 
     CHUNK = 256 << 20  # bytes per peer per all-to-all call
 
@@ -215,13 +229,16 @@ class DistShard:
             x = self._exchange(ob, e.outbox_pack)
             e.inbox_unpack(_ptr(x), x.numel())
             e.round_merge()
-            # push-pull: digests, then only the blocks that differ (local pairs overlap both)
-            dsz = e.ae_bytes()
-            dig = self._exchange(dsz, e.ae_pack, after_pack=e.ae_merge_local)
-            sizes = e.ae_delta_bytes(_ptr(dig), dig.numel())
-            self.wire.add_ae(dsz, sizes)
-            delta = self._exchange(sizes, e.ae_delta_pack)
-            e.ae_merge(_ptr(delta), delta.numel())
+            # push-pull: digests, lead blocks, return blocks (local pairs overlap the exchanges)
+            if e.is_ae_round():
+                dsz = e.ae_bytes()
+                dig = self._exchange(dsz, e.ae_pack, after_pack=e.ae_merge_local)
+                lsz = e.ae_delta_bytes(_ptr(dig), dig.numel())
+                lead = self._exchange(lsz, e.ae_delta_pack)
+                rsz = e.ae_return_bytes(_ptr(lead), lead.numel())
+                ret = self._exchange(rsz, lambda p, c: e.ae_return_pack(_ptr(lead), lead.numel(), p, c))
+                self.wire.add_ae(dsz, lsz, rsz)
+                e.ae_merge(_ptr(lead), lead.numel(), _ptr(ret), ret.numel())
             e.round_end()
 
     def stats(self) -> dict:

@@ -37,8 +37,9 @@ def test_gpu_shards_cfg2_small(gx_lib):
 
 
 def test_gpu_push_pull_wire_identical_to_oracle(gx_lib, oracle_lib):
-    """The HIP engine's digest and delta messages (gx.h wire formats) equal the oracle's byte for
-    byte, round after round, so either implementation can sit on either end of an exchange."""
+    """The HIP engine's digest, lead and return messages (gx.h wire formats) equal the oracle's
+    byte for byte, round after round, so either implementation can sit on either end of an
+    exchange."""
     kw = dict(n_hosts=160, n_services=16, init_mode=2, ae_period_rounds=4, partition_start=0,
               partition_end=10, storm_round=2, churn_ppm=40000, queue_cap=4096)
     g = LocalShards(gx_lib, 3, device="cuda:0", **kw)
@@ -47,12 +48,13 @@ def test_gpu_push_pull_wire_identical_to_oracle(gx_lib, oracle_lib):
     g.run_rounds(30)
     o.run_rounds(30)
     assert len(g.ae_trace) == len(o.ae_trace) > 0
-    for i, ((gd, gx), (od, ox)) in enumerate(zip(g.ae_trace, o.ae_trace)):
+    for i, ((gd, gl, gr), (od, ol, orr)) in enumerate(zip(g.ae_trace, o.ae_trace)):
         assert gd == od, f"digest inbox, push-pull round {i}"
-        assert gx == ox, f"delta inbox, push-pull round {i}"
+        assert gl == ol, f"lead inbox, push-pull round {i}"
+        assert gr == orr, f"return inbox, push-pull round {i}"
     assert g.wire.as_dict() == o.wire.as_dict()
     w = g.wire.as_dict()
-    assert w["ae_delta"] < w["ae_full_rows_equivalent"]
+    assert 0 < w["ae_lead"] and 0 < w["ae_return"] and w["ae_delta"] < w["ae_full_rows_equivalent"]
     assert g.stats() == o.stats()
     assert all((a.read_views() == b.read_views()).all() for a, b in zip(g.engines, o.engines))
 

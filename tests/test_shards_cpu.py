@@ -126,7 +126,8 @@ def test_gloo_world2_matches_whole(oracle_lib, name):
 
 
 def test_delta_ships_only_differing_blocks(oracle_lib):
-    """Push-pull across shards sends digests, then only the 512-slot blocks that differ: a
+    """Push-pull across shards sends digests, then only the 512-slot blocks that differ (each led
+    by one side, run-length coded, and answered with the words that change the leader's merge): a
     converged (warm) cluster ships no blocks at all; after a storm the delta is a fraction of
     the full rows; the views stay identical to the unsharded run either way."""
     kw = dict(n_hosts=96, n_services=16, init_mode=2, ae_period_rounds=5, partition_start=0,
@@ -138,9 +139,9 @@ def test_delta_ships_only_differing_blocks(oracle_lib):
     w = sh.wire.as_dict()
     assert w["ae_digest"] > 0 and w["ae_full_rows_equivalent"] > 0
     n_msgs = w["ae_digest"] // (16 + 16 * 3)
-    assert w["ae_delta"] == 16 * n_msgs  # headers only
+    assert w["ae_lead"] == 16 * n_msgs and w["ae_return"] == (8 + 16) * n_msgs  # headers only
     whole.run_rounds(29)
     sh.run_rounds(29)
     assert_sharded_equal(whole, sh, "delta")
     w = sh.wire.as_dict()
-    assert 16 * n_msgs < w["ae_delta"] < w["ae_full_rows_equivalent"]
+    assert 40 * n_msgs < w["ae_delta"] < w["ae_full_rows_equivalent"]
