@@ -313,10 +313,11 @@ int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + recei
  * (lead blocks) -> exchange -> gx_ae_return_bytes (received lead blocks) -> gx_ae_return_pack ->
  * exchange -> gx_ae_merge (both inboxes).
  * Digest of block b = slots [b*512, min(R, (b+1)*512)) of a row, i = slot index in the row,
- * w = slot word, mix(z) = SplitMix64 (z += 0x9E3779B97F4A7C15, then its two xor-shift-multiply
- * steps and the final xor-shift), sums mod 2^64, L = literal count of the block's lead encoding:
- *   d0 = sum_i mix(w ^ (i * 0xD6E8FEB86659FD93)),
- *   d1 = (sum_i mix(w + i * 0xC2B2AE3D27D4EB4F + 0x165667B19E3779F9) mod 2^54) | L << 54 */
+ * w = slot word, sums mod 2^64, L = literal count of the block's lead encoding, u32 arithmetic
+ * mod 2^32 in h: x = w ^ (i << 40) ^ i, lo/hi = its halves, a = (lo ^ rotl32(hi, 16)) * 0x85EBCA6B,
+ * b = (hi ^ a >> 15) * 0xC2B2AE35, a = (a ^ b >> 13) * 0x27D4EB2F, a ^= a >> 16,
+ * b = (b ^ a >> 11) * 0x165667B1, b ^= b >> 15, h_i = a << 32 | b:
+ *   d0 = sum_i h_i,  d1 = (sum_i (h_i ^ (h_i >> 29)) mod 2^54) | L << 54 */
 #define GX_DIGEST_SLOTS 512
 int gx_ae_bytes(gx_engine *e, uint64_t *bytes_per_shard); /* digest messages; 0s unless a push-pull round */
 int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap);

@@ -951,13 +951,26 @@ static uint32_t row_block(const gx_engine *e, const uint64_t *row, uint32_t b, u
   return n;
 }
 
+/* Slot hash of the block digest (gx.h): 32-bit multiply-xorshift rounds over (word, slot). */
+static uint64_t dig_hash(uint64_t w, uint32_t i) {
+  uint64_t x = w ^ ((uint64_t)i << 40) ^ i;
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t a = (lo ^ ((hi << 16) | (hi >> 16))) * 0x85EBCA6Bu;
+  uint32_t b = (hi ^ (a >> 15)) * 0xC2B2AE35u;
+  a = (a ^ (b >> 13)) * 0x27D4EB2Fu;
+  a ^= a >> 16;
+  b = (b ^ (a >> 11)) * 0x165667B1u;
+  b ^= b >> 15;
+  return (uint64_t)a << 32 | b;
+}
 /* Block digest of gx.h: slots [b*512, min(R, (b+1)*512)) of a row, the lead literal count on top. */
 static void block_digest(const gx_engine *e, const uint64_t *row, uint32_t b, uint64_t *d0, uint64_t *d1) {
   uint64_t s0 = 0, s1 = 0;
   uint32_t lo = b * GX_DIGEST_SLOTS, hi = lo + GX_DIGEST_SLOTS < e->R ? lo + GX_DIGEST_SLOTS : e->R;
   for (uint32_t i = lo; i < hi; i++) {
-    s0 += mix64(row[i] ^ ((uint64_t)i * 0xD6E8FEB86659FD93ull));
-    s1 += mix64(row[i] + (uint64_t)i * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+    uint64_t h = dig_hash(row[i], i);
+    s0 += h;
+    s1 += h ^ (h >> 29);
   }
   uint64_t w[GX_DIGEST_SLOTS];
   uint8_t pad[GX_DIGEST_SLOTS];

@@ -46,7 +46,12 @@ def minmax(engines):
 
 t0 = time.perf_counter()
 w = Engine(default_params(lib, **kw), lib=lib)
-w.run_rounds(ROUNDS)
+whole_round = []
+for r in range(ROUNDS):
+    a = time.perf_counter()
+    w.run_rounds(1)
+    torch.cuda.synchronize()
+    whole_round.append(time.perf_counter() - a)
 ref = (w.stats(), w.digests(), *minmax([w]))
 t_whole = time.perf_counter() - t0
 w.close()
@@ -70,6 +75,9 @@ ok = {
 }
 out = {"config": f"cfg5 schedule at H={kw['n_hosts']}", "G": G, "rounds": ROUNDS, "identical": ok, "wire_bytes": sh.wire.as_dict(),
        "wall_s": {"unsharded": round(t_whole, 2), "sharded_on_one_gpu": round(t_sharded, 2)},
-       "slowest_rounds": sorted(((round(x * 1e3, 1), i) for i, x in enumerate(per_round)), reverse=True)[:6]}
+       "slowest_rounds": sorted(((round(x * 1e3, 1), i) for i, x in enumerate(per_round)), reverse=True)[:6],
+       # rounds without push-pull or storm: host-side cost of the phase calls (G shards in turn)
+       "median_gossip_round_ms": {"unsharded": round(1e3 * float(np.median([x for i, x in enumerate(whole_round) if i % 10 and i != 5])), 3),
+                                  "sharded_on_one_gpu": round(1e3 * float(np.median([x for i, x in enumerate(per_round) if i % 10 and i != 5])), 3)}}
 print(json.dumps(out), flush=True)
 assert all(ok.values()), ok

@@ -67,6 +67,7 @@ struct gx_engine {
   grec *own_list;
   // sharded rounds: outbox entry list and push-pull plan (device), rebuilt per round
   uint32_t *ob_entries;
+  uint32_t *ob_counts;  // [G] packets per destination shard, then [chunks][G] counts and offsets
   uint32_t n_ob;
   uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t, *ae_pack_other;
   uint8_t *ae_pack_first, *ae_skip;  // this side is the pair's initiator; the pair does not run
@@ -80,6 +81,7 @@ struct gx_engine {
   uint32_t *ae_mask;   // [Hl][nmw] differing blocks this side leads
   uint32_t *ae_fmask;  // [Hl][nmw] differing blocks the partner leads
   uint16_t *ae_lt;     // [Hl][nblk] the partner's literal counts (its digests)
+  uint32_t *ae_bcnt;   // [Hl][nblk] own blocks: present | stale << 16 (digest pass)
   uint32_t *ae_cnt;    // [Hl] blocks this side leads
   uint32_t *ae_nfol;   // [Hl] blocks the partner leads
   uint64_t *ae_sz;     // [4][Hl] lead message size, partner's lead size, return size, scratch
@@ -435,7 +437,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf,
@@ -480,6 +482,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->digest_buf = nullptr;
   e->stream = nullptr;
   e->ob_entries = nullptr;
+  e->ob_counts = nullptr;
   e->n_ob = 0;
   e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = e->ae_pack_other = nullptr;
   e->ae_pack_first = e->ae_skip = nullptr;
@@ -489,6 +492,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ae_dig = nullptr;
   e->ae_mask = e->ae_fmask = e->ae_cnt = e->ae_nfol = e->ae_err = nullptr;
   e->ae_lt = nullptr;
+  e->ae_bcnt = nullptr;
   e->ae_sz = e->ae_off = e->ae_rioff = nullptr;
   e->ae_delta_round = e->ae_ret_round = -1;
   e->delta_total = e->lead_in_total = e->ret_total = 0;
@@ -564,6 +568,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
   if (d.G > 1) {
     ALLOC(e->ob_entries, sizeof(uint32_t) * H * K);
+    ALLOC(e->ob_counts, sizeof(uint32_t) * p->n_shards * (1 + 2 * ((H * K + 255) / 256)));
     size_t np = Hg / 2 + 1;
     ALLOC(e->ae_pa, sizeof(uint32_t) * np);
     ALLOC(e->ae_pb, sizeof(uint32_t) * np);
@@ -581,6 +586,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->ae_mask, sizeof(uint32_t) * H * e->nmw);
     ALLOC(e->ae_fmask, sizeof(uint32_t) * H * e->nmw);
     ALLOC(e->ae_lt, sizeof(uint16_t) * H * e->nblk);
+    ALLOC(e->ae_bcnt, sizeof(uint32_t) * H * e->nblk);
     ALLOC(e->ae_cnt, sizeof(uint32_t) * H);
     ALLOC(e->ae_nfol, sizeof(uint32_t) * H);
     ALLOC(e->ae_sz, sizeof(uint64_t) * 4 * H);
@@ -1182,8 +1188,9 @@ int gx_host_digests(gx_engine *e, uint64_t *out) {
 }
 
 // ------------------------------------------------------------------------- sharded rounds --
-static uint32_t shard_of(const Dev &d, uint32_t v) {
-  uint32_t g = 0;
+static uint32_t shard_of(const Dev &d, uint32_t v) {  // shard g owns [floor(g H / G), floor((g + 1) H / G))
+  uint32_t g = (uint32_t)(((uint64_t)v * d.G) / d.H);
+  while (g > 0 && (uint32_t)(((uint64_t)g * d.H) / d.G) > v) g--;
   while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= v) g++;
   return g;
 }
@@ -1210,22 +1217,24 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
   e->n_ob = 0;
   if (d.G < 2 || !d.K) return GX_OK;
-  size_t ne = (size_t)d.Hl * d.K;
-  std::vector<uint32_t> len(ne), dst(ne), nfd(ne, 0);
-  HIPCHK(hipStreamSynchronize(e->stream));
-  HIPCHK(hipMemcpy(len.data(), d.msg_len, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(dst.data(), d.msg_dst, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
-  if (d.p.fd_enable) HIPCHK(hipMemcpy(nfd.data(), d.fd_len, sizeof(uint32_t) * ne, hipMemcpyDeviceToHost));
-  std::vector<std::vector<uint32_t>> per(d.G);
-  for (size_t i = 0; i < ne; i++)
-    if ((len[i] || nfd[i]) && !own(e, dst[i])) per[shard_of(d, dst[i])].push_back((uint32_t)i);
-  std::vector<uint32_t> order;
+  set_round_fields(e);
+  const size_t ne = (size_t)d.Hl * d.K;
+  const uint32_t nchunk = (uint32_t)((ne + 255) / 256);
+  uint32_t *ccnt = e->ob_counts + d.G, *off = ccnt + (size_t)nchunk * d.G;
+  const size_t lds = sizeof(uint32_t) * 4 * d.G;
+  k_ob_count<<<nchunk, 256, lds, e->stream>>>(d, ccnt);
+  k_ob_scan<<<1, 256, 0, e->stream>>>(d, ccnt, nchunk, off, e->ob_counts);
+  k_ob_fill<<<nchunk, 256, lds, e->stream>>>(d, off, e->ob_entries);
+  std::vector<uint32_t> cnt(d.G);
+  HIPCHK(hipMemcpyAsync(cnt.data(), e->ob_counts, sizeof(uint32_t) * d.G, hipMemcpyDeviceToHost, e->stream));
+  int rc = sync_check(e);
+  if (rc) return rc;
+  uint64_t n = 0;
   for (uint32_t g = 0; g < d.G; g++) {
-    bytes[g] = per[g].size() * slot_bytes(d);
-    order.insert(order.end(), per[g].begin(), per[g].end());
+    bytes[g] = cnt[g] * slot_bytes(d);
+    n += cnt[g];
   }
-  e->n_ob = (uint32_t)order.size();
-  if (e->n_ob) HIPCHK(hipMemcpy(e->ob_entries, order.data(), sizeof(uint32_t) * e->n_ob, hipMemcpyHostToDevice));
+  e->n_ob = (uint32_t)n;
   return GX_OK;
 }
 
@@ -1271,64 +1280,66 @@ static int ae_plan(gx_engine *e, uint64_t *bytes) {
     groups[0][0] = 0; groups[0][1] = d.H;
     ng = 1;
   }
-  for (int gi = 0; gi < ng; gi++) {
-    uint32_t base = groups[gi][0], m = groups[gi][1];
-    uint64_t key = rng4(d.p.seed, ST_AE, (uint64_t)d.round, base, 0);
-    for (uint32_t t = 0; t + 1 < m; t += 2) {
-      pa.push_back(base + feistel_perm(key, t, m));
-      pb.push_back(base + feistel_perm(key, t + 1, m));
-    }
+  // the pair schedule (Feistel permutations, as k_ae draws it) on the device, read back once
+  uint32_t n0 = groups[0][1] / 2, n1 = ng > 1 ? groups[1][1] / 2 : 0, np = n0 + n1;
+  uint64_t key0 = rng4(d.p.seed, ST_AE, (uint64_t)d.round, groups[0][0], 0);
+  uint64_t key1 = ng > 1 ? rng4(d.p.seed, ST_AE, (uint64_t)d.round, groups[1][0], 0) : 0;
+  pa.resize(np);
+  pb.resize(np);
+  if (np) {
+    k_ae_pairs<<<(np + 255) / 256, 256, 0, e->stream>>>(groups[0][0], groups[0][1], key0, groups[1][0],
+                                                         ng > 1 ? groups[1][1] : 0, key1, n0, np, e->ae_pa, e->ae_pb);
+    HIPCHK(hipMemcpyAsync(pa.data(), e->ae_pa, 4ull * np, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(pb.data(), e->ae_pb, 4ull * np, hipMemcpyDeviceToHost, e->stream));
+    int rc = sync_check(e);
+    if (rc) return rc;
   }
   // a pair with a crashed member does not run (both shards skip it alike; pair indices unchanged)
   std::vector<uint8_t> runs(pa.size(), 1);
   if (d.departures)
     for (size_t t = 0; t < pa.size(); t++)
       runs[t] = !departed_at(d.p, d.round, pa[t]) && !departed_at(d.p, d.round, pb[t]);
+  // one pass over the pairs: cross pairs bucketed by the partner's shard (messages go out and
+  // come in grouped by shard, ascending t, so cross pair k has the same index both ways), then
+  // the pairs with both hosts here
+  std::vector<std::vector<uint32_t>> by_g(d.G);
+  std::vector<uint32_t> local_t;
+  for (size_t t = 0; t < pa.size(); t++) {
+    if (!runs[t]) continue;
+    bool la = own(e, pa[t]), lb = own(e, pb[t]);
+    if (la && lb) local_t.push_back((uint32_t)t);
+    else if (la != lb) by_g[shard_of(d, la ? pb[t] : pa[t])].push_back((uint32_t)t);
+  }
   std::vector<uint32_t> plan_a, plan_b, pack_host, pack_t, pack_other;
   std::vector<uint8_t> pack_first;
   std::vector<int32_t> plan_row;
   std::vector<uint8_t> plan_cnt;
   for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
   e->pack_gstart.assign(d.G + 1, 0);
-  for (uint32_t g = 0; g < d.G; g++) {  // digests (then deltas) to send to shard g (ascending t)
+  int32_t row = 0;
+  for (uint32_t g = 0; g < d.G; g++) {
     e->pack_gstart[g] = (uint32_t)pack_host.size();
-    if (g == d.gid) continue;
-    for (size_t t = 0; t < pa.size(); t++) {
-      bool la = own(e, pa[t]), lb = own(e, pb[t]);
-      if (la == lb || !runs[t]) continue;
+    for (uint32_t t : by_g[g]) {
+      bool la = own(e, pa[t]);
       uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
-      if (shard_of(d, other) != g) continue;
       pack_host.push_back(mine);
-      pack_t.push_back((uint32_t)t);
+      pack_t.push_back(t);
       pack_other.push_back(other);
       pack_first.push_back(la ? 1 : 0);
       bytes[g] += dig_bytes(e);
-    }
-  }
-  e->pack_gstart[d.G] = (uint32_t)pack_host.size();
-  // messages received from shard g come in the same (shard, ascending t) order as the ones sent,
-  // so cross pair k has the same index in both directions
-  int32_t row = 0;
-  for (uint32_t g = 0; g < d.G; g++) {
-    if (g == d.gid) continue;
-    for (size_t t = 0; t < pa.size(); t++) {
-      bool la = own(e, pa[t]), lb = own(e, pb[t]);
-      if (la == lb || !runs[t]) continue;
-      uint32_t mine = la ? pa[t] : pb[t], other = la ? pb[t] : pa[t];
-      if (shard_of(d, other) != g) continue;
       plan_a.push_back(mine);
       plan_b.push_back(other);
       plan_row.push_back(row++);
       plan_cnt.push_back(la ? 1 : 0);
     }
   }
-  for (size_t t = 0; t < pa.size(); t++)
-    if (own(e, pa[t]) && own(e, pb[t]) && runs[t]) {
-      plan_a.push_back(pa[t]);
-      plan_b.push_back(pb[t]);
-      plan_row.push_back(-1);
-      plan_cnt.push_back(0);
-    }
+  e->pack_gstart[d.G] = (uint32_t)pack_host.size();
+  for (uint32_t t : local_t) {
+    plan_a.push_back(pa[t]);
+    plan_b.push_back(pb[t]);
+    plan_row.push_back(-1);
+    plan_cnt.push_back(0);
+  }
   e->n_plan = (uint32_t)plan_a.size();
   e->n_plan_rows = (uint32_t)row;
   e->n_pack = (uint32_t)pack_host.size();
@@ -1368,11 +1379,11 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (e->d.R % 2 == 0)
     k_ae_digest<true><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other,
                                                          e->ae_pack_first, (uint8_t *)buf,
-                                                         e->ae_dig, e->nblk);
+                                                         e->ae_dig, e->nblk, e->ae_bcnt);
   else
     k_ae_digest<false><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other,
                                                           e->ae_pack_first, (uint8_t *)buf,
-                                                          e->ae_dig, e->nblk);
+                                                          e->ae_dig, e->nblk, e->ae_bcnt);
   return sync_check(e);
 }
 
@@ -1497,11 +1508,13 @@ static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *l
   in.fmask = e->ae_fmask;
   in.lt = e->ae_lt;
   in.nlead = e->ae_cnt;
+  in.bcnt = e->ae_bcnt;
   in.nmw = e->nmw;
   in.nblk = e->nblk;
+  const bool small = hi - lo < 1024;  // fewer than 4 pairs per CU: per-block bandwidth decides
 #define GX_AE_PLAN(V, E)                                                                                     \
-  (E ? k_ae_plan_ev<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(e->d, e->ae_pa + lo, e->ae_pb + lo, \
-                                                                        e->ae_prow + lo, e->ae_pcount + lo, in, e->ae_skip)
+  (E ? k_ae_plan_ev<V> : small ? k_ae_plan_pf2<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(             \
+      e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo, e->ae_pcount + lo, in, e->ae_skip)
   const bool ev = !e->log_views.empty();
   if (e->d.R % 2 == 0 && !ev) GX_AE_PLAN(true, false);
   else if (e->d.R % 2 == 0) GX_AE_PLAN(true, true);

@@ -1084,6 +1084,7 @@ struct XSrc {
   const uint32_t *rcnt;  // literal counts of the return blocks
   const uint32_t *lmask, *fmask;  // blocks this side leads / follows
   const uint16_t *lt;    // literal counts of the partner's blocks (its digests)
+  const uint32_t *bcnt;  // own blocks: present | stale << 16 (digest pass)
 };
 // Slots s, s + 1 (s even) of an encoded block (gx.h): own slots keep w[], the others take their
 // literal (popcount rank in the neu mask).
@@ -1131,8 +1132,10 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   // merged, written back and (only if something was accepted) compacted.
   uint64_t qa[PF][4], qb[PF][4];
   uint64_t xo_f = 0, xo_r = 0;  // byte offsets of the next lead / return block (block-uniform)
-  uint32_t xj = 0;
-  auto load_tile = [&](uint32_t base, uint64_t *xa, uint64_t *xb) {
+  uint32_t xj = 0, xskip = 0;   // return blocks used; slots of matching blocks not loaded
+  // returns the number of the tile's two blocks that were skipped (cross pairs, digests matched)
+  auto load_tile = [&](uint32_t base, uint64_t *xa, uint64_t *xb) -> uint32_t {
+    uint32_t skipped = 0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
@@ -1147,6 +1150,18 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         } else if ((xs->lmask[blk >> 5] >> (blk & 31)) & 1u) {
           enc = reinterpret_cast<const uint64_t *>(xs->ret + xo_r);
           xo_r += 128 + 8ull * xs->rcnt[xj++];
+        } else {
+          // digests matched: merging the partner's block = merging A's own, which changes
+          // nothing; count its present and stale records from the digest pass, load nothing
+          if (t == 0) {
+            const uint32_t c = xs->bcnt[blk];
+            c_merge += c & 0xffffu;
+            c_stale += c >> 16;
+          }
+          xskip += GX_DIGEST_SLOTS;
+          skipped++;
+          xa[2 * h] = xa[2 * h + 1] = xb[2 * h] = xb[2 * h + 1] = GX_SLOT_ABSENT;
+          continue;
         }
       }
       if (VEC && v0) {
@@ -1164,6 +1179,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       }
       if (enc) dec_pair(enc, r0 - blk * GX_DIGEST_SLOTS, v0, v1, &xb[2 * h]);
     }
+    return skipped;
   };
   auto merge_tile = [&](uint32_t base, const uint64_t *wa, const uint64_t *wb) {
     uint64_t nwa[4], nwb[4];
@@ -1286,9 +1302,12 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       nev_b += done >> 16;
     }
   };
+  uint32_t qk[PF];  // blocks of the tile in flight that were skipped (2 = nothing to merge)
 #pragma unroll
-  for (int s = 0; s < PF; s++)
-    if (s * TILE < d.R) load_tile(s * TILE, qa[s], qb[s]);
+  for (int s = 0; s < PF; s++) {
+    qk[s] = 0;
+    if (s * TILE < d.R) qk[s] = load_tile(s * TILE, qa[s], qb[s]);
+  }
   for (uint32_t base = 0; base < d.R; base += PF * TILE) {
 #pragma unroll
     for (int s = 0; s < PF; s++) {
@@ -1300,8 +1319,9 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
           wa[k] = qa[s][k];
           wb[k] = qb[s][k];
         }
-        if (bs + PF * TILE < d.R) load_tile(bs + PF * TILE, qa[s], qb[s]);
-        merge_tile(bs, wa, wb);
+        const uint32_t sk = qk[s];
+        if (bs + PF * TILE < d.R) qk[s] = load_tile(bs + PF * TILE, qa[s], qb[s]);
+        if (sk < 2) merge_tile(bs, wa, wb);  // block-uniform
       }
     }
   }
@@ -1347,7 +1367,8 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     ctr_atomic(d, C_RETX, oka + (both ? okb : 0));
     ctr_atomic(d, C_QDROP, (na - oka) + (both ? nb - okb : 0));
     ctr_atomic(d, C_AESLOTS, (unsigned long long)d.R * (both ? 2 : 1));
-    kbytes(d, GX_K_AE, 16ull * d.R + 32ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
+    const uint64_t loaded = d.R > xskip ? d.R - xskip : 0;  // cross pairs: matching blocks are not read
+    kbytes(d, GX_K_AE, 16ull * loaded + 32ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
     if (both || count_ex) ctr_atomic(d, C_AEX, 1);
   }
 }
@@ -1408,9 +1429,10 @@ struct AeIn {
   const uint32_t *lmask, *fmask;     // [k][nmw]
   const uint16_t *lt;                // [k][nblk]
   const uint32_t *nlead;             // [k]
+  const uint32_t *bcnt;              // [k][nblk] own blocks' present | stale << 16
   uint32_t nmw, nblk;
 };
-template <bool VEC, bool EV>
+template <bool VEC, bool EV, int PF = 1>
 GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
                       const uint8_t *pcount, const AeIn &in, const uint8_t *skip) {
   __shared__ unsigned long long s_wave[4];
@@ -1421,7 +1443,7 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
     return;  // memberlist pushPull: the initiator (pa) needs the path and sees the partner alive
   if (k >= 0 && skip[k]) return;  // the same decision for a cross-shard pair (digest flag)
   if (k < 0) {
-    ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], true, s_wave, s_red);
+    ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], true, s_wave, s_red);
   } else {
     const uint32_t nl = in.nlead[k];
     const uint8_t *rm = in.ret + in.rioff[k];
@@ -1432,7 +1454,8 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
     xs.lmask = in.lmask + (size_t)k * in.nmw;
     xs.fmask = in.fmask + (size_t)k * in.nmw;
     xs.lt = in.lt + (size_t)k * in.nblk;
-    ae_pair<VEC, 1, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, nullptr, pcount[i] != 0, &xs);
+    xs.bcnt = in.bcnt + (size_t)k * in.nblk;
+    ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, nullptr, pcount[i] != 0, &xs);
   }
 }
 template <bool VEC>
@@ -1441,15 +1464,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const uint8_t *skip) {
   ae_plan_pair<VEC, false>(d, pa, pb, prow, pcount, in, skip);
 }
+// Launches too small to fill the chip (a few pairs per CU): two tiles in flight per block.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_ae_plan_pf2(Dev d, const uint32_t *pa, const uint32_t *pb,
+                                                      const int32_t *prow, const uint8_t *pcount, AeIn in,
+                                                      const uint8_t *skip) {
+  ae_plan_pair<VEC, false, 2>(d, pa, pb, prow, pcount, in, skip);
+}
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_plan_ev(Dev d, const uint32_t *pa, const uint32_t *pb, const int32_t *prow,
                                                      const uint8_t *pcount, AeIn in, const uint8_t *skip) {
   ae_plan_pair<VEC, true>(d, pa, pb, prow, pcount, in, skip);
 }
 
+// Push-pull pairs of this round in global order t (group 0's n0 pairs, then group 1's), drawn
+// like k_ae draws them: (base + perm(2q), base + perm(2q + 1)).
+__global__ void k_ae_pairs(uint32_t base0, uint32_t m0, uint64_t key0, uint32_t base1, uint32_t m1, uint64_t key1,
+                           uint32_t n0, uint32_t np, uint32_t *pa, uint32_t *pb) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= np) return;
+  const bool g1 = t >= n0;
+  const uint32_t q = g1 ? t - n0 : t, base = g1 ? base1 : base0, m = g1 ? m1 : m0;
+  const uint64_t key = g1 ? key1 : key0;
+  pa[t] = base + feistel_perm(key, 2 * q, m);
+  pb[t] = base + feistel_perm(key, 2 * q + 1, m);
+}
+
 // Push-pull digests of this shard's cross-pair rows (gx.h "digest"): one block per pair, one wave
 // per 512-slot block at a time. Also kept in `own` for the comparison.
-GXD uint64_t dig_mix(uint64_t z) { return mix64(z); }
+// Slot hash of the block digest (gx.h): 32-bit multiply-xorshift rounds (no 64-bit multiplies,
+// which cost four 32-bit ones each and made the digest pass ALU-bound).
+GXD uint64_t dig_hash(uint64_t w, uint32_t i) {
+  const uint64_t x = w ^ ((uint64_t)i << 40) ^ i;
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t a = (lo ^ ((hi << 16) | (hi >> 16))) * 0x85EBCA6Bu;
+  uint32_t b = (hi ^ (a >> 15)) * 0xC2B2AE35u;
+  a = (a ^ (b >> 13)) * 0x27D4EB2Fu;
+  a ^= a >> 16;
+  b = (b ^ (a >> 11)) * 0x165667B1u;
+  b ^= b >> 15;
+  return (uint64_t)a << 32 | b;
+}
 // With the failure detector the initiator's side decides whether the pair runs (it needs the
 // path and sees the partner alive, memberlist pushPull) and says so in header word 3.
 GXD bool ae_initiator_runs(const Dev &d, uint32_t mine, uint32_t other) {
@@ -1462,7 +1517,7 @@ GXHD size_t dig_stride(const Dev &d, uint32_t nblk) {
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, const uint32_t *pair_t,
                                                     const uint32_t *other, const uint8_t *first, uint8_t *out,
-                                                    ulonglong2 *own, uint32_t nblk) {
+                                                    ulonglong2 *own, uint32_t nblk, uint32_t *bcnt) {
   const uint32_t k = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint8_t *msg = out + (size_t)k * dig_stride(d, nblk);
   if (d.p.fd_enable && d.p.fd_push_pull_state) {  // the member list, snapshot of this AE round (k_fd_snap)
@@ -1478,43 +1533,61 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
     hdr[3] = d.p.fd_enable && first[k] && ae_initiator_runs(d, host[k], other[k]) ? 1u : 0u;
   }
   const uint64_t *row = vrow(d, host[k]);
-  for (uint32_t b = wv; b < nblk; b += 4) {
-    uint64_t s0 = 0, s1 = 0, carry = 0;
-    uint32_t lits = 0;  // literal count of the block's lead encoding (neighbour rule, gx.h)
+  // software pipeline: the wave's next block is in flight while this one is hashed and reduced
+  ulonglong2 cur[4], nxt[4];
+  auto load_blk = [&](uint32_t b, ulonglong2 *x) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      uint32_t i = b * GX_DIGEST_SLOTS + 2 * (64 * q + lane);
-      uint64_t w0 = 0, w1 = 0;
-      bool v0 = i < d.R, v1 = i + 1 < d.R;
+      const uint32_t i = b * GX_DIGEST_SLOTS + 2 * (64 * q + lane);
+      const bool v0 = i < d.R, v1 = i + 1 < d.R;
       if (VEC && v0) {
-        ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(&row[i]);
-        w0 = x.x;
-        w1 = x.y;
+        x[q] = *reinterpret_cast<const ulonglong2 *>(&row[i]);
       } else {
-        if (v0) w0 = row[i];
-        if (v1) w1 = row[i + 1];
+        x[q].x = v0 ? row[i] : 0;
+        x[q].y = v1 ? row[i + 1] : 0;
       }
+    }
+  };
+  const int64_t thr = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+  if (wv < nblk) load_blk(wv, cur);
+  for (uint32_t b = wv; b < nblk; b += 4) {
+    if (b + 4 < nblk) load_blk(b + 4, nxt);
+    uint64_t s0 = 0, s1 = 0, carry = 0;
+    uint32_t lits = 0;  // literal count of the block's lead encoding (neighbour rule, gx.h)
+    uint32_t cnt = 0;   // present | stale << 16: what merging this block as-is counts
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t i = b * GX_DIGEST_SLOTS + 2 * (64 * q + lane);
+      const uint64_t w0 = cur[q].x, w1 = cur[q].y;
+      const bool v0 = i < d.R, v1 = i + 1 < d.R;
       if (v0) {
-        s0 += dig_mix(w0 ^ ((uint64_t)i * 0xD6E8FEB86659FD93ull));
-        s1 += dig_mix(w0 + (uint64_t)i * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+        const uint64_t h = dig_hash(w0, i);
+        s0 += h;
+        s1 += h ^ (h >> 29);
       }
       if (v1) {
-        s0 += dig_mix(w1 ^ ((uint64_t)(i + 1) * 0xD6E8FEB86659FD93ull));
-        s1 += dig_mix(w1 + (uint64_t)(i + 1) * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull);
+        const uint64_t h = dig_hash(w1, i + 1);
+        s0 += h;
+        s1 += h ^ (h >> 29);
       }
       uint64_t pw = __shfl_up(w1, 1, 64);  // the slot before 2 * (64q + lane)
       if (lane == 0) pw = carry;
       lits += (v0 && ((q == 0 && lane == 0) || w0 != pw)) + (v1 && w1 != w0);
+      if (v0 && st_of(w0) != GX_ABSENT) cnt += 1u + ((uint32_t)(ts_of(w0) < thr) << 16);
+      if (v1 && st_of(w1) != GX_ABSENT) cnt += 1u + ((uint32_t)(ts_of(w1) < thr) << 16);
       carry = __shfl(w1, 63, 64);
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
-    lits = (uint32_t)wave_sum((unsigned long long)lits);
+    const unsigned long long lc = wave_sum((unsigned long long)cnt | ((unsigned long long)lits << 32));
     if (lane == 0) {
-      ulonglong2 dg = make_ulonglong2(s0, (s1 & ((1ull << 54) - 1)) | (uint64_t)lits << 54);
+      bcnt[(size_t)k * nblk + b] = (uint32_t)lc;
+      ulonglong2 dg = make_ulonglong2(s0, (s1 & ((1ull << 54) - 1)) | (uint64_t)(lc >> 32) << 54);
       own[(size_t)k * nblk + b] = dg;
       *reinterpret_cast<ulonglong2 *>(msg + 16 + 16ull * b) = dg;
     }
+#pragma unroll
+    for (int q = 0; q < 4; q++) cur[q] = nxt[q];
   }
 }
 
@@ -1737,6 +1810,73 @@ __global__ __launch_bounds__(256) void k_ae_ret(Dev d, const uint32_t *host, con
     }
   }
   if (COUNT && t == 0) rsz[k] = o;
+}
+
+// Outbox plan on the device: block g lists, in entry order, this shard's packets (records or
+// memberlist messages) whose receiver lives on shard g, after those bound for shards < g; the
+// receiver's shard as in the host's contiguous blocks (floor(g * H / G)).
+GXD uint32_t ob_dest(const Dev &d, size_t i) {
+  const uint32_t len = d.msg_len[i], nfd = d.p.fd_enable ? d.fd_len[i] : 0u, dst = d.msg_dst[i];
+  if (!(len || nfd) || (dst >= d.lo && dst < d.lo + d.Hl)) return d.G;
+  uint32_t g = 0;
+  while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= dst) g++;
+  return g;
+}
+// Three launches over 256-entry chunks: per-chunk counts per shard, one block scans them into
+// offsets (shard-major, chunk order), then each chunk places its entries by wave ballots.
+GXD void ob_chunk_counts(const Dev &d, uint32_t gi, uint32_t *s_cnt) {  // s_cnt[4][G]
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t g = 0; g < d.G; g++) {
+    const unsigned long long m = __ballot(gi == g);
+    if (lane == 0) s_cnt[wv * d.G + g] = (uint32_t)__popcll(m);
+  }
+}
+__global__ __launch_bounds__(256) void k_ob_count(Dev d, uint32_t *cnt) {  // cnt[chunk][G]
+  extern __shared__ uint32_t s_cnt[];
+  const size_t ne = (size_t)d.Hl * d.K, i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  ob_chunk_counts(d, i < ne ? ob_dest(d, i) : d.G, s_cnt);
+  __syncthreads();
+  if (threadIdx.x < d.G) {
+    const uint32_t g = threadIdx.x;
+    cnt[(size_t)blockIdx.x * d.G + g] = s_cnt[g] + s_cnt[d.G + g] + s_cnt[2 * d.G + g] + s_cnt[3 * d.G + g];
+  }
+}
+// off[chunk][g] = entries bound for shards < g + entries for g in earlier chunks; tot[g] per shard
+__global__ __launch_bounds__(256) void k_ob_scan(Dev d, const uint32_t *cnt, uint32_t nchunk, uint32_t *off,
+                                                  uint32_t *tot) {
+  __shared__ unsigned long long s_wave[4];
+  unsigned long long base = 0;
+  for (uint32_t g = 0; g < d.G; g++) {
+    unsigned long long run = base;
+    for (uint32_t c0 = 0; c0 < nchunk; c0 += blockDim.x) {
+      const uint32_t c = c0 + threadIdx.x;
+      const unsigned long long x = c < nchunk ? cnt[(size_t)c * d.G + g] : 0;
+      unsigned long long t;
+      const unsigned long long pre = block_excl_scan64(x, s_wave, t);
+      if (c < nchunk) off[(size_t)c * d.G + g] = (uint32_t)(run + pre);
+      run += t;
+    }
+    if (threadIdx.x == 0) tot[g] = (uint32_t)(run - base);
+    base = run;
+  }
+}
+__global__ __launch_bounds__(256) void k_ob_fill(Dev d, const uint32_t *off, uint32_t *entries) {
+  extern __shared__ uint32_t s_cnt[];
+  const size_t ne = (size_t)d.Hl * d.K, i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t gi = i < ne ? ob_dest(d, i) : d.G;
+  ob_chunk_counts(d, gi, s_cnt);
+  __syncthreads();
+  unsigned long long mine = 0;
+  for (uint32_t g = 0; g < d.G; g++) {
+    const unsigned long long b = __ballot(gi == g);
+    if (gi == g) mine = b;
+  }
+  if (gi < d.G) {
+    uint32_t rank = (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
+    for (uint32_t w = 0; w < wv; w++) rank += s_cnt[w * d.G + gi];
+    entries[off[(size_t)blockIdx.x * d.G + gi] + rank] = (uint32_t)i;
+  }
 }
 
 // Outbox: fixed-size slots (16-B header + packet_cap records); slot index per local entry.

@@ -186,19 +186,20 @@ class DistShard:
     def _exchange(self, sizes: np.ndarray, packer, after_pack=None) -> torch.Tensor:
         """all-to-all of this shard's per-destination messages; returns the inbox (sources ascending)."""
         dist = self.dist
-        send_sizes = torch.tensor(sizes.astype(np.int64), device=self.device)
-        recv_sizes = torch.empty_like(send_sizes)
-        dist.all_to_all_single(recv_sizes, send_sizes, group=self.group)
-        rs = [int(x) for x in recv_sizes.tolist()]
-        ss = [int(x) for x in sizes.tolist()]
+        # every rank learns the whole size matrix in one collective: its receive sizes, and the
+        # number of chunked calls all ranks make
+        mine = torch.tensor(sizes.astype(np.int64), device=self.device)
+        rows = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(rows, mine, group=self.group)
+        m = torch.stack(rows).tolist()  # m[src][dst]
+        ss = [int(x) for x in m[self.rank]]
+        rs = [int(m[src][self.rank]) for src in range(self.world)]
         send = self.s.pack(sizes, packer)
         if after_pack is not None:
             after_pack()  # device work on the engine stream that overlaps the collective
         recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
         # every rank runs the same number of calls: ceil(largest per-peer segment / CHUNK)
-        mx = torch.tensor([max(ss + rs + [0])], dtype=torch.int64, device=self.device)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=self.group)
-        calls = (int(mx.item()) + self.CHUNK - 1) // self.CHUNK
+        calls = (max(max(r) for r in m) + self.CHUNK - 1) // self.CHUNK
         if calls == 1:
             dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
             calls = 0
