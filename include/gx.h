@@ -256,6 +256,16 @@ int gx_destroy(gx_engine *e);
 int gx_set_round(gx_engine *e, int64_t round); /* advance the clock; wakes due sleepers */
 int gx_get_round(gx_engine *e, int64_t *round);
 int gx_enable_timing(gx_engine *e, int on);
+/* Where this engine's device work goes. mode 0: its own stream. GX_STREAM_CALLER: the caller's
+ * HIP stream `stream` (NULL = the default stream), e.g. the stream an exchange layer runs its
+ * collectives on. GX_STREAM_ASYNC: the sharded phase calls below (round_send, outbox_pack,
+ * inbox_unpack, round_merge, ae_pack, ae_delta_pack, ae_return_pack, ae_merge, round_end) return
+ * once their work is queued; the stream orders the exchange after them, and a device error
+ * surfaces at the next call that waits. Calls that return sizes or data wait as before. The
+ * oracle accepts and ignores it. */
+#define GX_STREAM_CALLER 1
+#define GX_STREAM_ASYNC 2
+int gx_set_stream(gx_engine *e, void *stream, int mode);
 
 /* ---- whole-round driver (the hot path) ---------------------------------------------------- */
 /* Runs n_rounds rounds of the seeded schedule (DESIGN.md "Round model"). */

@@ -1801,6 +1801,11 @@ static uint64_t pair_dest(const gx_engine *e, uint32_t k, const uint32_t *pa, co
 
 /* Received digests -> which blocks differ and who leads each (the fewer literals; ties: the
  * pair's first host). Sizes of this side's lead messages per shard. */
+int gx_set_stream(gx_engine *e, void *stream, int mode) {
+  (void)stream;
+  return e && !(mode & ~(GX_STREAM_CALLER | GX_STREAM_ASYNC)) ? GX_OK : GX_EINVAL;
+}
+
 int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_t *out) {
   if (!e || !out || (bytes && !digests)) return GX_EINVAL;
   for (uint32_t g = 0; g < e->G; g++) out[g] = 0;

@@ -196,7 +196,7 @@ ABI_FUNCS = [
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
     "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
-    "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
+    "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_set_stream", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
     "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
     "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers", "gx_fd_converged", "gx_fd_merge_state",
@@ -251,6 +251,7 @@ def _declare(lib):
         "gx_ae_delta_bytes": ([vp, vp, C.c_uint64, vp], i32),
         "gx_ae_delta_pack": ([vp, vp, C.c_uint64], i32),
         "gx_ae_return_bytes": ([vp, vp, C.c_uint64, vp], i32),
+        "gx_set_stream": ([vp, vp, i32], i32),
         "gx_ae_return_pack": ([vp, vp, C.c_uint64, vp, C.c_uint64], i32),
         "gx_get_broadcasts_bytes": ([vp, u32, u32, u32, P(GxService), u32, P(u32)], i32),
         "gx_set_static_bytes": ([vp, u32, u32, P(u16)], i32),
@@ -690,6 +691,12 @@ class Engine:
         """This round is a push-pull round (every shard agrees: the schedule is global)."""
         p = self.params
         return bool(p.ae_period_rounds) and self.round % p.ae_period_rounds == p.ae_phase
+
+    def set_stream(self, stream_ptr, async_phases: bool):
+        """Run this engine's device work on the caller's HIP stream (0 = the default stream; None =
+        the engine's own); with async_phases the sharded phase calls return once queued (gx.h)."""
+        mode = (1 | (2 if async_phases else 0)) if stream_ptr is not None else 0  # gx.h GX_STREAM_*
+        check(self.lib.gx_set_stream(self.h, C.c_void_p(stream_ptr or None), mode), "gx_set_stream")
 
     def ae_merge_local(self):
         """Start this shard's local push-pull pairs (asynchronous; overlaps the row exchange)."""

@@ -56,7 +56,9 @@ struct TimedLaunch {
 
 struct gx_engine {
   Dev d;
-  hipStream_t stream;
+  hipStream_t stream;      // where all device work goes (own_stream, or the caller's: gx_set_stream)
+  hipStream_t own_stream;
+  int async_phases;         // sharded phase calls return without waiting (gx_set_stream)
   int device;
   int timing;
   std::vector<TimedLaunch> pending_ev;
@@ -201,6 +203,16 @@ static int sync_check(gx_engine *e) {
   return e->log_views.empty() ? GX_OK : deliver_events(e);
 }
 
+// End of a sharded phase call: with async phases (and no listeners to feed) the caller's stream
+// orders the next step, so only launch errors are checked here.
+static int phase_done(gx_engine *e) {
+  if (e->async_phases && e->log_views.empty()) {
+    HIPCHK(hipGetLastError());
+    return GX_OK;
+  }
+  return sync_check(e);
+}
+
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // Phases 0-3 (wake, owners, expiry scan, storm, GetBroadcasts) for this engine's hosts.
@@ -333,6 +345,15 @@ static int wake_all(gx_engine *e) {
 extern "C" {
 
 int gx_abi_version(void) { return GX_ABI_VERSION; }
+
+int gx_set_stream(gx_engine *e, void *stream, int mode) {
+  if (!e || (mode & ~(GX_STREAM_CALLER | GX_STREAM_ASYNC))) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipStreamSynchronize(e->stream));  // work queued so far completes first
+  e->stream = (mode & GX_STREAM_CALLER) ? (hipStream_t)stream : e->own_stream;
+  e->async_phases = (mode & GX_STREAM_ASYNC) ? 1 : 0;
+  return GX_OK;
+}
 const char *gx_backend(void) { return "hip-gfx950"; }
 
 void gx_params_default(gx_params *p) {
@@ -445,7 +466,7 @@ int gx_destroy(gx_engine *e) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
-  if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
   return GX_OK;
 }
@@ -480,7 +501,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->api_dev_bytes = 0;
   e->conv_bad = nullptr;
   e->digest_buf = nullptr;
-  e->stream = nullptr;
+  e->stream = e->own_stream = nullptr;
+  e->async_phases = 0;
   e->ob_entries = nullptr;
   e->ob_counts = nullptr;
   e->n_ob = 0;
@@ -519,10 +541,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.SQ = pow2_at_least(64 > d.K * (p->retransmit_rounds + 1) ? 64 : d.K * (p->retransmit_rounds + 1));
   d.DQ = pow2_at_least(d.L + p->pending_cap + 64);
   d.round = 0;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return GX_EIO;
   }
+  e->stream = e->own_stream;
+  e->async_phases = 0;
   // per-host arrays hold this shard's Hl hosts; the message table also takes the packets received
   // from other shards (at most (H - Hl) * K), so it is sized H * K.
   size_t Hg = d.H, H = d.Hl, K = d.K ? d.K : 1;
@@ -1205,7 +1229,7 @@ int gx_round_send(gx_engine *e) {
   if (!e) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   int rc = round_send_impl(e);
-  return rc ? rc : sync_check(e);
+  return rc ? rc : phase_done(e);
 }
 
 // Entries of this shard's packets bound for other shards, grouped by destination shard in key
@@ -1244,7 +1268,7 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (cap < e->n_ob * slot_bytes(e->d)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   k_outbox_pack<<<e->n_ob, 64, 0, e->stream>>>(e->d, e->ob_entries, e->n_ob, (uint8_t *)buf);
-  return sync_check(e);
+  return phase_done(e);
 }
 
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
@@ -1254,14 +1278,14 @@ int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
   HIPCHK(hipSetDevice(e->device));
   if (n) k_inbox_unpack<<<(unsigned)n, 64, 0, e->stream>>>(e->d, (const uint8_t *)buf, (uint32_t)n);
   e->d.n_remote = (uint32_t)n;
-  return sync_check(e);
+  return phase_done(e);
 }
 
 int gx_round_merge(gx_engine *e) {
   if (!e) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   int rc = round_merge_impl(e);
-  return rc ? rc : sync_check(e);
+  return rc ? rc : phase_done(e);
 }
 
 // Push-pull plan of this round (host side): global pairs t -> (a, b); local pairs, rows to send
@@ -1384,7 +1408,7 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
     k_ae_digest<false><<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other,
                                                           e->ae_pack_first, (uint8_t *)buf,
                                                           e->ae_dig, e->nblk, e->ae_bcnt);
-  return sync_check(e);
+  return phase_done(e);
 }
 
 // Received digests -> differing blocks and who leads each; lead message sizes per shard, and the
@@ -1439,7 +1463,7 @@ int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap) {
   HIPCHK(hipSetDevice(e->device));
   k_ae_lead_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
                                                     e->ae_off, e->nmw, (uint8_t *)buf);
-  return sync_check(e);
+  return phase_done(e);
 }
 
 // Received lead blocks -> return message sizes: per destination shard a u64 size table, then the
@@ -1490,7 +1514,7 @@ int gx_ae_return_pack(gx_engine *e, const void *lead, uint64_t lead_bytes, void 
                                              (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
                                              e->ae_sz + 2 * np, e->ae_off + 2 * np, e->ae_off + 3 * np,
                                              (uint8_t *)buf);
-  return sync_check(e);
+  return phase_done(e);
 }
 
 // Launch the planned pairs [lo, hi) (received-row pairs first, then shard-local pairs).
@@ -1554,7 +1578,8 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
       if (k1 == k0) continue;
       if (o + 8ull * (k1 - k0) > ret_bytes) return GX_EINVAL;
       tab.resize(k1 - k0);
-      HIPCHK(hipMemcpy(tab.data(), (const uint8_t *)ret + o, 8ull * (k1 - k0), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpyAsync(tab.data(), (const uint8_t *)ret + o, 8ull * (k1 - k0), hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(hipStreamSynchronize(e->stream));
       o += 8ull * (k1 - k0);
       for (uint32_t k = k0; k < k1; k++) {
         rio[k] = o;
@@ -1571,7 +1596,7 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
     k_fd_pushpull_plan<<<2 * e->n_plan, 64, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_skip,
                                                              e->fd_rsnap);
   }
-  return sync_check(e);
+  return phase_done(e);
 }
 
 int gx_round_end(gx_engine *e) {
@@ -1579,7 +1604,7 @@ int gx_round_end(gx_engine *e) {
   HIPCHK(hipSetDevice(e->device));
   e->d.round++;
   int rc = wake_all(e);
-  return rc ? rc : sync_check(e);
+  return rc ? rc : phase_done(e);
 }
 
 int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {

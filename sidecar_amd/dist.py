@@ -53,10 +53,13 @@ class _Shard:
     def __init__(self, params: GxParams, lib, device: torch.device):
         self.e = Engine(params, lib=lib)
         self.device = device
+        if device.type == "cuda":
+            # the engine queues its work on torch's stream, so packing, the collectives and
+            # unpacking are ordered by the stream; only calls that return sizes wait
+            self.e.set_stream(torch.cuda.current_stream(device).cuda_stream, True)
 
     def sync(self):
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
+        pass  # stream-ordered (CUDA) or synchronous (CPU oracle)
 
     def pack(self, sizes: np.ndarray, packer) -> torch.Tensor:
         buf = torch.empty(int(sizes.sum()), dtype=torch.uint8, device=self.device)
