@@ -377,6 +377,9 @@ int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *i
 /* ---- memberlist Delegate (services_delegate.go) ------------------------------------------- */
 /* NotifyMsg (:72-83) + Start() decode loop (:46-56): the records of one packet -> UpdateService. */
 int gx_notify_msg(gx_engine *e, uint32_t host, const gx_service *recs, uint32_t n);
+/* Batched NotifyMsg over many hosts in one call: recs[i] is delivered to
+ * hosts[i]; each run of consecutive entries with the same host is one message, in order. */
+int gx_notify_msgs(gx_engine *e, const uint32_t *hosts, const gx_service *recs, uint32_t n);
 /* GetBroadcasts(overhead, limit) (:85-144) with packPacket (:186-223). `limit` is the packet
  * budget in records (the caller converts memberlist's byte limit and per-message overhead);
  * GX_LIMIT_DEFAULT = params.packet_cap. 0 means nothing fits (the whole batch stays pending).
@@ -596,6 +599,9 @@ int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */
 int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);
+/* One view unpacked (SURVEY.md §8b gx_read_view): ts_ns[R] (INT64_MIN where the slot is empty)
+ * and status[R] (GX_ABSENT where empty), R = n_hosts * n_services. */
+int gx_read_view(gx_engine *e, uint32_t view, int64_t *ts_ns, uint8_t *status);
 int gx_write_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, const uint64_t *words);
 int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc); /* raw store, no merge rule */
 int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out);

@@ -1561,6 +1561,32 @@ int gx_read_views(gx_engine *e, uint32_t lo, uint32_t hi, uint64_t *out) {
   memcpy(out, &e->view[(size_t)lo * e->R], sizeof(uint64_t) * (size_t)(hi - lo) * e->R);
   return GX_OK;
 }
+int gx_notify_msgs(gx_engine *e, const uint32_t *hosts, const gx_service *recs, uint32_t n) {
+  if (!e || (n && (!hosts || !recs))) return GX_EINVAL;
+  for (uint32_t i = 0; i < n;) {
+    uint32_t j = i + 1;
+    while (j < n && hosts[j] == hosts[i]) j++;
+    int rc = gx_notify_msg(e, hosts[i], recs + i, j - i);
+    if (rc) return rc;
+    i = j;
+  }
+  return GX_OK;
+}
+
+int gx_read_view(gx_engine *e, uint32_t view, int64_t *ts_ns, uint8_t *status) {
+  if (!e || !ts_ns || !status) return GX_EINVAL;
+  size_t R = (size_t)e->R;
+  uint64_t *w = (uint64_t *)malloc(8 * R);
+  if (!w) return GX_ENOMEM;
+  int rc = gx_read_views(e, view, view + 1, w);
+  for (size_t r = 0; rc == GX_OK && r < R; r++) {
+    status[r] = (uint8_t)(w[r] & 7u);
+    ts_ns[r] = status[r] == GX_ABSENT ? INT64_MIN : (int64_t)(w[r] >> 3);
+  }
+  free(w);
+  return rc;
+}
+
 int gx_write_views(gx_engine *e, uint32_t lo, uint32_t hi, const uint64_t *in) {
   if (!e || lo > hi || hi > e->H || (hi > lo && !in)) return GX_EINVAL;
   for (size_t i = 0; i < (size_t)(hi - lo) * e->R; i++) {

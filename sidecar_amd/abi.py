@@ -189,7 +189,7 @@ ABI_FUNCS = [
     "gx_abi_version", "gx_backend", "gx_params_default", "gx_create", "gx_destroy", "gx_set_round",
     "gx_get_round", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
     "gx_tombstone_others", "gx_tombstone_services", "gx_expire_server", "gx_send_services",
-    "gx_broadcast_services", "gx_broadcast_tombstones", "gx_is_new_service", "gx_notify_msg",
+    "gx_broadcast_services", "gx_broadcast_tombstones", "gx_is_new_service", "gx_notify_msg", "gx_notify_msgs", "gx_read_view",
     "gx_get_broadcasts", "gx_local_state", "gx_merge_remote_state", "gx_notify_leave",
     "gx_read_views", "gx_write_views", "gx_write_slot", "gx_read_hosts", "gx_read_queue",
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
@@ -223,6 +223,8 @@ def _declare(lib):
         "gx_broadcast_tombstones": ([vp, u32, P(GxService), u32], i32),
         "gx_is_new_service": ([vp, u32, P(GxService), P(i32)], i32),
         "gx_notify_msg": ([vp, u32, P(GxService), u32], i32),
+        "gx_notify_msgs": ([vp, P(u32), P(GxService), u32], i32),
+        "gx_read_view": ([vp, u32, vp, vp], i32),
         "gx_get_broadcasts": ([vp, u32, u32, P(GxService), u32, P(u32)], i32),
         "gx_local_state": ([vp, u32, P(GxService), u32, P(u32)], i32),
         "gx_merge_remote_state": ([vp, u32, P(GxService), u32], i32),
@@ -454,6 +456,20 @@ class Engine:
     # delegate --------------------------------------------------------------------------
     def notify_msg(self, host: int, items: Sequence):
         check(self.lib.gx_notify_msg(self.h, host, svc_array(items), len(items)))
+
+    def notify_msgs(self, hosts: Sequence[int], items: Sequence):
+        """Batched NotifyMsg: items[i] to hosts[i], runs of one host form one message."""
+        hs = (C.c_uint32 * len(hosts))(*hosts)
+        check(self.lib.gx_notify_msgs(self.h, hs, svc_array(items), len(items)), "gx_notify_msgs")
+
+    def read_view(self, view: int):
+        """One view unpacked: (ts_ns int64[R], INT64_MIN where empty; status uint8[R])."""
+        R = self.H * self.S
+        ts = np.empty(R, dtype=np.int64)
+        st = np.empty(R, dtype=np.uint8)
+        check(self.lib.gx_read_view(self.h, view, ts.ctypes.data_as(C.c_void_p), st.ctypes.data_as(C.c_void_p)),
+              "gx_read_view")
+        return ts, st
 
     def get_broadcasts(self, host: int, limit: Optional[int] = None):
         cap = 256

@@ -753,4 +753,29 @@ def kat_pending_truncation(lib):
     assert e.stats()["pending_drops"] == 8
 
 
+# ---------------------------------------------------------------- batched boundary calls (§8b)
+def kat_notify_msgs_batched(lib):
+    """SURVEY.md §8b gx_notify_msgs: one call for many hosts equals NotifyMsg per run of one host
+    (services_delegate.go:71-83), in order; gx_read_view unpacks the same slots."""
+    recs = [(SH, 0, T0, ALIVE), (SH, 1, T0, ALIVE), (CH, 0, T0 + SEC, DRAINING), (SH, 0, T0 + 2 * SEC, ALIVE),
+            (CH, 0, T0, ALIVE)]
+    hosts = [LOCAL, LOCAL, OTHER, LOCAL, OTHER]
+    a, b = mk(lib), mk(lib)
+    a.notify_msgs(hosts, recs)
+    b.notify_msg(LOCAL, recs[:2])
+    b.notify_msg(OTHER, recs[2:3])
+    b.notify_msg(LOCAL, recs[3:4])
+    b.notify_msg(OTHER, recs[4:5])
+    assert (a.read_views() == b.read_views()).all()
+    assert a.stats() == b.stats()
+    for v in (LOCAL, OTHER):
+        assert [bytes(j) for j in a.queue(v)] == [bytes(j) for j in b.queue(v)]
+    ts, st = a.read_view(LOCAL)
+    assert (ts[SH * 8 + 0], st[SH * 8 + 0]) == (T0 + 2 * SEC, ALIVE)
+    assert (ts[SH * 8 + 1], st[SH * 8 + 1]) == (T0, ALIVE)
+    assert st[CH * 8 + 0] == 7 and ts[CH * 8 + 0] == -(2**63)  # empty in LOCAL's view
+    ts, st = a.read_view(OTHER)
+    assert (ts[CH * 8 + 0], st[CH * 8 + 0]) == (T0 + SEC, DRAINING)  # the older ALIVE lost
+
+
 ALL = [v for k, v in sorted(globals().items()) if k.startswith("kat_")]
