@@ -64,13 +64,21 @@ GXD void q_push(const Dev &d, uint32_t v, uint32_t m, uint32_t b) {  // newest o
   x->tx = (uint8_t)(b + 1);
   h->q_len++;
 }
-// encodeAndBroadcast -> QueueBroadcast: invalidates the queued message about m.
-GXD void fd_broadcast(const Dev &d, uint32_t v, uint32_t m, int kind, uint32_t inc, uint32_t from) {
+// encodeAndBroadcast -> QueueBroadcast: invalidates the queued message about m. With `defer`
+// (the membership merge's lanes), only the message is written and *defer set: the caller moves
+// the flagged nodes to the queue's front afterwards, in node order.
+GXD void fd_broadcast(const Dev &d, uint32_t v, uint32_t m, int kind, uint32_t inc, uint32_t from,
+                      bool *defer = nullptr) {
   gx_member *x = memp(d, v, m);
-  if (x->tx) q_unlink(d, v, m);
+  if (!defer && x->tx) q_unlink(d, v, m);
   x->msg_kind = (uint8_t)kind;
   x->msg_incarnation = inc;
   x->msg_from = (uint16_t)from;
+  if (defer) *defer = true;
+  else q_push(d, v, m, 0);
+}
+GXD void fd_requeue(const Dev &d, uint32_t v, uint32_t m) {  // the deferred half of fd_broadcast
+  if (memp(d, v, m)->tx) q_unlink(d, v, m);
   q_push(d, v, m, 0);
 }
 // TransmitLimitedQueue.GetBroadcasts with a message budget (<= 64).
@@ -104,17 +112,18 @@ GXD uint32_t fd_get_broadcasts(const Dev &d, FdAcc &f, uint32_t v, uint32_t limi
 }
 
 // --------------------------------------------------------------------- message handlers --
-GXD void fd_set_deadline(const Dev &d, uint32_t v, uint32_t m, int64_t dl) {
+GXD void fd_set_deadline(const Dev &d, uint32_t v, uint32_t m, int64_t dl, bool lanes = false) {
   if (dl > GX_FD_NO_DEADLINE - 1) dl = GX_FD_NO_DEADLINE - 1;
   *dlp(d, v, m) = (int32_t)dl;
-  if ((int32_t)dl < fdhp(d, v)->min_deadline) fdhp(d, v)->min_deadline = (int32_t)dl;
+  if (lanes) atomicMin(&fdhp(d, v)->min_deadline, (int32_t)dl);  // several lanes of one host
+  else if ((int32_t)dl < fdhp(d, v)->min_deadline) fdhp(d, v)->min_deadline = (int32_t)dl;
 }
-GXD void fd_refute(const Dev &d, FdAcc &f, uint32_t v, uint32_t accused) {
+GXD void fd_refute(const Dev &d, FdAcc &f, uint32_t v, uint32_t accused, bool *defer = nullptr) {
   gx_member *me = memp(d, v, v);
   uint32_t inc = me->incarnation + 1;
   if (accused >= inc) inc = accused + 1;
   me->incarnation = inc;
-  fd_broadcast(d, v, v, GX_M_ALIVE, inc, v);
+  fd_broadcast(d, v, v, GX_M_ALIVE, inc, v, defer);
   f.inc(C_FD_REFUTE);
 }
 // deadNode; NotifyLeave -> ExpireServer (services_delegate.go:173-176).
@@ -136,42 +145,44 @@ GXD void fd_dead_node(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_ms
   f.inc(C_FD_DEATH);
   expire_server(d, a, v, m);
 }
-GXD bool fd_confirm(const Dev &d, FdAcc &f, uint32_t v, uint32_t m, gx_member *x, uint32_t from) {
+GXD bool fd_confirm(const Dev &d, FdAcc &f, uint32_t v, uint32_t m, gx_member *x, uint32_t from,
+                    bool lanes = false) {
   if (x->n_conf >= d.p.fd_suspicion_k) return false;
   for (uint32_t i = 0; i <= x->n_conf; i++)
     if (x->susp_from[i] == from) return false;
   x->susp_from[1 + x->n_conf] = (uint16_t)from;
   x->n_conf++;
   *dlp(d, v, m) = GX_FD_NO_DEADLINE;
-  fd_set_deadline(d, v, m, (int64_t)x->change_round + d.p.fd_suspicion_rounds[x->n_conf]);
+  fd_set_deadline(d, v, m, (int64_t)x->change_round + d.p.fd_suspicion_rounds[x->n_conf], lanes);
   f.inc(C_FD_CONFIRM);
   return true;
 }
-GXD void fd_suspect_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+GXD void fd_suspect_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g, bool *defer = nullptr) {
   const uint32_t m = g.node;
   gx_member *x = memp(d, v, m);
   if (fd_reaped(d, v, x)) return;
   if (g.incarnation < x->incarnation) return;
   if (x->state == GX_M_SUSPECT) {
-    if (fd_confirm(d, f, v, m, x, g.from)) fd_broadcast(d, v, m, GX_M_SUSPECT, g.incarnation, g.from);
+    if (fd_confirm(d, f, v, m, x, g.from, defer != nullptr))
+      fd_broadcast(d, v, m, GX_M_SUSPECT, g.incarnation, g.from, defer);
     return;
   }
   if (x->state != GX_M_ALIVE) return;
   if (m == v) {
-    fd_refute(d, f, v, g.incarnation);
+    fd_refute(d, f, v, g.incarnation, defer);
     return;
   }
-  fd_broadcast(d, v, m, GX_M_SUSPECT, g.incarnation, g.from);
+  fd_broadcast(d, v, m, GX_M_SUSPECT, g.incarnation, g.from, defer);
   x->incarnation = g.incarnation;
   x->state = GX_M_SUSPECT;
   x->change_round = (int32_t)d.round;
   x->n_conf = 0;
   x->susp_from[0] = (uint16_t)g.from;
   x->susp_from[1] = x->susp_from[2] = GX_FD_NONE;
-  fd_set_deadline(d, v, m, d.round + (int64_t)d.p.fd_suspicion_rounds[0]);
+  fd_set_deadline(d, v, m, d.round + (int64_t)d.p.fd_suspicion_rounds[0], defer != nullptr);
   f.inc(C_FD_SUSPECT);
 }
-GXD void fd_alive_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+GXD void fd_alive_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g, bool *defer = nullptr) {
   const uint32_t m = g.node;
   gx_member *x = memp(d, v, m);
   if (fd_reaped(d, v, x)) {  // unknown node: re-added as dead, incarnation 0
@@ -184,13 +195,13 @@ GXD void fd_alive_node(const Dev &d, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
     uint32_t inc = x->incarnation + 1;
     if (g.incarnation >= inc) inc = g.incarnation + 1;
     x->incarnation = inc;
-    fd_broadcast(d, v, v, GX_M_ALIVE, inc, v);
+    fd_broadcast(d, v, v, GX_M_ALIVE, inc, v, defer);
     f.inc(C_FD_REFUTE);
     return;
   }
   if (g.incarnation <= x->incarnation) return;
   *dlp(d, v, m) = GX_FD_NO_DEADLINE;
-  fd_broadcast(d, v, m, GX_M_ALIVE, g.incarnation, g.from);
+  fd_broadcast(d, v, m, GX_M_ALIVE, g.incarnation, g.from, defer);
   x->incarnation = g.incarnation;
   if (x->state != GX_M_ALIVE) {
     x->state = GX_M_ALIVE;
@@ -334,7 +345,8 @@ GXD uint64_t fd_snap_word(const Dev &d, uint32_t v, uint32_t m) {
 // state.go mergeState into host v, node order: alive -> aliveNode, suspect or dead ->
 // suspectNode{From: v}. One wave: the lanes test 64 nodes at a time for an effect (a superset of
 // the nodes whose handler changes anything; a node's test reads only that node's row, which the
-// handlers of other nodes do not change), lane 0 runs the handlers of the flagged nodes in order.
+// handlers of other nodes do not change), run the flagged nodes' handlers side by side (each
+// touches only its node's row), and lane 0 then moves the broadcast nodes in the queue in order.
 GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t *remote) {
   const uint32_t lane = threadIdx.x & 63;
   const int64_t wrap = fdhp(d, v)->wrap_round, dead_rounds = d.p.fd_gossip_dead_rounds;
@@ -372,26 +384,36 @@ GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t 
         flag = !reaped && inc >= inc_l && (state == GX_M_ALIVE || confirm);
       }
     }
-    unsigned long long fm = __ballot(flag);
-    if (lane == 0)
-      while (fm) {
-        const uint32_t k = (uint32_t)__ffsll((long long)fm) - 1;
-        fm &= fm - 1;
-        const uint64_t x = remote[base + k];
-        gx_fd_msg g;
-        g.incarnation = (uint32_t)(x >> 32);
-        g.node = (uint16_t)(base + k);
-        g.pad[0] = g.pad[1] = g.pad[2] = 0;
-        if ((x & 0xffu) == GX_M_ALIVE) {
-          g.from = (uint16_t)(base + k);
-          g.kind = GX_M_ALIVE;
-          fd_alive_node(d, f, v, g);
-        } else {
-          g.from = (uint16_t)v;
-          g.kind = GX_M_SUSPECT;
-          fd_suspect_node(d, f, v, g);
-        }
+    // each flagged lane runs its node's handler (node-local state, deadline, counters); the
+    // queue moves (unlink, push to the front of bucket 0) follow on lane 0 in node order, which
+    // is the order the sequential handlers would have queued them in
+    bool bc = false;
+    if (flag) {
+      gx_fd_msg g;
+      g.incarnation = (uint32_t)(w >> 32);
+      g.node = (uint16_t)(base + lane);
+      g.pad[0] = g.pad[1] = g.pad[2] = 0;
+      if ((w & 0xffu) == GX_M_ALIVE) {
+        g.from = (uint16_t)(base + lane);
+        g.kind = GX_M_ALIVE;
+        fd_alive_node(d, f, v, g, &bc);
+      } else {
+        g.from = (uint16_t)v;
+        g.kind = GX_M_SUSPECT;
+        fd_suspect_node(d, f, v, g, &bc);
       }
+    }
+    unsigned long long qm = __ballot(bc);
+    if (qm) {
+      __threadfence_block();  // the lanes' row writes before lane 0 reads those rows
+      if (lane == 0)
+        while (qm) {
+          const uint32_t k = (uint32_t)__ffsll((long long)qm) - 1;
+          qm &= qm - 1;
+          fd_requeue(d, v, base + k);
+        }
+      __threadfence_block();
+    }
     w = wn;
     lo = lon;
     hi = hin;
