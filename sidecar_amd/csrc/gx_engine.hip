@@ -318,8 +318,7 @@ static int ae_whole_impl(gx_engine *e) {
     }
     if (np && pp_state(d)) {  // pushPull's membership half (mergeState), from round-start lists
       LaunchTimer t(e, GX_K_FD);
-      k_fd_snap<<<2048, 256, 0, s>>>(d);
-      k_fd_pushpull<<<2 * np, 64, 0, s>>>(d, key0, key1);
+      k_fd_pushpull_pair<<<np, 128, 0, s>>>(d, key0, key1);  // both directions in lockstep: no snapshot
     }
   }
   HIPCHK(hipGetLastError());

@@ -347,6 +347,69 @@ GXD uint64_t fd_snap_word(const Dev &d, uint32_t v, uint32_t m) {
 // the nodes whose handler changes anything; a node's test reads only that node's row, which the
 // handlers of other nodes do not change), run the flagged nodes' handlers side by side (each
 // touches only its node's row), and lane 0 then moves the broadcast nodes in the queue in order.
+// One 64-node chunk of the merge into host v: w = the remote list's word for node base + lane,
+// lo/hi = the node's row fields in v's list (read before any handler of this chunk ran).
+GXD void fd_merge_chunk(const Dev &d, FdAcc &f, uint32_t v, uint32_t base, uint64_t w, uint4 lo, uint4 hi,
+                        int64_t wrap, int64_t dead_rounds, unsigned &present_n) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool present = base + lane < d.H && (w & 0xffu) != FD_SNAP_ABSENT;
+  bool flag = false;
+  if (present) {
+    present_n++;
+    const uint32_t inc_l = lo.x, state = hi.x & 0xffu, n_conf = (hi.x >> 8) & 0xffu;
+    const bool reaped = state == GX_M_DEAD && wrap - (int64_t)(int32_t)lo.z > dead_rounds;
+    const uint32_t inc = (uint32_t)(w >> 32);
+    if ((w & 0xffu) == GX_M_ALIVE) {
+      flag = reaped || inc > inc_l;
+    } else {
+      const uint32_t from[3] = {hi.y >> 16, hi.z & 0xffffu, hi.z >> 16};
+      bool confirm = state == GX_M_SUSPECT && n_conf < d.p.fd_suspicion_k;
+      for (uint32_t i = 0; i < 3 && confirm; i++)
+        if (i <= n_conf && from[i] == v) confirm = false;
+      flag = !reaped && inc >= inc_l && (state == GX_M_ALIVE || confirm);
+    }
+  }
+  // each flagged lane runs its node's handler (node-local state, deadline, counters); the
+  // queue moves (unlink, push to the front of bucket 0) follow on lane 0 in node order, which
+  // is the order the sequential handlers would have queued them in
+  bool bc = false;
+  if (flag) {
+    gx_fd_msg g;
+    g.incarnation = (uint32_t)(w >> 32);
+    g.node = (uint16_t)(base + lane);
+    g.pad[0] = g.pad[1] = g.pad[2] = 0;
+    if ((w & 0xffu) == GX_M_ALIVE) {
+      g.from = (uint16_t)(base + lane);
+      g.kind = GX_M_ALIVE;
+      fd_alive_node(d, f, v, g, &bc);
+    } else {
+      g.from = (uint16_t)v;
+      g.kind = GX_M_SUSPECT;
+      fd_suspect_node(d, f, v, g, &bc);
+    }
+  }
+  unsigned long long qm = __ballot(bc);
+  if (qm) {
+    __threadfence_block();  // the lanes' row writes before lane 0 reads those rows
+    if (lane == 0)
+      while (qm) {
+        const uint32_t k = (uint32_t)__ffsll((long long)qm) - 1;
+        qm &= qm - 1;
+        fd_requeue(d, v, base + k);
+      }
+    __threadfence_block();
+  }
+}
+GXD void fd_row_fields(const Dev &d, uint32_t v, uint32_t m, uint4 &lo, uint4 &hi) {
+  const uint4 *x = reinterpret_cast<const uint4 *>(memp(d, v, m));
+  lo = x[0];  // incarnation, msg_incarnation, change_round, deadline
+  hi = x[1];  // state, n_conf, tx, msg_kind | msg_from, susp_from[0] | susp_from[1], susp_from[2] | q_prev, q_next
+}
+// state.go mergeState into host v, node order: alive -> aliveNode, suspect or dead ->
+// suspectNode{From: v}. One wave: the lanes test 64 nodes at a time for an effect (a superset of
+// the nodes whose handler changes anything; a node's test reads only that node's row, which the
+// handlers of other nodes do not change), run the flagged nodes' handlers side by side (each
+// touches only its node's row), and lane 0 then moves the broadcast nodes in the queue in order.
 GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t *remote) {
   const uint32_t lane = threadIdx.x & 63;
   const int64_t wrap = fdhp(d, v)->wrap_round, dead_rounds = d.p.fd_gossip_dead_rounds;
@@ -356,70 +419,52 @@ GXD void fd_merge_state_wave(const Dev &d, FdAcc &f, uint32_t v, const uint64_t 
   auto load = [&](uint32_t base, uint64_t &w, uint4 &lo, uint4 &hi) {
     const uint32_t m = base + lane;
     w = m < d.H ? remote[m] : FD_SNAP_ABSENT;
-    if (m < d.H && (w & 0xffu) != FD_SNAP_ABSENT) {
-      const uint4 *x = reinterpret_cast<const uint4 *>(memp(d, v, m));
-      lo = x[0];  // incarnation, msg_incarnation, change_round, deadline
-      hi = x[1];  // state, n_conf, tx, msg_kind | msg_from, susp_from[0] | susp_from[1], susp_from[2] | q_prev, q_next
-    }
+    if (m < d.H && (w & 0xffu) != FD_SNAP_ABSENT) fd_row_fields(d, v, m, lo, hi);
   };
   uint64_t w = 0, wn = 0;
   uint4 lo = make_uint4(0, 0, 0, 0), hi = lo, lon = lo, hin = lo;
   load(0, w, lo, hi);
   for (uint32_t base = 0; base < d.H; base += 64) {
     if (base + 64 < d.H) load(base + 64, wn, lon, hin);
-    const bool present = (w & 0xffu) != FD_SNAP_ABSENT;
-    bool flag = false;
-    if (present) {
-      present_n++;
-      const uint32_t inc_l = lo.x, state = hi.x & 0xffu, n_conf = (hi.x >> 8) & 0xffu;
-      const bool reaped = state == GX_M_DEAD && wrap - (int64_t)(int32_t)lo.z > dead_rounds;
-      const uint32_t inc = (uint32_t)(w >> 32);
-      if ((w & 0xffu) == GX_M_ALIVE) {
-        flag = reaped || inc > inc_l;
-      } else {
-        const uint32_t from[3] = {hi.y >> 16, hi.z & 0xffffu, hi.z >> 16};
-        bool confirm = state == GX_M_SUSPECT && n_conf < d.p.fd_suspicion_k;
-        for (uint32_t i = 0; i < 3 && confirm; i++)
-          if (i <= n_conf && from[i] == v) confirm = false;
-        flag = !reaped && inc >= inc_l && (state == GX_M_ALIVE || confirm);
-      }
-    }
-    // each flagged lane runs its node's handler (node-local state, deadline, counters); the
-    // queue moves (unlink, push to the front of bucket 0) follow on lane 0 in node order, which
-    // is the order the sequential handlers would have queued them in
-    bool bc = false;
-    if (flag) {
-      gx_fd_msg g;
-      g.incarnation = (uint32_t)(w >> 32);
-      g.node = (uint16_t)(base + lane);
-      g.pad[0] = g.pad[1] = g.pad[2] = 0;
-      if ((w & 0xffu) == GX_M_ALIVE) {
-        g.from = (uint16_t)(base + lane);
-        g.kind = GX_M_ALIVE;
-        fd_alive_node(d, f, v, g, &bc);
-      } else {
-        g.from = (uint16_t)v;
-        g.kind = GX_M_SUSPECT;
-        fd_suspect_node(d, f, v, g, &bc);
-      }
-    }
-    unsigned long long qm = __ballot(bc);
-    if (qm) {
-      __threadfence_block();  // the lanes' row writes before lane 0 reads those rows
-      if (lane == 0)
-        while (qm) {
-          const uint32_t k = (uint32_t)__ffsll((long long)qm) - 1;
-          qm &= qm - 1;
-          fd_requeue(d, v, base + k);
-        }
-      __threadfence_block();
-    }
+    fd_merge_chunk(d, f, v, base, w, lo, hi, wrap, dead_rounds, present_n);
     w = wn;
     lo = lon;
     hi = hin;
   }
   f.inc(C_FD_STATE_MERGE, present_n);
   if (lane == 0) kbytes(d, GX_K_FD, 24ull * d.H, d.H);  // remote word + the node's row fields, per node
+}
+// Both directions of a push-pull pair (a, b) in one workgroup, chunk by chunk: wave 0 merges b's
+// list into a's, wave 1 a's into b's. Each wave reads its own host's rows of a chunk, hands the
+// partner the round-start words (incarnation << 32 | state, reaped = absent) through LDS, and the
+// barrier keeps every read of a chunk ahead of both waves' handlers for it, so neither side
+// needs a snapshot of the other's list (the handlers of a chunk touch only its nodes' rows).
+GXD void fd_merge_pair_lockstep(const Dev &d, FdAcc &f, uint32_t a, uint32_t b, uint64_t *s_w) {
+  const uint32_t lane = threadIdx.x & 63, side = threadIdx.x >> 6;
+  const uint32_t v = side ? b : a;
+  const int64_t wrap = fdhp(d, v)->wrap_round, dead_rounds = d.p.fd_gossip_dead_rounds;
+  unsigned present_n = 0;
+  uint4 lo = make_uint4(0, 0, 0, 0), hi = lo, lon = lo, hin = lo;
+  if (lane < d.H) fd_row_fields(d, v, lane, lo, hi);
+  for (uint32_t base = 0; base < d.H; base += 64) {
+    const uint32_t m = base + lane;
+    uint64_t mine = FD_SNAP_ABSENT;  // fd_snap_word of v's row for m
+    if (m < d.H) {
+      const uint32_t state = hi.x & 0xffu;
+      const bool reaped = state == GX_M_DEAD && wrap - (int64_t)(int32_t)lo.z > dead_rounds;
+      mine = reaped ? FD_SNAP_ABSENT : ((uint64_t)lo.x << 32) | state;
+    }
+    s_w[side * 64 + lane] = mine;
+    __syncthreads();
+    const uint64_t w = s_w[(1 - side) * 64 + lane];
+    if (base + 64 + lane < d.H) fd_row_fields(d, v, base + 64 + lane, lon, hin);
+    fd_merge_chunk(d, f, v, base, w, lo, hi, wrap, dead_rounds, present_n);
+    __syncthreads();  // both waves are done with s_w
+    lo = lon;
+    hi = hin;
+  }
+  f.inc(C_FD_STATE_MERGE, present_n);
+  if (lane == 0) kbytes(d, GX_K_FD, 32ull * d.H, d.H);  // the node's row fields, per node and side
 }
 
 // ---------------------------------------------------------------------------- kernels -----
@@ -518,9 +563,12 @@ GXD bool pp_runs(const Dev &d, uint32_t a, uint32_t b) {
   return !departed(d, a) && !departed(d, b) && reach(d, a, b) && (snap_row(d, a)[b] & 0xffu) == GX_M_ALIVE;
 }
 // Unsharded push-pull round: pair t as k_ae derives it; wave 2t merges b's list into a, 2t+1 a's into b.
-__global__ __launch_bounds__(64) void k_fd_pushpull(Dev d, uint64_t key0, uint64_t key1) {
+// Unsharded push-pull membership: one 128-thread workgroup per pair, both directions in lockstep.
+__global__ __launch_bounds__(128) void k_fd_pushpull_pair(Dev d, uint64_t key0, uint64_t key1) {
+  __shared__ uint64_t s_w[128];
+  __shared__ uint32_t s_run;
   FdAcc f;
-  const uint32_t t = blockIdx.x >> 1, side = blockIdx.x & 1;
+  const uint32_t t = blockIdx.x;
   uint32_t base = 0, m = d.H, q = t;
   uint64_t key = key0;
   if (d.pair_split) {
@@ -535,7 +583,10 @@ __global__ __launch_bounds__(64) void k_fd_pushpull(Dev d, uint64_t key0, uint64
     }
   }
   const uint32_t a = base + feistel_perm(key, 2 * q, m), b = base + feistel_perm(key, 2 * q + 1, m);
-  if (pp_runs(d, a, b)) fd_merge_state_wave(d, f, side ? b : a, snap_row(d, side ? a : b));
+  if (threadIdx.x == 0)  // pp_runs on the lists as this phase starts (nothing merged yet)
+    s_run = !departed(d, a) && !departed(d, b) && reach(d, a, b) && (fd_snap_word(d, a, b) & 0xffu) == GX_M_ALIVE;
+  __syncthreads();
+  if (s_run) fd_merge_pair_lockstep(d, f, a, b, s_w);
   fd_flush(d, f);
 }
 // Sharded push-pull round over the plan (ae_plan): a local pair merges both ways from the local
