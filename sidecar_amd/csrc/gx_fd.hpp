@@ -77,9 +77,44 @@ GXD void fd_broadcast(const Dev &d, uint32_t v, uint32_t m, int kind, uint32_t i
   if (defer) *defer = true;
   else q_push(d, v, m, 0);
 }
-GXD void fd_requeue(const Dev &d, uint32_t v, uint32_t m) {  // the deferred half of fd_broadcast
-  if (memp(d, v, m)->tx) q_unlink(d, v, m);
-  q_push(d, v, m, 0);
+// The deferred half of fd_broadcast (unlink if queued, push on stack 0) for every node base + k
+// with bit k of qm set, in node order, by the lanes of one wave
+// (`mine` = this lane's bit). Sequential requeues unlink each node from its stack and push it on
+// stack 0, so the result is: every stack minus the set, with the set on top of stack 0 in
+// descending node order. Unlink: the lane that starts a run of set nodes in a stack (its q_prev is
+// not in the set) walks the run to its first successor s outside the set and splices prev <-> s;
+// runs are disjoint, so no two lanes write the same link. Push: each set lane links to its
+// neighbours in the set by lane order, the lowest onto the old top of stack 0.
+GXD void fd_requeue_chunk(const Dev &d, uint32_t v, uint32_t base, unsigned long long qm, bool mine) {
+  const uint32_t lane = threadIdx.x & 63, m = base + lane;
+  gx_fd_host *h = fdhp(d, v);
+  auto in_set = [&](uint32_t y) { return y != GX_FD_NONE && y - base < 64u && ((qm >> (y - base)) & 1ull); };
+  bool queued = false;
+  if (mine) {
+    gx_member *x = memp(d, v, m);
+    const uint32_t tx = x->tx, pv = x->q_prev;
+    queued = tx != 0;
+    if (queued && !in_set(pv)) {  // a run starts here: find its successor outside the set
+      uint32_t s = x->q_next;
+      while (in_set(s)) s = memp(d, v, s)->q_next;
+      if (pv != GX_FD_NONE) memp(d, v, pv)->q_next = (uint16_t)s;
+      else h->q_head[tx - 1] = (uint16_t)s;
+      if (s != GX_FD_NONE) memp(d, v, s)->q_prev = (uint16_t)pv;
+    }
+  }
+  const unsigned long long qq = __ballot(queued);
+  __threadfence_block();  // every splice is done before stack 0's top is read
+  const uint32_t top = h->q_head[0];
+  if (mine) {
+    gx_member *x = memp(d, v, m);
+    const unsigned long long below = qm & ((1ull << lane) - 1), above = lane == 63 ? 0ull : qm & (~0ull << (lane + 1));
+    x->q_next = below ? (uint16_t)(base + 63 - __builtin_clzll(below)) : (uint16_t)top;
+    x->q_prev = above ? (uint16_t)(base + __ffsll((long long)above) - 1) : (uint16_t)GX_FD_NONE;
+    x->tx = 1;
+    if (!below && top != GX_FD_NONE) memp(d, v, top)->q_prev = (uint16_t)m;
+    if (!above) h->q_head[0] = (uint16_t)m;
+  }
+  if (lane == 0) h->q_len += (uint32_t)__popcll(qm) - (uint32_t)__popcll(qq);
 }
 // TransmitLimitedQueue.GetBroadcasts with a message budget (<= 64).
 GXD uint32_t fd_get_broadcasts(const Dev &d, FdAcc &f, uint32_t v, uint32_t limit, gx_fd_msg *out) {
@@ -388,15 +423,10 @@ GXD void fd_merge_chunk(const Dev &d, FdAcc &f, uint32_t v, uint32_t base, uint6
       fd_suspect_node(d, f, v, g, &bc);
     }
   }
-  unsigned long long qm = __ballot(bc);
+  const unsigned long long qm = __ballot(bc);
   if (qm) {
-    __threadfence_block();  // the lanes' row writes before lane 0 reads those rows
-    if (lane == 0)
-      while (qm) {
-        const uint32_t k = (uint32_t)__ffsll((long long)qm) - 1;
-        qm &= qm - 1;
-        fd_requeue(d, v, base + k);
-      }
+    __threadfence_block();  // the lanes' row writes before other lanes read those rows
+    fd_requeue_chunk(d, v, base, qm, bc);
     __threadfence_block();
   }
 }
