@@ -116,32 +116,57 @@ GXD void fd_requeue_chunk(const Dev &d, uint32_t v, uint32_t base, unsigned long
   }
   if (lane == 0) h->q_len += (uint32_t)__popcll(qm) - (uint32_t)__popcll(qq);
 }
-// TransmitLimitedQueue.GetBroadcasts with a message budget (<= 64).
+// TransmitLimitedQueue.GetBroadcasts with a message budget (<= 64): the messages are taken from
+// the tops of the stacks in transmit-count order, then requeued one transmit count up (dropped at
+// the retransmit limit). As a sequence of unlinks in take order and pushes in reverse take order
+// (the oracle's restatement), stack b ends as: the segment taken from stack b - 1 (links kept)
+// followed by what stack b kept. So one walk does it: each visited stack is spliced as soon as its
+// taken prefix is known, and each taken node is read once (message fields and link in one row).
+GXD void q_splice(const Dev &d, gx_fd_host *h, uint32_t v, uint32_t b, uint32_t first, uint32_t last, uint32_t rest) {
+  if (first != GX_FD_NONE) {
+    h->q_head[b] = (uint16_t)first;
+    memp(d, v, last)->q_next = (uint16_t)rest;
+    if (rest != GX_FD_NONE) memp(d, v, rest)->q_prev = (uint16_t)last;
+  } else {
+    h->q_head[b] = (uint16_t)rest;
+    if (rest != GX_FD_NONE) memp(d, v, rest)->q_prev = GX_FD_NONE;
+  }
+}
 GXD uint32_t fd_get_broadcasts(const Dev &d, FdAcc &f, uint32_t v, uint32_t limit, gx_fd_msg *out) {
-  uint16_t taken[64];
-  uint8_t from_b[64];
-  uint32_t n = 0;
+  gx_fd_host *h = fdhp(d, v);
+  uint32_t n = 0, dropped = 0, pf = GX_FD_NONE, pl = GX_FD_NONE;  // segment taken from stack b - 1
   const uint32_t L = d.p.fd_retransmit_limit;
   if (limit > 64) limit = 64;
-  for (uint32_t b = 0; b < L && n < limit; b++)
-    for (uint32_t m = fdhp(d, v)->q_head[b]; m != GX_FD_NONE && n < limit; m = memp(d, v, m)->q_next) {
-      taken[n] = (uint16_t)m;
-      from_b[n] = (uint8_t)b;
-      n++;
+  uint32_t b = 0;
+  for (; b < L && n < limit; b++) {
+    uint32_t first = GX_FD_NONE, last = GX_FD_NONE, m = h->q_head[b];
+    while (m != GX_FD_NONE && n < limit) {
+      gx_member *x = memp(d, v, m);
+      const uint32_t nx = x->q_next;
+      gx_fd_msg g;
+      g.incarnation = x->msg_incarnation;
+      g.node = (uint16_t)m;
+      g.from = x->msg_from;
+      g.kind = x->msg_kind;
+      g.pad[0] = g.pad[1] = g.pad[2] = 0;
+      out[n++] = g;
+      if (b + 1 < L) {
+        x->tx = (uint8_t)(b + 2);
+      } else {  // transmitted the limit: leaves the queue
+        x->tx = 0;
+        x->q_prev = x->q_next = GX_FD_NONE;
+        dropped++;
+      }
+      if (first == GX_FD_NONE) first = m;
+      last = m;
+      m = nx;
     }
-  for (uint32_t i = 0; i < n; i++) {
-    const gx_member *x = memp(d, v, taken[i]);
-    gx_fd_msg g;
-    g.incarnation = x->msg_incarnation;
-    g.node = taken[i];
-    g.from = x->msg_from;
-    g.kind = x->msg_kind;
-    g.pad[0] = g.pad[1] = g.pad[2] = 0;
-    out[i] = g;
-    q_unlink(d, v, taken[i]);
+    q_splice(d, h, v, b, pf, pl, m);  // stack b := segment of stack b - 1 ++ what b kept
+    pf = b + 1 < L ? first : GX_FD_NONE;
+    pl = last;
   }
-  for (uint32_t i = n; i-- > 0;)
-    if ((uint32_t)from_b[i] + 1 < L) q_push(d, v, taken[i], from_b[i] + 1u);
+  if (b < L && pf != GX_FD_NONE) q_splice(d, h, v, b, pf, pl, h->q_head[b]);
+  h->q_len -= dropped;
   f.inc(C_FD_SENT, n);
   return n;
 }
