@@ -596,9 +596,17 @@ __global__ __launch_bounds__(64) void k_fd_recv(Dev d) {  // one thread per rece
   const uint32_t vi = blockIdx.x * blockDim.x + threadIdx.x, v = d.lo + vi;
   if (vi < d.Hl && !departed(d, v)) {
     const uint32_t cap = d.p.fd_msg_cap;
+    // the packets' messages are read-only here: the next one is loaded before the current
+    // message's handler runs, so its load is not ordered behind the handler's row writes
     for (uint32_t x = d.in_cnt[vi]; x < d.in_cnt[vi + 1]; x++) {
       const uint32_t e = d.in_sorted[x].x, n = d.fd_len[e];
-      for (uint32_t y = 0; y < n; y++) fd_handle(d, a, f, v, d.fdm[(size_t)e * cap + y]);
+      const gx_fd_msg *pk = &d.fdm[(size_t)e * cap];
+      gx_fd_msg cur = n ? pk[0] : gx_fd_msg{};
+      for (uint32_t y = 0; y < n; y++) {
+        const gx_fd_msg nxt = y + 1 < n ? pk[y + 1] : cur;
+        fd_handle(d, a, f, v, cur);
+        cur = nxt;
+      }
     }
   }
   acc_flush(d, a);
