@@ -82,25 +82,34 @@ GXD void fd_broadcast(const Dev &d, uint32_t v, uint32_t m, int kind, uint32_t i
 // (`mine` = this lane's bit). Sequential requeues unlink each node from its stack and push it on
 // stack 0, so the result is: every stack minus the set, with the set on top of stack 0 in
 // descending node order. Unlink: the lane that starts a run of set nodes in a stack (its q_prev is
-// not in the set) walks the run to its first successor s outside the set and splices prev <-> s;
-// runs are disjoint, so no two lanes write the same link. Push: each set lane links to its
+// not in the set) splices prev <-> s, s the run's first successor outside the set (found by
+// pointer jumping over the lanes' links in registers); runs are disjoint, so no two lanes write
+// the same link. Push: each set lane links to its
 // neighbours in the set by lane order, the lowest onto the old top of stack 0.
 GXD void fd_requeue_chunk(const Dev &d, uint32_t v, uint32_t base, unsigned long long qm, bool mine) {
   const uint32_t lane = threadIdx.x & 63, m = base + lane;
   gx_fd_host *h = fdhp(d, v);
   auto in_set = [&](uint32_t y) { return y != GX_FD_NONE && y - base < 64u && ((qm >> (y - base)) & 1ull); };
-  bool queued = false;
+  uint32_t tx = 0, pv = GX_FD_NONE, s = GX_FD_NONE;
   if (mine) {
-    gx_member *x = memp(d, v, m);
-    const uint32_t tx = x->tx, pv = x->q_prev;
-    queued = tx != 0;
-    if (queued && !in_set(pv)) {  // a run starts here: find its successor outside the set
-      uint32_t s = x->q_next;
-      while (in_set(s)) s = memp(d, v, s)->q_next;
-      if (pv != GX_FD_NONE) memp(d, v, pv)->q_next = (uint16_t)s;
-      else h->q_head[tx - 1] = (uint16_t)s;
-      if (s != GX_FD_NONE) memp(d, v, s)->q_prev = (uint16_t)pv;
-    }
+    const gx_member *x = memp(d, v, m);
+    tx = x->tx;
+    pv = x->q_prev;
+    s = x->q_next;
+  }
+  const bool queued = mine && tx != 0;
+  // each queued lane's first successor outside the set, by pointer jumping over the lanes'
+  // successors (a run has at most 64 nodes, so 6 doublings reach its end)
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const bool jump = queued && in_set(s);
+    const uint32_t t = (uint32_t)__shfl((int)s, jump ? (int)(s - base) : (int)lane, 64);
+    if (jump) s = t;
+  }
+  if (queued && !in_set(pv)) {  // a run starts here: splice its predecessor to s
+    if (pv != GX_FD_NONE) memp(d, v, pv)->q_next = (uint16_t)s;
+    else h->q_head[tx - 1] = (uint16_t)s;
+    if (s != GX_FD_NONE) memp(d, v, s)->q_prev = (uint16_t)pv;
   }
   const unsigned long long qq = __ballot(queued);
   __threadfence_block();  // every splice is done before stack 0's top is read
