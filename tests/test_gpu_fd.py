@@ -106,3 +106,59 @@ def test_gpu_fd_with_listeners(gx_lib, oracle_lib):
         assert_same(g, o, f"round {g.round}")
         assert_same_fd(g, o, f"round {g.round}")
     assert g.stats()["listener_drops"] > 0  # the 16-event channel overflowed during the deaths
+
+
+def test_gpu_fd_queue_fuzz(gx_lib, oracle_lib):
+    """The memberlist broadcast queue under mass updates: pushPull merges (mergeState) whose remote
+    lists flag many queued nodes at once, spread over several transmit stacks and chunks (H = 150:
+    three 64-node chunks, the last one ragged), interleaved with GetBroadcasts that move and drop
+    whole stack prefixes, notifies and round advances. The lane-parallel queue moves and the
+    one-walk GetBroadcasts must leave every member row, link and stack as the oracle's sequential
+    unlinks and pushes do."""
+    import random
+    from sidecar_amd.abi import M_ALIVE, M_DEAD, M_SUSPECT
+    rnd = random.Random(11)
+    H = 150
+    kw = dict(n_hosts=H, n_services=2, init_mode=INIT_WARM, fd_enable=1, fd_gossip_dead_rounds=40)
+    pg, po = default_params(gx_lib, **kw), default_params(oracle_lib, **kw)
+    pg.fd_retransmit_limit = po.fd_retransmit_limit = 3  # messages reach the limit and leave
+    g = Engine(pg, lib=gx_lib)
+    o = Engine(po, lib=oracle_lib)
+    inc = [0] * H  # a rising incarnation per node, so that alive entries keep winning
+    hosts = [3, 64, 127, 149]
+    for step in range(300):
+        host = rnd.choice(hosts)
+        op = rnd.random()
+        if (step // 40) % 2:  # drain epochs: messages climb the stacks and leave at the limit
+            op = 0.3 + 0.3 * op if op < 0.8 else op
+        if op < 0.3:
+            dens = rnd.choice((0.05, 0.3, 0.9, 1.0))
+            remote = []
+            for m in range(H):
+                if rnd.random() >= dens:
+                    remote.append(None if rnd.random() < 0.5 else (M_ALIVE, 0))
+                    continue
+                inc[m] += rnd.randrange(0, 3)
+                remote.append((rnd.choice((M_ALIVE, M_ALIVE, M_SUSPECT, M_DEAD)), inc[m]))
+            g.fd_merge_state(host, remote)
+            o.fd_merge_state(host, remote)
+        elif op < 0.6:
+            lim = rnd.choice((1, 5, 17, 40))
+            assert g.fd_get_broadcasts(host, lim) == o.fd_get_broadcasts(host, lim), f"step {step}"
+        elif op < 0.85:
+            msgs = [(rnd.choice((M_ALIVE, M_SUSPECT, M_DEAD)), m, inc[m] + rnd.randrange(0, 2), rnd.randrange(H))
+                    for m in rnd.sample(range(H), rnd.randrange(1, 30))]
+            g.fd_notify(host, msgs)
+            o.fd_notify(host, msgs)
+        elif op < 0.95:
+            g.fd_timers(host)
+            o.fd_timers(host)
+        else:
+            r = g.round + rnd.randrange(1, 20)
+            g.set_round(r)
+            o.set_round(r)
+        if step % 25 == 24:
+            for v in hosts:
+                assert g.fd_queue(v) == o.fd_queue(v), f"step {step}: queue of host {v}"
+            assert_same_fd(g, o, f"step {step}")
+    assert_same(g, o, "queue fuzz")
