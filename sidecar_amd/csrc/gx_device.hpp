@@ -631,21 +631,38 @@ GXD uint64_t tombstone_services(const Dev &d, Acc &a, uint32_t o, uint64_t runni
 // ExpireServer (services_state.go:150-192) for one (viewer, owner).
 GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
   uint64_t *row = &vrow(d, v)[(size_t)o * d.S];
-  uint64_t mask = 0;
+  const uint64_t nw = pack(d.now, GX_TOMBSTONE);
+  uint64_t mask = 0, diff = 0;
   bool live = false;
   for (uint32_t s = 0; s < d.S; s++) {
-    int st = st_of(row[s]);
+    const uint64_t w = row[s];
+    int st = st_of(w);
     if (st == GX_ABSENT) continue;
     mask |= 1ull << s;
+    if (w != nw) diff |= 1ull << s;
     if (st != GX_TOMBSTONE) live = true;
   }
   if (!live) return false;  // no server / no services / no live services (:154-170)
+  // Tombstone() + ServiceChanged for every record (:176-181). Every record gets the same word and
+  // the same owner, so the per-record bookkeeping (set_slot's expiry bound, svc_changed's server
+  // times and view LastChanged) collapses to one update each; the ChangeEvents (listening views
+  // only) go out in record order, before the slots are overwritten. The slot stores then issue
+  // back to back, with no load between them.
+  const int32_t k = d.ev_slot[li(d, v)];
+  if (k >= 0)
+    for (uint32_t s = 0; s < d.S; s++)
+      if ((mask >> s) & 1ull) ev_put(d, k, d.ev_cnt[k]++, o * d.S + s, nw, st_of(row[s]));
   for (uint32_t s = 0; s < d.S; s++)
-    if ((mask >> s) & 1ull) {  // Tombstone() + ServiceChanged for every record (:176-181)
-      int prev = st_of(row[s]);
-      set_slot(d, a, v, &row[s], pack(d.now, GX_TOMBSTONE));
-      svc_changed(d, a, v, o * d.S + s, row[s], prev);
-    }
+    if ((diff >> s) & 1ull) row[s] = nw;
+  if (diff) {
+    a.changed = true;
+    atomicMin(&d.minexp[li(d, v)], exp_time(d.p, nw));
+  }
+  gx_server_times *t = srv_times(d, v, o);
+  t->last_updated_ns = ts_of(nw);
+  t->last_changed_ns = ts_of(nw);
+  d.vlc[li(d, v)] = ts_of(nw);
+  a.c[C_CHG] += (unsigned)__popcll(mask);
   a.c[C_EXPSRV]++;
   push_job(d, a, v, make_job((uint64_t)d.now, mask, o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count)));
   return true;

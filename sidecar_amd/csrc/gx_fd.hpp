@@ -9,10 +9,10 @@
 //
 // Kernels (one host per thread or wave; the work is pointer-chasing integer logic, latency-
 // bound, not bandwidth-bound):
-//   k_fd_tick   one wave per host: suspicion timers due -> deadNode (NotifyLeave ->
-//               ExpireServer), the due deadlines found by a coalesced scan of the host's fd_dl
-//               row (only when its exact lower bound min_deadline has passed); then probe() on
-//               the host's probe tick (lane 0)
+//   k_fd_tick   one wave per host: suspicion timers due -> deadNode on the due nodes' lanes,
+//               then ExpireServer in node order on lane 0 (NotifyLeave), the due deadlines found
+//               by a coalesced scan of the host's fd_dl row (only when its exact lower bound
+//               min_deadline has passed); then probe() on the host's probe tick (lane 0)
 //   k_fd_send   one thread per host: kRandomNodes gossip targets, then the memberlist messages
 //               of every packet (TransmitLimitedQueue.GetBroadcasts)
 //   k_fd_recv   one thread per receiver, after the catalog merge: the packets' memberlist
@@ -196,7 +196,10 @@ GXD void fd_refute(const Dev &d, FdAcc &f, uint32_t v, uint32_t accused, bool *d
   f.inc(C_FD_REFUTE);
 }
 // deadNode; NotifyLeave -> ExpireServer (services_delegate.go:173-176).
-GXD void fd_dead_node(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_msg &g) {
+// With `defer` (the timer scan's lanes), the queue move is deferred as in fd_broadcast and, on a
+// death, *died is set instead of running ExpireServer, which the caller then runs in node order.
+GXD void fd_dead_node(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_msg &g, bool *defer = nullptr,
+                      bool *died = nullptr) {
   const uint32_t m = g.node;
   gx_member *x = memp(d, v, m);
   if (fd_reaped(d, v, x)) return;
@@ -204,15 +207,16 @@ GXD void fd_dead_node(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_ms
   *dlp(d, v, m) = GX_FD_NO_DEADLINE;  // delete(m.nodeTimers, d.Node)
   if (x->state == GX_M_DEAD) return;
   if (m == v) {
-    fd_refute(d, f, v, g.incarnation);
+    fd_refute(d, f, v, g.incarnation, defer);
     return;
   }
-  fd_broadcast(d, v, m, GX_M_DEAD, g.incarnation, g.from);
+  fd_broadcast(d, v, m, GX_M_DEAD, g.incarnation, g.from, defer);
   x->incarnation = g.incarnation;
   x->state = GX_M_DEAD;
   x->change_round = (int32_t)d.round;
   f.inc(C_FD_DEATH);
-  expire_server(d, a, v, m);
+  if (died) *died = true;
+  else expire_server(d, a, v, m);
 }
 GXD bool fd_confirm(const Dev &d, FdAcc &f, uint32_t v, uint32_t m, gx_member *x, uint32_t from,
                     bool lanes = false) {
@@ -344,9 +348,9 @@ GXD bool fd_probe_tick(const Dev &d, uint32_t v) {
   return (uint64_t)d.round % P == rng4(d.p.seed, ST_FD_PHASE, v, 0, 0) % P;
 }
 
-// Suspicion timers of host v due this round, one wave: coalesced scan of the fd_dl row, lane 0
-// declares the due nodes dead in node order; the new exact min_deadline is the wave minimum of
-// the rest.
+// Suspicion timers of host v due this round, one wave: coalesced scan of the fd_dl row, the due
+// nodes declared dead with the effects of sequential handlers in node order; the new exact
+// min_deadline is the wave minimum of the rest.
 GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
   const uint32_t lane = threadIdx.x & 63;
   if (fdhp(d, v)->min_deadline > d.round) return;  // uniform
@@ -357,17 +361,31 @@ GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
     const int32_t dl = m < d.H ? *dlp(d, v, m) : GX_FD_NO_DEADLINE;
     const bool due = dl <= d.round;
     if (!due) mn = dl < mn ? dl : mn;
-    unsigned long long due_mask = __ballot(due);
+    // the due nodes' deadNode handlers run side by side (each touches only its node's row and
+    // deadline); their queue moves follow in node order (fd_requeue_chunk), then lane 0 runs
+    // ExpireServer for the new deaths in node order (the catalog side never reads member rows)
+    bool bc = false, died = false;
+    if (due) {
+      gx_fd_msg g;
+      g.incarnation = memp(d, v, m)->incarnation;
+      g.node = (uint16_t)m;
+      g.from = (uint16_t)v;
+      g.kind = GX_M_DEAD;
+      g.pad[0] = g.pad[1] = g.pad[2] = 0;
+      fd_dead_node(d, a, f, v, g, &bc, &died);
+    }
+    const unsigned long long qm = __ballot(bc);
+    if (qm) {
+      __threadfence_block();
+      fd_requeue_chunk(d, v, base, qm, bc);
+      __threadfence_block();
+    }
+    unsigned long long dm = __ballot(died);
     if (lane == 0)
-      while (due_mask) {
-        const uint32_t k = (uint32_t)__ffsll((long long)due_mask) - 1;
-        due_mask &= due_mask - 1;
-        gx_fd_msg g;
-        g.incarnation = memp(d, v, base + k)->incarnation;
-        g.node = (uint16_t)(base + k);
-        g.from = (uint16_t)v;
-        g.kind = GX_M_DEAD;
-        fd_dead_node(d, a, f, v, g);
+      while (dm) {
+        const uint32_t k = (uint32_t)__ffsll((long long)dm) - 1;
+        dm &= dm - 1;
+        expire_server(d, a, v, base + k);
       }
   }
 #pragma unroll
