@@ -29,10 +29,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 CONFIGS = {
     # BASELINE.json configs[4]: 32768 x 16, 2-way partition for 50 rounds, departure storm, heal
     "cfg5": dict(desc="32768 hosts x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds "
-                      "[0,50) + ExpireServer storm at round 5 + heal, push-pull every 10 rounds",
+                      "[0,50) + ExpireServer storm at round 5 + heal",
                  p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
                         queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
-                        partition_end=50, storm_round=5, ae_period_rounds=10)),
+                        partition_end=50, storm_round=5, ae_period_rounds=10),
+                 ref_variant="cfg5_ref"),
+    # cfg 5 at the reference's own anti-entropy cadence: PushPullInterval 20 s (config/config.go:45,
+    # main.go:252-256) = 100 rounds of GossipInterval 200 ms; reported beside cfg5 for its
+    # rounds-to-converge
+    "cfg5_ref": dict(desc="cfg5 at Sidecar's default PushPullInterval 20 s: 32768 hosts x 16 services, fanout 3, "
+                          "cap 32 records/msg, 2-way partition rounds [0,50) + ExpireServer storm at round 5 + heal",
+                     p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
+                            queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                            partition_end=50, storm_round=5, ae_period_rounds=100)),
     # configs[1]: 4096 x 16, fanout 3, cap 32, one GPU (cold start: every view knows its own records)
     "cfg2": dict(desc="4096 hosts x 16 services, fanout 3, cap 32 records/msg, own-records start, "
                       "push-pull every 10 rounds",
@@ -72,6 +81,24 @@ CONFIGS = {
 }
 
 KNAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode", "fd"]
+GOSSIP_KERNELS = ("owner", "scan", "send", "merge")  # the kernels every gossip round runs
+
+
+def workload_text(cfg):
+    """Config description with the anti-entropy cadence and pairing spelled out."""
+    c = CONFIGS[cfg]
+    p = c["p"]
+    ae = p.get("ae_period_rounds", 0)
+    if ae:
+        pairing = ("per-node initiation (every live host starts one exchange with a random peer)"
+                   if p.get("push_pull_mode", 0) else
+                   "seeded perfect matching (every host in exactly one exchange per push-pull round)")
+        cad = f"push-pull every {ae} rounds ({ae * 0.2:g} s), {pairing}"
+    else:
+        cad = "no push-pull"
+    gm = p.get("gossip_messages", 0)
+    gms = f", GossipMessages {gm}" if gm > 1 else ""
+    return f"{cfg}: {c['desc']}; {cad}{gms}"
 
 
 def make_engine(lib, cfg, seed, device):
@@ -217,6 +244,7 @@ def main():
     ap.add_argument("--converge-max", type=int, default=3000)
     ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-split", action="store_true", help="skip the instrumented per-kernel pass")
     ap.add_argument("--cpu-hosts", type=int, default=16384, help="H of the multi-threaded CPU sample")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     args = ap.parse_args()
@@ -240,19 +268,20 @@ def main():
     from sidecar_amd.abi import load_product
     lib = load_product()
     seed = args.seed
+
+    # headline window: no per-launch instrumentation inside it (event records are host
+    # work inside the wall-clock window)
     c = Cluster(lib, args.config, seed, rank, world, local_rank, barrier)
-    e = c.e
-    e.enable_timing(True)
     if args.warmup:
         c.run_rounds(args.warmup)
-    st0, tm0 = c.stats(), e.timing()
+    st0 = c.stats()
     x0 = c.exchange_bytes()
     barrier()
     t0 = time.perf_counter()
     c.run_rounds(args.steps)
     barrier()
     dt = time.perf_counter() - t0
-    st1, tm1 = c.stats(), e.timing()
+    st1 = c.stats()
     x1 = c.exchange_bytes()
     xfer = {k: x1[k] - x0[k] for k in x1} if x1 else None
     c.close()
@@ -265,30 +294,50 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt_max = float(t.item())
 
+    # per-kernel split: the same window again on a fresh cluster, with HIP events around every
+    # launch on the engine's stream (device time per kernel class and algorithmic bytes)
     kern = {}
-    for i, k in enumerate(KNAMES):
-        ms = tm1[k]["ms"] - tm0[k]["ms"]
-        nl = tm1[k]["launches"] - tm0[k]["launches"]
-        b = tm1[k]["bytes"] - tm0[k]["bytes"]
-        if nl:
-            kern[k] = {"ms": round(ms, 3), "launches": nl, "bytes": b,
-                       "GBps": round(b / (ms * 1e6), 1) if ms > 0 else None}
-    dom = max(kern, key=lambda k: kern[k]["ms"]) if kern else None
-    roof = None
-    if dom:
-        ach = kern[dom]["GBps"] or 0.0
-        traffic = None
-        try:
-            pmc = json.load(open(args.pmc))
-            ent = pmc.get(args.config, {}).get(dom)
-            if ent:
-                traffic = ent.get("hbm_bytes_per_launch")
-        except Exception:
-            pass
-        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    if not args.no_kernel_split:
+        c = Cluster(lib, args.config, seed, rank, world, local_rank, barrier)
+        if args.warmup:
+            c.run_rounds(args.warmup)
+        c.e.enable_timing(True)
+        tm0 = c.e.timing()
+        c.run_rounds(args.steps)
+        tm1 = c.e.timing()
+        c.close()
+        for k in KNAMES:
+            ms = tm1[k]["ms"] - tm0[k]["ms"]
+            nl = tm1[k]["launches"] - tm0[k]["launches"]
+            b = tm1[k]["bytes"] - tm0[k]["bytes"]
+            if nl:
+                kern[k] = {"ms": round(ms, 4), "launches": nl, "bytes": b,
+                           "GBps": round(b / (ms * 1e6), 1) if ms > 0 else None}
+    pmc = {}
+    try:
+        pmc = json.load(open(args.pmc)).get(args.config, {})
+    except Exception:
+        pass
+
+    def roofline(k):
+        if k not in kern or not kern[k]["ms"]:
+            return None
+        ach = kern[k]["GBps"] or 0.0
+        traffic = (pmc.get(k) or {}).get("hbm_bytes_per_launch")
+        return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
-                "bytes_per_launch": kern[dom]["bytes"] // max(1, kern[dom]["launches"]),
+                "bytes_per_launch": kern[k]["bytes"] // max(1, kern[k]["launches"]),
+                "us_per_launch": round(1e3 * kern[k]["ms"] / kern[k]["launches"], 2),
                 "traffic": traffic}
+
+    dom = max(kern, key=lambda k: kern[k]["ms"]) if kern else None
+    roof = roofline(dom) if dom else None
+    gossip = None
+    if kern:
+        gms = sum(kern[k]["ms"] for k in GOSSIP_KERNELS if k in kern)
+        gossip = {"kernels": list(GOSSIP_KERNELS), "device_us_per_round": round(1e3 * gms / args.steps, 2),
+                  "gossip_merges": split["gossip_merges"],
+                  "record_merges_per_s": split["gossip_merges"] / (gms * 1e-3) if gms else None}
 
     conv = None
     if not args.no_converge:
@@ -296,6 +345,14 @@ def main():
                                  args.check_every)
         conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
                 "rounds_run": ran, "simulated_s": (r * 0.2) if r else None}
+    conv_ref = None
+    ref = CONFIGS[args.config].get("ref_variant")
+    if ref and not args.no_converge:
+        r, w, ran = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
+                                 args.check_every)
+        conv_ref = {"config": workload_text(ref), "rounds_to_converge": r,
+                    "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
+                    "simulated_s": (r * 0.2) if r else None}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.warmup, args.steps, h_mt=args.cpu_hosts)
@@ -308,11 +365,12 @@ def main():
             "ms_per_step": dt_max * 1000.0 / args.steps, "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None, "dtype": "int64", "data": "synthetic (seeded gossip schedule)",
-            "config": {"workload": f"{args.config}: " + CONFIGS[args.config]["desc"],
+            "config": {"workload": workload_text(args.config),
                        "hosts": cfgp["n_hosts"], "services": cfgp["n_services"],
                        "fanout": cfgp.get("fanout", 3),
                        "parallelism": f"host-sharded over {world} GPUs (RCCL all-to-all)" if world > 1 else "single GPU"},
-            "merges": split, "converge": conv, "roofline": roof, "cpu_baseline": cpu, "kernels": kern,
+            "merges": split, "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
+            "roofline": roof, "roofline_merge": roofline("merge"), "cpu_baseline": cpu, "kernels": kern,
             "exchange": xfer,
         }
         if cfgp.get("fd_enable") or cfgp.get("depart_ppm"):

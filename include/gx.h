@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 3
+#define GX_ABI_VERSION 4
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -165,7 +165,23 @@ typedef struct gx_params {
    * other's round-start member list, alive -> aliveNode, suspect or dead -> suspectNode{From: us}.
    * 1 = memberlist's behaviour (default), 0 = catalog only. */
   uint32_t fd_push_pull_state;
+  /* GossipMessages (config/config.go:46, main.go:257-259; README.md:180 "How many times to gather
+   * messages per round", Sidecar's default 15): memberlist gathers up to this many GetBroadcasts
+   * results per gossip target per round, each sent to that target as its own packet. 0 or 1 = one
+   * call per target. The memberlist fork is absent, so this reading is parity unpinned. */
+  uint32_t gossip_messages;
+  /* Push-pull pairing on anti-entropy rounds (memberlist pushPullTrigger every PushPullInterval,
+   * config/config.go:45). GX_PP_MATCHING: a seeded perfect matching, every host in one exchange.
+   * GX_PP_INITIATE: every live host initiates one exchange with a peer drawn at random, so a host
+   * takes part in 1 + (number of initiators that drew it) exchanges, as with memberlist's
+   * per-node timers. Both sides of an exchange merge the other's round-start state. */
+  uint32_t push_pull_mode;
+  /* Engine bound (no reference counterpart): inbox slots per receiver, 1..64 (0 = 64). A receiver
+   * with more packets in a round takes the serial overflow path; results are identical. */
+  uint32_t inbox_slots;
 } gx_params;
+#define GX_PP_MATCHING 0
+#define GX_PP_INITIATE 1
 
 /* Per-host bookkeeping (read-back for parity). */
 typedef struct gx_host_state {

@@ -36,6 +36,7 @@ enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS =
 struct gx_engine {
   gx_params p;
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  uint32_t NG, KE; /* GossipMessages gathers per target; packet entries per host = K * NG */
   uint32_t G, gid, lo, hi; /* shards; this engine owns hosts [lo, hi). Arrays stay H-sized. */
   /* cross-shard push-pull pairs of this AE round, in (partner shard, pair index) order, which is
    * the order of the digest and delta messages in both directions */
@@ -60,11 +61,11 @@ struct gx_engine {
   grec *dq;             /* H * DQ  delegate pendingBroadcasts deque */
   grec *arena;          /* H * A * L SendServices lists */
   uint32_t *arena_len;  /* H * A */
-  grec *msg;            /* H * K * packet_cap  this round's packets */
-  uint32_t *msg_len;    /* H * K */
-  uint32_t *msg_dst;    /* H * K */
+  grec *msg;            /* H * KE * packet_cap  this round's packets */
+  uint32_t *msg_len;    /* H * KE */
+  uint32_t *msg_dst;    /* H * KE */
   uint32_t *in_cnt;     /* H + 1 */
-  uint32_t *in_list;    /* H * K  (sender * K + j), grouped by receiver, sender-ascending */
+  uint32_t *in_list;    /* H * KE  (sender * KE + j * NG + n), grouped by receiver, sender-ascending */
   uint16_t *sbytes;     /* R  encoded bytes of every Service field but Updated and Status */
   gx_server_times *srvt; /* H * H  Server.LastUpdated / LastChanged per (view, owner) */
   int64_t *vlc;          /* H  state.LastChanged per view */
@@ -745,30 +746,40 @@ static void ph_storm(gx_engine *e, uint32_t i, void *ctx) {
  * records. */
 static void ph_send(gx_engine *e, uint32_t i, void *ctx) {
   (void)ctx;
-  uint32_t u = e->lo + i, K = e->K, cap = e->p.packet_cap;
+  uint32_t u = e->lo + i, K = e->K, NG = e->NG, cap = e->p.packet_cap;
   if (departed(e, u)) return;
   uint32_t peers[64];
   const int fd = e->p.fd_enable != 0;
   uint32_t np = fd ? e->fd_np[u] : sample_peers(e, u, peers);
   for (uint32_t j = 0; j < np; j++) {
-    size_t x = (size_t)u * K + j;
-    uint32_t peer = fd ? e->fd_peers[x] : peers[j], nf = fd ? e->fd_len[x] : 0, l;
-    if (fd && e->p.limit_bytes) {
-      uint32_t used = nf * (e->p.fd_msg_bytes + 2);
-      uint32_t avail = e->p.limit_bytes > used ? e->p.limit_bytes - used : 0;
-      l = avail > e->p.overhead_bytes
-              ? get_broadcasts(e, u, cap, &e->msg[x * cap], avail, e->p.overhead_bytes)
-              : 0;
-    } else {
-      l = get_broadcasts(e, u, cap, &e->msg[x * cap], e->p.limit_bytes, e->p.overhead_bytes);
-    }
-    e->msg_len[x] = l;
-    e->msg_dst[x] = peer;
-    int stop = l == 0 && nf == 0 && e->p.gossip_stop_on_empty;
-    if ((l || nf) && !reach(e, u, peer)) {
-      e->st.lost_packets++;
-      e->msg_len[x] = 0;
-      if (fd) e->fd_len[x] = 0;
+    /* GossipMessages (config/config.go:46, README.md:180): up to NG gathers per target, each sent
+     * as its own packet; a target's gathering ends at an empty result, and an empty first gather
+     * ends the round (memberlist gossip() returns when there is nothing to send). Entries are
+     * numbered sender * KE + j * NG + n, so receivers take them in that order. */
+    int stop = 0;
+    for (uint32_t n = 0; n < NG; n++) {
+      size_t x = (size_t)u * e->KE + (size_t)j * NG + n;
+      uint32_t peer = fd ? e->fd_peers[(size_t)u * K + j] : peers[j], nf = fd ? e->fd_len[x] : 0, l;
+      if (fd && e->p.limit_bytes) {
+        uint32_t used = nf * (e->p.fd_msg_bytes + 2);
+        uint32_t avail = e->p.limit_bytes > used ? e->p.limit_bytes - used : 0;
+        l = avail > e->p.overhead_bytes
+                ? get_broadcasts(e, u, cap, &e->msg[x * cap], avail, e->p.overhead_bytes)
+                : 0;
+      } else {
+        l = get_broadcasts(e, u, cap, &e->msg[x * cap], e->p.limit_bytes, e->p.overhead_bytes);
+      }
+      e->msg_len[x] = l;
+      e->msg_dst[x] = peer;
+      if ((l || nf) && !reach(e, u, peer)) {
+        e->st.lost_packets++;
+        e->msg_len[x] = 0;
+        if (fd) e->fd_len[x] = 0;
+      }
+      if (l == 0 && nf == 0) {
+        stop = n == 0 && e->p.gossip_stop_on_empty;
+        break;
+      }
     }
     if (stop) break;
   }
@@ -780,7 +791,7 @@ static void round_send(gx_engine *e) {
   for_hosts(e, n, ph_owner, &now);
   if (e->p.storm_round >= 0 && e->round == e->p.storm_round) for_hosts(e, n, ph_storm, &now);
   if (e->p.fd_enable) for_hosts(e, n, ph_fd_tick, &now);
-  for (size_t i = 0; i < (size_t)e->H * e->K; i++) e->msg_len[i] = 0;
+  for (size_t i = 0; i < (size_t)e->H * e->KE; i++) e->msg_len[i] = 0;
   if (e->p.fd_enable) {
     memset(e->fd_len, 0, sizeof(uint32_t) * (size_t)e->H * (e->K ? e->K : 1));
     for_hosts(e, n, ph_fd_send, NULL);
@@ -804,7 +815,7 @@ static void ph_receive(gx_engine *e, uint32_t i, void *ctx) {
 }
 static void round_merge(gx_engine *e) {
   int64_t now = now_of(e);
-  uint32_t H = e->H, K = e->K;
+  uint32_t H = e->H, K = e->KE;
   memset(e->in_cnt, 0, sizeof(uint32_t) * (H + 1));
   for (size_t m = 0; m < (size_t)H * K; m++)
     if (pkt_live(e, m) && is_local(e, e->msg_dst[m])) e->in_cnt[e->msg_dst[m] + 1]++;
@@ -893,8 +904,13 @@ static void ph_ae_pair(gx_engine *e, uint32_t t, void *ctx) {
   if (is_local(e, c->pa[t]) && is_local(e, c->pb[t]) && ae_pair_ok(e, c->pa[t], c->pb[t]))
     ae_exchange(e, c->pa[t], c->pb[t], c->now);
 }
+static void ae_phase_initiate(gx_engine *e);
 /* Phase 5, pairs with both hosts here: both merge the other's round-start row. */
 static void ae_phase_local(gx_engine *e) {
+  if (e->p.push_pull_mode == GX_PP_INITIATE) { /* unsharded engines only (check_params) */
+    ae_phase_initiate(e);
+    return;
+  }
   if (!ae_round(e) || e->ae_local_round == e->round) return;
   int64_t now = now_of(e);
   uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
@@ -904,6 +920,76 @@ static void ae_phase_local(gx_engine *e) {
   for_hosts(e, np, ph_ae_pair, &c); /* pairs are disjoint: every host is in at most one */
   free(pa);
   free(pb);
+  e->ae_local_round = e->round;
+}
+
+/* GX_PP_INITIATE: every live host starts one push-pull with a partner drawn at random among the
+ * other hosts of its side (memberlist's per-node pushPull timers, one exchange per host per
+ * PushPullInterval; the partner choice is the absent fork's, parity unpinned). Exchanges run in
+ * initiator order, each as ae_exchange (both sides merge the other's state as it was before the
+ * exchange). Exchanges with no host in common commute, so they run in batches: an exchange goes
+ * into the batch after the last one that holds either of its hosts (pp_batches, identical on the
+ * GPU engine). */
+static int ae_partner(const gx_engine *e, uint32_t i, uint32_t *out) {
+  uint32_t base = 0, m = e->H;
+  if (partitioned(e) && !e->p.fd_enable) {
+    uint32_t half = e->H / 2;
+    base = i < half ? 0 : half;
+    m = i < half ? half : e->H - half;
+  }
+  if (m < 2) return 0;
+  const uint64_t x = rng4(e->p.seed, ST_AE, (uint64_t)e->round, i, 1);
+  const uint32_t idx = unif(x, m - 1), self = i - base;
+  *out = base + (idx >= self ? idx + 1 : idx);
+  return 1;
+}
+/* pa/pb: the exchanges grouped by batch (boff[b] .. boff[b + 1]); returns the batch count. */
+static uint32_t pp_batches(const gx_engine *e, uint32_t *pa, uint32_t *pb, uint32_t *boff) {
+  uint32_t *last = (uint32_t *)calloc(e->H, sizeof(uint32_t)), *bat = (uint32_t *)malloc(sizeof(uint32_t) * e->H);
+  uint32_t *ia = (uint32_t *)malloc(sizeof(uint32_t) * e->H), *ib = (uint32_t *)malloc(sizeof(uint32_t) * e->H);
+  uint32_t n = 0, nb = 0;
+  for (uint32_t i = 0; i < e->H; i++) {
+    uint32_t b;
+    if (departed(e, i) || !ae_partner(e, i, &b) || departed(e, b)) continue;
+    const uint32_t k = 1 + (last[i] > last[b] ? last[i] : last[b]);
+    last[i] = last[b] = k;
+    ia[n] = i;
+    ib[n] = b;
+    bat[n++] = k - 1;
+    if (k > nb) nb = k;
+  }
+  for (uint32_t q = 0; q <= nb; q++) boff[q] = 0;
+  for (uint32_t t = 0; t < n; t++) boff[bat[t] + 1]++;
+  for (uint32_t q = 0; q < nb; q++) boff[q + 1] += boff[q];
+  uint32_t *cur = (uint32_t *)malloc(sizeof(uint32_t) * (nb + 1));
+  memcpy(cur, boff, sizeof(uint32_t) * (nb + 1));
+  for (uint32_t t = 0; t < n; t++) {  /* stable: initiator order inside a batch */
+    pa[cur[bat[t]]] = ia[t];
+    pb[cur[bat[t]]++] = ib[t];
+  }
+  free(cur);
+  free(last);
+  free(bat);
+  free(ia);
+  free(ib);
+  return nb;
+}
+static void ph_pp_exchange(gx_engine *e, uint32_t t, void *ctx) {
+  const struct ae_ctx *c = (const struct ae_ctx *)ctx;
+  if (ae_pair_ok(e, c->pa[t], c->pb[t])) ae_exchange(e, c->pa[t], c->pb[t], c->now);
+}
+static void ae_phase_initiate(gx_engine *e) {
+  if (!ae_round(e) || e->ae_local_round == e->round) return;
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H + 1)), *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H + 1));
+  uint32_t *boff = (uint32_t *)malloc(sizeof(uint32_t) * (e->H + 2));
+  const uint32_t nb = pp_batches(e, pa, pb, boff);
+  for (uint32_t q = 0; q < nb; q++) {
+    struct ae_ctx c = {pa + boff[q], pb + boff[q], now_of(e)};
+    for_hosts(e, boff[q + 1] - boff[q], ph_pp_exchange, &c);
+  }
+  free(pa);
+  free(pb);
+  free(boff);
   e->ae_local_round = e->round;
 }
 
@@ -1084,6 +1170,10 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
+  if (p->gossip_messages > 16 || (p->gossip_messages > 1 && p->fd_enable)) return GX_EINVAL;
+  if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
+    return GX_EINVAL;
+  if (p->inbox_slots > 64) return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1150,11 +1240,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->A = p->list_slots;
   e->L = p->packet_cap + p->pending_cap;
   e->K = p->fanout;
+  e->NG = p->gossip_messages > 1 ? p->gossip_messages : 1;
+  e->KE = e->K * e->NG;
   e->G = p->n_shards > 1 ? p->n_shards : 1;
   e->gid = e->G > 1 ? p->shard_id : 0;
   e->lo = shard_lo(e, e->gid);
   e->hi = shard_lo(e, e->gid + 1);
-  e->SQ = pow2_at_least(64 > e->K * (p->retransmit_rounds + 1) ? 64 : e->K * (p->retransmit_rounds + 1));
+  e->SQ = pow2_at_least(64 > e->KE * (p->retransmit_rounds + 1) ? 64 : e->KE * (p->retransmit_rounds + 1));
   e->DQ = pow2_at_least(e->L + p->pending_cap + 64);
   size_t H = e->H;
   e->view = (uint64_t *)malloc(sizeof(uint64_t) * H * e->R);
@@ -1165,11 +1257,11 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->dq = (grec *)calloc(H * e->DQ, sizeof(grec));
   e->arena = (grec *)calloc(H * e->A * e->L, sizeof(grec));
   e->arena_len = (uint32_t *)calloc(H * e->A, sizeof(uint32_t));
-  e->msg = (grec *)calloc(H * (e->K ? e->K : 1) * p->packet_cap, sizeof(grec));
-  e->msg_len = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
-  e->msg_dst = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
+  e->msg = (grec *)calloc(H * (e->KE ? e->KE : 1) * p->packet_cap, sizeof(grec));
+  e->msg_len = (uint32_t *)calloc(H * (e->KE ? e->KE : 1), sizeof(uint32_t));
+  e->msg_dst = (uint32_t *)calloc(H * (e->KE ? e->KE : 1), sizeof(uint32_t));
   e->in_cnt = (uint32_t *)calloc(H + 1, sizeof(uint32_t));
-  e->in_list = (uint32_t *)calloc(H * (e->K ? e->K : 1), sizeof(uint32_t));
+  e->in_list = (uint32_t *)calloc(H * (e->KE ? e->KE : 1), sizeof(uint32_t));
   e->sbytes = (uint16_t *)malloc(sizeof(uint16_t) * e->R);
   e->srvt = (gx_server_times *)malloc(sizeof(gx_server_times) * H * H);
   e->vlc = (int64_t *)malloc(sizeof(int64_t) * H);
@@ -1706,7 +1798,7 @@ int gx_round_send(gx_engine *e) {
 int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   if (!e || !bytes) return GX_EINVAL;
   for (uint32_t g = 0; g < e->G; g++) bytes[g] = 0;
-  for (size_t m = (size_t)e->lo * e->K; m < (size_t)e->hi * e->K; m++)
+  for (size_t m = (size_t)e->lo * e->KE; m < (size_t)e->hi * e->KE; m++)
     if ((e->msg_len[m] || fd_len_of(e, m)) && !is_local(e, e->msg_dst[m])) bytes[shard_of(e, e->msg_dst[m])] += slot_bytes(e);
   return GX_OK;
 }
@@ -1715,7 +1807,7 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   uint8_t *p = (uint8_t *)buf;
   size_t off = 0, sb = slot_bytes(e);
   for (uint32_t g = 0; g < e->G; g++)
-    for (size_t m = (size_t)e->lo * e->K; m < (size_t)e->hi * e->K; m++) {
+    for (size_t m = (size_t)e->lo * e->KE; m < (size_t)e->hi * e->KE; m++) {
       if ((!e->msg_len[m] && !fd_len_of(e, m)) || is_local(e, e->msg_dst[m]) || shard_of(e, e->msg_dst[m]) != g) continue;
       if (off + sb > cap) return GX_EINVAL;
       uint32_t nfd = fd_len_of(e, m);
@@ -1741,7 +1833,7 @@ int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
     uint32_t hdr[4];
     memcpy(hdr, p + off, 16);
     uint32_t m = hdr[0], dst = hdr[1], len = hdr[2], nfd = e->p.fd_enable ? hdr[3] : 0;
-    if (m >= e->H * e->K || !is_local(e, dst) || len > e->p.packet_cap || nfd > e->p.fd_msg_cap) return GX_EINVAL;
+    if (m >= e->H * e->KE || !is_local(e, dst) || len > e->p.packet_cap || nfd > e->p.fd_msg_cap) return GX_EINVAL;
     memcpy(&e->msg[(size_t)m * e->p.packet_cap], p + off + 16, 16ull * len);
     e->msg_len[m] = len;
     e->msg_dst[m] = dst;
@@ -2096,18 +2188,32 @@ int gx_round_end(gx_engine *e) {
   round_end(e);
   return GX_OK;
 }
+/* Row-major: each chunk of records is folded over the views in view order (streaming reads). */
 int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
   if (!e || !mn || !mx) return GX_EINVAL;
-  for (uint32_t r = 0; r < e->R; r++) {
-    uint64_t a = ~0ull, b = 0;
+  const uint32_t CH = 4096, nch = (e->R + CH - 1) / CH;
+#ifdef GX_ORACLE_OMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t r0 = c * CH, r1 = r0 + CH < e->R ? r0 + CH : e->R;
+    for (uint32_t r = r0; r < r1; r++) {
+      mn[r] = ~0ull;
+      mx[r] = 0;
+    }
     for (uint32_t v = e->lo; v < e->hi; v++) {
       if (departed(e, v)) continue;
-      uint64_t w = e->view[(size_t)v * e->R + r];
-      a = w < a ? w : a;
-      b = w > b ? w : b;
+      const uint64_t *row = &e->view[(size_t)v * e->R];
+      for (uint32_t r = r0; r < r1; r++) {
+        const uint64_t w = row[r];
+        mn[r] = w < mn[r] ? w : mn[r];
+        mx[r] = w > mx[r] ? w : mx[r];
+      }
     }
-    mn[r] = a ^ (1ull << 63);
-    mx[r] = b ^ (1ull << 63);
+    for (uint32_t r = r0; r < r1; r++) {
+      mn[r] ^= 1ull << 63;
+      mx[r] ^= 1ull << 63;
+    }
   }
   return GX_OK;
 }

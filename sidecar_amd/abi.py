@@ -88,6 +88,7 @@ class GxParams(C.Structure):
         ("fd_gossip_dead_rounds", C.c_uint32), ("fd_suspicion_k", C.c_uint32),
         ("fd_suspicion_rounds", C.c_uint32 * 8), ("depart_round", C.c_int32), ("depart_ppm", C.c_uint32),
         ("fd_push_pull_state", C.c_uint32),
+        ("gossip_messages", C.c_uint32), ("push_pull_mode", C.c_uint32), ("inbox_slots", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)

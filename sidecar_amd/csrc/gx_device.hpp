@@ -9,6 +9,7 @@
 //   dq        grec [H][DQ]    delegate pendingBroadcasts as a deque (push-front batch, pop packet)
 //   arena     grec [H][A][L]  SendServices lists (L = packet_cap + pending_cap)
 //   msg       grec [H][K][cap] this round's packets, msg_len/msg_dst [H][K]
+//   in_hdr    uint4 [H][DI]   receiver inboxes: packet headers registered by the senders
 //
 // The scalar helpers below are the one-thread-per-host form of the reference semantics, used by
 // the per-host round kernels (owner ticks, GetBroadcasts) and by the single-host ABI entry points.
@@ -58,9 +59,10 @@ enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS =
 struct Dev {
   gx_params p;
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  uint32_t NG, KE;           // GossipMessages gathers per target; packet entries per host = K * NG
   uint32_t lo, Hl, G, gid;  // this engine owns hosts [lo, lo + Hl); per-host arrays are local
   uint32_t n_remote;        // packets received from other shards this round
-  uint32_t *msg_key;        // [H*K] global sender * K + j of each packet entry
+  uint32_t *msg_key;        // [H*KE] global sender * KE + j * NG + n of each packet entry
   int64_t round, now;
   int partitioned;
   uint64_t *view;
@@ -75,10 +77,17 @@ struct Dev {
   grec *msg;
   uint32_t *msg_len;
   uint32_t *msg_dst;
-  uint32_t *in_cnt;    // [H+1] receiver counts, then exclusive offsets
-  uint32_t *in_cur;    // [H] fill cursors
-  uint32_t *in_fill;   // [H*K] entries in arrival order (atomic fill)
-  uint2 *in_sorted;    // [H*K] (entry, length) sender-ordered per receiver
+  // Receiver inboxes: a sender registers each packet straight into its receiver's
+  // inbox with one atomic; the merge sorts a receiver's few headers by global sender key itself.
+  uint32_t DI;         // inbox slots per receiver (<= 64); packets past them go to the overflow list
+  uint32_t DR;         // inbox slots whose records are stored inline (in_rec); the rest stay in msg
+  uint32_t *in_cnt;    // [Hl] packets registered per receiver this round
+  uint4 *in_hdr;       // [Hl][DI] {global key = sender * K + j, entry, len, slot}, arrival order
+  uint4 *in_ovf;       // [H*K] {key, entry, len, local receiver} past a receiver's DI slots
+  grec *in_rec;        // [Hl][DR][packet_cap] records of a receiver's first DR packets
+  uint32_t *work_cnt;  // [0] expiry-scan worklist, [1] unused, [2] overflow count, [3] error bits
+  uint32_t *work;      // [Hl] views whose expiry scan must stream the row this round
+  uint8_t *mflag;      // [Hl] receivers k_merge_lean left to k_merge (a live record or > DR packets)
   grec *scan_list;     // [H][L] first L expired records of this round's scan
   uint32_t *scan_cnt;  // [H]
   uint8_t *tick;       // [H] BroadcastTombstones tick this round
@@ -201,6 +210,7 @@ GXD void kbytes(const Dev &d, int k, unsigned long long b, unsigned long long u)
 }
 GXD void acc_flush(const Dev &d, const Acc &a) {
   for (int i = 0; i < C_NCTR; i++) {
+    if (__ballot(a.c[i] != 0) == 0) continue;  // most counters are zero in most waves
     unsigned long long x = wave_sum((unsigned long long)a.c[i]);
     if ((threadIdx.x & 63) == 0) ctr_atomic(d, i, x);
   }
@@ -215,6 +225,49 @@ GXD uint32_t owner_of(const Dev &d, uint32_t r) { return d.S == 1 ? r : (uint32_
 // r belongs to owner o (r / S == o) as one range compare
 GXD bool owned_by(const Dev &d, uint32_t r, uint32_t o) { return r - o * d.S < d.S; }
 GXD bool departed(const Dev &d, uint32_t u) { return d.departures && departed_at(d.p, d.round, u); }
+
+// ------------------------------------------------------------------------ receiver inboxes --
+#define GX_ERR_INBOX 1u  // work_cnt[3]: a received packet slot failed validation (k_inbox_unpack)
+// Register a packet (global sender key, message entry) in local receiver vi's inbox: one atomic
+// on the receiver's count; returns the inbox position (slot). The header itself (with the record
+// count) is written by inbox_header once the packet is packed.
+GXD uint32_t inbox_claim(const Dev &d, uint32_t vi) { return atomicAdd(&d.in_cnt[vi], 1u); }
+GXD void inbox_header(const Dev &d, uint32_t vi, uint32_t pos, uint32_t key, uint32_t entry, uint32_t len) {
+  if (pos < d.DI) d.in_hdr[(size_t)vi * d.DI + pos] = make_uint4(key, entry, len, pos);
+  else d.in_ovf[atomicAdd(&d.work_cnt[2], 1u)] = make_uint4(key, entry, len, vi);
+}
+GXD void inbox_put(const Dev &d, uint32_t vi, uint32_t key, uint32_t entry, uint32_t len) {
+  inbox_header(d, vi, inbox_claim(d, vi), key, entry, len);
+}
+// Where the records of a packet registered at inbox position `slot` live: inline in the receiver's
+// inbox for its first DR packets, else in the sender's message entry.
+GXD grec *packet_recs(const Dev &d, uint32_t vi, uint32_t slot, uint32_t entry) {
+  return slot < d.DR ? &d.in_rec[((size_t)vi * d.DR + slot) * d.p.packet_cap] : &d.msg[(size_t)entry * d.p.packet_cap];
+}
+// Overflowed inboxes (more than DI packets): the header of receiver vi with the smallest key
+// above `after` (-1: the first). O(DI + overflow list) per call; the merge then walks the inbox in
+// key order one header at a time. Keys are distinct (one packet per sender slot).
+GXD uint4 inbox_next(const Dev &d, uint32_t vi, int64_t after) {
+  uint4 best = make_uint4(0xffffffffu, 0u, 0u, 0u);
+  bool found = false;
+  const uint32_t cnt = d.in_cnt[vi], n = cnt < d.DI ? cnt : d.DI;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint4 h = d.in_hdr[(size_t)vi * d.DI + i];
+    if ((int64_t)h.x > after && (!found || h.x < best.x)) {
+      best = h;
+      found = true;
+    }
+  }
+  const uint32_t no = d.work_cnt[2];
+  for (uint32_t i = 0; i < no; i++) {
+    const uint4 h = d.in_ovf[i];
+    if (h.w == vi && (int64_t)h.x > after && (!found || h.x < best.x)) {
+      best = make_uint4(h.x, h.y, h.z, 0xffffffffu);  // past DI: records in the message entry
+      found = true;
+    }
+  }
+  return best;
+}
 // memberlist state of this engine's host v (rows are shard-local, like the views)
 GXD gx_member *memp(const Dev &d, uint32_t v, uint32_t m) { return &d.mem[(size_t)li(d, v) * d.H + m]; }
 GXD int32_t *dlp(const Dev &d, uint32_t v, uint32_t m) { return &d.fd_dl[(size_t)li(d, v) * d.H + m]; }
@@ -432,9 +485,11 @@ GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const
 // record i from the job, then the pending ring); only the batch records that stay pending are
 // written to the ring. limit = record budget (the packet buffer); limit_bytes > 0 adds the byte
 // budget + overhead. Every lane of the team calls it; ring writes are fenced before the next call.
+// pj: the job at the FIFO head when the caller loaded it ahead of the call (LDS), else null.
 template <int T>
 GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, uint32_t limit,
-                                 grec *packet, uint32_t limit_bytes, uint32_t overhead) {
+                                 grec *packet, uint32_t limit_bytes, uint32_t overhead,
+                                 const gx_job *pj = nullptr) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lane0 = tl == 0;
   const uint32_t mask = d.DQ - 1;
@@ -442,7 +497,7 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
   gx_job j = make_job(0, 0, 0, 0);
   uint32_t m = 0;
   if (hs.fifo_head != hs.fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
-    j = d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_head % d.Q)];
+    j = pj ? *pj : d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_head % d.Q)];
     hs.fifo_head++;
     if (lane0) a.c[C_DEQ]++;
     m = job_len(d, j);
@@ -517,13 +572,19 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
       a.c[C_BYTESENT] += (unsigned)total;
     }
   }
-  for (uint32_t i = tl; i < l; i += T) packet[i] = item(i);
+  // Ring position p is read and written only by team lane p % T (T divides DQ), so a record that
+  // a call leaves pending is seen by the same lane in the next call without a fence; batch records
+  // (list arena, job) and packet slots are not written and read back here, any lane moves them.
+  const uint32_t lb = l < m ? l : m;
+  for (uint32_t i = tl; i < lb; i += T) packet[i] = item(i);
+  if (l > m)  // the pending prefix, ring positions head .. head + l - m - 1, by their owner lanes
+    for (uint32_t q = (tl - head) & (T - 1); q < l - m; q += T) packet[m + q] = dq[(head + q) & mask];
   // leftover = broadcast[l:]; batch records that stay pending go in front of the old head
   uint32_t nh;
   if (l < m) {
     uint32_t k = m - l;
     nh = (head - k) & mask;
-    for (uint32_t i = tl; i < k; i += T) dq[(nh + i) & mask] = item(l + i);
+    for (uint32_t q = (tl - nh) & (T - 1); q < k; q += T) dq[(nh + q) & mask] = item(l + q);
   } else {
     nh = (head + (l - m)) & mask;
   }
@@ -537,7 +598,9 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
     a.c[C_PACKETS]++;
     a.c[C_RECSENT] += l;
   }
-  __threadfence_block();  // ring and FIFO stores are visible to the wave's next call
+  // Byte mode reads ring records on any lane (the byte scan), and with no retransmit sleep a
+  // re-armed job is pushed to the FIFO and may be dequeued by the next call: those need the fence.
+  if (limit_bytes || d.p.retransmit_rounds == 0) __threadfence_block();
   return l;
 }
 

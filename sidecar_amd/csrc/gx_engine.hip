@@ -3,18 +3,21 @@
 // Implements include/gx.h. One engine object owns one GPU's slice of the simulated cluster and
 // advances it one gossip round at a time (gx_run_rounds). Round phases and the kernels that run
 // them (DESIGN.md "Round model", "Kernels"):
-//   0+1 k_owner      wake re-armed SendServices passes; discovery churn; BroadcastServices tick
-//                    (services_state.go:525-574) + TrackNewServices; flag BroadcastTombstones ticks
-//   1   k_scan       TombstoneOthersServices full-view expiry scan (services_state.go:635-683),
-//                    one 256-thread block streams one 4 MB view row, ordered compaction of tombstones
-//   1   k_bt_finish  TombstoneServices + SendServices(TOMBSTONE_COUNT) or nil (services_state.go:606-633)
+//   0+1 k_owner      a team of S lanes per host: wake re-armed SendServices passes; discovery churn;
+//                    BroadcastServices tick (services_state.go:525-574) + TrackNewServices; the
+//                    BroadcastTombstones tick lists the views whose expiry scan can change anything
+//   1   k_scan       TombstoneOthersServices full-view expiry scan (services_state.go:635-683) over
+//                    that worklist: one 256-thread block streams one 4 MB view row, ordered compaction
+//   1   k_bt_finish  TombstoneServices + SendServices(TOMBSTONE_COUNT) or nil (services_state.go:606-633);
+//                    folded into k_send unless another phase queues jobs in between (storm, detector)
 //   2   k_storm      NotifyLeave -> ExpireServer for every host of the other half (services_state.go:150-192)
-//   3   k_send       peer sampling + GetBroadcasts/packPacket per peer (services_delegate.go:85-144,186-223)
-//   3b  k_route_*    receiver-side CSR of this round's packets, sender-ordered (deterministic)
-//   4   k_merge      gather-then-merge: one wave per receiver stages its inbound records in LDS,
-//                    folds duplicates of a key in arrival order with the AddServiceEntry rule
-//                    (services_state.go:293-347), writes each touched slot once, and compacts
-//                    accepted foreign records into the receiver's broadcast FIFO with a wave ballot
+//   3   k_send       peer sampling + GetBroadcasts/packPacket per peer (services_delegate.go:85-144,186-223);
+//                    each packet is registered in its receiver's inbox with one atomic
+//   4   k_merge      gather-then-merge: one wave per receiver sorts its inbox by sender key, takes its
+//                    inbound records straight from the packets, folds duplicates of a key in arrival
+//                    order with the AddServiceEntry rule (services_state.go:293-347), writes each
+//                    touched slot once, and compacts accepted foreign records into the receiver's
+//                    broadcast FIFO with a wave ballot
 //   5   k_ae         anti-entropy push-pull: one 256-thread block per host pair streams both views
 //                    and merges each into the other (services_delegate.go:153-167, Merge :367-373)
 // No MFMA: the work is int64 compare/select over HBM-resident views (memory-bound).
@@ -25,6 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <deque>
 #include <vector>
 
@@ -62,11 +66,13 @@ struct gx_engine {
   int device;
   int timing;
   std::vector<TimedLaunch> pending_ev;
+  std::vector<uint32_t> pp_host;  // GX_PP_INITIATE: this round's exchanges, batch by batch (a then b)
+  uint32_t *pp_dev;
+  int32_t *pp_prow;               // all -1: every exchange is local
   double ms[GX_K_COUNT];
   uint64_t launches[GX_K_COUNT];
   uint64_t host_bytes[GX_K_COUNT], host_units[GX_K_COUNT];  // codec classes (gx_codec_host.hpp)
   struct CodecState *codec;
-  grec *own_list;
   // sharded rounds: outbox entry list and push-pull plan (device), rebuilt per round
   uint32_t *ob_entries;
   uint32_t *ob_counts;  // [G] packets per destination shard, then [chunks][G] counts and offsets
@@ -197,9 +203,22 @@ static int deliver_events(gx_engine *e) {
   return GX_OK;
 }
 
+// A received packet slot that failed validation (k_inbox_unpack: the oracle's gx_inbox_unpack
+// checks) was skipped on the device; the next call that waits reports it, once.
+static int take_device_error(gx_engine *e) {
+  if (e->d.G < 2) return GX_OK;
+  uint32_t err = 0;
+  HIPCHK(hipMemcpy(&err, &e->d.work_cnt[3], sizeof(err), hipMemcpyDeviceToHost));
+  if (!err) return GX_OK;
+  HIPCHK(hipMemset(&e->d.work_cnt[3], 0, sizeof(err)));
+  return GX_EINVAL;
+}
+
 static int sync_check(gx_engine *e) {
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipGetLastError());
+  int rc = take_device_error(e);
+  if (rc) return rc;
   return e->log_views.empty() ? GX_OK : deliver_events(e);
 }
 
@@ -216,28 +235,49 @@ static int phase_done(gx_engine *e) {
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // Phases 0-3 (wake, owners, expiry scan, storm, GetBroadcasts) for this engine's hosts.
+// k_owner with a team of T >= S lanes per host (lane s = service s)
+template <int T>
+static void launch_owner(const Dev &d, hipStream_t s) {
+  k_owner<T><<<nblk(d.Hl, 256 / T), 256, 0, s>>>(d);
+}
+static void owner_launch(const Dev &d, hipStream_t s) {
+  if (d.S <= 1) launch_owner<1>(d, s);
+  else if (d.S <= 2) launch_owner<2>(d, s);
+  else if (d.S <= 4) launch_owner<4>(d, s);
+  else if (d.S <= 8) launch_owner<8>(d, s);
+  else if (d.S <= 16) launch_owner<16>(d, s);
+  else if (d.S <= 32) launch_owner<32>(d, s);
+  else launch_owner<64>(d, s);
+}
+#define SCAN_GRID 2048  // worklist blocks: 8 per CU when many views expire, a quick exit when none do
+
+// Phases 0-3 (wake, owners, expiry scan, storm, GetBroadcasts) for this engine's hosts.
 static int round_send_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
   d.n_remote = 0;
   hipStream_t s = e->stream;
   bool vec = (d.R % 2) == 0;
+  const bool storm = d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2;
+  // BroadcastTombstones' SendServices is queued before the detector's and the storm's jobs
+  const bool bt_apart = d.p.fd_enable || storm;
   {
     LaunchTimer t(e, GX_K_OWNER);
-    k_owner<<<nblk(d.Hl, 256), 256, 0, s>>>(d, e->own_list);
+    owner_launch(d, s);
   }
   {
     LaunchTimer t(e, GX_K_SCAN);
     const bool ev = !e->log_views.empty();
+    const unsigned grid = d.Hl < SCAN_GRID ? d.Hl : SCAN_GRID;
     (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
-        <<<d.Hl, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
-    k_bt_finish<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
+        <<<grid, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
+    if (bt_apart) k_bt_finish<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   }
   if (d.p.fd_enable) {  // suspicion timers -> deadNode -> NotifyLeave; probe ticks
     LaunchTimer t(e, GX_K_FD);
     k_fd_tick<<<d.Hl, 64, 0, s>>>(d);
   }
-  if (d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2) {
+  if (storm) {
     LaunchTimer t(e, GX_K_STORM);
     const bool ev = !e->log_views.empty();
     if (d.S >= 2 && 64 % d.S == 0) (ev ? k_storm_p2<true> : k_storm_p2<false>)<<<d.Hl, 256, 0, s>>>(d);
@@ -247,32 +287,25 @@ static int round_send_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_SEND);
     if (d.p.fd_enable) k_fd_send<<<nblk(d.Hl, 64), 64, 0, s>>>(d);  // memberlist's targets + messages
     // 4 lanes per host: measured best of 1/4/8/16/64 (profiles/send_team.sh)
-    if (d.p.fd_enable || d.departures) k_send<4, true><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
-    else k_send<4, false><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
+    if (d.p.fd_enable || d.departures) k_send<4, true><<<nblk(d.Hl, 64), 256, 0, s>>>(d, bt_apart ? 0 : 1);
+    else k_send<4, false><<<nblk(d.Hl, 64), 256, 0, s>>>(d, bt_apart ? 0 : 1);
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
 }
 
-// Phase 4: receiver CSR over local + received packets, then gather-then-merge.
+// Phase 4: gather-then-merge of every receiver's inbox (local and received packets).
 static int round_merge_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
   hipStream_t s = e->stream;
-  size_t ne = (size_t)d.Hl * d.K + d.n_remote;
   if (d.K) {
-    {
-      LaunchTimer t(e, GX_K_ROUTE);
-      k_route_offsets<<<1, 1024, 0, s>>>(d);
-      if (ne) {
-        k_route_fill<<<nblk(ne, 256), 256, 0, s>>>(d);
-        k_route_rank<<<nblk(ne, 256), 256, 0, s>>>(d);
-      }
-    }
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
-    if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<d.Hl, 64, 0, s>>>(d);  // 32-bit keys
-    else (ev ? k_merge<false, true> : k_merge<false, false>)<<<d.Hl, 64, 0, s>>>(d);
+    k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);
+    const unsigned g = nblk(d.Hl, MERGE_WAVES);
+    if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
+    else (ev ? k_merge<false, true> : k_merge<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
   }
   if (d.p.fd_enable && d.K) {  // the packets' memberlist messages, after the catalog merge
     LaunchTimer t(e, GX_K_FD);
@@ -287,13 +320,75 @@ static bool ae_round(const gx_engine *e) {
   return d.p.ae_period_rounds && (uint64_t)d.round % d.p.ae_period_rounds == d.p.ae_phase;
 }
 
+// GX_PP_INITIATE (unsharded engines): every live host starts one exchange with a partner drawn
+// at random on its side; the exchanges run in initiator order, in batches of exchanges with no
+// host in common (an exchange goes into the batch after the last one holding either of its hosts).
+// The oracle's pp_batches computes the same batches; each batch is one k_ae_plan launch over its
+// pair list (local pairs: both sides merge the other's pre-exchange row).
+static bool ae_partner(const Dev &d, uint32_t i, uint32_t *out) {
+  uint32_t base = 0, m = d.H;
+  if (d.partitioned && !d.p.fd_enable) {
+    const uint32_t half = d.H / 2;
+    base = i < half ? 0 : half;
+    m = i < half ? half : d.H - half;
+  }
+  if (m < 2) return false;
+  const uint64_t x = rng4(d.p.seed, ST_AE, (uint64_t)d.round, i, 1);
+  const uint32_t idx = unif(x, m - 1), self = i - base;
+  *out = base + (idx >= self ? idx + 1 : idx);
+  return true;
+}
+static int ae_initiate(gx_engine *e) {
+  Dev &d = e->d;
+  const bool dep = d.departures;
+  std::vector<uint32_t> last(d.H, 0), bat, ia, ib;
+  uint32_t nb = 0;
+  for (uint32_t i = 0; i < d.H; i++) {
+    uint32_t b;
+    if ((dep && departed_at(d.p, d.round, i)) || !ae_partner(d, i, &b) || (dep && departed_at(d.p, d.round, b))) continue;
+    const uint32_t k = 1 + std::max(last[i], last[b]);
+    last[i] = last[b] = k;
+    ia.push_back(i);
+    ib.push_back(b);
+    bat.push_back(k - 1);
+    nb = std::max(nb, k);
+  }
+  const size_t n = ia.size();
+  if (!n) return GX_OK;
+  std::vector<uint32_t> off(nb + 1, 0);
+  for (uint32_t x : bat) off[x + 1]++;
+  for (uint32_t q = 0; q < nb; q++) off[q + 1] += off[q];
+  std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+  e->pp_host.assign(2 * n, 0);
+  for (size_t t = 0; t < n; t++) {  // stable: initiator order inside a batch
+    const uint32_t at = cur[bat[t]]++;
+    e->pp_host[at] = ia[t];
+    e->pp_host[n + at] = ib[t];
+  }
+  HIPCHK(hipMemcpyAsync(e->pp_dev, e->pp_host.data(), sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, e->stream));
+  const bool vec = (d.R % 2) == 0, ev = !e->log_views.empty();
+  AeIn none;
+  memset(&none, 0, sizeof(none));
+  LaunchTimer t(e, GX_K_AE);
+  for (uint32_t q = 0; q < nb; q++) {
+    const uint32_t *pa = e->pp_dev + off[q], *pb = e->pp_dev + n + off[q];
+    const unsigned np = off[q + 1] - off[q];
+    if (ev) (vec ? k_ae_plan_ev<true> : k_ae_plan_ev<false>)<<<np, 256, 0, e->stream>>>(d, pa, pb, e->pp_prow, nullptr, none, nullptr);
+    else (vec ? k_ae_plan<true> : k_ae_plan<false>)<<<np, 256, 0, e->stream>>>(d, pa, pb, e->pp_prow, nullptr, none, nullptr);
+  }
+  return GX_OK;
+}
+
 // Phase 5 on an unsharded engine: pairs derived on device.
 static int ae_whole_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
   hipStream_t s = e->stream;
   bool vec = (d.R % 2) == 0;
-  if (ae_round(e)) {
+  if (ae_round(e) && d.p.push_pull_mode == GX_PP_INITIATE) {
+    int rc = ae_initiate(e);
+    if (rc) return rc;
+  } else if (ae_round(e)) {
     uint32_t np;
     uint64_t key0, key1 = 0;
     if (d.pair_split) {
@@ -438,6 +533,10 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
+  if (p->gossip_messages > 16 || (p->gossip_messages > 1 && p->fd_enable)) return GX_EINVAL;
+  if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
+    return GX_EINVAL;
+  if (p->inbox_slots > 64) return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -459,8 +558,8 @@ int gx_destroy(gx_engine *e) {
   Dev &d = e->d;
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
-                  d.msg_dst, d.in_cnt, d.in_cur, d.in_fill, d.in_sorted, d.scan_list, d.scan_cnt, d.tick,
-                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, e->own_list, e->api_dev, e->conv_bad, e->digest_buf,
+                  d.msg_dst, d.in_cnt, d.scan_list, d.scan_cnt, d.tick,
+                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->api_dev, e->conv_bad, e->digest_buf,
                   d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -495,7 +594,6 @@ int gx_create(const gx_params *p, gx_engine **out) {
   memset(e->host_bytes, 0, sizeof(e->host_bytes));
   memset(e->host_units, 0, sizeof(e->host_units));
   e->codec = nullptr;
-  e->own_list = nullptr;
   e->api_dev = nullptr;
   e->api_dev_bytes = 0;
   e->conv_bad = nullptr;
@@ -520,6 +618,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->n_plan = e->n_pack = e->n_plan_rows = 0;
   e->ae_planned_round = -1;
   e->ae_local_round = -1;
+  e->pp_dev = nullptr;
+  e->pp_prow = nullptr;
   Dev &d = e->d;
   d.p = *p;
   d.H = p->n_hosts;
@@ -529,6 +629,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.A = p->list_slots;
   d.L = p->packet_cap + p->pending_cap;
   d.K = p->fanout;
+  d.NG = p->gossip_messages > 1 ? p->gossip_messages : 1;
+  d.KE = d.K * d.NG;
   d.divS = d.S > 1 ? ~0ull / d.S + 1 : 0;
   d.logS = 0;
   while ((1u << d.logS) < d.S) d.logS++;  // used where S divides 64 (a power of two)
@@ -537,7 +639,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.lo = (uint32_t)(((uint64_t)d.gid * d.H) / d.G);
   d.Hl = (uint32_t)(((uint64_t)(d.gid + 1) * d.H) / d.G) - d.lo;
   d.n_remote = 0;
-  d.SQ = pow2_at_least(64 > d.K * (p->retransmit_rounds + 1) ? 64 : d.K * (p->retransmit_rounds + 1));
+  d.SQ = pow2_at_least(64 > d.KE * (p->retransmit_rounds + 1) ? 64 : d.KE * (p->retransmit_rounds + 1));
   d.DQ = pow2_at_least(d.L + p->pending_cap + 64);
   d.round = 0;
   if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -548,7 +650,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->async_phases = 0;
   // per-host arrays hold this shard's Hl hosts; the message table also takes the packets received
   // from other shards (at most (H - Hl) * K), so it is sized H * K.
-  size_t Hg = d.H, H = d.Hl, K = d.K ? d.K : 1;
+  size_t Hg = d.H, H = d.Hl, K = d.KE ? d.KE : 1;
   ALLOC(d.view, sizeof(uint64_t) * H * d.R);
   ALLOC(d.own_status, H * d.S);
   ALLOC(d.hs, sizeof(gx_host_state) * H);
@@ -561,12 +663,22 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.msg_len, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_dst, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_key, sizeof(uint32_t) * Hg * K);
-  size_t in_pad = ((H + 1 + 16383) / 16384) * 16384 + 16;  // k_route_offsets reads 16-count rows
-  ALLOC(d.in_cnt, sizeof(uint32_t) * in_pad);
+  ALLOC(d.in_cnt, sizeof(uint32_t) * H);
+  d.DI = p->inbox_slots ? p->inbox_slots : 64;
+  d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
+  if (const char *x = getenv("GX_AB_INLINE_SLOTS")) d.DR = std::min<uint32_t>(d.DI, (uint32_t)atoi(x));  // A/B only
+  ALLOC(d.in_hdr, sizeof(uint4) * H * d.DI);
+  ALLOC(d.in_ovf, sizeof(uint4) * Hg * K);
+  ALLOC(d.in_rec, sizeof(grec) * H * d.DR * p->packet_cap);
+  ALLOC(d.work_cnt, sizeof(uint32_t) * 4);
+  ALLOC(d.work, sizeof(uint32_t) * H);
+  if (p->push_pull_mode == GX_PP_INITIATE) {
+    ALLOC(e->pp_dev, sizeof(uint32_t) * 2 * Hg);
+    ALLOC(e->pp_prow, sizeof(int32_t) * Hg);
+    HIPCHK(hipMemset(e->pp_prow, 0xff, sizeof(int32_t) * Hg));
+  }
+  ALLOC(d.mflag, H);
   ALLOC(d.minexp, sizeof(unsigned long long) * H);
-  ALLOC(d.in_cur, sizeof(uint32_t) * H);
-  ALLOC(d.in_fill, sizeof(uint32_t) * Hg * K);
-  ALLOC(d.in_sorted, sizeof(uint2) * Hg * K);
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
   ALLOC(d.tick, H);
@@ -575,7 +687,6 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.vlc, sizeof(int64_t) * H);
   ALLOC(d.ev_slot, sizeof(int32_t) * H);
   ALLOC(d.ctr, sizeof(DevCtr));
-  ALLOC(e->own_list, sizeof(grec) * H * d.S);
   d.departures = p->depart_round >= 0 && p->depart_ppm;
   if (p->fd_enable) {  // member rows of this shard's hosts
     ALLOC(d.mem, sizeof(gx_member) * H * Hg);
@@ -623,7 +734,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   HIPCHK(hipMemsetAsync(d.ctr, 0, sizeof(DevCtr), s));
   HIPCHK(hipMemsetAsync(d.arena_len, 0, sizeof(uint32_t) * H * d.A, s));
   HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * Hg * K, s));
-  HIPCHK(hipMemsetAsync(d.in_cnt, 0, sizeof(uint32_t) * in_pad, s));
+  HIPCHK(hipMemsetAsync(d.in_cnt, 0, sizeof(uint32_t) * H, s));
+  HIPCHK(hipMemsetAsync(d.work_cnt, 0, sizeof(uint32_t) * 4, s));
   HIPCHK(hipMemsetAsync(d.tick, 0, H, s));
   HIPCHK(hipMemsetAsync(d.ev_slot, 0xff, sizeof(int32_t) * H, s));  // -1: no listener
   k_fill_u16<<<256, 256, 0, s>>>(d.sbytes, d.R, (uint16_t)GX_STATIC_BYTES_DEFAULT);
@@ -1267,7 +1379,7 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   e->n_ob = 0;
   if (d.G < 2 || !d.K) return GX_OK;
   set_round_fields(e);
-  const size_t ne = (size_t)d.Hl * d.K;
+  const size_t ne = (size_t)d.Hl * d.KE;
   const uint32_t nchunk = (uint32_t)((ne + 255) / 256);
   uint32_t *ccnt = e->ob_counts + d.G, *off = ccnt + (size_t)nchunk * d.G;
   const size_t lds = sizeof(uint32_t) * 4 * d.G;
@@ -1299,7 +1411,7 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
   if (!e || (bytes && !buf) || bytes % slot_bytes(e->d)) return GX_EINVAL;
   uint64_t n = bytes / slot_bytes(e->d);
-  if (n > (uint64_t)(e->d.H - e->d.Hl) * e->d.K) return GX_EINVAL;
+  if (n > (uint64_t)(e->d.H - e->d.Hl) * e->d.KE) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   if (n) k_inbox_unpack<<<(unsigned)n, 64, 0, e->stream>>>(e->d, (const uint8_t *)buf, (uint32_t)n);
   e->d.n_remote = (uint32_t)n;

@@ -625,8 +625,13 @@ __global__ __launch_bounds__(64) void k_fd_recv(Dev d) {  // one thread per rece
     const uint32_t cap = d.p.fd_msg_cap;
     // the packets' messages are read-only here: the next one is loaded before the current
     // message's handler runs, so its load is not ordered behind the handler's row writes
-    for (uint32_t x = d.in_cnt[vi]; x < d.in_cnt[vi + 1]; x++) {
-      const uint32_t e = d.in_sorted[x].x, n = d.fd_len[e];
+    // the inbox in sender order (a selection walk over the few headers)
+    const uint32_t cnt = d.in_cnt[vi];
+    int64_t after = -1;
+    for (uint32_t x = 0; x < cnt; x++) {
+      const uint4 hx = inbox_next(d, vi, after);
+      after = hx.x;
+      const uint32_t e = hx.y, n = d.fd_len[e];
       const gx_fd_msg *pk = &d.fdm[(size_t)e * cap];
       gx_fd_msg cur = n ? pk[0] : gx_fd_msg{};
       for (uint32_t y = 0; y < n; y++) {

@@ -157,81 +157,175 @@ __global__ void k_wake(Dev d) {
 }
 
 // ================================================================= phase 0+1: owner ticks ==
-// One thread per host: wake re-armed passes, discovery churn, BroadcastServices tick +
-// TrackNewServices, and flag the BroadcastTombstones tick. Also clears this round's CSR counts.
-__global__ __launch_bounds__(256) void k_owner(Dev d, grec *own_list) {
+// A team of T >= S lanes per host (lane s = service s): wake re-armed passes, discovery churn,
+// the BroadcastServices tick (services_state.go:525-574) with IsNewService (:509-521) and
+// TrackNewServices (:446-453), and the BroadcastTombstones tick. The looper state is the team's
+// register copy of the host's bookkeeping; the lead lane stores it and the FIFO pushes. The S
+// IsNewService reads and the S AddServiceEntry merges of the tick are independent (distinct own
+// keys), so they run on their lanes; everything the reference orders (list order, LastUpdated /
+// LastChanged, the ChangeEvents) follows from ballots in list order. Every included record is
+// restamped `now`, so the server's times all take that value.
+// A ticking view whose exact expiry bound is in the future cannot change in
+// TombstoneOthersServices (:645-662); the others go to the expiry scan's worklist. Also clears this
+// round's inbox counts.
+template <int T>
+__global__ __launch_bounds__(256) void k_owner(Dev d) {
+  __shared__ gx_job s_sl[256];  // the head of each host's sleep ring, one job per team lane
   Acc a;
-  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < d.Hl) {
-    uint32_t o = d.lo + idx;
-    d.in_cnt[idx] = 0;
-    d.in_cur[idx] = 0;
-    if (idx == 0) d.in_cnt[d.Hl] = 0;
-    if (departed(d, o)) {  // a crashed host runs no loopers
-      d.tick[idx] = 0;
-      goto done;
-    }
-    wake_host(d, a, o);
-    gx_host_state *h = &d.hs[idx];
-    if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
-      uint64_t x = rng4(d.p.seed, ST_CHURN, (uint64_t)d.round, o, 0);
-      if ((uint32_t)(x & 0xffffffffu) % 1000000u < d.p.churn_ppm) {
-        uint32_t s = (uint32_t)((x >> 32) % d.S);
-        h->running ^= 1ull << s;
-        if ((h->running >> s) & 1ull) d.own_status[(size_t)idx * d.S + s] = GX_ALIVE;
-        a.c[C_CHURN]++;
-      }
-    }
-    if (!(h->flags & 1u) && h->bs_next <= d.round) {
-      grec *list = &own_list[(size_t)idx * d.S];  // fn(): running services, restamped now
-      uint32_t n = 0;
-      uint64_t run = h->running;
-      for (uint32_t s = 0; s < d.S; s++)
-        if ((run >> s) & 1ull) {
-          list[n].w = pack(d.now, d.own_status[(size_t)idx * d.S + s]);
-          list[n].r = o * d.S + s;
-          list[n].pad = 0;
-          n++;
-        }
-      uint64_t inc = 0;
-      bs_body_list(d, a, o, list, n, inc);
-      if (inc) {
-        h->bs_next = d.round + d.p.alive_interval_rounds;
-        for (uint32_t i = 0; i < n; i++)
-          if ((inc >> i) & 1ull) add_entry(d, a, o, list[i], SRC_LOCAL);  // TrackNewServices
-      }
-    }
-    d.tick[idx] = (!(h->flags & 2u) && h->bt_next <= d.round) ? 1 : 0;
+  const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
+  const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
+  const bool lead = tl == 0;
+  const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.work_cnt[2] = 0;  // this round's inbox overflow list
+  const bool act = idx < d.Hl && !departed(d, d.lo + idx);
+  gx_host_state hs;
+  gx_job *sj = &s_sl[threadIdx.x - tl];
+  if (act) {
+    hs = d.hs[idx];
+    if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
   }
-done:
+  __syncthreads();
+  if (idx < d.Hl) {
+    const uint32_t o = d.lo + idx;
+    if (lead) d.in_cnt[idx] = 0;
+    if (!act) {  // a crashed host runs no loopers
+      if (lead) d.tick[idx] = 0;
+    } else {
+      // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO in order
+      for (uint32_t w = 0; hs.sleep_head != hs.sleep_tail; w++) {
+        const gx_job j = w < (uint32_t)T ? sj[w] : d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
+        if ((int64_t)j.wake > d.round) break;
+        hs.sleep_head++;
+        push_job_r(d, a, o, hs, j, lead);
+      }
+      const uint32_t s = tl;
+      const bool svc = s < d.S;
+      uint8_t ost = svc ? d.own_status[(size_t)idx * d.S + s] : (uint8_t)GX_ALIVE;
+      if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
+        const uint64_t x = rng4(d.p.seed, ST_CHURN, (uint64_t)d.round, o, 0);
+        if ((uint32_t)(x & 0xffffffffu) % 1000000u < d.p.churn_ppm) {
+          const uint32_t cs = (uint32_t)((x >> 32) % d.S);
+          hs.running ^= 1ull << cs;
+          if (s == cs && ((hs.running >> cs) & 1ull)) {
+            ost = GX_ALIVE;
+            d.own_status[(size_t)idx * d.S + s] = GX_ALIVE;
+          }
+          if (lead) a.c[C_CHURN]++;
+        }
+      }
+      if (!(hs.flags & 1u) && hs.bs_next <= d.round) {
+        // fn(): the running services in key order, restamped now; lane s holds service s
+        const bool run = svc && ((hs.running >> s) & 1ull);
+        const uint32_t r = o * d.S + s;
+        uint64_t *slot = &vrow(d, o)[run ? r : o * d.S];
+        const uint64_t sw = pack(d.now, ost);
+        const uint64_t cur = run ? *slot : GX_SLOT_ABSENT;
+        const bool isnew = run && (st_of(cur) == GX_ABSENT || (st_of(sw) != GX_TOMBSTONE && st_of(sw) != st_of(cur)));
+        const bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > hs.last_bcast_ns;  // (:547)
+        const uint64_t newm = (__ballot(isnew) >> (tw * T)) & tmask;
+        const bool inc = isnew || (run && refresh);
+        const uint64_t incm = (__ballot(inc) >> (tw * T)) & tmask;
+        if (incm) {
+          hs.last_bcast_ns = d.now;
+          const uint32_t freeb = ~hs.arena_used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1u));
+          if (!freeb) {
+            if (lead) a.c[C_LDROP]++;
+          } else {  // SendServices(list, ALIVE_COUNT if anything is new, else 1) (:555-558)
+            const uint32_t li_ = (uint32_t)__builtin_ctz(freeb);
+            hs.arena_used |= 1u << li_;
+            const uint32_t rank = (uint32_t)__popcll(incm & ((1ull << s) - 1ull));
+            if (inc && rank < d.L) {
+              grec g;
+              g.w = sw;
+              g.r = r;
+              g.pad = 0;
+              list_ptr(d, o, li_)[rank] = g;
+            }
+            const uint32_t m = (uint32_t)__popcll(incm) < d.L ? (uint32_t)__popcll(incm) : d.L;
+            if (lead) {
+              d.arena_len[(size_t)idx * d.A + li_] = m;
+              a.c[C_SENDJOBS]++;
+            }
+            push_job_r(d, a, o, hs, make_job(0, 0, li_ | (m << 16), meta_of(GX_JOB_SEND, 0, newm ? d.p.alive_count : 1)),
+                       lead);
+          }
+          hs.bs_next = d.round + d.p.alive_interval_rounds;
+          // TrackNewServices: AddServiceEntry of every included record into the own view
+          bool acc = false, stale = false, chg = false;
+          uint64_t nw = cur;
+          if (inc) {
+            a.c[C_LOCAL_MERGES]++;
+            nw = merge_word(d, cur, sw, acc, stale);
+            if (stale) a.c[C_STALE]++;
+            if (acc) {
+              a.c[C_LOCAL_ACC]++;
+              if (nw != cur) {
+                *slot = nw;
+                a.changed = true;
+                atomicMin(&d.minexp[idx], exp_time(d.p, nw));
+              }
+              chg = st_of(cur) == GX_ABSENT || st_of(cur) != st_of(nw);
+            }
+          }
+          const uint64_t accm = (__ballot(acc) >> (tw * T)) & tmask, chgm = (__ballot(chg) >> (tw * T)) & tmask;
+          if (chg) a.c[C_CHG]++;
+          if (lead && accm) {
+            gx_server_times *t = srv_times(d, o, o);
+            t->last_updated_ns = d.now;  // server.LastUpdated (:323)
+            if (chgm) {
+              t->last_changed_ns = d.now;  // ServiceChanged (:195-215)
+              d.vlc[idx] = d.now;
+            }
+          }
+          const int32_t k = d.ev_slot[idx];
+          if (k >= 0 && chgm) {  // ChangeEvents in list order
+            const uint32_t ev0 = d.ev_cnt[k];
+            if (chg)
+              ev_put(d, k, ev0 + (uint32_t)__popcll(chgm & ((1ull << s) - 1ull)), r, nw,
+                     st_of(cur) == GX_ABSENT ? GX_UNKNOWN : st_of(cur));
+            if (lead) d.ev_cnt[k] = ev0 + (uint32_t)__popcll(chgm);
+          }
+        } else {  // Broadcasts <- nil (:569): the looper blocks until the nil is consumed
+          push_job_r(d, a, o, hs, make_job(0, 0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)), lead);
+          hs.flags |= 1u;
+        }
+      }
+      if (lead) {
+        const bool tick = !(hs.flags & 2u) && hs.bt_next <= d.round;
+        d.tick[idx] = tick ? 1 : 0;
+        if (tick) {
+          if (d.minexp[idx] >= (unsigned long long)d.now) {  // nothing can expire in this view
+            d.scan_cnt[idx] = 0;
+            a.c[C_SCANSLOTS] += d.R;
+          } else {
+            d.work[atomicAdd(&d.work_cnt[0], 1u)] = idx;
+          }
+        }
+        d.hs[idx] = hs;
+      }
+    }
+  }
   acc_flush(d, a);
 }
 
 // ============================================== phase 1: TombstoneOthersServices full scan ==
-// One 256-thread block per scanned view. A view whose expiry bound is >= now cannot change (no
-// slot has ts + lifespan < now), so its scan is skipped: identical results, no HBM traffic.
-// Otherwise the row is streamed with 16-B loads (4 slots per thread per 1024-slot tile), the
+// One 256-thread block per scanned view. k_owner left only the ticking views whose expiry bound
+// is in the past on the worklist (a view with bound >= now cannot change: no slot has
+// ts + lifespan < now), so a round with nothing to expire launches a small grid that exits at
+// once. A listed row is streamed with 16-B loads (4 slots per thread per 1024-slot tile), the
 // lifespans applied, and the first list_cap tombstones compacted in key order (packed block scan).
+struct ScanLds {
+  unsigned long long wave[4];
+  unsigned long long red[4];
+  uint32_t lu[TILE_OWNERS];
+  uint32_t last;
+};
 template <bool VEC, bool EV>
-__global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t list_stride, uint32_t list_cap,
-                                               uint32_t *cnt_out, int only_host) {
-  __shared__ unsigned long long s_wave[4];
-  __shared__ unsigned long long s_red[4];
-  __shared__ uint32_t s_lu[TILE_OWNERS];
-  __shared__ uint32_t s_last;
-  uint32_t oi = only_host >= 0 ? li(d, (uint32_t)only_host) : blockIdx.x;  // local index
-  if (only_host < 0) {
-    if (!d.tick[oi]) return;
-    if (d.minexp[oi] >= (unsigned long long)d.now) {  // nothing can expire in this view
-      if (threadIdx.x == 0) {
-        cnt_out[oi] = 0;
-        ctr_atomic(d, C_SCANSLOTS, d.R);
-      }
-      return;
-    }
-  }
+GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t *cnt_out, ScanLds &sm) {
+  unsigned long long *s_wave = sm.wave, *s_red = sm.red;
+  uint32_t *s_lu = sm.lu;
+  uint32_t &s_last = sm.last;
   uint64_t *row = &d.view[(size_t)oi * d.R];
-  grec *list = &list_base[only_host >= 0 ? 0 : (size_t)oi * list_stride];
   const int32_t evk = d.ev_slot[oi];
   const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
   uint32_t last_key = 0;  // 1 + the last expired key (state.LastChanged)
@@ -318,7 +412,7 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   }
   mexp = block_min(mexp, s_red);
   if (threadIdx.x == 0) {
-    cnt_out[only_host >= 0 ? 0 : oi] = n_exp;
+    *cnt_out = n_exp;
     d.minexp[oi] = mexp;  // exact bound after the scan
     if (last_key) d.vlc[oi] = ts_of(row[last_key - 1]);
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_exp;
@@ -335,6 +429,26 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   block_ctr(d, C_SCANSLOTS, threadIdx.x == 0 ? d.R : 0, s_red);
 }
 
+// only_host >= 0: that one view (the API's TombstoneOthersServices), list at list_base, count in
+// cnt_out[0]. Otherwise the round's worklist, block-strided; view oi's list at oi * list_stride.
+template <bool VEC, bool EV>
+__global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t list_stride, uint32_t list_cap,
+                                               uint32_t *cnt_out, int only_host) {
+  __shared__ ScanLds sm;
+  if (only_host >= 0) {
+    scan_view<VEC, EV>(d, li(d, (uint32_t)only_host), list_base, list_cap, cnt_out, sm);
+    return;
+  }
+  const uint32_t n = d.work_cnt[0];
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t oi = d.work[w];
+    scan_view<VEC, EV>(d, oi, &list_base[(size_t)oi * list_stride], list_cap, &cnt_out[oi], sm);
+    __syncthreads();
+  }
+}
+
+// The rest of a BroadcastTombstones tick on its own, for rounds where other phases push to the
+// FIFO between the scan and the send (failure detector, storm); otherwise k_send runs it.
 __global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
   Acc a;
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -647,23 +761,34 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
   return cnt;
 }
 
-// A team of T lanes per host: GetBroadcasts once per sampled peer, in order
-// (get_broadcasts_team). Each packet is counted into its receiver's CSR bucket.
+// A team of T lanes per host: first the rest of a BroadcastTombstones tick (TombstoneServices +
+// SendServices of own ++ others, services_state.go:606-633; lane 0, after the expiry scan), then
+// GetBroadcasts once per sampled peer, in order (get_broadcasts_team). Each packet is registered
+// in its receiver's inbox (inbox_claim / inbox_header).
 // X (failure detector or departures): the targets are memberlist's (k_fd_send took their
 // memberlist messages first and, in byte mode, the delegate gets the bytes left; the round stops
 // at a packet that would be empty), and a packet to an unreachable peer is lost after
 // GetBroadcasts took its records.
 template <int T, bool X>
-__global__ __launch_bounds__(256) void k_send(Dev d) {
+__global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
+  __shared__ gx_job s_pj[256 / T][T];  // FIFO head jobs of the block's hosts, loaded ahead
   Acc a;
   uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T, lane = threadIdx.x & (T - 1);
   unsigned lost = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.work_cnt[0] = 0;  // the scan worklist was consumed
   if (idx < d.Hl) {
     uint32_t u = d.lo + idx;
     uint32_t cap = d.p.packet_cap;
-    for (uint32_t j = lane; j < d.K; j += T) {
-      d.msg_len[(size_t)idx * d.K + j] = 0;
-      d.msg_key[(size_t)idx * d.K + j] = u * d.K + j;
+    for (uint32_t j = lane; j < d.KE; j += T) {
+      d.msg_len[(size_t)idx * d.KE + j] = 0;
+      d.msg_key[(size_t)idx * d.KE + j] = u * d.KE + j;
+    }
+    if (do_bt && d.tick[idx]) {  // departed hosts never tick
+      if (lane == 0) {
+        const uint32_t n = d.scan_cnt[idx];
+        bt_finish(d, a, u, d.hs[idx].running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
+      }
+      __threadfence_block();  // the team reads the host's bookkeeping below
     }
     if (!X || !departed(d, u)) {
       const bool fd = X && d.p.fd_enable;
@@ -677,26 +802,68 @@ __global__ __launch_bounds__(256) void k_send(Dev d) {
       }
       gx_host_state *h = &d.hs[idx];
       gx_host_state hs = *h;
-      for (uint32_t j = 0; j < np; j++) {
-        const size_t x = (size_t)idx * d.K + j;
-        uint32_t nf = fd ? d.fd_len[x] : 0, lim = d.p.limit_bytes, l = 0;
-        bool call = true;
-        if (fd && lim) {
-          uint32_t used = nf * (d.p.fd_msg_bytes + 2);
-          lim = lim > used ? lim - used : 0;
-          call = lim > d.p.overhead_bytes;
+      // The jobs at the FIFO head that this round's calls will dequeue are loaded up front, one
+      // per team lane (call c takes job c while c < the jobs queued at the start: later pushes go
+      // to the tail and cannot overwrite them), so a call waits on its list records only.
+      const uint32_t head0 = hs.fifo_head, n0 = hs.fifo_tail - head0;
+      gx_job *pjs = s_pj[threadIdx.x / T];
+      if (lane < n0 && lane < np * d.NG) pjs[lane] = d.fifo[(size_t)idx * d.Q + ((head0 + lane) % d.Q)];
+      // A packet to a reachable peer on this shard takes its receiver inbox slot before it is
+      // packed, so its records go straight into the receiver's inbox when the slot is one of the
+      // DR inline ones. With np <= T the claims are made up front, one lane per peer, their
+      // atomics in flight together; otherwise lane 0 claims before each call.
+      const bool early = np <= (uint32_t)T && d.NG == 1;
+      uint32_t my_pos = 0xffffffffu;
+      if (early && lane < np && (!X || reach(d, u, peers[lane])) && peers[lane] - d.lo < d.Hl)
+        my_pos = inbox_claim(d, peers[lane] - d.lo);
+      uint32_t called = 0;
+      bool stop = false;
+      for (uint32_t j = 0; j < np && !stop; j++) {
+        const uint32_t pj = peers[j];
+        const bool ok = !X || reach(d, u, pj), local = pj - d.lo < d.Hl;
+        // GossipMessages: up to NG gathers per target, each its own packet (entry j * NG + n); a
+        // target's gathering ends at an empty result, an empty first gather ends the round
+        for (uint32_t n = 0; n < d.NG; n++) {
+          const uint32_t c = j * d.NG + n;
+          const size_t x = (size_t)idx * d.KE + c;
+          uint32_t pos;
+          if (early) {
+            pos = __shfl(my_pos, (int)j, T);
+          } else {
+            pos = lane == 0 && ok && local ? inbox_claim(d, pj - d.lo) : 0xffffffffu;
+            pos = __shfl(pos, 0, T);
+          }
+          uint32_t nf = fd ? d.fd_len[x] : 0, lim = d.p.limit_bytes, l = 0;
+          bool call = true;
+          if (fd && lim) {
+            uint32_t used = nf * (d.p.fd_msg_bytes + 2);
+            lim = lim > used ? lim - used : 0;
+            call = lim > d.p.overhead_bytes;
+          }
+          grec *pk = pos < d.DR ? &d.in_rec[((size_t)(pj - d.lo) * d.DR + pos) * cap] : &d.msg[x * cap];
+          if (call) {
+            const uint32_t q = hs.fifo_head - head0;
+            const bool pf = q < n0 && q < (uint32_t)T;
+            l = get_broadcasts_team<T>(d, a, u, hs, cap, pk, lim, d.p.overhead_bytes, pf ? &pjs[q] : nullptr);
+          }
+          called = j + 1;
+          const bool live = l || nf;
+          if (lane == 0) {
+            d.msg_len[x] = ok ? l : 0;
+            if (fd && !ok) d.fd_len[x] = 0;
+            lost += live && !ok;
+            d.msg_dst[x] = pj;
+            if (pos != 0xffffffffu) inbox_header(d, pj - d.lo, pos, u * d.KE + c, (uint32_t)x, l);
+          }
+          if (l == 0 && nf == 0) {
+            stop = n == 0 && d.p.gossip_stop_on_empty;
+            break;
+          }
         }
-        if (call) l = get_broadcasts_team<T>(d, a, u, hs, cap, &d.msg[x * cap], lim, d.p.overhead_bytes);
-        if (lane == 0) {
-          bool live = l || nf, ok = !X || reach(d, u, peers[j]);
-          d.msg_len[x] = ok ? l : 0;
-          if (fd && !ok) d.fd_len[x] = 0;
-          lost += live && !ok;
-          d.msg_dst[x] = peers[j];
-          if (live && ok && peers[j] - d.lo < d.Hl) atomicAdd(&d.in_cnt[peers[j] - d.lo], 1u);
-        }
-        if (l == 0 && nf == 0 && d.p.gossip_stop_on_empty) break;
       }
+      // slots claimed for peers the round stopped before (gossip() returned at an empty packet)
+      if (early && lane >= called && my_pos != 0xffffffffu)
+        inbox_header(d, peers[lane] - d.lo, my_pos, u * d.KE + lane, (uint32_t)((size_t)idx * d.KE + lane), 0);
       if (lane == 0) *h = hs;
     }
   }
@@ -704,78 +871,20 @@ __global__ __launch_bounds__(256) void k_send(Dev d) {
   if (X && lost) ctr_atomic(d, C_LOST, lost);
 }
 
-// ====================================================== phase 3b: receiver CSR, sender-ordered ==
-// Exclusive scan of H counts in place into in_cnt[0..H], in_cnt[H] = total. One block of 1024
-// threads, 16 contiguous counts per thread per pass (4 x 16-B loads); in_cnt is padded.
-#define ROUTE_ITEMS 16
-__global__ __launch_bounds__(1024) void k_route_offsets(Dev d) {
-  __shared__ unsigned long long s_wave[16];
-  uint32_t t = threadIdx.x;
-  uint32_t carry = 0;
-  for (uint32_t base = 0; base < d.Hl; base += 1024 * ROUTE_ITEMS) {
-    uint32_t i0 = base + t * ROUTE_ITEMS;
-    uint32_t v[ROUTE_ITEMS];
-#pragma unroll
-    for (int q = 0; q < ROUTE_ITEMS / 4; q++) {
-      uint4 x = *reinterpret_cast<const uint4 *>(&d.in_cnt[i0 + 4 * q]);
-      v[4 * q] = i0 + 4 * q < d.Hl ? x.x : 0;
-      v[4 * q + 1] = i0 + 4 * q + 1 < d.Hl ? x.y : 0;
-      v[4 * q + 2] = i0 + 4 * q + 2 < d.Hl ? x.z : 0;
-      v[4 * q + 3] = i0 + 4 * q + 3 < d.Hl ? x.w : 0;
-    }
-    uint32_t sum = 0;
-#pragma unroll
-    for (int q = 0; q < ROUTE_ITEMS; q++) sum += v[q];
-    unsigned long long tot;
-    uint32_t pre = (uint32_t)block_excl_scan64(sum, s_wave, tot) + carry;
-#pragma unroll
-    for (int q = 0; q < ROUTE_ITEMS; q++) {
-      uint32_t c = v[q];
-      v[q] = pre;
-      pre += c;
-    }
-#pragma unroll
-    for (int q = 0; q < ROUTE_ITEMS / 4; q++)
-      if (i0 + 4 * q < d.Hl) *reinterpret_cast<uint4 *>(&d.in_cnt[i0 + 4 * q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-    carry += (uint32_t)tot;
-  }
-  __syncthreads();
-  if (t == 0) d.in_cnt[d.Hl] = carry;
-}
-
-// Entries: [0, Hl*K) packets of this shard's senders, then n_remote packets from other shards.
-__global__ void k_route_fill(Dev d) {
-  uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.Hl * d.K + d.n_remote) return;
-  if (d.msg_len[e] == 0 && !(d.p.fd_enable && d.fd_len[e])) return;  // memberlist-only packets count
-  uint32_t dst = d.msg_dst[e] - d.lo;
-  if (dst >= d.Hl) return;  // bound for another shard (outbox)
-  uint32_t pos = atomicAdd(&d.in_cur[dst], 1u);
-  d.in_fill[d.in_cnt[dst] + pos] = e;
-}
-
-// Deterministic order: rank of each entry (= sender * K + j) inside its receiver segment.
-// Deterministic order: rank of each entry's global key (sender * K + j) inside its receiver segment.
-__global__ void k_route_rank(Dev d) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.in_cnt[d.Hl]) return;
-  uint32_t e = d.in_fill[i];
-  uint32_t key = d.msg_key[e];
-  uint32_t dst = d.msg_dst[e] - d.lo;
-  uint32_t lo = d.in_cnt[dst], hi = d.in_cnt[dst + 1];
-  uint32_t rank = 0;
-  for (uint32_t x = lo; x < hi; x++) rank += d.msg_key[d.in_fill[x]] < key;
-  d.in_sorted[lo + rank] = make_uint2(e, d.msg_len[e]);
-}
-
 // ============================================================== phase 4: gather-then-merge ==
-// One wave per receiver, one inbound record per lane per 64-record tile (its packets in sender
-// order). The tile's view slots are prefetched as soon as the keys are known; duplicate keys are
-// grouped by an in-register bitonic sort of (key, arrival lane), and each group folds its
-// occurrences in arrival order with the AddServiceEntry rule (one wave-uniform step per
-// occurrence of the longest group, usually 1). The group's first lane writes the slot once.
-// Accepted foreign records are compacted with a wave ballot into the receiver's FIFO
-// (retransmit), in arrival order.
+// One wave per receiver. Its inbox (the packet headers the senders registered, in arrival order)
+// is loaded together with its count; the few headers are ranked by global sender key in
+// registers and staged sorted in LDS, so the fold order is the reference receiver's (ascending
+// sender, then packet order). Each 64-record tile takes one record per lane straight from the
+// senders' packets (one predicated load per packet overlapping the tile, all independent) and
+// prefetches the tile's view slots as soon as the keys are known: three dependent global loads
+// per receiver (inbox, records, view slots), no routing pass. Duplicate keys are grouped by an
+// in-register bitonic sort of (key, arrival lane), and each group folds its occurrences in
+// arrival order with the AddServiceEntry rule (one wave-uniform step per occurrence of the
+// longest group, usually 1). The group's first lane writes the slot once. Accepted foreign
+// records are compacted with a wave ballot into the receiver's FIFO (retransmit), in arrival
+// order. A receiver with more than DI packets (overflow list) is folded by one lane walking its
+// inbox in key order through the scalar AddServiceEntry path (add_entry): same semantics, slow.
 template <bool K32>
 GXD uint64_t bitonic64(uint64_t x, uint32_t lane) {  // ascending across the 64 lanes
 #pragma unroll
@@ -792,19 +901,149 @@ GXD uint64_t bitonic64(uint64_t x, uint32_t lane) {  // ascending across the 64 
   return x;
 }
 
+GXD uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
+
+// Overflowed inbox: one lane folds every packet in key order through the scalar path and
+// flushes its own counters.
+GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
+  Acc a;
+  const uint32_t v = d.lo + vi, cnt = d.in_cnt[vi];
+  int64_t after = -1;
+  unsigned long long recs = 0;
+  for (uint32_t n = 0; n < cnt; n++) {
+    const uint4 h = inbox_next(d, vi, after);
+    after = h.x;
+    const grec *pk = packet_recs(d, vi, h.w, h.y);
+    for (uint32_t x = 0; x < h.z; x++) add_entry(d, a, v, pk[x], SRC_GOSSIP);
+    recs += h.z;
+  }
+  kbytes(d, GX_K_MERGE, 28ull * recs + 16ull * cnt + 4, recs);
+  for (int i = 0; i < C_NCTR; i++) ctr_atomic(d, i, a.c[i]);
+  if (a.changed) mark_change(d);
+}
+
+// Phase 4a, one half-wave per receiver and two dependent loads: the receiver's inbox count, the
+// headers of its first DR packets and those packets' inline records (whole slots, loaded before
+// the count is known), then the view slot of every record. A receiver whose records are all no-ops
+// (stale, or no newer than the slot: see k_merge) is finished here, its merges and stale drops
+// counted. A receiver with a live record, or with more than DR packets, is flagged (mflag) and
+// merged in full by k_merge.
+#define LEAN_LPR 32  // lanes per receiver
+#define LEAN_Q 4     // records per lane per batch
+__global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
+  const uint32_t lane = threadIdx.x & 63, l = threadIdx.x & (LEAN_LPR - 1);
+  const uint32_t vi = blockIdx.x * (256 / LEAN_LPR) + threadIdx.x / LEAN_LPR;
+  const uint32_t gbase = lane & ~(uint32_t)(LEAN_LPR - 1);
+  const uint64_t gmask = (LEAN_LPR == 64 ? ~0ull : ((1ull << LEAN_LPR) - 1ull)) << gbase;
+  unsigned long long c_merge = 0, c_stale = 0, c_hdr = 0;
+  if (vi < d.Hl) {
+    const uint32_t cap = d.p.packet_cap, nspec = d.DR * cap;
+    const grec *base = &d.in_rec[(size_t)vi * nspec];
+    grec g[LEAN_Q];
+#pragma unroll
+    for (int q = 0; q < LEAN_Q; q++) {  // hop 1: inline records, speculatively
+      const uint32_t p = l + LEAN_LPR * q;
+      if (p < nspec) g[q] = base[p];
+    }
+    const uint4 hd = l < d.DR ? d.in_hdr[(size_t)vi * d.DI + l] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t cnt = d.in_cnt[vi];
+    bool defer = cnt > d.DR;
+    if (cnt && !defer) {
+      const uint64_t *row = &d.view[(size_t)vi * d.R];
+      const uint32_t npos = cnt * cap;
+      c_hdr = l == 0 ? cnt : 0;
+      for (uint32_t p0 = 0; p0 < npos; p0 += LEAN_LPR * LEAN_Q) {
+        if (p0) {
+#pragma unroll
+          for (int q = 0; q < LEAN_Q; q++) {
+            const uint32_t p = p0 + l + LEAN_LPR * q;
+            if (p < npos) g[q] = base[p];
+          }
+        }
+        bool valid[LEAN_Q];
+        uint64_t w0[LEAN_Q];
+#pragma unroll
+        for (int q = 0; q < LEAN_Q; q++) {
+          const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
+          const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
+          valid[q] = p < npos && p - sl * cap < len;
+          w0[q] = valid[q] ? row[g[q].r] : 0;  // hop 2
+        }
+        bool live = false;
+#pragma unroll
+        for (int q = 0; q < LEAN_Q; q++) {
+          const int64_t ts = ts_of(g[q].w);
+          const bool stale = valid[q] && ts < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+          live |= valid[q] && !stale && (st_of(w0[q]) == GX_ABSENT || ts > ts_of(w0[q]));
+          c_merge += valid[q];
+          c_stale += stale;
+        }
+        if (__ballot(live) & gmask) {
+          defer = true;
+          break;
+        }
+      }
+    }
+    if (defer) c_merge = c_stale = c_hdr = 0;  // k_merge merges and counts this receiver
+    if (l == 0) d.mflag[vi] = defer ? 1 : 0;
+  }
+  c_merge = wave_sum(c_merge);
+  c_stale = wave_sum(c_stale);
+  c_hdr = wave_sum(c_hdr);
+  if (lane == 0 && c_merge) {
+    // 12 B per record + 8 B per slot read, 16 B per inbox header + the count
+    kbytes(d, GX_K_MERGE, 20ull * c_merge + 16ull * c_hdr + 4ull * c_hdr, c_merge);
+    ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
+    ctr_atomic(d, C_STALE, c_stale);
+  }
+}
+
+#define INBOX_PREFETCH 8
+#define MERGE_WAVES 4
+// Orders a wave's LDS and global accesses across its lanes (the waves of a block do not meet).
+GXD void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 template <bool K32, bool EV>
-__global__ __launch_bounds__(64) void k_merge(Dev d) {
-  __shared__ uint32_t s_start[65];
-  __shared__ uint32_t s_ent[64];
-  __shared__ uint8_t s_accf[64];
-  __shared__ uint8_t s_chg[64];
-  __shared__ uint8_t s_prev[64];
-  __shared__ uint64_t s_accw[64];
-  const uint32_t vi = blockIdx.x, v = d.lo + vi;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t off = d.in_cnt[vi], deg = d.in_cnt[vi + 1] - off;
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
+  // one receiver per wave, MERGE_WAVES per block; the waves share nothing (wave-level sync only)
+  __shared__ uint4 s_hdr_[MERGE_WAVES][64];
+  __shared__ uint8_t s_accf_[MERGE_WAVES][64];
+  __shared__ uint8_t s_chg_[MERGE_WAVES][64];
+  __shared__ uint8_t s_prev_[MERGE_WAVES][64];
+  __shared__ uint64_t s_accw_[MERGE_WAVES][64];
+  const uint32_t wv = threadIdx.x >> 6;
+  uint4 *s_hdr = s_hdr_[wv];
+  uint8_t *s_accf = s_accf_[wv], *s_chg = s_chg_[wv], *s_prev = s_prev_[wv];
+  uint64_t *s_accw = s_accw_[wv];
+  const uint32_t vi = blockIdx.x * MERGE_WAVES + wv, v = d.lo + vi;
+  if (vi >= d.Hl || !d.mflag[vi]) return;  // k_merge_lean finished this receiver
+  const uint32_t lane = threadIdx.x & 63;
+  // hop 1: the inbox count and its first headers together (most inboxes hold a few packets)
+  const uint32_t npre = d.DI < INBOX_PREFETCH ? d.DI : INBOX_PREFETCH;
+  uint4 hd = lane < npre ? d.in_hdr[(size_t)vi * d.DI + lane] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t deg = d.in_cnt[vi];
   if (deg == 0) return;
-  const uint32_t cap = d.p.packet_cap;
+  if (deg > d.DI) {
+    if (lane == 0) merge_inbox_serial(d, vi);
+    return;
+  }
+  if (deg > npre && lane >= npre && lane < deg) hd = d.in_hdr[(size_t)vi * d.DI + lane];
+  // sender order: rank of each header's key among the deg distinct keys
+  const uint32_t hkey = lane < deg ? hd.x : 0xffffffffu;
+  uint32_t hrank = 0;
+  for (uint32_t j = 0; j < deg; j++) hrank += rdl(hkey, j) < hkey;
+  if (lane < deg) s_hdr[hrank] = hd;
+  wave_sync();
+  const uint4 sh = lane < deg ? s_hdr[lane] : make_uint4(0u, 0u, 0u, 0u);  // {key, entry, len, slot} of packet `lane`
+  uint32_t incl = sh.z;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(incl, o, 64);
+    if ((int)lane >= o) incl += y;
+  }
+  const uint32_t pstart = incl - sh.z, total = __shfl(incl, 63, 64);
   gx_host_state *h = &d.hs[vi];
   const uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   const uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
@@ -816,137 +1055,138 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
   const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
   int64_t vlc_ts = 0;
   bool vlc_set = false;
-  for (uint32_t c0 = 0; c0 < deg; c0 += 64) {
-    uint32_t cn = deg - c0 < 64 ? deg - c0 : 64;
-    uint2 el = lane < cn ? d.in_sorted[off + c0 + lane] : make_uint2(0, 0);  // (entry, length)
-    uint32_t incl = el.y;
+  uint32_t kc = 0;  // first packet that can overlap the tile
+  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+    const uint32_t i = t0 + lane;
+    const bool valid = i < total;
+    while (kc < deg && rdl(pstart, kc) + rdl(sh.z, kc) <= t0) kc++;
+    grec g;
+    g.w = 0;
+    g.r = INV;
+    g.pad = 0;
+    for (uint32_t k = kc; k < deg; k++) {  // hop 2: one predicated load per overlapping packet
+      const uint32_t st = rdl(pstart, k);
+      if (st >= t0 + 64) break;
+      const uint32_t off = i - st;
+      if (off < rdl(sh.z, k)) g = packet_recs(d, vi, rdl(sh.w, k), rdl(sh.y, k))[off];
+    }
+    uint32_t key = INV;
+    uint64_t val = 0, w0 = 0;
+    if (valid) {
+      key = g.r;
+      val = g.w;
+      w0 = row[key];  // hop 3
+    }
+    c_merge += valid;
+    c_rd += valid;  // one view slot read per inbound record
+    // A record that is stale, or no newer than the slot's word at the start of the tile, is a
+    // no-op whatever its position in the fold: the slot's timestamp only grows (an accept needs a
+    // strictly newer one, services_state.go:321), and IsStale does not depend on the slot. Only the
+    // other records ("live") enter the fold; a tile without any (every copy of an epidemic
+    // broadcast after the first) is done here.
+    const bool stale0 = valid && ts_of(val) < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+    const bool live = valid && !stale0 && (st_of(w0) == GX_ABSENT || ts_of(val) > ts_of(w0));
+    c_stale += stale0;
+    if (__ballot(live) == 0) continue;
+    if (!live) key = INV;
+    uint64_t sk = K32 ? (uint64_t)((key << 6) | lane) : (((uint64_t)key << 6) | lane);
+    sk = bitonic64<K32>(sk, lane);
+    const uint32_t src = (uint32_t)(sk & 63), skey = (uint32_t)(sk >> 6);
+    const bool vs = skey != INV;
+    const uint64_t sval = __shfl(val, (int)src, 64), sw0 = __shfl(w0, (int)src, 64);
+    uint32_t pkey = __shfl_up(skey, 1, 64);
+    const bool head = vs && (lane == 0 || pkey != skey);
+    const uint64_t heads = __ballot(head);
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const uint32_t gs = 63 - (uint32_t)__clzll((heads & le) | 1ull);  // first lane of this group
+    const uint32_t kpos = lane - gs;
+    const uint64_t after = heads & ~le;
+    const uint32_t nvs = (uint32_t)__popcll(__ballot(vs));
+    const uint32_t glen = (after ? (uint32_t)__ffsll((long long)after) - 1 : nvs) - lane;  // heads only
+    uint32_t kmax = vs ? kpos : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      uint32_t y = __shfl_xor(kmax, o, 64);
+      kmax = y > kmax ? y : kmax;
+    }
+    uint64_t wg = sw0, wme = 0, wprev = GX_SLOT_ABSENT;
+    bool acc = false, stl = false;
+    for (uint32_t kk = 0; kk <= kmax; kk++) {  // occurrence kk of every group, arrival order
+      uint64_t wcur = __shfl(wg, (int)gs, 64);
+      if (vs && kpos == kk) {
+        wprev = wcur;
+        wme = merge_word(d, wcur, sval, acc, stl);
+      }
+      uint64_t wn = __shfl(wme, (int)((gs + kk) & 63), 64);
+      if (head && kk < glen) wg = wn;
+    }
+    c_stale += stl;
+    c_acc += acc;
+    if (head) {
+      if (wg != sw0) {
+        row[skey] = wg;
+        c_wr++;
+        unsigned long long x = exp_time(d.p, wg);
+        mexp = x < mexp ? x : mexp;
+      }
+    }
+    // ServiceChanged: an insert, or a stored status that differs (:317-340)
+    const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
+    c_chg += chg;
+    s_accf[src] = vs && acc && !owned_by(d, skey, v);
+    if (EV) {
+      s_chg[src] = chg;
+      s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
+    }
+    s_accw[src] = wme;
+    // per owner (contiguous in key order): its last accepted and last status-changing
+    // occurrence in arrival order (segmented max of arrival lane + 1)
+    const uint32_t own = vs ? owner_of(d, skey) : 0xffffffffu;
+    uint32_t mu = acc ? src + 1 : 0, mc = chg ? src + 1 : 0;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      uint32_t y = __shfl_up(incl, o, 64);
-      if ((int)lane >= o) incl += y;
+      uint32_t yu = __shfl_down(mu, o, 64), yc = __shfl_down(mc, o, 64), yo = __shfl_down(own, o, 64);
+      if (lane + o < 64 && yo == own) {
+        mu = yu > mu ? yu : mu;
+        mc = yc > mc ? yc : mc;
+      }
     }
-    uint32_t total = __shfl(incl, 63, 64);
-    s_start[lane] = incl - el.y;
-    s_ent[lane] = el.x;
-    __syncthreads();
-    for (uint32_t t0 = 0; t0 < total; t0 += 64) {
-      uint32_t i = t0 + lane;
-      bool valid = i < total;
-      uint32_t key = INV;
-      uint64_t val = 0, w0 = 0;
-      if (valid) {
-        uint32_t lo = 0, hi = cn - 1;  // last packet with start <= i
-        while (lo < hi) {
-          uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_start[mid] <= i) lo = mid;
-          else hi = mid - 1;
-        }
-        grec g = d.msg[(size_t)s_ent[lo] * cap + (i - s_start[lo])];
-        key = g.r;
-        val = g.w;
-        w0 = row[key];  // prefetch: in flight during the sort
-      }
-      c_merge += valid;
-      uint64_t sk = K32 ? (uint64_t)((key << 6) | lane) : (((uint64_t)key << 6) | lane);
-      sk = bitonic64<K32>(sk, lane);
-      const uint32_t src = (uint32_t)(sk & 63), skey = (uint32_t)(sk >> 6);
-      const bool vs = skey != INV;
-      const uint64_t sval = __shfl(val, (int)src, 64), sw0 = __shfl(w0, (int)src, 64);
-      uint32_t pkey = __shfl_up(skey, 1, 64);
-      const bool head = vs && (lane == 0 || pkey != skey);
-      const uint64_t heads = __ballot(head);
-      const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-      const uint32_t gs = 63 - (uint32_t)__clzll((heads & le) | 1ull);  // first lane of this group
-      const uint32_t kpos = lane - gs;
-      const uint64_t after = heads & ~le;
-      const uint32_t nvs = (uint32_t)__popcll(__ballot(vs));
-      const uint32_t glen = (after ? (uint32_t)__ffsll((long long)after) - 1 : nvs) - lane;  // heads only
-      uint32_t kmax = vs ? kpos : 0;
+    uint32_t pown = __shfl_up(own, 1, 64);
+    const bool ohead = vs && (lane == 0 || pown != own);
+    uint32_t mcmax = mc;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        uint32_t y = __shfl_xor(kmax, o, 64);
-        kmax = y > kmax ? y : kmax;
-      }
-      uint64_t wg = sw0, wme = 0, wprev = GX_SLOT_ABSENT;
-      bool acc = false, stl = false;
-      for (uint32_t kk = 0; kk <= kmax; kk++) {  // occurrence kk of every group, arrival order
-        uint64_t wcur = __shfl(wg, (int)gs, 64);
-        if (vs && kpos == kk) {
-          wprev = wcur;
-          wme = merge_word(d, wcur, sval, acc, stl);
-        }
-        uint64_t wn = __shfl(wme, (int)((gs + kk) & 63), 64);
-        if (head && kk < glen) wg = wn;
-      }
-      c_stale += stl;
-      c_acc += acc;
-      if (head) {
-        c_rd++;
-        if (wg != sw0) {
-          row[skey] = wg;
-          c_wr++;
-          unsigned long long x = exp_time(d.p, wg);
-          mexp = x < mexp ? x : mexp;
-        }
-      }
-      // ServiceChanged: an insert, or a stored status that differs (:317-340)
-      const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
-      c_chg += chg;
-      s_accf[src] = vs && acc && !owned_by(d, skey, v);
-      if (EV) {
-        s_chg[src] = chg;
-        s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
-      }
-      s_accw[src] = wme;
-      // per owner (contiguous in key order): its last accepted and last status-changing
-      // occurrence in arrival order (segmented max of arrival lane + 1)
-      const uint32_t own = vs ? owner_of(d, skey) : 0xffffffffu;
-      uint32_t mu = acc ? src + 1 : 0, mc = chg ? src + 1 : 0;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        uint32_t yu = __shfl_down(mu, o, 64), yc = __shfl_down(mc, o, 64), yo = __shfl_down(own, o, 64);
-        if (lane + o < 64 && yo == own) {
-          mu = yu > mu ? yu : mu;
-          mc = yc > mc ? yc : mc;
-        }
-      }
-      uint32_t pown = __shfl_up(own, 1, 64);
-      const bool ohead = vs && (lane == 0 || pown != own);
-      uint32_t mcmax = mc;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        uint32_t y = __shfl_xor(mcmax, o, 64);
-        mcmax = y > mcmax ? y : mcmax;
-      }
-      __threadfence_block();  // slot stores land before a later tile reads the same keys
-      __syncthreads();
-      if (ohead && (mu || mc)) {
-        gx_server_times *st = srv_times(d, v, own);
-        if (mu) st->last_updated_ns = ts_of(s_accw[mu - 1]);  // server.LastUpdated (:323)
-        if (mc) st->last_changed_ns = ts_of(s_accw[mc - 1]);  // serverChanged (:204-215)
-        c_wr += (mu != 0) + (mc != 0);                        // counted as written words
-      }
-      if (mcmax) {
-        vlc_ts = ts_of(s_accw[mcmax - 1]);  // state.LastChanged
-        vlc_set = true;
-      }
-      if (EV && evk >= 0) {  // ChangeEvents in arrival order
-        bool fe = s_chg[lane] != 0;
-        unsigned long long me = __ballot(fe);
-        if (fe)
-          ev_put(d, evk, ev0 + n_ev + (uint32_t)__popcll(me & ((1ull << lane) - 1ull)), key, s_accw[lane],
-                 s_prev[lane]);
-        n_ev += (uint32_t)__popcll(me);
-      }
-      bool f = s_accf[lane];  // ordered ballot compaction -> retransmit jobs (arrival order)
-      unsigned long long m = __ballot(f);
-      uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-      if (f && n_retx + pos < room)
-        d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
-            make_job(s_accw[lane], 0, key, meta_of(GX_JOB_RETX, 0, 1));
-      n_retx += (uint32_t)__popcll(m);
-      __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) {
+      uint32_t y = __shfl_xor(mcmax, o, 64);
+      mcmax = y > mcmax ? y : mcmax;
     }
+    __threadfence_block();  // slot stores land before a later tile reads the same keys
+    wave_sync();
+    if (ohead && (mu || mc)) {
+      gx_server_times *st = srv_times(d, v, own);
+      if (mu) st->last_updated_ns = ts_of(s_accw[mu - 1]);  // server.LastUpdated (:323)
+      if (mc) st->last_changed_ns = ts_of(s_accw[mc - 1]);  // serverChanged (:204-215)
+      c_wr += (mu != 0) + (mc != 0);                        // counted as written words
+    }
+    if (mcmax) {
+      vlc_ts = ts_of(s_accw[mcmax - 1]);  // state.LastChanged
+      vlc_set = true;
+    }
+    if (EV && evk >= 0) {  // ChangeEvents in arrival order
+      bool fe = s_chg[lane] != 0;
+      unsigned long long me = __ballot(fe);
+      if (fe)
+        ev_put(d, evk, ev0 + n_ev + (uint32_t)__popcll(me & ((1ull << lane) - 1ull)), key, s_accw[lane],
+               s_prev[lane]);
+      n_ev += (uint32_t)__popcll(me);
+    }
+    bool f = s_accf[lane];  // ordered ballot compaction -> retransmit jobs (arrival order)
+    unsigned long long m = __ballot(f);
+    uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (f && n_retx + pos < room)
+      d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
+          make_job(s_accw[lane], 0, key, meta_of(GX_JOB_RETX, 0, 1));
+    n_retx += (uint32_t)__popcll(m);
+    wave_sync();
   }
   c_merge = wave_sum(c_merge);
   c_acc = wave_sum(c_acc);
@@ -961,7 +1201,9 @@ __global__ __launch_bounds__(64) void k_merge(Dev d) {
     if (vlc_set) d.vlc[vi] = vlc_ts;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     ctr_atomic(d, C_CHG, c_chg);
-    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 8ull * deg, c_merge);
+    // 12 B per record (word + key) + 8 B per slot read / written + 32 B per retransmit job
+    // + 16 B per inbox header + the count
+    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 16ull * deg + 4, c_merge);
     ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
     ctr_atomic(d, C_GOSSIP_ACC, c_acc);
     ctr_atomic(d, C_STALE, c_stale);
@@ -1833,7 +2075,7 @@ GXD void ob_chunk_counts(const Dev &d, uint32_t gi, uint32_t *s_cnt) {  // s_cnt
 }
 __global__ __launch_bounds__(256) void k_ob_count(Dev d, uint32_t *cnt) {  // cnt[chunk][G]
   extern __shared__ uint32_t s_cnt[];
-  const size_t ne = (size_t)d.Hl * d.K, i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t ne = (size_t)d.Hl * d.KE, i = (size_t)blockIdx.x * 256 + threadIdx.x;
   ob_chunk_counts(d, i < ne ? ob_dest(d, i) : d.G, s_cnt);
   __syncthreads();
   if (threadIdx.x < d.G) {
@@ -1862,7 +2104,7 @@ __global__ __launch_bounds__(256) void k_ob_scan(Dev d, const uint32_t *cnt, uin
 }
 __global__ __launch_bounds__(256) void k_ob_fill(Dev d, const uint32_t *off, uint32_t *entries) {
   extern __shared__ uint32_t s_cnt[];
-  const size_t ne = (size_t)d.Hl * d.K, i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t ne = (size_t)d.Hl * d.KE, i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t gi = i < ne ? ob_dest(d, i) : d.G;
   ob_chunk_counts(d, gi, s_cnt);
@@ -1918,7 +2160,10 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
   }
 }
 
-// Inbox: received slots -> message entries [Hl*K, Hl*K + n) with receiver counts.
+// Inbox: received slots -> message entries [Hl*K, Hl*K + n), registered in the receivers'
+// inboxes. A slot is checked like the oracle's gx_inbox_unpack does (sender key < H*K, receiver on
+// this shard, len <= packet_cap, n_fd <= fd_msg_cap) and its record keys < R; a bad slot is
+// skipped and flagged (work_cnt[3]), and the next call that waits returns GX_EINVAL.
 __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   uint32_t i = blockIdx.x;
   if (i >= n) return;
@@ -1927,9 +2172,20 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   const uint8_t *src = in + (size_t)i * sb;
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(src);
   uint32_t key = hdr[0], dst = hdr[1], len = hdr[2], nfd = fcap ? hdr[3] : 0;
-  size_t e = (size_t)d.Hl * d.K + i;
+  size_t e = (size_t)d.Hl * d.KE + i;
   const grec *recs = reinterpret_cast<const grec *>(src + 16);
-  for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) d.msg[e * d.p.packet_cap + x] = recs[x];
+  bool bad = key >= d.H * d.KE || dst - d.lo >= d.Hl || len > d.p.packet_cap || nfd > fcap;
+  for (uint32_t x = threadIdx.x; !bad && x < len; x += blockDim.x) bad |= recs[x].r >= d.R;
+  if (__ballot(bad) != 0) {
+    if (threadIdx.x == 0) atomicOr(&d.work_cnt[3], GX_ERR_INBOX);
+    return;
+  }
+  const uint32_t vi = dst - d.lo;
+  uint32_t pos = 0;
+  if (threadIdx.x == 0 && (len || nfd)) pos = inbox_claim(d, vi);
+  pos = __shfl(pos, 0, 64);
+  grec *pk = (len || nfd) ? packet_recs(d, vi, pos, (uint32_t)e) : &d.msg[e * d.p.packet_cap];
+  for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) pk[x] = recs[x];
   const uint4 *fm = reinterpret_cast<const uint4 *>(src + 16 + 16ull * d.p.packet_cap);
   for (uint32_t x = threadIdx.x; x < nfd; x += blockDim.x) {
     const uint4 w = fm[x];
@@ -1946,7 +2202,7 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
     d.msg_dst[e] = dst;
     d.msg_len[e] = len;
     if (fcap) d.fd_len[e] = nfd;
-    if (len || nfd) atomicAdd(&d.in_cnt[dst - d.lo], 1u);
+    if (len || nfd) inbox_header(d, vi, pos, key, (uint32_t)e, len);
   }
 }
 

@@ -295,4 +295,8 @@ SCENARIOS = {
                                 packet_cap=48, ae_period_rounds=10, queue_cap=4096), 250),
     "depart_no_fd": (dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, depart_round=5, depart_ppm=100_000,
                           ae_period_rounds=10, queue_cap=4096), 200),
+    # the packets' memberlist messages walked in key order through overflowed inboxes
+    "depart_inbox_overflow": (dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, fd_enable=1, depart_round=5,
+                                   depart_ppm=100_000, ae_period_rounds=10, queue_cap=4096, fanout=6,
+                                   inbox_slots=2), 200),
 }

@@ -6,6 +6,9 @@
 * cfg 5 (32768 x 16, partition + storm + push-pull) through size-independent properties: every
   record sent is merged exactly once, the run is deterministic (two engines, same seed, identical
   counters, host digests and per-record min/max), and the catalog converges.
+* the cfg 5 schedule at H = 16384 against the OpenMP oracle, bit for bit, for rounds 0..101
+  (storm, heal and every post-heal push-pull round), and cfg 3 as the bench runs it (queue_cap
+  4096, push-pull) for 51 rounds.
 """
 import numpy as np
 import pytest
@@ -127,3 +130,81 @@ def test_fd_depart_full_parity(gx_lib):
     for v in np.linspace(0, 16383, 64).astype(int):
         assert g.fd_members(int(v)) == o.fd_members(int(v)), v
     _slabs_equal(g, o, 4096)
+
+
+def _minmax_any(e):
+    """Per-record (min, max) slot word over every view: device buffers for the HIP engine, host
+    buffers for the oracle (gx_view_minmax, XOR 2^63 form)."""
+    if e.backend.startswith("hip"):
+        return _minmax(e)
+    R = e.H * e.S
+    mn, mx = np.empty(R, dtype=np.int64), np.empty(R, dtype=np.int64)
+    e.view_minmax(mn.ctypes.data, mx.ctypes.data)
+    return mn, mx
+
+
+def _rows_equal(g, o, views, what):
+    for v in views:
+        v = int(v)
+        assert np.array_equal(g.read_views(v, v + 1), o.read_views(v, v + 1)), f"{what}: view {v}"
+        assert np.array_equal(g.server_times(v), o.server_times(v)), f"{what}: server times of view {v}"
+
+
+CFG5_H16K = dict(CFG5, n_hosts=16384)
+
+
+def test_cfg5_schedule_h16384_parity(gx_lib):
+    """The bench's own cfg 5 schedule (2-way partition for rounds [0, 50), ExpireServer storm of the
+    other half at round 5, heal, push-pull every 10 rounds, queue_cap 20480) at H = 16384 against
+    the OpenMP oracle for rounds 0..101: the storm, every partitioned and every post-heal
+    push-pull round. At each checkpoint: every counter, every host's queue digest and bookkeeping,
+    the per-record min and max word over all 16384 views, 24 full rows with their server times,
+    and state.LastChanged of every view."""
+    orc = _omp_oracle()
+    g = Engine(default_params(gx_lib, **CFG5_H16K), lib=gx_lib)
+    o = Engine(default_params(orc, **CFG5_H16K), lib=orc)
+    H = 16384
+    sample = np.linspace(0, H - 1, 24).astype(int)
+    for stop in (6, 11, 31, 51, 52, 61, 71, 81, 91, 101):
+        n = stop - g.round
+        g.run_rounds(n)
+        o.run_rounds(n)
+        what = f"cfg5@16384 round {g.round}"
+        print(what, flush=True)  # progress (long test)
+        sg, so = g.stats(), o.stats()
+        assert sg == so, what
+        assert np.array_equal(g.digests(), o.digests()), what
+        assert [bytes(h) for h in g.hosts()] == [bytes(h) for h in o.hosts()], what
+        mg, xg = _minmax_any(g)
+        mo, xo = _minmax_any(o)
+        assert np.array_equal(mg, mo) and np.array_equal(xg, xo), what
+        _rows_equal(g, o, sample, what)
+        assert np.array_equal(g.last_changed(), o.last_changed()), what
+    st = g.stats()
+    assert st["expire_server"] == H * (H // 2)
+    assert st["ae_exchanges"] == 11 * (H // 2)
+    assert st["gossip_accepts"] > 0 and st["ae_accepts"] > 0
+
+
+CFG3_BENCH = dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2, churn_ppm=50000,
+                  aged_ppm=50000, ae_period_rounds=10)
+
+
+def test_cfg3_bench_schedule_51_rounds(gx_lib):
+    """cfg 3 as bench.py runs it (queue_cap 4096, push-pull every 10 rounds, 5 % churn, 5 % of
+    records aged U[0, 100 s]) against the OpenMP oracle for 51 rounds: five expiry scans per view
+    (alive-lifespan expiry of the aged records) and six push-pull rounds, every view compared."""
+    orc = _omp_oracle()
+    g = Engine(default_params(gx_lib, **CFG3_BENCH), lib=gx_lib)
+    o = Engine(default_params(orc, **CFG3_BENCH), lib=orc)
+    for stop in (21, 51):
+        n = stop - g.round
+        g.run_rounds(n)
+        o.run_rounds(n)
+        print(f"cfg3 round {g.round}", flush=True)  # progress (long test)
+        assert g.stats() == o.stats(), g.round
+        assert np.array_equal(g.digests(), o.digests()), g.round
+    st = g.stats()
+    assert st["expired"] > 0 and st["ae_exchanges"] == 6 * 8192 and st["churn_events"] > 0
+    _slabs_equal(g, o, 4096)
+    _rows_equal(g, o, np.linspace(0, 16383, 16).astype(int), "cfg3 round 51")

@@ -41,6 +41,24 @@ SCENARIOS = {
     "storm_s16_qfull": dict(n_hosts=300, n_services=16, init_mode=INIT_WARM, partition_start=0,
                             partition_end=12, storm_round=1, queue_cap=40),
     "high_fanout": dict(n_hosts=20, n_services=4, init_mode=INIT_OWN, fanout=16, packet_cap=8),
+    # receiver inboxes with fewer slots than packets: the serial overflow path (key-order walk of
+    # the inbox slots + the shared overflow list) must fold exactly like the in-wave path
+    "inbox_overflow": dict(n_hosts=40, n_services=4, init_mode=INIT_OWN, fanout=12, packet_cap=8,
+                           inbox_slots=3, ae_period_rounds=10, churn_ppm=50000, queue_cap=1024),
+    "inbox_overflow_storm": dict(n_hosts=100, n_services=8, init_mode=INIT_WARM, partition_start=0,
+                                 partition_end=12, storm_round=2, queue_cap=256, inbox_slots=1, fanout=4),
+    # GossipMessages (config/config.go:46): up to 15 gathers per target and round
+    "gossip_messages15": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, gossip_messages=15,
+                              ae_period_rounds=10, churn_ppm=50000, queue_cap=2048),
+    "gossip_messages4_storm": dict(n_hosts=96, n_services=4, init_mode=INIT_WARM, gossip_messages=4,
+                                   partition_start=0, partition_end=15, storm_round=3, queue_cap=1024,
+                                   inbox_slots=6),
+    # memberlist's per-node push-pull initiation (every live host starts one exchange per interval)
+    "pp_initiate": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, push_pull_mode=1, ae_period_rounds=5,
+                        churn_ppm=30000),
+    "pp_initiate_storm_depart": dict(n_hosts=80, n_services=4, init_mode=INIT_WARM, push_pull_mode=1,
+                                     ae_period_rounds=4, partition_start=0, partition_end=20, storm_round=3,
+                                     queue_cap=1024, depart_round=6, depart_ppm=50000),
 }
 
 
@@ -66,6 +84,9 @@ LISTEN = {  # scenario -> [(view, listener id, capacity)]
     "cfg1_churn_aged": [(3, 1, 64), (17, 2, 4096)],
     "storm_s3": [(5, 1, 2048), (60, 1, 17)],
     "odd_sizes": [(0, 1, 100), (36, 1, 4096)],
+    "inbox_overflow": [(0, 1, 4096), (5, 2, 60)],
+    "pp_initiate": [(0, 1, 4096), (9, 1, 100)],
+    "gossip_messages15": [(2, 1, 4096)],
 }
 
 

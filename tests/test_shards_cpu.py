@@ -33,6 +33,9 @@ SCEN = {
                partition_end=45, depart_round=3, depart_ppm=100000, fd_enable=1, queue_cap=4096),
     "fd_bytes": dict(n_hosts=50, n_services=6, init_mode=1, ae_period_rounds=4, churn_ppm=30000, depart_round=10,
                      depart_ppm=100000, fd_enable=1, limit_bytes=1398, packet_cap=48, queue_cap=2048),
+    # received packets registered in overflowed inboxes (inbox_slots is an engine bound)
+    "inbox_overflow": dict(n_hosts=45, n_services=4, init_mode=1, fanout=8, packet_cap=6, inbox_slots=2,
+                           ae_period_rounds=6, churn_ppm=50000, queue_cap=512),
 }
 
 
