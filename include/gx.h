@@ -390,6 +390,24 @@ int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list,
 /* IsNewService, services_state.go:509-521. */
 int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *is_new);
 
+/* ---- catalog readers (catalog/view.go, services_state.go:726-748) ----------------------------
+ * EachServiceSorted (view.go:14-26): the view's present records ordered by Updated; records with
+ * equal Updated stay in key order (Go's sort.Sort leaves their order unspecified). With owner =
+ * GX_ALL_OWNERS every server's records, else one server's: Server.SortedServices (view.go:48-58).
+ * n_out = count (at most cap written). Sorted on the device (stable radix sort). */
+#define GX_ALL_OWNERS 0xffffffffu
+int gx_each_service_sorted(gx_engine *e, uint32_t view, uint32_t owner, gx_service *out, uint32_t cap,
+                           uint32_t *n_out);
+/* Service.Name of every record, for ByService: names[off[r] .. off[r + 1]) is the Name of record
+ * r = host * S + svc (R + 1 offsets, off[0] = 0). Replaces any earlier table. */
+int gx_set_service_names(gx_engine *e, const char *names, const uint64_t *off);
+/* ByService (services_state.go:738-748): the view's present records grouped by Service.Name, in
+ * EachServiceSorted order inside each group; groups in bytewise Name order (the reference returns a
+ * Go map); group_out[i] (optional) = index of out[i]'s Name among the distinct names of the table.
+ * GX_ENOENT if no names were set. */
+int gx_by_service(gx_engine *e, uint32_t view, gx_service *out, uint32_t *group_out, uint32_t cap,
+                  uint32_t *n_out);
+
 /* ---- memberlist Delegate (services_delegate.go) ------------------------------------------- */
 /* NotifyMsg (:72-83) + Start() decode loop (:46-56): the records of one packet -> UpdateService. */
 int gx_notify_msg(gx_engine *e, uint32_t host, const gx_service *recs, uint32_t n);

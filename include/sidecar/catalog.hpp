@@ -35,9 +35,10 @@ struct Service {
   std::string Hostname;
   int64_t Updated = 0;
   int Status = ALIVE;
+  std::string Name;  // Service.Name (ByService groups by it); not part of the merge path
   bool IsTombstone() const { return Status == TOMBSTONE; }
   bool operator==(const Service &o) const {
-    return ID == o.ID && Hostname == o.Hostname && Updated == o.Updated && Status == o.Status;
+    return ID == o.ID && Hostname == o.Hostname && Updated == o.Updated && Status == o.Status;  // Name: metadata
   }
 };
 
@@ -114,6 +115,13 @@ class Cluster {
   }
   gx_service Rec(const Service &svc) {
     uint32_t h = Host(svc.Hostname);
+    if (!svc.Name.empty()) {  // remember the Name of the (host, ID) record for ByService
+      std::string &n = names_[(uint64_t)h * p_.n_services + Id(h, svc.ID)];
+      if (n != svc.Name) {
+        n = svc.Name;
+        names_dirty_ = true;
+      }
+    }
     gx_service r{};
     r.updated_ns = svc.Updated;
     r.host = h;
@@ -128,8 +136,25 @@ class Cluster {
                                                                              : "svc-" + std::to_string(r.svc);
     s.Updated = r.updated_ns;
     s.Status = r.status;
+    auto it = names_.find((uint64_t)r.host * p_.n_services + r.svc);
+    if (it != names_.end()) s.Name = it->second;
     return s;
   }
+  // Hands the engine the Service.Name of every record (gx_set_service_names) when one changed.
+  void SyncNames() {
+    if (!names_dirty_) return;
+    const uint64_t R = (uint64_t)p_.n_hosts * p_.n_services;
+    std::string blob;
+    std::vector<uint64_t> off(R + 1, 0);
+    for (uint64_t r = 0; r < R; r++) {
+      auto it = names_.find(r);
+      if (it != names_.end()) blob += it->second;
+      off[r + 1] = blob.size();
+    }
+    check(gx_set_service_names(e_, blob.data(), off.data()), "gx_set_service_names");
+    names_dirty_ = false;
+  }
+  const std::vector<std::string> &HostNames() const { return host_names_; }
   // Encoded length of every field of svc's Service except Updated and Status (the Go side gets it
   // from len(svc.Encode()) minus those two); used by the byte-limited GetBroadcasts.
   void SetStaticBytes(const std::string &hostname, const std::string &id, uint16_t bytes) {
@@ -156,6 +181,8 @@ class Cluster {
   std::vector<std::map<std::string, uint16_t>> ids_;
   std::vector<std::vector<std::string>> id_names_;
   std::map<uint32_t, std::vector<uint16_t>> static_;
+  std::map<uint64_t, std::string> names_;  // record key -> Service.Name
+  bool names_dirty_ = false;
 };
 
 namespace catalog {
@@ -256,11 +283,40 @@ class ServicesState {
     }
   }
   // EachServiceSorted (catalog/view.go:14-26): by Updated; ties in key order (Go's sort.Sort
-  // leaves them unspecified).
-  std::vector<Service> EachServiceSorted() {
-    auto v = EachService();
-    std::stable_sort(v.begin(), v.end(), [](const Service &a, const Service &b) { return a.Updated < b.Updated; });
-    return v;
+  // leaves them unspecified). Sorted by the engine (gx_each_service_sorted).
+  std::vector<Service> EachServiceSorted() { return Sorted(GX_ALL_OWNERS); }
+  // Server.SortedServices (view.go:48-58): one server's services by Updated.
+  std::vector<Service> SortedServices(const std::string &hostname) { return Sorted(c_.Host(hostname)); }
+  // SortedServers (view.go:82-92): the names of the servers this view holds, sorted.
+  std::vector<std::string> SortedServers() {
+    std::vector<std::string> out;
+    for (auto &s : EachService())
+      if (std::find(out.begin(), out.end(), s.Hostname) == out.end()) out.push_back(s.Hostname);
+    std::sort(out.begin(), out.end());
+    return out;
+  }
+  // ByService (services_state.go:738-748): services grouped by Service.Name, each group in
+  // EachServiceSorted order (gx_by_service).
+  std::map<std::string, std::vector<Service>> ByService() {
+    c_.SyncNames();
+    uint32_t n = 0;
+    check(gx_by_service(c_.engine(), self_, nullptr, nullptr, 0, &n), "ByService");
+    std::vector<gx_service> out(n ? n : 1);
+    check(gx_by_service(c_.engine(), self_, out.data(), nullptr, n, &n), "ByService");
+    std::map<std::string, std::vector<Service>> m;
+    for (uint32_t i = 0; i < n; i++) {
+      Service s = c_.Svc(out[i]);
+      m[s.Name].push_back(s);
+    }
+    return m;
+  }
+  std::vector<Service> Sorted(uint32_t owner) {
+    uint32_t n = 0;
+    check(gx_each_service_sorted(c_.engine(), self_, owner, nullptr, 0, &n), "EachServiceSorted");
+    std::vector<gx_service> out(n ? n : 1);
+    check(gx_each_service_sorted(c_.engine(), self_, owner, out.data(), n, &n), "EachServiceSorted");
+    out.resize(n);
+    return c_.Svcs(out);
   }
   // state.Servers[hostname].Services[id], or nothing
   std::optional<Service> Get(const std::string &hostname, const std::string &id) {

@@ -82,6 +82,7 @@ struct gx_engine {
   uint32_t *fd_len;       /* H * K */
   uint32_t *fd_peers;     /* H * K  gossip targets (memberlist's choice) */
   uint32_t *fd_np;        /* H */
+  uint32_t *name_rank;    /* R  ByService: rank of each record's Service.Name, NULL until set */
   gx_stats st;
 };
 static void free_names(gx_engine *e);
@@ -1331,6 +1332,7 @@ int gx_destroy(gx_engine *e) {
   free(e->sbytes);
   free(e->srvt);
   free(e->vlc);
+  free(e->name_rank);
   for (int i = 0; i < GX_MAX_LISTENERS; i++) free(e->lst[i].ring);
   free(e->x_t);
   free(e->x_mine);
@@ -1592,6 +1594,87 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
   }
   if (n_out) *n_out = n;
   return GX_OK;
+}
+
+/* ---- catalog readers (catalog/view.go:14-58, services_state.go:726-748) ---------------------- */
+struct sorted_ent {
+  uint64_t key; /* name rank (ByService) */
+  int64_t ts;
+  uint32_t r;
+  uint64_t w;
+};
+static int cmp_sorted(const void *pa, const void *pb) {
+  const struct sorted_ent *a = (const struct sorted_ent *)pa, *b = (const struct sorted_ent *)pb;
+  if (a->key != b->key) return a->key < b->key ? -1 : 1;
+  if (a->ts != b->ts) return a->ts < b->ts ? -1 : 1; /* ServicesByAge: Updated.Before */
+  return a->r < b->r ? -1 : (a->r > b->r); /* equal Updated: key order */
+}
+static int sorted_view(gx_engine *e, uint32_t view, uint32_t owner, int by_name, gx_service *out, uint32_t *group_out,
+                       uint32_t cap, uint32_t *n_out) {
+  struct sorted_ent *v = (struct sorted_ent *)malloc(sizeof(struct sorted_ent) * (e->R ? e->R : 1));
+  uint32_t n = 0;
+  const uint64_t *row = &e->view[(size_t)view * e->R];
+  for (uint32_t r = 0; r < e->R; r++) {
+    if (st_of(row[r]) == GX_ABSENT || (owner != GX_ALL_OWNERS && r / e->S != owner)) continue;
+    v[n].key = by_name ? e->name_rank[r] : 0;
+    v[n].ts = ts_of(row[r]);
+    v[n].r = r;
+    v[n].w = row[r];
+    n++;
+  }
+  qsort(v, n, sizeof(*v), cmp_sorted);
+  for (uint32_t i = 0; i < n && i < cap; i++) {
+    grec g = {v[i].w, v[i].r, 0};
+    to_svc(e, &g, &out[i]);
+    if (group_out) group_out[i] = (uint32_t)v[i].key;
+  }
+  if (n_out) *n_out = n;
+  free(v);
+  return GX_OK;
+}
+int gx_each_service_sorted(gx_engine *e, uint32_t view, uint32_t owner, gx_service *out, uint32_t cap,
+                           uint32_t *n_out) {
+  if (!e || !is_local(e, view) || (owner != GX_ALL_OWNERS && owner >= e->H) || (cap && !out)) return GX_EINVAL;
+  return sorted_view(e, view, owner, 0, out, NULL, cap, n_out);
+}
+static const char *sn_base;
+static const uint64_t *sn_off;
+static int cmp_name(const void *pa, const void *pb) {
+  const uint32_t a = *(const uint32_t *)pa, b = *(const uint32_t *)pb;
+  const uint64_t la = sn_off[a + 1] - sn_off[a], lb = sn_off[b + 1] - sn_off[b];
+  const int c = memcmp(sn_base + sn_off[a], sn_base + sn_off[b], la < lb ? la : lb);
+  if (c) return c;
+  if (la != lb) return la < lb ? -1 : 1;
+  return a < b ? -1 : (a > b);
+}
+int gx_set_service_names(gx_engine *e, const char *names, const uint64_t *off) {
+  if (!e || !off || off[0] != 0) return GX_EINVAL;
+  for (uint32_t r = 0; r < e->R; r++)
+    if (off[r + 1] < off[r]) return GX_EINVAL;
+  if (off[e->R] && !names) return GX_EINVAL;
+  static const char empty[1] = {0};
+  uint32_t *idx = (uint32_t *)malloc(sizeof(uint32_t) * (e->R ? e->R : 1));
+  for (uint32_t r = 0; r < e->R; r++) idx[r] = r;
+  sn_base = names ? names : empty;
+  sn_off = off;
+  qsort(idx, e->R, sizeof(uint32_t), cmp_name); /* distinct names in bytewise order */
+  if (!e->name_rank) e->name_rank = (uint32_t *)malloc(sizeof(uint32_t) * (e->R ? e->R : 1));
+  uint32_t g = 0;
+  for (uint32_t k = 0; k < e->R; k++) {
+    if (k) {
+      const uint32_t a = idx[k - 1], b = idx[k];
+      const uint64_t la = off[a + 1] - off[a], lb = off[b + 1] - off[b];
+      if (la != lb || memcmp(sn_base + off[a], sn_base + off[b], la)) g++;
+    }
+    e->name_rank[idx[k]] = g;
+  }
+  free(idx);
+  return GX_OK;
+}
+int gx_by_service(gx_engine *e, uint32_t view, gx_service *out, uint32_t *group_out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !is_local(e, view) || (cap && !out)) return GX_EINVAL;
+  if (!e->name_rank) return GX_ENOENT;
+  return sorted_view(e, view, GX_ALL_OWNERS, 1, out, group_out, cap, n_out);
 }
 
 int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, gx_server_times *out) {

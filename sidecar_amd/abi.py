@@ -201,7 +201,9 @@ ABI_FUNCS = [
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
     "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
     "gx_fd_get_broadcasts", "gx_fd_probe", "gx_fd_timers", "gx_fd_converged", "gx_fd_merge_state",
+    "gx_each_service_sorted", "gx_set_service_names", "gx_by_service",
 ]
+ALL_OWNERS = 0xFFFFFFFF
 
 
 def _declare(lib):
@@ -273,6 +275,9 @@ def _declare(lib):
         "gx_fd_timers": ([vp, u32], i32),
         "gx_fd_converged": ([vp, P(i32), P(C.c_uint64)], i32),
         "gx_fd_merge_state": ([vp, u32, vp], i32),
+        "gx_each_service_sorted": ([vp, u32, u32, P(GxService), u32, P(u32)], i32),
+        "gx_set_service_names": ([vp, vp, P(C.c_uint64)], i32),
+        "gx_by_service": ([vp, u32, P(GxService), P(u32), u32, P(u32)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -608,6 +613,33 @@ class Engine:
         n = C.c_uint32()
         check(self.lib.gx_read_list(self.h, host, slot, out, 1024, C.byref(n)))
         return [out[i] for i in range(min(n.value, 1024))]
+
+    def each_service_sorted(self, view: int, owner: int = ALL_OWNERS) -> list:
+        """EachServiceSorted (catalog/view.go:14-26), or one server's SortedServices (:48-58)."""
+        n = C.c_uint32()
+        check(self.lib.gx_each_service_sorted(self.h, view, owner, None, 0, C.byref(n)), "gx_each_service_sorted")
+        out = (GxService * max(1, n.value))()
+        check(self.lib.gx_each_service_sorted(self.h, view, owner, out, n.value, C.byref(n)), "gx_each_service_sorted")
+        return [out[i] for i in range(n.value)]
+
+    def set_service_names(self, names) -> None:
+        """Service.Name of every record r = host * S + svc (a list of R str/bytes)."""
+        bs = [x.encode() if isinstance(x, str) else bytes(x) for x in names]
+        assert len(bs) == self.H * self.S
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs])
+        blob = b"".join(bs) or b"\0"
+        check(self.lib.gx_set_service_names(self.h, blob, off.ctypes.data_as(C.POINTER(C.c_uint64))),
+              "gx_set_service_names")
+
+    def by_service(self, view: int):
+        """ByService (services_state.go:738-748): [(group, record)] in group order."""
+        n = C.c_uint32()
+        check(self.lib.gx_by_service(self.h, view, None, None, 0, C.byref(n)), "gx_by_service")
+        out = (GxService * max(1, n.value))()
+        grp = (C.c_uint32 * max(1, n.value))()
+        check(self.lib.gx_by_service(self.h, view, out, grp, n.value, C.byref(n)), "gx_by_service")
+        return [(grp[i], out[i]) for i in range(n.value)]
 
     def server_times(self, view: int, lo: int = 0, hi: Optional[int] = None) -> np.ndarray:
         """Server.LastUpdated / LastChanged of owners [lo, hi) in `view`: int64 [n, 2]."""

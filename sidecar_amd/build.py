@@ -6,7 +6,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", "gx_engine.hip")]
+SRC = [os.path.join(HERE, "csrc", "gx_engine.hip"), os.path.join(HERE, "csrc", "gx_sort.hip")]
 DEPS = SRC + sorted(glob.glob(os.path.join(HERE, "csrc", "*.hpp"))) + [os.path.join(ROOT, "include", "gx.h")]
 OUT = os.path.join(HERE, "libgx.so")
 ARCH = os.environ.get("GX_OFFLOAD_ARCH", "gfx950")

@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <string>
 #include <vector>
 
 
@@ -62,6 +63,11 @@ struct gx_engine {
   Dev d;
   hipStream_t stream;      // where all device work goes (own_stream, or the caller's: gx_set_stream)
   hipStream_t own_stream;
+  // shard-local push-pull pairs run on side_stream, between side_start (recorded on `stream` after
+  // the rows are packed) and side_done (joined back into `stream` before anything reads them)
+  hipStream_t side_stream;
+  hipEvent_t side_start, side_done;
+  bool side_pending;
   int async_phases;         // sharded phase calls return without waiting (gx_set_stream)
   int device;
   int timing;
@@ -69,6 +75,7 @@ struct gx_engine {
   std::vector<uint32_t> pp_host;  // GX_PP_INITIATE: this round's exchanges, batch by batch (a then b)
   uint32_t *pp_dev;
   int32_t *pp_prow;               // all -1: every exchange is local
+  uint32_t *name_rank;            // [R] ByService: rank of each record's Service.Name (gx_set_service_names)
   double ms[GX_K_COUNT];
   uint64_t launches[GX_K_COUNT];
   uint64_t host_bytes[GX_K_COUNT], host_units[GX_K_COUNT];  // codec classes (gx_codec_host.hpp)
@@ -145,17 +152,18 @@ struct LaunchTimer {
   gx_engine *e;
   int cls;
   hipEvent_t a, b;
-  LaunchTimer(gx_engine *e_, int cls_) : e(e_), cls(cls_), a(nullptr), b(nullptr) {
+  hipStream_t st;
+  LaunchTimer(gx_engine *e_, int cls_, hipStream_t s_ = nullptr) : e(e_), cls(cls_), a(nullptr), b(nullptr), st(s_ ? s_ : e_->stream) {
     e->launches[cls]++;
     if (e->timing) {
       (void)hipEventCreate(&a);
       (void)hipEventCreate(&b);
-      (void)hipEventRecord(a, e->stream);
+      (void)hipEventRecord(a, st);
     }
   }
   ~LaunchTimer() {
     if (e->timing) {
-      (void)hipEventRecord(b, e->stream);
+      (void)hipEventRecord(b, st);
       e->pending_ev.push_back({cls, a, b});
     }
   }
@@ -214,7 +222,17 @@ static int take_device_error(gx_engine *e) {
   return GX_EINVAL;
 }
 
+// The shard-local push-pull merges rejoin the engine's stream (gx_ae_merge_local).
+static int join_side(gx_engine *e) {
+  if (!e->side_pending) return GX_OK;
+  HIPCHK(hipStreamWaitEvent(e->stream, e->side_done, 0));
+  e->side_pending = false;
+  return GX_OK;
+}
+
 static int sync_check(gx_engine *e) {
+  int jr = join_side(e);
+  if (jr) return jr;
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipGetLastError());
   int rc = take_device_error(e);
@@ -249,7 +267,7 @@ static void owner_launch(const Dev &d, hipStream_t s) {
   else if (d.S <= 32) launch_owner<32>(d, s);
   else launch_owner<64>(d, s);
 }
-#define SCAN_GRID 2048  // worklist blocks: 8 per CU when many views expire, a quick exit when none do
+#define SCAN_GRID 512  // worklist blocks: 2 per CU stream the rows when views expire, a quick exit when none do
 
 // Phases 0-3 (wake, owners, expiry scan, storm, GetBroadcasts) for this engine's hosts.
 static int round_send_impl(gx_engine *e) {
@@ -303,7 +321,7 @@ static int round_merge_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
     k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);
-    const unsigned g = nblk(d.Hl, MERGE_WAVES);
+    const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE);
     if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
     else (ev ? k_merge<false, true> : k_merge<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
   }
@@ -443,6 +461,8 @@ int gx_abi_version(void) { return GX_ABI_VERSION; }
 int gx_set_stream(gx_engine *e, void *stream, int mode) {
   if (!e || (mode & ~(GX_STREAM_CALLER | GX_STREAM_ASYNC))) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
+  if (e->side_pending) HIPCHK(hipStreamSynchronize(e->side_stream));
+  e->side_pending = false;
   HIPCHK(hipStreamSynchronize(e->stream));  // work queued so far completes first
   e->stream = (mode & GX_STREAM_CALLER) ? (hipStream_t)stream : e->own_stream;
   e->async_phases = (mode & GX_STREAM_ASYNC) ? 1 : 0;
@@ -551,6 +571,7 @@ int gx_destroy(gx_engine *e) {
   if (!e) return GX_EINVAL;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->side_stream) (void)hipStreamSynchronize(e->side_stream);
   for (auto &t : e->pending_ev) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
@@ -559,12 +580,15 @@ int gx_destroy(gx_engine *e) {
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, d.in_cnt, d.scan_list, d.scan_cnt, d.tick,
-                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->api_dev, e->conv_bad, e->digest_buf,
+                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf,
                   d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+  if (e->side_stream) (void)hipStreamDestroy(e->side_stream);
+  if (e->side_start) (void)hipEventDestroy(e->side_start);
+  if (e->side_done) (void)hipEventDestroy(e->side_done);
   delete e;
   return GX_OK;
 }
@@ -598,7 +622,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->api_dev_bytes = 0;
   e->conv_bad = nullptr;
   e->digest_buf = nullptr;
-  e->stream = e->own_stream = nullptr;
+  e->stream = e->own_stream = e->side_stream = nullptr;
+  e->side_start = e->side_done = nullptr;
+  e->side_pending = false;
   e->async_phases = 0;
   e->ob_entries = nullptr;
   e->ob_counts = nullptr;
@@ -620,6 +646,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ae_local_round = -1;
   e->pp_dev = nullptr;
   e->pp_prow = nullptr;
+  e->name_rank = nullptr;
   Dev &d = e->d;
   d.p = *p;
   d.H = p->n_hosts;
@@ -648,6 +675,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
   }
   e->stream = e->own_stream;
   e->async_phases = 0;
+  if (hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->side_start, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    gx_destroy(e);
+    return GX_EIO;
+  }
   // per-host arrays hold this shard's Hl hosts; the message table also takes the packets received
   // from other shards (at most (H - Hl) * K), so it is sized H * K.
   size_t Hg = d.H, H = d.Hl, K = d.KE ? d.KE : 1;
@@ -666,7 +700,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.in_cnt, sizeof(uint32_t) * H);
   d.DI = p->inbox_slots ? p->inbox_slots : 64;
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
-  if (const char *x = getenv("GX_AB_INLINE_SLOTS")) d.DR = std::min<uint32_t>(d.DI, (uint32_t)atoi(x));  // A/B only
+  d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
   ALLOC(d.in_hdr, sizeof(uint4) * H * d.DI);
   ALLOC(d.in_ovf, sizeof(uint4) * Hg * K);
   ALLOC(d.in_rec, sizeof(grec) * H * d.DR * p->packet_cap);
@@ -677,7 +711,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->pp_prow, sizeof(int32_t) * Hg);
     HIPCHK(hipMemset(e->pp_prow, 0xff, sizeof(int32_t) * Hg));
   }
-  ALLOC(d.mflag, H);
+  ALLOC(d.mflag, (H + 7) & ~(size_t)7);  // read 8 flags at a time
+  HIPCHK(hipMemset(d.mflag, 0, (H + 7) & ~(size_t)7));
   ALLOC(d.minexp, sizeof(unsigned long long) * H);
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
@@ -1093,6 +1128,119 @@ int gx_local_state(gx_engine *e, uint32_t view, gx_service *out, uint32_t cap, u
   }
   if (n_out) *n_out = n;
   return GX_OK;
+}
+
+extern "C" int gx_sort_u64_pairs(void *tmp, size_t *tmp_bytes, uint64_t *keys_in, uint64_t *keys_out,
+                                 uint32_t *vals_in, uint32_t *vals_out, uint32_t n, int end_bit, hipStream_t s);
+extern "C" int gx_sort_u32_pairs(void *tmp, size_t *tmp_bytes, uint32_t *keys_in, uint32_t *keys_out,
+                                 uint32_t *vals_in, uint32_t *vals_out, uint32_t n, int end_bit, hipStream_t s);
+
+// EachServiceSorted / SortedServices / ByService on the device: the view's present records
+// compacted in key order, stable radix sort by Updated (ties stay in key order), for ByService a
+// second stable sort by the Name rank, then written out as gx_service.
+static int sorted_view(gx_engine *e, uint32_t view, uint32_t owner, bool by_name, gx_service *out, uint32_t *group_out,
+                       uint32_t cap, uint32_t *n_out) {
+  Dev &d = e->d;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const uint32_t vi = view - d.lo, nb = (d.R + VC_CHUNK - 1) / VC_CHUNK;
+  uint32_t *cnt = nullptr, *v0 = nullptr, *v1 = nullptr, *k32a = nullptr, *k32b = nullptr;
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  gx_service *dout = nullptr;
+  void *tmp = nullptr;
+  int rc = GX_OK;
+  uint32_t n = 0;
+  auto fail = [&](hipError_t err) { return err == hipSuccess ? GX_OK : (err == hipErrorOutOfMemory ? GX_ENOMEM : GX_EIO); };
+#define VCK(x)                    \
+  do {                            \
+    rc = fail(x);                 \
+    if (rc) goto done;            \
+  } while (0)
+  VCK(hipMalloc(&cnt, sizeof(uint32_t) * (nb + 1)));
+  k_vc_count<<<nb, 256, 0, s>>>(d, vi, owner, cnt);
+  k_vc_scan<<<1, 1024, 0, s>>>(cnt, nb);
+  VCK(hipMemcpyAsync(&n, &cnt[nb], sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  VCK(hipStreamSynchronize(s));
+  if (n) {
+    VCK(hipMalloc(&k0, sizeof(uint64_t) * n));
+    VCK(hipMalloc(&k1, sizeof(uint64_t) * n));
+    VCK(hipMalloc(&v0, sizeof(uint32_t) * n));
+    VCK(hipMalloc(&v1, sizeof(uint32_t) * n));
+    VCK(hipMalloc(&dout, sizeof(gx_service) * n));
+    k_vc_write<<<nb, 256, 0, s>>>(d, vi, owner, cnt, k0, v0);
+    size_t tb = 0, tb2 = 0;
+    if (gx_sort_u64_pairs(nullptr, &tb, k0, k1, v0, v1, n, 64 - GX_TS_SHIFT, s)) VCK(hipErrorUnknown);
+    if (by_name) {
+      VCK(hipMalloc(&k32a, sizeof(uint32_t) * n));
+      VCK(hipMalloc(&k32b, sizeof(uint32_t) * n));
+      if (gx_sort_u32_pairs(nullptr, &tb2, k32a, k32b, v1, v0, n, 32, s)) VCK(hipErrorUnknown);
+    }
+    VCK(hipMalloc(&tmp, std::max<size_t>(std::max(tb, tb2), 1)));
+    if (gx_sort_u64_pairs(tmp, &tb, k0, k1, v0, v1, n, 64 - GX_TS_SHIFT, s)) VCK(hipErrorUnknown);
+    uint32_t *order = v1;
+    if (by_name) {
+      k_vc_rank<<<nblk(n, 256), 256, 0, s>>>(e->name_rank, v1, k32a, n);
+      if (gx_sort_u32_pairs(tmp, &tb2, k32a, k32b, v1, v0, n, 32, s)) VCK(hipErrorUnknown);
+      order = v0;
+    }
+    k_vc_out<<<nblk(n, 256), 256, 0, s>>>(d, vi, order, n, dout);
+    const uint32_t m = n < cap ? n : cap;
+    if (m) {
+      VCK(hipMemcpyAsync(out, dout, sizeof(gx_service) * m, hipMemcpyDeviceToHost, s));
+      if (by_name && group_out) VCK(hipMemcpyAsync(group_out, k32b, sizeof(uint32_t) * m, hipMemcpyDeviceToHost, s));
+    }
+    VCK(hipStreamSynchronize(s));
+    VCK(hipGetLastError());
+  }
+  if (n_out) *n_out = n;
+done:
+#undef VCK
+  for (void *p : {(void *)cnt, (void *)k0, (void *)k1, (void *)v0, (void *)v1, (void *)k32a, (void *)k32b, (void *)dout, tmp})
+    if (p) (void)hipFree(p);
+  return rc;
+}
+
+int gx_each_service_sorted(gx_engine *e, uint32_t view, uint32_t owner, gx_service *out, uint32_t cap,
+                           uint32_t *n_out) {
+  if (!e || !own(e, view) || (owner != GX_ALL_OWNERS && owner >= e->d.H) || (cap && !out)) return GX_EINVAL;
+  return sorted_view(e, view, owner, false, out, nullptr, cap, n_out);
+}
+
+int gx_set_service_names(gx_engine *e, const char *names, const uint64_t *off) {
+  if (!e || !off) return GX_EINVAL;
+  const uint32_t R = e->d.R;
+  if (off[0] != 0) return GX_EINVAL;
+  for (uint32_t r = 0; r < R; r++)
+    if (off[r + 1] < off[r]) return GX_EINVAL;
+  if (off[R] && !names) return GX_EINVAL;
+  // rank = index of the record's Name among the distinct names in bytewise order
+  std::vector<uint32_t> idx(R), rank(R);
+  for (uint32_t r = 0; r < R; r++) idx[r] = r;
+  auto name = [&](uint32_t r) { return std::string(names ? names + off[r] : "", (size_t)(off[r + 1] - off[r])); };
+  std::vector<std::string> nm(R);
+  for (uint32_t r = 0; r < R; r++) nm[r] = name(r);
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return nm[a] < nm[b]; });
+  uint32_t g = 0;
+  for (uint32_t k = 0; k < R; k++) {
+    if (k && nm[idx[k]] != nm[idx[k - 1]]) g++;
+    rank[idx[k]] = g;
+  }
+  HIPCHK(hipSetDevice(e->device));
+  if (!e->name_rank) {
+    if (hipMalloc(&e->name_rank, sizeof(uint32_t) * R) != hipSuccess) {
+      (void)hipGetLastError();
+      e->name_rank = nullptr;
+      return GX_ENOMEM;
+    }
+  }
+  HIPCHK(hipMemcpy(e->name_rank, rank.data(), sizeof(uint32_t) * R, hipMemcpyHostToDevice));
+  return GX_OK;
+}
+
+int gx_by_service(gx_engine *e, uint32_t view, gx_service *out, uint32_t *group_out, uint32_t cap, uint32_t *n_out) {
+  if (!e || !own(e, view) || (cap && !out)) return GX_EINVAL;
+  if (!e->name_rank) return GX_ENOENT;
+  return sorted_view(e, view, GX_ALL_OWNERS, true, out, group_out, cap, n_out);
 }
 
 int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, gx_server_times *out) {
@@ -1655,10 +1803,12 @@ int gx_ae_return_pack(gx_engine *e, const void *lead, uint64_t lead_bytes, void 
 }
 
 // Launch the planned pairs [lo, hi) (received-row pairs first, then shard-local pairs).
-static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *lead, const void *ret) {
+static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *lead, const void *ret,
+                           hipStream_t st = nullptr) {
   if (hi <= lo) return;
+  if (!st) st = e->stream;
   set_round_fields(e);
-  LaunchTimer t(e, GX_K_AE);
+  LaunchTimer t(e, GX_K_AE, st);
   const uint32_t np = e->n_pack;
   AeIn in;
   in.lead = (const uint8_t *)lead;
@@ -1674,7 +1824,7 @@ static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *l
   in.nblk = e->nblk;
   const bool small = hi - lo < 1024;  // fewer than 4 pairs per CU: per-block bandwidth decides
 #define GX_AE_PLAN(V, E)                                                                                     \
-  (E ? k_ae_plan_ev<V> : small ? k_ae_plan_pf2<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, e->stream>>>(             \
+  (E ? k_ae_plan_ev<V> : small ? k_ae_plan_pf2<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, st>>>(                    \
       e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo, e->ae_pcount + lo, in, e->ae_skip)
   const bool ev = !e->log_views.empty();
   if (e->d.R % 2 == 0 && !ev) GX_AE_PLAN(true, false);
@@ -1689,7 +1839,13 @@ int gx_ae_merge_local(gx_engine *e) {
   HIPCHK(hipSetDevice(e->device));
   if (!ae_round(e) || e->d.G < 2 || e->ae_local_round == e->d.round) return GX_OK;
   if (e->ae_planned_round != (int)e->d.round) return GX_EINVAL;
-  ae_plan_launch(e, e->n_plan_rows, e->n_plan, nullptr, nullptr);  // asynchronous: overlaps the exchange
+  // on the side stream, after the rows are packed: the exchange layer's collectives (ordered
+  // behind `stream`) run while these merges do; gx_ae_merge joins them back
+  HIPCHK(hipEventRecord(e->side_start, e->stream));
+  HIPCHK(hipStreamWaitEvent(e->side_stream, e->side_start, 0));
+  ae_plan_launch(e, e->n_plan_rows, e->n_plan, nullptr, nullptr, e->side_stream);
+  HIPCHK(hipEventRecord(e->side_done, e->side_stream));
+  e->side_pending = true;
   HIPCHK(hipGetLastError());
   e->ae_local_round = e->d.round;
   return GX_OK;
@@ -1733,14 +1889,18 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
     k_fd_pushpull_plan<<<2 * e->n_plan, 64, 0, e->stream>>>(e->d, e->ae_pa, e->ae_pb, e->ae_prow, e->ae_skip,
                                                              e->fd_rsnap);
   }
+  int jr = join_side(e);  // the next round's phases see the local pairs merged
+  if (jr) return jr;
   return phase_done(e);
 }
 
 int gx_round_end(gx_engine *e) {
   if (!e) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
+  int rc = join_side(e);
+  if (rc) return rc;
   e->d.round++;
-  int rc = wake_all(e);
+  rc = wake_all(e);
   return rc ? rc : phase_done(e);
 }
 

@@ -180,8 +180,19 @@ __global__ __launch_bounds__(256) void k_owner(Dev d) {
   const bool act = idx < d.Hl && !departed(d, d.lo + idx);
   gx_host_state hs;
   gx_job *sj = &s_sl[threadIdx.x - tl];
+  // everything the tick may read is loaded up front: the bookkeeping, the own records' view slots
+  // (one 128-B row segment), their local status and the view's expiry bound
+  uint64_t cur0 = GX_SLOT_ABSENT;
+  uint8_t ost0 = GX_ALIVE;
+  unsigned long long mexp0 = 0;
   if (act) {
     hs = d.hs[idx];
+    const uint32_t o = d.lo + idx;
+    if (tl < d.S) {
+      cur0 = vrow(d, o)[o * d.S + tl];
+      ost0 = d.own_status[(size_t)idx * d.S + tl];
+    }
+    if (tl == 0) mexp0 = d.minexp[idx];
     if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
   }
   __syncthreads();
@@ -200,7 +211,7 @@ __global__ __launch_bounds__(256) void k_owner(Dev d) {
       }
       const uint32_t s = tl;
       const bool svc = s < d.S;
-      uint8_t ost = svc ? d.own_status[(size_t)idx * d.S + s] : (uint8_t)GX_ALIVE;
+      uint8_t ost = ost0;
       if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
         const uint64_t x = rng4(d.p.seed, ST_CHURN, (uint64_t)d.round, o, 0);
         if ((uint32_t)(x & 0xffffffffu) % 1000000u < d.p.churn_ppm) {
@@ -219,7 +230,7 @@ __global__ __launch_bounds__(256) void k_owner(Dev d) {
         const uint32_t r = o * d.S + s;
         uint64_t *slot = &vrow(d, o)[run ? r : o * d.S];
         const uint64_t sw = pack(d.now, ost);
-        const uint64_t cur = run ? *slot : GX_SLOT_ABSENT;
+        const uint64_t cur = run ? cur0 : GX_SLOT_ABSENT;  // no other writer of own slots before this
         const bool isnew = run && (st_of(cur) == GX_ABSENT || (st_of(sw) != GX_TOMBSTONE && st_of(sw) != st_of(cur)));
         const bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > hs.last_bcast_ns;  // (:547)
         const uint64_t newm = (__ballot(isnew) >> (tw * T)) & tmask;
@@ -294,7 +305,8 @@ __global__ __launch_bounds__(256) void k_owner(Dev d) {
         const bool tick = !(hs.flags & 2u) && hs.bt_next <= d.round;
         d.tick[idx] = tick ? 1 : 0;
         if (tick) {
-          if (d.minexp[idx] >= (unsigned long long)d.now) {  // nothing can expire in this view
+          // (the tick's own merges only lower the bound to values >= now: same decision)
+          if (mexp0 >= (unsigned long long)d.now) {  // nothing can expire in this view
             d.scan_cnt[idx] = 0;
             a.c[C_SCANSLOTS] += d.R;
           } else {
@@ -779,16 +791,20 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   if (idx < d.Hl) {
     uint32_t u = d.lo + idx;
     uint32_t cap = d.p.packet_cap;
+    gx_host_state *h = &d.hs[idx];
+    gx_host_state hs = *h;  // loaded with the tick flag (both before any store)
+    const bool tick = do_bt && d.tick[idx];
     for (uint32_t j = lane; j < d.KE; j += T) {
       d.msg_len[(size_t)idx * d.KE + j] = 0;
       d.msg_key[(size_t)idx * d.KE + j] = u * d.KE + j;
     }
-    if (do_bt && d.tick[idx]) {  // departed hosts never tick
+    if (tick) {  // departed hosts never tick
       if (lane == 0) {
         const uint32_t n = d.scan_cnt[idx];
-        bt_finish(d, a, u, d.hs[idx].running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
+        bt_finish(d, a, u, hs.running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
       }
       __threadfence_block();  // the team reads the host's bookkeeping below
+      hs = *h;
     }
     if (!X || !departed(d, u)) {
       const bool fd = X && d.p.fd_enable;
@@ -800,8 +816,6 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       } else {
         np = sample_peers(d, u, peers);
       }
-      gx_host_state *h = &d.hs[idx];
-      gx_host_state hs = *h;
       // The jobs at the FIFO head that this round's calls will dequeue are loaded up front, one
       // per team lane (call c takes job c while c < the jobs queued at the start: later pushes go
       // to the tail and cannot overwrite them), so a call waits on its list records only.
@@ -928,7 +942,7 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
 // (stale, or no newer than the slot: see k_merge) is finished here, its merges and stale drops
 // counted. A receiver with a live record, or with more than DR packets, is flagged (mflag) and
 // merged in full by k_merge.
-#define LEAN_LPR 32  // lanes per receiver
+#define LEAN_LPR 32  // lanes per receiver (16 lanes x 8 records measured slower: profiles/ab_flags.sh)
 #define LEAN_Q 4     // records per lane per batch
 __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
   const uint32_t lane = threadIdx.x & 63, l = threadIdx.x & (LEAN_LPR - 1);
@@ -1000,6 +1014,7 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
 
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
+#define MERGE_RANGE 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
 // Orders a wave's LDS and global accesses across its lanes (the waves of a block do not meet).
 GXD void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1017,17 +1032,27 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
   uint4 *s_hdr = s_hdr_[wv];
   uint8_t *s_accf = s_accf_[wv], *s_chg = s_chg_[wv], *s_prev = s_prev_[wv];
   uint64_t *s_accw = s_accw_[wv];
-  const uint32_t vi = blockIdx.x * MERGE_WAVES + wv, v = d.lo + vi;
-  if (vi >= d.Hl || !d.mflag[vi]) return;  // k_merge_lean finished this receiver
   const uint32_t lane = threadIdx.x & 63;
+  // each wave takes the flags of MERGE_RANGE consecutive receivers and merges the flagged ones in
+  // turn (one receiver per wave measured fastest: the flagged receivers' chains run side by side)
+  const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * MERGE_RANGE;
+  if (r0 >= d.Hl) return;
+  uint64_t fl = 0;
+  if (MERGE_RANGE == 8 && r0 + MERGE_RANGE <= d.Hl) {
+    fl = *reinterpret_cast<const uint64_t *>(&d.mflag[r0]);
+  } else {
+    for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)d.mflag[r0 + k] << (8 * k);
+  }
+  for (; fl; fl &= fl - 1) {
+  const uint32_t vi = r0 + (uint32_t)(__builtin_ctzll(fl) >> 3), v = d.lo + vi;
   // hop 1: the inbox count and its first headers together (most inboxes hold a few packets)
   const uint32_t npre = d.DI < INBOX_PREFETCH ? d.DI : INBOX_PREFETCH;
   uint4 hd = lane < npre ? d.in_hdr[(size_t)vi * d.DI + lane] : make_uint4(0u, 0u, 0u, 0u);
   const uint32_t deg = d.in_cnt[vi];
-  if (deg == 0) return;
+  if (deg == 0) continue;
   if (deg > d.DI) {
     if (lane == 0) merge_inbox_serial(d, vi);
-    return;
+    continue;
   }
   if (deg > npre && lane >= npre && lane < deg) hd = d.in_hdr[(size_t)vi * d.DI + lane];
   // sender order: rank of each header's key among the deg distinct keys
@@ -1213,6 +1238,8 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
       mark_change(d);
       atomicMin(&d.minexp[vi], mexp);
     }
+  }
+  wave_sync();
   }
 }
 
@@ -2279,6 +2306,86 @@ __global__ void k_digest(Dev d, uint64_t *out) {
   h = feed(h, (uint64_t)s.last_bcast_ns);
   h = feed(h, s.running);
   out[v] = h;
+}
+
+// ============================================== catalog readers (EachServiceSorted, ByService) ==
+// A view's present records (of one owner, or all: owner = 0xffffffff) compacted in key order: per
+// 1024-slot chunk counts, one exclusive scan, then ordered writes by wave ballots.
+#define VC_CHUNK 1024
+GXD bool vc_take(const Dev &d, uint64_t w, uint32_t r, uint32_t owner) {
+  return st_of(w) != GX_ABSENT && (owner == 0xffffffffu || owned_by(d, r, owner));
+}
+__global__ __launch_bounds__(256) void k_vc_count(Dev d, uint32_t vi, uint32_t owner, uint32_t *cnt) {
+  __shared__ uint32_t s_n;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const uint64_t *row = &d.view[(size_t)vi * d.R];
+  uint32_t n = 0;
+  for (uint32_t k = threadIdx.x; k < VC_CHUNK; k += blockDim.x) {
+    const uint32_t r = blockIdx.x * VC_CHUNK + k;
+    n += r < d.R && vc_take(d, row[r], r, owner);
+  }
+  n = (uint32_t)wave_sum(n);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&s_n, n);
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = s_n;
+}
+__global__ __launch_bounds__(1024) void k_vc_scan(uint32_t *cnt, uint32_t nb) {  // exclusive, cnt[nb] = total
+  __shared__ unsigned long long s_wave[16];
+  unsigned long long carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+    const uint32_t b = b0 + threadIdx.x;
+    const unsigned long long x = b < nb ? cnt[b] : 0;
+    unsigned long long tot;
+    const unsigned long long pre = block_excl_scan64(x, s_wave, tot);
+    if (b < nb) cnt[b] = (uint32_t)(carry + pre);
+    carry += tot;
+  }
+  if (threadIdx.x == 0) cnt[nb] = (uint32_t)carry;
+}
+__global__ __launch_bounds__(256) void k_vc_write(Dev d, uint32_t vi, uint32_t owner, const uint32_t *off,
+                                                  uint64_t *keys, uint32_t *vals) {
+  __shared__ uint32_t s_w[VC_CHUNK / 64];
+  const uint64_t *row = &d.view[(size_t)vi * d.R];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t base = off[blockIdx.x];
+  for (uint32_t k0 = 0; k0 < VC_CHUNK; k0 += blockDim.x) {
+    const uint32_t r = blockIdx.x * VC_CHUNK + k0 + threadIdx.x;
+    const uint64_t w = r < d.R ? row[r] : GX_SLOT_ABSENT;
+    const bool t = r < d.R && vc_take(d, w, r, owner);
+    const unsigned long long m = __ballot(t);
+    if (lane == 0) s_w[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (uint32_t q = 0; q < blockDim.x / 64; q++) {
+      pre += q < wv ? s_w[q] : 0;
+      tot += s_w[q];
+    }
+    if (t) {
+      const uint32_t at = base + pre + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      keys[at] = w >> GX_TS_SHIFT;  // Updated only: equal times keep key order (stable sort)
+      vals[at] = r;
+    }
+    base += tot;
+    __syncthreads();
+  }
+}
+__global__ void k_vc_rank(const uint32_t *name_rank, const uint32_t *vals, uint32_t *keys, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keys[i] = name_rank[vals[i]];
+}
+__global__ void k_vc_out(Dev d, uint32_t vi, const uint32_t *vals, uint32_t n, gx_service *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = vals[i];
+  const uint64_t w = d.view[(size_t)vi * d.R + r];
+  gx_service g;
+  g.updated_ns = ts_of(w);
+  g.host = r / d.S;
+  g.svc = (uint16_t)(r % d.S);
+  g.status = (uint8_t)st_of(w);
+  g.flags = 0;
+  out[i] = g;
 }
 
 // ========================================================= single-host ABI kernels (64 lanes) ==

@@ -330,7 +330,61 @@ static void test_change_bookkeeping() {
   So(sorted.size() == 2 && sorted[0].ID == "older");
 }
 
+// Test_ServerSorting (catalog/view_test.go:17-95) and ByService (services_state.go:738-748)
+static void test_view_sorting() {
+  const std::string h1 = "shakespeare", h2 = "chaucer", h3 = "bocaccio";
+  const std::string id1 = "deadbeef123", id2 = "deadbeef101", id3 = "deadbeef105";
+  Cluster c(params());
+  ServicesState state(c, local);
+  const int64_t base = c.Now();
+  state.AddServiceEntry(Service{id1, h1, base + 5 * SEC, sidecar::ALIVE, "web"});
+  state.AddServiceEntry(Service{id2, h2, base, sidecar::ALIVE, "db"});
+  state.AddServiceEntry(Service{id3, h3, base + 10 * SEC, sidecar::ALIVE, "web"});
+  {
+    cur = "Returns a list of Servers sorted by Name (view_test.go:36-48)";
+    auto names = state.SortedServers();
+    So(names.size() == 3 && names[0] == "bocaccio" && names[1] == "chaucer" && names[2] == "shakespeare");
+  }
+  {
+    cur = "Returns a list of Services sorted by Updates (view_test.go:50-69)";
+    ServicesState s2(c, "view2");
+    s2.AddServiceEntry(Service{id3, h3, base + 10 * SEC, sidecar::ALIVE});
+    s2.AddServiceEntry(Service{id2, h3, base, sidecar::ALIVE});
+    s2.AddServiceEntry(Service{id1, h3, base + 5 * SEC, sidecar::ALIVE});
+    auto v = s2.SortedServices(h3);
+    So(v.size() == 3 && v[0].ID == id2 && v[1].ID == id1 && v[2].ID == id3);
+  }
+  {
+    cur = "Returs a list of Services sorted on sorted Servers (view_test.go:71-91)";
+    state.AddServiceEntry(Service{id1, h3, base + 5 * SEC, sidecar::ALIVE, "web"});
+    state.AddServiceEntry(Service{id2, h3, base, sidecar::ALIVE, "db"});
+    state.AddServiceEntry(Service{id3, h3, base + 10 * SEC, sidecar::ALIVE, "web"});
+    std::vector<std::string> ids;
+    for (auto &s : state.EachServiceSorted()) ids.push_back(s.ID);
+    const std::vector<std::string> should = {id2, id2, id1, id1, id3};
+    So(ids == should);
+  }
+  {
+    cur = "ByService groups by Service.Name in EachServiceSorted order (services_state.go:738-748)";
+    auto m = state.ByService();
+    So(m.size() == 2 && m.count("db") && m.count("web"));
+    So(m["db"].size() == 2 && m["db"][0].Updated == base && m["db"][1].Updated == base);
+    So(m["web"].size() == 3 && m["web"][0].ID == id1 && m["web"][2].ID == id3);
+  }
+  {
+    cur = "A server and services first seen by gossip are created (services_state.go:310-318)";
+    ServicesState s3(c, "newcomer-view");
+    ServicesDelegate del(c, s3);
+    del.NotifyMsg({Service{"fresh-1", "brand-new-host", base, sidecar::ALIVE}, Service{"fresh-2", "brand-new-host", base + SEC, sidecar::ALIVE}});
+    So(s3.HasServer("brand-new-host"));
+    So(s3.Get("brand-new-host", "fresh-2").has_value());
+    auto v = s3.SortedServices("brand-new-host");
+    So(v.size() == 2 && v[0].ID == "fresh-1");
+  }
+}
+
 int main() {
+  test_view_sorting();
   test_services_state_with_data();
   test_tracking_and_broadcasting();
   test_cluster_membership();

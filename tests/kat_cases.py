@@ -778,4 +778,81 @@ def kat_notify_msgs_batched(lib):
     assert (ts[CH * 8 + 0], st[CH * 8 + 0]) == (T0 + SEC, DRAINING)  # the older ALIVE lost
 
 
+# ------------------------------------------------------------------------- catalog/view_test.go
+# hostname1..3 = shakespeare, chaucer, bocaccio; svcId1/2/3 = deadbeef123 / deadbeef101 / deadbeef105
+# interned as service slots 1, 0, 2 of every host (slot = the ID's rank, so key order = ID order
+# among one host's records). baseTime is a whole second.
+BOC = 3  # "bocaccio"
+ID1, ID2, ID3 = 1, 0, 2  # deadbeef123, deadbeef101, deadbeef105
+IDS = {ID1: "deadbeef123", ID2: "deadbeef101", ID3: "deadbeef105"}
+
+
+def _view_state(lib):
+    e = mk(lib)
+    e.add_service_entry(LOCAL, (SH, ID1, T0 + 5 * SEC, ALIVE))
+    e.add_service_entry(LOCAL, (CH, ID2, T0, ALIVE))
+    e.add_service_entry(LOCAL, (BOC, ID3, T0 + 10 * SEC, ALIVE))
+    return e
+
+
+def kat_view_sorted_services(lib):
+    """view_test.go:50-69 — Server.SortedServices: bocaccio's services by Updated."""
+    e = _view_state(lib)
+    e.add_service_entry(LOCAL, (BOC, ID3, T0 + 10 * SEC, ALIVE))
+    e.add_service_entry(LOCAL, (BOC, ID2, T0, ALIVE))
+    e.add_service_entry(LOCAL, (BOC, ID1, T0 + 5 * SEC, ALIVE))
+    ids = [IDS[x.svc] for x in e.each_service_sorted(LOCAL, BOC)]
+    assert ids == ["deadbeef101", "deadbeef123", "deadbeef105"]
+
+
+def kat_view_each_service_sorted(lib):
+    """view_test.go:71-91 — EachServiceSorted over every server: IDs by Updated
+    (deadbeef101 x2 at baseTime, deadbeef123 x2 at +5 s, deadbeef105 at +10 s). bocaccio's
+    deadbeef105 at the same time is not newer, so it is not added twice."""
+    e = _view_state(lib)
+    e.add_service_entry(LOCAL, (BOC, ID1, T0 + 5 * SEC, ALIVE))
+    e.add_service_entry(LOCAL, (BOC, ID2, T0, ALIVE))
+    e.add_service_entry(LOCAL, (BOC, ID3, T0 + 10 * SEC, ALIVE))
+    got = e.each_service_sorted(LOCAL)
+    assert [IDS[x.svc] for x in got] == ["deadbeef101", "deadbeef101", "deadbeef123", "deadbeef123", "deadbeef105"]
+    times = [x.updated_ns for x in got]
+    assert times == sorted(times)
+    # equal Updated: key order (Go's sort.Sort leaves it unspecified)
+    assert [(x.host, x.svc) for x in got[:2]] == [(CH, ID2), (BOC, ID2)]
+
+
+def kat_by_service_groups_by_name(lib):
+    """services_state.go:738-748 — ByService groups EachServiceSorted's services by Service.Name.
+    Names: every deadbeef123 record is "web", deadbeef101 "db", deadbeef105 "web"."""
+    e = _view_state(lib)
+    e.add_service_entry(LOCAL, (BOC, ID1, T0 + 5 * SEC, ALIVE))
+    e.add_service_entry(LOCAL, (BOC, ID2, T0, ALIVE))
+    names = []
+    for h in range(e.H):
+        for sv in range(e.S):
+            names.append({ID1: "web", ID2: "db", ID3: "web"}.get(sv, f"other{sv}"))
+    e.set_service_names(names)
+    got = e.by_service(LOCAL)
+    groups = {}
+    for g, x in got:
+        groups.setdefault(g, []).append((x.host, IDS[x.svc], x.updated_ns))
+    # groups in bytewise name order: "db" < "web"
+    assert list(groups) == sorted(groups)
+    db, web = groups[min(groups)], groups[max(groups)]
+    assert [i for _, i, _ in db] == ["deadbeef101", "deadbeef101"]
+    assert [(h, i) for h, i, _ in web] == [(SH, "deadbeef123"), (BOC, "deadbeef123"), (BOC, "deadbeef105")]
+
+
+def kat_by_service_needs_names(lib):
+    """ByService without a name table: GX_ENOENT."""
+    from sidecar_amd.abi import GxError
+    e = _view_state(lib)
+    try:
+        e.by_service(LOCAL)
+    except GxError as x:
+        assert "-2" in str(x) or "ENOENT" in str(x)
+    else:
+        raise AssertionError("expected GX_ENOENT")
+
+
 ALL = [v for k, v in sorted(globals().items()) if k.startswith("kat_")]
