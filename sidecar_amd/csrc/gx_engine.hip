@@ -230,6 +230,14 @@ static int join_side(gx_engine *e) {
   return GX_OK;
 }
 
+// The push-pull exchange stages read sizes back without waiting for the shard-local merges on
+// side_stream (they touch rows no exchange stage reads); gx_ae_merge / gx_round_end join them.
+static int sync_main(gx_engine *e) {
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipGetLastError());
+  return take_device_error(e);
+}
+
 static int sync_check(gx_engine *e) {
   int jr = join_side(e);
   if (jr) return jr;
@@ -1720,7 +1728,7 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
     uint32_t err = 0;
     HIPCHK(hipMemcpyAsync(&err, e->ae_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(sz.data(), e->ae_sz, sizeof(uint64_t) * 2 * np, hipMemcpyDeviceToHost, e->stream));
-    int rc = sync_check(e);
+    int rc = sync_main(e);
     if (rc) return rc;
     if (err) return GX_EINVAL;  // digests of another pair or another row size
   }
@@ -1768,7 +1776,7 @@ int gx_ae_return_bytes(gx_engine *e, const void *lead, uint64_t lead_bytes, uint
                                             e->ae_sz + 2 * np, nullptr, nullptr, nullptr);
   std::vector<uint64_t> rsz(np);
   HIPCHK(hipMemcpyAsync(rsz.data(), e->ae_sz + 2 * np, sizeof(uint64_t) * np, hipMemcpyDeviceToHost, e->stream));
-  int rc = sync_check(e);
+  int rc = sync_main(e);
   if (rc) return rc;
   std::vector<uint64_t> off(2 * (size_t)np);  // message offsets, size-table entry offsets
   uint64_t o = 0;
