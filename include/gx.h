@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 4
+#define GX_ABI_VERSION 5
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -53,11 +53,32 @@ extern "C" {
 #define GX_DRAINING 4
 #define GX_ABSENT 7
 
-/* A view slot is one packed 64-bit word: (updated_ns << 3) | status.
- * updated_ns must lie in [0, 2^61) (1970 .. 2043). The empty slot is the word GX_SLOT_ABSENT. */
+/* A view slot is one packed 64-bit word: ((updated_ns - epoch) << 3) | status, the time relative
+ * to the engine epoch (gx_epoch) in [0, 2^61). The epoch centres the 73-year window on t0_ns:
+ * epoch = t0_ns - 2^60 rounded down to a whole second, or 0 when t0_ns < 2^60 (the window is then
+ * 1970 .. 2043). With t0 in November 2023 the window is May 1987 .. May 2060. Times are clamped
+ * into the window where records enter (gx_service inputs, Decode): a time before it stores as
+ * the window's start, which IsStale drops for every lifespan (the reference drops such records
+ * too: a pre-1970 or zero time.Time Updated is stale); a time after it stores as the window's
+ * end, which still wins every merge, as the reference's far-future record does, and reads back
+ * as that end. Every gx_service, event and server time handed out is absolute (epoch added back;
+ * a server time or state.LastChanged never set reads 0, the reference's time.Unix(0, 0)); the
+ * packed words of gx_read_views, gx_read_job and the sharded wire formats are epoch-relative
+ * (the shards of a cluster share t0_ns, so its epoch). The empty slot is GX_SLOT_ABSENT. */
 #define GX_TS_SHIFT 3
 #define GX_SLOT_ABSENT ((uint64_t)GX_ABSENT)
 #define GX_TS_LIMIT ((int64_t)1 << 61)
+#define GX_SEC_NS 1000000000ll
+static inline int64_t gx_epoch_of(int64_t t0_ns) {
+  const int64_t half = (int64_t)1 << 60;
+  return t0_ns < half ? 0 : (t0_ns - half) / GX_SEC_NS * GX_SEC_NS;
+}
+/* absolute Unix ns -> epoch-relative slot time, clamped to [0, 2^61) */
+static inline int64_t gx_ts_in(int64_t abs_ns, int64_t epoch) {
+  if (abs_ns <= epoch) return 0;
+  const int64_t d = abs_ns - epoch; /* epoch >= 0: no overflow */
+  return d >= GX_TS_LIMIT ? GX_TS_LIMIT - 1 : d;
+}
 
 /* Record across the ABI: the fields of service.Service (service/service.go:32-42) that the
  * merge path reads. Hostname and ID strings are interned to (host, svc) indices by the caller;
@@ -114,7 +135,7 @@ typedef struct gx_params {
   uint32_t ae_period_rounds;          /* anti-entropy push-pull period, 0 = off */
   uint32_t ae_phase;                  /* AE rounds are those with round % period == phase */
   uint32_t init_mode;                 /* GX_INIT_* */
-  int64_t t0_ns;                      /* simulated clock at round 0 */
+  int64_t t0_ns;                      /* simulated clock at round 0, Unix ns in [0, 2^62] */
   int64_t round_ns;                   /* GossipInterval 200ms (config/config.go:47) */
   int64_t alive_lifespan_ns;          /* ALIVE_LIFESPAN 80s (:32) */
   int64_t draining_lifespan_ns;       /* DRAINING_LIFESPAN 10min (:33) */
@@ -155,7 +176,7 @@ typedef struct gx_params {
   uint32_t fd_msg_cap;             /* memberlist messages per gossip packet, 1..64 */
   uint32_t fd_msg_bytes;           /* byte mode: encoded length of one memberlist message */
   uint32_t fd_gossip_dead_rounds;  /* GossipToTheDeadTime 30 s = 150 rounds */
-  uint32_t fd_suspicion_k;         /* SuspicionMult - 2 confirmations (0 when n - 2 < k), <= 7 */
+  uint32_t fd_suspicion_k;         /* SuspicionMult - 2 confirmations (0 when n - 2 < k), <= 2 */
   uint32_t fd_suspicion_rounds[8]; /* suspicion timeout after c confirmations, c = 0..k */
   /* Host departures (crash): from depart_round on, a seeded depart_ppm fraction of the hosts
    * stops every activity and drops every packet sent to it (both models). -1 = none. */
@@ -271,6 +292,7 @@ int gx_create(const gx_params *p, gx_engine **out);
 int gx_destroy(gx_engine *e);
 int gx_set_round(gx_engine *e, int64_t round); /* advance the clock; wakes due sleepers */
 int gx_get_round(gx_engine *e, int64_t *round);
+int gx_epoch(gx_engine *e, int64_t *epoch_ns); /* gx_epoch_of(t0_ns): packed words' time origin */
 int gx_enable_timing(gx_engine *e, int on);
 /* Where this engine's device work goes. mode 0: its own stream. GX_STREAM_CALLER: the caller's
  * HIP stream `stream` (NULL = the default stream), e.g. the stream an exchange layer runs its
@@ -510,10 +532,11 @@ int gx_listener_drain(gx_engine *e, uint32_t view, uint32_t id, gx_change_event 
  * or service (the reference panics in Merge), a repeated key inside the Servers map or one
  * Services map, two records with the same (Hostname, ID), nesting deeper than GX_JSON_MAX_DEPTH.
  * Records whose Hostname/ID are not in the names table are skipped and counted (`unknown`; the
- * reference would create them, the engine's key space is fixed). Status outside 0..6 or Updated
- * at or after 2^61 ns are skipped and counted (`invalid`). Updated before 1970 merges as
- * time 0, which IsStale drops exactly like the original time. The decoded records are merged in
- * key order (the model's Merge order), as anti-entropy merges. */
+ * reference would create them, the engine's key space is fixed). Status outside 0..6 is skipped
+ * and counted (`invalid`). Updated is clamped into the engine's time window (GX_TS_SHIFT above):
+ * a pre-1970, zero or otherwise pre-window time merges as the window's start, which IsStale drops
+ * exactly like the original time; a time past the window merges as its end. The decoded records
+ * are merged in key order (the model's Merge order), as anti-entropy merges. */
 #define GX_JSON_MAX_DEPTH 16
 typedef struct gx_names {
   const char *cluster_name;
@@ -533,7 +556,7 @@ typedef struct gx_decode_stats {
   uint32_t services; /* Service objects under the winning Servers / Services members */
   uint32_t records;  /* records decoded (merged, for the merge call) */
   uint32_t unknown;  /* Hostname/ID not in the names table */
-  uint32_t invalid;  /* Status outside 0..6 or Updated >= 2^61 ns */
+  uint32_t invalid;  /* Status outside 0..6 */
   int64_t error_at;  /* byte offset of the first error found, -1 = none (diagnostic only) */
 } gx_decode_stats;
 int gx_set_names(gx_engine *e, const gx_names *names);
@@ -633,7 +656,7 @@ int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree);
 
 /* ---- read-back, import, parity ------------------------------------------------------------ */
 int gx_read_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, uint64_t *out_words);
-/* One view unpacked (SURVEY.md §8b gx_read_view): ts_ns[R] (INT64_MIN where the slot is empty)
+/* One view unpacked (SURVEY.md §8b gx_read_view): ts_ns[R] absolute Updated (INT64_MIN where empty)
  * and status[R] (GX_ABSENT where empty), R = n_hosts * n_services. */
 int gx_read_view(gx_engine *e, uint32_t view, int64_t *ts_ns, uint8_t *status);
 int gx_write_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, const uint64_t *words);

@@ -53,6 +53,7 @@ struct gx_engine {
   uint64_t x_total, x_lin, x_rtotal;
   int64_t x_round, x_delta_round, x_ret_round;
   int64_t round;
+  int64_t epoch;        /* absolute time of slot time 0 (gx.h GX_TS_SHIFT); p.t0_ns is epoch-relative */
   uint64_t *view;       /* H * R packed slots */
   uint8_t *own_status;  /* H * S local service status (discovery/health) */
   gx_host_state *hs;    /* H */
@@ -107,6 +108,10 @@ static inline int st_of(uint64_t w) { return (int)(w & 7u); }
 static inline int64_t ts_of(uint64_t w) { return (int64_t)(w >> GX_TS_SHIFT); }
 static inline uint64_t pack(int64_t ts, int st) { return ((uint64_t)ts << GX_TS_SHIFT) | (uint64_t)st; }
 static inline int64_t now_of(const gx_engine *e) { return e->p.t0_ns + e->round * e->p.round_ns; }
+/* slot time -> absolute: records; server times and state.LastChanged (0 = never set, which the
+ * reference holds as time.Unix(0, 0), services_state.go:62-63,95) */
+static inline int64_t abs_ts(const gx_engine *e, int64_t t) { return t + e->epoch; }
+static inline int64_t abs_tm(const gx_engine *e, int64_t t) { return t ? t + e->epoch : 0; }
 static inline uint32_t meta_of(int kind, uint32_t pass, uint32_t np) {
   return (uint32_t)kind | (pass << 8) | (np << 16);
 }
@@ -391,11 +396,11 @@ static void notify_listeners(gx_engine *e, uint32_t v, uint32_t r, uint64_t nw, 
     }
     gx_change_event *ev = &l->ring[(l->head + l->count) % l->cap];
     memset(ev, 0, sizeof *ev);
-    ev->service.updated_ns = ts_of(nw);
+    ev->service.updated_ns = abs_ts(e, ts_of(nw));
     ev->service.host = r / e->S;
     ev->service.svc = (uint16_t)(r % e->S);
     ev->service.status = (uint8_t)st_of(nw);
-    ev->time_ns = e->vlc[v];
+    ev->time_ns = abs_tm(e, e->vlc[v]);
     ev->previous_status = (uint32_t)prev;
     l->count++;
   }
@@ -1165,7 +1170,14 @@ static int check_params(const gx_params *p) {
   if (p->retransmit_rounds > 1000) return GX_EINVAL;
   if (p->alive_count < 1 || p->alive_count > 255 || p->tombstone_count < 1 || p->tombstone_count > 255) return GX_EINVAL;
   if (p->init_mode > GX_INIT_WARM) return GX_EINVAL;
-  if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
+  if (p->t0_ns < 0 || p->t0_ns > ((int64_t)1 << 62) || p->round_ns <= 0) return GX_EINVAL;
+  { /* lifespans stay far inside the half window before t0 (gx.h GX_TS_SHIFT) */
+    const int64_t lim = (int64_t)1 << 58;
+    if (p->alive_lifespan_ns < 0 || p->alive_lifespan_ns > lim || p->draining_lifespan_ns < 0 ||
+        p->draining_lifespan_ns > lim || p->tombstone_lifespan_ns < 0 || p->tombstone_lifespan_ns > lim ||
+        p->stale_fudge_ns < 0 || p->stale_fudge_ns > lim || p->aged_max_ns < 0 || p->aged_max_ns > lim)
+      return GX_EINVAL;
+  }
   if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
@@ -1234,6 +1246,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   gx_engine *e = (gx_engine *)calloc(1, sizeof(gx_engine));
   if (!e) return GX_ENOMEM;
   e->p = *p;
+  e->epoch = gx_epoch_of(p->t0_ns);
+  e->p.t0_ns -= e->epoch; /* every internal time is epoch-relative */
   e->H = p->n_hosts;
   e->S = p->n_services;
   e->R = p->n_hosts * p->n_services;
@@ -1369,6 +1383,11 @@ int gx_get_round(gx_engine *e, int64_t *round) {
   *round = e->round;
   return GX_OK;
 }
+int gx_epoch(gx_engine *e, int64_t *epoch_ns) {
+  if (!e || !epoch_ns) return GX_EINVAL;
+  *epoch_ns = e->epoch;
+  return GX_OK;
+}
 int gx_enable_timing(gx_engine *e, int on) {
   (void)on;
   return e ? GX_OK : GX_EINVAL;
@@ -1381,15 +1400,14 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
 }
 
 static int to_grec(const gx_engine *e, const gx_service *s, grec *g) {
-  if (s->host >= e->H || s->svc >= e->S || s->status > 6 || s->updated_ns < 0 || s->updated_ns >= GX_TS_LIMIT)
-    return GX_EINVAL;
-  g->w = pack(s->updated_ns, s->status);
+  if (s->host >= e->H || s->svc >= e->S || s->status > 6) return GX_EINVAL;
+  g->w = pack(gx_ts_in(s->updated_ns, e->epoch), s->status);
   g->r = s->host * e->S + s->svc;
   g->pad = 0;
   return GX_OK;
 }
 static void to_svc(const gx_engine *e, const grec *g, gx_service *s) {
-  s->updated_ns = ts_of(g->w);
+  s->updated_ns = abs_ts(e, ts_of(g->w));
   s->host = g->r / e->S;
   s->svc = (uint16_t)(g->r % e->S);
   s->status = (uint8_t)st_of(g->w);
@@ -1679,12 +1697,16 @@ int gx_by_service(gx_engine *e, uint32_t view, gx_service *out, uint32_t *group_
 
 int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, gx_server_times *out) {
   if (!e || view >= e->H || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
-  memcpy(out, &e->srvt[(size_t)view * e->H + lo], sizeof(gx_server_times) * (hi - lo));
+  for (uint32_t o = lo; o < hi; o++) {
+    const gx_server_times *t = &e->srvt[(size_t)view * e->H + o];
+    out[o - lo].last_updated_ns = abs_tm(e, t->last_updated_ns);
+    out[o - lo].last_changed_ns = abs_tm(e, t->last_changed_ns);
+  }
   return GX_OK;
 }
 int gx_read_last_changed(gx_engine *e, uint32_t lo, uint32_t hi, int64_t *out) {
   if (!e || lo > hi || hi > e->H || (hi > lo && !out)) return GX_EINVAL;
-  memcpy(out, &e->vlc[lo], sizeof(int64_t) * (hi - lo));
+  for (uint32_t v = lo; v < hi; v++) out[v - lo] = abs_tm(e, e->vlc[v]);
   return GX_OK;
 }
 static struct olistener *find_listener(gx_engine *e, uint32_t view, uint32_t id) {
@@ -1756,7 +1778,7 @@ int gx_read_view(gx_engine *e, uint32_t view, int64_t *ts_ns, uint8_t *status) {
   int rc = gx_read_views(e, view, view + 1, w);
   for (size_t r = 0; rc == GX_OK && r < R; r++) {
     status[r] = (uint8_t)(w[r] & 7u);
-    ts_ns[r] = status[r] == GX_ABSENT ? INT64_MIN : (int64_t)(w[r] >> 3);
+    ts_ns[r] = status[r] == GX_ABSENT ? INT64_MIN : (int64_t)(w[r] >> 3) + e->epoch;
   }
   free(w);
   return rc;

@@ -336,20 +336,20 @@ int gx_local_state_json(gx_engine *e, uint32_t view, char *out, uint64_t cap, ui
       sb_put(&b, nm->eid.p + nm->eid_off[r], nm->eid_off[r + 1] - nm->eid_off[r]);
       sb_putc(&b, ':');
       sb_put(&b, nm->pre + nm->pre_off[r], nm->pre_off[r + 1] - nm->pre_off[r]);
-      json_time(&b, ts_of(w));
+      json_time(&b, abs_ts(e, ts_of(w)));
       sb_put(&b, nm->post + nm->post_off[r], nm->post_off[r + 1] - nm->post_off[r]);
       sb_putc(&b, (char)('0' + st_of(w)));
       sb_putc(&b, '}');
     }
     const gx_server_times *st = &e->srvt[(size_t)view * e->H + o];
     sb_puts(&b, "},\"LastUpdated\":");
-    json_time(&b, st->last_updated_ns);
+    json_time(&b, abs_tm(e, st->last_updated_ns));
     sb_puts(&b, ",\"LastChanged\":");
-    json_time(&b, st->last_changed_ns);
+    json_time(&b, abs_tm(e, st->last_changed_ns));
     sb_putc(&b, '}');
   }
   sb_puts(&b, "},\"LastChanged\":");
-  json_time(&b, e->vlc[view]);
+  json_time(&b, abs_tm(e, e->vlc[view]));
   sb_puts(&b, ",\"ClusterName\":");
   sb_put(&b, nm->ecluster.p, nm->ecluster.n);
   sb_puts(&b, ",\"Hostname\":");
@@ -669,8 +669,19 @@ static int dup_keys(const jdoc *d, const jnode *m) {
   return rc;
 }
 
+/* Updated (Unix seconds + ns) -> slot time, clamped into the engine's window like gx_ts_in
+ * (gx.h GX_TS_SHIFT): before it (pre-1970, zero time.Time) -> 0, stale for every lifespan; past
+ * it -> the window's end. The epoch is a whole number of seconds. */
+static int64_t slot_time(const gx_engine *e, int64_t sec, int64_t nsec) {
+  const int64_t es = e->epoch / GX_SEC_NS;
+  if (sec < es) return 0;
+  if (sec - es > GX_TS_LIMIT / GX_SEC_NS) return GX_TS_LIMIT - 1;
+  const int64_t t = (sec - es) * GX_SEC_NS + nsec;
+  return t >= GX_TS_LIMIT ? GX_TS_LIMIT - 1 : t;
+}
+
 typedef struct jrec {
-  int64_t ns;     /* Updated, ns since the epoch (clamped to 0 below) */
+  int64_t ns;     /* Updated as a slot time (slot_time) */
   uint32_t r;     /* record key */
   uint32_t st;
   uint64_t doc;   /* document order */
@@ -810,11 +821,8 @@ static int j_decode(const gx_engine *e, jdoc *d, jout *out) {
       int64_t sec = -62135596800ll, nsec = 0, stv = 0; /* zero time.Time, zero Status */
       if (un && un->type == JT_STR) parse_rfc3339(d->s + un->a, un->b - un->a, &sec, &nsec);
       if (stn && stn->type == JT_NUM) int_value(d, stn, &stv);
-      int64_t ns;
-      int bad = stv < 0 || stv > 6;
-      if (sec < 0) ns = 0; /* before 1970: merges as time 0, stale either way */
-      else if (sec > GX_TS_LIMIT / 1000000000ll || sec * 1000000000ll + nsec >= GX_TS_LIMIT) { bad = 1; ns = 0; }
-      else ns = sec * 1000000000ll + nsec;
+      const int bad = stv < 0 || stv > 6;
+      const int64_t ns = slot_time(e, sec, nsec);
       if (bad) {
         out->invalid++;
         continue;
@@ -876,7 +884,7 @@ int gx_decode_state_json(gx_engine *e, const char *buf, uint64_t len, gx_service
   int rc = j_run(e, buf, len, &o, ds);
   if (rc == GX_OK) {
     for (size_t i = 0; i < o.n && i < cap; i++) {
-      out[i].updated_ns = o.v[i].ns;
+      out[i].updated_ns = abs_ts(e, o.v[i].ns);
       out[i].host = o.v[i].r / e->S;
       out[i].svc = (uint16_t)(o.v[i].r % e->S);
       out[i].status = (uint8_t)o.v[i].st;

@@ -188,7 +188,7 @@ class GxDecodeStats(C.Structure):
 
 ABI_FUNCS = [
     "gx_abi_version", "gx_backend", "gx_params_default", "gx_create", "gx_destroy", "gx_set_round",
-    "gx_get_round", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
+    "gx_get_round", "gx_epoch", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
     "gx_tombstone_others", "gx_tombstone_services", "gx_expire_server", "gx_send_services",
     "gx_broadcast_services", "gx_broadcast_tombstones", "gx_is_new_service", "gx_notify_msg", "gx_notify_msgs", "gx_read_view",
     "gx_get_broadcasts", "gx_local_state", "gx_merge_remote_state", "gx_notify_leave",
@@ -214,7 +214,7 @@ def _declare(lib):
         "gx_abi_version": ([], i32), "gx_backend": ([], C.c_char_p),
         "gx_params_default": ([P(GxParams)], None), "gx_create": ([P(GxParams), P(vp)], i32),
         "gx_destroy": ([vp], i32), "gx_set_round": ([vp, i64], i32),
-        "gx_get_round": ([vp, P(i64)], i32), "gx_enable_timing": ([vp, i32], i32),
+        "gx_get_round": ([vp, P(i64)], i32), "gx_epoch": ([vp, P(i64)], i32), "gx_enable_timing": ([vp, i32], i32),
         "gx_run_rounds": ([vp, u32], i32),
         "gx_add_service_entries": ([vp, P(u32), P(GxService), u32, P(u32)], i32),
         "gx_merge": ([vp, u32, u32], i32),
@@ -393,6 +393,19 @@ class Engine:
         r = C.c_int64()
         check(self.lib.gx_get_round(self.h, C.byref(r)))
         return r.value
+
+    @property
+    def epoch(self) -> int:
+        """Absolute time of slot time 0: view words hold (updated_ns - epoch) << 3 (gx.h GX_TS_SHIFT)."""
+        if not hasattr(self, "_epoch"):
+            x = C.c_int64()
+            check(self.lib.gx_epoch(self.h, C.byref(x)), "gx_epoch")
+            self._epoch = x.value
+        return self._epoch
+
+    def word_time(self, w: int) -> int:
+        """Absolute Updated of a packed view word."""
+        return (int(w) >> TS_SHIFT) + self.epoch
 
     def now(self, round_=None) -> int:
         r = self.round if round_ is None else round_
@@ -579,7 +592,7 @@ class Engine:
         w = int(row[host * self.S + s])
         if w & 7 == ABSENT:
             return None
-        return (w >> TS_SHIFT, w & 7)
+        return (self.word_time(w), w & 7)
 
     def hosts(self, lo=None, hi=None):
         lo = self.lo if lo is None else lo

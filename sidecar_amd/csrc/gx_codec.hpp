@@ -118,6 +118,8 @@ GXHD uint32_t fmt_time(int64_t ns, char *t) {
   t[k++] = '"';
   return k;
 }
+// The length depends on the fraction only, so slot times (epoch-relative, the epoch a whole
+// number of seconds) and absolute times have the same length.
 GXHD uint32_t time_len(int64_t ns) {
   int64_t frac = ns % 1000000000ll;
   if (!frac) return 22;
@@ -315,6 +317,18 @@ __global__ __launch_bounds__(256) void k_enc_len(Dev d, Names nm, uint32_t vi, u
 // dword stores (bytes only at the two ends). A server larger than the buffer is written by the
 // same steps straight to the output.
 #define ENC_LDS 12288
+// server times and state.LastChanged: slot time -> absolute, 0 = never set (time.Unix(0, 0))
+GXD int64_t abs_tm(const Dev &d, int64_t t) { return t ? t + d.epoch : 0; }
+// Updated (Unix seconds + ns) -> slot time, clamped into the window like gx_ts_in (gx.h
+// GX_TS_SHIFT): before it (pre-1970, zero time.Time) -> 0, stale for every lifespan; past it ->
+// the window's end. The epoch is a whole number of seconds. (gx_oracle_json.c slot_time)
+GXD int64_t slot_time(int64_t epoch, int64_t sec, int64_t nsec) {
+  const int64_t es = epoch / GX_SEC_NS;
+  if (sec < es) return 0;
+  if (sec - es > GX_TS_LIMIT / GX_SEC_NS) return GX_TS_LIMIT - 1;
+  const int64_t t = (sec - es) * GX_SEC_NS + nsec;
+  return t >= GX_TS_LIMIT ? GX_TS_LIMIT - 1 : t;
+}
 GXD void put_bytes(char *dst, const char *src, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) dst[i] = src[i];
 }
@@ -376,7 +390,7 @@ __global__ __launch_bounds__(256) void k_enc_write(Dev d, Names nm, uint32_t vi,
     char *q = ent + (inc - len);
     q[kn] = ':';
     q += kn + 1 + pn;
-    q += fmt_time(ts_of(w), q) + qn;
+    q += fmt_time(ts_of(w) + d.epoch, q) + qn;
     q[0] = (char)('0' + st_of(w));
     q[1] = '}';
     if (pall >> (lane + 1)) q[2] = ',';  // not the last entry; the footer follows the last one
@@ -389,10 +403,10 @@ __global__ __launch_bounds__(256) void k_enc_write(Dev d, Names nm, uint32_t vi,
     const gx_server_times st = d.srvt[(size_t)vi * d.H + o];
     put_bytes(f, L_LU, LLEN(L_LU));
     f += LLEN(L_LU);
-    f += fmt_time(st.last_updated_ns, f);
+    f += fmt_time(abs_tm(d, st.last_updated_ns), f);
     put_bytes(f, L_LC, LLEN(L_LC));
     f += LLEN(L_LC);
-    f += fmt_time(st.last_changed_ns, f);
+    f += fmt_time(abs_tm(d, st.last_changed_ns), f);
     f[0] = '}';
     if (srv_off[k] + srv_len[k] != srv_off[d.H]) f[1] = ',';
   }
@@ -420,7 +434,7 @@ __global__ void k_enc_frame(Dev d, Names nm, uint32_t vi, const uint32_t *srv_of
   wcopy(p, L_TLC, LLEN(L_TLC), lane);
   p += LLEN(L_TLC);
   uint32_t tn = time_len(d.vlc[vi]);
-  if (lane == 0) fmt_time(d.vlc[vi], p);
+  if (lane == 0) fmt_time(abs_tm(d, d.vlc[vi]), p);
   p += tn;
   wcopy(p, L_CN, LLEN(L_CN), lane);
   p += LLEN(L_CN);
@@ -440,6 +454,7 @@ GXHD uint64_t enc_frame_len(const Names &nm, int64_t vlc, uint32_t v_ehn) {
 
 // ----------------------------------------------------------------------------- decoder --
 struct Dec {
+  int64_t epoch;     // the engine's (slot time 0)
   const uint8_t *s;  // input
   uint32_t n;        // input bytes
   uint32_t nc;       // chunks
@@ -1262,13 +1277,9 @@ __global__ __launch_bounds__(256) void k_dec_svc(Dec x, Names nm, uint32_t H, ui
     int64_t sec = -62135596800ll, nsec = 0, st = 0;  // zero time.Time, zero Status
     if (vu != GXC_NONE && x.tkind[vu] == T_STR) time_ok(x, vu, sec, nsec);
     if (vs != GXC_NONE && x.tkind[vs] == T_SCL && x.tflag[vs] == SC_INT) int_value(x, vs, st);
-    int64_t ns = 0;
-    bool bad = st < 0 || st > 6;
-    if (sec < 0) ns = 0;  // before 1970: merges as time 0, which IsStale drops like the original
-    else if (sec > GX_TS_LIMIT / 1000000000ll || sec * 1000000000ll + nsec >= GX_TS_LIMIT) bad = true;
-    else ns = sec * 1000000000ll + nsec;
+    const bool bad = st < 0 || st > 6;
     flag = bad ? 3 : 1;
-    g.w = pack(ns, (int)st);
+    g.w = pack(slot_time(x.epoch, sec, nsec), (int)st);
     g.r = r;
   }
   x.rtmp[i] = g;

@@ -255,6 +255,7 @@ static int dec_impl(gx_engine *e, const char *buf, uint64_t len, gx_decode_stats
   int rc = dbuf(c->in, len + 64, &inp);
   if (rc) return rc;
   x.s = (const uint8_t *)inp;
+  x.epoch = e->d.epoch;
   // phase 1: chunk summaries and scans
   const size_t sc1 = mscan_scratch<gxc::MMap, 16>(nc + 1) + mscan_scratch<gxc::MTD, 8>(nc + 1) +
                      mscan_scratch<gxc::MLO, 1>(nc + 1);

@@ -57,7 +57,8 @@ enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS =
        ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11 };
 
 struct Dev {
-  gx_params p;
+  gx_params p;      // t0_ns epoch-relative (gx.h GX_TS_SHIFT)
+  int64_t epoch;    // absolute time of slot time 0
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
   uint32_t NG, KE;           // GossipMessages gathers per target; packet entries per host = K * NG
   uint32_t lo, Hl, G, gid;  // this engine owns hosts [lo, lo + Hl); per-host arrays are local

@@ -142,6 +142,9 @@ static bool own(const gx_engine *e, uint32_t v) { return v >= e->d.lo && v < e->
 // push-pull also merges memberlist state (mergeState)
 static bool pp_state(const Dev &d) { return d.p.fd_enable && d.p.fd_push_pull_state; }
 static int64_t now_of(const gx_engine *e) { return e->d.p.t0_ns + e->d.round * e->d.p.round_ns; }
+// slot time -> absolute for server times and state.LastChanged: 0 = never set (time.Unix(0, 0),
+// services_state.go:62-63,95)
+static int64_t abs_tm(const gx_engine *e, int64_t t) { return t ? t + e->d.epoch : 0; }
 static void set_round_fields(gx_engine *e) {
   e->d.now = now_of(e);
   e->d.partitioned = e->d.round >= e->d.p.partition_start && e->d.round < e->d.p.partition_end;
@@ -199,6 +202,10 @@ static int deliver_events(gx_engine *e) {
     uint32_t n = cnt[k] < e->d.ev_cap ? cnt[k] : e->d.ev_cap;
     std::vector<gx_change_event> ev(n);
     HIPCHK(hipMemcpy(ev.data(), &e->d.ev_log[k * e->d.ev_cap], sizeof(gx_change_event) * n, hipMemcpyDeviceToHost));
+    for (auto &x : ev) {
+      x.service.updated_ns += e->d.epoch;
+      x.time_ns = abs_tm(e, x.time_ns);
+    }
     for (auto &l : e->listeners) {
       if (l.view != e->log_views[k]) continue;
       uint32_t room = l.cap - (uint32_t)l.ring.size();
@@ -555,7 +562,13 @@ static int check_params(const gx_params *p) {
   if (p->retransmit_rounds > 1000) return GX_EINVAL;
   if (p->alive_count < 1 || p->alive_count > 255 || p->tombstone_count < 1 || p->tombstone_count > 255) return GX_EINVAL;
   if (p->init_mode > GX_INIT_WARM) return GX_EINVAL;
-  if (p->t0_ns < 0 || p->t0_ns >= GX_TS_LIMIT - ((int64_t)1 << 56) || p->round_ns <= 0) return GX_EINVAL;
+  if (p->t0_ns < 0 || p->t0_ns > ((int64_t)1 << 62) || p->round_ns <= 0) return GX_EINVAL;
+  {  // lifespans stay far inside the half window before t0 (gx.h GX_TS_SHIFT)
+    const int64_t lim = (int64_t)1 << 58;
+    for (int64_t x : {p->alive_lifespan_ns, p->draining_lifespan_ns, p->tombstone_lifespan_ns, p->stale_fudge_ns,
+                      p->aged_max_ns})
+      if (x < 0 || x > lim) return GX_EINVAL;
+  }
   if ((uint64_t)p->n_hosts * p->n_services > 0xffffffffull) return GX_EINVAL;
   if (p->ae_period_rounds && p->ae_phase >= p->ae_period_rounds) return GX_EINVAL;
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
@@ -657,6 +670,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->name_rank = nullptr;
   Dev &d = e->d;
   d.p = *p;
+  d.epoch = gx_epoch_of(p->t0_ns);
+  d.p.t0_ns -= d.epoch;  // every device time is epoch-relative
   d.H = p->n_hosts;
   d.S = p->n_services;
   d.R = p->n_hosts * p->n_services;
@@ -840,15 +855,14 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
 
 // ---------------------------------------------------------------------- record helpers --
 static int to_grec(const gx_engine *e, const gx_service *s, grec *g) {
-  if (s->host >= e->d.H || s->svc >= e->d.S || s->status > 6 || s->updated_ns < 0 || s->updated_ns >= GX_TS_LIMIT)
-    return GX_EINVAL;
-  g->w = pack(s->updated_ns, s->status);
+  if (s->host >= e->d.H || s->svc >= e->d.S || s->status > 6) return GX_EINVAL;
+  g->w = pack(gx_ts_in(s->updated_ns, e->d.epoch), s->status);
   g->r = s->host * e->d.S + s->svc;
   g->pad = 0;
   return GX_OK;
 }
 static void to_svc(const gx_engine *e, const grec *g, gx_service *s) {
-  s->updated_ns = ts_of(g->w);
+  s->updated_ns = ts_of(g->w) + e->d.epoch;
   s->host = g->r / e->d.S;
   s->svc = (uint16_t)(g->r % e->d.S);
   s->status = (uint8_t)st_of(g->w);
@@ -1251,6 +1265,12 @@ int gx_by_service(gx_engine *e, uint32_t view, gx_service *out, uint32_t *group_
   return sorted_view(e, view, GX_ALL_OWNERS, true, out, group_out, cap, n_out);
 }
 
+int gx_epoch(gx_engine *e, int64_t *epoch_ns) {
+  if (!e || !epoch_ns) return GX_EINVAL;
+  *epoch_ns = e->d.epoch;
+  return GX_OK;
+}
+
 int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, gx_server_times *out) {
   if (!e || !own(e, view) || lo > hi || hi > e->d.H || (hi > lo && !out)) return GX_EINVAL;
   if (hi == lo) return GX_OK;
@@ -1258,6 +1278,10 @@ int gx_read_server_times(gx_engine *e, uint32_t view, uint32_t lo, uint32_t hi, 
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(out, &e->d.srvt[(size_t)(view - e->d.lo) * e->d.H + lo], sizeof(gx_server_times) * (hi - lo),
                    hipMemcpyDeviceToHost));
+  for (uint32_t o = 0; o < hi - lo; o++) {
+    out[o].last_updated_ns = abs_tm(e, out[o].last_updated_ns);
+    out[o].last_changed_ns = abs_tm(e, out[o].last_changed_ns);
+  }
   return GX_OK;
 }
 
@@ -1267,6 +1291,7 @@ int gx_read_last_changed(gx_engine *e, uint32_t lo, uint32_t hi, int64_t *out) {
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(out, &e->d.vlc[lo - e->d.lo], sizeof(int64_t) * (hi - lo), hipMemcpyDeviceToHost));
+  for (uint32_t v = 0; v < hi - lo; v++) out[v] = abs_tm(e, out[v]);
   return GX_OK;
 }
 
@@ -1380,7 +1405,7 @@ int gx_read_view(gx_engine *e, uint32_t view, int64_t *ts_ns, uint8_t *status) {
   int rc = gx_read_views(e, view, view + 1, w);
   for (size_t r = 0; rc == GX_OK && r < R; r++) {
     status[r] = (uint8_t)(w[r] & 7u);
-    ts_ns[r] = status[r] == GX_ABSENT ? INT64_MIN : (int64_t)(w[r] >> 3);
+    ts_ns[r] = status[r] == GX_ABSENT ? INT64_MIN : (int64_t)(w[r] >> 3) + e->d.epoch;
   }
   free(w);
   return rc;

@@ -2380,7 +2380,7 @@ __global__ void k_vc_out(Dev d, uint32_t vi, const uint32_t *vals, uint32_t n, g
   const uint32_t r = vals[i];
   const uint64_t w = d.view[(size_t)vi * d.R + r];
   gx_service g;
-  g.updated_ns = ts_of(w);
+  g.updated_ns = ts_of(w) + d.epoch;
   g.host = r / d.S;
   g.svc = (uint16_t)(r % d.S);
   g.status = (uint8_t)st_of(w);

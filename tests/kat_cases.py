@@ -614,12 +614,14 @@ def kat_message_bytes_rfc3339nano(lib):
     e = mk(lib)
     e.set_static_bytes(0, e.H, [0] * (e.H * e.S))
     ts = [T0, T0 + 1, T0 + 10, T0 + 50, T0 + 100, T0 + 120_000_000, T0 + 999_999_999, T0 + SEC,
-          _T46, _T32, _T46 + 50, _T46 + 4 * 50, 0, 1, 86_399 * SEC + 500_000_000, 2**60 + 12345,
-          T0 - 3 * HOUR - MIN, T0 + 1_000_000]
+          _T46, _T32, _T46 + 50, _T46 + 4 * 50, T0 - 3 * HOUR - MIN, T0 + 1_000_000]
+    # across the engine's whole time window (gx.h GX_TS_SHIFT; the epoch is whole seconds)
+    E = e.epoch
+    ts += [E + 1, E + 86_399 * SEC + 500_000_000, E + 2**60 + 12345, E + 2**61 - 1]
     import random as _r
     rnd = _r.Random(7)
-    ts += [rnd.randrange(0, 2**61) for _ in range(200)]
-    ts += [rnd.randrange(0, 2**50) * 10 ** rnd.randrange(0, 10) % 2**61 for _ in range(200)]
+    ts += [E + rnd.randrange(1, 2**61) for _ in range(200)]
+    ts += [E + 1 + (rnd.randrange(0, 2**50) * 10 ** rnd.randrange(0, 10) % (2**61 - 1)) for _ in range(200)]
     st = [ALIVE, TOMBSTONE, UNHEALTHY, UNKNOWN, DRAINING]
     recs = [(i % e.H, i % e.S, t, st[i % 5]) for i, t in enumerate(ts)]
     want = [len('"' + go_rfc3339nano(t) + '"') + len(str(s_)) for (_, _, t, s_) in recs]
@@ -853,6 +855,95 @@ def kat_by_service_needs_names(lib):
         assert "-2" in str(x) or "ENOENT" in str(x)
     else:
         raise AssertionError("expected GX_ENOENT")
+
+
+# ---------------------------------------------------- the engine's time window (gx.h GX_TS_SHIFT)
+# The packed slot keeps Updated relative to the engine epoch (t0 - 2^60, whole seconds): with t0
+# in November 2023 the 73-year window runs May 1987 .. May 2060. Records from both sides of 2043
+# (the old 2^61 ns horizon) merge exactly; times outside the window clamp to its ends.
+Y2050 = 2_524_608_000 * SEC  # 2050-01-01T00:00:00Z
+Y2055 = 2_682_374_400 * SEC  # 2055-01-01T00:00:00Z
+Y2100 = 4_102_444_800 * SEC  # 2100-01-01T00:00:00Z, past the window
+ZERO_TIME_NS = -(2**63)      # time.Time{} (year 1) has no UnixNano; a binding passes INT64_MIN
+
+
+def kat_time_window_far_future(lib):
+    """services_state_test.go:177-183 (a newer record replaces the stored Updated) and :135-155
+    (an older one is ignored) with Updated past 2043: 2050 and 2055 merge and read back exactly; a
+    record from 2100 (past the window) still wins every later merge, as the reference's would, and
+    reads back as the window's end (engine bound)."""
+    e = mk(lib)
+    E = e.epoch
+    assert E % SEC == 0 and E < T0 - 2**59 and E + 2**61 > Y2055
+    assert e.add_service_entry(LOCAL, (CH, 0, Y2050, ALIVE)) == 1
+    assert e.slot(LOCAL, CH, 0) == (Y2050, ALIVE)
+    assert e.add_service_entry(LOCAL, (CH, 0, T0, TOMBSTONE)) == 0  # older
+    assert e.add_service_entry(LOCAL, (CH, 0, Y2055 + 123, DRAINING)) == 1
+    assert e.slot(LOCAL, CH, 0) == (Y2055 + 123, DRAINING)
+    assert e.add_service_entry(LOCAL, (CH, 0, Y2100, TOMBSTONE)) == 1
+    end = E + 2**61 - 1
+    assert e.slot(LOCAL, CH, 0) == (end, TOMBSTONE)
+    assert e.add_service_entry(LOCAL, (CH, 0, Y2055 + 124, ALIVE)) == 0
+    # every reader hands out absolute times
+    got = [tup(x) for x in e.local_state(LOCAL) if x.host == CH]
+    assert got == [(CH, 0, end, TOMBSTONE)]
+    ts, st = e.read_view(LOCAL)
+    assert (ts[CH * e.S], st[CH * e.S]) == (end, TOMBSTONE)
+
+
+def kat_time_window_pre_1970_and_zero(lib):
+    """service/service.go:68-72 IsStale + services_state.go:302-308: a record whose Updated is
+    before 1970, the zero time.Time, or any time before the window is older than now - 3h - 1min,
+    so AddServiceEntry drops it (stale) and creates nothing."""
+    e = mk(lib)
+    e.set_round(1)
+    for t in (-SEC, -500_000_000, ZERO_TIME_NS, 0, 315_532_800 * SEC):  # 1969, zero, 1970, 1980
+        assert e.add_service_entries([LOCAL], [(CH, 1, t, ALIVE)]) == 0
+        assert e.add_service_entries([LOCAL], [(CH, 2, t, TOMBSTONE)]) == 0
+    assert all(e.slot(LOCAL, CH, s) is None for s in range(e.S))
+    assert e.stats()["stale_drops"] == 10
+
+
+def _window_doc(e, names, recs):
+    """A ServicesState JSON holding `recs` = [(host, svc, Updated text or None, Status)]."""
+    import json as _json
+    servers = {}
+    for h, sv, upd, st in recs:
+        host = names.hosts[h].decode()
+        svc = {"ID": names.ids[h * e.S + sv].decode(), "Hostname": host, "Status": st}
+        if upd is not None:
+            svc["Updated"] = upd
+        servers.setdefault(host, {"Name": host, "Services": {}})["Services"][svc["ID"]] = svc
+    return _json.dumps({"Servers": servers, "ClusterName": "default"}).encode()
+
+
+def kat_time_window_decode(lib):
+    """catalog.Decode + MergeRemoteState (services_state.go:355-373) of records from 2050, past the
+    window (2100), 1969, and with Updated missing (the zero time.Time): Decode reads them all (none
+    invalid), the merge keeps the 2050 and 2100 records and drops the other two as stale."""
+    from sidecar_amd.codec import synthetic_names
+    e = mk(lib)
+    names = synthetic_names(e.H, e.S, seed=5)
+    e.set_names(names)
+    e.set_round(1)
+    recs = [(CH, 0, "2050-01-01T00:00:00.5Z", ALIVE), (CH, 1, "2100-01-01T00:00:00Z", DRAINING),
+            (SH, 0, "1969-12-31T23:59:59.5Z", ALIVE), (SH, 1, None, TOMBSTONE),
+            (SH, 2, "0001-01-01T00:00:00Z", ALIVE)]
+    doc = _window_doc(e, names, recs)
+    rc, got, ds = e.decode_state_json(doc)
+    assert rc == 0 and ds["invalid"] == 0 and ds["unknown"] == 0 and ds["records"] == 5, ds
+    E, end = e.epoch, e.epoch + 2**61 - 1
+    want = {(CH, 0): (Y2050 + 500_000_000, ALIVE), (CH, 1): (end, DRAINING), (SH, 0): (E, ALIVE),
+            (SH, 1): (E, TOMBSTONE), (SH, 2): (E, ALIVE)}
+    assert {(h, sv): (t, st) for t, h, sv, st in got} == want
+    rc, ds = e.merge_remote_state_json(LOCAL, doc)
+    assert rc == 0
+    assert e.slot(LOCAL, CH, 0) == (Y2050 + 500_000_000, ALIVE)
+    assert e.slot(LOCAL, CH, 1) == (end, DRAINING)
+    assert all(e.slot(LOCAL, SH, s) is None for s in range(3))
+    assert e.stats()["stale_drops"] == 3
+    # and the encoder writes the 2050 record back as Go would
+    assert b'"Updated":"2050-01-01T00:00:00.5Z"' in e.local_state_json(LOCAL)
 
 
 ALL = [v for k, v in sorted(globals().items()) if k.startswith("kat_")]

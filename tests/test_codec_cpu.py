@@ -69,7 +69,7 @@ def python_state_json(e, names, view):
             w = int(row[r])
             if w & 7 == 7:
                 continue
-            ents.append(go_json_string(names.ids[r]) + b":" + names.pre[r] + json_time(w >> 3) + names.post[r] +
+            ents.append(go_json_string(names.ids[r]) + b":" + names.pre[r] + json_time(e.word_time(w)) + names.post[r] +
                         str(w & 7).encode() + b"}")
         if not ents:
             continue
@@ -116,7 +116,7 @@ def test_encode_decode_roundtrip_and_junk(oracle_lib):
             for s in sorted(range(e.S), key=lambda s: names.ids[o * e.S + s]):
                 w = int(row[o * e.S + s])
                 if w & 7 != 7:
-                    want.append((w >> 3, o, s, w & 7))
+                    want.append((e.word_time(w), o, s, w & 7))
         assert recs == want
     rc, recs, ds = e.decode_state_json(b"asdf")
     assert rc == GX_EINVAL and recs == [] and ds["error_at"] >= 0
@@ -150,7 +150,12 @@ def test_variants_accept_reject(oracle_lib):
         rc, recs, ds = e.decode_state_json(doc)
         assert (rc == 0) == ok, (name, rc, ds)
         if name == "edge_records":
-            assert ds["unknown"] == 2 and ds["invalid"] == 2, ds
+            # status 7 is invalid; 2050 is inside the engine's window (stored exactly); the
+            # pre-1970 and missing (zero time.Time) Updated clamp to the window's start
+            assert ds["unknown"] == 2 and ds["invalid"] == 1, ds
+            times = [t for t, _, _, _ in recs]
+            assert parse_rfc3339("2050-01-01T00:00:00Z") in times
+            assert times.count(e.epoch) == 2 and e.epoch > 0
         if name in ("pretty", "ascii_escaped", "escaped_names"):
             assert recs == e.decode_state_json(base)[1], name
         if name == "shuffled_keys":  # document order changes with the key order

@@ -17,14 +17,13 @@ def check(lib, name):
     assert json.loads(str(ref["params"])) == kw and int(ref["rounds"]) == rounds
     got = run(lib, kw, rounds)
     got_stats, ref_stats = json.loads(got["stats"]), json.loads(str(ref["stats"]))
-    # counters added after the fixtures were made: byte-limit packing (zero in record mode),
-    # listener drops (no listeners), ServiceChanged calls (not in the fixtures), packet loss and
-    # memberlist failure detection (off in these cases)
+    # counters added after a fixture was made (a regenerated fixture holds them all): byte-limit
+    # packing (zero in record mode), listener drops (no listeners), ServiceChanged calls, packet
+    # loss and memberlist failure detection (off in these cases)
     extra = {k: v for k, v in got_stats.items() if k not in ref_stats}
     fd = {k for k in extra if k.startswith("fd_")} | {"lost_packets"}
-    assert set(extra) == {"bytes_sent", "cap_cuts", "change_events", "listener_drops"} | fd
-    assert extra["bytes_sent"] == extra["cap_cuts"] == extra["listener_drops"] == 0
-    assert all(extra[k] == 0 for k in fd)
+    assert set(extra) <= {"bytes_sent", "cap_cuts", "change_events", "listener_drops"} | fd
+    assert all(extra[k] == 0 for k in extra if k != "change_events")
     assert {k: got_stats[k] for k in ref_stats} == ref_stats
     assert np.array_equal(got["views"], ref["views"])
     assert np.array_equal(got["hosts"], ref["hosts"])

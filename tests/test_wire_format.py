@@ -158,7 +158,7 @@ def test_push_pull_messages_follow_the_spec(oracle_lib, name):
         whole.round_send()
         whole.round_merge()
         V = whole.read_views().reshape(whole.H, R).astype(np.uint64) if ae else None
-        now = whole.now()
+        now = whole.now() - whole.epoch  # slot time (the words are epoch-relative)
         whole.ae_merge()
         whole.round_end()
         n_trace = len(sh.ae_trace)
