@@ -82,11 +82,17 @@ struct Dev {
   // inbox with one atomic; the merge sorts a receiver's few headers by global sender key itself.
   uint32_t DI;         // inbox slots per receiver (<= 64); packets past them go to the overflow list
   uint32_t DR;         // inbox slots whose records are stored inline (in_rec); the rest stay in msg
+  // Per-round counters come in two buffers by round parity (set_round_fields): this round's, and
+  // the next round's, which this round's owner phase zeroes (nothing reads it during this round),
+  // so no kernel of a round has to wait for a reset of its counters.
   uint32_t *in_cnt;    // [Hl] packets registered per receiver this round
+  uint32_t *in_cnt_nx; // [Hl] the same for the next round
   uint4 *in_hdr;       // [Hl][DI] {global key = sender * K + j, entry, len, slot}, arrival order
   uint4 *in_ovf;       // [H*K] {key, entry, len, local receiver} past a receiver's DI slots
   grec *in_rec;        // [Hl][DR][packet_cap] records of a receiver's first DR packets
-  uint32_t *work_cnt;  // [0] expiry-scan worklist, [1] unused, [2] overflow count, [3] error bits
+  uint32_t *work_cnt;  // [0..1] expiry-scan worklist, [2..3] overflow list counts by round parity, [4] error bits
+  uint32_t *wl_cnt, *wl_cnt_nx;    // this / next round's worklist count (into work_cnt)
+  uint32_t *ovf_cnt, *ovf_cnt_nx;  // this / next round's overflow-list count
   uint32_t *work;      // [Hl] views whose expiry scan must stream the row this round
   uint8_t *mflag;      // [Hl] receivers k_merge_lean left to k_merge (a live record or > DR packets)
   grec *scan_list;     // [H][L] first L expired records of this round's scan
@@ -228,15 +234,23 @@ GXD uint32_t owner_of(const Dev &d, uint32_t r) { return d.S == 1 ? r : (uint32_
 GXD bool owned_by(const Dev &d, uint32_t r, uint32_t o) { return r - o * d.S < d.S; }
 GXD bool departed(const Dev &d, uint32_t u) { return d.departures && departed_at(d.p, d.round, u); }
 
+// Orders a wave's LDS and global accesses across its lanes (a team lives inside one wave).
+GXD void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // ------------------------------------------------------------------------ receiver inboxes --
-#define GX_ERR_INBOX 1u  // work_cnt[3]: a received packet slot failed validation (k_inbox_unpack)
+#define GX_ERR_INBOX 1u  // work_cnt[4]: a received packet slot failed validation (k_inbox_unpack)
+#define GX_WC_ERR 4
+#define GX_WC_N 8
 // Register a packet (global sender key, message entry) in local receiver vi's inbox: one atomic
 // on the receiver's count; returns the inbox position (slot). The header itself (with the record
 // count) is written by inbox_header once the packet is packed.
 GXD uint32_t inbox_claim(const Dev &d, uint32_t vi) { return atomicAdd(&d.in_cnt[vi], 1u); }
 GXD void inbox_header(const Dev &d, uint32_t vi, uint32_t pos, uint32_t key, uint32_t entry, uint32_t len) {
   if (pos < d.DI) d.in_hdr[(size_t)vi * d.DI + pos] = make_uint4(key, entry, len, pos);
-  else d.in_ovf[atomicAdd(&d.work_cnt[2], 1u)] = make_uint4(key, entry, len, vi);
+  else d.in_ovf[atomicAdd(d.ovf_cnt, 1u)] = make_uint4(key, entry, len, vi);
 }
 GXD void inbox_put(const Dev &d, uint32_t vi, uint32_t key, uint32_t entry, uint32_t len) {
   inbox_header(d, vi, inbox_claim(d, vi), key, entry, len);
@@ -260,7 +274,7 @@ GXD uint4 inbox_next(const Dev &d, uint32_t vi, int64_t after) {
       found = true;
     }
   }
-  const uint32_t no = d.work_cnt[2];
+  const uint32_t no = *d.ovf_cnt;
   for (uint32_t i = 0; i < no; i++) {
     const uint4 h = d.in_ovf[i];
     if (h.w == vi && (int64_t)h.x > after && (!found || h.x < best.x)) {

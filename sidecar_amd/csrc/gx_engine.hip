@@ -68,6 +68,7 @@ struct gx_engine {
   hipStream_t side_stream;
   hipEvent_t side_start, side_done;
   bool side_pending;
+  uint32_t *in_cnt_buf;     // [2][Hl] inbox counts by round parity (Dev::in_cnt, in_cnt_nx)
   int async_phases;         // sharded phase calls return without waiting (gx_set_stream)
   int device;
   int timing;
@@ -146,6 +147,14 @@ static int64_t now_of(const gx_engine *e) { return e->d.p.t0_ns + e->d.round * e
 // services_state.go:62-63,95)
 static int64_t abs_tm(const gx_engine *e, int64_t t) { return t ? t + e->d.epoch : 0; }
 static void set_round_fields(gx_engine *e) {
+  Dev &d = e->d;
+  const uint32_t par = (uint32_t)(d.round & 1);
+  d.in_cnt = e->in_cnt_buf + (size_t)par * d.Hl;
+  d.in_cnt_nx = e->in_cnt_buf + (size_t)(par ^ 1u) * d.Hl;
+  d.wl_cnt = d.work_cnt + par;
+  d.wl_cnt_nx = d.work_cnt + (par ^ 1u);
+  d.ovf_cnt = d.work_cnt + 2 + par;
+  d.ovf_cnt_nx = d.work_cnt + 2 + (par ^ 1u);
   e->d.now = now_of(e);
   e->d.partitioned = e->d.round >= e->d.p.partition_start && e->d.round < e->d.p.partition_end;
   e->d.pair_split = e->d.partitioned && !e->d.p.fd_enable;
@@ -223,9 +232,9 @@ static int deliver_events(gx_engine *e) {
 static int take_device_error(gx_engine *e) {
   if (e->d.G < 2) return GX_OK;
   uint32_t err = 0;
-  HIPCHK(hipMemcpy(&err, &e->d.work_cnt[3], sizeof(err), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&err, &e->d.work_cnt[GX_WC_ERR], sizeof(err), hipMemcpyDeviceToHost));
   if (!err) return GX_OK;
-  HIPCHK(hipMemset(&e->d.work_cnt[3], 0, sizeof(err)));
+  HIPCHK(hipMemset(&e->d.work_cnt[GX_WC_ERR], 0, sizeof(err)));
   return GX_EINVAL;
 }
 
@@ -298,7 +307,9 @@ static int round_send_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_OWNER);
     owner_launch(d, s);
   }
-  {
+  // with the tick finished in k_send, the expiry scans run in k_send's prologue (no k_scan launch)
+  const bool scan_in_send = !bt_apart && d.K && !(d.ab & 4u);
+  if (!scan_in_send) {
     LaunchTimer t(e, GX_K_SCAN);
     const bool ev = !e->log_views.empty();
     const unsigned grid = d.Hl < SCAN_GRID ? d.Hl : SCAN_GRID;
@@ -320,8 +331,20 @@ static int round_send_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_SEND);
     if (d.p.fd_enable) k_fd_send<<<nblk(d.Hl, 64), 64, 0, s>>>(d);  // memberlist's targets + messages
     // 4 lanes per host: measured best of 1/4/8/16/64 (profiles/send_team.sh)
-    if (d.p.fd_enable || d.departures) k_send<4, true><<<nblk(d.Hl, 64), 256, 0, s>>>(d, bt_apart ? 0 : 1);
-    else k_send<4, false><<<nblk(d.Hl, 64), 256, 0, s>>>(d, bt_apart ? 0 : 1);
+    const bool ev = !e->log_views.empty();
+    const unsigned g = nblk(d.Hl, 64);
+    if (scan_in_send) {
+      if (d.departures)
+        (vec ? (ev ? k_send<4, true, true, true, true> : k_send<4, true, true, true, false>)
+             : (ev ? k_send<4, true, true, false, true> : k_send<4, true, true, false, false>))<<<g, 256, 0, s>>>(d, 1);
+      else
+        (vec ? (ev ? k_send<4, false, true, true, true> : k_send<4, false, true, true, false>)
+             : (ev ? k_send<4, false, true, false, true> : k_send<4, false, true, false, false>))<<<g, 256, 0, s>>>(d, 1);
+    } else if (d.p.fd_enable || d.departures) {
+      k_send<4, true><<<g, 256, 0, s>>>(d, bt_apart ? 0 : 1);
+    } else {
+      k_send<4, false><<<g, 256, 0, s>>>(d, bt_apart ? 0 : 1);
+    }
   }
   HIPCHK(hipGetLastError());
   return GX_OK;
@@ -600,7 +623,7 @@ int gx_destroy(gx_engine *e) {
   Dev &d = e->d;
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
-                  d.msg_dst, d.in_cnt, d.scan_list, d.scan_cnt, d.tick,
+                  d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf,
                   d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
   for (void *p : ptrs)
@@ -644,6 +667,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->conv_bad = nullptr;
   e->digest_buf = nullptr;
   e->stream = e->own_stream = e->side_stream = nullptr;
+  e->in_cnt_buf = nullptr;
   e->side_start = e->side_done = nullptr;
   e->side_pending = false;
   e->async_phases = 0;
@@ -720,14 +744,14 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.msg_len, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_dst, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_key, sizeof(uint32_t) * Hg * K);
-  ALLOC(d.in_cnt, sizeof(uint32_t) * H);
+  ALLOC(e->in_cnt_buf, sizeof(uint32_t) * 2 * H);
   d.DI = p->inbox_slots ? p->inbox_slots : 64;
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
   d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
   ALLOC(d.in_hdr, sizeof(uint4) * H * d.DI);
   ALLOC(d.in_ovf, sizeof(uint4) * Hg * K);
   ALLOC(d.in_rec, sizeof(grec) * H * d.DR * p->packet_cap);
-  ALLOC(d.work_cnt, sizeof(uint32_t) * 4);
+  ALLOC(d.work_cnt, sizeof(uint32_t) * GX_WC_N);
   ALLOC(d.work, sizeof(uint32_t) * H);
   if (p->push_pull_mode == GX_PP_INITIATE) {
     ALLOC(e->pp_dev, sizeof(uint32_t) * 2 * Hg);
@@ -792,8 +816,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   HIPCHK(hipMemsetAsync(d.ctr, 0, sizeof(DevCtr), s));
   HIPCHK(hipMemsetAsync(d.arena_len, 0, sizeof(uint32_t) * H * d.A, s));
   HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * Hg * K, s));
-  HIPCHK(hipMemsetAsync(d.in_cnt, 0, sizeof(uint32_t) * H, s));
-  HIPCHK(hipMemsetAsync(d.work_cnt, 0, sizeof(uint32_t) * 4, s));
+  HIPCHK(hipMemsetAsync(e->in_cnt_buf, 0, sizeof(uint32_t) * 2 * H, s));
+  HIPCHK(hipMemsetAsync(d.work_cnt, 0, sizeof(uint32_t) * GX_WC_N, s));
   HIPCHK(hipMemsetAsync(d.tick, 0, H, s));
   HIPCHK(hipMemsetAsync(d.ev_slot, 0xff, sizeof(int32_t) * H, s));  // -1: no listener
   k_fill_u16<<<256, 256, 0, s>>>(d.sbytes, d.R, (uint16_t)GX_STATIC_BYTES_DEFAULT);
@@ -820,7 +844,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
 int gx_set_round(gx_engine *e, int64_t round) {
   if (!e || round < e->d.round) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
+  if (round != e->d.round) {  // a jump: this round's and the next round's counters start empty
+    HIPCHK(hipMemsetAsync(e->in_cnt_buf, 0, sizeof(uint32_t) * 2 * e->d.Hl, e->stream));
+    HIPCHK(hipMemsetAsync(e->d.work_cnt, 0, sizeof(uint32_t) * GX_WC_ERR, e->stream));
+  }
   e->d.round = round;
+  set_round_fields(e);
   int rc = wake_all(e);
   return rc ? rc : sync_check(e);
 }

@@ -166,20 +166,19 @@ __global__ void k_wake(Dev d) {
 // LastChanged, the ChangeEvents) follows from ballots in list order. Every included record is
 // restamped `now`, so the server's times all take that value.
 // A ticking view whose exact expiry bound is in the future cannot change in
-// TombstoneOthersServices (:645-662); the others go to the expiry scan's worklist. Also clears this
-// round's inbox counts.
+// TombstoneOthersServices (:645-662); the others go to the expiry scan's worklist. Also clears the
+// next round's inbox counts (round-parity buffers, Dev::in_cnt_nx).
+// The tick of host idx by its team (T lanes inside one wave); sj = the team's T LDS job slots (the
+// head of the sleep ring). Returns, on the lead lane, whether the host went on the expiry-scan
+// worklist (its BroadcastTombstones tick then finishes after the scan).
 template <int T>
-__global__ __launch_bounds__(256) void k_owner(Dev d) {
-  __shared__ gx_job s_sl[256];  // the head of each host's sleep ring, one job per team lane
-  Acc a;
+GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
-  const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   const bool lead = tl == 0;
   const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.work_cnt[2] = 0;  // this round's inbox overflow list
   const bool act = idx < d.Hl && !departed(d, d.lo + idx);
+  bool queued = false;
   gx_host_state hs;
-  gx_job *sj = &s_sl[threadIdx.x - tl];
   // everything the tick may read is loaded up front: the bookkeeping, the own records' view slots
   // (one 128-B row segment), their local status and the view's expiry bound
   uint64_t cur0 = GX_SLOT_ABSENT;
@@ -195,10 +194,10 @@ __global__ __launch_bounds__(256) void k_owner(Dev d) {
     if (tl == 0) mexp0 = d.minexp[idx];
     if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
   }
-  __syncthreads();
+  wave_sync();  // the team's sleep-ring slots
   if (idx < d.Hl) {
     const uint32_t o = d.lo + idx;
-    if (lead) d.in_cnt[idx] = 0;
+    if (lead) d.in_cnt_nx[idx] = 0;
     if (!act) {  // a crashed host runs no loopers
       if (lead) d.tick[idx] = 0;
     } else {
@@ -310,13 +309,27 @@ __global__ __launch_bounds__(256) void k_owner(Dev d) {
             d.scan_cnt[idx] = 0;
             a.c[C_SCANSLOTS] += d.R;
           } else {
-            d.work[atomicAdd(&d.work_cnt[0], 1u)] = idx;
+            d.work[atomicAdd(d.wl_cnt, 1u)] = idx;
+            d.tick[idx] = 2;  // the tick streams the view first (k_scan, or k_send's prologue)
+            queued = true;
           }
         }
         d.hs[idx] = hs;
       }
     }
   }
+  return queued;
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void k_owner(Dev d) {
+  __shared__ gx_job s_sl[256];  // the head of each host's sleep ring, one job per team lane
+  Acc a;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next round's lists start empty
+    *d.ovf_cnt_nx = 0;
+    *d.wl_cnt_nx = 0;
+  }
+  owner_tick<T>(d, a, blockIdx.x * (256 / T) + threadIdx.x / T, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
   acc_flush(d, a);
 }
 
@@ -451,13 +464,14 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
     scan_view<VEC, EV>(d, li(d, (uint32_t)only_host), list_base, list_cap, cnt_out, sm);
     return;
   }
-  const uint32_t n = d.work_cnt[0];
+  const uint32_t n = *d.wl_cnt;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const uint32_t oi = d.work[w];
     scan_view<VEC, EV>(d, oi, &list_base[(size_t)oi * list_stride], list_cap, &cnt_out[oi], sm);
     __syncthreads();
   }
 }
+
 
 // The rest of a BroadcastTombstones tick on its own, for rounds where other phases push to the
 // FIFO between the scan and the send (failure detector, storm); otherwise k_send runs it.
@@ -782,13 +796,9 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 // at a packet that would be empty), and a packet to an unreachable peer is lost after
 // GetBroadcasts took its records.
 template <int T, bool X>
-__global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
-  __shared__ gx_job s_pj[256 / T][T];  // FIFO head jobs of the block's hosts, loaded ahead
-  Acc a;
-  uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T, lane = threadIdx.x & (T - 1);
-  unsigned lost = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.work_cnt[0] = 0;  // the scan worklist was consumed
-  if (idx < d.Hl) {
+GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, unsigned &lost) {
+  const uint32_t lane = threadIdx.x & (T - 1);
+  {
     uint32_t u = d.lo + idx;
     uint32_t cap = d.p.packet_cap;
     gx_host_state *h = &d.hs[idx];
@@ -820,7 +830,6 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       // per team lane (call c takes job c while c < the jobs queued at the start: later pushes go
       // to the tail and cannot overwrite them), so a call waits on its list records only.
       const uint32_t head0 = hs.fifo_head, n0 = hs.fifo_tail - head0;
-      gx_job *pjs = s_pj[threadIdx.x / T];
       if (lane < n0 && lane < np * d.NG) pjs[lane] = d.fifo[(size_t)idx * d.Q + ((head0 + lane) % d.Q)];
       // A packet to a reachable peer on this shard takes its receiver inbox slot before it is
       // packed, so its records go straight into the receiver's inbox when the slot is one of the
@@ -881,9 +890,35 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       if (lane == 0) *h = hs;
     }
   }
+}
+
+// SCAN: the round's expiry scans run here instead of in k_scan: the block first streams the views
+// of its hosts whose tick needs one (tick == 2; scan_view, block-wide, one view at a time), then
+// sends. A host's scan and send touch no other host's state, so no block waits for another.
+template <int T, bool X, bool SCAN = false, bool VEC = false, bool EV = false>
+__global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
+  __shared__ gx_job s_pj[256 / T][T];  // FIFO head jobs of the block's hosts, loaded ahead
+  __shared__ ScanLds sm;
+  __shared__ uint32_t s_scan[256 / T], s_nscan;
+  Acc a;
+  const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
+  unsigned lost = 0;
+  if (SCAN) {
+    if (threadIdx.x == 0) s_nscan = 0;
+    __syncthreads();
+    if ((threadIdx.x & (T - 1)) == 0 && idx < d.Hl && d.tick[idx] == 2) s_scan[atomicAdd(&s_nscan, 1u)] = idx;
+    __syncthreads();
+    for (uint32_t k = 0; k < s_nscan; k++) {
+      const uint32_t oi = s_scan[k];
+      scan_view<VEC, EV>(d, oi, &d.scan_list[(size_t)oi * d.L], d.L, &d.scan_cnt[oi], sm);
+      __syncthreads();  // the list and count before the tick's finish reads them
+    }
+  }
+  if (idx < d.Hl) send_host<T, X>(d, a, idx, s_pj[threadIdx.x / T], do_bt, lost);
   acc_flush(d, a);
   if (X && lost) ctr_atomic(d, C_LOST, lost);
 }
+
 
 // ============================================================== phase 4: gather-then-merge ==
 // One wave per receiver. Its inbox (the packet headers the senders registered, in arrival order)
@@ -954,10 +989,13 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
     const uint32_t cap = d.p.packet_cap, nspec = d.DR * cap;
     const grec *base = &d.in_rec[(size_t)vi * nspec];
     grec g[LEAN_Q];
+    // A/B: bit 0 limits the speculative loads to the first `fanout` slots, bit 1 loads records
+    // only once the count and lengths are known
+    const uint32_t nsp = (d.ab & 2u) ? 0u : (d.ab & 1u) ? (d.K * cap < nspec ? d.K * cap : nspec) : nspec;
 #pragma unroll
     for (int q = 0; q < LEAN_Q; q++) {  // hop 1: inline records, speculatively
       const uint32_t p = l + LEAN_LPR * q;
-      if (p < nspec) g[q] = base[p];
+      if (p < nsp) g[q] = base[p];
     }
     const uint4 hd = l < d.DR ? d.in_hdr[(size_t)vi * d.DI + l] : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t cnt = d.in_cnt[vi];
@@ -967,11 +1005,12 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
       const uint32_t npos = cnt * cap;
       c_hdr = l == 0 ? cnt : 0;
       for (uint32_t p0 = 0; p0 < npos; p0 += LEAN_LPR * LEAN_Q) {
-        if (p0) {
+        if (p0 || nsp < LEAN_LPR * LEAN_Q) {
 #pragma unroll
           for (int q = 0; q < LEAN_Q; q++) {
-            const uint32_t p = p0 + l + LEAN_LPR * q;
-            if (p < npos) g[q] = base[p];
+            const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
+            const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
+            if (p < npos && (p0 || p >= nsp) && p - sl * cap < len) g[q] = base[p];
           }
         }
         bool valid[LEAN_Q];
@@ -1015,11 +1054,6 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
 #define MERGE_RANGE 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
-// Orders a wave's LDS and global accesses across its lanes (the waves of a block do not meet).
-GXD void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
 template <bool K32, bool EV>
 __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
   // one receiver per wave, MERGE_WAVES per block; the waves share nothing (wave-level sync only)
@@ -2190,7 +2224,7 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
 // Inbox: received slots -> message entries [Hl*K, Hl*K + n), registered in the receivers'
 // inboxes. A slot is checked like the oracle's gx_inbox_unpack does (sender key < H*K, receiver on
 // this shard, len <= packet_cap, n_fd <= fd_msg_cap) and its record keys < R; a bad slot is
-// skipped and flagged (work_cnt[3]), and the next call that waits returns GX_EINVAL.
+// skipped and flagged (work_cnt[GX_WC_ERR]), and the next call that waits returns GX_EINVAL.
 __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   uint32_t i = blockIdx.x;
   if (i >= n) return;
@@ -2204,7 +2238,7 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   bool bad = key >= d.H * d.KE || dst - d.lo >= d.Hl || len > d.p.packet_cap || nfd > fcap;
   for (uint32_t x = threadIdx.x; !bad && x < len; x += blockDim.x) bad |= recs[x].r >= d.R;
   if (__ballot(bad) != 0) {
-    if (threadIdx.x == 0) atomicOr(&d.work_cnt[3], GX_ERR_INBOX);
+    if (threadIdx.x == 0) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);
     return;
   }
   const uint32_t vi = dst - d.lo;
