@@ -89,3 +89,15 @@ def test_gpu_distshard_rccl_world1(gx_lib):
         assert np.array_equal(sh.e.read_views(), whole.read_views())
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("field", ["key", "receiver", "len"])
+def test_gpu_corrupt_inbox_slot_refused(gx_lib, field):
+    """The device-side validation of received slots matches the oracle's refusal."""
+    import torch
+    from tests.corrupt_inbox import run, run_valid
+    dev = torch.device("cuda:0")
+    assert run_valid(gx_lib, dev) >= 0
+    assert run(gx_lib, dev, field) == "einval"
+    # the flag is taken once: a fresh exchange on new engines goes through again
+    assert run_valid(gx_lib, dev) >= 0

@@ -148,3 +148,11 @@ def test_delta_ships_only_differing_blocks(oracle_lib):
     assert_sharded_equal(whole, sh, "delta")
     w = sh.wire.as_dict()
     assert 40 * n_msgs < w["ae_delta"] < w["ae_full_rows_equivalent"]
+
+
+@pytest.mark.parametrize("field", ["key", "receiver", "len"])
+def test_corrupt_inbox_slot_refused(oracle_lib, field):
+    import torch
+    from tests.corrupt_inbox import run, run_valid
+    assert run_valid(oracle_lib, torch.device("cpu")) >= 0
+    assert run(oracle_lib, torch.device("cpu"), field) == "einval"
