@@ -120,6 +120,7 @@ struct Dev {
   uint64_t divS;       // r / S as a 64x32 multiply-high (Lemire: M = (2^64 - 1) / S + 1), S > 1
   uint32_t logS;       // log2(S) when S is a power of two
   int departures;      // p.depart_round >= 0 && p.depart_ppm
+  uint32_t nblk_ae;    // digest blocks per row, ceil(R / GX_DIGEST_SLOTS)
   uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels)
 };
 

@@ -745,6 +745,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.msg_dst, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_key, sizeof(uint32_t) * Hg * K);
   ALLOC(e->in_cnt_buf, sizeof(uint32_t) * 2 * H);
+  d.nblk_ae = (d.R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
   d.DI = p->inbox_slots ? p->inbox_slots : 64;
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
   d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
@@ -1884,7 +1885,9 @@ static void ae_plan_launch(gx_engine *e, uint32_t lo, uint32_t hi, const void *l
   in.bcnt = e->ae_bcnt;
   in.nmw = e->nmw;
   in.nblk = e->nblk;
-  const bool small = hi - lo < 1024;  // fewer than 4 pairs per CU: per-block bandwidth decides
+  // fewer than 4 pairs per CU: per-block bandwidth decides (2 tiles in flight measured slower for
+  // the cross pairs of a post-heal round: 8.2 -> 9.3 ms at G = 2, H = 16384)
+  const bool small = hi - lo < 1024;
 #define GX_AE_PLAN(V, E)                                                                                     \
   (E ? k_ae_plan_ev<V> : small ? k_ae_plan_pf2<V> : k_ae_plan<V>)<<<hi - lo, 256, 0, st>>>(                    \
       e->d, e->ae_pa + lo, e->ae_pb + lo, e->ae_prow + lo, e->ae_pcount + lo, in, e->ae_skip)

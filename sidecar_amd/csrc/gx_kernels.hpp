@@ -1381,6 +1381,7 @@ GXD uint32_t ae_book(const Dev &d, uint32_t a, uint32_t b, bool both, uint32_t b
 // word), and every other block is A's own block (the digests matched), which merges with the
 // counts of the identical remote block and no change.
 // PF = tiles whose loads are in flight while one is merged; NT = non-temporal loads.
+#define XS_MAXB 2048  // digest blocks per row whose offsets ae_pair stages in LDS (R <= 2^20)
 struct XSrc {
   const uint8_t *lead;   // the partner's lead blocks (message + 16)
   const uint8_t *ret;    // the partner's return blocks (after the count table)
@@ -1390,12 +1391,19 @@ struct XSrc {
   const uint32_t *bcnt;  // own blocks: present | stale << 16 (digest pass)
 };
 // Slots s, s + 1 (s even) of an encoded block (gx.h): own slots keep w[], the others take their
-// literal (popcount rank in the neu mask).
-GXD void dec_pair(const uint64_t *enc, uint32_t s, bool v0, bool v1, uint64_t *w) {
+// literal (popcount rank in the neu mask). The prefix popcount of the neu words below slot s's
+// word is eight independent loads of the block header (one 128-B line the whole wave reads).
+GXD void dec_pair_u(const uint64_t *enc, uint32_t s, bool v0, bool v1, uint64_t *w) {
   const uint32_t wi = s >> 6;
-  const uint64_t om = enc[wi], nm = enc[8 + wi];
   int32_t pre = -1;
-  for (uint32_t i = 0; i < wi; i++) pre += __popcll(enc[8 + i]);
+  uint64_t om = 0, nm = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint64_t x = enc[8 + i];
+    pre += i < wi ? __popcll(x) : 0;
+    nm = i == wi ? x : nm;
+  }
+  om = enc[wi];
 #pragma unroll
   for (int e = 0; e < 2; e++) {
     const uint32_t b = (s + e) & 63;
@@ -1436,6 +1444,40 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint64_t qa[PF][4], qb[PF][4];
   uint64_t xo_f = 0, xo_r = 0;  // byte offsets of the next lead / return block (block-uniform)
   uint32_t xj = 0, xskip = 0;   // return blocks used; slots of matching blocks not loaded
+  // Cross pairs: every block's class and message offset up front in LDS (two block scans), so a
+  // tile's blocks wait on their encoded words only, not on the previous block's length.
+  __shared__ uint32_t s_xo[XS_MAXB];  // offset | class << 30 (0 digests matched, 1 lead msg, 2 return msg)
+  const bool xs_lds = xs && d.nblk_ae <= XS_MAXB;
+  if (xs_lds) {
+    const uint32_t nb = d.nblk_ae, c = (nb + blockDim.x - 1) / blockDim.x, b0 = t * c;
+    const uint32_t b1 = b0 + c < nb ? b0 + c : nb;
+    uint32_t fsz = 0, nl = 0;
+    for (uint32_t b = b0; b < b1; b++) {
+      if ((xs->fmask[b >> 5] >> (b & 31)) & 1u) fsz += 128 + 8u * xs->lt[b];
+      else if ((xs->lmask[b >> 5] >> (b & 31)) & 1u) nl++;
+    }
+    unsigned long long tot;
+    const unsigned long long pre = block_excl_scan64((unsigned long long)fsz | ((unsigned long long)nl << 32), s_wave, tot);
+    uint32_t fo = (uint32_t)pre, li_ = (uint32_t)(pre >> 32), rsz = 0;
+    for (uint32_t b = b0; b < b1; b++)
+      if (!((xs->fmask[b >> 5] >> (b & 31)) & 1u) && ((xs->lmask[b >> 5] >> (b & 31)) & 1u))
+        rsz += 128 + 8u * xs->rcnt[li_++];
+    const unsigned long long rpre = block_excl_scan64(rsz, s_wave, tot);
+    uint32_t ro = (uint32_t)rpre;
+    li_ = (uint32_t)(pre >> 32);
+    for (uint32_t b = b0; b < b1; b++) {
+      if ((xs->fmask[b >> 5] >> (b & 31)) & 1u) {
+        s_xo[b] = fo | (1u << 30);
+        fo += 128 + 8u * xs->lt[b];
+      } else if ((xs->lmask[b >> 5] >> (b & 31)) & 1u) {
+        s_xo[b] = ro | (2u << 30);
+        ro += 128 + 8u * xs->rcnt[li_++];
+      } else {
+        s_xo[b] = 0;
+      }
+    }
+    __syncthreads();
+  }
   // returns the number of the tile's two blocks that were skipped (cross pairs, digests matched)
   auto load_tile = [&](uint32_t base, uint64_t *xa, uint64_t *xb) -> uint32_t {
     uint32_t skipped = 0;
@@ -1446,7 +1488,22 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       const uint64_t *Bp = B + r0;  // B[r0], B[r0 + 1]
       const uint64_t *enc = nullptr;
       uint32_t blk = (base >> 9) + h;
-      if (xs && base + GX_DIGEST_SLOTS * h < d.R) {
+      if (xs_lds && base + GX_DIGEST_SLOTS * h < d.R) {
+        const uint32_t x = s_xo[blk];
+        if (x >> 30) {
+          enc = reinterpret_cast<const uint64_t *>((x >> 30) == 1 ? xs->lead : xs->ret) + ((x & 0x3fffffffu) >> 3);
+        } else {
+          if (t == 0) {
+            const uint32_t c = xs->bcnt[blk];
+            c_merge += c & 0xffffu;
+            c_stale += c >> 16;
+          }
+          xskip += GX_DIGEST_SLOTS;
+          skipped++;
+          xa[2 * h] = xa[2 * h + 1] = xb[2 * h] = xb[2 * h + 1] = GX_SLOT_ABSENT;
+          continue;
+        }
+      } else if (xs && base + GX_DIGEST_SLOTS * h < d.R) {
         if ((xs->fmask[blk >> 5] >> (blk & 31)) & 1u) {
           enc = reinterpret_cast<const uint64_t *>(xs->lead + xo_f);
           xo_f += 128 + 8ull * xs->lt[blk];
@@ -1467,6 +1524,18 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
           continue;
         }
       }
+      if (enc) {  // a decoded block starts from A's own words (B == A): one load
+        if (VEC && v0) {
+          ulonglong2 pa = ld16<NT>(&A[r0]);
+          xa[2 * h] = xb[2 * h] = pa.x;
+          xa[2 * h + 1] = xb[2 * h + 1] = pa.y;
+        } else {
+          xa[2 * h] = xb[2 * h] = v0 ? A[r0] : GX_SLOT_ABSENT;
+          xa[2 * h + 1] = xb[2 * h + 1] = v1 ? A[r0 + 1] : GX_SLOT_ABSENT;
+        }
+        dec_pair_u(enc, r0 - blk * GX_DIGEST_SLOTS, v0, v1, &xb[2 * h]);
+        continue;
+      }
       if (VEC && v0) {
         ulonglong2 pa = ld16<NT>(&A[r0]);
         ulonglong2 pb = ld16<NT>(Bp);
@@ -1480,7 +1549,6 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         xb[2 * h] = v0 ? Bp[0] : GX_SLOT_ABSENT;
         xb[2 * h + 1] = v1 ? Bp[1] : GX_SLOT_ABSENT;
       }
-      if (enc) dec_pair(enc, r0 - blk * GX_DIGEST_SLOTS, v0, v1, &xb[2 * h]);
     }
     return skipped;
   };
