@@ -410,6 +410,11 @@ int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, u
 /* One BroadcastTombstones looper body with fn() = list, services_state.go:606-633. */
 int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list, uint32_t n);
 /* IsNewService, services_state.go:509-521. */
+/* Dynamic key space (host mirror, catalog.hpp): bit s of *mask is set when some view of this engine
+ * holds a record of any status for (owner, s). A slot that no view holds (never written, or
+ * removed everywhere after TOMBSTONE_LIFESPAN, services_state.go:645-653) can take a service ID
+ * seen for the first time. A sharded engine answers for its own views. */
+int gx_owner_slots_in_use(gx_engine *e, uint32_t owner, uint64_t *mask);
 int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *is_new);
 
 /* ---- catalog readers (catalog/view.go, services_state.go:726-748) ----------------------------

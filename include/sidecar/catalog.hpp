@@ -103,14 +103,35 @@ class Cluster {
     id_names_.emplace_back();
     return id;
   }
+  // A service ID seen for the first time takes the owner's next free slot (the reference creates
+  // it, services_state.go:310-318). When all S are taken, a slot that no view holds any more
+  // (garbage-collected everywhere after TOMBSTONE_LIFESPAN, :645-653) is reused; a queued copy
+  // of its old record is older than the lifespan, so IsStale drops it wherever it arrives.
   uint16_t Id(uint32_t host, const std::string &id) {
     auto &m = ids_[host];
     auto it = m.find(id);
     if (it != m.end()) return it->second;
-    if (id_names_[host].size() >= p_.n_services) throw std::runtime_error("service table full: " + id);
-    uint16_t s = (uint16_t)id_names_[host].size();
+    uint16_t s;
+    if (id_names_[host].size() < p_.n_services) {
+      s = (uint16_t)id_names_[host].size();
+      id_names_[host].push_back(id);
+    } else {
+      uint64_t used = 0;
+      check(gx_owner_slots_in_use(e_, host, &used), "gx_owner_slots_in_use");
+      s = 0;
+      while (s < p_.n_services && ((used >> s) & 1u)) s++;
+      if (s == p_.n_services) throw std::runtime_error("service table full: " + id);
+      m.erase(id_names_[host][s]);  // the slot's old ID is forgotten, with its metadata
+      id_names_[host][s] = id;
+      const uint64_t key = (uint64_t)host * p_.n_services + s;
+      if (names_.erase(key)) names_dirty_ = true;
+      auto st = static_.find(host);
+      if (st != static_.end() && st->second[s] != (uint16_t)GX_STATIC_BYTES_DEFAULT) {
+        st->second[s] = (uint16_t)GX_STATIC_BYTES_DEFAULT;
+        check(gx_set_static_bytes(e_, host, host + 1, st->second.data()), "gx_set_static_bytes");
+      }
+    }
     m[id] = s;
-    id_names_[host].push_back(id);
     return s;
   }
   gx_service Rec(const Service &svc) {

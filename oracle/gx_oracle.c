@@ -1535,6 +1535,16 @@ int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list,
   return GX_OK;
 }
 
+int gx_owner_slots_in_use(gx_engine *e, uint32_t owner, uint64_t *mask) {
+  if (!e || !mask || owner >= e->H) return GX_EINVAL;
+  uint64_t m = 0;
+  for (uint32_t v = e->lo; v < e->hi; v++)
+    for (uint32_t s = 0; s < e->S; s++)
+      if (st_of(e->view[(size_t)v * e->R + (size_t)owner * e->S + s]) != GX_ABSENT) m |= 1ull << s;
+  *mask = m;
+  return GX_OK;
+}
+
 int gx_is_new_service(gx_engine *e, uint32_t view, const gx_service *svc, int *out) {
   grec g;
   if (!e || !svc || !out || view >= e->H || to_grec(e, svc, &g)) return GX_EINVAL;

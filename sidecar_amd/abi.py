@@ -188,7 +188,7 @@ class GxDecodeStats(C.Structure):
 
 ABI_FUNCS = [
     "gx_abi_version", "gx_backend", "gx_params_default", "gx_create", "gx_destroy", "gx_set_round",
-    "gx_get_round", "gx_epoch", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
+    "gx_get_round", "gx_epoch", "gx_owner_slots_in_use", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
     "gx_tombstone_others", "gx_tombstone_services", "gx_expire_server", "gx_send_services",
     "gx_broadcast_services", "gx_broadcast_tombstones", "gx_is_new_service", "gx_notify_msg", "gx_notify_msgs", "gx_read_view",
     "gx_get_broadcasts", "gx_local_state", "gx_merge_remote_state", "gx_notify_leave",
@@ -214,7 +214,7 @@ def _declare(lib):
         "gx_abi_version": ([], i32), "gx_backend": ([], C.c_char_p),
         "gx_params_default": ([P(GxParams)], None), "gx_create": ([P(GxParams), P(vp)], i32),
         "gx_destroy": ([vp], i32), "gx_set_round": ([vp, i64], i32),
-        "gx_get_round": ([vp, P(i64)], i32), "gx_epoch": ([vp, P(i64)], i32), "gx_enable_timing": ([vp, i32], i32),
+        "gx_get_round": ([vp, P(i64)], i32), "gx_epoch": ([vp, P(i64)], i32), "gx_owner_slots_in_use": ([vp, u32, P(C.c_uint64)], i32), "gx_enable_timing": ([vp, i32], i32),
         "gx_run_rounds": ([vp, u32], i32),
         "gx_add_service_entries": ([vp, P(u32), P(GxService), u32, P(u32)], i32),
         "gx_merge": ([vp, u32, u32], i32),
@@ -402,6 +402,12 @@ class Engine:
             check(self.lib.gx_epoch(self.h, C.byref(x)), "gx_epoch")
             self._epoch = x.value
         return self._epoch
+
+    def owner_slots_in_use(self, owner: int) -> int:
+        """Bit s set: some view of this engine holds a record for (owner, s) (gx.h)."""
+        m = C.c_uint64()
+        check(self.lib.gx_owner_slots_in_use(self.h, owner, C.byref(m)), "gx_owner_slots_in_use")
+        return m.value
 
     def word_time(self, w: int) -> int:
         """Absolute Updated of a packed view word."""

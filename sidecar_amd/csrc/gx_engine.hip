@@ -283,6 +283,8 @@ static void launch_owner(const Dev &d, hipStream_t s) {
   k_owner<T><<<nblk(d.Hl, 256 / T), 256, 0, s>>>(d);
 }
 static void owner_launch(const Dev &d, hipStream_t s) {
+  if ((d.ab & 4096u) && d.S <= 32) return launch_owner<32>(d, s);  // A/B: wider owner teams
+  if ((d.ab & 8192u) && d.S <= 64) return launch_owner<64>(d, s);
   if (d.S <= 1) launch_owner<1>(d, s);
   else if (d.S <= 2) launch_owner<2>(d, s);
   else if (d.S <= 4) launch_owner<4>(d, s);
@@ -1078,6 +1080,17 @@ int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list,
   (e->d.R % 2 == 0 ? k_scan<true, true> : k_scan<false, true>)<<<1, 256, 0, e->stream>>>(e->d, dlist, 0, e->d.L, dcnt,
                                                                                         (int)host);
   k_api_bt<<<1, 64, 0, e->stream>>>(e->d, host, mask, dlist, dcnt);
+  return sync_check(e);
+}
+
+int gx_owner_slots_in_use(gx_engine *e, uint32_t owner, uint64_t *mask) {
+  if (!e || !mask || owner >= e->d.H) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, 64);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(e->api_dev, 0, sizeof(uint64_t), e->stream));
+  k_slots_in_use<<<nblk(e->d.Hl, 256), 256, 0, e->stream>>>(e->d, owner, (unsigned long long *)e->api_dev);
+  HIPCHK(hipMemcpyAsync(mask, e->api_dev, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
   return sync_check(e);
 }
 

@@ -903,7 +903,7 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   Acc a;
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
-  if (SCAN) {
+  if (SCAN && *d.wl_cnt) {  // block-uniform: a round with no scan anywhere skips the barriers
     if (threadIdx.x == 0) s_nscan = 0;
     __syncthreads();
     if ((threadIdx.x & (T - 1)) == 0 && idx < d.Hl && d.tick[idx] == 2) s_scan[atomicAdd(&s_nscan, 1u)] = idx;
@@ -971,32 +971,25 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
   if (a.changed) mark_change(d);
 }
 
-// Phase 4a, one half-wave per receiver and two dependent loads: the receiver's inbox count, the
-// headers of its first DR packets and those packets' inline records (whole slots, loaded before
-// the count is known), then the view slot of every record. A receiver whose records are all no-ops
+// Phase 4a, LEAN_LPR lanes per receiver and three dependent loads: the receiver's inbox count and
+// the headers of its first DR packets, then the records the headers name (inline slots, only the
+// lengths given), then the view slot of every record. A receiver whose records are all no-ops
 // (stale, or no newer than the slot: see k_merge) is finished here, its merges and stale drops
 // counted. A receiver with a live record, or with more than DR packets, is flagged (mflag) and
-// merged in full by k_merge.
-#define LEAN_LPR 32  // lanes per receiver (16 lanes x 8 records measured slower: profiles/ab_flags.sh)
-#define LEAN_Q 4     // records per lane per batch
+// merged in full by k_merge. Measured (profiles/ab_gossip.sh, cfg5): 16 lanes x 4 records per
+// batch 17.8 us; 32 x 4 22.6 us; 64 x 2 24.2 us; 8 x 4 21.1 us; loading the inline slots
+// speculatively with the count (one hop less) 19-23 us: the wasted bytes cost more than the hop.
+#define LEAN_LPR 16
+#define LEAN_Q 4
 __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
   const uint32_t lane = threadIdx.x & 63, l = threadIdx.x & (LEAN_LPR - 1);
   const uint32_t vi = blockIdx.x * (256 / LEAN_LPR) + threadIdx.x / LEAN_LPR;
   const uint32_t gbase = lane & ~(uint32_t)(LEAN_LPR - 1);
-  const uint64_t gmask = (LEAN_LPR == 64 ? ~0ull : ((1ull << LEAN_LPR) - 1ull)) << gbase;
+  const uint64_t gmask = ((1ull << LEAN_LPR) - 1ull) << gbase;
   unsigned long long c_merge = 0, c_stale = 0, c_hdr = 0;
   if (vi < d.Hl) {
-    const uint32_t cap = d.p.packet_cap, nspec = d.DR * cap;
-    const grec *base = &d.in_rec[(size_t)vi * nspec];
-    grec g[LEAN_Q];
-    // A/B: bit 0 limits the speculative loads to the first `fanout` slots, bit 1 loads records
-    // only once the count and lengths are known
-    const uint32_t nsp = (d.ab & 2u) ? 0u : (d.ab & 1u) ? (d.K * cap < nspec ? d.K * cap : nspec) : nspec;
-#pragma unroll
-    for (int q = 0; q < LEAN_Q; q++) {  // hop 1: inline records, speculatively
-      const uint32_t p = l + LEAN_LPR * q;
-      if (p < nsp) g[q] = base[p];
-    }
+    const uint32_t cap = d.p.packet_cap;
+    const grec *base = &d.in_rec[(size_t)vi * d.DR * cap];
     const uint4 hd = l < d.DR ? d.in_hdr[(size_t)vi * d.DI + l] : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t cnt = d.in_cnt[vi];
     bool defer = cnt > d.DR;
@@ -1005,23 +998,18 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
       const uint32_t npos = cnt * cap;
       c_hdr = l == 0 ? cnt : 0;
       for (uint32_t p0 = 0; p0 < npos; p0 += LEAN_LPR * LEAN_Q) {
-        if (p0 || nsp < LEAN_LPR * LEAN_Q) {
-#pragma unroll
-          for (int q = 0; q < LEAN_Q; q++) {
-            const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
-            const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
-            if (p < npos && (p0 || p >= nsp) && p - sl * cap < len) g[q] = base[p];
-          }
-        }
+        grec g[LEAN_Q];
         bool valid[LEAN_Q];
-        uint64_t w0[LEAN_Q];
 #pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) {
+        for (int q = 0; q < LEAN_Q; q++) {  // hop 2: the records of the packets' used slots
           const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
           const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
           valid[q] = p < npos && p - sl * cap < len;
-          w0[q] = valid[q] ? row[g[q].r] : 0;  // hop 2
+          if (valid[q]) g[q] = base[p];
         }
+        uint64_t w0[LEAN_Q];
+#pragma unroll
+        for (int q = 0; q < LEAN_Q; q++) w0[q] = valid[q] ? row[g[q].r] : 0;  // hop 3
         bool live = false;
 #pragma unroll
         for (int q = 0; q < LEAN_Q; q++) {
@@ -2558,6 +2546,18 @@ __global__ void k_api_msg_bytes(Dev d, const grec *recs, uint32_t n, uint32_t *o
 }
 __global__ void k_fill_u16(uint16_t *p, size_t n, uint16_t v) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+// OR over this engine's views of the presence bits of owner o's S slots (gx_owner_slots_in_use):
+// one thread per view, one atomic per wave.
+__global__ void k_slots_in_use(Dev d, uint32_t o, unsigned long long *out) {
+  const uint32_t vi = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long m = 0;
+  if (vi < d.Hl) {
+    const uint64_t *w = &d.view[(size_t)vi * d.R + (size_t)o * d.S];
+    for (uint32_t s = 0; s < d.S; s++) m |= (unsigned long long)(st_of(w[s]) != GX_ABSENT) << s;
+  }
+  for (int k = 32; k > 0; k >>= 1) m |= __shfl_xor(m, k, 64);
+  if ((threadIdx.x & 63) == 0 && m) atomicOr(out, m);
 }
 __global__ void k_api_is_new(Dev d, uint32_t v, uint64_t w, uint32_t r, uint32_t *out) {
   if (threadIdx.x == 0) *out = is_new(d, v, w, r);

@@ -383,7 +383,45 @@ static void test_view_sorting() {
   }
 }
 
+// Dynamic key space of the host mirror: a new ID takes a free slot, and once the owner's S slots
+// are taken, one whose record every view has garbage-collected (services_state.go:645-653).
+static void test_slot_reuse() {
+  gx_params p = params();
+  p.n_services = 2;
+  Cluster c(p);
+  ServicesState state(c, local);
+  const std::string h = "bocaccio";
+  const int64_t t = c.Now();
+  state.AddServiceEntry(Service{"a1", h, t, sidecar::ALIVE});
+  state.AddServiceEntry(Service{"a2", h, t, sidecar::ALIVE});
+  {
+    cur = "A full table of live services refuses a third ID";
+    bool threw = false;
+    try {
+      state.AddServiceEntry(Service{"a3", h, t, sidecar::ALIVE});
+    } catch (const std::runtime_error &) {
+      threw = true;
+    }
+    So(threw);
+  }
+  {
+    cur = "After the tombstones are collected everywhere, a new ID reuses a slot";
+    state.AddServiceEntry(Service{"a1", h, t + SEC, sidecar::TOMBSTONE});
+    state.AddServiceEntry(Service{"a2", h, t + SEC, sidecar::TOMBSTONE});
+    c.Advance((3 * HOUR + 2 * MIN) / p.round_ns + 10);  // past TOMBSTONE_LIFESPAN
+    state.TombstoneOthersServices();                     // removes the old tombstones (:645-653)
+    So(!state.Get(h, "a1").has_value() && !state.Get(h, "a2").has_value());
+    state.AddServiceEntry(Service{"a3", h, c.Now(), sidecar::ALIVE});
+    So(state.Get(h, "a3").has_value());
+    auto v = state.SortedServices(h);
+    So(v.size() == 1 && v[0].ID == "a3");
+    state.AddServiceEntry(Service{"a4", h, c.Now(), sidecar::ALIVE});
+    So(state.Get(h, "a4").has_value() && state.SortedServices(h).size() == 2);
+  }
+}
+
 int main() {
+  test_slot_reuse();
   test_view_sorting();
   test_services_state_with_data();
   test_tracking_and_broadcasting();
