@@ -350,6 +350,12 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
 int gx_round_send(gx_engine *e);  /* phases 0-3: wake, owner ticks, storm, GetBroadcasts */
 int gx_outbox_bytes(gx_engine *e, uint64_t *bytes_per_shard);
 int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap);
+/* gx_outbox_bytes without waiting: the sizes are written to `bytes_per_shard` in the engine's
+ * memory (device memory for the HIP engine) by work queued on its stream, so an exchange layer
+ * can hand them to a collective (all-gather of the size matrix) with one host wait for both. The
+ * following gx_outbox_pack packs as many slots as the device counted; a `cap` smaller than that
+ * is reported as GX_EINVAL at the next call that waits. */
+int gx_outbox_sizes_async(gx_engine *e, uint64_t *bytes_per_shard);
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes);
 int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + received packets */
 /* Push-pull across shards exchanges block digests first and then only the blocks that differ

@@ -1917,6 +1917,7 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
     if ((e->msg_len[m] || fd_len_of(e, m)) && !is_local(e, e->msg_dst[m])) bytes[shard_of(e, e->msg_dst[m])] += slot_bytes(e);
   return GX_OK;
 }
+int gx_outbox_sizes_async(gx_engine *e, uint64_t *bytes) { return gx_outbox_bytes(e, bytes); }
 int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!e || (cap && !buf)) return GX_EINVAL;
   uint8_t *p = (uint8_t *)buf;

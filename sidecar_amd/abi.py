@@ -188,7 +188,7 @@ class GxDecodeStats(C.Structure):
 
 ABI_FUNCS = [
     "gx_abi_version", "gx_backend", "gx_params_default", "gx_create", "gx_destroy", "gx_set_round",
-    "gx_get_round", "gx_epoch", "gx_owner_slots_in_use", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
+    "gx_get_round", "gx_epoch", "gx_outbox_sizes_async", "gx_owner_slots_in_use", "gx_enable_timing", "gx_run_rounds", "gx_add_service_entries", "gx_merge",
     "gx_tombstone_others", "gx_tombstone_services", "gx_expire_server", "gx_send_services",
     "gx_broadcast_services", "gx_broadcast_tombstones", "gx_is_new_service", "gx_notify_msg", "gx_notify_msgs", "gx_read_view",
     "gx_get_broadcasts", "gx_local_state", "gx_merge_remote_state", "gx_notify_leave",
@@ -214,7 +214,7 @@ def _declare(lib):
         "gx_abi_version": ([], i32), "gx_backend": ([], C.c_char_p),
         "gx_params_default": ([P(GxParams)], None), "gx_create": ([P(GxParams), P(vp)], i32),
         "gx_destroy": ([vp], i32), "gx_set_round": ([vp, i64], i32),
-        "gx_get_round": ([vp, P(i64)], i32), "gx_epoch": ([vp, P(i64)], i32), "gx_owner_slots_in_use": ([vp, u32, P(C.c_uint64)], i32), "gx_enable_timing": ([vp, i32], i32),
+        "gx_get_round": ([vp, P(i64)], i32), "gx_epoch": ([vp, P(i64)], i32), "gx_outbox_sizes_async": ([vp, vp], i32), "gx_owner_slots_in_use": ([vp, u32, P(C.c_uint64)], i32), "gx_enable_timing": ([vp, i32], i32),
         "gx_run_rounds": ([vp, u32], i32),
         "gx_add_service_entries": ([vp, P(u32), P(GxService), u32, P(u32)], i32),
         "gx_merge": ([vp, u32, u32], i32),
@@ -712,6 +712,10 @@ class Engine:
         out = np.zeros(self.G, dtype=np.uint64)
         check(self.lib.gx_outbox_bytes(self.h, out.ctypes.data_as(C.c_void_p)), "gx_outbox_bytes")
         return out
+
+    def outbox_sizes_async(self, ptr: int):
+        """Per-shard outbox bytes into engine memory at ptr (device memory on the HIP engine)."""
+        check(self.lib.gx_outbox_sizes_async(self.h, C.c_void_p(ptr)), "gx_outbox_sizes_async")
 
     def outbox_pack(self, ptr: int, cap: int):
         check(self.lib.gx_outbox_pack(self.h, C.c_void_p(ptr), cap), "gx_outbox_pack")

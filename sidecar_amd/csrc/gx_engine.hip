@@ -85,6 +85,8 @@ struct gx_engine {
   uint32_t *ob_entries;
   uint32_t *ob_counts;  // [G] packets per destination shard, then [chunks][G] counts and offsets
   uint32_t n_ob;
+  bool ob_async;        // the outbox slot count is on the device only (gx_outbox_sizes_async)
+  uint32_t *ob_total;   // [1] that count
   uint32_t *ae_pa, *ae_pb, *ae_pack_host, *ae_pack_t, *ae_pack_other;
   uint8_t *ae_pack_first, *ae_skip;  // this side is the pair's initiator; the pair does not run
   uint64_t *fd_rsnap;                // [pairs][H] partner member lists received with the digests
@@ -622,7 +624,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf,
@@ -675,6 +677,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ob_entries = nullptr;
   e->ob_counts = nullptr;
   e->n_ob = 0;
+  e->ob_async = false;
+  e->ob_total = nullptr;
   e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = e->ae_pack_other = nullptr;
   e->ae_pack_first = e->ae_skip = nullptr;
   e->fd_rsnap = nullptr;
@@ -786,6 +790,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
   if (d.G > 1) {
     ALLOC(e->ob_entries, sizeof(uint32_t) * H * K);
+    ALLOC(e->ob_total, sizeof(uint32_t));
     ALLOC(e->ob_counts, sizeof(uint32_t) * p->n_shards * (1 + 2 * ((H * K + 255) / 256)));
     size_t np = Hg / 2 + 1;
     ALLOC(e->ae_pa, sizeof(uint32_t) * np);
@@ -1600,6 +1605,7 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   Dev &d = e->d;
   for (uint32_t g = 0; g < d.G; g++) bytes[g] = 0;
   e->n_ob = 0;
+  e->ob_async = false;
   if (d.G < 2 || !d.K) return GX_OK;
   set_round_fields(e);
   const size_t ne = (size_t)d.Hl * d.KE;
@@ -1622,8 +1628,39 @@ int gx_outbox_bytes(gx_engine *e, uint64_t *bytes) {
   return GX_OK;
 }
 
+int gx_outbox_sizes_async(gx_engine *e, uint64_t *bytes) {
+  if (!e || !bytes) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  Dev &d = e->d;
+  e->n_ob = 0;
+  e->ob_async = false;
+  if (d.G < 2 || !d.K) {
+    HIPCHK(hipMemsetAsync(bytes, 0, sizeof(uint64_t) * d.G, e->stream));
+    return phase_done(e);
+  }
+  set_round_fields(e);
+  const size_t ne = (size_t)d.Hl * d.KE;
+  const uint32_t nchunk = (uint32_t)((ne + 255) / 256);
+  uint32_t *ccnt = e->ob_counts + d.G, *off = ccnt + (size_t)nchunk * d.G;
+  const size_t lds = sizeof(uint32_t) * 4 * d.G;
+  k_ob_count<<<nchunk, 256, lds, e->stream>>>(d, ccnt);
+  k_ob_scan<<<1, 256, 0, e->stream>>>(d, ccnt, nchunk, off, e->ob_counts);
+  k_ob_fill<<<nchunk, 256, lds, e->stream>>>(d, off, e->ob_entries);
+  k_ob_bytes<<<1, 64, 0, e->stream>>>(d, e->ob_counts, (unsigned long long *)bytes, e->ob_total);
+  e->ob_async = true;
+  return phase_done(e);
+}
+
 int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!e || (cap && !buf)) return GX_EINVAL;
+  if (e->ob_async) {  // the slot count is on the device: a grid of the largest possible count
+    HIPCHK(hipSetDevice(e->device));
+    e->ob_async = false;
+    const uint32_t cap_slots = (uint32_t)(cap / slot_bytes(e->d));
+    const uint32_t nmax = e->d.Hl * e->d.KE;
+    if (nmax) k_outbox_pack<<<nmax, 64, 0, e->stream>>>(e->d, e->ob_entries, 0, (uint8_t *)buf, e->ob_total, cap_slots);
+    return phase_done(e);
+  }
   if (!e->n_ob) return GX_OK;
   if (cap < e->n_ob * slot_bytes(e->d)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));

@@ -2239,8 +2239,26 @@ __global__ __launch_bounds__(256) void k_ob_fill(Dev d, const uint32_t *off, uin
 }
 
 // Outbox: fixed-size slots (16-B header + packet_cap records); slot index per local entry.
-__global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t *out) {
+// gx_outbox_sizes_async: bytes per destination shard and the slot total, from k_ob_scan's counts
+__global__ void k_ob_bytes(Dev d, const uint32_t *tot, unsigned long long *bytes, uint32_t *n_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t sb = 16 + 16ull * d.p.packet_cap + 16ull * (d.p.fd_enable ? d.p.fd_msg_cap : 0);
+  uint32_t n = 0;
+  for (uint32_t g = 0; g < d.G; g++) {
+    bytes[g] = (unsigned long long)tot[g] * sb;
+    n += tot[g];
+  }
+  *n_out = n;
+}
+// n_dev: the slot count on the device (gx_outbox_sizes_async); slots past cap_slots are refused
+__global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t *out, const uint32_t *n_dev = nullptr,
+                              uint32_t cap_slots = 0xffffffffu) {
   uint32_t i = blockIdx.x;
+  if (n_dev) {
+    n = *n_dev;
+    if (i == 0 && threadIdx.x == 0 && n > cap_slots) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);
+    if (n > cap_slots) n = cap_slots;
+  }
   if (i >= n) return;
   uint32_t e = entry[i];
   const uint32_t fcap = d.p.fd_enable ? d.p.fd_msg_cap : 0;

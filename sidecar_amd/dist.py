@@ -91,7 +91,7 @@ class LocalShards:
 
     def _exchange(self, sizes_fn, pack_fn, after_pack=None) -> List[torch.Tensor]:
         """Every shard packs per destination; returns each shard's inbox (sources ascending)."""
-        sizes = [sizes_fn(s.e) for s in self.shards]  # sizes[src][dst]
+        sizes = [sizes_fn(s) for s in self.shards]  # sizes[src][dst]
         self.last_sizes = sizes
         bufs = [s.pack(sz, lambda p, n, e=s.e: pack_fn(e, p, n)) for s, sz in zip(self.shards, sizes)]
         if after_pack is not None:
@@ -110,11 +110,17 @@ class LocalShards:
             s.sync()
         return inboxes
 
+    def _outbox_sizes(self, s) -> np.ndarray:
+        """The shard's outbox sizes through gx_outbox_sizes_async (written by the device)."""
+        t = torch.zeros(self.G, dtype=torch.int64, device=self.device)
+        s.e.outbox_sizes_async(_ptr(t))
+        return t.cpu().numpy().astype(np.uint64)
+
     def run_rounds(self, n: int):
         for _ in range(n):
             for s in self.shards:
                 s.e.round_send()
-            inb = self._exchange(lambda e: e.outbox_bytes(), lambda e, p, c: e.outbox_pack(p, c))
+            inb = self._exchange(self._outbox_sizes, lambda e, p, c: e.outbox_pack(p, c))
             self.wire.packets += int(sum(int(x.sum()) for x in self.last_sizes))
             for s, x in zip(self.shards, inb):
                 s.e.inbox_unpack(_ptr(x), x.numel())
@@ -123,15 +129,15 @@ class LocalShards:
             # push-pull: digests, the blocks each side leads, the partners' return blocks (gx.h);
             # shard-local pairs overlap the exchanges. Every shard agrees on the AE rounds.
             if self.shards[0].e.is_ae_round():
-                dig = self._exchange(lambda e: e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
+                dig = self._exchange(lambda s: s.e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
                                      after_pack=lambda e: e.ae_merge_local())
                 dig_sizes = self.last_sizes
                 lead_sizes = {id(s.e): s.e.ae_delta_bytes(_ptr(x), x.numel()) for s, x in zip(self.shards, dig)}
-                lead = self._exchange(lambda e: lead_sizes[id(e)], lambda e, p, c: e.ae_delta_pack(p, c))
+                lead = self._exchange(lambda s: lead_sizes[id(s.e)], lambda e, p, c: e.ae_delta_pack(p, c))
                 lead_sz = self.last_sizes
                 ret_sizes = {id(s.e): s.e.ae_return_bytes(_ptr(x), x.numel()) for s, x in zip(self.shards, lead)}
                 lead_of = {id(s.e): x for s, x in zip(self.shards, lead)}
-                ret = self._exchange(lambda e: ret_sizes[id(e)],
+                ret = self._exchange(lambda s: ret_sizes[id(s.e)],
                                      lambda e, p, c: e.ae_return_pack(_ptr(lead_of[id(e)]), lead_of[id(e)].numel(), p, c))
                 for a, b, c in zip(dig_sizes, lead_sz, self.last_sizes):
                     self.wire.add_ae(a, b, c)
@@ -186,18 +192,24 @@ class DistShard:
 
     CHUNK = 256 << 20  # bytes per peer per all-to-all call
 
-    def _exchange(self, sizes: np.ndarray, packer, after_pack=None) -> torch.Tensor:
-        """all-to-all of this shard's per-destination messages; returns the inbox (sources ascending)."""
+    def _exchange(self, sizes, packer, after_pack=None) -> torch.Tensor:
+        """all-to-all of this shard's per-destination messages; returns the inbox (sources ascending).
+        `sizes`: host array, or a device tensor the engine filled (gx_outbox_sizes_async), which
+        then travels in the size all-gather without a host wait of its own."""
         dist = self.dist
         # every rank learns the whole size matrix in one collective: its receive sizes, and the
         # number of chunked calls all ranks make
-        mine = torch.tensor(sizes.astype(np.int64), device=self.device)
+        if isinstance(sizes, torch.Tensor):
+            mine = sizes
+        else:
+            mine = torch.tensor(sizes.astype(np.int64), device=self.device)
         rows = [torch.empty_like(mine) for _ in range(self.world)]
         dist.all_gather(rows, mine, group=self.group)
-        m = torch.stack(rows).tolist()  # m[src][dst]
+        m = torch.stack(rows).tolist()  # m[src][dst]: the one host wait of the exchange
         ss = [int(x) for x in m[self.rank]]
         rs = [int(m[src][self.rank]) for src in range(self.world)]
-        send = self.s.pack(sizes, packer)
+        self.last_sizes = np.array(ss, dtype=np.uint64)
+        send = self.s.pack(self.last_sizes, packer)
         if after_pack is not None:
             after_pack()  # device work on the engine stream that overlaps the collective
         recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
@@ -228,9 +240,10 @@ class DistShard:
         e = self.e
         for _ in range(n):
             e.round_send()
-            ob = e.outbox_bytes()
-            self.wire.packets += int(ob.sum())
+            ob = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+            e.outbox_sizes_async(_ptr(ob))  # no host wait: the sizes join the size all-gather
             x = self._exchange(ob, e.outbox_pack)
+            self.wire.packets += int(self.last_sizes.sum())
             e.inbox_unpack(_ptr(x), x.numel())
             e.round_merge()
             # push-pull: digests, lead blocks, return blocks (local pairs overlap the exchanges)
