@@ -282,7 +282,7 @@ static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1
 // k_owner with a team of T >= S lanes per host (lane s = service s)
 template <int T>
 static void launch_owner(const Dev &d, hipStream_t s) {
-  k_owner<T><<<nblk(d.Hl, 256 / T), 256, 0, s>>>(d);
+  k_owner<T><<<nblk(d.Hl, 256 / T), 256, 0, s>>>(d);  // 64- and 128-thread blocks measured 13.6 / 12.6 vs 12.5 us
 }
 // teams of the smallest power of two >= S (16 -> 32 -> 64 lanes measured 12.3 / 17.4 / 29.2 us at cfg 5)
 static void owner_launch(const Dev &d, hipStream_t s) {
@@ -336,6 +336,7 @@ static int round_send_impl(gx_engine *e) {
     // 4 lanes per host: measured best of 1/4/8/16/64 (profiles/send_team.sh)
     const bool ev = !e->log_views.empty();
     const unsigned g = nblk(d.Hl, 64);
+    // teams of 2 / 8 lanes measured 25.6 / 28.7 vs 21.1 us (profiles/r02/gossip/send_team_ab.log)
     if (scan_in_send) {
       if (d.departures)
         (vec ? (ev ? k_send<4, true, true, true, true> : k_send<4, true, true, true, false>)
@@ -362,7 +363,8 @@ static int round_merge_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
     k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);
-    const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE);
+    const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE_DEF);
+    // 2 or 4 receivers per wave measured 14.2 / 13.7 vs 14.3 us (profiles/r02/gossip)
     if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
     else (ev ? k_merge<false, true> : k_merge<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
   }

@@ -321,15 +321,15 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
   return queued;
 }
 
-template <int T>
-__global__ __launch_bounds__(256) void k_owner(Dev d) {
-  __shared__ gx_job s_sl[256];  // the head of each host's sleep ring, one job per team lane
+template <int T, int B = 256>
+__global__ __launch_bounds__(B) void k_owner(Dev d) {
+  __shared__ gx_job s_sl[B];  // the head of each host's sleep ring, one job per team lane
   Acc a;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next round's lists start empty
     *d.ovf_cnt_nx = 0;
     *d.wl_cnt_nx = 0;
   }
-  owner_tick<T>(d, a, blockIdx.x * (256 / T) + threadIdx.x / T, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
+  owner_tick<T>(d, a, blockIdx.x * (B / T) + threadIdx.x / T, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
   acc_flush(d, a);
 }
 
@@ -1041,8 +1041,8 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
 
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
-#define MERGE_RANGE 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
-template <bool K32, bool EV>
+#define MERGE_RANGE_DEF 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
+template <bool K32, bool EV, int MERGE_RANGE = MERGE_RANGE_DEF>
 __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
   // one receiver per wave, MERGE_WAVES per block; the waves share nothing (wave-level sync only)
   __shared__ uint4 s_hdr_[MERGE_WAVES][64];
