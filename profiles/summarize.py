@@ -38,7 +38,15 @@ for k, v in agg.items():
         v["hbm_bytes_per_launch"] = int((2 * f + w) * 1024)
     for kk, c in cls.items():
         if k == kk:
-            summary[c] = v
+            summary[c] = dict(v)
+# the gossip merge class is two launches per round (k_merge_lean, then k_merge for the flagged
+# receivers): its traffic per round is their sum (both launch once per round)
+if "k_merge_lean" in agg and "merge" in summary:
+    m, l = summary["merge"], agg["k_merge_lean"]
+    for key in ("FETCH_SIZE_KB_per_launch", "WRITE_SIZE_KB_per_launch", "hbm_bytes_per_launch"):
+        if key in m and key in l:
+            m[key] = m[key] + l[key]
+    m["kernels"] = ["k_merge_lean", "k_merge"]
 json.dump(dict(agg), open(f"{dst}/cfg5_pmc.json", "w"), indent=1, sort_keys=True)
 pmc = {}
 if os.path.exists("profiles/pmc_summary.json"):
