@@ -99,6 +99,7 @@ struct gx_engine {
   uint32_t *ae_mask;   // [Hl][nmw] differing blocks this side leads
   uint32_t *ae_fmask;  // [Hl][nmw] differing blocks the partner leads
   uint16_t *ae_lt;     // [Hl][nblk] the partner's literal counts (its digests)
+  uint16_t *ae_retL;   // [Hl][nblk] literal counts of this side's return blocks (follow order)
   uint32_t *ae_bcnt;   // [Hl][nblk] own blocks: present | stale << 16 (digest pass)
   uint32_t *ae_cnt;    // [Hl] blocks this side leads
   uint32_t *ae_nfol;   // [Hl] blocks the partner leads
@@ -626,7 +627,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf,
@@ -689,6 +690,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->ae_dig = nullptr;
   e->ae_mask = e->ae_fmask = e->ae_cnt = e->ae_nfol = e->ae_err = nullptr;
   e->ae_lt = nullptr;
+  e->ae_retL = nullptr;
   e->ae_bcnt = nullptr;
   e->ae_sz = e->ae_off = e->ae_rioff = nullptr;
   e->ae_delta_round = e->ae_ret_round = -1;
@@ -811,6 +813,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->ae_mask, sizeof(uint32_t) * H * e->nmw);
     ALLOC(e->ae_fmask, sizeof(uint32_t) * H * e->nmw);
     ALLOC(e->ae_lt, sizeof(uint16_t) * H * e->nblk);
+    ALLOC(e->ae_retL, sizeof(uint16_t) * H * e->nblk);
     ALLOC(e->ae_bcnt, sizeof(uint32_t) * H * e->nblk);
     ALLOC(e->ae_cnt, sizeof(uint32_t) * H);
     ALLOC(e->ae_nfol, sizeof(uint32_t) * H);
@@ -1860,8 +1863,13 @@ int gx_ae_delta_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (!e->n_pack) return GX_OK;
   if (e->ae_delta_round != (int)e->d.round || cap < e->delta_total) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  k_ae_lead_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
-                                                    e->ae_off, e->nmw, (uint8_t *)buf);
+  if (e->nblk <= XS_MAXB)  // offsets up front, a wave per block (profiles/ab_shard_ae.sh)
+    k_ae_lead_pack_w<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
+                                                        e->ae_off, e->nmw, (const ulonglong2 *)e->ae_dig, e->nblk,
+                                                        (uint8_t *)buf);
+  else
+    k_ae_lead_pack<<<e->n_pack, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_mask, e->ae_cnt,
+                                                      e->ae_off, e->nmw, (uint8_t *)buf);
   return phase_done(e);
 }
 
@@ -1877,9 +1885,14 @@ int gx_ae_return_bytes(gx_engine *e, const void *lead, uint64_t lead_bytes, uint
   const uint32_t np = e->n_pack;
   if (d.G < 2 || !ae_round(e) || !np) return lead_bytes ? GX_EINVAL : GX_OK;
   if (e->ae_delta_round != (int)d.round || lead_bytes != e->lead_in_total) return GX_EINVAL;
-  k_ae_ret<true><<<np, 256, 0, e->stream>>>(d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
-                                            (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
-                                            e->ae_sz + 2 * np, nullptr, nullptr, nullptr);
+  if (e->nblk <= XS_MAXB)
+    k_ae_ret_w<true><<<np, 256, 0, e->stream>>>(d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
+                                                (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
+                                                e->ae_sz + 2 * np, nullptr, nullptr, nullptr, e->ae_retL);
+  else
+    k_ae_ret<true><<<np, 256, 0, e->stream>>>(d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
+                                              (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
+                                              e->ae_sz + 2 * np, nullptr, nullptr, nullptr);
   std::vector<uint64_t> rsz(np);
   HIPCHK(hipMemcpyAsync(rsz.data(), e->ae_sz + 2 * np, sizeof(uint64_t) * np, hipMemcpyDeviceToHost, e->stream));
   int rc = sync_main(e);
@@ -1909,10 +1922,16 @@ int gx_ae_return_pack(gx_engine *e, const void *lead, uint64_t lead_bytes, void 
   if (!np) return GX_OK;
   if (e->ae_ret_round != (int)e->d.round || cap < e->ret_total || lead_bytes != e->lead_in_total) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  k_ae_ret<false><<<np, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
-                                             (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
-                                             e->ae_sz + 2 * np, e->ae_off + 2 * np, e->ae_off + 3 * np,
-                                             (uint8_t *)buf);
+  if (e->nblk <= XS_MAXB)
+    k_ae_ret_w<false><<<np, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol,
+                                                 e->ae_lt, (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
+                                                 e->ae_sz + 2 * np, e->ae_off + 2 * np, e->ae_off + 3 * np,
+                                                 (uint8_t *)buf, e->ae_retL);
+  else
+    k_ae_ret<false><<<np, 256, 0, e->stream>>>(e->d, e->ae_pack_host, e->ae_pack_t, e->ae_fmask, e->ae_nfol, e->ae_lt,
+                                               (const uint8_t *)lead, e->ae_off + np, e->nblk, e->nmw,
+                                               e->ae_sz + 2 * np, e->ae_off + 2 * np, e->ae_off + 3 * np,
+                                               (uint8_t *)buf);
   return phase_done(e);
 }
 

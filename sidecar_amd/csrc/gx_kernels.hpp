@@ -2097,6 +2097,200 @@ GXD bool ret_own(const Dev &d, uint64_t x, uint64_t y) {
   if (sy) return sx;
   return !sx && ts_of(y) <= ts_of(x);
 }
+// ---- wave-per-block lead and return encoding (nblk <= XS_MAXB) --------------------------------
+// Every lead (follow) block's message offset is computed up front by a block scan into LDS, then
+// the four waves encode blocks side by side with no barrier between blocks. Slot s of a block is
+// lane s % 64 of word s / 64, so the own and neu mask words are plain wave ballots.
+GXD uint64_t lanes_below(uint32_t lane) { return (1ull << lane) - 1ull; }
+// a wave writes one encoded block: masks from lane 0, literals from the lanes that start a run
+GXD void wave_enc_store(uint64_t *enc, const uint64_t *w, const bool *nwf, const uint64_t *om, const uint64_t *nm,
+                        uint32_t lane) {
+  uint32_t base = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    if (nwf[q]) enc[16 + base + __popcll(nm[q] & lanes_below(lane))] = w[q];
+    base += __popcll(nm[q]);
+  }
+  if (lane < 8) {
+    uint64_t a = 0, b = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      a = lane == (uint32_t)q ? om[q] : a;
+      b = lane == (uint32_t)q ? nm[q] : b;
+    }
+    enc[lane] = a;
+    enc[8 + lane] = b;
+  }
+}
+__global__ __launch_bounds__(256) void k_ae_lead_pack_w(Dev d, const uint32_t *host, const uint32_t *pair_t,
+                                                         const uint32_t *lmask, const uint32_t *nlead,
+                                                         const uint64_t *off, uint32_t nmw, const ulonglong2 *own,
+                                                         uint32_t nblk, uint8_t *out) {
+  __shared__ uint32_t s_off[XS_MAXB];
+  __shared__ uint16_t s_blk[XS_MAXB];
+  __shared__ unsigned long long s_wave[4];
+  const uint32_t k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint8_t *msg = out + off[k];
+  if (t == 0) {
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
+    hdr[0] = pair_t[k];
+    hdr[1] = host[k];
+    hdr[2] = nlead[k];
+    hdr[3] = 0;
+  }
+  const uint32_t *lm = lmask + (size_t)k * nmw;
+  const ulonglong2 *dg = own + (size_t)k * nblk;
+  const uint32_t c = (nblk + blockDim.x - 1) / blockDim.x, b0 = t * c, b1 = b0 + c < nblk ? b0 + c : nblk;
+  uint32_t nl = 0, sz = 0;
+  for (uint32_t b = b0; b < b1; b++)
+    if ((lm[b >> 5] >> (b & 31)) & 1u) {
+      nl++;
+      sz += 128 + 8u * (uint32_t)(dg[b].y >> 54);  // the block's literal count (digest pass)
+    }
+  unsigned long long tot;
+  const unsigned long long pre = block_excl_scan64((unsigned long long)nl | ((unsigned long long)sz << 32), s_wave, tot);
+  uint32_t j = (uint32_t)pre, o = (uint32_t)(pre >> 32);
+  for (uint32_t b = b0; b < b1; b++)
+    if ((lm[b >> 5] >> (b & 31)) & 1u) {
+      s_blk[j] = (uint16_t)b;
+      s_off[j++] = o;
+      o += 128 + 8u * (uint32_t)(dg[b].y >> 54);
+    }
+  __syncthreads();
+  const uint32_t n_lead = (uint32_t)tot;
+  const uint64_t *row = vrow(d, host[k]);
+  for (uint32_t jj = wv; jj < n_lead; jj += 4) {
+    const uint32_t b = s_blk[jj], lo = b * GX_DIGEST_SLOTS;
+    const uint32_t nv = lo + GX_DIGEST_SLOTS <= d.R ? GX_DIGEST_SLOTS : d.R - lo;
+    uint64_t w[8], om[8], nm[8];
+    bool nwf[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) w[q] = 64u * q + lane < nv ? row[lo + 64u * q + lane] : 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t sl = 64u * q + lane;
+      uint64_t pw = __shfl_up(w[q], 1, 64);
+      const uint64_t carry = q ? __shfl(w[q - 1], 63, 64) : 0;  // every lane shuffles (lane 63 must be active)
+      if (lane == 0) pw = carry;
+      const bool v = sl < nv;
+      nwf[q] = v && (sl == 0 || w[q] != pw);
+      om[q] = __ballot(!v);
+      nm[q] = __ballot(nwf[q]);
+    }
+    wave_enc_store(reinterpret_cast<uint64_t *>(msg + 16 + s_off[jj]), w, nwf, om, nm, lane);
+  }
+}
+// COUNT: the return message sizes (rsz) and every block's literal count (retL, in follow order);
+// the pack pass lays the blocks out from those counts.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_ae_ret_w(Dev d, const uint32_t *host, const uint32_t *pair_t,
+                                                   const uint32_t *fmask, const uint32_t *nfol, const uint16_t *lt,
+                                                   const uint8_t *lead, const uint64_t *ioff, uint32_t nblk,
+                                                   uint32_t nmw, uint64_t *rsz, const uint64_t *roff,
+                                                   const uint64_t *rtab, uint8_t *out, uint16_t *retL) {
+  __shared__ uint32_t s_li[XS_MAXB], s_ro[XS_MAXB];
+  __shared__ uint16_t s_blk[XS_MAXB];
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_sum;
+  const uint32_t k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nf = nfol[k];
+  const uint8_t *lm = lead + ioff[k];
+  uint8_t *msg = COUNT ? nullptr : out + roff[k];
+  uint16_t *rl = retL + (size_t)k * nblk;
+  const uint32_t hdr_bytes = 16 + 4u * (nf + (nf & 1u));
+  if (t == 0) {
+    s_sum = 0;
+    if (!COUNT) {
+      uint32_t *hdr = reinterpret_cast<uint32_t *>(msg);
+      hdr[0] = pair_t[k];
+      hdr[1] = host[k];
+      hdr[2] = nf;
+      hdr[3] = 0;
+      if (nf & 1u) hdr[4 + nf] = 0;
+      *reinterpret_cast<uint64_t *>(out + rtab[k]) = rsz[k];
+    }
+  }
+  const uint32_t *fm = fmask + (size_t)k * nmw;
+  const uint16_t *plt = lt + (size_t)k * nblk;
+  const uint32_t c = (nblk + blockDim.x - 1) / blockDim.x, b0 = t * c, b1 = b0 + c < nblk ? b0 + c : nblk;
+  uint32_t n = 0, lsz = 0;
+  for (uint32_t b = b0; b < b1; b++)
+    if ((fm[b >> 5] >> (b & 31)) & 1u) {
+      n++;
+      lsz += 128 + 8u * plt[b];
+    }
+  unsigned long long tot;
+  const unsigned long long pre = block_excl_scan64((unsigned long long)n | ((unsigned long long)lsz << 32), s_wave, tot);
+  uint32_t j = (uint32_t)pre, li_ = 16 + (uint32_t)(pre >> 32);
+  const uint32_t j0 = j;
+  uint32_t rs = 0;
+  for (uint32_t b = b0; b < b1; b++)
+    if ((fm[b >> 5] >> (b & 31)) & 1u) {
+      s_blk[j] = (uint16_t)b;
+      s_li[j] = li_;
+      li_ += 128 + 8u * plt[b];
+      if (!COUNT) rs += 128 + 8u * rl[j];
+      j++;
+    }
+  if (!COUNT) {
+    const unsigned long long rpre = block_excl_scan64(rs, s_wave, tot);
+    uint32_t ro = hdr_bytes + (uint32_t)rpre;
+    for (uint32_t q = j0; q < j; q++) {
+      s_ro[q] = ro;
+      ro += 128 + 8u * rl[q];
+    }
+  }
+  __syncthreads();
+  const uint64_t *row = vrow(d, host[k]);
+  unsigned long long wsum = 0;
+  for (uint32_t jj = wv; jj < nf; jj += 4) {
+    const uint32_t b = s_blk[jj], lo = b * GX_DIGEST_SLOTS;
+    const uint32_t nv = lo + GX_DIGEST_SLOTS <= d.R ? GX_DIGEST_SLOTS : d.R - lo;
+    const uint64_t *xe = reinterpret_cast<const uint64_t *>(lm + s_li[jj]);  // the partner's lead block
+    uint64_t xm[8], y[8], om[8], nm[8];
+    bool ownf[8], nwf[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      xm[q] = xe[8 + q];
+      y[q] = 64u * q + lane < nv ? row[lo + 64u * q + lane] : 0;
+    }
+    uint32_t base = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const bool v = 64u * q + lane < nv;
+      // the partner's word: the literal of the run holding this slot (its own bits are padding)
+      const uint32_t rank = base + __popcll(xm[q] & ((2ull << lane) - 1ull)) - 1;
+      ownf[q] = !v || ret_own(d, xe[16 + rank], y[q]);
+      base += __popcll(xm[q]);
+      om[q] = __ballot(ownf[q]);
+    }
+    uint32_t L = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t sl = 64u * q + lane;
+      uint64_t yp = __shfl_up(y[q], 1, 64);
+      const uint64_t carry = q ? __shfl(y[q - 1], 63, 64) : 0;
+      if (lane == 0) yp = carry;
+      const bool op = sl == 0 || (lane ? (om[q] >> (lane - 1)) & 1ull : (q ? om[q - 1] >> 63 : 1ull));
+      nwf[q] = !ownf[q] && (op || y[q] != yp);
+      nm[q] = __ballot(nwf[q]);
+      L += __popcll(nm[q]);
+    }
+    if (COUNT) {
+      if (lane == 0) rl[jj] = (uint16_t)L;
+      wsum += 128 + 8ull * L;
+    } else {
+      wave_enc_store(reinterpret_cast<uint64_t *>(msg + s_ro[jj]), y, nwf, om, nm, lane);
+      if (lane == 0) reinterpret_cast<uint32_t *>(msg + 16)[jj] = L;
+    }
+  }
+  if (COUNT) {
+    if (lane == 0 && wsum) atomicAdd(&s_sum, wsum);
+    __syncthreads();
+    if (t == 0) rsz[k] = hdr_bytes + s_sum;
+  }
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_ae_ret(Dev d, const uint32_t *host, const uint32_t *pair_t,
                                                  const uint32_t *fmask, const uint32_t *nfol, const uint16_t *lt,
