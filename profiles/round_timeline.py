@@ -1,6 +1,7 @@
 """Per-round kernel timeline of the gossip path from a rocprofv3 kernel trace: for every round
-(delimited by k_owner dispatches), each kernel's duration and the round's device span from the
-first dispatch's start to the last gossip kernel's end (push-pull and storm kernels excluded).
+(from k_owner, or from k_send when it runs the owner ticks itself), each kernel's duration and
+the round's device span from the first dispatch's start to the last gossip kernel's end
+(push-pull and storm kernels excluded).
 
   python profiles/round_timeline.py <run_kernel_trace.csv> [skip_rounds]
 """
@@ -18,7 +19,8 @@ for r in rows:
 ks.sort()
 rounds, cur = [], None
 for s, e, n in ks:
-    if n == "k_owner":
+    # a round starts at k_owner, or at k_send when the owner ticks run inside it (fused launch)
+    if n == "k_owner" or (n == "k_send" and (cur is None or any(x[2] == "k_merge" for x in cur))):
         cur = []
         rounds.append(cur)
     if cur is not None and n in GOSSIP:

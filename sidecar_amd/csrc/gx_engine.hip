@@ -307,6 +307,21 @@ static int round_send_impl(gx_engine *e) {
   const bool storm = d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2;
   // BroadcastTombstones' SendServices is queued before the detector's and the storm's jobs
   const bool bt_apart = d.p.fd_enable || storm;
+  // a plain round without listeners: owner ticks, expiry scans and sends in one launch
+  const bool fused = !bt_apart && !d.departures && d.K && e->log_views.empty() && !(d.ab & 8u);
+  if (fused) {
+    LaunchTimer t(e, GX_K_SEND);
+    const unsigned g = nblk(d.Hl, 64);
+#define GX_TICK_SEND(SPL) (vec ? k_send<4, false, true, true, false, SPL> : k_send<4, false, true, false, false, SPL>)<<<g, 256, 0, s>>>(d, 1)
+    if (d.S <= 4) GX_TICK_SEND(1);
+    else if (d.S <= 8) GX_TICK_SEND(2);
+    else if (d.S <= 16) GX_TICK_SEND(4);
+    else if (d.S <= 32) GX_TICK_SEND(8);
+    else GX_TICK_SEND(16);
+#undef GX_TICK_SEND
+    HIPCHK(hipGetLastError());
+    return GX_OK;
+  }
   {
     LaunchTimer t(e, GX_K_OWNER);
     owner_launch(d, s);

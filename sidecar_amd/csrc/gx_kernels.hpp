@@ -169,9 +169,11 @@ __global__ void k_wake(Dev d) {
 // TombstoneOthersServices (:645-662); the others go to the expiry scan's worklist. Also clears the
 // next round's inbox counts (round-parity buffers, Dev::in_cnt_nx).
 // The tick of host idx by its team (T lanes inside one wave); sj = the team's T LDS job slots (the
-// head of the sleep ring). Returns, on the lead lane, whether the host went on the expiry-scan
-// worklist (its BroadcastTombstones tick then finishes after the scan).
-template <int T>
+// head of the sleep ring). Lane tl holds services tl + T*i, i < SPL (SPL = 1 when T >= S); a
+// team-wide service mask is the OR of each lane's ballot shifted by T*i. Returns, on the lead
+// lane, whether the host went on the expiry-scan worklist (its BroadcastTombstones tick then
+// finishes after the scan).
+template <int T, int SPL = 1>
 GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lead = tl == 0;
@@ -179,17 +181,32 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
   const bool act = idx < d.Hl && !departed(d, d.lo + idx);
   bool queued = false;
   gx_host_state hs;
+  auto team_mask = [&](const bool *p) -> uint64_t {  // bit s = service s's predicate
+    uint64_t m = 0;
+#pragma unroll
+    for (int i = 0; i < SPL; i++) m |= ((__ballot(p[i]) >> (tw * T)) & tmask) << (T * i);
+    return m;
+  };
   // everything the tick may read is loaded up front: the bookkeeping, the own records' view slots
   // (one 128-B row segment), their local status and the view's expiry bound
-  uint64_t cur0 = GX_SLOT_ABSENT;
-  uint8_t ost0 = GX_ALIVE;
+  uint64_t cur0[SPL];
+  uint8_t ost0[SPL];
+#pragma unroll
+  for (int i = 0; i < SPL; i++) {
+    cur0[i] = GX_SLOT_ABSENT;
+    ost0[i] = GX_ALIVE;
+  }
   unsigned long long mexp0 = 0;
   if (act) {
     hs = d.hs[idx];
     const uint32_t o = d.lo + idx;
-    if (tl < d.S) {
-      cur0 = vrow(d, o)[o * d.S + tl];
-      ost0 = d.own_status[(size_t)idx * d.S + tl];
+#pragma unroll
+    for (int i = 0; i < SPL; i++) {
+      const uint32_t sv = tl + T * i;
+      if (sv < d.S) {
+        cur0[i] = vrow(d, o)[o * d.S + sv];
+        ost0[i] = d.own_status[(size_t)idx * d.S + sv];
+      }
     }
     if (tl == 0) mexp0 = d.minexp[idx];
     if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
@@ -208,33 +225,40 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
         hs.sleep_head++;
         push_job_r(d, a, o, hs, j, lead);
       }
-      const uint32_t s = tl;
-      const bool svc = s < d.S;
-      uint8_t ost = ost0;
+      uint8_t ost[SPL];
+#pragma unroll
+      for (int i = 0; i < SPL; i++) ost[i] = ost0[i];
       if (d.p.churn_ppm) {  // discovery churn: one service starts or stops
         const uint64_t x = rng4(d.p.seed, ST_CHURN, (uint64_t)d.round, o, 0);
         if ((uint32_t)(x & 0xffffffffu) % 1000000u < d.p.churn_ppm) {
           const uint32_t cs = (uint32_t)((x >> 32) % d.S);
           hs.running ^= 1ull << cs;
-          if (s == cs && ((hs.running >> cs) & 1ull)) {
-            ost = GX_ALIVE;
-            d.own_status[(size_t)idx * d.S + s] = GX_ALIVE;
-          }
+#pragma unroll
+          for (int i = 0; i < SPL; i++)
+            if (tl + T * i == cs && ((hs.running >> cs) & 1ull)) {
+              ost[i] = GX_ALIVE;
+              d.own_status[(size_t)idx * d.S + cs] = GX_ALIVE;
+            }
           if (lead) a.c[C_CHURN]++;
         }
       }
       if (!(hs.flags & 1u) && hs.bs_next <= d.round) {
-        // fn(): the running services in key order, restamped now; lane s holds service s
-        const bool run = svc && ((hs.running >> s) & 1ull);
-        const uint32_t r = o * d.S + s;
-        uint64_t *slot = &vrow(d, o)[run ? r : o * d.S];
-        const uint64_t sw = pack(d.now, ost);
-        const uint64_t cur = run ? cur0 : GX_SLOT_ABSENT;  // no other writer of own slots before this
-        const bool isnew = run && (st_of(cur) == GX_ABSENT || (st_of(sw) != GX_TOMBSTONE && st_of(sw) != st_of(cur)));
+        // fn(): the running services in key order, restamped now; lane tl holds services tl + T*i
         const bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > hs.last_bcast_ns;  // (:547)
-        const uint64_t newm = (__ballot(isnew) >> (tw * T)) & tmask;
-        const bool inc = isnew || (run && refresh);
-        const uint64_t incm = (__ballot(inc) >> (tw * T)) & tmask;
+        bool run[SPL], isnew[SPL], inc[SPL];
+        uint64_t sw[SPL], cur[SPL];
+#pragma unroll
+        for (int i = 0; i < SPL; i++) {
+          const uint32_t sv = tl + T * i;
+          run[i] = sv < d.S && ((hs.running >> sv) & 1ull);
+          sw[i] = pack(d.now, ost[i]);
+          cur[i] = run[i] ? cur0[i] : GX_SLOT_ABSENT;  // no other writer of own slots before this
+          isnew[i] = run[i] && (st_of(cur[i]) == GX_ABSENT ||
+                                (st_of(sw[i]) != GX_TOMBSTONE && st_of(sw[i]) != st_of(cur[i])));
+          inc[i] = isnew[i] || (run[i] && refresh);
+        }
+        const uint64_t newm = team_mask(isnew);
+        const uint64_t incm = team_mask(inc);
         if (incm) {
           hs.last_bcast_ns = d.now;
           const uint32_t freeb = ~hs.arena_used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1u));
@@ -243,13 +267,17 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
           } else {  // SendServices(list, ALIVE_COUNT if anything is new, else 1) (:555-558)
             const uint32_t li_ = (uint32_t)__builtin_ctz(freeb);
             hs.arena_used |= 1u << li_;
-            const uint32_t rank = (uint32_t)__popcll(incm & ((1ull << s) - 1ull));
-            if (inc && rank < d.L) {
-              grec g;
-              g.w = sw;
-              g.r = r;
-              g.pad = 0;
-              list_ptr(d, o, li_)[rank] = g;
+#pragma unroll
+            for (int i = 0; i < SPL; i++) {
+              const uint32_t sv = tl + T * i;
+              const uint32_t rank = (uint32_t)__popcll(incm & ((1ull << sv) - 1ull));
+              if (inc[i] && rank < d.L) {
+                grec g;
+                g.w = sw[i];
+                g.r = o * d.S + sv;
+                g.pad = 0;
+                list_ptr(d, o, li_)[rank] = g;
+              }
             }
             const uint32_t m = (uint32_t)__popcll(incm) < d.L ? (uint32_t)__popcll(incm) : d.L;
             if (lead) {
@@ -261,24 +289,30 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
           }
           hs.bs_next = d.round + d.p.alive_interval_rounds;
           // TrackNewServices: AddServiceEntry of every included record into the own view
-          bool acc = false, stale = false, chg = false;
-          uint64_t nw = cur;
-          if (inc) {
-            a.c[C_LOCAL_MERGES]++;
-            nw = merge_word(d, cur, sw, acc, stale);
-            if (stale) a.c[C_STALE]++;
-            if (acc) {
-              a.c[C_LOCAL_ACC]++;
-              if (nw != cur) {
-                *slot = nw;
-                a.changed = true;
-                atomicMin(&d.minexp[idx], exp_time(d.p, nw));
+          bool acc[SPL], chg[SPL];
+          uint64_t nw[SPL];
+#pragma unroll
+          for (int i = 0; i < SPL; i++) {
+            bool stale = false;
+            acc[i] = chg[i] = false;
+            nw[i] = cur[i];
+            if (inc[i]) {
+              a.c[C_LOCAL_MERGES]++;
+              nw[i] = merge_word(d, cur[i], sw[i], acc[i], stale);
+              if (stale) a.c[C_STALE]++;
+              if (acc[i]) {
+                a.c[C_LOCAL_ACC]++;
+                if (nw[i] != cur[i]) {
+                  vrow(d, o)[o * d.S + tl + T * i] = nw[i];
+                  a.changed = true;
+                  atomicMin(&d.minexp[idx], exp_time(d.p, nw[i]));
+                }
+                chg[i] = st_of(cur[i]) == GX_ABSENT || st_of(cur[i]) != st_of(nw[i]);
               }
-              chg = st_of(cur) == GX_ABSENT || st_of(cur) != st_of(nw);
             }
+            if (chg[i]) a.c[C_CHG]++;
           }
-          const uint64_t accm = (__ballot(acc) >> (tw * T)) & tmask, chgm = (__ballot(chg) >> (tw * T)) & tmask;
-          if (chg) a.c[C_CHG]++;
+          const uint64_t accm = team_mask(acc), chgm = team_mask(chg);
           if (lead && accm) {
             gx_server_times *t = srv_times(d, o, o);
             t->last_updated_ns = d.now;  // server.LastUpdated (:323)
@@ -290,9 +324,13 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
           const int32_t k = d.ev_slot[idx];
           if (k >= 0 && chgm) {  // ChangeEvents in list order
             const uint32_t ev0 = d.ev_cnt[k];
-            if (chg)
-              ev_put(d, k, ev0 + (uint32_t)__popcll(chgm & ((1ull << s) - 1ull)), r, nw,
-                     st_of(cur) == GX_ABSENT ? GX_UNKNOWN : st_of(cur));
+#pragma unroll
+            for (int i = 0; i < SPL; i++) {
+              const uint32_t sv = tl + T * i;
+              if (chg[i])
+                ev_put(d, k, ev0 + (uint32_t)__popcll(chgm & ((1ull << sv) - 1ull)), o * d.S + sv, nw[i],
+                       st_of(cur[i]) == GX_ABSENT ? GX_UNKNOWN : st_of(cur[i]));
+            }
             if (lead) d.ev_cnt[k] = ev0 + (uint32_t)__popcll(chgm);
           }
         } else {  // Broadcasts <- nil (:569): the looper blocks until the nil is consumed
@@ -895,15 +933,37 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
 // SCAN: the round's expiry scans run here instead of in k_scan: the block first streams the views
 // of its hosts whose tick needs one (tick == 2; scan_view, block-wide, one view at a time), then
 // sends. A host's scan and send touch no other host's state, so no block waits for another.
-template <int T, bool X, bool SCAN = false, bool VEC = false, bool EV = false>
+// OWN > 0: the owner ticks run here too (phases 0-3 in one launch, plain rounds without
+// listeners): the block's hosts tick with the same 4-lane teams, OWN services per lane, then the
+// block scans its queued views and sends. Nothing of one host's tick or send reads another host's
+// state except the receivers' inbox counts, zeroed a round ahead (Dev::in_cnt_nx).
+template <int T, bool X, bool SCAN = false, bool VEC = false, bool EV = false, int OWN = 0>
 __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   __shared__ gx_job s_pj[256 / T][T];  // FIFO head jobs of the block's hosts, loaded ahead
   __shared__ ScanLds sm;
   __shared__ uint32_t s_scan[256 / T], s_nscan;
+  __shared__ gx_job s_sl[OWN ? 256 : 1];  // sleep-ring heads of the owner ticks
   Acc a;
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
-  if (SCAN && *d.wl_cnt) {  // block-uniform: a round with no scan anywhere skips the barriers
+  if constexpr (OWN > 0) {
+    if (threadIdx.x == 0) {
+      s_nscan = 0;
+      if (blockIdx.x == 0) {  // the next round's lists start empty
+        *d.ovf_cnt_nx = 0;
+        *d.wl_cnt_nx = 0;
+      }
+    }
+    __syncthreads();
+    const bool q = owner_tick<T, OWN>(d, a, idx, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
+    if (q) s_scan[atomicAdd(&s_nscan, 1u)] = idx;  // lead lanes only
+    __syncthreads();  // the block's ticks before its scans and sends read them
+    for (uint32_t k = 0; k < s_nscan; k++) {
+      const uint32_t oi = s_scan[k];
+      scan_view<VEC, EV>(d, oi, &d.scan_list[(size_t)oi * d.L], d.L, &d.scan_cnt[oi], sm);
+      __syncthreads();
+    }
+  } else if (SCAN && *d.wl_cnt) {  // block-uniform: a round with no scan anywhere skips the barriers
     if (threadIdx.x == 0) s_nscan = 0;
     __syncthreads();
     if ((threadIdx.x & (T - 1)) == 0 && idx < d.Hl && d.tick[idx] == 2) s_scan[atomicAdd(&s_nscan, 1u)] = idx;
