@@ -307,18 +307,27 @@ static int round_send_impl(gx_engine *e) {
   const bool storm = d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2;
   // BroadcastTombstones' SendServices is queued before the detector's and the storm's jobs
   const bool bt_apart = d.p.fd_enable || storm;
-  // a plain round without listeners: owner ticks, expiry scans and sends in one launch
-  const bool fused = !bt_apart && !d.departures && d.K && e->log_views.empty() && !(d.ab & 8u);
+  // a round without the detector or the storm: owner ticks, expiry scans and sends in one launch
+  // (S <= 16: owner teams of the send's 4 lanes with up to 4 services each)
+  const bool fused = !bt_apart && d.K && d.S <= 16 && !(d.ab & 8u);
   if (fused) {
     LaunchTimer t(e, GX_K_SEND);
     const unsigned g = nblk(d.Hl, 64);
-#define GX_TICK_SEND(SPL) (vec ? k_send<4, false, true, true, false, SPL> : k_send<4, false, true, false, false, SPL>)<<<g, 256, 0, s>>>(d, 1)
-    if (d.S <= 4) GX_TICK_SEND(1);
-    else if (d.S <= 8) GX_TICK_SEND(2);
-    else if (d.S <= 16) GX_TICK_SEND(4);
-    else if (d.S <= 32) GX_TICK_SEND(8);
-    else GX_TICK_SEND(16);
+    const bool ev = !e->log_views.empty();
+#define GX_TS(X, SPL)                                                                                    \
+  (vec ? (ev ? k_send<4, X, true, true, true, SPL> : k_send<4, X, true, true, false, SPL>)             \
+       : (ev ? k_send<4, X, true, false, true, SPL> : k_send<4, X, true, false, false, SPL>))<<<g, 256, 0, s>>>(d, 1)
+#define GX_TICK_SEND(SPL) \
+  if (d.departures) GX_TS(true, SPL); else GX_TS(false, SPL)
+    if (d.S <= 4) {
+      GX_TICK_SEND(1);
+    } else if (d.S <= 8) {
+      GX_TICK_SEND(2);
+    } else {
+      GX_TICK_SEND(4);
+    }
 #undef GX_TICK_SEND
+#undef GX_TS
     HIPCHK(hipGetLastError());
     return GX_OK;
   }
