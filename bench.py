@@ -167,6 +167,36 @@ class Cluster:
         self.e.close()
 
 
+def gossip_round_span(lib, cfg, seed, local_rank):
+    """Device time per gossip round without per-launch instrumentation: the second stretch of rounds
+    between two push-pull rounds after the storm (inside the bench window; no storm, no push-pull
+    in it), bracketed by two events on the engine's stream (the caller's torch stream). The
+    per-class split above records an event pair around every launch, which adds about 10 us per
+    round."""
+    import torch
+    p = CONFIGS[cfg]["p"]
+    period = p.get("ae_period_rounds", 0) or 10
+    phase = p.get("ae_phase", 0)
+    e = make_engine(lib, cfg, seed, local_rank)
+    r0 = phase + 1  # the round after a push-pull round, past the storm
+    while r0 <= p.get("storm_round", -1):
+        r0 += period
+    e.run_rounds(r0)
+    st = torch.cuda.Stream()  # a stream of its own (launches on the legacy default stream are slower)
+    e.set_stream(st.cuda_stream, False)
+    n = period - 1
+    e.run_rounds(n + 1)  # the first stretch on a new stream starts with ~0.15 ms of queue set-up
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    e.run_rounds(n)  # (run_rounds ends with one wake-up kernel, ~25 us, inside the span)
+    b.record(st)
+    b.synchronize()
+    us = 1e3 * a.elapsed_time(b) / n
+    e.set_stream(None, False)
+    e.close()
+    return round(us, 2)
+
+
 def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
     """Fresh cluster from round 0: chunks of `check_every` rounds, catalog agreement checked
     between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run)."""
@@ -338,6 +368,8 @@ def main():
         gossip = {"kernels": list(GOSSIP_KERNELS), "device_us_per_round": round(1e3 * gms / args.steps, 2),
                   "gossip_merges": split["gossip_merges"],
                   "record_merges_per_s": split["gossip_merges"] / (gms * 1e-3) if gms else None}
+        if world == 1:  # without per-launch events: the span of a stretch of gossip-only rounds
+            gossip["round_span_us"] = gossip_round_span(lib, args.config, seed, local_rank)
 
     conv = None
     if not args.no_converge:
