@@ -20,7 +20,7 @@ ks.sort()
 rounds, cur = [], None
 for s, e, n in ks:
     # a round starts at k_owner, or at k_send when the owner ticks run inside it (fused launch)
-    if n == "k_owner" or (n == "k_send" and (cur is None or any(x[2] == "k_merge" for x in cur))):
+    if n == "k_owner" or (n == "k_send" and (cur is None or any(x[2] in ("k_merge", "k_merge_lean") for x in cur))):
         cur = []
         rounds.append(cur)
     if cur is not None and n in GOSSIP:

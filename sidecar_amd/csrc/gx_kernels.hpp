@@ -1039,102 +1039,31 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
 // merged in full by k_merge. Measured (profiles/ab_gossip.sh, cfg5): 16 lanes x 4 records per
 // batch 17.8 us; 32 x 4 22.6 us; 64 x 2 24.2 us; 8 x 4 21.1 us; loading the inline slots
 // speculatively with the count (one hop less) 19-23 us: the wasted bytes cost more than the hop.
-#define LEAN_LPR 16
-#define LEAN_Q 4
-__global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
-  const uint32_t lane = threadIdx.x & 63, l = threadIdx.x & (LEAN_LPR - 1);
-  const uint32_t vi = blockIdx.x * (256 / LEAN_LPR) + threadIdx.x / LEAN_LPR;
-  const uint32_t gbase = lane & ~(uint32_t)(LEAN_LPR - 1);
-  const uint64_t gmask = ((1ull << LEAN_LPR) - 1ull) << gbase;
-  unsigned long long c_merge = 0, c_stale = 0, c_hdr = 0;
-  if (vi < d.Hl) {
-    const uint32_t cap = d.p.packet_cap;
-    const grec *base = &d.in_rec[(size_t)vi * d.DR * cap];
-    const uint4 hd = l < d.DR ? d.in_hdr[(size_t)vi * d.DI + l] : make_uint4(0u, 0u, 0u, 0u);
-    const uint32_t cnt = d.in_cnt[vi];
-    bool defer = cnt > d.DR;
-    if (cnt && !defer) {
-      const uint64_t *row = &d.view[(size_t)vi * d.R];
-      const uint32_t npos = cnt * cap;
-      c_hdr = l == 0 ? cnt : 0;
-      for (uint32_t p0 = 0; p0 < npos; p0 += LEAN_LPR * LEAN_Q) {
-        grec g[LEAN_Q];
-        bool valid[LEAN_Q];
-#pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) {  // hop 2: the records of the packets' used slots
-          const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
-          const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
-          valid[q] = p < npos && p - sl * cap < len;
-          if (valid[q]) g[q] = base[p];
-        }
-        uint64_t w0[LEAN_Q];
-#pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) w0[q] = valid[q] ? row[g[q].r] : 0;  // hop 3
-        bool live = false;
-#pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) {
-          const int64_t ts = ts_of(g[q].w);
-          const bool stale = valid[q] && ts < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
-          live |= valid[q] && !stale && (st_of(w0[q]) == GX_ABSENT || ts > ts_of(w0[q]));
-          c_merge += valid[q];
-          c_stale += stale;
-        }
-        if (__ballot(live) & gmask) {
-          defer = true;
-          break;
-        }
-      }
-    }
-    if (defer) c_merge = c_stale = c_hdr = 0;  // k_merge merges and counts this receiver
-    if (l == 0) d.mflag[vi] = defer ? 1 : 0;
-  }
-  c_merge = wave_sum(c_merge);
-  c_stale = wave_sum(c_stale);
-  c_hdr = wave_sum(c_hdr);
-  if (lane == 0 && c_merge) {
-    // 12 B per record + 8 B per slot read, 16 B per inbox header + the count
-    kbytes(d, GX_K_MERGE, 20ull * c_merge + 16ull * c_hdr + 4ull * c_hdr, c_merge);
-    ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
-    ctr_atomic(d, C_STALE, c_stale);
-  }
-}
-
+// Fused with k_merge (each wave merging its own flagged receivers after the filter, inbox still in
+// L2): 31.1 us vs 16.1 + 14.4 us, the merge body's 116 VGPRs halving the filter's occupancy.
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
 #define MERGE_RANGE_DEF 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
-template <bool K32, bool EV, int MERGE_RANGE = MERGE_RANGE_DEF>
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
-  // one receiver per wave, MERGE_WAVES per block; the waves share nothing (wave-level sync only)
-  __shared__ uint4 s_hdr_[MERGE_WAVES][64];
-  __shared__ uint8_t s_accf_[MERGE_WAVES][64];
-  __shared__ uint8_t s_chg_[MERGE_WAVES][64];
-  __shared__ uint8_t s_prev_[MERGE_WAVES][64];
-  __shared__ uint64_t s_accw_[MERGE_WAVES][64];
-  const uint32_t wv = threadIdx.x >> 6;
-  uint4 *s_hdr = s_hdr_[wv];
-  uint8_t *s_accf = s_accf_[wv], *s_chg = s_chg_[wv], *s_prev = s_prev_[wv];
-  uint64_t *s_accw = s_accw_[wv];
-  const uint32_t lane = threadIdx.x & 63;
-  // each wave takes the flags of MERGE_RANGE consecutive receivers and merges the flagged ones in
-  // turn (one receiver per wave measured fastest: the flagged receivers' chains run side by side)
-  const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * MERGE_RANGE;
-  if (r0 >= d.Hl) return;
-  uint64_t fl = 0;
-  if (MERGE_RANGE == 8 && r0 + MERGE_RANGE <= d.Hl) {
-    fl = *reinterpret_cast<const uint64_t *>(&d.mflag[r0]);
-  } else {
-    for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)d.mflag[r0 + k] << (8 * k);
-  }
-  for (; fl; fl &= fl - 1) {
-  const uint32_t vi = r0 + (uint32_t)(__builtin_ctzll(fl) >> 3), v = d.lo + vi;
+struct MergeLds {  // one wave's staging for one receiver at a time
+  uint4 hdr[64];
+  uint64_t accw[64];
+  uint8_t accf[64], chg[64], prev[64];
+};
+// The full gather-then-merge of receiver vi by one wave (every lane calls it, wave-uniform vi).
+template <bool K32, bool EV>
+GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
+  uint4 *s_hdr = L.hdr;
+  uint8_t *s_accf = L.accf, *s_chg = L.chg, *s_prev = L.prev;
+  uint64_t *s_accw = L.accw;
+  const uint32_t lane = threadIdx.x & 63, v = d.lo + vi;
   // hop 1: the inbox count and its first headers together (most inboxes hold a few packets)
   const uint32_t npre = d.DI < INBOX_PREFETCH ? d.DI : INBOX_PREFETCH;
   uint4 hd = lane < npre ? d.in_hdr[(size_t)vi * d.DI + lane] : make_uint4(0u, 0u, 0u, 0u);
   const uint32_t deg = d.in_cnt[vi];
-  if (deg == 0) continue;
+  if (deg == 0) return;
   if (deg > d.DI) {
     if (lane == 0) merge_inbox_serial(d, vi);
-    continue;
+    return;
   }
   if (deg > npre && lane >= npre && lane < deg) hd = d.in_hdr[(size_t)vi * d.DI + lane];
   // sender order: rank of each header's key among the deg distinct keys
@@ -1322,8 +1251,86 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
     }
   }
   wave_sync();
+}
+
+template <bool K32, bool EV, int MERGE_RANGE = MERGE_RANGE_DEF>
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
+  // one receiver per wave, MERGE_WAVES per block; the waves share nothing (wave-level sync only)
+  __shared__ MergeLds s_l[MERGE_WAVES];
+  const uint32_t wv = threadIdx.x >> 6;
+  // each wave takes the flags of MERGE_RANGE consecutive receivers and merges the flagged ones in
+  // turn (one receiver per wave measured fastest: the flagged receivers' chains run side by side)
+  const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * MERGE_RANGE;
+  if (r0 >= d.Hl) return;
+  uint64_t fl = 0;
+  if (MERGE_RANGE == 8 && r0 + MERGE_RANGE <= d.Hl) {
+    fl = *reinterpret_cast<const uint64_t *>(&d.mflag[r0]);
+  } else {
+    for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)d.mflag[r0 + k] << (8 * k);
+  }
+  for (; fl; fl &= fl - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)(__builtin_ctzll(fl) >> 3), s_l[wv]);
+}
+
+#define LEAN_LPR 16
+#define LEAN_Q 4
+__global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
+  const uint32_t lane = threadIdx.x & 63, l = threadIdx.x & (LEAN_LPR - 1);
+  const uint32_t vi = blockIdx.x * (256 / LEAN_LPR) + threadIdx.x / LEAN_LPR;
+  const uint32_t gbase = lane & ~(uint32_t)(LEAN_LPR - 1);
+  const uint64_t gmask = ((1ull << LEAN_LPR) - 1ull) << gbase;
+  unsigned long long c_merge = 0, c_stale = 0, c_hdr = 0;
+  if (vi < d.Hl) {
+    const uint32_t cap = d.p.packet_cap;
+    const grec *base = &d.in_rec[(size_t)vi * d.DR * cap];
+    const uint4 hd = l < d.DR ? d.in_hdr[(size_t)vi * d.DI + l] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t cnt = d.in_cnt[vi];
+    bool defer = cnt > d.DR;
+    if (cnt && !defer) {
+      const uint64_t *row = &d.view[(size_t)vi * d.R];
+      const uint32_t npos = cnt * cap;
+      c_hdr = l == 0 ? cnt : 0;
+      for (uint32_t p0 = 0; p0 < npos; p0 += LEAN_LPR * LEAN_Q) {
+        grec g[LEAN_Q];
+        bool valid[LEAN_Q];
+#pragma unroll
+        for (int q = 0; q < LEAN_Q; q++) {  // hop 2: the records of the packets' used slots
+          const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
+          const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
+          valid[q] = p < npos && p - sl * cap < len;
+          if (valid[q]) g[q] = base[p];
+        }
+        uint64_t w0[LEAN_Q];
+#pragma unroll
+        for (int q = 0; q < LEAN_Q; q++) w0[q] = valid[q] ? row[g[q].r] : 0;  // hop 3
+        bool live = false;
+#pragma unroll
+        for (int q = 0; q < LEAN_Q; q++) {
+          const int64_t ts = ts_of(g[q].w);
+          const bool stale = valid[q] && ts < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+          live |= valid[q] && !stale && (st_of(w0[q]) == GX_ABSENT || ts > ts_of(w0[q]));
+          c_merge += valid[q];
+          c_stale += stale;
+        }
+        if (__ballot(live) & gmask) {
+          defer = true;
+          break;
+        }
+      }
+    }
+    if (defer) c_merge = c_stale = c_hdr = 0;  // k_merge merges and counts this receiver
+    if (l == 0) d.mflag[vi] = defer ? 1 : 0;
+  }
+  c_merge = wave_sum(c_merge);
+  c_stale = wave_sum(c_stale);
+  c_hdr = wave_sum(c_hdr);
+  if (lane == 0 && c_merge) {
+    // 12 B per record + 8 B per slot read, 16 B per inbox header + the count
+    kbytes(d, GX_K_MERGE, 20ull * c_merge + 16ull * c_hdr + 4ull * c_hdr, c_merge);
+    ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
+    ctr_atomic(d, C_STALE, c_stale);
   }
 }
+
 
 // ============================================================= phase 5: anti-entropy push-pull ==
 // Dense view-pair merge: a <- b and, when `both`, b <- a's pre-exchange words. VEC streams both
