@@ -160,7 +160,7 @@ class Cluster:
         keys = sorted(w)
         import torch
         t = torch.tensor([w[k] for k in keys], dtype=torch.int64, device=self.shard.device)
-        self.shard.dist.all_reduce(t, op=self.shard.dist.ReduceOp.SUM, group=self.shard.group)
+        self.shard._all_reduce(t, self.shard.dist.ReduceOp.SUM)
         return dict(zip(keys, [int(x) for x in t.tolist()]))
 
     def close(self):
@@ -284,11 +284,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    backend = os.environ.get("GX_BENCH_BACKEND", "nccl")  # gloo: rehearsal of N ranks on one GPU
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "gloo":  # ranks share the visible GPUs (collectives staged through the host)
+            local_rank %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
 
     def barrier():
         torch.cuda.synchronize()
@@ -320,7 +323,7 @@ def main():
     tot_merges = merges(st1) - merges(st0)  # whole cluster (summed over shards)
     dt_max = dt
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt_max = float(t.item())
 
@@ -353,7 +356,9 @@ def main():
         if k not in kern or not kern[k]["ms"]:
             return None
         ach = kern[k]["GBps"] or 0.0
-        traffic = (pmc.get(k) or {}).get("hbm_bytes_per_launch")
+        # PMC traffic is measured on the N = 1 run (profiles/pmc_summary.json): per launch of the
+        # whole engine, so only comparable with this line at N = 1
+        traffic = (pmc.get(k) or {}).get("hbm_bytes_per_launch") if world == 1 else None
         return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
                 "bytes_per_launch": kern[k]["bytes"] // max(1, kern[k]["launches"]),
@@ -400,9 +405,12 @@ def main():
             "config": {"workload": workload_text(args.config),
                        "hosts": cfgp["n_hosts"], "services": cfgp["n_services"],
                        "fanout": cfgp.get("fanout", 3),
-                       "parallelism": f"host-sharded over {world} GPUs (RCCL all-to-all)" if world > 1 else "single GPU"},
+                       "parallelism": (f"host-sharded over {world} ranks ("
+                                       + ("RCCL all-to-all)" if backend == "nccl" else "gloo, host-staged all-to-all)")
+                                       if world > 1 else "single GPU")},
             "merges": split, "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
             "roofline": roof, "roofline_merge": roofline("merge"), "cpu_baseline": cpu, "kernels": kern,
+            "kernels_scope": "whole engine" if world == 1 else "rank 0's shard (device time and bytes of its launches)",
             "exchange": xfer,
         }
         if cfgp.get("fd_enable") or cfgp.get("depart_ppm"):

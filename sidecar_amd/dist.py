@@ -189,6 +189,26 @@ class DistShard:
         self.s = _Shard(p, lib, self.device)
         self.e = self.s.e
         self.wire = WireBytes(self.e)
+        # gloo has no device all-to-all / all-gather: a gloo group over device shards (the one-GPU
+        # rehearsal of the RCCL path in tests/test_gpu_dist.py) stages collectives through the host
+        self.stage = self.device.type == "cuda" and dist.get_backend(group) == "gloo"
+
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu() if self.stage else t
+
+    def _a2a(self, recv, send, rs, ss):
+        if not self.stage:
+            self.dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+            return
+        r = torch.empty(recv.numel(), dtype=recv.dtype)
+        self.dist.all_to_all_single(r, send.cpu(), output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+        recv.copy_(r)
+
+    def _all_reduce(self, t: torch.Tensor, op):
+        h = self._host(t)
+        self.dist.all_reduce(h, op=op, group=self.group)
+        if h is not t:
+            t.copy_(h)
 
     CHUNK = 256 << 20  # bytes per peer per all-to-all call
 
@@ -203,6 +223,7 @@ class DistShard:
             mine = sizes
         else:
             mine = torch.tensor(sizes.astype(np.int64), device=self.device)
+        mine = self._host(mine)
         rows = [torch.empty_like(mine) for _ in range(self.world)]
         dist.all_gather(rows, mine, group=self.group)
         m = torch.stack(rows).tolist()  # m[src][dst]: the one host wait of the exchange
@@ -216,7 +237,7 @@ class DistShard:
         # every rank runs the same number of calls: ceil(largest per-peer segment / CHUNK)
         calls = (max(max(r) for r in m) + self.CHUNK - 1) // self.CHUNK
         if calls == 1:
-            dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+            self._a2a(recv, send, rs, ss)
             calls = 0
         soff = np.concatenate([[0], np.cumsum(ss)])
         roff = np.concatenate([[0], np.cumsum(rs)])
@@ -226,8 +247,7 @@ class DistShard:
             r_part = [max(0, min(self.CHUNK, n - lo)) for n in rs]
             s_buf = torch.cat([send[int(soff[p]) + lo:int(soff[p]) + lo + s_part[p]] for p in range(self.world)])
             r_buf = torch.empty(sum(r_part), dtype=torch.uint8, device=self.device)
-            dist.all_to_all_single(r_buf, s_buf, output_split_sizes=r_part, input_split_sizes=s_part,
-                                   group=self.group)
+            self._a2a(r_buf, s_buf, r_part, s_part)
             o = 0
             for p in range(self.world):
                 if r_part[p]:
@@ -263,23 +283,27 @@ class DistShard:
         keys = sorted(st)
         t = torch.tensor([st[k] for k in keys], dtype=torch.int64, device=self.device)
         mx = t.clone()
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
-        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
+        self._all_reduce(t, self.dist.ReduceOp.SUM)
+        self._all_reduce(mx, self.dist.ReduceOp.MAX)
         out = dict(zip(keys, t.tolist()))
         for k in ("round", "last_change_round"):
             out[k] = int(mx[keys.index(k)].item())
         return out
 
     def converged(self):
+        """(agreed, n) as LocalShards.converged: n = catalog records on which the live views disagree
+        (all shards); once they agree, with the failure detector, the sum over shards of the nodes
+        some of the shard's live views misjudge (a node misjudged in several shards counts once
+        per shard). Every rank takes the same branch: `bad` is all-reduced first."""
         R = self.e.H * self.e.S
         mn = torch.empty(R, dtype=torch.int64, device=self.device)
         mx = torch.empty(R, dtype=torch.int64, device=self.device)
         self.e.view_minmax(_ptr(mn), _ptr(mx))
-        self.dist.all_reduce(mn, op=self.dist.ReduceOp.MIN, group=self.group)
-        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
+        self._all_reduce(mn, self.dist.ReduceOp.MIN)
+        self._all_reduce(mx, self.dist.ReduceOp.MAX)
         bad = int((mn != mx).sum().item())
-        if self.e.params.fd_enable:  # membership agrees with the truth on every shard too
-            t = torch.tensor([bad + self.e.fd_converged()[1]], dtype=torch.int64, device=self.device)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        if bad == 0 and self.e.params.fd_enable:  # membership agrees with the truth on every shard too
+            t = torch.tensor([self.e.fd_converged()[1]], dtype=torch.int64, device=self.device)
+            self._all_reduce(t, self.dist.ReduceOp.SUM)
             bad = int(t.item())
         return bad == 0, bad
