@@ -352,7 +352,10 @@ static int round_send_impl(gx_engine *e) {
   if (storm) {
     LaunchTimer t(e, GX_K_STORM);
     const bool ev = !e->log_views.empty();
-    if (d.S >= 2 && 64 % d.S == 0) (ev ? k_storm_p2<true> : k_storm_p2<false>)<<<d.Hl, 256, 0, s>>>(d);
+    const bool nt = d.ab & 16u;
+    if (d.S >= 2 && 64 % d.S == 0)
+      (ev ? (nt ? k_storm_p2<true, true> : k_storm_p2<true, false>)
+          : (nt ? k_storm_p2<false, true> : k_storm_p2<false, false>))<<<d.Hl, 256, 0, s>>>(d);
     else (ev ? k_storm<true> : k_storm<false>)<<<d.Hl, 256, 0, s>>>(d);
   }
   {

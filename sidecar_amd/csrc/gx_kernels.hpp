@@ -647,7 +647,8 @@ GXD uint64_t spread32(uint64_t x) {  // bit i -> bit 2i
   x = (x | (x << 1)) & 0x5555555555555555ull;
   return x;
 }
-template <bool EV>
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+template <bool EV, bool NT>
 __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   __shared__ uint32_t s_cnt[2][8];
   __shared__ uint32_t s_ecnt[2][8];
@@ -675,8 +676,16 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
 #pragma unroll
     for (int c = 0; c < 2; c++) {
       uint32_t r0 = base + 512 * c + 2 * t;
-      q[c] = r0 < nw ? *reinterpret_cast<const ulonglong2 *>(&row[r0])
-                     : make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+      if (r0 < nw) {
+        if (NT) {
+          v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r0]));
+          q[c] = make_ulonglong2(x.x, x.y);
+        } else {
+          q[c] = *reinterpret_cast<const ulonglong2 *>(&row[r0]);
+        }
+      } else {
+        q[c] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+      }
     }
   };
   load(0, q0);
@@ -698,7 +707,14 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       live_c[c] = live;
       sh_c[c] = sh;
       c_chg += live ? (unsigned)(p0 + p1) : 0u;  // ServiceChanged per record of a live owner
-      if (ch0 || ch1) *reinterpret_cast<ulonglong2 *>(&row[base + 512 * c + 2 * t]) = make_ulonglong2(n0, n1);
+      if (ch0 || ch1) {
+        if (NT) {
+          v2u64 x = {n0, n1};
+          __builtin_nontemporal_store(x, reinterpret_cast<v2u64 *>(&row[base + 512 * c + 2 * t]));
+        } else {
+          *reinterpret_cast<ulonglong2 *>(&row[base + 512 * c + 2 * t]) = make_ulonglong2(n0, n1);
+        }
+      }
       c_wr += ch0 + ch1;
       lead_live[c] = leader && live;
       uint64_t bj = __ballot(lead_live[c]);
