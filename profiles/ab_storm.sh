@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of the departure-storm kernel (k_storm_p2): GX_AB_FLAGS bit 4 (=16) streams the rows with
-# nontemporal loads and stores. The driver's bench window [5, 25) holds the storm; per-kernel
+# A/B of the departure-storm kernel (k_storm_p2): nontemporal row loads and stores (the shipped
+# kernel since round 2) vs default ones (GX_AB_FLAGS=16; before this A/B the flag selected NT). The driver's bench window [5, 25) holds the storm; per-kernel
 # device time from the bench's split pass, three runs per variant.
 set -e
 for f in 0 16 0 16 0 16; do

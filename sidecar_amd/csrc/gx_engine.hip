@@ -352,7 +352,7 @@ static int round_send_impl(gx_engine *e) {
   if (storm) {
     LaunchTimer t(e, GX_K_STORM);
     const bool ev = !e->log_views.empty();
-    const bool nt = d.ab & 16u;
+    const bool nt = !(d.ab & 16u);  // nontemporal row stream (A/B bit 16: default loads/stores)
     if (d.S >= 2 && 64 % d.S == 0)
       (ev ? (nt ? k_storm_p2<true, true> : k_storm_p2<true, false>)
           : (nt ? k_storm_p2<false, true> : k_storm_p2<false, false>))<<<d.Hl, 256, 0, s>>>(d);
@@ -491,11 +491,13 @@ static int ae_whole_impl(gx_engine *e) {
     }
     if (np) {
       LaunchTimer t(e, GX_K_AE);
-      // PF = 1, default cache policy: deeper prefetch and nt loads measured within noise
-      // (profiles/ae_variants.sh)
+      // PF = 1: deeper prefetch measured within noise (profiles/ae_variants.sh)
       // the ChangeEvent variant only while some view has a listener
       const bool ev = !e->log_views.empty();
-      if (vec && !ev) k_ae<true><<<np, 256, 0, s>>>(d, key0, key1);
+      // nontemporal row loads and stores: -1% over the bench window (profiles/ab/ae_nt_ab_r02.log);
+      // A/B bit 32: default cache policy
+      if (vec && !ev && (d.ab & 32u)) k_ae<true><<<np, 256, 0, s>>>(d, key0, key1);
+      else if (vec && !ev) k_ae<true, 1, true, true><<<np, 256, 0, s>>>(d, key0, key1);
       else if (vec) k_ae_ev<true><<<np, 256, 0, s>>>(d, key0, key1);
       else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
       else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);

@@ -1481,7 +1481,7 @@ GXD void dec_pair_u(const uint64_t *enc, uint32_t s, bool v0, bool v1, uint64_t 
     if ((e ? v1 : v0) && !((om >> b) & 1ull)) w[e] = enc[16 + pre + __popcll(nm & ((2ull << b) - 1ull))];
   }
 }
-template <bool VEC, int PF = 1, bool NT = false, bool EV = false>
+template <bool VEC, int PF = 1, bool NT = false, bool EV = false, bool NTS = false>
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
                  unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false,
                  const XSrc *xs = nullptr) {
@@ -1673,8 +1673,14 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       bool cha = nwa[2 * h] != wa[2 * h] || nwa[2 * h + 1] != wa[2 * h + 1];
       bool chb = nwb[2 * h] != wb[2 * h] || nwb[2 * h + 1] != wb[2 * h + 1];
       if (VEC) {
-        if (cha) *reinterpret_cast<ulonglong2 *>(&A[r0]) = make_ulonglong2(nwa[2 * h], nwa[2 * h + 1]);
-        if (chb) *reinterpret_cast<ulonglong2 *>(&B[r0]) = make_ulonglong2(nwb[2 * h], nwb[2 * h + 1]);
+        if (NTS) {  // nontemporal stores (A/B)
+          typedef unsigned long long v2u64s __attribute__((ext_vector_type(2)));
+          if (cha) __builtin_nontemporal_store((v2u64s){nwa[2 * h], nwa[2 * h + 1]}, reinterpret_cast<v2u64s *>(&A[r0]));
+          if (chb) __builtin_nontemporal_store((v2u64s){nwb[2 * h], nwb[2 * h + 1]}, reinterpret_cast<v2u64s *>(&B[r0]));
+        } else {
+          if (cha) *reinterpret_cast<ulonglong2 *>(&A[r0]) = make_ulonglong2(nwa[2 * h], nwa[2 * h + 1]);
+          if (chb) *reinterpret_cast<ulonglong2 *>(&B[r0]) = make_ulonglong2(nwb[2 * h], nwb[2 * h + 1]);
+        }
       } else {
         if (nwa[2 * h] != wa[2 * h]) A[r0] = nwa[2 * h];
         if (nwa[2 * h + 1] != wa[2 * h + 1]) A[r0 + 1] = nwa[2 * h + 1];
@@ -1815,7 +1821,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   }
 }
 
-template <bool VEC, bool EV, int PF, bool NT>
+template <bool VEC, bool EV, int PF, bool NT, bool NTS = false>
 GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
@@ -1841,15 +1847,15 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
     if (ok && d.p.fd_enable) ok = reach(d, a, b) && memp(d, a, b)->state == GX_M_ALIVE;
     if (!ok) return;
   }
-  ae_pair<VEC, PF, NT, EV>(d, a, b, true, s_wave, s_red);
+  ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red);
 }
 
 // The push-pull kernel, without ChangeEvents (no listener anywhere): kept within 128 VGPRs so
 // that 4 waves per SIMD stay resident; with events (listeners present) a separate entry point.
-template <bool VEC, int PF = 1, bool NT = false>
+template <bool VEC, int PF = 1, bool NT = false, bool NTS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae(Dev d, uint64_t key0,
                                                                                    uint64_t key1) {
-  ae_round_pair<VEC, false, PF, NT>(d, key0, key1);
+  ae_round_pair<VEC, false, PF, NT, NTS>(d, key0, key1);
 }
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_ae_ev(Dev d, uint64_t key0, uint64_t key1) {
