@@ -232,7 +232,7 @@ class DistShard:
         self.last_sizes = np.array(ss, dtype=np.uint64)
         send = self.s.pack(self.last_sizes, packer)
         if after_pack is not None:
-            after_pack()  # device work on the engine stream that overlaps the collective
+            after_pack()  # shard-local pairs on the engine's side stream, beside the collective
         recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
         # every rank runs the same number of calls: ceil(largest per-peer segment / CHUNK)
         calls = (max(max(r) for r in m) + self.CHUNK - 1) // self.CHUNK
