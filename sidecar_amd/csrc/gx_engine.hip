@@ -521,7 +521,7 @@ static int run_one_round(gx_engine *e) {
 
 static int wake_all(gx_engine *e) {
   set_round_fields(e);
-  k_wake<<<nblk(e->d.Hl, 256), 256, 0, e->stream>>>(e->d);
+  k_wake<<<nblk(e->d.Hl, 64), 64, 0, e->stream>>>(e->d);
   HIPCHK(hipGetLastError());
   return GX_OK;
 }

@@ -149,10 +149,35 @@ __global__ __launch_bounds__(256) void k_minexp_recompute(Dev d, uint32_t lo_idx
   if (threadIdx.x == 0) d.minexp[v] = m;
 }
 
-__global__ void k_wake(Dev d) {
+// wake_host on a register copy of the host's counters: the counters and the sleep ring's head
+// job are the only dependent loads when nothing is due (64-thread blocks: 4x the CUs of 256)
+__global__ __launch_bounds__(64) void k_wake(Dev d) {
   Acc a;
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < d.Hl && !departed(d, d.lo + idx)) wake_host(d, a, d.lo + idx);  // a crashed host stays frozen
+  if (idx < d.Hl && !departed(d, d.lo + idx)) {  // a crashed host stays frozen
+    gx_host_state *h = &d.hs[idx];
+    const uint4 c = *reinterpret_cast<const uint4 *>(h);  // fifo_head, fifo_tail, sleep_head, sleep_tail
+    if (c.z != c.w) {
+      gx_host_state hs;
+      hs.fifo_head = c.x;
+      hs.fifo_tail = c.y;
+      hs.sleep_head = c.z;
+      hs.sleep_tail = c.w;
+      hs.arena_used = h->arena_used;
+      const uint32_t au0 = hs.arena_used;
+      while (hs.sleep_head != hs.sleep_tail) {
+        gx_job j = d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
+        if ((int64_t)j.wake > d.round) break;
+        hs.sleep_head++;
+        push_job_r(d, a, d.lo + idx, hs, j, true);
+      }
+      if (hs.sleep_head != c.z) {
+        h->fifo_tail = hs.fifo_tail;
+        h->sleep_head = hs.sleep_head;
+        if (hs.arena_used != au0) h->arena_used = hs.arena_used;
+      }
+    }
+  }
   acc_flush(d, a);
 }
 
