@@ -121,6 +121,7 @@ struct Dev {
   uint32_t logS;       // log2(S) when S is a power of two
   int departures;      // p.depart_round >= 0 && p.depart_ppm
   uint32_t nblk_ae;    // digest blocks per row, ceil(R / GX_DIGEST_SLOTS)
+  uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
   uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels): bit 2
                        // expiry scans in k_scan, bit 3 owner ticks in k_owner (not inside k_send)
 };
@@ -507,7 +508,8 @@ GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const
 template <int T>
 GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, uint32_t limit,
                                  grec *packet, uint32_t limit_bytes, uint32_t overhead,
-                                 const gx_job *pj = nullptr) {
+                                 const gx_job *pj = nullptr, const uint64_t *rrow = nullptr,
+                                 uint8_t *rflag = nullptr) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lane0 = tl == 0;
   const uint32_t mask = d.DQ - 1;
@@ -593,10 +595,42 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
   // Ring position p is read and written only by team lane p % T (T divides DQ), so a record that
   // a call leaves pending is seen by the same lane in the next call without a fence; batch records
   // (list arena, job) and packet slots are not written and read back here, any lane moves them.
+  // Send-side filter (rrow: the local receiver's view row): a record that is stale, or no newer
+  // than the receiver's slot, is a no-op in the receiver's merge whatever the other packets hold
+  // (see k_merge). Phases 0-3 only raise a slot's timestamp, except the expiry scan's GC of a
+  // tombstone older than the tombstone lifespan, which is read as absent; so a record this sees
+  // as a no-op is one, and the receiver is flagged for k_merge only when some record is live.
+  // The senders count the receivers' gossip merges and stale drops (k_merge then does not).
+  bool lv = false;
+  uint32_t fm = 0, fs = 0;
+  const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+  const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
+  auto filt = [&](const grec &g) {
+    const uint64_t w0 = rrow[g.r];
+    const int64_t ts = ts_of(g.w);
+    const bool stale = ts < t_stale;
+    const bool gc = st_of(w0) == GX_TOMBSTONE && ts_of(w0) < t_gc;
+    lv |= !stale && (st_of(w0) == GX_ABSENT || ts > ts_of(w0) || gc);
+    fm++;
+    fs += stale;
+  };
   const uint32_t lb = l < m ? l : m;
-  for (uint32_t i = tl; i < lb; i += T) packet[i] = item(i);
+  for (uint32_t i = tl; i < lb; i += T) {
+    const grec g = item(i);
+    packet[i] = g;
+    if (rrow) filt(g);
+  }
   if (l > m)  // the pending prefix, ring positions head .. head + l - m - 1, by their owner lanes
-    for (uint32_t q = (tl - head) & (T - 1); q < l - m; q += T) packet[m + q] = dq[(head + q) & mask];
+    for (uint32_t q = (tl - head) & (T - 1); q < l - m; q += T) {
+      const grec g = dq[(head + q) & mask];
+      packet[m + q] = g;
+      if (rrow) filt(g);
+    }
+  if (rrow) {
+    a.c[C_GOSSIP_MERGES] += fm;
+    a.c[C_STALE] += fs;
+    if (lv) *rflag = 1;  // any lane of the team that saw a live record (the same byte value)
+  }
   // leftover = broadcast[l:]; batch records that stay pending go in front of the old head
   uint32_t nh;
   if (l < m) {

@@ -390,7 +390,7 @@ static int round_merge_impl(gx_engine *e) {
   if (d.K) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
-    k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);
+    if (!d.sfilt) k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);  // else the senders filtered
     const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE_DEF);
     // 2 or 4 receivers per wave measured 14.2 / 13.7 vs 14.3 us (profiles/r02/gossip)
     if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
@@ -787,6 +787,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.DI = p->inbox_slots ? p->inbox_slots : 64;
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
   d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
+  // one shard: every packet's receiver is local, so its sender reads the receiver's view slots
+  // (A/B bit 128: the receivers' own filter pass, k_merge_lean)
+  d.sfilt = (d.G == 1 && !(d.ab & 128u)) ? 1u : 0u;
   ALLOC(d.in_hdr, sizeof(uint4) * H * d.DI);
   ALLOC(d.in_ovf, sizeof(uint4) * Hg * K);
   ALLOC(d.in_rec, sizeof(grec) * H * d.DR * p->packet_cap);

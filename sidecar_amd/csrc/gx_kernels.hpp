@@ -946,7 +946,10 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
           if (call) {
             const uint32_t q = hs.fifo_head - head0;
             const bool pf = q < n0 && q < (uint32_t)T;
-            l = get_broadcasts_team<T>(d, a, u, hs, cap, pk, lim, d.p.overhead_bytes, pf ? &pjs[q] : nullptr);
+            const bool filt = d.sfilt && pos != 0xffffffffu;  // a packet registered in a local inbox
+            l = get_broadcasts_team<T>(d, a, u, hs, cap, pk, lim, d.p.overhead_bytes, pf ? &pjs[q] : nullptr,
+                                       filt ? &d.view[(size_t)(pj - d.lo) * d.R] : nullptr,
+                                       filt ? &d.mflag[pj - d.lo] : nullptr);
           }
           called = j + 1;
           const bool live = l || nf;
@@ -1067,6 +1070,7 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
     for (uint32_t x = 0; x < h.z; x++) add_entry(d, a, v, pk[x], SRC_GOSSIP);
     recs += h.z;
   }
+  if (d.sfilt) a.c[C_GOSSIP_MERGES] = a.c[C_STALE] = 0;  // counted by the senders
   kbytes(d, GX_K_MERGE, 28ull * recs + 16ull * cnt + 4, recs);
   for (int i = 0; i < C_NCTR; i++) ctr_atomic(d, i, a.c[i]);
   if (a.changed) mark_change(d);
@@ -1281,9 +1285,11 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     // 12 B per record (word + key) + 8 B per slot read / written + 32 B per retransmit job
     // + 16 B per inbox header + the count
     kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 16ull * deg + 4, c_merge);
-    ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
+    if (!d.sfilt) {  // else counted by the senders
+      ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
+      ctr_atomic(d, C_STALE, c_stale);
+    }
     ctr_atomic(d, C_GOSSIP_ACC, c_acc);
-    ctr_atomic(d, C_STALE, c_stale);
     ctr_atomic(d, C_RETX, ok);
     ctr_atomic(d, C_QDROP, n_retx - ok);
     if (c_wr) {
@@ -1306,8 +1312,11 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
   uint64_t fl = 0;
   if (MERGE_RANGE == 8 && r0 + MERGE_RANGE <= d.Hl) {
     fl = *reinterpret_cast<const uint64_t *>(&d.mflag[r0]);
+    if (fl && d.sfilt) *reinterpret_cast<uint64_t *>(&d.mflag[r0]) = 0;  // the senders flag next round's
   } else {
     for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)d.mflag[r0 + k] << (8 * k);
+    if (fl && d.sfilt)
+      for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) d.mflag[r0 + k] = 0;
   }
   for (; fl; fl &= fl - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)(__builtin_ctzll(fl) >> 3), s_l[wv]);
 }
