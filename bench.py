@@ -187,14 +187,23 @@ def gossip_round_span(lib, cfg, seed, local_rank):
     n = period - 1
     e.run_rounds(n + 1)  # the first stretch on a new stream starts with ~0.15 ms of queue set-up
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0 = e.stats()
     a.record(st)
-    e.run_rounds(n)  # (run_rounds ends with one wake-up kernel, ~25 us, inside the span)
+    e.run_rounds(n)  # (run_rounds ends with one wake-up kernel, ~8 us, inside the span)
     b.record(st)
     b.synchronize()
+    s1 = e.stats()
     us = 1e3 * a.elapsed_time(b) / n
     e.set_stream(None, False)
     e.close()
-    return round(us, 2)
+    # SURVEY §8(d) algorithmic bytes of a gossip record-merge: 22 B (inbound record 13 + slot 9)
+    # + 9 B per accept + 13 B per retransmit queued; the stretch holds gossip rounds only
+    m, acc, rx = (s1[k] - s0[k] for k in ("gossip_merges", "gossip_accepts", "retransmits"))
+    byts = (22 * m + 9 * acc + 13 * rx) / n
+    gbs = byts / (us * 1e3)
+    return round(us, 2), {"bound": "hbm", "scope": "whole gossip round (send + merge kernels), SURVEY 8(d) bytes",
+                          "bytes_per_round": int(byts), "merges_per_round": m // n, "achieved": round(gbs, 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
 def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
@@ -374,7 +383,7 @@ def main():
                   "gossip_merges": split["gossip_merges"],
                   "record_merges_per_s": split["gossip_merges"] / (gms * 1e-3) if gms else None}
         if world == 1:  # without per-launch events: the span of a stretch of gossip-only rounds
-            gossip["round_span_us"] = gossip_round_span(lib, args.config, seed, local_rank)
+            gossip["round_span_us"], gossip["roofline"] = gossip_round_span(lib, args.config, seed, local_rank)
 
     conv = None
     if not args.no_converge:

@@ -246,6 +246,7 @@ GXD void wave_sync() {
 // ------------------------------------------------------------------------ receiver inboxes --
 #define GX_ERR_INBOX 1u  // work_cnt[4]: a received packet slot failed validation (k_inbox_unpack)
 #define GX_WC_ERR 4
+#define GX_WC_SCANS 5  // work_cnt[5]: views streamed by expiry scans so far (wraps; differences only)
 #define GX_WC_N 8
 // Register a packet (global sender key, message entry) in local receiver vi's inbox: one atomic
 // on the receiver's count; returns the inbox position (slot). The header itself (with the record

@@ -68,6 +68,17 @@ struct gx_engine {
   hipStream_t side_stream;
   hipEvent_t side_start, side_done;
   bool side_pending;
+  // Where a round's expiry scans run (round_send_impl): in k_send's prologue (one launch with the
+  // owner ticks and the sends; a block streams its own listed views, fine while almost no view
+  // needs a scan) or, while views do get scanned, in k_owner + k_scan + k_send, where k_scan
+  // streams the listed rows with the whole chip. Decided from the device's count of scanned views
+  // (work_cnt[GX_WC_SCANS]) read back without stalling the device: a snapshot is copied to pinned
+  // memory every few rounds and consumed two snapshots later (scan_probe). Both placements give
+  // the same results; only the time differs.
+  bool scan_heavy;
+  uint32_t *scan_snap;      // [2] pinned host copies of work_cnt[GX_WC_SCANS]
+  hipEvent_t scan_ev[2];
+  uint32_t scan_k, scan_last;
   uint32_t *in_cnt_buf;     // [2][Hl] inbox counts by round parity (Dev::in_cnt, in_cnt_nx)
   int async_phases;         // sharded phase calls return without waiting (gx_set_stream)
   int device;
@@ -295,7 +306,26 @@ static void owner_launch(const Dev &d, hipStream_t s) {
   else if (d.S <= 32) launch_owner<32>(d, s);
   else launch_owner<64>(d, s);
 }
-#define SCAN_GRID 512  // worklist blocks: 2 per CU stream the rows when views expire, a quick exit when none do
+#define SCAN_GRID 2048  // worklist blocks: every listed row of a round streams at once, a quick exit when none do
+
+// Takes the scanned-view count of the snapshot two probes back (its copy completed long ago
+// unless the host runs far ahead; then this waits for it while the device works through the
+// rounds queued since) and records a new one. A view scanned since the previous consumed
+// snapshot selects the k_scan placement.
+static int scan_probe(gx_engine *e) {
+  const uint32_t i = e->scan_k & 1u;
+  if (e->scan_k >= 2) {
+    HIPCHK(hipEventSynchronize(e->scan_ev[i]));
+    const uint32_t v = e->scan_snap[i];
+    e->scan_heavy = v != e->scan_last;
+    e->scan_last = v;
+  }
+  HIPCHK(hipMemcpyAsync(&e->scan_snap[i], &e->d.work_cnt[GX_WC_SCANS], sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIPCHK(hipEventRecord(e->scan_ev[i], e->stream));
+  e->scan_k++;
+  return GX_OK;
+}
 
 // Phases 0-3 (wake, owners, expiry scan, storm, GetBroadcasts) for this engine's hosts.
 static int round_send_impl(gx_engine *e) {
@@ -309,7 +339,7 @@ static int round_send_impl(gx_engine *e) {
   const bool bt_apart = d.p.fd_enable || storm;
   // a round without the detector or the storm: owner ticks, expiry scans and sends in one launch
   // (S <= 16: owner teams of the send's 4 lanes with up to 4 services each)
-  const bool fused = !bt_apart && d.K && d.S <= 16 && !(d.ab & 8u);
+  const bool fused = !bt_apart && d.K && d.S <= 16 && !(d.ab & 8u) && !e->scan_heavy;
   if (fused) {
     LaunchTimer t(e, GX_K_SEND);
     const unsigned g = nblk(d.Hl, 64);
@@ -336,7 +366,7 @@ static int round_send_impl(gx_engine *e) {
     owner_launch(d, s);
   }
   // with the tick finished in k_send, the expiry scans run in k_send's prologue (no k_scan launch)
-  const bool scan_in_send = !bt_apart && d.K && !(d.ab & 4u);
+  const bool scan_in_send = !bt_apart && d.K && !(d.ab & 4u) && !e->scan_heavy;
   if (!scan_in_send) {
     LaunchTimer t(e, GX_K_SCAN);
     const bool ev = !e->log_views.empty();
@@ -668,6 +698,9 @@ int gx_destroy(gx_engine *e) {
   if (e->side_stream) (void)hipStreamDestroy(e->side_stream);
   if (e->side_start) (void)hipEventDestroy(e->side_start);
   if (e->side_done) (void)hipEventDestroy(e->side_done);
+  for (int i = 0; i < 2; i++)
+    if (e->scan_ev[i]) (void)hipEventDestroy(e->scan_ev[i]);
+  if (e->scan_snap) (void)hipHostFree(e->scan_snap);
   delete e;
   return GX_OK;
 }
@@ -705,6 +738,10 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->in_cnt_buf = nullptr;
   e->side_start = e->side_done = nullptr;
   e->side_pending = false;
+  e->scan_heavy = false;
+  e->scan_snap = nullptr;
+  e->scan_ev[0] = e->scan_ev[1] = nullptr;
+  e->scan_k = e->scan_last = 0;
   e->async_phases = 0;
   e->ob_entries = nullptr;
   e->ob_counts = nullptr;
@@ -762,11 +799,15 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->async_phases = 0;
   if (hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&e->side_start, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->scan_ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->scan_ev[1], hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc((void **)&e->scan_snap, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     (void)hipGetLastError();
     gx_destroy(e);
     return GX_EIO;
   }
+  e->scan_snap[0] = e->scan_snap[1] = 0;
   // per-host arrays hold this shard's Hl hosts; the message table also takes the packets received
   // from other shards (at most (H - Hl) * K), so it is sized H * K.
   size_t Hg = d.H, H = d.Hl, K = d.KE ? d.KE : 1;
@@ -914,6 +955,10 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
   if (!e || e->d.G > 1) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   for (uint32_t i = 0; i < n_rounds; i++) {
+    if (i % 2 == 0) {  // the device then runs at most ~4 rounds behind the host
+      int rc = scan_probe(e);
+      if (rc) return rc;
+    }
     int rc = run_one_round(e);
     if (rc) return rc;
     if (e->pending_ev.size() > 4096) {
@@ -2068,6 +2113,7 @@ int gx_round_end(gx_engine *e) {
   if (rc) return rc;
   e->d.round++;
   rc = wake_all(e);
+  if (!rc) rc = scan_probe(e);
   return rc ? rc : phase_done(e);
 }
 

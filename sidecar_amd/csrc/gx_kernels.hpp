@@ -402,6 +402,7 @@ __global__ __launch_bounds__(B) void k_owner(Dev d) {
 // ts + lifespan < now), so a round with nothing to expire launches a small grid that exits at
 // once. A listed row is streamed with 16-B loads (4 slots per thread per 1024-slot tile), the
 // lifespans applied, and the first list_cap tombstones compacted in key order (packed block scan).
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 struct ScanLds {
   unsigned long long wave[4];
   unsigned long long red[4];
@@ -420,6 +421,22 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   uint32_t n_exp = 0;
   unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, mexp = ~0ull;
   uint32_t t = threadIdx.x;
+  // VEC: the next tile's two 16-B words per thread are in flight while this tile is processed
+  // (nontemporal: a scanned row is not re-read soon)
+  ulonglong2 nx[2];
+  auto ld_tile = [&](uint32_t base) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t r0 = base + 512 * h + 2 * t;
+      if (r0 < d.R) {
+        v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r0]));
+        nx[h] = make_ulonglong2(x.x, x.y);
+      } else {
+        nx[h] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+      }
+    }
+  };
+  if (VEC) ld_tile(0);
   for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
     uint64_t w[4], nw[4];
     bool ex[4];
@@ -429,15 +446,15 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
       valid[2 * h] = r0 < d.R;
       valid[2 * h + 1] = r0 + 1 < d.R;
-      if (VEC && valid[2 * h]) {
-        ulonglong2 p = *reinterpret_cast<const ulonglong2 *>(&row[r0]);
-        w[2 * h] = p.x;
-        w[2 * h + 1] = p.y;
+      if (VEC) {
+        w[2 * h] = nx[h].x;
+        w[2 * h + 1] = nx[h].y;
       } else {
         w[2 * h] = valid[2 * h] ? row[r0] : GX_SLOT_ABSENT;
         w[2 * h + 1] = valid[2 * h + 1] ? row[r0 + 1] : GX_SLOT_ABSENT;
       }
     }
+    if (VEC && base + 4 * blockDim.x < d.R) ld_tile(base + 4 * blockDim.x);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       bool gc;
@@ -459,6 +476,8 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
         if (ch1) row[r0 + 1] = nw[2 * h + 1];
       }
     }
+    // a tile without expirations (GC writes only) needs no compaction: one barrier
+    if (!__syncthreads_or(ex[0] || ex[1] || ex[2] || ex[3])) continue;
     unsigned long long cnt = (unsigned long long)(ex[0] + ex[1]) | ((unsigned long long)(ex[2] + ex[3]) << 16);
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
@@ -500,6 +519,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   }
   mexp = block_min(mexp, s_red);
   if (threadIdx.x == 0) {
+    atomicAdd(&d.work_cnt[GX_WC_SCANS], 1u);
     *cnt_out = n_exp;
     d.minexp[oi] = mexp;  // exact bound after the scan
     if (last_key) d.vlc[oi] = ts_of(row[last_key - 1]);
@@ -672,7 +692,6 @@ GXD uint64_t spread32(uint64_t x) {  // bit i -> bit 2i
   x = (x | (x << 1)) & 0x5555555555555555ull;
   return x;
 }
-typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 template <bool EV, bool NT>
 __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   __shared__ uint32_t s_cnt[2][8];
