@@ -121,6 +121,7 @@ struct Dev {
   uint32_t logS;       // log2(S) when S is a power of two
   int departures;      // p.depart_round >= 0 && p.depart_ppm
   uint32_t nblk_ae;    // digest blocks per row, ceil(R / GX_DIGEST_SLOTS)
+  uint32_t *snap;      // this round's k_send stores work_cnt[GX_WC_SCANS] here (pinned host memory), or null
   uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
   uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels): bit 2
                        // expiry scans in k_scan, bit 3 owner ticks in k_owner (not inside k_send)

@@ -73,10 +73,11 @@ struct gx_engine {
   // needs a scan) or, while views do get scanned, in k_owner + k_scan + k_send, where k_scan
   // streams the listed rows with the whole chip. Decided from the device's count of scanned views
   // (work_cnt[GX_WC_SCANS]) read back without stalling the device: a snapshot is copied to pinned
-  // memory every few rounds and consumed two snapshots later (scan_probe). Both placements give
+  // memory every second round and consumed two snapshots later (scan_probe_begin). Both placements give
   // the same results; only the time differs.
   bool scan_heavy;
-  uint32_t *scan_snap;      // [2] pinned host copies of work_cnt[GX_WC_SCANS]
+  uint32_t *scan_snap;      // [2] pinned host copies of work_cnt[GX_WC_SCANS], written by k_send
+  uint32_t *scan_snap_dev;  // the same memory as the device addresses it
   hipEvent_t scan_ev[2];
   uint32_t scan_k, scan_last;
   uint32_t *in_cnt_buf;     // [2][Hl] inbox counts by round parity (Dev::in_cnt, in_cnt_nx)
@@ -308,11 +309,14 @@ static void owner_launch(const Dev &d, hipStream_t s) {
 }
 #define SCAN_GRID 2048  // worklist blocks: every listed row of a round streams at once, a quick exit when none do
 
-// Takes the scanned-view count of the snapshot two probes back (its copy completed long ago
-// unless the host runs far ahead; then this waits for it while the device works through the
-// rounds queued since) and records a new one. A view scanned since the previous consumed
-// snapshot selects the k_scan placement.
-static int scan_probe(gx_engine *e) {
+// Every second round: takes the scanned-view count of the snapshot two probes back (its kernel
+// finished long ago unless the host runs far ahead; then this waits for it while the device works
+// through the rounds queued since) and has this round's k_send store a new one (Dev::snap, one
+// 4-B store to pinned host memory; scan_probe_end records its event). A view scanned between the
+// two consumed snapshots selects the k_scan placement.
+static int scan_probe_begin(gx_engine *e) {
+  e->d.snap = nullptr;
+  if (e->d.round % 2) return GX_OK;
   const uint32_t i = e->scan_k & 1u;
   if (e->scan_k >= 2) {
     HIPCHK(hipEventSynchronize(e->scan_ev[i]));
@@ -320,10 +324,14 @@ static int scan_probe(gx_engine *e) {
     e->scan_heavy = v != e->scan_last;
     e->scan_last = v;
   }
-  HIPCHK(hipMemcpyAsync(&e->scan_snap[i], &e->d.work_cnt[GX_WC_SCANS], sizeof(uint32_t), hipMemcpyDeviceToHost,
-                        e->stream));
-  HIPCHK(hipEventRecord(e->scan_ev[i], e->stream));
+  e->d.snap = &e->scan_snap_dev[i];
+  return GX_OK;
+}
+static int scan_probe_end(gx_engine *e) {
+  if (!e->d.snap) return GX_OK;
+  HIPCHK(hipEventRecord(e->scan_ev[e->scan_k & 1u], e->stream));
   e->scan_k++;
+  e->d.snap = nullptr;
   return GX_OK;
 }
 
@@ -331,6 +339,10 @@ static int scan_probe(gx_engine *e) {
 static int round_send_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
+  {
+    int rc = scan_probe_begin(e);
+    if (rc) return rc;
+  }
   d.n_remote = 0;
   hipStream_t s = e->stream;
   bool vec = (d.R % 2) == 0;
@@ -359,7 +371,7 @@ static int round_send_impl(gx_engine *e) {
 #undef GX_TICK_SEND
 #undef GX_TS
     HIPCHK(hipGetLastError());
-    return GX_OK;
+    return scan_probe_end(e);
   }
   {
     LaunchTimer t(e, GX_K_OWNER);
@@ -409,7 +421,7 @@ static int round_send_impl(gx_engine *e) {
     }
   }
   HIPCHK(hipGetLastError());
-  return GX_OK;
+  return scan_probe_end(e);
 }
 
 // Phase 4: gather-then-merge of every receiver's inbox (local and received packets).
@@ -739,7 +751,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->side_start = e->side_done = nullptr;
   e->side_pending = false;
   e->scan_heavy = false;
-  e->scan_snap = nullptr;
+  e->scan_snap = e->scan_snap_dev = nullptr;
   e->scan_ev[0] = e->scan_ev[1] = nullptr;
   e->scan_k = e->scan_last = 0;
   e->async_phases = 0;
@@ -802,7 +814,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
       hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->scan_ev[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->scan_ev[1], hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&e->scan_snap, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void **)&e->scan_snap, 2 * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&e->scan_snap_dev, e->scan_snap, 0) != hipSuccess) {
     (void)hipGetLastError();
     gx_destroy(e);
     return GX_EIO;
@@ -955,10 +968,6 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
   if (!e || e->d.G > 1) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   for (uint32_t i = 0; i < n_rounds; i++) {
-    if (i % 2 == 0) {  // the device then runs at most ~4 rounds behind the host
-      int rc = scan_probe(e);
-      if (rc) return rc;
-    }
     int rc = run_one_round(e);
     if (rc) return rc;
     if (e->pending_ev.size() > 4096) {
@@ -2113,7 +2122,6 @@ int gx_round_end(gx_engine *e) {
   if (rc) return rc;
   e->d.round++;
   rc = wake_all(e);
-  if (!rc) rc = scan_probe(e);
   return rc ? rc : phase_done(e);
 }
 

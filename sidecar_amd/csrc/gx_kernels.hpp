@@ -1009,6 +1009,7 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   Acc a;
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
+  if (d.snap && blockIdx.x == 0 && threadIdx.x == 0) *d.snap = d.work_cnt[GX_WC_SCANS];  // scan_probe_begin
   if constexpr (OWN > 0) {
     if (threadIdx.x == 0) {
       s_nscan = 0;
