@@ -750,7 +750,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->in_cnt_buf = nullptr;
   e->side_start = e->side_done = nullptr;
   e->side_pending = false;
-  e->scan_heavy = false;
+  e->scan_heavy = true;  // k_scan placement until the first snapshots say no view gets scanned
   e->scan_snap = e->scan_snap_dev = nullptr;
   e->scan_ev[0] = e->scan_ev[1] = nullptr;
   e->scan_k = e->scan_last = 0;

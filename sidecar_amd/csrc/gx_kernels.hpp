@@ -409,6 +409,7 @@ struct ScanLds {
   uint32_t lu[TILE_OWNERS];
   uint32_t last;
 };
+#define SCAN_PF 1  // 4 tiles in flight (139 VGPRs, 3 waves/SIMD) measured slower on cfg 3: 1.59 vs 1.29 ms per round
 template <bool VEC, bool EV>
 GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t *cnt_out, ScanLds &sm) {
   unsigned long long *s_wave = sm.wave, *s_red = sm.red;
@@ -423,21 +424,32 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   uint32_t t = threadIdx.x;
   // VEC: the next tile's two 16-B words per thread are in flight while this tile is processed
   // (nontemporal: a scanned row is not re-read soon)
-  ulonglong2 nx[2];
-  auto ld_tile = [&](uint32_t base) {
+  // (SCAN_PF tiles in flight per block: one 2 MB row per block is latency-bound otherwise)
+  ulonglong2 nx[SCAN_PF][2];
+  auto ld_into = [&](uint32_t base, ulonglong2 *dst) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint32_t r0 = base + 512 * h + 2 * t;
       if (r0 < d.R) {
         v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r0]));
-        nx[h] = make_ulonglong2(x.x, x.y);
+        dst[h] = make_ulonglong2(x.x, x.y);
       } else {
-        nx[h] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+        dst[h] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
       }
     }
   };
-  if (VEC) ld_tile(0);
-  for (uint32_t base = 0; base < d.R; base += 4 * blockDim.x) {
+  if (VEC) {
+#pragma unroll
+    for (int q = 0; q < SCAN_PF; q++) ld_into(1024u * q, nx[q]);
+  }
+  // S | 128: an owner's slots sit in S/2 adjacent lanes of one wave, so the server times of a
+  // tile's owners (the last expired record of each, key order) come from a ballot, with no LDS
+  const bool wave_times = VEC && d.S >= 2 && (128 % d.S) == 0;
+  const bool ev_on = EV && evk >= 0;
+  bool listing = true;     // block-uniform: list positions (or event positions) still needed
+  uint32_t my_last = 0;    // 1 + this thread's last expired key (state.LastChanged)
+  unsigned long long cnt_tail = 0;  // expirations counted per thread once the list is full
+  auto tile = [&](uint32_t base, const ulonglong2 *cur) {
     uint64_t w[4], nw[4];
     bool ex[4];
     bool valid[4];
@@ -447,14 +459,13 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
       valid[2 * h] = r0 < d.R;
       valid[2 * h + 1] = r0 + 1 < d.R;
       if (VEC) {
-        w[2 * h] = nx[h].x;
-        w[2 * h + 1] = nx[h].y;
+        w[2 * h] = cur[h].x;
+        w[2 * h + 1] = cur[h].y;
       } else {
         w[2 * h] = valid[2 * h] ? row[r0] : GX_SLOT_ABSENT;
         w[2 * h + 1] = valid[2 * h + 1] ? row[r0 + 1] : GX_SLOT_ABSENT;
       }
     }
-    if (VEC && base + 4 * blockDim.x < d.R) ld_tile(base + 4 * blockDim.x);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       bool gc;
@@ -476,8 +487,33 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
         if (ch1) row[r0 + 1] = nw[2 * h + 1];
       }
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+      if (ex[k]) my_last = r + 1;  // keys rise with k within a thread and across tiles
+    }
+    if (wave_times) {
+      const uint32_t lane = t & 63, lpo = d.S / 2, gb = lane & ~(lpo - 1);
+      const uint64_t gm = (lpo == 64 ? ~0ull : ((1ull << lpo) - 1ull)) << gb;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const bool e0 = ex[2 * h], e1 = ex[2 * h + 1];
+        const uint64_t gbits = __ballot(e0 || e1) & gm;
+        if (gbits && lane == 63u - (uint32_t)__clzll(gbits)) {  // the owner's last lane with an expiry
+          const uint32_t r = base + 512 * h + 2 * t + (e1 ? 1u : 0u);
+          gx_server_times *st = srv_times(d, oi + d.lo, r / d.S);
+          const int64_t ts = ts_of(e1 ? nw[2 * h + 1] : nw[2 * h]);
+          st->last_updated_ns = ts;
+          st->last_changed_ns = ts;
+        }
+      }
+    }
+    if (!listing) {  // the list is full and nothing needs positions: count only
+      cnt_tail += ex[0] + ex[1] + ex[2] + ex[3];
+      return;
+    }
     // a tile without expirations (GC writes only) needs no compaction: one barrier
-    if (!__syncthreads_or(ex[0] || ex[1] || ex[2] || ex[3])) continue;
+    if (!__syncthreads_or(ex[0] || ex[1] || ex[2] || ex[3])) return;
     unsigned long long cnt = (unsigned long long)(ex[0] + ex[1]) | ((unsigned long long)(ex[2] + ex[3]) << 16);
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
@@ -498,7 +534,16 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
       }
     }
     uint32_t tn = (uint32_t)(fld(tot, 0) + fld(tot, 1));
-    if (tn) {  // ServiceChanged per expiry (:673-676): server times, state.LastChanged, events
+    if (tn && wave_times) {  // server times done above; events in list order
+      if (ev_on) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          if (!ex[k]) continue;
+          uint32_t r = base + 512 * (k >> 1) + 2 * t + (k & 1);
+          ev_put(d, evk, ev0 + pos[k], r, nw[k], st_of(w[k]));
+        }
+      }
+    } else if (tn) {  // ServiceChanged per expiry (:673-676): server times, state.LastChanged, events
       uint32_t o0 = base / d.S, oe = ((base + 4 * blockDim.x < d.R ? base + 4 * blockDim.x : d.R) - 1) / d.S;
       for (uint32_t i = t; i <= oe - o0; i += blockDim.x) s_lu[i] = 0;
       __syncthreads();
@@ -516,6 +561,24 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
       __syncthreads();
     }
     n_exp += tn;
+    listing = ev_on || !wave_times || n_exp < list_cap;  // without wave_times the LDS path keeps the server times
+  };
+  for (uint32_t base = 0; base < d.R; base += SCAN_PF * 1024u) {
+#pragma unroll
+    for (int q = 0; q < SCAN_PF; q++) {
+      const uint32_t b = base + 1024u * q;
+      if (b >= d.R) break;
+      ulonglong2 cur[2] = {nx[q][0], nx[q][1]};
+      if (VEC && b + SCAN_PF * 1024u < d.R) ld_into(b + SCAN_PF * 1024u, nx[q]);
+      tile(b, cur);
+    }
+  }
+  {
+    unsigned long long tail;
+    (void)block_excl_scan64(cnt_tail, s_wave, tail);
+    n_exp += (uint32_t)tail;
+    const unsigned long long lk = ~block_min(~(unsigned long long)my_last, s_red);
+    last_key = (uint32_t)lk;
   }
   mexp = block_min(mexp, s_red);
   if (threadIdx.x == 0) {
