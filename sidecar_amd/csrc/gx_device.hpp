@@ -124,7 +124,9 @@ struct Dev {
   uint32_t *snap;      // this round's k_send stores work_cnt[GX_WC_SCANS] here (pinned host memory), or null
   uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
   uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels): bit 2
-                       // expiry scans in k_scan, bit 3 owner ticks in k_owner (not inside k_send)
+                       // expiry scans in k_scan, bit 3 owner ticks in k_owner (not inside k_send),
+                       // bit 4 default-policy storm stream, bit 5 default-policy k_ae, bit 7 the
+                       // receivers' own dead-record filter (k_merge_lean) instead of the senders'
 };
 
 // ------------------------------------------------------------------- schedule RNG (seeded) --
