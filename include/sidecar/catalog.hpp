@@ -101,12 +101,19 @@ class Cluster {
     host_names_.push_back(name);
     ids_.emplace_back();
     id_names_.emplace_back();
+    slot_free_since_.emplace_back();
     return id;
   }
   // A service ID seen for the first time takes the owner's next free slot (the reference creates
   // it, services_state.go:310-318). When all S are taken, a slot that no view holds any more
-  // (garbage-collected everywhere after TOMBSTONE_LIFESPAN, :645-653) is reused; a queued copy
-  // of its old record is older than the lifespan, so IsStale drops it wherever it arrives.
+  // (garbage-collected everywhere after TOMBSTONE_LIFESPAN, :645-653) is reused, but only once no
+  // copy of its old record can still be merged anywhere. Every copy in a queue or in flight
+  // carries the Updated of a stored version (+ at most 9 SendServices passes of 50 ns), and a
+  // view collects a tombstone only once Updated < now - TOMBSTONE_LIFESPAN; IsStale drops a copy
+  // once Updated < now - TOMBSTONE_LIFESPAN - 1 min (service.go:68-71). So when a slot is first
+  // seen unused at time t1, every copy is stale from t1 + stale_fudge on: the slot is reused
+  // only after that (slot_free_since_); a record of the old ID that is not stale yet restarts the
+  // clock (Rec), since it may be stored again.
   uint16_t Id(uint32_t host, const std::string &id) {
     auto &m = ids_[host];
     auto it = m.find(id);
@@ -118,9 +125,20 @@ class Cluster {
     } else {
       uint64_t used = 0;
       check(gx_owner_slots_in_use(e_, host, &used), "gx_owner_slots_in_use");
-      s = 0;
-      while (s < p_.n_services && ((used >> s) & 1u)) s++;
+      auto &since = slot_free_since_[host];
+      since.resize(p_.n_services, -1);
+      const int64_t now = Now();
+      s = p_.n_services;
+      for (uint16_t k = 0; k < p_.n_services; k++) {
+        if ((used >> k) & 1u) {
+          since[k] = -1;
+        } else {
+          if (since[k] < 0) since[k] = now;  // first seen unused
+          if (s == p_.n_services && now - since[k] > p_.stale_fudge_ns + 1000) s = k;
+        }
+      }
       if (s == p_.n_services) throw std::runtime_error("service table full: " + id);
+      since[s] = -1;
       m.erase(id_names_[host][s]);  // the slot's old ID is forgotten, with its metadata
       id_names_[host][s] = id;
       const uint64_t key = (uint64_t)host * p_.n_services + s;
@@ -147,6 +165,10 @@ class Cluster {
     r.updated_ns = svc.Updated;
     r.host = h;
     r.svc = Id(h, svc.ID);
+    auto &since = slot_free_since_[h];
+    if (r.svc < since.size() && since[r.svc] >= 0 &&
+        svc.Updated >= Now() - p_.tombstone_lifespan_ns - p_.stale_fudge_ns)  // not IsStale: may be stored
+      since[r.svc] = -1;
     r.status = (uint8_t)svc.Status;
     return r;
   }
@@ -201,6 +223,7 @@ class Cluster {
   std::vector<std::string> host_names_;
   std::vector<std::map<std::string, uint16_t>> ids_;
   std::vector<std::vector<std::string>> id_names_;
+  std::vector<std::vector<int64_t>> slot_free_since_;  // per owner slot: first time seen unused, -1
   std::map<uint32_t, std::vector<uint16_t>> static_;
   std::map<uint64_t, std::string> names_;  // record key -> Service.Name
   bool names_dirty_ = false;

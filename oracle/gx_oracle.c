@@ -84,6 +84,7 @@ struct gx_engine {
   uint32_t *fd_peers;     /* H * K  gossip targets (memberlist's choice) */
   uint32_t *fd_np;        /* H */
   uint32_t *name_rank;    /* R  ByService: rank of each record's Service.Name, NULL until set */
+  int64_t *in_stamp;      /* H * KE  round a received slot last carried the sender key (sharded), lazy */
   gx_stats st;
 };
 static void free_names(gx_engine *e);
@@ -1347,6 +1348,7 @@ int gx_destroy(gx_engine *e) {
   free(e->srvt);
   free(e->vlc);
   free(e->name_rank);
+  free(e->in_stamp);
   for (int i = 0; i < GX_MAX_LISTENERS; i++) free(e->lst[i].ring);
   free(e->x_t);
   free(e->x_mine);
@@ -1665,15 +1667,19 @@ int gx_each_service_sorted(gx_engine *e, uint32_t view, uint32_t owner, gx_servi
   if (!e || !is_local(e, view) || (owner != GX_ALL_OWNERS && owner >= e->H) || (cap && !out)) return GX_EINVAL;
   return sorted_view(e, view, owner, 0, out, NULL, cap, n_out);
 }
-static const char *sn_base;
-static const uint64_t *sn_off;
+/* one record's Service.Name for the comparator: no file-static state, so engines may sort in
+ * parallel threads */
+typedef struct {
+  const char *p;
+  uint64_t len;
+  uint32_t r;
+} name_ref;
 static int cmp_name(const void *pa, const void *pb) {
-  const uint32_t a = *(const uint32_t *)pa, b = *(const uint32_t *)pb;
-  const uint64_t la = sn_off[a + 1] - sn_off[a], lb = sn_off[b + 1] - sn_off[b];
-  const int c = memcmp(sn_base + sn_off[a], sn_base + sn_off[b], la < lb ? la : lb);
+  const name_ref *a = (const name_ref *)pa, *b = (const name_ref *)pb;
+  const int c = memcmp(a->p, b->p, a->len < b->len ? a->len : b->len);
   if (c) return c;
-  if (la != lb) return la < lb ? -1 : 1;
-  return a < b ? -1 : (a > b);
+  if (a->len != b->len) return a->len < b->len ? -1 : 1;
+  return a->r < b->r ? -1 : (a->r > b->r);
 }
 int gx_set_service_names(gx_engine *e, const char *names, const uint64_t *off) {
   if (!e || !off || off[0] != 0) return GX_EINVAL;
@@ -1681,20 +1687,19 @@ int gx_set_service_names(gx_engine *e, const char *names, const uint64_t *off) {
     if (off[r + 1] < off[r]) return GX_EINVAL;
   if (off[e->R] && !names) return GX_EINVAL;
   static const char empty[1] = {0};
-  uint32_t *idx = (uint32_t *)malloc(sizeof(uint32_t) * (e->R ? e->R : 1));
-  for (uint32_t r = 0; r < e->R; r++) idx[r] = r;
-  sn_base = names ? names : empty;
-  sn_off = off;
-  qsort(idx, e->R, sizeof(uint32_t), cmp_name); /* distinct names in bytewise order */
+  const char *base = names ? names : empty;
+  name_ref *idx = (name_ref *)malloc(sizeof(name_ref) * (e->R ? e->R : 1));
+  for (uint32_t r = 0; r < e->R; r++) {
+    idx[r].p = base + off[r];
+    idx[r].len = off[r + 1] - off[r];
+    idx[r].r = r;
+  }
+  qsort(idx, e->R, sizeof(name_ref), cmp_name); /* distinct names in bytewise order */
   if (!e->name_rank) e->name_rank = (uint32_t *)malloc(sizeof(uint32_t) * (e->R ? e->R : 1));
   uint32_t g = 0;
   for (uint32_t k = 0; k < e->R; k++) {
-    if (k) {
-      const uint32_t a = idx[k - 1], b = idx[k];
-      const uint64_t la = off[a + 1] - off[a], lb = off[b + 1] - off[b];
-      if (la != lb || memcmp(sn_base + off[a], sn_base + off[b], la)) g++;
-    }
-    e->name_rank[idx[k]] = g;
+    if (k && (idx[k - 1].len != idx[k].len || memcmp(idx[k - 1].p, idx[k].p, idx[k].len))) g++;
+    e->name_rank[idx[k].r] = g;
   }
   free(idx);
   return GX_OK;
@@ -1940,16 +1945,49 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
     }
   return GX_OK;
 }
+/* A received slot is refused (GX_EINVAL, nothing of the call applied) unless: its sender key m <
+ * H*KE names a packet entry of another shard's host, no slot of this round carried m before
+ * (one packet per sender entry), the receiver is on this shard, len <= packet_cap, n_fd <=
+ * fd_msg_cap, and every record key < R. */
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
   if (!e || (bytes && !buf)) return GX_EINVAL;
   size_t sb = slot_bytes(e);
   if (bytes % sb) return GX_EINVAL;
   const uint8_t *p = (const uint8_t *)buf;
+  if (!e->in_stamp) {
+    e->in_stamp = (int64_t *)malloc(sizeof(int64_t) * (size_t)e->H * (e->KE ? e->KE : 1));
+    if (!e->in_stamp) return GX_ENOMEM;
+    for (size_t m = 0; m < (size_t)e->H * (e->KE ? e->KE : 1); m++) e->in_stamp[m] = -1;
+  }
+  uint8_t *seen = (uint8_t *)calloc((size_t)e->H * (e->KE ? e->KE : 1), 1);
+  if (!seen) return GX_ENOMEM;
+  int bad = 0;
+  for (size_t off = 0; off < bytes && !bad; off += sb) { /* validate every slot before applying any */
+    uint32_t hdr[4];
+    memcpy(hdr, p + off, 16);
+    uint32_t m = hdr[0], dst = hdr[1], len = hdr[2], nfd = e->p.fd_enable ? hdr[3] : 0;
+    (void)nfd;
+    if (m >= e->H * e->KE || is_local(e, m / e->KE) || !is_local(e, dst) || len > e->p.packet_cap ||
+        (e->p.fd_enable && hdr[3] > e->p.fd_msg_cap)) {
+      bad = 1;
+      break;
+    }
+    for (uint32_t y = 0; y < len; y++) {
+      grec g;
+      memcpy(&g, p + off + 16 + 16ull * y, sizeof(g));
+      if (g.r >= e->R) bad = 1;
+    }
+    /* a key seen twice in this call, or taken by an earlier call of this round */
+    if (seen[m] || e->in_stamp[m] == e->round) bad = 1;
+    seen[m] = 1;
+  }
+  free(seen);
+  if (bad) return GX_EINVAL;
   for (size_t off = 0; off < bytes; off += sb) {
     uint32_t hdr[4];
     memcpy(hdr, p + off, 16);
     uint32_t m = hdr[0], dst = hdr[1], len = hdr[2], nfd = e->p.fd_enable ? hdr[3] : 0;
-    if (m >= e->H * e->KE || !is_local(e, dst) || len > e->p.packet_cap || nfd > e->p.fd_msg_cap) return GX_EINVAL;
+    e->in_stamp[m] = e->round;
     memcpy(&e->msg[(size_t)m * e->p.packet_cap], p + off + 16, 16ull * len);
     e->msg_len[m] = len;
     e->msg_dst[m] = dst;

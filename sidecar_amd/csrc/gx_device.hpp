@@ -64,6 +64,7 @@ struct Dev {
   uint32_t lo, Hl, G, gid;  // this engine owns hosts [lo, lo + Hl); per-host arrays are local
   uint32_t n_remote;        // packets received from other shards this round
   uint32_t *msg_key;        // [H*KE] global sender * KE + j * NG + n of each packet entry
+  uint32_t *in_stamp;       // [H*KE] sharded: round + 1 when a received slot last carried the key
   int64_t round, now;
   int partitioned;
   uint64_t *view;

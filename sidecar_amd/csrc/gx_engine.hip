@@ -698,7 +698,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, d.in_stamp, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf,
@@ -841,6 +841,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.DI = p->inbox_slots ? p->inbox_slots : 64;
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
   d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
+  if (d.ab) fprintf(stderr, "gx: GX_AB_FLAGS=%u: A/B measurement kernel paths active\n", d.ab);
   // one shard: every packet's receiver is local, so its sender reads the receiver's view slots
   // (A/B bit 128: the receivers' own filter pass, k_merge_lean)
   d.sfilt = (d.G == 1 && !(d.ab & 128u)) ? 1u : 0u;
@@ -880,6 +881,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
   if (d.G > 1) {
     ALLOC(e->ob_entries, sizeof(uint32_t) * H * K);
+    ALLOC(d.in_stamp, sizeof(uint32_t) * Hg * K);
+    HIPCHK(hipMemset(d.in_stamp, 0, sizeof(uint32_t) * Hg * K));
     ALLOC(e->ob_total, sizeof(uint32_t));
     ALLOC(e->ob_counts, sizeof(uint32_t) * p->n_shards * (1 + 2 * ((H * K + 255) / 256)));
     size_t np = Hg / 2 + 1;

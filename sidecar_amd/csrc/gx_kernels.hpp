@@ -1196,8 +1196,8 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
   if (deg > npre && lane >= npre && lane < deg) hd = d.in_hdr[(size_t)vi * d.DI + lane];
   // sender order: rank of each header's key among the deg distinct keys
   const uint32_t hkey = lane < deg ? hd.x : 0xffffffffu;
-  uint32_t hrank = 0;
-  for (uint32_t j = 0; j < deg; j++) hrank += rdl(hkey, j) < hkey;
+  uint32_t hrank = 0;  // ties (refused by k_inbox_unpack) broken by lane: every rank is written once
+  for (uint32_t j = 0; j < deg; j++) hrank += rdl(hkey, j) < hkey || (rdl(hkey, j) == hkey && j < lane);
   if (lane < deg) s_hdr[hrank] = hd;
   wave_sync();
   const uint4 sh = lane < deg ? s_hdr[lane] : make_uint4(0u, 0u, 0u, 0u);  // {key, entry, len, slot} of packet `lane`
@@ -2696,9 +2696,11 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
 }
 
 // Inbox: received slots -> message entries [Hl*K, Hl*K + n), registered in the receivers'
-// inboxes. A slot is checked like the oracle's gx_inbox_unpack does (sender key < H*K, receiver on
-// this shard, len <= packet_cap, n_fd <= fd_msg_cap) and its record keys < R; a bad slot is
-// skipped and flagged (work_cnt[GX_WC_ERR]), and the next call that waits returns GX_EINVAL.
+// inboxes. A slot is checked like the oracle's gx_inbox_unpack does: sender key < H*K and its
+// sender on another shard, the key not seen before this round (one key per sender packet entry;
+// a repeated key would give the merge two headers of equal rank), receiver on this shard, len <=
+// packet_cap, n_fd <= fd_msg_cap, record keys < R. A bad slot is skipped and flagged
+// (work_cnt[GX_WC_ERR]), and the next call that waits returns GX_EINVAL.
 __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   uint32_t i = blockIdx.x;
   if (i >= n) return;
@@ -2709,9 +2711,16 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   uint32_t key = hdr[0], dst = hdr[1], len = hdr[2], nfd = fcap ? hdr[3] : 0;
   size_t e = (size_t)d.Hl * d.KE + i;
   const grec *recs = reinterpret_cast<const grec *>(src + 16);
-  bool bad = key >= d.H * d.KE || dst - d.lo >= d.Hl || len > d.p.packet_cap || nfd > fcap;
+  bool bad = key >= d.H * d.KE || key / d.KE - d.lo < d.Hl || dst - d.lo >= d.Hl || len > d.p.packet_cap ||
+             nfd > fcap;
   for (uint32_t x = threadIdx.x; !bad && x < len; x += blockDim.x) bad |= recs[x].r >= d.R;
-  if (__ballot(bad) != 0) {
+  if (__ballot(bad) == 0) {  // a key seen twice this round: the later slot is refused
+    const uint32_t stamp = (uint32_t)d.round + 1u;
+    uint32_t dup = 0;
+    if (threadIdx.x == 0) dup = atomicExch(&d.in_stamp[key], stamp) == stamp;
+    bad = __shfl(dup, 0, 64) != 0;
+  }
+  if (bad) {
     if (threadIdx.x == 0) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);
     return;
   }

@@ -404,17 +404,43 @@ static void test_slot_reuse() {
     }
     So(threw);
   }
+  auto refused = [&](const Service &svc) {
+    try {
+      state.AddServiceEntry(svc);
+    } catch (const std::runtime_error &) {
+      return true;
+    }
+    return false;
+  };
   {
-    cur = "After the tombstones are collected everywhere, a new ID reuses a slot";
+    cur = "A collected slot is not reused while a queued copy of its tombstone can still merge";
     state.AddServiceEntry(Service{"a1", h, t + SEC, sidecar::TOMBSTONE});
     state.AddServiceEntry(Service{"a2", h, t + SEC, sidecar::TOMBSTONE});
-    c.Advance((3 * HOUR + 2 * MIN) / p.round_ns + 10);  // past TOMBSTONE_LIFESPAN
-    state.TombstoneOthersServices();                     // removes the old tombstones (:645-653)
+    // just past TOMBSTONE_LIFESPAN: collected (:645-653) but not yet stale (+1 min, service.go:68-71)
+    c.Advance((3 * HOUR + 2 * SEC) / p.round_ns);
+    state.TombstoneOthersServices();
+    So(!state.Get(h, "a1").has_value() && !state.Get(h, "a2").has_value());
+    So(refused(Service{"a3", h, c.Now(), sidecar::ALIVE}));
+    // a peer still had a1's tombstone queued: it merges as a1, not as a new ID on a1's slot
+    ServicesDelegate peer(c, state);
+    peer.NotifyMsg({Service{"a1", h, t + SEC, sidecar::TOMBSTONE}});
+    So(state.Get(h, "a1").has_value() && state.Get(h, "a1")->Status == sidecar::TOMBSTONE);
+    So(!state.Get(h, "a3").has_value());
+  }
+  {
+    cur = "After the tombstones are collected everywhere, a new ID reuses a slot";
+    c.Advance(2 * MIN / p.round_ns);  // a2's slot: unused for longer than the stale fudge
+    state.TombstoneOthersServices();  // collects a1's tombstone again (:645-653)
     So(!state.Get(h, "a1").has_value() && !state.Get(h, "a2").has_value());
     state.AddServiceEntry(Service{"a3", h, c.Now(), sidecar::ALIVE});
     So(state.Get(h, "a3").has_value());
     auto v = state.SortedServices(h);
     So(v.size() == 1 && v[0].ID == "a3");
+    So(refused(Service{"a4", h, c.Now(), sidecar::ALIVE}));  // a1's slot: its clock restarted by the merge
+    ServicesDelegate peer(c, state);
+    peer.NotifyMsg({Service{"a1", h, t + SEC, sidecar::TOMBSTONE}});  // stale by now: dropped
+    So(!state.Get(h, "a1").has_value());
+    c.Advance(2 * MIN / p.round_ns);
     state.AddServiceEntry(Service{"a4", h, c.Now(), sidecar::ALIVE});
     So(state.Get(h, "a4").has_value() && state.SortedServices(h).size() == 2);
   }

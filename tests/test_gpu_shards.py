@@ -91,7 +91,7 @@ def test_gpu_distshard_rccl_world1(gx_lib):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("field", ["key", "receiver", "len"])
+@pytest.mark.parametrize("field", ["key", "receiver", "len", "local_key", "rec_key", "dup"])
 def test_gpu_corrupt_inbox_slot_refused(gx_lib, field):
     """The device-side validation of received slots matches the oracle's refusal."""
     import torch

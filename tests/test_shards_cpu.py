@@ -150,7 +150,7 @@ def test_delta_ships_only_differing_blocks(oracle_lib):
     assert 40 * n_msgs < w["ae_delta"] < w["ae_full_rows_equivalent"]
 
 
-@pytest.mark.parametrize("field", ["key", "receiver", "len"])
+@pytest.mark.parametrize("field", ["key", "receiver", "len", "local_key", "rec_key", "dup"])
 def test_corrupt_inbox_slot_refused(oracle_lib, field):
     import torch
     from tests.corrupt_inbox import run, run_valid
