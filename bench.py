@@ -42,6 +42,14 @@ CONFIGS = {
                      p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
                             queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
                             partition_end=50, storm_round=5, ae_period_rounds=100)),
+    # cfg 5 at Sidecar's own defaults (config/config.go:45-47, main.go:252-259): PushPullInterval 20 s
+    # (100 rounds) and GossipMessages 15 (up to 15 GetBroadcasts packets per gossip target per round)
+    "cfg5_defaults": dict(desc="cfg5 at Sidecar's defaults (PushPullInterval 20 s, GossipMessages 15): 32768 hosts "
+                               "x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds [0,50) + "
+                               "ExpireServer storm at round 5 + heal",
+                          p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
+                                 queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                                 partition_end=50, storm_round=5, ae_period_rounds=100, gossip_messages=15)),
     # configs[1]: 4096 x 16, fanout 3, cap 32, one GPU (cold start: every view knows its own records)
     "cfg2": dict(desc="4096 hosts x 16 services, fanout 3, cap 32 records/msg, own-records start, "
                       "push-pull every 10 rounds",
@@ -167,25 +175,50 @@ class Cluster:
         self.e.close()
 
 
-def gossip_round_span(lib, cfg, seed, local_rank):
-    """Device time per gossip round without per-launch instrumentation: the second stretch of rounds
-    between two push-pull rounds after the storm (inside the bench window; no storm, no push-pull
-    in it), bracketed by two events on the engine's stream (the caller's torch stream). The
-    per-class split above records an event pair around every launch, which adds about 10 us per
-    round."""
+def gossip_stretch_start(cfg, accepting=False):
+    """First round of a stretch of 9 gossip-only rounds (no storm, no push-pull): by default the
+    second such stretch after the storm (rounds 21..29 of cfg 5: every record gossiped there is
+    already held, the senders' filter drops all of it); `accepting`: the first stretch after the
+    heal (rounds 51..59 of cfg 5), where the heal's push-pull accepts are retransmitted and gossip
+    records are live. None when the config has no partition (accepting)."""
+    p = CONFIGS[cfg]["p"]
+    period = p.get("ae_period_rounds", 0)
+    phase = p.get("ae_phase", 0)
+    p10 = min(period or 10, 10)
+
+    def has_ae(r0):
+        return period and any(r % period == phase for r in range(r0, r0 + p10 - 1))
+
+    if accepting:
+        if not p.get("partition_end", 0):
+            return None
+        s = p["partition_end"] + 1
+    else:
+        s = phase + 1  # the round after a push-pull round, past the storm, then one stretch later
+        while s <= p.get("storm_round", -1):
+            s += p10
+        s += p10
+    while has_ae(s):
+        s += 1
+    return s
+
+
+def gossip_round_span(lib, cfg, seed, local_rank, start=None):
+    """Device time per gossip round without per-launch instrumentation: a stretch of period - 1
+    gossip-only rounds from `start` (gossip_stretch_start), bracketed by two events on the engine's
+    stream (the caller's torch stream). The per-class split above records an event pair around
+    every launch, which adds about 10 us per round."""
     import torch
     p = CONFIGS[cfg]["p"]
-    period = p.get("ae_period_rounds", 0) or 10
-    phase = p.get("ae_phase", 0)
+    period = min(p.get("ae_period_rounds", 0) or 10, 10)
+    if start is None:
+        start = gossip_stretch_start(cfg)
     e = make_engine(lib, cfg, seed, local_rank)
-    r0 = phase + 1  # the round after a push-pull round, past the storm
-    while r0 <= p.get("storm_round", -1):
-        r0 += period
-    e.run_rounds(r0)
+    e.run_rounds(start - period)
     st = torch.cuda.Stream()  # a stream of its own (launches on the legacy default stream are slower)
     e.set_stream(st.cuda_stream, False)
     n = period - 1
-    e.run_rounds(n + 1)  # the first stretch on a new stream starts with ~0.15 ms of queue set-up
+    e.run_rounds(period)  # the first stretch on a new stream starts with ~0.15 ms of queue set-up
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s0 = e.stats()
     a.record(st)
@@ -202,8 +235,55 @@ def gossip_round_span(lib, cfg, seed, local_rank):
     byts = (22 * m + 9 * acc + 13 * rx) / n
     gbs = byts / (us * 1e3)
     return round(us, 2), {"bound": "hbm", "scope": "whole gossip round (send + merge kernels), SURVEY 8(d) bytes",
-                          "bytes_per_round": int(byts), "merges_per_round": m // n, "achieved": round(gbs, 1),
+                          "rounds": [start, start + n - 1],
+                          "bytes_per_round": int(byts), "merges_per_round": m // n,
+                          "accepts_per_round": acc // n, "accept_fraction": round(acc / m, 4) if m else None,
+                          "achieved": round(gbs, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+def dissemination(lib, cfg, seed, local_rank, start=100, rounds=300):
+    """Rounds for a catalog change to reach every view (README.md:13-15 "a few seconds"), measured
+    on the device from per-record min/max words (gx_view_minmax) after every round of
+    [start, start + rounds): a record's version is born in the round its newest word (the max over
+    all views) changes, and has spread once every view holds it (min == max). Latency = rounds from
+    the birth round to the round after which all views agree. A version replaced by a newer one
+    before it spread is counted as superseded; one still spreading at the end, as unfinished."""
+    import torch
+    e = make_engine(lib, cfg, seed, local_rank)
+    try:
+        e.run_rounds(start)
+        R = e.H * e.S
+        dev = torch.device(f"cuda:{local_rank}")
+        mn = torch.empty(R, dtype=torch.int64, device=dev)
+        mx = torch.empty(R, dtype=torch.int64, device=dev)
+        e.view_minmax(mn.data_ptr(), mx.data_ptr())
+        prev = mx.clone()
+        born = torch.full((R,), -1, dtype=torch.int64, device=dev)
+        lats, superseded = [], 0
+        for _ in range(rounds):
+            r = e.round
+            e.run_rounds(1)
+            e.view_minmax(mn.data_ptr(), mx.data_ptr())
+            new = mx != prev
+            superseded += int((new & (born >= 0)).sum().item())
+            born = torch.where(new, torch.full_like(born, r), born)
+            done = (mn == mx) & (born >= 0)
+            lats.append((r - born[done]).cpu())
+            born = torch.where(done, torch.full_like(born, -1), born)
+            prev.copy_(mx)
+        lat = torch.cat(lats).double() if lats else torch.empty(0, dtype=torch.float64)
+        out = {"rounds_measured": [start, start + rounds - 1], "changes_spread": int(lat.numel()),
+               "superseded": superseded, "unfinished": int((born >= 0).sum().item()),
+               "round_s": 0.2, "definition": "rounds from a version's birth round to the round after which "
+                                              "every view holds it (per-record min == max over all views)"}
+        if lat.numel():
+            q = torch.quantile(lat, torch.tensor([0.5, 0.99], dtype=torch.float64))
+            out.update({"p50_rounds": float(q[0]), "p99_rounds": float(q[1]), "max_rounds": float(lat.max()),
+                        "mean_rounds": round(float(lat.mean()), 2)})
+        return out
+    finally:
+        e.close()
 
 
 def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
@@ -384,6 +464,10 @@ def main():
                   "record_merges_per_s": split["gossip_merges"] / (gms * 1e-3) if gms else None}
         if world == 1:  # without per-launch events: the span of a stretch of gossip-only rounds
             gossip["round_span_us"], gossip["roofline"] = gossip_round_span(lib, args.config, seed, local_rank)
+            acc0 = gossip_stretch_start(args.config, accepting=True)
+            if acc0 is not None:  # the post-heal stretch, where gossip records are live
+                gossip["round_span_us_accepting"], gossip["roofline_accepting"] = gossip_round_span(
+                    lib, args.config, seed, local_rank, start=acc0)
 
     conv = None
     if not args.no_converge:
@@ -399,6 +483,9 @@ def main():
         conv_ref = {"config": workload_text(ref), "rounds_to_converge": r,
                     "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
                     "simulated_s": (r * 0.2) if r else None}
+    dis = None
+    if world == 1 and CONFIGS[args.config]["p"].get("churn_ppm") and not args.no_converge:
+        dis = dissemination(lib, args.config, seed, local_rank)  # churn never converges: spread latency
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.warmup, args.steps, h_mt=args.cpu_hosts)
@@ -418,7 +505,9 @@ def main():
                                        + ("RCCL all-to-all)" if backend == "nccl" else "gloo, host-staged all-to-all)")
                                        if world > 1 else "single GPU")},
             "merges": split, "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
-            "roofline": roof, "roofline_merge": roofline("merge"), "cpu_baseline": cpu, "kernels": kern,
+            "dissemination": dis,
+            "roofline": roof, "roofline_merge": roofline("merge"), "roofline_send": roofline("send"),
+            "cpu_baseline": cpu, "kernels": kern,
             "kernels_scope": "whole engine" if world == 1 else "rank 0's shard (device time and bytes of its launches)",
             "exchange": xfer,
         }

@@ -124,6 +124,7 @@ struct Dev {
   uint32_t nblk_ae;    // digest blocks per row, ceil(R / GX_DIGEST_SLOTS)
   uint32_t *snap;      // this round's k_send stores work_cnt[GX_WC_SCANS] here (pinned host memory), or null
   uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
+  unsigned long long *kprof;  // diagnostics (env GX_KPROF): wall-clock phase marks of k_send per wave, or null
   uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels): bit 2
                        // expiry scans in k_scan, bit 3 owner ticks in k_owner (not inside k_send),
                        // bit 4 default-policy storm stream, bit 5 default-policy k_ae, bit 7 the
@@ -256,9 +257,15 @@ GXD void wave_sync() {
 // on the receiver's count; returns the inbox position (slot). The header itself (with the record
 // count) is written by inbox_header once the packet is packed.
 GXD uint32_t inbox_claim(const Dev &d, uint32_t vi) { return atomicAdd(&d.in_cnt[vi], 1u); }
-GXD void inbox_header(const Dev &d, uint32_t vi, uint32_t pos, uint32_t key, uint32_t entry, uint32_t len) {
-  if (pos < d.DI) d.in_hdr[(size_t)vi * d.DI + pos] = make_uint4(key, entry, len, pos);
+// slot: where the records are (packet_recs): the inbox position (inline for the first DR), or
+// 0xffffffff for the message entry
+GXD void inbox_header(const Dev &d, uint32_t vi, uint32_t pos, uint32_t key, uint32_t entry, uint32_t len,
+                      uint32_t slot) {
+  if (pos < d.DI) d.in_hdr[(size_t)vi * d.DI + pos] = make_uint4(key, entry, len, slot);
   else d.in_ovf[atomicAdd(d.ovf_cnt, 1u)] = make_uint4(key, entry, len, vi);
+}
+GXD void inbox_header(const Dev &d, uint32_t vi, uint32_t pos, uint32_t key, uint32_t entry, uint32_t len) {
+  inbox_header(d, vi, pos, key, entry, len, pos);
 }
 GXD void inbox_put(const Dev &d, uint32_t vi, uint32_t key, uint32_t entry, uint32_t len) {
   inbox_header(d, vi, inbox_claim(d, vi), key, entry, len);
@@ -738,8 +745,9 @@ GXD uint64_t tombstone_services(const Dev &d, Acc &a, uint32_t o, uint64_t runni
   uint64_t *row = &vrow(d, o)[(size_t)o * d.S];
   uint64_t m = 0;
   for (uint32_t s = 0; s < d.S; s++) {
+    if ((running >> s) & 1ull) continue;  // running: no slot read (each read waits on the last store)
     uint64_t w = row[s];
-    if (st_of(w) == GX_ABSENT || ((running >> s) & 1ull) || st_of(w) == GX_TOMBSTONE) continue;
+    if (st_of(w) == GX_ABSENT || st_of(w) == GX_TOMBSTONE) continue;
     set_slot(d, a, o, &row[s], pack(d.now, GX_TOMBSTONE));  // svc.Tombstone() (service.go:91-94)
     svc_changed(d, a, o, o * d.S + s, row[s], st_of(w));     // (:703-705)
     m |= 1ull << s;

@@ -138,6 +138,7 @@ struct gx_engine {
   size_t api_dev_bytes;
   unsigned long long *conv_bad;
   uint64_t *digest_buf;
+  size_t kprof_n;  // diagnostics: u64 marks in d.kprof (env GX_KPROF)
 };
 
 static void codec_free(gx_engine *e);  // gx_codec_host.hpp
@@ -352,6 +353,25 @@ static int round_send_impl(gx_engine *e) {
   // a round without the detector or the storm: owner ticks, expiry scans and sends in one launch
   // (S <= 16: owner teams of the send's 4 lanes with up to 4 services each)
   const bool fused = !bt_apart && d.K && d.S <= 16 && !(d.ab & 8u) && !e->scan_heavy;
+  // planned GetBroadcasts (send_planned): record budget, no detector or departures, re-armed
+  // passes sleep, senders' filter; teams of 4 lanes per host (A/B bit 256: the per-call path)
+  const bool plan = !d.p.limit_bytes && d.p.retransmit_rounds > 0 && d.sfilt && !d.departures && !d.p.fd_enable &&
+                    !(d.ab & 256u);
+  if (fused && plan) {
+    LaunchTimer t(e, GX_K_SEND);
+    const unsigned g = nblk(d.Hl, 64);
+    const bool ev = !e->log_views.empty();
+#define GX_TSP(SPL)                                                                                               \
+  (vec ? (ev ? k_send<4, false, true, true, true, SPL, true> : k_send<4, false, true, true, false, SPL, true>)    \
+       : (ev ? k_send<4, false, true, false, true, SPL, true> : k_send<4, false, true, false, false, SPL, true>)) \
+      <<<g, 256, 0, s>>>(d, 1)
+    if (d.S <= 4) GX_TSP(1);
+    else if (d.S <= 8) GX_TSP(2);
+    else GX_TSP(4);
+#undef GX_TSP
+    HIPCHK(hipGetLastError());
+    return scan_probe_end(e);
+  }
   if (fused) {
     LaunchTimer t(e, GX_K_SEND);
     const unsigned g = nblk(d.Hl, 64);
@@ -407,7 +427,14 @@ static int round_send_impl(gx_engine *e) {
     const bool ev = !e->log_views.empty();
     const unsigned g = nblk(d.Hl, 64);
     // teams of 2 / 8 lanes measured 25.6 / 28.7 vs 21.1 us (profiles/r02/gossip/send_team_ab.log)
-    if (scan_in_send) {
+    if (plan) {
+      if (scan_in_send)
+        (vec ? (ev ? k_send<4, false, true, true, true, 0, true> : k_send<4, false, true, true, false, 0, true>)
+             : (ev ? k_send<4, false, true, false, true, 0, true> : k_send<4, false, true, false, false, 0, true>))
+            <<<g, 256, 0, s>>>(d, 1);
+      else
+        k_send<4, false, false, false, false, 0, true><<<g, 256, 0, s>>>(d, bt_apart ? 0 : 1);
+    } else if (scan_in_send) {
       if (d.departures)
         (vec ? (ev ? k_send<4, true, true, true, true> : k_send<4, true, true, true, false>)
              : (ev ? k_send<4, true, true, false, true> : k_send<4, true, true, false, false>))<<<g, 256, 0, s>>>(d, 1);
@@ -701,7 +728,7 @@ int gx_destroy(gx_engine *e) {
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, d.in_stamp, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
-                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf,
+                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
                   d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -842,9 +869,10 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
   d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
   if (d.ab) fprintf(stderr, "gx: GX_AB_FLAGS=%u: A/B measurement kernel paths active\n", d.ab);
-  // one shard: every packet's receiver is local, so its sender reads the receiver's view slots
-  // (A/B bit 128: the receivers' own filter pass, k_merge_lean)
-  d.sfilt = (d.G == 1 && !(d.ab & 128u)) ? 1u : 0u;
+  // senders read their local receivers' view slots and drop no-op records; packets from other
+  // shards are filtered the same way on arrival (k_inbox_unpack). A/B bit 128: the receivers' own
+  // filter pass (k_merge_lean) instead.
+  d.sfilt = !(d.ab & 128u) ? 1u : 0u;
   ALLOC(d.in_hdr, sizeof(uint4) * H * d.DI);
   ALLOC(d.in_ovf, sizeof(uint4) * Hg * K);
   ALLOC(d.in_rec, sizeof(grec) * H * d.DR * p->packet_cap);
@@ -878,6 +906,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
     if (p->fd_push_pull_state) ALLOC(d.fd_snap, sizeof(uint64_t) * H * Hg);
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
+  e->kprof_n = 0;
+  if (getenv("GX_KPROF")) {  // diagnostics: phase marks of every k_send wave (gx_kprof_read)
+    e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8;
+    ALLOC(d.kprof, sizeof(unsigned long long) * e->kprof_n);
+    HIPCHK(hipMemset(d.kprof, 0, sizeof(unsigned long long) * e->kprof_n));
+  }
   ALLOC(e->digest_buf, sizeof(uint64_t) * H);
   if (d.G > 1) {
     ALLOC(e->ob_entries, sizeof(uint32_t) * H * K);
@@ -2374,6 +2408,18 @@ int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   if (rc) return rc;
   if (converged) *converged = bad == 0;
   if (n_disagree) *n_disagree = bad;
+  return GX_OK;
+}
+
+// Diagnostics outside gx.h (env GX_KPROF at gx_create): the wall-clock phase marks (100 MHz) of the
+// last k_send launch, 8 per wave: start, ticks done, block barrier, sends begin, send_host begin,
+// first chunk planned, first chunk's records stored, sends done (0 = not reached).
+int gx_kprof_read(gx_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) {
+  if (!e || !n_out) return GX_EINVAL;
+  *n_out = e->kprof_n;
+  if (!e->kprof_n || !out) return GX_OK;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(out, e->d.kprof, sizeof(uint64_t) * (cap < e->kprof_n ? cap : e->kprof_n), hipMemcpyDeviceToHost));
   return GX_OK;
 }
 

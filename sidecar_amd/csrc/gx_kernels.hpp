@@ -948,6 +948,339 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
   return cnt;
 }
 
+// Diagnostics: wall-clock mark k of this wave (k_send phases; Dev::kprof, env GX_KPROF).
+#define GX_KP(k)                                                                                   \
+  do {                                                                                             \
+    if (d.kprof && (threadIdx.x & 63) == 0)                                                        \
+      d.kprof[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = wall_clock64(); \
+  } while (0)
+
+// ---------------------------------------------------------------- planned GetBroadcasts --
+// The same GetBroadcasts calls (record budget, no byte limit, no failure detector or departures,
+// TOMBSTONE_RETRANSMIT > 0 so re-armed passes sleep and nothing is pushed to the FIFO during the
+// sends) in two steps per chunk of up to PLAN_CH calls:
+//  1. the control plan: each call's dequeued job (from the FIFO head jobs loaded up front), batch
+//     length m, packet length l, and the pending ring's head before and after, with every FIFO,
+//     sleep-ring and counter update of the call. This touches no record, so the calls of a chunk
+//     plan back to back with no memory round trip.
+//  2. the records of all the chunk's packets at once: record f of the chunk belongs to call k
+//     (prefix sums of l) at index i; i < m is batch item i of k's job (list arena, job fields),
+//     else pending ring position head_k + i - m, whose content is the batch of an earlier call of
+//     the chunk that left records pending there (the latest such call), or the ring as loaded.
+//     Every record load of the chunk is in flight together, then every receiver slot read of the
+//     senders' filter, then the stores: a record that is stale or no newer than the receiver's
+//     slot is a no-op at any position of the receiver's fold (see k_merge), so only live records
+//     are written, compacted per packet, and a packet without one is not registered at all.
+// Batch records that stay pending are written to the ring after the chunk's loads, position p by
+// team lane p % T in call order (the sequential order of the ring writes).
+#define PLAN_CH 4  // calls planned per chunk
+#define PLAN_RECS 64  // records of a chunk in flight per team (64 / T per lane)
+struct PlanCall {
+  // batch item i (i < m) as the record phase builds it: EXPIRE {bw, rb + (emask ? nth set bit : i)},
+  // SEND {list[i].w + bw, list[i].r}, RETX {bw, rb}
+  uint64_t bw;        // EXPIRE: the tombstone word; SEND: the pass increment; RETX: the record word
+  uint64_t emask;     // EXPIRE: the service mask unless it is every service (0)
+  const grec *list;   // SEND: the list records
+  const uint64_t *row;  // the receiver's view row when it is on this shard (the filter), else null
+  uint32_t kind, rb;  // job kind (0xff: none); EXPIRE: owner * S; RETX: the record key
+  uint32_t m, l;      // batch length, packet length (> 0)
+  uint32_t head, nh;  // pending ring head before and after the call
+  uint32_t push;      // batch records left pending (written at nh .. nh + push - 1)
+  uint32_t x, key;    // packet entry, global packet key
+  uint32_t peer;      // receiver (global id)
+  uint32_t lpre;      // records of the chunk's earlier calls
+};
+static_assert(sizeof(PlanCall) >= 16 * sizeof(uint32_t), "a PlanCall slot holds a team's 16 peers");
+#define GX_NOSLOT 0xffffffffu  // inbox header slot: the records are in the message entry
+
+// Batch item i of a planned call's job (get_broadcasts_team's item() for i < m).
+GXD grec plan_item(const Dev &d, const PlanCall &c, uint32_t i) {
+  grec g;
+  g.pad = 0;
+  if (c.kind == GX_JOB_SEND) {  // Updated + pass * 50ns (services_state.go:588-599)
+    const grec s = c.list[i];
+    g.w = s.w + c.bw;
+    g.r = s.r;
+  } else if (c.kind == GX_JOB_EXPIRE) {  // the i-th tombstoned service of the owner
+    g.w = c.bw;
+    g.r = c.rb + (c.emask ? nth_set_bit(c.emask, i) : i);
+  } else {  // RETX
+    g.w = c.bw;
+    g.r = c.rb;
+  }
+  return g;
+}
+
+// Every lane of host idx's team calls it (team-uniform hs, peers, np); lead lane stores.
+// kb: algorithmic bytes (the caller flushes them to GX_K_SEND).
+template <int T>
+GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_job *pjs, PlanCall *pl,
+                      const uint32_t *peers, uint32_t np, unsigned long long &kb) {
+  constexpr int PLAN_Q = PLAN_RECS / T;
+  const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
+  const bool lead = tl == 0;
+  const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
+  const uint32_t u = d.lo + idx, cap = d.p.packet_cap, mask = d.DQ - 1;
+  grec *dq = &d.dq[(size_t)idx * d.DQ];
+  const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+  const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
+  // FIFO head jobs, T at a time: position pf0 + q in pjs[q], q < npf
+  uint32_t pf0 = hs.fifo_head, npf = 0;
+  uint32_t j = 0, n = 0;
+  bool stop = np == 0;
+  unsigned fm = 0, fs = 0;
+  while (!stop) {
+    // ---- 1. plan up to PLAN_CH calls (control state only)
+    uint32_t nc = 0, tot = 0;
+    bool any_push = false;
+    while (nc < PLAN_CH && !stop) {
+      PlanCall c;
+      c.kind = 0xffu;
+      c.bw = c.emask = 0;
+      c.rb = 0;
+      c.list = nullptr;
+      c.m = 0;
+      c.push = 0;
+      c.peer = peers[j];
+      c.row = c.peer - d.lo < d.Hl ? &d.view[(size_t)(c.peer - d.lo) * d.R] : nullptr;
+      c.x = idx * d.KE + j * d.NG + n;
+      c.key = u * d.KE + j * d.NG + n;
+      bool empty = false;
+      if (hs.fifo_head != hs.fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
+        uint32_t q = hs.fifo_head - pf0;
+        if (q >= npf) {  // load the next T head jobs
+          const uint32_t left = hs.fifo_tail - hs.fifo_head;
+          wave_sync();
+          if (tl < left) pjs[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
+          wave_sync();
+          pf0 = hs.fifo_head;
+          npf = left < (uint32_t)T ? left : (uint32_t)T;
+          q = 0;
+          if (lead) kb += 32ull * npf;
+        }
+        const gx_job jb = pjs[q];
+        hs.fifo_head++;
+        if (lead) a.c[C_DEQ]++;
+        const uint32_t kind = jb.meta & 0xff, pass = (jb.meta >> 8) & 0xff, npass = (jb.meta >> 16) & 0xff;
+        if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
+          if (lead) a.c[C_NIL]++;
+          hs.flags &= ~1u;
+          hs.bs_next = d.round + d.p.alive_interval_rounds;
+        } else if (kind == GX_JOB_NIL_BT) {  // ... BroadcastTombstones (:628)
+          if (lead) a.c[C_NIL]++;
+          hs.flags &= ~2u;
+          hs.bt_next = d.round + d.p.tombstone_interval_rounds;
+        } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
+          if (pass + 1 < npass) {  // the looper re-arms after TOMBSTONE_RETRANSMIT (:585-601)
+            gx_job nj = jb;
+            nj.meta = meta_of((int)kind, pass + 1, npass);
+            nj.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
+            push_sleep_r(d, a, u, hs, nj, lead);
+          } else {
+            free_list_r(hs, jb);  // read below; nothing reallocates it during the sends
+          }
+        }
+        c.m = job_len(d, jb);
+        c.kind = kind;
+        const uint64_t dw = ((uint64_t)pass * (uint64_t)d.p.pass_increment_ns) << GX_TS_SHIFT;
+        if (kind == GX_JOB_RETX) {
+          c.bw = jb.a;
+          c.rb = jb.c;
+        } else if (kind == GX_JOB_SEND) {
+          c.bw = dw;
+          c.list = list_ptr(d, u, jb.c & 0xffff);
+        } else if (kind == GX_JOB_EXPIRE) {
+          c.bw = pack((int64_t)jb.a, GX_TOMBSTONE) + dw;
+          c.rb = jb.c * d.S;
+          c.emask = (uint32_t)__popcll(jb.b) == d.S ? 0ull : jb.b;
+        }
+      } else if (hs.dq_len == 0) {  // default: nothing pending (:96-98)
+        empty = true;
+      }
+      uint32_t l = 0;
+      if (!empty) {  // packPacket's greedy prefix (:186-223) of batch ++ pendingBroadcasts
+        const uint32_t nn = c.m + hs.dq_len;
+        l = nn < cap ? nn : cap;
+        c.head = hs.dq_head;
+        if (l < c.m) {  // leftover = broadcast[l:]: batch records stay pending in front
+          c.push = c.m - l;
+          c.nh = (c.head - c.push) & mask;
+          any_push = true;
+        } else {
+          c.nh = (c.head + (l - c.m)) & mask;
+        }
+        hs.dq_head = c.nh;
+        hs.dq_len = nn - l;
+        if (hs.dq_len > d.p.pending_cap) {  // pendingBroadcasts = leftover[:MAX_PENDING_LENGTH]
+          if (lead) a.c[C_PDROP] += hs.dq_len - d.p.pending_cap;
+          hs.dq_len = d.p.pending_cap;
+        }
+        if (l && lead) {
+          a.c[C_PACKETS]++;
+          a.c[C_RECSENT] += l;
+          // records read from a list or the ring, and the receiver slots the filter reads
+          const uint32_t lb = l < c.m ? l : c.m;
+          kb += 16ull * ((c.kind == GX_JOB_SEND ? lb : 0u) + (l - lb)) + (c.row ? 8ull * l : 0ull);
+          if (c.row) fm += l;
+        }
+      }
+      c.l = l;
+      c.lpre = tot;
+      if (l) {
+        if (lead) pl[nc] = c;
+        nc++;
+        tot += l;
+      }
+      // GossipMessages: up to NG gathers per target; a target's gathering ends at an empty result,
+      // an empty first gather ends the round (gossip_stop_on_empty)
+      if (l == 0) {
+        if (n == 0 && d.p.gossip_stop_on_empty) stop = true;
+        j++;
+        n = 0;
+      } else if (++n == d.NG) {
+        j++;
+        n = 0;
+      }
+      if (j >= np) stop = true;
+    }
+    if (nc == 0) break;
+    wave_sync();  // the plan in LDS
+    if (j <= PLAN_CH) GX_KP(5);
+    // ---- 2. the chunk's records: loads, receiver slots, compacted stores. Record f of the chunk
+    // belongs to call k (lpre), its live rank in the packet is run(f) - run(lpre_k), where run(x)
+    // counts the live records before x (ballot prefix over the team, call starts in cb[]).
+    uint32_t lp[PLAN_CH], cb[PLAN_CH];
+#pragma unroll
+    for (int k = 0; k < PLAN_CH; k++) {
+      lp[k] = (uint32_t)k < nc ? pl[k].lpre : 0xffffffffu;
+      cb[k] = 0;
+    }
+    uint32_t run = 0;
+    for (uint32_t fb = 0; fb < tot; fb += T * PLAN_Q) {
+      grec g[PLAN_Q];
+      uint32_t ck[PLAN_Q];
+      bool ld[PLAN_Q];
+#pragma unroll
+      for (int q = 0; q < PLAN_Q; q++) {  // the records: computed from the job, or one load each
+        const uint32_t f = fb + tl + T * q;
+        uint32_t k = 0;
+#pragma unroll
+        for (int kk = 1; kk < PLAN_CH; kk++) k += f >= lp[kk] ? 1u : 0u;
+        ck[q] = k;
+        g[q].w = 0;
+        g[q].r = 0;
+        g[q].pad = 0;
+        ld[q] = false;
+        if (f < tot) {
+          const PlanCall &c = pl[k];
+          const uint32_t i = f - c.lpre;
+          const grec *src = nullptr;
+          if (i < c.m) {
+            if (c.kind == GX_JOB_EXPIRE) {
+              g[q].w = c.bw;
+              g[q].r = c.rb + (c.emask ? nth_set_bit(c.emask, i) : i);
+            } else if (c.kind == GX_JOB_RETX) {
+              g[q].w = c.bw;
+              g[q].r = c.rb;
+            } else {
+              src = &c.list[i];
+            }
+          } else {  // pending ring position p: an earlier call of the chunk may have left a batch there
+            const uint32_t p = (c.head + (i - c.m)) & mask;
+            src = &dq[p];
+            if (any_push) {
+#pragma unroll
+              for (int kk = PLAN_CH - 2; kk >= 0; kk--) {
+                if (src == &dq[p] && (uint32_t)kk < k && pl[kk].push) {
+                  const uint32_t o = (p - pl[kk].nh) & mask;
+                  if (o < pl[kk].push) {
+                    g[q] = plan_item(d, pl[kk], pl[kk].l + o);
+                    src = nullptr;
+                  }
+                }
+              }
+            }
+          }
+          if (src) {
+            g[q] = *src;
+            ld[q] = true;
+          }
+        }
+      }
+      uint64_t w0[PLAN_Q];
+#pragma unroll
+      for (int q = 0; q < PLAN_Q; q++) {  // the senders' filter: the local receiver's slot
+        const uint32_t f = fb + tl + T * q;
+        const PlanCall &c = pl[ck[q]];
+        if (ld[q] && c.kind == GX_JOB_SEND && f - c.lpre < c.m) g[q].w += c.bw;  // + pass * 50 ns
+        w0[q] = GX_SLOT_ABSENT;
+        if (f < tot && c.row) w0[q] = c.row[g[q].r];
+      }
+#pragma unroll
+      for (int q = 0; q < PLAN_Q; q++) {
+        const uint32_t f = fb + tl + T * q, base = fb + T * q;
+        const uint32_t k = ck[q];
+        const PlanCall &c = pl[k];
+        const bool valid = f < tot;
+        bool live = valid;
+        if (valid && c.row) {
+          const int64_t ts = ts_of(g[q].w);
+          const bool stale = ts < t_stale;
+          const bool gc = st_of(w0[q]) == GX_TOMBSTONE && ts_of(w0[q]) < t_gc;
+          live = !stale && (st_of(w0[q]) == GX_ABSENT || ts > ts_of(w0[q]) || gc);
+          fs += stale;
+        }
+        const uint64_t lm = (__ballot(live) >> (tw * T)) & tmask;
+#pragma unroll
+        for (int kk = 1; kk < PLAN_CH; kk++)  // run() at the calls starting in this block
+          if (lp[kk] >= base && lp[kk] < base + T) cb[kk] = run + (uint32_t)__popcll(lm & ((1ull << (lp[kk] - base)) - 1ull));
+        uint32_t cbk = 0;
+#pragma unroll
+        for (int kk = 1; kk < PLAN_CH; kk++) cbk = (uint32_t)kk == k ? cb[kk] : cbk;
+        const uint32_t rank = c.row ? run + (uint32_t)__popcll(lm & ((1ull << tl) - 1ull)) - cbk : f - c.lpre;
+        if (live) d.msg[(size_t)c.x * cap + rank] = g[q];
+        run += (uint32_t)__popcll(lm);
+      }
+    }
+    uint32_t stored_all = 0;  // records this team stores: the packets' headers below
+    // ---- packet headers: lane k registers call k's packet when it holds a record
+    if (j <= PLAN_CH) GX_KP(6);
+    if (tl < nc) {
+      const PlanCall &c = pl[tl];
+      uint32_t stored = 0;
+#pragma unroll
+      for (int kk = 0; kk < PLAN_CH; kk++) {
+        const uint32_t end = kk + 1 < PLAN_CH && (uint32_t)(kk + 1) < nc ? cb[kk + 1] : run;
+        stored = (uint32_t)kk == tl ? end - cb[kk] : stored;
+      }
+      const uint32_t rv = c.peer - d.lo;
+      if (!c.row) stored = c.l;  // another shard's receiver filters on arrival (k_inbox_unpack)
+      d.msg_len[c.x] = stored;
+      d.msg_dst[c.x] = c.peer;
+      if (c.row && stored) {
+        inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, GX_NOSLOT);
+        d.mflag[rv] = 1;
+      }
+      stored_all = stored + ((c.row && stored) ? 2u : 0u);  // a header and its count ~ 2 records
+    }
+    kb += 16ull * stored_all;
+    // ---- batch records left pending: position p by lane p % T, in call order
+    if (any_push) {
+      for (uint32_t k = 0; k < nc; k++) {
+        const PlanCall &c = pl[k];
+        for (uint32_t qq = (tl - c.nh) & (T - 1); qq < c.push; qq += T) {
+          dq[(c.nh + qq) & mask] = plan_item(d, c, c.l + qq);
+          kb += 16;
+        }
+      }
+      __threadfence_block();  // the next chunk may read them on other lanes
+    }
+    wave_sync();  // the plan slots are rewritten by the next chunk
+  }
+  a.c[C_GOSSIP_MERGES] += fm;
+  a.c[C_STALE] += fs;
+}
+
 // A team of T lanes per host: first the rest of a BroadcastTombstones tick (TombstoneServices +
 // SendServices of own ++ others, services_state.go:606-633; lane 0, after the expiry scan), then
 // GetBroadcasts once per sampled peer, in order (get_broadcasts_team). Each packet is registered
@@ -956,8 +1289,12 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 // memberlist messages first and, in byte mode, the delegate gets the bytes left; the round stops
 // at a packet that would be empty), and a packet to an unreachable peer is lost after
 // GetBroadcasts took its records.
-template <int T, bool X>
-GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, unsigned &lost) {
+GXD bool filt_used(const Dev &d, uint32_t pos) { return d.sfilt && pos != 0xffffffffu; }
+// PLAN: send_planned (the engine picks it when its conditions hold: record budget, !X, retransmit
+// sleep > 0, senders' filter).
+template <int T, bool X, bool PLAN = false>
+GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, unsigned &lost, PlanCall *pl,
+                   unsigned long long &kb) {
   const uint32_t lane = threadIdx.x & (T - 1);
   {
     uint32_t u = d.lo + idx;
@@ -977,7 +1314,21 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       __threadfence_block();  // the team reads the host's bookkeeping below
       hs = *h;
     }
-    if (!X || !departed(d, u)) {
+    if (lane == 0) kb += 128;  // the host's bookkeeping read and written
+    GX_KP(4);
+    if (PLAN) {
+      uint32_t *peers = reinterpret_cast<uint32_t *>(&pl[PLAN_CH]);  // the team's 16 peer slots (LDS)
+      uint32_t np = 0;
+      if (lane == 0) {
+        uint32_t pr[16];
+        np = sample_peers(d, u, pr);
+        for (uint32_t k = 0; k < np; k++) peers[k] = pr[k];
+      }
+      np = __shfl(np, (int)(threadIdx.x & 63 & ~(uint32_t)(T - 1)), 64);
+      wave_sync();
+      send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb);
+      if (lane == 0) *h = hs;
+    } else if (!X || !departed(d, u)) {
       const bool fd = X && d.p.fd_enable;
       uint32_t peers[16];
       uint32_t np;
@@ -1034,6 +1385,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
                                        filt ? &d.mflag[pj - d.lo] : nullptr);
           }
           called = j + 1;
+          if (lane == 0) kb += 32 + 32ull * l + (filt_used(d, pos) ? 8ull * l : 0);  // job, records in/out, slots
           const bool live = l || nf;
           if (lane == 0) {
             d.msg_len[x] = ok ? l : 0;
@@ -1063,15 +1415,18 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
 // listeners): the block's hosts tick with the same 4-lane teams, OWN services per lane, then the
 // block scans its queued views and sends. Nothing of one host's tick or send reads another host's
 // state except the receivers' inbox counts, zeroed a round ahead (Dev::in_cnt_nx).
-template <int T, bool X, bool SCAN = false, bool VEC = false, bool EV = false, int OWN = 0>
+template <int T, bool X, bool SCAN = false, bool VEC = false, bool EV = false, int OWN = 0, bool PLAN = false>
 __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   __shared__ gx_job s_pj[256 / T][T];  // FIFO head jobs of the block's hosts, loaded ahead
+  // send_planned's chunk plans, then the team's peers (16 u32 = one PlanCall's 64 B)
+  __shared__ PlanCall s_pl[PLAN ? 256 / T : 1][PLAN_CH + 1];
   __shared__ ScanLds sm;
   __shared__ uint32_t s_scan[256 / T], s_nscan;
   __shared__ gx_job s_sl[OWN ? 256 : 1];  // sleep-ring heads of the owner ticks
   Acc a;
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
+  GX_KP(0);
   if (d.snap && blockIdx.x == 0 && threadIdx.x == 0) *d.snap = d.work_cnt[GX_WC_SCANS];  // scan_probe_begin
   if constexpr (OWN > 0) {
     if (threadIdx.x == 0) {
@@ -1084,7 +1439,9 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
     __syncthreads();
     const bool q = owner_tick<T, OWN>(d, a, idx, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
     if (q) s_scan[atomicAdd(&s_nscan, 1u)] = idx;  // lead lanes only
+    GX_KP(1);
     __syncthreads();  // the block's ticks before its scans and sends read them
+    GX_KP(2);
     for (uint32_t k = 0; k < s_nscan; k++) {
       const uint32_t oi = s_scan[k];
       scan_view<VEC, EV>(d, oi, &d.scan_list[(size_t)oi * d.L], d.L, &d.scan_cnt[oi], sm);
@@ -1101,9 +1458,17 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       __syncthreads();  // the list and count before the tick's finish reads them
     }
   }
-  if (idx < d.Hl) send_host<T, X>(d, a, idx, s_pj[threadIdx.x / T], do_bt, lost);
+  unsigned long long kb = 0;
+  GX_KP(3);
+  if (idx < d.Hl)
+    send_host<T, X, PLAN>(d, a, idx, s_pj[threadIdx.x / T], do_bt, lost, s_pl[PLAN ? threadIdx.x / T : 0], kb);
+  GX_KP(7);
   acc_flush(d, a);
   if (X && lost) ctr_atomic(d, C_LOST, lost);
+  // algorithmic bytes: bookkeeping, FIFO jobs, records read (lists, ring), receiver slots read,
+  // records and headers written (send_planned; the record-budget path counts the same per record)
+  kb = wave_sum(kb);
+  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SEND, kb, 0);
 }
 
 
@@ -2725,6 +3090,58 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
     return;
   }
   const uint32_t vi = dst - d.lo;
+  if (d.sfilt) {  // the receiver's filter: only live records are kept (compacted, see send_planned)
+    const uint64_t *row = &d.view[(size_t)vi * d.R];
+    const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+    const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
+    grec *pk = &d.msg[e * d.p.packet_cap];
+    uint32_t nlive = 0, nstale = 0;
+    for (uint32_t x0 = 0; x0 < len; x0 += 64) {
+      const uint32_t x = x0 + threadIdx.x;
+      grec g;
+      g.w = 0;
+      g.r = 0;
+      g.pad = 0;
+      bool live = false;
+      if (x < len) {
+        g = recs[x];
+        const uint64_t w0 = row[g.r];
+        const int64_t ts = ts_of(g.w);
+        const bool stale = ts < t_stale;
+        const bool gc = st_of(w0) == GX_TOMBSTONE && ts_of(w0) < t_gc;
+        live = !stale && (st_of(w0) == GX_ABSENT || ts > ts_of(w0) || gc);
+        nstale += stale;
+      }
+      const unsigned long long m = __ballot(live);
+      if (live) pk[nlive + (uint32_t)__popcll(m & ((1ull << threadIdx.x) - 1ull))] = g;
+      nlive += (uint32_t)__popcll(m);
+    }
+    nstale = (uint32_t)wave_sum(nstale);
+    const uint4 *fm = reinterpret_cast<const uint4 *>(src + 16 + 16ull * d.p.packet_cap);
+    for (uint32_t x = threadIdx.x; x < nfd; x += blockDim.x) {
+      const uint4 w = fm[x];
+      gx_fd_msg g;
+      g.incarnation = w.x;
+      g.node = (uint16_t)(w.y & 0xffffu);
+      g.from = (uint16_t)(w.y >> 16);
+      g.kind = (uint8_t)w.z;
+      g.pad[0] = g.pad[1] = g.pad[2] = 0;
+      d.fdm[e * fcap + x] = g;
+    }
+    if (threadIdx.x == 0) {
+      d.msg_key[e] = key;
+      d.msg_dst[e] = dst;
+      d.msg_len[e] = nlive;
+      if (fcap) d.fd_len[e] = nfd;
+      if (nlive || nfd) inbox_header(d, vi, inbox_claim(d, vi), key, (uint32_t)e, nlive, GX_NOSLOT);
+      if (nlive) d.mflag[vi] = 1;
+      ctr_atomic(d, C_GOSSIP_MERGES, len);
+      ctr_atomic(d, C_STALE, nstale);
+      // 16 B per slot read, 8 B per receiver slot, 16 B per live record written, header + count
+      kbytes(d, GX_K_MERGE, 16ull + 24ull * len + 16ull * nlive + ((nlive || nfd) ? 20ull : 0ull), 0);
+    }
+    return;
+  }
   uint32_t pos = 0;
   if (threadIdx.x == 0 && (len || nfd)) pos = inbox_claim(d, vi);
   pos = __shfl(pos, 0, 64);

@@ -208,3 +208,28 @@ def test_cfg3_bench_schedule_51_rounds(gx_lib):
     assert st["expired"] > 0 and st["ae_exchanges"] == 6 * 8192 and st["churn_events"] > 0
     _slabs_equal(g, o, 4096)
     _rows_equal(g, o, np.linspace(0, 16383, 16).astype(int), "cfg3 round 51")
+
+
+def test_cfg5_gossip_messages15_h16384_parity(gx_lib):
+    """Sidecar's own GossipMessages default (15, config/config.go:46, main.go:257-259) on the cfg 5
+    schedule at H = 16384 against the OpenMP oracle for 61 rounds (storm, heal, the first
+    post-heal push-pull): up to 45 packets per host and round, receivers with many packets."""
+    orc = _omp_oracle()
+    kw = dict(CFG5_H16K, gossip_messages=15)
+    g = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    o = Engine(default_params(orc, **kw), lib=orc)
+    sample = np.linspace(0, 16383, 16).astype(int)
+    for stop in (6, 31, 52, 61):
+        n = stop - g.round
+        g.run_rounds(n)
+        o.run_rounds(n)
+        what = f"cfg5 GM15 @16384 round {g.round}"
+        print(what, flush=True)  # progress (long test)
+        assert g.stats() == o.stats(), what
+        assert np.array_equal(g.digests(), o.digests()), what
+        mg, xg = _minmax_any(g)
+        mo, xo = _minmax_any(o)
+        assert np.array_equal(mg, mo) and np.array_equal(xg, xo), what
+        _rows_equal(g, o, sample, what)
+    st = g.stats()
+    assert st["packets"] > 3 * 16384 * 10

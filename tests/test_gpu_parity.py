@@ -53,6 +53,15 @@ SCENARIOS = {
     "gossip_messages4_storm": dict(n_hosts=96, n_services=4, init_mode=INIT_WARM, gossip_messages=4,
                                    partition_start=0, partition_end=15, storm_round=3, queue_cap=1024,
                                    inbox_slots=6),
+    # planned GetBroadcasts (send_planned): batches longer than the packet (lists of expired and own
+    # tombstones, EXPIRE jobs of 16 records) leave records pending in front of the ring, several
+    # calls of a chunk read what earlier calls left there, pending truncation, ring wrap-around
+    "plan_pushes": dict(n_hosts=72, n_services=16, init_mode=INIT_WARM, packet_cap=5, pending_cap=7,
+                        queue_cap=512, list_slots=4, churn_ppm=80000, aged_ppm=60000, ae_period_rounds=9,
+                        partition_start=0, partition_end=14, storm_round=3, fanout=4),
+    # many chunks per host: GossipMessages 16 with 3-record packets
+    "plan_gm16_cap3": dict(n_hosts=50, n_services=8, init_mode=INIT_OWN, gossip_messages=16, packet_cap=3,
+                           pending_cap=9, churn_ppm=60000, queue_cap=1024, ae_period_rounds=12),
     # memberlist's per-node push-pull initiation (every live host starts one exchange per interval)
     "pp_initiate": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, push_pull_mode=1, ae_period_rounds=5,
                         churn_ppm=30000),

@@ -10,7 +10,7 @@ from tests.test_shards_cpu import SCEN, assert_sharded_equal
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("G", [2, 3, 5])
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
 @pytest.mark.parametrize("name", sorted(SCEN))
 def test_gpu_local_shards_match_whole(gx_lib, oracle_lib, name, G):
     kw = SCEN[name]
@@ -101,3 +101,28 @@ def test_gpu_corrupt_inbox_slot_refused(gx_lib, field):
     assert run(gx_lib, dev, field) == "einval"
     # the flag is taken once: a fresh exchange on new engines goes through again
     assert run_valid(gx_lib, dev) >= 0
+
+
+CFG5_H2048 = dict(n_hosts=2048, n_services=16, fanout=3, packet_cap=32, pending_cap=100, queue_cap=20480,
+                  list_slots=16, init_mode=2, partition_start=0, partition_end=50, storm_round=5,
+                  ae_period_rounds=10)
+
+
+def test_gpu_eight_shards_cfg5_schedule(gx_lib, oracle_lib):
+    """The 8-way host split of BASELINE configs[4] (G = 8, as bench.py shards over 8 GPUs) on the
+    cfg 5 schedule at H = 2048: partition, ExpireServer storm at round 5, heal at 50, push-pull
+    through round 81; views, counters, queue digests and server times against the unsharded HIP
+    engine and the CPU oracle at every checkpoint, and packets and push-pull blocks cross shards."""
+    kw = CFG5_H2048
+    whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    orc = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    sh = LocalShards(gx_lib, 8, device="cuda:0", **kw)
+    for stop in (6, 25, 51, 52, 61, 82):
+        n = stop - whole.round
+        whole.run_rounds(n)
+        orc.run_rounds(n)
+        sh.run_rounds(n)
+        assert_sharded_equal(whole, sh, f"cfg5@2048 G=8 round {whole.round}")
+        assert_sharded_equal(orc, sh, f"cfg5@2048 G=8 round {whole.round} vs oracle")
+    w = sh.wire.as_dict()
+    assert w["packets"] > 0 and w["ae_lead"] > 0 and w["ae_delta"] < w["ae_full_rows_equivalent"]

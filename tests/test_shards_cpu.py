@@ -70,7 +70,7 @@ def assert_sharded_equal(whole: Engine, shards, what):
         assert all(e.fd_converged()[0] for e in shards.engines) == whole.fd_converged()[0], what
 
 
-@pytest.mark.parametrize("G", [2, 3, 5])
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
 @pytest.mark.parametrize("name", sorted(SCEN))
 def test_local_shards_match_whole(oracle_lib, name, G):
     kw = SCEN[name]
