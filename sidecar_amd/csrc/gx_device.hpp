@@ -25,11 +25,43 @@
 #define GXD __device__ __forceinline__
 #define GXHD __host__ __device__ __forceinline__
 
+// Global (address space 1) loads and stores through pointers the compiler only knows as generic
+// (taken from LDS or selected at run time): a flat access counts in lgkmcnt as well as vmcnt, so the
+// next wait for an LDS read would also wait for it; global ones leave the loads in flight.
+#define GX_GLOBAL __attribute__((address_space(1)))
+typedef unsigned int gx_u32x4 __attribute__((ext_vector_type(4)));
+template <class T>
+GXD T gld(const T *p) {  // scalars
+  return *(const GX_GLOBAL T *)p;
+}
+typedef unsigned int gx_u32x3 __attribute__((ext_vector_type(3)));
+GXD gx_u32x4 gld4(const void *p) { return *(const GX_GLOBAL gx_u32x4 *)p; }
+// a record's word and key only (dwordx3): no dead destination register for the allocator to reuse
+// while the load is in flight (that reuse makes it wait for the load on the spot)
+GXD gx_u32x3 gld3(const void *p) { return *(const GX_GLOBAL gx_u32x3 *)p; }
+GXD void gst4(void *p, gx_u32x4 v) { *(GX_GLOBAL gx_u32x4 *)p = v; }
+
 struct grec {
   uint64_t w;  // packed (ts << 3) | status
   uint32_t r;  // record key = owner * S + svc
   uint32_t pad;
 };
+GXD grec gld_rec(const grec *p) {  // one global dwordx4 load
+  const gx_u32x4 x = gld4(p);
+  grec g;
+  g.w = (uint64_t)x.x | ((uint64_t)x.y << 32);
+  g.r = x.z;
+  g.pad = x.w;
+  return g;
+}
+GXD void gst_rec(grec *p, const grec &g) {
+  gx_u32x4 x;
+  x.x = (uint32_t)g.w;
+  x.y = (uint32_t)(g.w >> 32);
+  x.z = g.r;
+  x.w = g.pad;
+  gst4(p, x);
+}
 
 enum {
   C_GOSSIP_MERGES, C_AE_MERGES, C_LOCAL_MERGES, C_GOSSIP_ACC, C_AE_ACC, C_LOCAL_ACC, C_STALE,

@@ -460,10 +460,16 @@ static int round_merge_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
     if (!d.sfilt) k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);  // else the senders filtered
-    const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE_DEF);
-    // 2 or 4 receivers per wave measured 14.2 / 13.7 vs 14.3 us (profiles/r02/gossip)
-    if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
-    else (ev ? k_merge<false, true> : k_merge<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+    if (!(d.ab & 512u)) {  // receivers merged MERGE_SEG lanes each (A/B bit 512: a wave each)
+      const unsigned g = nblk(d.Hl, MERGE_WAVES * (64 / MERGE_SEG));
+      if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      else (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+    } else {
+      const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE_DEF);
+      // 2 or 4 receivers per wave measured 14.2 / 13.7 vs 14.3 us (profiles/r02/gossip)
+      if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
+      else (ev ? k_merge<false, true> : k_merge<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+    }
   }
   if (d.p.fd_enable && d.K) {  // the packets' memberlist messages, after the catalog merge
     LaunchTimer t(e, GX_K_FD);

@@ -974,7 +974,7 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 // Batch records that stay pending are written to the ring after the chunk's loads, position p by
 // team lane p % T in call order (the sequential order of the ring writes).
 #define PLAN_CH 4  // calls planned per chunk
-#define PLAN_RECS 64  // records of a chunk in flight per team (64 / T per lane)
+#define PLAN_RECS 32  // records of a chunk in flight per team (32 / T per lane)
 struct PlanCall {
   // batch item i (i < m) as the record phase builds it: EXPIRE {bw, rb + (emask ? nth set bit : i)},
   // SEND {list[i].w + bw, list[i].r}, RETX {bw, rb}
@@ -1131,6 +1131,9 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         nc++;
         tot += l;
       }
+      // a call that leaves batch records pending ends the chunk: its ring writes follow the
+      // chunk's loads, so no call of a chunk reads what another call of it wrote
+      const bool pushed = c.push != 0;
       // GossipMessages: up to NG gathers per target; a target's gathering ends at an empty result,
       // an empty first gather ends the round (gossip_stop_on_empty)
       if (l == 0) {
@@ -1142,6 +1145,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         n = 0;
       }
       if (j >= np) stop = true;
+      if (pushed) break;
     }
     if (nc == 0) break;
     wave_sync();  // the plan in LDS
@@ -1157,64 +1161,46 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
     }
     uint32_t run = 0;
     for (uint32_t fb = 0; fb < tot; fb += T * PLAN_Q) {
-      grec g[PLAN_Q];
-      uint32_t ck[PLAN_Q];
-      bool ld[PLAN_Q];
+      // Every load of the block is issued unconditionally (a record that needs none loads ring
+      // slot 0, one past the end of the chunk loads it too) and used only after all are in flight:
+      // a load guarded by a branch makes the compiler wait for it on the spot.
+      uint64_t w[PLAN_Q];
+      uint32_t r[PLAN_Q], ck[PLAN_Q];
+      uint32_t sel[PLAN_Q];  // 0: computed from the job; 1: loaded list record (+ pass); 2: loaded ring record
+      gx_u32x3 lx[PLAN_Q];   // the loads, kept apart from the computed words until all are issued
 #pragma unroll
-      for (int q = 0; q < PLAN_Q; q++) {  // the records: computed from the job, or one load each
+      for (int q = 0; q < PLAN_Q; q++) {
         const uint32_t f = fb + tl + T * q;
         uint32_t k = 0;
 #pragma unroll
         for (int kk = 1; kk < PLAN_CH; kk++) k += f >= lp[kk] ? 1u : 0u;
         ck[q] = k;
-        g[q].w = 0;
-        g[q].r = 0;
-        g[q].pad = 0;
-        ld[q] = false;
-        if (f < tot) {
-          const PlanCall &c = pl[k];
-          const uint32_t i = f - c.lpre;
-          const grec *src = nullptr;
-          if (i < c.m) {
-            if (c.kind == GX_JOB_EXPIRE) {
-              g[q].w = c.bw;
-              g[q].r = c.rb + (c.emask ? nth_set_bit(c.emask, i) : i);
-            } else if (c.kind == GX_JOB_RETX) {
-              g[q].w = c.bw;
-              g[q].r = c.rb;
-            } else {
-              src = &c.list[i];
-            }
-          } else {  // pending ring position p: an earlier call of the chunk may have left a batch there
-            const uint32_t p = (c.head + (i - c.m)) & mask;
-            src = &dq[p];
-            if (any_push) {
-#pragma unroll
-              for (int kk = PLAN_CH - 2; kk >= 0; kk--) {
-                if (src == &dq[p] && (uint32_t)kk < k && pl[kk].push) {
-                  const uint32_t o = (p - pl[kk].nh) & mask;
-                  if (o < pl[kk].push) {
-                    g[q] = plan_item(d, pl[kk], pl[kk].l + o);
-                    src = nullptr;
-                  }
-                }
-              }
-            }
-          }
-          if (src) {
-            g[q] = *src;
-            ld[q] = true;
-          }
+        const PlanCall &c = pl[k];
+        const uint32_t i = f - c.lpre;
+        const bool valid = f < tot, batch = i < c.m;
+        const grec *src = dq;
+        sel[q] = 0;
+        if (valid && batch && c.kind == GX_JOB_SEND) {
+          src = &c.list[i];
+          sel[q] = 1;
+        } else if (valid && !batch) {
+          src = &dq[(c.head + (i - c.m)) & mask];
+          sel[q] = 2;
         }
+        lx[q] = gld3(src);
+        w[q] = c.bw;  // computed: the job's word
+        r[q] = c.rb + (c.kind == GX_JOB_EXPIRE ? (c.emask ? nth_set_bit(c.emask, i) : i) : 0u);
       }
       uint64_t w0[PLAN_Q];
 #pragma unroll
       for (int q = 0; q < PLAN_Q; q++) {  // the senders' filter: the local receiver's slot
-        const uint32_t f = fb + tl + T * q;
         const PlanCall &c = pl[ck[q]];
-        if (ld[q] && c.kind == GX_JOB_SEND && f - c.lpre < c.m) g[q].w += c.bw;  // + pass * 50 ns
-        w0[q] = GX_SLOT_ABSENT;
-        if (f < tot && c.row) w0[q] = c.row[g[q].r];
+        if (sel[q]) {  // loaded (+ pass * 50 ns for a list record, services_state.go:588-599)
+          w[q] = ((uint64_t)lx[q].x | ((uint64_t)lx[q].y << 32)) + (sel[q] == 1 ? w[q] : 0ull);
+          r[q] = lx[q].z;
+        }
+        const uint64_t *row = c.row ? c.row : d.view;
+        w0[q] = gld(&row[r[q] < d.R ? r[q] : 0u]);
       }
 #pragma unroll
       for (int q = 0; q < PLAN_Q; q++) {
@@ -1224,7 +1210,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         const bool valid = f < tot;
         bool live = valid;
         if (valid && c.row) {
-          const int64_t ts = ts_of(g[q].w);
+          const int64_t ts = ts_of(w[q]);
           const bool stale = ts < t_stale;
           const bool gc = st_of(w0[q]) == GX_TOMBSTONE && ts_of(w0[q]) < t_gc;
           live = !stale && (st_of(w0[q]) == GX_ABSENT || ts > ts_of(w0[q]) || gc);
@@ -1238,7 +1224,13 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
 #pragma unroll
         for (int kk = 1; kk < PLAN_CH; kk++) cbk = (uint32_t)kk == k ? cb[kk] : cbk;
         const uint32_t rank = c.row ? run + (uint32_t)__popcll(lm & ((1ull << tl) - 1ull)) - cbk : f - c.lpre;
-        if (live) d.msg[(size_t)c.x * cap + rank] = g[q];
+        if (live) {
+          grec g;
+          g.w = w[q];
+          g.r = r[q];
+          g.pad = 0;
+          gst_rec(&d.msg[(size_t)c.x * cap + rank], g);
+        }
         run += (uint32_t)__popcll(lm);
       }
     }
@@ -1746,6 +1738,230 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     }
   }
   wave_sync();
+}
+
+// The same merge for receivers whose live records fit one segment of SEG lanes (64 / SEG
+// receivers per wave): their inbox (deg <= SEG headers, within DI) holds at most SEG records, which
+// is one tile. Every step of merge_receiver runs within the segment: header ranking and the
+// packet scan by segment shuffles, one record per lane, the bitonic sort of (key, arrival lane)
+// over SEG lanes, the per-group fold in arrival order, the per-owner server times, the ordered
+// ballot compaction of retransmits and ChangeEvents on the segment's ballot bits. Returns false
+// (nothing done) for a receiver that does not fit: the caller merges it with the whole wave.
+template <int SEG>
+GXD uint32_t seg_sum(uint32_t x) {
+#pragma unroll
+  for (int o = SEG / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, SEG);
+  return x;
+}
+template <int SEG>
+GXD uint32_t seg_max(uint32_t x) {
+#pragma unroll
+  for (int o = SEG / 2; o > 0; o >>= 1) {
+    const uint32_t y = __shfl_xor(x, o, SEG);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+template <bool K32, bool EV, int SEG>
+GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L) {
+  const uint32_t lane = threadIdx.x & 63, sl = lane & (SEG - 1), sb = lane - sl;
+  const uint64_t smask = SEG == 64 ? ~0ull : ((1ull << SEG) - 1ull);
+  auto sballot = [&](bool p) -> uint64_t { return (__ballot(p) >> sb) & smask; };
+  const uint32_t v = d.lo + vi;
+  // hop 1: count, headers, FIFO counters and the event log slot together
+  uint4 hd = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t deg = 0, tail0 = 0, head0 = 0;
+  int32_t evk = -1;
+  if (act) {
+    if (sl < d.DI) hd = d.in_hdr[(size_t)vi * d.DI + sl];
+    deg = d.in_cnt[vi];
+    tail0 = d.hs[vi].fifo_tail;
+    head0 = d.hs[vi].fifo_head;
+    if (EV) evk = d.ev_slot[vi];
+  }
+  const uint32_t len = sl < deg ? hd.z : 0u;
+  const uint32_t total = seg_sum<SEG>(len);
+  const bool fits = !act || (deg <= d.DI && deg <= (uint32_t)SEG && total <= (uint32_t)SEG);
+  if (sballot(!fits)) return false;  // the segment's receiver takes the full path
+  if (!act || deg == 0) return true;
+  // sender order: rank of each header's key among the segment's deg keys (ties by lane)
+  const uint32_t hkey = sl < deg ? hd.x : 0xffffffffu;
+  uint32_t hrank = 0;
+  for (uint32_t j = 0; j < deg; j++) {
+    const uint32_t kj = (uint32_t)__shfl((int)hkey, (int)j, SEG);
+    hrank += kj < hkey || (kj == hkey && j < sl);
+  }
+  uint4 *s_hdr = &L.hdr[sb];
+  if (sl < deg) s_hdr[hrank] = hd;
+  wave_sync();
+  const uint4 sh = sl < deg ? s_hdr[sl] : make_uint4(0u, 0u, 0u, 0u);  // packet sl in sender order
+  uint32_t incl = sh.z;
+#pragma unroll
+  for (int o = 1; o < SEG; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, SEG);
+    if ((int)sl >= o) incl += y;
+  }
+  const uint32_t pstart = incl - sh.z;
+  // record sl: packet k with pstart_k <= sl < pstart_k + len_k
+  const bool valid = sl < total;
+  uint32_t kp = 0;
+  for (uint32_t j = 1; j < deg; j++) kp += sl >= (uint32_t)__shfl((int)pstart, (int)j, SEG) ? 1u : 0u;
+  const uint32_t ps = (uint32_t)__shfl((int)pstart, (int)kp, SEG);
+  const uint32_t pe = (uint32_t)__shfl((int)sh.y, (int)kp, SEG), pw = (uint32_t)__shfl((int)sh.w, (int)kp, SEG);
+  const uint32_t INV = K32 ? 0x3ffffffu : 0xffffffffu;  // sorts after every real key
+  uint32_t key = INV;
+  uint64_t val = 0, w0 = 0;
+  uint64_t *row = &d.view[(size_t)vi * d.R];
+  if (valid) {  // hop 2, hop 3
+    const grec g = gld_rec(&packet_recs(d, vi, pw, pe)[sl - ps]);
+    key = g.r;
+    val = g.w;
+    w0 = row[key];
+  }
+  const uint32_t room = tail0 - head0 < d.Q - 2 ? d.Q - 2 - (tail0 - head0) : 0;
+  const uint32_t ev0 = (EV && evk >= 0) ? d.ev_cnt[evk] : 0;
+  const bool stale0 = valid && ts_of(val) < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
+  const bool live = valid && !stale0 && (st_of(w0) == GX_ABSENT || ts_of(val) > ts_of(w0));
+  unsigned long long c_wr = 0, mexp = ~0ull;
+  uint32_t c_acc = 0, c_chg = 0, n_retx = 0;
+  if (!live) key = INV;
+  uint64_t sk = K32 ? (uint64_t)((key << 6) | sl) : (((uint64_t)key << 6) | sl);
+#pragma unroll
+  for (uint32_t k = 2; k <= (uint32_t)SEG; k <<= 1) {  // bitonic sort over the segment
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      uint64_t o;
+      if (K32) o = (uint32_t)__shfl_xor((uint32_t)sk, (int)j, SEG);
+      else o = __shfl_xor(sk, (int)j, SEG);
+      const bool keep_min = ((sl & j) == 0) == ((sl & k) == 0);
+      sk = keep_min ? (o < sk ? o : sk) : (o > sk ? o : sk);
+    }
+  }
+  const uint32_t src = (uint32_t)(sk & 63), skey = (uint32_t)(sk >> 6);
+  const bool vs = skey != INV;
+  const uint64_t sval = __shfl(val, (int)src, SEG), sw0 = __shfl(w0, (int)src, SEG);
+  const uint32_t pkey = __shfl_up(skey, 1, SEG);
+  const bool head = vs && (sl == 0 || pkey != skey);
+  const uint64_t heads = sballot(head);
+  const uint64_t le = sl == 63 ? ~0ull : ((2ull << sl) - 1);
+  const uint32_t gs = 63 - (uint32_t)__clzll((heads & le) | 1ull);  // first lane of this group
+  const uint32_t kpos = sl - gs;
+  const uint64_t after = heads & ~le;
+  const uint32_t nvs = (uint32_t)__popcll(sballot(vs));
+  const uint32_t glen = (after ? (uint32_t)__ffsll((long long)after) - 1 : nvs) - sl;  // heads only
+  const uint32_t kmax = seg_max<SEG>(vs ? kpos : 0);
+  uint64_t wg = sw0, wme = 0, wprev = GX_SLOT_ABSENT;
+  bool acc = false, stl = false;
+  for (uint32_t kk = 0; kk <= kmax; kk++) {  // occurrence kk of every group, arrival order
+    const uint64_t wcur = __shfl(wg, (int)gs, SEG);
+    if (vs && kpos == kk) {
+      wprev = wcur;
+      wme = merge_word(d, wcur, sval, acc, stl);
+    }
+    const uint64_t wn = __shfl(wme, (int)((gs + kk) & (SEG - 1)), SEG);
+    if (head && kk < glen) wg = wn;
+  }
+  c_acc += acc;
+  if (head && wg != sw0) {
+    row[skey] = wg;
+    c_wr++;
+    const unsigned long long x = exp_time(d.p, wg);
+    mexp = x < mexp ? x : mexp;
+  }
+  // ServiceChanged: an insert, or a stored status that differs (:317-340)
+  const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
+  c_chg += chg;
+  uint8_t *s_accf = &L.accf[sb], *s_chg = &L.chg[sb], *s_prev = &L.prev[sb];
+  uint64_t *s_accw = &L.accw[sb];
+  s_accf[src] = vs && acc && !owned_by(d, skey, v);
+  if (EV) {
+    s_chg[src] = chg;
+    s_prev[src] = (uint8_t)(st_of(wprev) == GX_ABSENT ? GX_UNKNOWN : st_of(wprev));
+  }
+  s_accw[src] = wme;
+  // per owner (contiguous in key order): its last accepted and last status-changing occurrence
+  const uint32_t own = vs ? owner_of(d, skey) : 0xffffffffu;
+  uint32_t mu = acc ? src + 1 : 0, mc = chg ? src + 1 : 0;
+#pragma unroll
+  for (int o = 1; o < SEG; o <<= 1) {
+    const uint32_t yu = __shfl_down(mu, o, SEG), yc = __shfl_down(mc, o, SEG), yo = __shfl_down(own, o, SEG);
+    if (sl + o < (uint32_t)SEG && yo == own) {
+      mu = yu > mu ? yu : mu;
+      mc = yc > mc ? yc : mc;
+    }
+  }
+  const uint32_t pown = __shfl_up(own, 1, SEG);
+  const bool ohead = vs && (sl == 0 || pown != own);
+  const uint32_t mcmax = seg_max<SEG>(mc);
+  __threadfence_block();
+  wave_sync();
+  if (ohead && (mu || mc)) {
+    gx_server_times *st = srv_times(d, v, own);
+    if (mu) st->last_updated_ns = ts_of(s_accw[mu - 1]);  // server.LastUpdated (:323)
+    if (mc) st->last_changed_ns = ts_of(s_accw[mc - 1]);  // serverChanged (:204-215)
+    c_wr += (mu != 0) + (mc != 0);
+  }
+  uint32_t n_ev = 0;
+  if (EV && evk >= 0) {  // ChangeEvents in arrival order
+    const bool fe = s_chg[sl] != 0;
+    const uint64_t me = sballot(fe);
+    if (fe) ev_put(d, evk, ev0 + (uint32_t)__popcll(me & ((1ull << sl) - 1ull)), key, s_accw[sl], s_prev[sl]);
+    n_ev = (uint32_t)__popcll(me);
+  }
+  const bool f = s_accf[sl];  // ordered ballot compaction -> retransmit jobs (arrival order)
+  const uint64_t m = sballot(f);
+  const uint32_t pos = (uint32_t)__popcll(m & ((1ull << sl) - 1ull));
+  if (f && pos < room) d.fifo[(size_t)vi * d.Q + ((tail0 + pos) % d.Q)] = make_job(s_accw[sl], 0, key, meta_of(GX_JOB_RETX, 0, 1));
+  n_retx = (uint32_t)__popcll(m);
+  c_wr = seg_sum<SEG>((uint32_t)c_wr);
+  c_acc = seg_sum<SEG>(c_acc);
+  c_chg = seg_sum<SEG>(c_chg);
+#pragma unroll
+  for (int o = SEG / 2; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(mexp, o, SEG);
+    mexp = y < mexp ? y : mexp;
+  }
+  if (sl == 0) {
+    const uint32_t ok = n_retx < room ? n_retx : room;
+    if (ok) d.hs[vi].fifo_tail = tail0 + ok;
+    if (mcmax) d.vlc[vi] = ts_of(s_accw[mcmax - 1]);  // state.LastChanged
+    if (EV && evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
+    ctr_atomic(d, C_CHG, c_chg);
+    // 12 B per record + 8 B per slot read / written + 32 B per retransmit + 16 B per header + count
+    kbytes(d, GX_K_MERGE, 12ull * total + 8ull * (total + c_wr) + 32ull * ok + 16ull * deg + 4, total);
+    if (!d.sfilt) {  // else counted by the senders
+      ctr_atomic(d, C_GOSSIP_MERGES, total);
+      ctr_atomic(d, C_STALE, (unsigned long long)__popcll(sballot(stale0)) + 0 * stl);
+    }
+    ctr_atomic(d, C_GOSSIP_ACC, c_acc);
+    ctr_atomic(d, C_RETX, ok);
+    ctr_atomic(d, C_QDROP, n_retx - ok);
+    if (c_wr) {
+      mark_change(d);
+      atomicMin(&d.minexp[vi], mexp);
+    }
+  }
+  wave_sync();
+  return true;
+}
+
+#define MERGE_SEG 16
+// 64 / MERGE_SEG receivers per wave (merge_seg); a receiver whose inbox does not fit a segment is
+// merged afterwards by the whole wave (merge_receiver).
+template <bool K32, bool EV>
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_seg(Dev d) {
+  __shared__ MergeLds s_l[MERGE_WAVES];
+  constexpr uint32_t NS = 64 / MERGE_SEG;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63, seg = lane / MERGE_SEG;
+  const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * NS;
+  if (r0 >= d.Hl) return;
+  const uint32_t vi = r0 + seg;
+  bool fl = false;
+  if (vi < d.Hl) fl = d.mflag[vi] != 0;
+  if (fl && d.sfilt && (lane & (MERGE_SEG - 1)) == 0) d.mflag[vi] = 0;  // the senders flag next round's
+  const bool done = merge_seg<K32, EV, MERGE_SEG>(d, vi, fl, s_l[wv]);
+  uint64_t rest = __ballot(!done && (lane & (MERGE_SEG - 1)) == 0);
+  for (; rest; rest &= rest - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)__builtin_ctzll(rest) / MERGE_SEG, s_l[wv]);
 }
 
 template <bool K32, bool EV, int MERGE_RANGE = MERGE_RANGE_DEF>
