@@ -35,6 +35,10 @@ GXD T gld(const T *p) {  // scalars
   return *(const GX_GLOBAL T *)p;
 }
 typedef unsigned int gx_u32x3 __attribute__((ext_vector_type(3)));
+template <class T>
+GXD void gst(T *p, T v) {  // scalars
+  *(GX_GLOBAL T *)p = v;
+}
 GXD gx_u32x4 gld4(const void *p) { return *(const GX_GLOBAL gx_u32x4 *)p; }
 // a record's word and key only (dwordx3): no dead destination register for the allocator to reuse
 // while the load is in flight (that reuse makes it wait for the load on the spot)
@@ -109,6 +113,7 @@ struct Dev {
   grec *arena;
   uint32_t *arena_len;
   grec *msg;
+  uint64_t *msg_w0;    // [H*K][cap] the receiver's slot word each live record was filtered against
   uint32_t *msg_len;
   uint32_t *msg_dst;
   // Receiver inboxes: a sender registers each packet straight into its receiver's
@@ -154,7 +159,7 @@ struct Dev {
   uint32_t logS;       // log2(S) when S is a power of two
   int departures;      // p.depart_round >= 0 && p.depart_ppm
   uint32_t nblk_ae;    // digest blocks per row, ceil(R / GX_DIGEST_SLOTS)
-  uint32_t *snap;      // this round's k_send stores work_cnt[GX_WC_SCANS] here (pinned host memory), or null
+  uint64_t *snap;      // this round's k_send stores (round << 32 | work_cnt[GX_WC_SCANS]) here (pinned host memory), or null
   uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
   unsigned long long *kprof;  // diagnostics (env GX_KPROF): wall-clock phase marks of k_send per wave, or null
   uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels): bit 2

@@ -76,9 +76,9 @@ struct gx_engine {
   // memory every second round and consumed two snapshots later (scan_probe_begin). Both placements give
   // the same results; only the time differs.
   bool scan_heavy;
-  uint32_t *scan_snap;      // [2] pinned host copies of work_cnt[GX_WC_SCANS], written by k_send
-  uint32_t *scan_snap_dev;  // the same memory as the device addresses it
-  hipEvent_t scan_ev[2];
+  uint64_t *scan_snap;      // [2] pinned host copies of (round << 32 | work_cnt[GX_WC_SCANS]), written by k_send
+  uint64_t *scan_snap_dev;  // the same memory as the device addresses it
+  uint32_t scan_tag[2];     // the round each slot's snapshot was asked for
   uint32_t scan_k, scan_last;
   uint32_t *in_cnt_buf;     // [2][Hl] inbox counts by round parity (Dev::in_cnt, in_cnt_nx)
   int async_phases;         // sharded phase calls return without waiting (gx_set_stream)
@@ -310,27 +310,28 @@ static void owner_launch(const Dev &d, hipStream_t s) {
 }
 #define SCAN_GRID 2048  // worklist blocks: every listed row of a round streams at once, a quick exit when none do
 
-// Every second round: takes the scanned-view count of the snapshot two probes back (its kernel
-// finished long ago unless the host runs far ahead; then this waits for it while the device works
-// through the rounds queued since) and has this round's k_send store a new one (Dev::snap, one
-// 4-B store to pinned host memory; scan_probe_end records its event). A view scanned between the
-// two consumed snapshots selects the k_scan placement.
+// Every second round: takes the scanned-view count of the snapshot two probes back, if the device
+// has written it by now (the slot carries the round it was asked for; nothing waits for it: with the
+// device further behind, the last decision stands), and has this round's k_send store a new one
+// (Dev::snap, one 8-B store to pinned host memory, no event in the stream). A view scanned between
+// the two consumed snapshots selects the k_scan placement.
 static int scan_probe_begin(gx_engine *e) {
   e->d.snap = nullptr;
   if (e->d.round % 2) return GX_OK;
   const uint32_t i = e->scan_k & 1u;
   if (e->scan_k >= 2) {
-    HIPCHK(hipEventSynchronize(e->scan_ev[i]));
-    const uint32_t v = e->scan_snap[i];
-    e->scan_heavy = v != e->scan_last;
-    e->scan_last = v;
+    const uint64_t v = __atomic_load_n(&e->scan_snap[i], __ATOMIC_ACQUIRE);
+    if ((uint32_t)(v >> 32) == e->scan_tag[i]) {
+      e->scan_heavy = (uint32_t)v != e->scan_last;
+      e->scan_last = (uint32_t)v;
+    }
   }
+  e->scan_tag[i] = (uint32_t)e->d.round;
   e->d.snap = &e->scan_snap_dev[i];
   return GX_OK;
 }
 static int scan_probe_end(gx_engine *e) {
   if (!e->d.snap) return GX_OK;
-  HIPCHK(hipEventRecord(e->scan_ev[e->scan_k & 1u], e->stream));
   e->scan_k++;
   e->d.snap = nullptr;
   return GX_OK;
@@ -732,7 +733,7 @@ int gx_destroy(gx_engine *e) {
   }
   Dev &d = e->d;
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, d.in_stamp, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
-                  e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_len,
+                  e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_w0, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
                   d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
@@ -743,8 +744,6 @@ int gx_destroy(gx_engine *e) {
   if (e->side_stream) (void)hipStreamDestroy(e->side_stream);
   if (e->side_start) (void)hipEventDestroy(e->side_start);
   if (e->side_done) (void)hipEventDestroy(e->side_done);
-  for (int i = 0; i < 2; i++)
-    if (e->scan_ev[i]) (void)hipEventDestroy(e->scan_ev[i]);
   if (e->scan_snap) (void)hipHostFree(e->scan_snap);
   delete e;
   return GX_OK;
@@ -785,7 +784,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->side_pending = false;
   e->scan_heavy = true;  // k_scan placement until the first snapshots say no view gets scanned
   e->scan_snap = e->scan_snap_dev = nullptr;
-  e->scan_ev[0] = e->scan_ev[1] = nullptr;
+  e->scan_tag[0] = e->scan_tag[1] = 0xffffffffu;
   e->scan_k = e->scan_last = 0;
   e->async_phases = 0;
   e->ob_entries = nullptr;
@@ -845,15 +844,13 @@ int gx_create(const gx_params *p, gx_engine **out) {
   if (hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&e->side_start, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->side_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->scan_ev[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->scan_ev[1], hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc((void **)&e->scan_snap, 2 * sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc((void **)&e->scan_snap, 2 * sizeof(uint64_t), hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void **)&e->scan_snap_dev, e->scan_snap, 0) != hipSuccess) {
     (void)hipGetLastError();
     gx_destroy(e);
     return GX_EIO;
   }
-  e->scan_snap[0] = e->scan_snap[1] = 0;
+  e->scan_snap[0] = e->scan_snap[1] = ~0ull;
   // per-host arrays hold this shard's Hl hosts; the message table also takes the packets received
   // from other shards (at most (H - Hl) * K), so it is sized H * K.
   size_t Hg = d.H, H = d.Hl, K = d.KE ? d.KE : 1;
@@ -866,6 +863,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.arena, sizeof(grec) * H * d.A * d.L);
   ALLOC(d.arena_len, sizeof(uint32_t) * H * d.A);
   ALLOC(d.msg, sizeof(grec) * Hg * K * p->packet_cap);
+  ALLOC(d.msg_w0, sizeof(uint64_t) * Hg * K * p->packet_cap);
   ALLOC(d.msg_len, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_dst, sizeof(uint32_t) * Hg * K);
   ALLOC(d.msg_key, sizeof(uint32_t) * Hg * K);

@@ -198,8 +198,18 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
 // team-wide service mask is the OR of each lane's ballot shifted by T*i. Returns, on the lead
 // lane, whether the host went on the expiry-scan worklist (its BroadcastTombstones tick then
 // finishes after the scan).
-template <int T, int SPL = 1>
-GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
+// fwd (k_send's planned sends): the tick also loads the FIFO head jobs into fwd->pj (with the
+// sleep-ring head, in the same round trip) and hands its register copy of the bookkeeping to the
+// sends, which then neither reload it nor wait for the jobs.
+struct TickFwd {
+  gx_job *pj;         // the team's T LDS job slots
+  uint32_t *peers;    // the team's peer slots (count in [16]), sampled while the tick's loads fly
+  gx_host_state hs;   // the bookkeeping after the tick
+  uint32_t pf0, npf;  // FIFO position of pj[0], jobs loaded
+  uint32_t tick;      // d.tick[idx] as the tick set it
+};
+template <int T, int SPL = 1, bool FWD = false>
+GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lead = tl == 0;
   const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
@@ -235,7 +245,37 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
     }
     if (tl == 0) mexp0 = d.minexp[idx];
     if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
+    if (FWD) {  // the tick pushes at the FIFO tail only: the jobs at the head stay where they are
+      const uint32_t q = hs.fifo_tail - hs.fifo_head;
+      if (tl < q) fwd.pj[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
+      fwd.pf0 = hs.fifo_head;
+      fwd.npf = q < (uint32_t)T ? q : (uint32_t)T;
+    }
   }
+  if (FWD && tl == 0 && idx < d.Hl) {  // the sends' peers: ALU while the loads above are in flight
+    const uint64_t h3 = mix64(mix64(mix64(d.p.seed ^ ((uint64_t)ST_PEER * 0xD1B54A32D192ED03ull)) ^ (uint64_t)d.round) ^
+                              (uint64_t)(d.lo + idx));
+    uint32_t base = 0, m = d.H;
+    const uint32_t u = d.lo + idx;
+    if (d.partitioned) {
+      const uint32_t half = d.H / 2;
+      base = u < half ? 0 : half;
+      m = u < half ? half : d.H - half;
+    }
+    uint32_t cnt = 0;
+    if (m >= 2) {
+      const uint32_t want = d.K < m - 1 ? d.K : m - 1;
+      for (uint32_t at = 0; cnt < want && at < 64u * d.K; at++) {  // = sample_peers
+        const uint32_t ix = unif(mix64(h3 ^ at), m - 1), self = u - base;
+        const uint32_t pp = base + (ix >= self ? ix + 1 : ix);
+        bool dup = false;
+        for (uint32_t i = 0; i < cnt; i++) dup |= fwd.peers[i] == pp;
+        if (!dup) fwd.peers[cnt++] = pp;
+      }
+    }
+    fwd.peers[16] = cnt;
+  }
+  if (FWD) fwd.tick = 0;
   wave_sync();  // the team's sleep-ring slots
   if (idx < d.Hl) {
     const uint32_t o = d.lo + idx;
@@ -363,8 +403,8 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
           hs.flags |= 1u;
         }
       }
+      const bool tick = !(hs.flags & 2u) && hs.bt_next <= d.round;
       if (lead) {
-        const bool tick = !(hs.flags & 2u) && hs.bt_next <= d.round;
         d.tick[idx] = tick ? 1 : 0;
         if (tick) {
           // (the tick's own merges only lower the bound to values >= now: same decision)
@@ -379,6 +419,10 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj) {
         }
         d.hs[idx] = hs;
       }
+      if (FWD) {
+        fwd.hs = hs;
+        fwd.tick = tick ? 1u : 0u;  // the sends reload what the tick's finish changes
+      }
     }
   }
   return queued;
@@ -392,7 +436,8 @@ __global__ __launch_bounds__(B) void k_owner(Dev d) {
     *d.ovf_cnt_nx = 0;
     *d.wl_cnt_nx = 0;
   }
-  owner_tick<T>(d, a, blockIdx.x * (B / T) + threadIdx.x / T, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
+  TickFwd none;
+  owner_tick<T>(d, a, blockIdx.x * (B / T) + threadIdx.x / T, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)], none);
   acc_flush(d, a);
 }
 
@@ -922,6 +967,36 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
 }
 
 // ========================================================================= phase 3: gossip send ==
+// The part of rng4(seed, ST_PEER, round, u, a) shared by every host of a round (sample_peers_h).
+GXD uint64_t peer_seed(const Dev &d) {
+  return mix64(mix64(d.p.seed ^ ((uint64_t)ST_PEER * 0xD1B54A32D192ED03ull)) ^ (uint64_t)d.round);
+}
+// sample_peers with the round's shared hash levels hoisted: rng4(...) = mix64(mix64(h2 ^ u) ^ a).
+GXD uint32_t sample_peers_h(const Dev &d, uint64_t h2, uint32_t u, uint32_t *peers) {
+  uint32_t base = 0, m = d.H;
+  if (d.partitioned) {
+    uint32_t half = d.H / 2;
+    if (u < half) {
+      base = 0;
+      m = half;
+    } else {
+      base = half;
+      m = d.H - half;
+    }
+  }
+  if (m < 2) return 0;
+  const uint64_t h3 = mix64(h2 ^ u);
+  uint32_t want = d.K < m - 1 ? d.K : m - 1, cnt = 0;
+  for (uint32_t a = 0; cnt < want && a < 64u * d.K; a++) {
+    uint64_t x = mix64(h3 ^ a);
+    uint32_t idx = unif(x, m - 1), self = u - base;
+    uint32_t p = base + (idx >= self ? idx + 1 : idx);
+    bool dup = false;
+    for (uint32_t i = 0; i < cnt; i++) dup |= peers[i] == p;
+    if (!dup) peers[cnt++] = p;
+  }
+  return cnt;
+}
 // memberlist kRandomNodes restated as a seeded sampler: k distinct peers != u on u's side.
 GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
   uint32_t base = 0, m = d.H;
@@ -990,8 +1065,16 @@ struct PlanCall {
   uint32_t peer;      // receiver (global id)
   uint32_t lpre;      // records of the chunk's earlier calls
 };
-static_assert(sizeof(PlanCall) >= 16 * sizeof(uint32_t), "a PlanCall slot holds a team's 16 peers");
+static_assert(sizeof(PlanCall) >= 17 * sizeof(uint32_t), "a PlanCall slot holds a team's 16 peers and their count");
 #define GX_NOSLOT 0xffffffffu  // inbox header slot: the records are in the message entry
+// ... and each carries the receiver's slot word it was filtered against (msg_w0). Between that read
+// and the receiver's merge only the receiver's own tick (its own records) and its expiry scan
+// (a view whose tick is 2) write the view, so for every other record the merge takes that word
+// instead of reading the slot again.
+#define GX_NOSLOT_W0 0xfffffffeu
+GXD bool w0_fwd(const Dev &d, uint32_t slot, uint32_t tick, uint32_t key, uint32_t v) {
+  return slot == GX_NOSLOT_W0 && tick != 2 && !owned_by(d, key, v);
+}
 
 // Batch item i of a planned call's job (get_broadcasts_team's item() for i < m).
 GXD grec plan_item(const Dev &d, const PlanCall &c, uint32_t i) {
@@ -1015,7 +1098,7 @@ GXD grec plan_item(const Dev &d, const PlanCall &c, uint32_t i) {
 // kb: algorithmic bytes (the caller flushes them to GX_K_SEND).
 template <int T>
 GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_job *pjs, PlanCall *pl,
-                      const uint32_t *peers, uint32_t np, unsigned long long &kb) {
+                      const uint32_t *peers, uint32_t np, unsigned long long &kb, uint32_t npf0 = 0) {
   constexpr int PLAN_Q = PLAN_RECS / T;
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lead = tl == 0;
@@ -1024,8 +1107,8 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   grec *dq = &d.dq[(size_t)idx * d.DQ];
   const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
   const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
-  // FIFO head jobs, T at a time: position pf0 + q in pjs[q], q < npf
-  uint32_t pf0 = hs.fifo_head, npf = 0;
+  // FIFO head jobs, T at a time: position pf0 + q in pjs[q], q < npf (npf0 already loaded)
+  uint32_t pf0 = hs.fifo_head, npf = npf0;
   uint32_t j = 0, n = 0;
   bool stop = np == 0;
   unsigned fm = 0, fs = 0;
@@ -1230,6 +1313,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
           g.r = r[q];
           g.pad = 0;
           gst_rec(&d.msg[(size_t)c.x * cap + rank], g);
+          if (c.row) gst(&d.msg_w0[(size_t)c.x * cap + rank], w0[q]);
         }
         run += (uint32_t)__popcll(lm);
       }
@@ -1250,7 +1334,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       d.msg_len[c.x] = stored;
       d.msg_dst[c.x] = c.peer;
       if (c.row && stored) {
-        inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, GX_NOSLOT);
+        inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, GX_NOSLOT_W0);
         d.mflag[rv] = 1;
       }
       stored_all = stored + ((c.row && stored) ? 2u : 0u);  // a header and its count ~ 2 records
@@ -1284,16 +1368,18 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
 GXD bool filt_used(const Dev &d, uint32_t pos) { return d.sfilt && pos != 0xffffffffu; }
 // PLAN: send_planned (the engine picks it when its conditions hold: record budget, !X, retransmit
 // sleep > 0, senders' filter).
-template <int T, bool X, bool PLAN = false>
+template <int T, bool X, bool PLAN = false, bool FWD = false>
 GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, unsigned &lost, PlanCall *pl,
-                   unsigned long long &kb) {
+                   unsigned long long &kb, const TickFwd &fwd) {
   const uint32_t lane = threadIdx.x & (T - 1);
   {
     uint32_t u = d.lo + idx;
     uint32_t cap = d.p.packet_cap;
     gx_host_state *h = &d.hs[idx];
-    gx_host_state hs = *h;  // loaded with the tick flag (both before any store)
-    const bool tick = do_bt && d.tick[idx];
+    // the bookkeeping and tick flag: from the owner tick of this launch, or loaded (both before any store)
+    gx_host_state hs = FWD ? fwd.hs : *h;
+    const bool tick = do_bt && (FWD ? fwd.tick != 0 : d.tick[idx] != 0);
+    bool pre = FWD;  // the FIFO head jobs the tick loaded are still at the head
     for (uint32_t j = lane; j < d.KE; j += T) {
       d.msg_len[(size_t)idx * d.KE + j] = 0;
       d.msg_key[(size_t)idx * d.KE + j] = u * d.KE + j;
@@ -1305,20 +1391,14 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       }
       __threadfence_block();  // the team reads the host's bookkeeping below
       hs = *h;
+      pre = false;  // the finish pushed to the FIFO: its head jobs are loaded again
     }
     if (lane == 0) kb += 128;  // the host's bookkeeping read and written
     GX_KP(4);
     if (PLAN) {
-      uint32_t *peers = reinterpret_cast<uint32_t *>(&pl[PLAN_CH]);  // the team's 16 peer slots (LDS)
-      uint32_t np = 0;
-      if (lane == 0) {
-        uint32_t pr[16];
-        np = sample_peers(d, u, pr);
-        for (uint32_t k = 0; k < np; k++) peers[k] = pr[k];
-      }
-      np = __shfl(np, (int)(threadIdx.x & 63 & ~(uint32_t)(T - 1)), 64);
-      wave_sync();
-      send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb);
+      uint32_t *peers = reinterpret_cast<uint32_t *>(&pl[PLAN_CH]);  // the team's peers (k_send's prologue)
+      const uint32_t np = peers[16];
+      send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb, (pre && fwd.pf0 == hs.fifo_head) ? fwd.npf : 0u);
       if (lane == 0) *h = hs;
     } else if (!X || !departed(d, u)) {
       const bool fd = X && d.p.fd_enable;
@@ -1419,7 +1499,21 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
   GX_KP(0);
-  if (d.snap && blockIdx.x == 0 && threadIdx.x == 0) *d.snap = d.work_cnt[GX_WC_SCANS];  // scan_probe_begin
+  TickFwd fwd;
+  fwd.peers = reinterpret_cast<uint32_t *>(&s_pl[PLAN ? threadIdx.x / T : 0][PLAN_CH]);
+  if (PLAN && OWN == 0 && (threadIdx.x & (T - 1)) == 0 && idx < d.Hl) {  // the sends' peers (count in [16])
+    uint32_t pr[16];
+    const uint32_t np = sample_peers_h(d, peer_seed(d), d.lo + idx, pr);
+    for (uint32_t k = 0; k < np; k++) fwd.peers[k] = pr[k];
+    fwd.peers[16] = np;
+  }
+  if (PLAN) wave_sync();
+  fwd.pj = s_pj[threadIdx.x / T];
+  fwd.npf = 0;
+  fwd.pf0 = 0;
+  fwd.tick = 0;
+  if (d.snap && blockIdx.x == 0 && threadIdx.x == 0)  // scan_probe_begin: tagged with the round
+    *d.snap = ((uint64_t)(uint32_t)d.round << 32) | d.work_cnt[GX_WC_SCANS];
   if constexpr (OWN > 0) {
     if (threadIdx.x == 0) {
       s_nscan = 0;
@@ -1429,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       }
     }
     __syncthreads();
-    const bool q = owner_tick<T, OWN>(d, a, idx, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)]);
+    const bool q = owner_tick<T, OWN, PLAN>(d, a, idx, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)], fwd);
     if (q) s_scan[atomicAdd(&s_nscan, 1u)] = idx;  // lead lanes only
     GX_KP(1);
     __syncthreads();  // the block's ticks before its scans and sends read them
@@ -1452,8 +1546,9 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   }
   unsigned long long kb = 0;
   GX_KP(3);
-  if (idx < d.Hl)
-    send_host<T, X, PLAN>(d, a, idx, s_pj[threadIdx.x / T], do_bt, lost, s_pl[PLAN ? threadIdx.x / T : 0], kb);
+  if (idx < d.Hl)  // (PLAN runs without departures: every host ticked)
+    send_host<T, X, PLAN, PLAN && (OWN > 0)>(d, a, idx, s_pj[threadIdx.x / T], do_bt, lost,
+                                            s_pl[PLAN ? threadIdx.x / T : 0], kb, fwd);
   GX_KP(7);
   acc_flush(d, a);
   if (X && lost) ctr_atomic(d, C_LOST, lost);
@@ -1565,6 +1660,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     if ((int)lane >= o) incl += y;
   }
   const uint32_t pstart = incl - sh.z, total = __shfl(incl, 63, 64);
+  const uint32_t vtick = d.tick[vi];
   gx_host_state *h = &d.hs[vi];
   const uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   const uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
@@ -1585,18 +1681,26 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     g.w = 0;
     g.r = INV;
     g.pad = 0;
+    uint64_t fw0 = 0;
+    uint32_t fslot = 0;
     for (uint32_t k = kc; k < deg; k++) {  // hop 2: one predicated load per overlapping packet
       const uint32_t st = rdl(pstart, k);
       if (st >= t0 + 64) break;
       const uint32_t off = i - st;
-      if (off < rdl(sh.z, k)) g = packet_recs(d, vi, rdl(sh.w, k), rdl(sh.y, k))[off];
+      if (off < rdl(sh.z, k)) {
+        fslot = rdl(sh.w, k);
+        g = packet_recs(d, vi, fslot, rdl(sh.y, k))[off];
+        if (fslot == GX_NOSLOT_W0) fw0 = d.msg_w0[(size_t)rdl(sh.y, k) * d.p.packet_cap + off];
+      }
     }
     uint32_t key = INV;
     uint64_t val = 0, w0 = 0;
     if (valid) {
       key = g.r;
       val = g.w;
-      w0 = row[key];  // hop 3
+      // hop 3 only where the sender's word can be stale: own records, a scanned view, and every
+      // tile after the first (an earlier tile may have written the slot)
+      w0 = (t0 == 0 && w0_fwd(d, fslot, vtick, key, v)) ? fw0 : row[key];
     }
     c_merge += valid;
     c_rd += valid;  // one view slot read per inbound record
@@ -1772,11 +1876,13 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
   uint4 hd = make_uint4(0u, 0u, 0u, 0u);
   uint32_t deg = 0, tail0 = 0, head0 = 0;
   int32_t evk = -1;
+  uint32_t vtick = 2;
   if (act) {
     if (sl < d.DI) hd = d.in_hdr[(size_t)vi * d.DI + sl];
     deg = d.in_cnt[vi];
     tail0 = d.hs[vi].fifo_tail;
     head0 = d.hs[vi].fifo_head;
+    vtick = d.tick[vi];
     if (EV) evk = d.ev_slot[vi];
   }
   const uint32_t len = sl < deg ? hd.z : 0u;
@@ -1812,11 +1918,12 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
   uint32_t key = INV;
   uint64_t val = 0, w0 = 0;
   uint64_t *row = &d.view[(size_t)vi * d.R];
-  if (valid) {  // hop 2, hop 3
+  if (valid) {  // hop 2 (the record and the slot word its sender read), hop 3 only where that can be stale
     const grec g = gld_rec(&packet_recs(d, vi, pw, pe)[sl - ps]);
+    const uint64_t fw0 = pw == GX_NOSLOT_W0 ? gld(&d.msg_w0[(size_t)pe * d.p.packet_cap + (sl - ps)]) : 0ull;
     key = g.r;
     val = g.w;
-    w0 = row[key];
+    w0 = w0_fwd(d, pw, vtick, key, v) ? fw0 : row[key];
   }
   const uint32_t room = tail0 - head0 < d.Q - 2 ? d.Q - 2 - (tail0 - head0) : 0;
   const uint32_t ev0 = (EV && evk >= 0) ? d.ev_cnt[evk] : 0;
@@ -3319,9 +3426,10 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
       g.r = 0;
       g.pad = 0;
       bool live = false;
+      uint64_t w0 = 0;
       if (x < len) {
         g = recs[x];
-        const uint64_t w0 = row[g.r];
+        w0 = row[g.r];
         const int64_t ts = ts_of(g.w);
         const bool stale = ts < t_stale;
         const bool gc = st_of(w0) == GX_TOMBSTONE && ts_of(w0) < t_gc;
@@ -3329,7 +3437,11 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
         nstale += stale;
       }
       const unsigned long long m = __ballot(live);
-      if (live) pk[nlive + (uint32_t)__popcll(m & ((1ull << threadIdx.x) - 1ull))] = g;
+      if (live) {
+        const uint32_t at = nlive + (uint32_t)__popcll(m & ((1ull << threadIdx.x) - 1ull));
+        pk[at] = g;
+        d.msg_w0[e * d.p.packet_cap + at] = w0;
+      }
       nlive += (uint32_t)__popcll(m);
     }
     nstale = (uint32_t)wave_sum(nstale);
@@ -3349,7 +3461,7 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
       d.msg_dst[e] = dst;
       d.msg_len[e] = nlive;
       if (fcap) d.fd_len[e] = nfd;
-      if (nlive || nfd) inbox_header(d, vi, inbox_claim(d, vi), key, (uint32_t)e, nlive, GX_NOSLOT);
+      if (nlive || nfd) inbox_header(d, vi, inbox_claim(d, vi), key, (uint32_t)e, nlive, GX_NOSLOT_W0);
       if (nlive) d.mflag[vi] = 1;
       ctr_atomic(d, C_GOSSIP_MERGES, len);
       ctr_atomic(d, C_STALE, nstale);
