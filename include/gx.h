@@ -357,6 +357,17 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap);
  * is reported as GX_EINVAL at the next call that waits. */
 int gx_outbox_sizes_async(gx_engine *e, uint64_t *bytes_per_shard);
 int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes);
+/* The gossip exchange with sizes every shard knows ahead, so no exchange layer waits on the device
+ * for them: the packets shard s sends shard g in round n are bounded by the seeded peer sample
+ * (GossipMessages slots per sampled peer of a host of s on g), which every shard can compute.
+ * gx_exchange_plan fills sizes[s * G + g] = that bound in packet-slot bytes for the engine's current
+ * round (from a batch of rounds computed ahead on the device); gx_outbox_pack_planned packs this
+ * shard's packets for shard g into its sizes[me * G + g] bytes: the packets first (as
+ * gx_outbox_pack), then empty slots (sender key 0xffffffff), which gx_inbox_unpack skips. Not with
+ * the failure detector, whose targets come from the member lists: GX_ENOSYS. */
+#define GX_SLOT_EMPTY 0xffffffffu
+int gx_exchange_plan(gx_engine *e, uint64_t *sizes);
+int gx_outbox_pack_planned(gx_engine *e, void *buf, uint64_t cap);
 int gx_round_merge(gx_engine *e); /* phase 4: gather-then-merge of local + received packets */
 /* Push-pull across shards exchanges block digests first and then only the blocks that differ
  * (Dynamo-style anti-entropy), each once: its leader ships it run-length coded, the follower

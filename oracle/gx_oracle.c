@@ -1945,6 +1945,71 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
     }
   return GX_OK;
 }
+/* Planned gossip exchange (gx.h gx_exchange_plan): slots shard s sends shard g this round are
+ * bounded by GossipMessages slots per sampled peer on another shard, from the seeded sampler of
+ * every host of the cluster. */
+static void exchange_counts(gx_engine *e, uint64_t *cnt) {
+  for (uint32_t i = 0; i < e->G * e->G; i++) cnt[i] = 0;
+  if (e->G < 2 || !e->K) return;
+  uint32_t peers[64];
+  for (uint32_t u = 0; u < e->H; u++) {
+    const uint32_t n = sample_peers(e, u, peers), su = shard_of(e, u);
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t sp = shard_of(e, peers[j]);
+      if (sp != su) cnt[su * e->G + sp] += e->NG;
+    }
+  }
+}
+int gx_exchange_plan(gx_engine *e, uint64_t *sizes) {
+  if (!e || !sizes) return GX_EINVAL;
+  if (e->p.fd_enable) return GX_ENOSYS;
+  exchange_counts(e, sizes);
+  for (uint32_t i = 0; i < e->G * e->G; i++) sizes[i] *= slot_bytes(e);
+  return GX_OK;
+}
+int gx_outbox_pack_planned(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  if (e->p.fd_enable) return GX_ENOSYS;
+  if (e->G < 2 || !e->K) return GX_OK;
+  uint64_t *cnt = (uint64_t *)malloc(sizeof(uint64_t) * e->G * e->G);
+  exchange_counts(e, cnt);
+  const uint32_t me = shard_of(e, e->lo);
+  uint64_t slots = 0;
+  for (uint32_t g = 0; g < e->G; g++) slots += cnt[me * e->G + g];
+  const size_t sb = slot_bytes(e);
+  if (cap < slots * sb) {
+    free(cnt);
+    return GX_EINVAL;
+  }
+  uint8_t *p = (uint8_t *)buf;
+  size_t off = 0;
+  int rc = GX_OK;
+  for (uint32_t g = 0; g < e->G; g++) {
+    uint64_t used = 0;
+    for (size_t m = (size_t)e->lo * e->KE; m < (size_t)e->hi * e->KE; m++) {
+      if ((!e->msg_len[m] && !fd_len_of(e, m)) || is_local(e, e->msg_dst[m]) || shard_of(e, e->msg_dst[m]) != g) continue;
+      if (used == cnt[me * e->G + g]) { /* more packets than sampled peers: cannot happen */
+        rc = GX_EIO;
+        break;
+      }
+      uint32_t hdr[4] = {(uint32_t)m, e->msg_dst[m], e->msg_len[m], 0};
+      memset(p + off, 0, sb);
+      memcpy(p + off, hdr, 16);
+      memcpy(p + off + 16, &e->msg[m * e->p.packet_cap], 16ull * e->msg_len[m]);
+      off += sb;
+      used++;
+    }
+    for (; used < cnt[me * e->G + g]; used++) { /* empty slots */
+      uint32_t hdr[4] = {GX_SLOT_EMPTY, 0, 0, 0};
+      memset(p + off, 0, sb);
+      memcpy(p + off, hdr, 16);
+      off += sb;
+    }
+  }
+  free(cnt);
+  return rc;
+}
+
 /* A received slot is refused (GX_EINVAL, nothing of the call applied) unless: its sender key m <
  * H*KE names a packet entry of another shard's host, no slot of this round carried m before
  * (one packet per sender entry), the receiver is on this shard, len <= packet_cap, n_fd <=
@@ -1965,6 +2030,7 @@ int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
   for (size_t off = 0; off < bytes && !bad; off += sb) { /* validate every slot before applying any */
     uint32_t hdr[4];
     memcpy(hdr, p + off, 16);
+    if (hdr[0] == GX_SLOT_EMPTY) continue; /* an unused slot of a planned exchange */
     uint32_t m = hdr[0], dst = hdr[1], len = hdr[2], nfd = e->p.fd_enable ? hdr[3] : 0;
     (void)nfd;
     if (m >= e->H * e->KE || is_local(e, m / e->KE) || !is_local(e, dst) || len > e->p.packet_cap ||
@@ -1986,6 +2052,7 @@ int gx_inbox_unpack(gx_engine *e, const void *buf, uint64_t bytes) {
   for (size_t off = 0; off < bytes; off += sb) {
     uint32_t hdr[4];
     memcpy(hdr, p + off, 16);
+    if (hdr[0] == GX_SLOT_EMPTY) continue;
     uint32_t m = hdr[0], dst = hdr[1], len = hdr[2], nfd = e->p.fd_enable ? hdr[3] : 0;
     e->in_stamp[m] = e->round;
     memcpy(&e->msg[(size_t)m * e->p.packet_cap], p + off + 16, 16ull * len);

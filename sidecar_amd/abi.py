@@ -195,7 +195,7 @@ ABI_FUNCS = [
     "gx_read_views", "gx_write_views", "gx_write_slot", "gx_read_hosts", "gx_read_queue",
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
-    "gx_inbox_unpack", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
+    "gx_inbox_unpack", "gx_exchange_plan", "gx_outbox_pack_planned", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
     "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_set_stream", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
@@ -244,6 +244,7 @@ def _declare(lib):
         "gx_converged": ([vp, P(i32), P(C.c_uint64)], i32),
         "gx_round_send": ([vp], i32), "gx_outbox_bytes": ([vp, vp], i32),
         "gx_outbox_pack": ([vp, vp, C.c_uint64], i32), "gx_inbox_unpack": ([vp, vp, C.c_uint64], i32),
+        "gx_exchange_plan": ([vp, vp], i32), "gx_outbox_pack_planned": ([vp, vp, C.c_uint64], i32),
         "gx_round_merge": ([vp], i32), "gx_ae_bytes": ([vp, vp], i32),
         "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64, vp, C.c_uint64], i32),
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
@@ -712,6 +713,16 @@ class Engine:
         out = np.zeros(self.G, dtype=np.uint64)
         check(self.lib.gx_outbox_bytes(self.h, out.ctypes.data_as(C.c_void_p)), "gx_outbox_bytes")
         return out
+
+    def exchange_plan(self) -> np.ndarray:
+        """(G, G) bytes shard s sends shard g this round in the planned exchange (gx.h)."""
+        G = max(1, self.params.n_shards)
+        out = np.zeros(G * G, dtype=np.uint64)
+        check(self.lib.gx_exchange_plan(self.h, out.ctypes.data_as(C.c_void_p)), "gx_exchange_plan")
+        return out.reshape(G, G)
+
+    def outbox_pack_planned(self, ptr: int, cap: int):
+        check(self.lib.gx_outbox_pack_planned(self.h, C.c_void_p(ptr), C.c_uint64(cap)), "gx_outbox_pack_planned")
 
     def outbox_sizes_async(self, ptr: int):
         """Per-shard outbox bytes into engine memory at ptr (device memory on the HIP engine)."""

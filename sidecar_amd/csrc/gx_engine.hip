@@ -139,6 +139,15 @@ struct gx_engine {
   unsigned long long *conv_bad;
   uint64_t *digest_buf;
   size_t kprof_n;  // diagnostics: u64 marks in d.kprof (env GX_KPROF)
+  // planned gossip exchange (gx_exchange_plan): slot bounds of XPLAN_BATCH rounds computed ahead on
+  // xplan_stream into pinned host memory, two batches (the current one and the next)
+  hipStream_t xplan_stream;
+  uint32_t *xplan_dev;           // [XPLAN_BATCH][G][G]
+  uint32_t *xplan_host;          // [2][XPLAN_BATCH][G][G] pinned
+  int64_t xplan_start[2];
+  hipEvent_t xplan_ev[2];
+  int64_t xbound_round;          // the round xbound holds
+  XBound xbound;                 // this shard's slots per destination this round
 };
 
 static void codec_free(gx_engine *e);  // gx_codec_host.hpp
@@ -745,6 +754,12 @@ int gx_destroy(gx_engine *e) {
   if (e->side_start) (void)hipEventDestroy(e->side_start);
   if (e->side_done) (void)hipEventDestroy(e->side_done);
   if (e->scan_snap) (void)hipHostFree(e->scan_snap);
+  if (e->xplan_stream) (void)hipStreamSynchronize(e->xplan_stream);
+  if (e->xplan_dev) (void)hipFree(e->xplan_dev);
+  if (e->xplan_host) (void)hipHostFree(e->xplan_host);
+  for (int i = 0; i < 2; i++)
+    if (e->xplan_ev[i]) (void)hipEventDestroy(e->xplan_ev[i]);
+  if (e->xplan_stream) (void)hipStreamDestroy(e->xplan_stream);
   delete e;
   return GX_OK;
 }
@@ -910,6 +925,11 @@ int gx_create(const gx_params *p, gx_engine **out) {
     if (p->fd_push_pull_state) ALLOC(d.fd_snap, sizeof(uint64_t) * H * Hg);
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
+  e->xplan_stream = nullptr;
+  e->xplan_dev = e->xplan_host = nullptr;
+  e->xplan_start[0] = e->xplan_start[1] = -1;
+  e->xplan_ev[0] = e->xplan_ev[1] = nullptr;
+  e->xbound_round = -1;
   e->kprof_n = 0;
   if (getenv("GX_KPROF")) {  // diagnostics: phase marks of every k_send wave (gx_kprof_read)
     e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8;
@@ -1797,6 +1817,90 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   if (cap < e->n_ob * slot_bytes(e->d)) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   k_outbox_pack<<<e->n_ob, 64, 0, e->stream>>>(e->d, e->ob_entries, e->n_ob, (uint8_t *)buf);
+  return phase_done(e);
+}
+
+// Batch `start` of slot bounds into host slot k (asynchronous, on xplan_stream).
+static int xplan_launch(gx_engine *e, int k, int64_t start) {
+  Dev &d = e->d;
+  const size_t n = (size_t)XPLAN_BATCH * d.G * d.G;
+  HIPCHK(hipMemsetAsync(e->xplan_dev, 0, sizeof(uint32_t) * n, e->xplan_stream));
+  k_xplan<<<dim3(nblk(d.H, 256), XPLAN_BATCH), 256, 0, e->xplan_stream>>>(d, start, e->xplan_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->xplan_host + (size_t)k * n, e->xplan_dev, sizeof(uint32_t) * n, hipMemcpyDeviceToHost,
+                        e->xplan_stream));
+  HIPCHK(hipEventRecord(e->xplan_ev[k], e->xplan_stream));
+  e->xplan_start[k] = start;
+  return GX_OK;
+}
+// The counts of the current round: its batch (computed XPLAN_BATCH rounds ahead, so the wait below
+// finds it done except for the first batch) and the next batch queued behind it.
+static int xplan_counts(gx_engine *e, const uint32_t **out) {
+  Dev &d = e->d;
+  if (!e->xplan_dev) {
+    if (hipStreamCreateWithFlags(&e->xplan_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->xplan_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->xplan_ev[1], hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void **)&e->xplan_dev, sizeof(uint32_t) * XPLAN_BATCH * d.G * d.G) != hipSuccess ||
+        hipHostMalloc((void **)&e->xplan_host, sizeof(uint32_t) * 2 * XPLAN_BATCH * d.G * d.G) != hipSuccess) {
+      (void)hipGetLastError();
+      return GX_ENOMEM;
+    }
+  }
+  const int64_t start = d.round - d.round % XPLAN_BATCH;
+  const int k = (int)((start / XPLAN_BATCH) & 1);
+  int rc = GX_OK;
+  if (e->xplan_start[k] != start) rc = xplan_launch(e, k, start);
+  if (!rc && e->xplan_start[k ^ 1] != start + XPLAN_BATCH) rc = xplan_launch(e, k ^ 1, start + XPLAN_BATCH);
+  if (rc) return rc;
+  HIPCHK(hipEventSynchronize(e->xplan_ev[k]));
+  *out = e->xplan_host + ((size_t)k * XPLAN_BATCH + (size_t)(d.round - start)) * d.G * d.G;
+  return GX_OK;
+}
+
+int gx_exchange_plan(gx_engine *e, uint64_t *sizes) {
+  if (!e || !sizes) return GX_EINVAL;
+  Dev &d = e->d;
+  if (d.p.fd_enable) return GX_ENOSYS;
+  if (d.G > XPLAN_GMAX) return GX_EINVAL;
+  for (uint32_t i = 0; i < d.G * d.G; i++) sizes[i] = 0;
+  if (d.G < 2 || !d.K) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  const uint32_t *c = nullptr;
+  int rc = xplan_counts(e, &c);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < d.G * d.G; i++) sizes[i] = (uint64_t)c[i] * slot_bytes(d);
+  for (uint32_t g = 0; g < XPLAN_GMAX; g++) e->xbound.n[g] = g < d.G ? c[d.gid * d.G + g] : 0u;
+  e->xbound_round = d.round;
+  return GX_OK;
+}
+
+int gx_outbox_pack_planned(gx_engine *e, void *buf, uint64_t cap) {
+  if (!e || (cap && !buf)) return GX_EINVAL;
+  Dev &d = e->d;
+  if (d.p.fd_enable) return GX_ENOSYS;
+  if (d.G < 2 || !d.K) return GX_OK;
+  if (e->xbound_round != d.round) {  // the plan of this round, if the caller did not ask for it
+    std::vector<uint64_t> tmp((size_t)d.G * d.G);
+    int rc = gx_exchange_plan(e, tmp.data());
+    if (rc) return rc;
+  }
+  uint64_t slots = 0;
+  for (uint32_t g = 0; g < d.G; g++) slots += e->xbound.n[g];
+  if (cap < slots * slot_bytes(d)) return GX_EINVAL;
+  if (!slots) return GX_OK;
+  HIPCHK(hipSetDevice(e->device));
+  set_round_fields(e);
+  const size_t ne = (size_t)d.Hl * d.KE;
+  const uint32_t nchunk = (uint32_t)((ne + 255) / 256);
+  uint32_t *ccnt = e->ob_counts + d.G, *off = ccnt + (size_t)nchunk * d.G;
+  const size_t lds = sizeof(uint32_t) * 4 * d.G;
+  k_ob_count<<<nchunk, 256, lds, e->stream>>>(d, ccnt);
+  k_ob_scan<<<1, 256, 0, e->stream>>>(d, ccnt, nchunk, off, e->ob_counts);
+  k_ob_fill<<<nchunk, 256, lds, e->stream>>>(d, off, e->ob_entries);
+  k_outbox_pack_planned<<<(unsigned)slots, 64, 0, e->stream>>>(d, e->ob_entries, e->ob_counts, e->xbound, (uint8_t *)buf);
+  e->n_ob = 0;
+  e->ob_async = false;
   return phase_done(e);
 }
 

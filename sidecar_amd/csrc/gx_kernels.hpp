@@ -3338,20 +3338,9 @@ __global__ void k_ob_bytes(Dev d, const uint32_t *tot, unsigned long long *bytes
   }
   *n_out = n;
 }
-// n_dev: the slot count on the device (gx_outbox_sizes_async); slots past cap_slots are refused
-__global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t *out, const uint32_t *n_dev = nullptr,
-                              uint32_t cap_slots = 0xffffffffu) {
-  uint32_t i = blockIdx.x;
-  if (n_dev) {
-    n = *n_dev;
-    if (i == 0 && threadIdx.x == 0 && n > cap_slots) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);
-    if (n > cap_slots) n = cap_slots;
-  }
-  if (i >= n) return;
-  uint32_t e = entry[i];
+// One packet slot (message entry e) into the wire buffer at dst (a 64-thread block).
+GXD void pack_slot(const Dev &d, uint32_t e, uint8_t *dst) {
   const uint32_t fcap = d.p.fd_enable ? d.p.fd_msg_cap : 0;
-  size_t sb = 16 + 16ull * d.p.packet_cap + 16ull * fcap;
-  uint8_t *dst = out + (size_t)i * sb;
   uint32_t len = d.msg_len[e], nfd = fcap ? d.fd_len[e] : 0;
   if (threadIdx.x == 0) {
     uint32_t *hdr = reinterpret_cast<uint32_t *>(dst);
@@ -3382,6 +3371,86 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
     recs[x] = g;
   }
 }
+// n_dev: the slot count on the device (gx_outbox_sizes_async); slots past cap_slots are refused
+__global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t *out, const uint32_t *n_dev = nullptr,
+                              uint32_t cap_slots = 0xffffffffu) {
+  uint32_t i = blockIdx.x;
+  if (n_dev) {
+    n = *n_dev;
+    if (i == 0 && threadIdx.x == 0 && n > cap_slots) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);
+    if (n > cap_slots) n = cap_slots;
+  }
+  if (i >= n) return;
+  const size_t sb = 16 + 16ull * d.p.packet_cap + 16ull * (d.p.fd_enable ? d.p.fd_msg_cap : 0);
+  pack_slot(d, entry[i], out + (size_t)i * sb);
+}
+
+// ------------------------------------------------------------ planned gossip exchange --
+// Packet-slot bounds of the exchange, from the seeded sampler alone (gx_exchange_plan): for every
+// round r of a batch and host u of the cluster, GossipMessages slots per sampled peer on another
+// shard, counted per (shard of u, shard of the peer). Every shard computes the same matrix, so the
+// collective's split sizes are known without waiting for the device.
+#define XPLAN_BATCH 64
+#define XPLAN_GMAX 64
+struct XBound {
+  uint32_t n[XPLAN_GMAX];  // slots this shard sends each shard this round
+};
+GXD uint32_t shard_of_d(const Dev &d, uint32_t v) {
+  uint32_t g = (uint32_t)(((uint64_t)v * d.G) / d.H);
+  while (g > 0 && (uint32_t)(((uint64_t)g * d.H) / d.G) > v) g--;
+  while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= v) g++;
+  return g;
+}
+__global__ __launch_bounds__(256) void k_xplan(Dev d, int64_t r0, uint32_t *cnt) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x, rr = blockIdx.y;
+  if (u >= d.H) return;
+  const int64_t round = r0 + rr;
+  // sample_peers of that round (its partition state)
+  uint32_t base = 0, m = d.H;
+  if (round >= d.p.partition_start && round < d.p.partition_end) {
+    const uint32_t half = d.H / 2;
+    base = u < half ? 0 : half;
+    m = u < half ? half : d.H - half;
+  }
+  if (m < 2) return;
+  const uint64_t h3 = mix64(mix64(mix64(d.p.seed ^ ((uint64_t)ST_PEER * 0xD1B54A32D192ED03ull)) ^ (uint64_t)round) ^ u);
+  const uint32_t want = d.K < m - 1 ? d.K : m - 1, su = shard_of_d(d, u);
+  uint32_t peers[16], c = 0;
+  for (uint32_t at = 0; c < want && at < 64u * d.K; at++) {
+    const uint32_t ix = unif(mix64(h3 ^ at), m - 1), self = u - base;
+    const uint32_t p = base + (ix >= self ? ix + 1 : ix);
+    bool dup = false;
+    for (uint32_t i = 0; i < c; i++) dup |= peers[i] == p;
+    if (!dup) peers[c++] = p;
+  }
+  for (uint32_t i = 0; i < c; i++) {
+    const uint32_t sp = shard_of_d(d, peers[i]);
+    if (sp != su) atomicAdd(&cnt[((size_t)rr * d.G + su) * d.G + sp], d.NG);
+  }
+}
+// Slot i of the planned outbox: destination shard g's region holds bound.n[g] slots, its packets
+// first (ob_fill's entries for g, tot[g] of them), then empty ones (sender key GX_SLOT_EMPTY).
+__global__ void k_outbox_pack_planned(Dev d, const uint32_t *entry, const uint32_t *tot, XBound bound, uint8_t *out) {
+  const uint32_t i = blockIdx.x;
+  uint32_t g = 0, acc = 0, eoff = 0;
+  while (g < d.G && i >= acc + bound.n[g]) {
+    acc += bound.n[g];
+    eoff += tot[g];
+    g++;
+  }
+  if (g >= d.G) return;
+  const uint32_t j = i - acc;
+  const size_t sb = 16 + 16ull * d.p.packet_cap + 16ull * (d.p.fd_enable ? d.p.fd_msg_cap : 0);
+  uint8_t *dst = out + (size_t)i * sb;
+  if (j == 0 && threadIdx.x == 0 && tot[g] > bound.n[g]) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);  // cannot happen
+  if (j < tot[g]) {
+    pack_slot(d, entry[eoff + j], dst);
+  } else if (threadIdx.x == 0) {
+    uint32_t *hdr = reinterpret_cast<uint32_t *>(dst);
+    hdr[0] = GX_SLOT_EMPTY;
+    hdr[1] = hdr[2] = hdr[3] = 0;
+  }
+}
 
 // Inbox: received slots -> message entries [Hl*K, Hl*K + n), registered in the receivers'
 // inboxes. A slot is checked like the oracle's gx_inbox_unpack does: sender key < H*K and its
@@ -3397,6 +3466,7 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   const uint8_t *src = in + (size_t)i * sb;
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(src);
   uint32_t key = hdr[0], dst = hdr[1], len = hdr[2], nfd = fcap ? hdr[3] : 0;
+  if (key == GX_SLOT_EMPTY) return;  // an unused slot of a planned exchange (gx_outbox_pack_planned)
   size_t e = (size_t)d.Hl * d.KE + i;
   const grec *recs = reinterpret_cast<const grec *>(src + 16);
   bool bad = key >= d.H * d.KE || key / d.KE - d.lo < d.Hl || dst - d.lo >= d.Hl || len > d.p.packet_cap ||

@@ -117,10 +117,16 @@ class LocalShards:
         return t.cpu().numpy().astype(np.uint64)
 
     def run_rounds(self, n: int):
+        planned = not self.shards[0].e.params.fd_enable  # sizes from the seeded plan (gx_exchange_plan)
         for _ in range(n):
             for s in self.shards:
                 s.e.round_send()
-            inb = self._exchange(self._outbox_sizes, lambda e, p, c: e.outbox_pack(p, c))
+            if planned:
+                plan = self.shards[0].e.exchange_plan()
+                inb = self._exchange(lambda s: plan[s.e.params.shard_id].copy(),
+                                     lambda e, p, c: e.outbox_pack_planned(p, c))
+            else:
+                inb = self._exchange(self._outbox_sizes, lambda e, p, c: e.outbox_pack(p, c))
             self.wire.packets += int(sum(int(x.sum()) for x in self.last_sizes))
             for s, x in zip(self.shards, inb):
                 s.e.inbox_unpack(_ptr(x), x.numel())
@@ -256,13 +262,45 @@ class DistShard:
         self.s.sync()
         return recv
 
+    def _exchange_planned(self, plan: np.ndarray, packer) -> torch.Tensor:
+        """all-to-all with split sizes every rank knows ahead (gx_exchange_plan): no size collective
+        and no wait on the device."""
+        ss = [int(x) for x in plan[self.rank]]
+        rs = [int(plan[src][self.rank]) for src in range(self.world)]
+        self.last_sizes = np.array(ss, dtype=np.uint64)
+        send = self.s.pack(self.last_sizes, packer)
+        recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
+        calls = (int(plan.max()) + self.CHUNK - 1) // self.CHUNK
+        if calls <= 1:
+            self._a2a(recv, send, rs, ss)
+            return recv
+        soff = np.concatenate([[0], np.cumsum(ss)])
+        roff = np.concatenate([[0], np.cumsum(rs)])
+        for c in range(calls):
+            lo = c * self.CHUNK
+            s_part = [max(0, min(self.CHUNK, n - lo)) for n in ss]
+            r_part = [max(0, min(self.CHUNK, n - lo)) for n in rs]
+            s_buf = torch.cat([send[int(soff[p]) + lo:int(soff[p]) + lo + s_part[p]] for p in range(self.world)])
+            r_buf = torch.empty(sum(r_part), dtype=torch.uint8, device=self.device)
+            self._a2a(r_buf, s_buf, r_part, s_part)
+            o = 0
+            for p in range(self.world):
+                if r_part[p]:
+                    recv[int(roff[p]) + lo:int(roff[p]) + lo + r_part[p]].copy_(r_buf[o:o + r_part[p]])
+                o += r_part[p]
+        return recv
+
     def run_rounds(self, n: int):
         e = self.e
+        planned = not e.params.fd_enable  # sizes from the seeded plan: no host wait in gossip rounds
         for _ in range(n):
             e.round_send()
-            ob = torch.zeros(self.world, dtype=torch.int64, device=self.device)
-            e.outbox_sizes_async(_ptr(ob))  # no host wait: the sizes join the size all-gather
-            x = self._exchange(ob, e.outbox_pack)
+            if planned:
+                x = self._exchange_planned(e.exchange_plan(), e.outbox_pack_planned)
+            else:
+                ob = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+                e.outbox_sizes_async(_ptr(ob))  # no host wait: the sizes join the size all-gather
+                x = self._exchange(ob, e.outbox_pack)
             self.wire.packets += int(self.last_sizes.sum())
             e.inbox_unpack(_ptr(x), x.numel())
             e.round_merge()

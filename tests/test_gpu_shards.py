@@ -81,7 +81,14 @@ def test_gpu_distshard_rccl_world1(gx_lib):
         kw = SCEN["storm"]
         sh = DistShard(gx_lib, 0, 1, "cuda:0", **kw)
         whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
-        sh.run_rounds(25)
+        sh.run_rounds(11)
+        torch.cuda.synchronize()
+        torch.cuda.set_sync_debug_mode("error")  # gossip rounds 11..19: no wait on the device
+        try:
+            sh.run_rounds(9)
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+        sh.run_rounds(5)
         whole.run_rounds(25)
         assert sh.stats() == whole.stats()
         assert sh.converged() == whole.converged()
@@ -126,3 +133,29 @@ def test_gpu_eight_shards_cfg5_schedule(gx_lib, oracle_lib):
         assert_sharded_equal(orc, sh, f"cfg5@2048 G=8 round {whole.round} vs oracle")
     w = sh.wire.as_dict()
     assert w["packets"] > 0 and w["ae_lead"] > 0 and w["ae_delta"] < w["ae_full_rows_equivalent"]
+
+
+def test_gpu_planned_exchange_sync_free(gx_lib, oracle_lib):
+    """The sharded gossip round with the planned exchange (gx_exchange_plan: split sizes from the
+    seeded sampler, empty slots padded) queues a stretch of gossip-only rounds without any torch
+    call that waits on the device (torch.cuda.set_sync_debug_mode("error")), and stays
+    bit-identical to the unsharded engine and the oracle: 4 shards on the cfg 5 schedule at H = 512
+    (partition, storm at round 5, rounds 11..19 between two push-pull rounds)."""
+    import torch
+    kw = dict(CFG5_H2048, n_hosts=512)
+    whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    orc = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    sh = LocalShards(gx_lib, 4, device="cuda:0", **kw)
+    sh.run_rounds(11)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        sh.run_rounds(9)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    sh.run_rounds(40)  # the heal and the post-heal push-pull rounds
+    whole.run_rounds(60)
+    orc.run_rounds(60)
+    assert_sharded_equal(whole, sh, "planned exchange, round 60")
+    assert_sharded_equal(orc, sh, "planned exchange vs oracle, round 60")
+    assert sh.wire.as_dict()["packets"] > 0
