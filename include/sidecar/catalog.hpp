@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <functional>
 #include <map>
 #include <optional>
@@ -30,17 +31,117 @@ namespace sidecar {
 enum Status { ALIVE = GX_ALIVE, TOMBSTONE = GX_TOMBSTONE, UNHEALTHY = GX_UNHEALTHY, UNKNOWN = GX_UNKNOWN,
               DRAINING = GX_DRAINING };
 
+struct Port {  // service.Port (service/service.go:25-30)
+  std::string Type;
+  int64_t Port = 0;
+  int64_t ServicePort = 0;
+  std::string IP;
+};
+
 struct Service {
   std::string ID;
   std::string Hostname;
   int64_t Updated = 0;
   int Status = ALIVE;
-  std::string Name;  // Service.Name (ByService groups by it); not part of the merge path
+  // metadata the merge path does not read: ByService groups by Name; Encode() writes them all
+  std::string Name;
+  std::string Image;
+  int64_t Created = 0;     // UTC ns
+  std::vector<Port> Ports;
+  std::string ProxyMode;
   bool IsTombstone() const { return Status == TOMBSTONE; }
   bool operator==(const Service &o) const {
-    return ID == o.ID && Hostname == o.Hostname && Updated == o.Updated && Status == o.Status;  // Name: metadata
+    return ID == o.ID && Hostname == o.Hostname && Updated == o.Updated && Status == o.Status;  // the rest: metadata
   }
 };
+
+// ---- the reference's JSON for a Service (service/service_ffjson.go:370-436), as the engine's
+// full-state codec needs it: the bytes before and after the Updated value (gx.h gx_names).
+namespace json {
+// encoding/json string encoding with HTML escaping (Go 1.13 encodeState.string, escapeHTML=true)
+inline std::string quote(const std::string &in) {
+  static const char *hex = "0123456789abcdef";
+  std::string out = "\"";
+  const unsigned char *b = reinterpret_cast<const unsigned char *>(in.data());
+  const size_t n = in.size();
+  for (size_t i = 0; i < n;) {
+    const unsigned c = b[i];
+    if (c < 0x80) {
+      if (c >= 0x20 && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&') out += (char)c;
+      else if (c == '"' || c == '\\') (out += '\\') += (char)c;
+      else if (c == '\n') out += "\\n";
+      else if (c == '\r') out += "\\r";
+      else if (c == '\t') out += "\\t";
+      else ((out += "\\u00") += hex[c >> 4]) += hex[c & 15];
+      i++;
+      continue;
+    }
+    // utf8.DecodeRune: an invalid sequence is one byte of U+FFFD
+    uint32_t r = 0xFFFD, sz = 1;
+    auto cont = [&](size_t k) { return i + k < n && (b[i + k] & 0xC0) == 0x80; };
+    if (c >= 0xC2 && c <= 0xDF && cont(1)) {
+      r = ((c & 0x1Fu) << 6) | (b[i + 1] & 0x3Fu);
+      sz = 2;
+    } else if (c >= 0xE0 && c <= 0xEF && cont(1) && cont(2)) {
+      const uint32_t x = ((c & 0x0Fu) << 12) | ((b[i + 1] & 0x3Fu) << 6) | (b[i + 2] & 0x3Fu);
+      if (x >= 0x800 && !(x >= 0xD800 && x <= 0xDFFF)) r = x, sz = 3;
+    } else if (c >= 0xF0 && c <= 0xF4 && cont(1) && cont(2) && cont(3)) {
+      const uint32_t x = ((c & 0x07u) << 18) | ((b[i + 1] & 0x3Fu) << 12) | ((b[i + 2] & 0x3Fu) << 6) | (b[i + 3] & 0x3Fu);
+      if (x >= 0x10000 && x <= 0x10FFFF) r = x, sz = 4;
+    }
+    if (r == 0xFFFD && sz == 1) out += "\\ufffd";
+    else if (r == 0x2028) out += "\\u2028";
+    else if (r == 0x2029) out += "\\u2029";
+    else out.append(in, i, sz);
+    i += sz;
+  }
+  return out + "\"";
+}
+// time.Time.MarshalJSON of a UTC instant: quoted RFC3339Nano, fraction without trailing zeros
+inline std::string time(int64_t ns) {
+  int64_t secs = ns / 1000000000, frac = ns % 1000000000;
+  if (frac < 0) frac += 1000000000, secs--;
+  int64_t days = secs / 86400, rem = secs % 86400;
+  if (rem < 0) rem += 86400, days--;
+  // civil_from_days (proleptic Gregorian)
+  const int64_t z = days + 719468, era = (z >= 0 ? z : z - 146096) / 146097;
+  const int64_t doe = z - era * 146097, yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100), mp = (5 * doy + 2) / 153;
+  const int64_t d = doy - (153 * mp + 2) / 5 + 1, m = mp < 10 ? mp + 3 : mp - 9, y = yoe + era * 400 + (m <= 2);
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%04lld-%02lld-%02lldT%02lld:%02lld:%02lld", (long long)y, (long long)m, (long long)d,
+                (long long)(rem / 3600), (long long)(rem / 60 % 60), (long long)(rem % 60));
+  std::string s = std::string("\"") + buf;
+  if (frac) {
+    char f[16];
+    std::snprintf(f, sizeof f, ".%09lld", (long long)frac);
+    std::string fs = f;
+    while (fs.back() == '0') fs.pop_back();
+    s += fs;
+  }
+  return s + "Z\"";
+}
+// (pre, post) of svc's JSON around its Updated value: {"ID":..,"Name":..,"Image":..,"Created":..,
+// "Hostname":..,"Ports":..,"Updated":  and  ,"ProxyMode":..,"Status":
+inline std::pair<std::string, std::string> fragments(const Service &svc) {
+  std::string ports = "null";
+  if (!svc.Ports.empty()) {
+    ports = "[";
+    for (size_t i = 0; i < svc.Ports.size(); i++) {
+      const Port &p = svc.Ports[i];
+      if (i) ports += ",";
+      ports += "{\"Type\":" + quote(p.Type) + ",\"Port\":" + std::to_string(p.Port) + ",\"ServicePort\":" +
+               std::to_string(p.ServicePort) + ",\"IP\":" + quote(p.IP) + "}";
+    }
+    ports += "]";
+  }
+  std::string pre = "{\"ID\":" + quote(svc.ID) + ",\"Name\":" + quote(svc.Name) + ",\"Image\":" + quote(svc.Image) +
+                    ",\"Created\":" + time(svc.Created) + ",\"Hostname\":" + quote(svc.Hostname) + ",\"Ports\":" +
+                    ports + ",\"Updated\":";
+  std::string post = ",\"ProxyMode\":" + quote(svc.ProxyMode) + ",\"Status\":";
+  return {pre, post};
+}
+}  // namespace json
 
 // catalog.ChangeEvent (services_state.go:38-43)
 struct ChangeEvent {
@@ -143,6 +244,7 @@ class Cluster {
       id_names_[host][s] = id;
       const uint64_t key = (uint64_t)host * p_.n_services + s;
       if (names_.erase(key)) names_dirty_ = true;
+      if (last_.erase(key)) codec_dirty_ = true;
       auto st = static_.find(host);
       if (st != static_.end() && st->second[s] != (uint16_t)GX_STATIC_BYTES_DEFAULT) {
         st->second[s] = (uint16_t)GX_STATIC_BYTES_DEFAULT;
@@ -165,6 +267,12 @@ class Cluster {
     r.updated_ns = svc.Updated;
     r.host = h;
     r.svc = Id(h, svc.ID);
+    {
+      const uint64_t key = (uint64_t)h * p_.n_services + r.svc;
+      auto it = last_.find(key);
+      if (it == last_.end() || !SameMeta(it->second, svc)) codec_dirty_ = true;
+      last_[key] = svc;
+    }
     auto &since = slot_free_since_[h];
     if (r.svc < since.size() && since[r.svc] >= 0 &&
         svc.Updated >= Now() - p_.tombstone_lifespan_ns - p_.stale_fudge_ns)  // not IsStale: may be stored
@@ -181,7 +289,64 @@ class Cluster {
     s.Status = r.status;
     auto it = names_.find((uint64_t)r.host * p_.n_services + r.svc);
     if (it != names_.end()) s.Name = it->second;
+    auto lt = last_.find((uint64_t)r.host * p_.n_services + r.svc);
+    if (lt != last_.end() && lt->second.ID == s.ID) {  // the metadata last seen for the record
+      s.Image = lt->second.Image;
+      s.Created = lt->second.Created;
+      s.Ports = lt->second.Ports;
+      s.ProxyMode = lt->second.ProxyMode;
+      if (s.Name.empty()) s.Name = lt->second.Name;
+    }
     return s;
+  }
+  static bool SameMeta(const Service &a, const Service &b) {
+    bool ports = a.Ports.size() == b.Ports.size();
+    for (size_t i = 0; ports && i < a.Ports.size(); i++)
+      ports = a.Ports[i].Type == b.Ports[i].Type && a.Ports[i].Port == b.Ports[i].Port &&
+              a.Ports[i].ServicePort == b.Ports[i].ServicePort && a.Ports[i].IP == b.Ports[i].IP;
+    return ports && a.ID == b.ID && a.Hostname == b.Hostname && a.Name == b.Name && a.Image == b.Image &&
+           a.Created == b.Created && a.ProxyMode == b.ProxyMode;
+  }
+  // Hands the engine the full-state codec's names (gx_set_names) when a record's metadata changed:
+  // every host's name and every record's ID and JSON fragments (records never seen get placeholder
+  // names the reference could not produce, so a peer's document never matches them).
+  void SyncCodec(const std::string &cluster = "default") {
+    if (!codec_dirty_ && cluster == codec_cluster_) return;
+    const uint32_t H = p_.n_hosts, S = p_.n_services;
+    std::string hosts, ids, pre, post;
+    std::vector<uint64_t> ho(H + 1, 0), io((size_t)H * S + 1, 0), po((size_t)H * S + 1, 0), qo((size_t)H * S + 1, 0);
+    for (uint32_t h = 0; h < H; h++) {
+      hosts += h < host_names_.size() ? host_names_[h] : "\x01unused-host-" + std::to_string(h);
+      ho[h + 1] = hosts.size();
+      for (uint32_t j = 0; j < S; j++) {
+        const uint64_t k = (uint64_t)h * S + j;
+        Service svc;
+        auto it = last_.find(k);
+        if (it != last_.end()) svc = it->second;
+        else svc.ID = "\x01unused-" + std::to_string(k), svc.Hostname = h < host_names_.size() ? host_names_[h] : "";
+        const auto fr = json::fragments(svc);
+        ids += svc.ID;
+        pre += fr.first;
+        post += fr.second;
+        io[k + 1] = ids.size();
+        po[k + 1] = pre.size();
+        qo[k + 1] = post.size();
+      }
+    }
+    gx_names n{};
+    n.cluster_name = cluster.data();
+    n.cluster_name_len = cluster.size();
+    n.hosts = hosts.data();
+    n.host_off = ho.data();
+    n.ids = ids.data();
+    n.id_off = io.data();
+    n.pre = pre.data();
+    n.pre_off = po.data();
+    n.post = post.data();
+    n.post_off = qo.data();
+    check(gx_set_names(e_, &n), "gx_set_names");
+    codec_dirty_ = false;
+    codec_cluster_ = cluster;
   }
   // Hands the engine the Service.Name of every record (gx_set_service_names) when one changed.
   void SyncNames() {
@@ -227,6 +392,9 @@ class Cluster {
   std::map<uint32_t, std::vector<uint16_t>> static_;
   std::map<uint64_t, std::string> names_;  // record key -> Service.Name
   bool names_dirty_ = false;
+  std::map<uint64_t, Service> last_;       // record key -> the last full Service seen (codec metadata)
+  bool codec_dirty_ = true;
+  std::string codec_cluster_;
 };
 
 namespace catalog {
@@ -242,8 +410,28 @@ class ServicesState {
     uint32_t v = self_;
     check(gx_add_service_entries(c_.engine(), &v, &r, 1, nullptr), "AddServiceEntry");
   }
-  // Merge (services_state.go:367-373)
+  // Merge (services_state.go:367-373): another view of the same cluster
   void Merge(const ServicesState &other) { check(gx_merge(c_.engine(), self_, other.self_), "Merge"); }
+  // Merge(otherState) with a state decoded from another node (catalog::Decode): AddServiceEntry of
+  // each of its services in key order (services_state.go:367-373)
+  void Merge(const std::vector<Service> &otherState) {
+    std::vector<gx_service> rs;
+    for (auto &svc : otherState) rs.push_back(c_.Rec(svc));
+    if (!rs.empty())
+      check(gx_merge_remote_state(c_.engine(), self_, rs.data(), (uint32_t)rs.size()), "Merge");
+  }
+  // UpdateService (services_state.go:137-140): the update reaches AddServiceEntry through the
+  // ServiceMsgs loop (:129-135); here it is applied at once
+  void UpdateService(const Service &svc) { AddServiceEntry(svc); }
+  // Encode (services_state.go:115-125): the view's ServicesState JSON, the reference's bytes
+  std::string Encode(const std::string &clusterName = "default") {
+    c_.SyncCodec(clusterName);
+    uint64_t n = 0;
+    check(gx_local_state_json(c_.engine(), self_, nullptr, 0, &n), "Encode");
+    std::string out(n, '\0');
+    check(gx_local_state_json(c_.engine(), self_, n ? &out[0] : nullptr, n, &n), "Encode");
+    return out;
+  }
   // ExpireServer (services_state.go:150-192)
   void ExpireServer(const std::string &hostname) {
     check(gx_expire_server(c_.engine(), self_, c_.Host(hostname), nullptr), "ExpireServer");
@@ -406,6 +594,25 @@ class ServicesState {
  private:
   uint32_t self_;
 };
+
+// catalog.Decode (services_state.go:774-782): the services of a ServicesState JSON, document order.
+// ok = false where the reference's UnmarshalJSON fails ("Decode() returns an error when handed
+// junk", services_state_test.go:109-114); the services are then empty.
+inline std::vector<Service> Decode(Cluster &c, const std::string &data, bool *ok = nullptr) {
+  c.SyncCodec();
+  std::vector<gx_service> out(64);
+  uint32_t n = 0;
+  gx_decode_stats ds{};
+  int rc = gx_decode_state_json(c.engine(), data.data(), data.size(), out.data(), (uint32_t)out.size(), &n, &ds);
+  if (rc == GX_OK && n > out.size()) {
+    out.resize(n);
+    rc = gx_decode_state_json(c.engine(), data.data(), data.size(), out.data(), n, &n, &ds);
+  }
+  if (ok) *ok = rc == GX_OK;
+  if (rc != GX_OK) return {};
+  out.resize(n);
+  return c.Svcs(out);
+}
 
 }  // namespace catalog
 

@@ -446,6 +446,84 @@ static void test_slot_reuse() {
   }
 }
 
+// Encode / Decode / Merge(decoded state) / UpdateService (services_state_test.go:102-115, :299-308;
+// services_state.go:115-140, 367-373, 774-782). The expected Service bytes are the Python codec's
+// (sidecar_amd/codec.py service_json, pinned to the services_delegate_test.go:15-20 records).
+static std::string full_json(const Service &s) {
+  auto fr = sidecar::json::fragments(s);
+  return fr.first + sidecar::json::time(s.Updated) + fr.second + std::to_string(s.Status) + "}";
+}
+static void test_codec() {
+  {
+    cur = "Service JSON: ffjson field order, HTML-escaped strings, RFC3339Nano";
+    Service a{"deadbeef123", "chaucer", 1700000000000000000ll, sidecar::TOMBSTONE, "web<1>", "img:1",
+              1425431552630357657ll, {{"tcp", 8080, 10001, "192.168.1.1"}, {"udp", 53, 0, ""}}, "http"};
+    So(full_json(a) ==
+       "{\"ID\":\"deadbeef123\",\"Name\":\"web\\u003c1\\u003e\",\"Image\":\"img:1\",\"Created\":"
+       "\"2015-03-04T01:12:32.630357657Z\",\"Hostname\":\"chaucer\",\"Ports\":[{\"Type\":\"tcp\",\"Port\":8080,"
+       "\"ServicePort\":10001,\"IP\":\"192.168.1.1\"},{\"Type\":\"udp\",\"Port\":53,\"ServicePort\":0,\"IP\":\"\"}],"
+       "\"Updated\":\"2023-11-14T22:13:20Z\",\"ProxyMode\":\"http\",\"Status\":1}");
+    Service b{"x\xe2\x80\xa8\xc3\xa9", "h", 1700000000123000000ll, sidecar::UNHEALTHY};
+    So(full_json(b) ==
+       "{\"ID\":\"x\\u2028\xc3\xa9\",\"Name\":\"\",\"Image\":\"\",\"Created\":\"1970-01-01T00:00:00Z\",\"Hostname\":"
+       "\"h\",\"Ports\":null,\"Updated\":\"2023-11-14T22:13:20.123Z\",\"ProxyMode\":\"\",\"Status\":2}");
+    Service c{"a\x01\"b\\", "h\xc3\xbf", 1, sidecar::ALIVE, "n"};
+    c.Created = -1;
+    So(full_json(c) ==
+       "{\"ID\":\"a\\u0001\\\"b\\\\\",\"Name\":\"n\",\"Image\":\"\",\"Created\":\"1969-12-31T23:59:59.999999999Z\","
+       "\"Hostname\":\"h\xc3\xbf\",\"Ports\":null,\"Updated\":\"1970-01-01T00:00:00.000000001Z\",\"ProxyMode\":\"\","
+       "\"Status\":0}");
+    So(sidecar::json::quote("\xff") == "\"\\ufffd\"");
+  }
+  {
+    cur = "Encode() generates JSON that we can Decode() (:102-107)";
+    Cluster c(params());
+    ServicesState state(c, hostname);
+    Service svc{"deadbeef123", hostname, c.Now(), sidecar::ALIVE, "web", "img"};
+    state.AddServiceEntry(svc);
+    std::string enc = state.Encode();
+    So(enc.rfind("{\"Servers\":{\"shakespeare\":{\"Name\":\"shakespeare\",\"Services\":{\"deadbeef123\":", 0) == 0);
+    So(enc.find(full_json(svc)) != std::string::npos);
+    bool ok = false;
+    auto decoded = sidecar::catalog::Decode(c, enc, &ok);
+    So(ok && decoded.size() == 1 && decoded[0] == svc && decoded[0].Hostname == hostname);
+    So(decoded.size() == 1 && decoded[0].Name == "web" && decoded[0].Image == "img");
+  }
+  {
+    cur = "Decode() returns an error when handed junk (:109-114)";
+    Cluster c(params());
+    ServicesState state(c, hostname);
+    state.AddServiceEntry(Service{"deadbeef123", hostname, c.Now(), sidecar::ALIVE});
+    bool ok = true;
+    auto decoded = sidecar::catalog::Decode(c, "asdf", &ok);
+    So(!ok && decoded.empty());
+  }
+  {
+    cur = "Merge() of a decoded remote state (:299-308 through Encode/Decode)";
+    Cluster c(params());
+    ServicesState firstState(c, "first"), secondState(c, "second");
+    firstState.AddServiceEntry(Service{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE});
+    firstState.AddServiceEntry(Service{"cafe", hostname, c.Now(), sidecar::DRAINING});
+    auto other = sidecar::catalog::Decode(c, firstState.Encode());
+    So(other.size() == 2);
+    secondState.Merge(other);
+    So(secondState.EachService() == firstState.EachService());
+  }
+  {
+    cur = "UpdateService() reaches AddServiceEntry (services_state.go:129-140)";
+    Cluster c(params());
+    ServicesState state(c, local);
+    Service svc{"deadbeef123", anotherHostname, c.Now(), sidecar::ALIVE};
+    state.UpdateService(svc);
+    So(state.Get(anotherHostname, svc.ID).has_value());
+    c.Advance(1);
+    svc.Status = sidecar::TOMBSTONE;
+    svc.Updated = c.Now();
+    state.UpdateService(svc);
+    So(state.Get(anotherHostname, svc.ID)->Status == sidecar::TOMBSTONE);
+  }
+}
+
 int main() {
   test_slot_reuse();
   test_view_sorting();
@@ -455,6 +533,7 @@ int main() {
   test_get_broadcasts();
   test_get_broadcasts_bytes();
   test_change_bookkeeping();
+  test_codec();
   std::printf("backend=%s checks=%d failures=%d\n", gx_backend(), checks, failures);
   return failures ? 1 : 0;
 }
