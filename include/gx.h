@@ -197,8 +197,9 @@ typedef struct gx_params {
    * takes part in 1 + (number of initiators that drew it) exchanges, as with memberlist's
    * per-node timers. Both sides of an exchange merge the other's round-start state. */
   uint32_t push_pull_mode;
-  /* Engine bound (no reference counterpart): inbox slots per receiver, 1..64 (0 = 64). A receiver
-   * with more packets in a round takes the serial overflow path; results are identical. */
+  /* Engine bound (no reference counterpart): inbox slots per receiver, 1..256 (0 = 64, or 256 with
+   * gossip_messages > 1). A receiver with more packets in a round takes the serial overflow path;
+   * results are identical. */
   uint32_t inbox_slots;
 } gx_params;
 #define GX_PP_MATCHING 0

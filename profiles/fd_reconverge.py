@@ -3,7 +3,9 @@ with memberlist's detector, then the heal. Prints, every `step` rounds, the memb
 that disagree with the truth (gx_fd_converged), the deaths / refutations so far, and the
 catalogs' disagreeing records.
 
-  python profiles/fd_reconverge.py [H] [rounds] [partition_end] [step] [oracle]
+  python profiles/fd_reconverge.py [H] [rounds] [partition_end] [step] [oracle|gpu] [gossip_messages]
+
+gossip_messages 15 is Sidecar's default (config/config.go:46); the bench's cfg5fd runs 1.
 """
 import json
 import os
@@ -25,9 +27,11 @@ if len(sys.argv) > 5 and sys.argv[5] == "oracle":
 else:
     lib = load_product()
 kw = dict(bench.CONFIGS["cfg5fd"]["p"], n_hosts=H, partition_end=pe)
+if len(sys.argv) > 6:
+    kw["gossip_messages"] = int(sys.argv[6])
 e = Engine(default_params(lib, **kw), lib=lib)
 p = e.params
-print(json.dumps({"H": H, "partition_end": pe, "suspicion_rounds": list(p.fd_suspicion_rounds[:p.fd_suspicion_k + 1]),
+print(json.dumps({"H": H, "partition_end": pe, "gossip_messages": kw.get("gossip_messages", 1), "suspicion_rounds": list(p.fd_suspicion_rounds[:p.fd_suspicion_k + 1]),
                   "retransmit_limit": p.fd_retransmit_limit, "gossip_dead_rounds": p.fd_gossip_dead_rounds}),
       flush=True)
 t = time.time()

@@ -9,7 +9,7 @@ import csv
 import statistics
 import sys
 
-GOSSIP = ("k_owner", "k_scan", "k_bt_finish", "k_send", "k_merge_lean", "k_merge")
+GOSSIP = ("k_owner", "k_scan", "k_bt_finish", "k_send", "k_merge_lean", "k_merge", "k_merge_seg")
 rows = list(csv.DictReader(open(sys.argv[1])))
 skip = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 ks = []
@@ -20,7 +20,7 @@ ks.sort()
 rounds, cur = [], None
 for s, e, n in ks:
     # a round starts at k_owner, or at k_send when the owner ticks run inside it (fused launch)
-    if n == "k_owner" or (n == "k_send" and (cur is None or any(x[2] in ("k_merge", "k_merge_lean") for x in cur))):
+    if n == "k_owner" or (n == "k_send" and (cur is None or any(x[2] in ("k_merge", "k_merge_lean", "k_merge_seg") for x in cur))):
         cur = []
         rounds.append(cur)
     if cur is not None and n in GOSSIP:

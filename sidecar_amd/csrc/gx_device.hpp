@@ -81,6 +81,9 @@ enum {
 #define GX_NCTR_SLOTS 48
 
 #define GX_SHARDS 64
+// inbox slots per receiver, upper bound (gx_params.inbox_slots): the wave merge ranks up to this
+// many headers in LDS; with GossipMessages > 1 the default (256) holds 17 senders' 15 packets
+#define GX_DI_MAX 256
 struct DevCtr {
   unsigned long long c[GX_SHARDS][GX_NCTR_SLOTS];   // counter shards (shard = block % 64)
   unsigned long long last_change_p1[GX_SHARDS][8];  // last round with a slot change + 1
@@ -118,7 +121,7 @@ struct Dev {
   uint32_t *msg_dst;
   // Receiver inboxes: a sender registers each packet straight into its receiver's
   // inbox with one atomic; the merge sorts a receiver's few headers by global sender key itself.
-  uint32_t DI;         // inbox slots per receiver (<= 64); packets past them go to the overflow list
+  uint32_t DI;         // inbox slots per receiver (<= GX_DI_MAX); packets past them go to the overflow list
   uint32_t DR;         // inbox slots whose records are stored inline (in_rec); the rest stay in msg
   // Per-round counters come in two buffers by round parity (set_round_fields): this round's, and
   // the next round's, which this round's owner phase zeroes (nothing reads it during this round),

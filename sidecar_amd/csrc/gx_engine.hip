@@ -720,7 +720,7 @@ static int check_params(const gx_params *p) {
   if (p->gossip_messages > 16 || (p->gossip_messages > 1 && p->fd_enable)) return GX_EINVAL;
   if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
     return GX_EINVAL;
-  if (p->inbox_slots > 64) return GX_EINVAL;
+  if (p->inbox_slots > GX_DI_MAX) return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -884,7 +884,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.msg_key, sizeof(uint32_t) * Hg * K);
   ALLOC(e->in_cnt_buf, sizeof(uint32_t) * 2 * H);
   d.nblk_ae = (d.R + GX_DIGEST_SLOTS - 1) / GX_DIGEST_SLOTS;
-  d.DI = p->inbox_slots ? p->inbox_slots : 64;
+  // default: 64 slots; with GossipMessages > 1 (up to NG packets per sender) GX_DI_MAX, so the
+  // wave merge takes the wide inboxes instead of the serial overflow path
+  d.DI = p->inbox_slots ? p->inbox_slots : (d.NG > 1 ? GX_DI_MAX : 64);
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
   d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
   if (d.ab) fprintf(stderr, "gx: GX_AB_FLAGS=%u: A/B measurement kernel paths active\n", d.ab);

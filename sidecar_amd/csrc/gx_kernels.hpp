@@ -1625,7 +1625,8 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
 #define MERGE_WAVES 4
 #define MERGE_RANGE_DEF 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
 struct MergeLds {  // one wave's staging for one receiver at a time
-  uint4 hdr[64];
+  uint4 hdr[GX_DI_MAX];     // headers in sender order (inboxes of more than 64 packets use all of it)
+  uint32_t pst[GX_DI_MAX];  // wide inboxes: keys while ranking, then each packet's first record index
   uint64_t accw[64];
   uint8_t accf[64], chg[64], prev[64];
 };
@@ -1645,21 +1646,72 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     if (lane == 0) merge_inbox_serial(d, vi);
     return;
   }
-  if (deg > npre && lane >= npre && lane < deg) hd = d.in_hdr[(size_t)vi * d.DI + lane];
-  // sender order: rank of each header's key among the deg distinct keys
-  const uint32_t hkey = lane < deg ? hd.x : 0xffffffffu;
-  uint32_t hrank = 0;  // ties (refused by k_inbox_unpack) broken by lane: every rank is written once
-  for (uint32_t j = 0; j < deg; j++) hrank += rdl(hkey, j) < hkey || (rdl(hkey, j) == hkey && j < lane);
-  if (lane < deg) s_hdr[hrank] = hd;
-  wave_sync();
-  const uint4 sh = lane < deg ? s_hdr[lane] : make_uint4(0u, 0u, 0u, 0u);  // {key, entry, len, slot} of packet `lane`
-  uint32_t incl = sh.z;
+  // wide inbox (more than 64 packets, GossipMessages > 1): the headers are ranked and staged in
+  // LDS, with each packet's first record index beside them; the fold below reads both from there
+  const bool wide = deg > 64;
+  uint4 sh = make_uint4(0u, 0u, 0u, 0u);  // {key, entry, len, slot} of packet `lane` (deg <= 64)
+  uint32_t pstart = 0, total = 0;
+  if (!wide) {
+    if (deg > npre && lane >= npre && lane < deg) hd = d.in_hdr[(size_t)vi * d.DI + lane];
+    // sender order: rank of each header's key among the deg distinct keys
+    const uint32_t hkey = lane < deg ? hd.x : 0xffffffffu;
+    uint32_t hrank = 0;  // ties (refused by k_inbox_unpack) broken by lane: every rank is written once
+    for (uint32_t j = 0; j < deg; j++) hrank += rdl(hkey, j) < hkey || (rdl(hkey, j) == hkey && j < lane);
+    if (lane < deg) s_hdr[hrank] = hd;
+    wave_sync();
+    sh = lane < deg ? s_hdr[lane] : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t incl = sh.z;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(incl, o, 64);
-    if ((int)lane >= o) incl += y;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t y = __shfl_up(incl, o, 64);
+      if ((int)lane >= o) incl += y;
+    }
+    pstart = incl - sh.z;
+    total = __shfl(incl, 63, 64);
+  } else {
+    constexpr int HPL = GX_DI_MAX / 64;  // headers per lane
+    uint4 hw[HPL];
+#pragma unroll
+    for (int c = 0; c < HPL; c++) {  // every header in one round trip
+      const uint32_t j = lane + 64u * c;
+      hw[c] = j < deg ? (j < npre ? hd : d.in_hdr[(size_t)vi * d.DI + j]) : make_uint4(0u, 0u, 0u, 0u);
+      if (j < deg) L.pst[j] = hw[c].x;
+    }
+    wave_sync();
+    uint32_t rk[HPL];
+#pragma unroll
+    for (int c = 0; c < HPL; c++) rk[c] = 0;
+    for (uint32_t j = 0; j < deg; j++) {  // rank by key, ties by arrival index (broadcast LDS reads)
+      const uint32_t kj = L.pst[j];
+#pragma unroll
+      for (int c = 0; c < HPL; c++) {
+        const uint32_t me = lane + 64u * c;
+        rk[c] += kj < hw[c].x || (kj == hw[c].x && j < me);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < HPL; c++)
+      if (lane + 64u * c < deg) s_hdr[rk[c]] = hw[c];
+    wave_sync();
+    for (uint32_t c0 = 0; c0 < deg; c0 += 64) {  // first record index of every packet, in sender order
+      const uint32_t j = c0 + lane;
+      const uint32_t ln = j < deg ? s_hdr[j].z : 0u;
+      uint32_t incl = ln;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += y;
+      }
+      if (j < deg) L.pst[j] = total + incl - ln;
+      total += __shfl(incl, 63, 64);
+    }
+    wave_sync();
   }
-  const uint32_t pstart = incl - sh.z, total = __shfl(incl, 63, 64);
+  // packet k's first record index, length, message entry and record slot (k wave-uniform)
+  auto p_start = [&](uint32_t k) -> uint32_t { return wide ? L.pst[k] : rdl(pstart, k); };
+  auto p_len = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].z : rdl(sh.z, k); };
+  auto p_entry = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].y : rdl(sh.y, k); };
+  auto p_slot = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].w : rdl(sh.w, k); };
   const uint32_t vtick = d.tick[vi];
   gx_host_state *h = &d.hs[vi];
   const uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
@@ -1676,7 +1728,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
   for (uint32_t t0 = 0; t0 < total; t0 += 64) {
     const uint32_t i = t0 + lane;
     const bool valid = i < total;
-    while (kc < deg && rdl(pstart, kc) + rdl(sh.z, kc) <= t0) kc++;
+    while (kc < deg && p_start(kc) + p_len(kc) <= t0) kc++;
     grec g;
     g.w = 0;
     g.r = INV;
@@ -1684,13 +1736,14 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     uint64_t fw0 = 0;
     uint32_t fslot = 0;
     for (uint32_t k = kc; k < deg; k++) {  // hop 2: one predicated load per overlapping packet
-      const uint32_t st = rdl(pstart, k);
+      const uint32_t st = p_start(k);
       if (st >= t0 + 64) break;
       const uint32_t off = i - st;
-      if (off < rdl(sh.z, k)) {
-        fslot = rdl(sh.w, k);
-        g = packet_recs(d, vi, fslot, rdl(sh.y, k))[off];
-        if (fslot == GX_NOSLOT_W0) fw0 = d.msg_w0[(size_t)rdl(sh.y, k) * d.p.packet_cap + off];
+      if (off < p_len(k)) {
+        fslot = p_slot(k);
+        const uint32_t en = p_entry(k);
+        g = packet_recs(d, vi, fslot, en)[off];
+        if (fslot == GX_NOSLOT_W0) fw0 = d.msg_w0[(size_t)en * d.p.packet_cap + off];
       }
     }
     uint32_t key = INV;

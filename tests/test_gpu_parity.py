@@ -62,6 +62,14 @@ SCENARIOS = {
     # many chunks per host: GossipMessages 16 with 3-record packets
     "plan_gm16_cap3": dict(n_hosts=50, n_services=8, init_mode=INIT_OWN, gossip_messages=16, packet_cap=3,
                            pending_cap=9, churn_ppm=60000, queue_cap=1024, ae_period_rounds=12),
+    # wide inboxes (65..256 packets per receiver, the default 256 slots with GossipMessages > 1): the
+    # wave merge ranks the headers in LDS; receivers past the slots still take the serial path
+    "wide_inbox_gm15_storm": dict(n_hosts=96, n_services=8, init_mode=INIT_WARM, fanout=8, gossip_messages=15,
+                                  packet_cap=4, partition_start=0, partition_end=12, storm_round=2,
+                                  queue_cap=2048, churn_ppm=50000, ae_period_rounds=10),
+    "wide_inbox_slots100": dict(n_hosts=80, n_services=4, init_mode=INIT_OWN, fanout=10, gossip_messages=12,
+                                packet_cap=3, inbox_slots=100, churn_ppm=80000, queue_cap=1024,
+                                ae_period_rounds=9),
     # memberlist's per-node push-pull initiation (every live host starts one exchange per interval)
     "pp_initiate": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, push_pull_mode=1, ae_period_rounds=5,
                         churn_ppm=30000),
@@ -96,6 +104,7 @@ LISTEN = {  # scenario -> [(view, listener id, capacity)]
     "inbox_overflow": [(0, 1, 4096), (5, 2, 60)],
     "pp_initiate": [(0, 1, 4096), (9, 1, 100)],
     "gossip_messages15": [(2, 1, 4096)],
+    "wide_inbox_gm15_storm": [(0, 1, 4096), (50, 1, 200)],
 }
 
 
