@@ -17,6 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("GX_KPROF", "1")
 
+MERGE_N = 64  # GX_KPROF_MERGE_N: the merge path counters after the per-wave marks
+MERGE_NAMES = ["receivers", "seg16", "seg32", "wave", "fallback_wave", "live_records"]
 NAMES = ["start", "ticks_done", "barrier", "sends_begin", "send_host", "chunk_planned", "chunk_stored", "sends_done"]
 
 
@@ -25,7 +27,8 @@ def marks(e, lib):
     lib.gx_kprof_read(e.h, None, ctypes.c_uint64(0), ctypes.byref(n))
     buf = (ctypes.c_uint64 * n.value)()
     assert lib.gx_kprof_read(e.h, buf, ctypes.c_uint64(n.value), ctypes.byref(n)) == 0
-    return np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
+    return a[:-MERGE_N].reshape(-1, 8), a[-MERGE_N:]
 
 
 def summarize(m):
@@ -57,8 +60,11 @@ def main():
     res = {}
     for r in sorted(a.rounds):
         e.run_rounds(r - e.round)
-        e.run_rounds(1)  # round r: its k_send's marks
-        res[r] = summarize(marks(e, lib))
+        _, m0 = marks(e, lib)
+        e.run_rounds(1)  # round r: its k_send's marks, its merge's path counts
+        wm, m1 = marks(e, lib)
+        res[r] = summarize(wm)
+        res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES)}
         print(json.dumps({"config": a.config, "round": r, **res[r]}), flush=True)
     e.close()
 

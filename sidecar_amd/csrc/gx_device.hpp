@@ -135,7 +135,9 @@ struct Dev {
   uint32_t *wl_cnt, *wl_cnt_nx;    // this / next round's worklist count (into work_cnt)
   uint32_t *ovf_cnt, *ovf_cnt_nx;  // this / next round's overflow-list count
   uint32_t *work;      // [Hl] views whose expiry scan must stream the row this round
-  uint8_t *mflag;      // [Hl] receivers k_merge_lean left to k_merge (a live record or > DR packets)
+  // [Hl] live records registered for receiver vi this round (flag_live; the merge's routing hint,
+  // 0 = nothing to merge), cleared by the merge
+  uint32_t *mrec;
   grec *scan_list;     // [H][L] first L expired records of this round's scan
   uint32_t *scan_cnt;  // [H]
   uint8_t *tick;       // [H] BroadcastTombstones tick this round
@@ -339,6 +341,9 @@ GXD uint4 inbox_next(const Dev &d, uint32_t vi, int64_t after) {
   }
   return best;
 }
+// n live records were registered for local receiver vi (no return value: the senders never wait
+// for it). The merge folds exactly the receivers with a count and routes them by it (k_merge_seg).
+GXD void flag_live(const Dev &d, uint32_t vi, uint32_t n) { atomicAdd(&d.mrec[vi], n); }
 // memberlist state of this engine's host v (rows are shard-local, like the views)
 GXD gx_member *memp(const Dev &d, uint32_t v, uint32_t m) { return &d.mem[(size_t)li(d, v) * d.H + m]; }
 GXD int32_t *dlp(const Dev &d, uint32_t v, uint32_t m) { return &d.fd_dl[(size_t)li(d, v) * d.H + m]; }
@@ -561,7 +566,7 @@ template <int T>
 GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, uint32_t limit,
                                  grec *packet, uint32_t limit_bytes, uint32_t overhead,
                                  const gx_job *pj = nullptr, const uint64_t *rrow = nullptr,
-                                 uint8_t *rflag = nullptr) {
+                                 uint32_t rvi = 0) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lane0 = tl == 0;
   const uint32_t mask = d.DQ - 1;
@@ -653,8 +658,7 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
   // tombstone older than the tombstone lifespan, which is read as absent; so a record this sees
   // as a no-op is one, and the receiver is flagged for k_merge only when some record is live.
   // The senders count the receivers' gossip merges and stale drops (k_merge then does not).
-  bool lv = false;
-  uint32_t fm = 0, fs = 0;
+  uint32_t nlv = 0, fm = 0, fs = 0;
   const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
   const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
   auto filt = [&](const grec &g) {
@@ -662,7 +666,7 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
     const int64_t ts = ts_of(g.w);
     const bool stale = ts < t_stale;
     const bool gc = st_of(w0) == GX_TOMBSTONE && ts_of(w0) < t_gc;
-    lv |= !stale && (st_of(w0) == GX_ABSENT || ts > ts_of(w0) || gc);
+    nlv += !stale && (st_of(w0) == GX_ABSENT || ts > ts_of(w0) || gc);
     fm++;
     fs += stale;
   };
@@ -681,7 +685,7 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
   if (rrow) {
     a.c[C_GOSSIP_MERGES] += fm;
     a.c[C_STALE] += fs;
-    if (lv) *rflag = 1;  // any lane of the team that saw a live record (the same byte value)
+    if (nlv) flag_live(d, rvi, nlv);  // each lane its live records
   }
   // leftover = broadcast[l:]; batch records that stay pending go in front of the old head
   uint32_t nh;

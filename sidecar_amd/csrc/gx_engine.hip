@@ -470,8 +470,12 @@ static int round_merge_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
     if (!d.sfilt) k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);  // else the senders filtered
-    if (!(d.ab & 512u)) {  // receivers merged MERGE_SEG lanes each (A/B bit 512: a wave each)
+    if (d.ab & 2048u) {  // A/B: round 2's merge (consecutive receivers, a wave's fallbacks in turn)
       const unsigned g = nblk(d.Hl, MERGE_WAVES * (64 / MERGE_SEG));
+      if (d.R < (1u << 26)) (ev ? k_merge_seg_v1<true, true> : k_merge_seg_v1<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      else (ev ? k_merge_seg_v1<false, true> : k_merge_seg_v1<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+    } else if (!(d.ab & 512u)) {  // receivers routed by their live records (A/B bit 512: a wave each)
+      const unsigned g = nblk(d.Hl, MERGE_NR);
       if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
       else (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else {
@@ -744,7 +748,7 @@ int gx_destroy(gx_engine *e) {
   void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, d.in_stamp, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_w0, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
-                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mflag, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
+                  d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mrec, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
                   d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -904,8 +908,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(e->pp_prow, sizeof(int32_t) * Hg);
     HIPCHK(hipMemset(e->pp_prow, 0xff, sizeof(int32_t) * Hg));
   }
-  ALLOC(d.mflag, (H + 7) & ~(size_t)7);  // read 8 flags at a time
-  HIPCHK(hipMemset(d.mflag, 0, (H + 7) & ~(size_t)7));
+  ALLOC(d.mrec, sizeof(uint32_t) * H);
+  HIPCHK(hipMemset(d.mrec, 0, sizeof(uint32_t) * H));
   ALLOC(d.minexp, sizeof(unsigned long long) * H);
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
@@ -934,7 +938,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->xbound_round = -1;
   e->kprof_n = 0;
   if (getenv("GX_KPROF")) {  // diagnostics: phase marks of every k_send wave (gx_kprof_read)
-    e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8;
+    e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8 + GX_KPROF_MERGE_N;  // + the merge path counts
     ALLOC(d.kprof, sizeof(unsigned long long) * e->kprof_n);
     HIPCHK(hipMemset(d.kprof, 0, sizeof(unsigned long long) * e->kprof_n));
   }

@@ -1023,6 +1023,14 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
   return cnt;
 }
 
+// Diagnostics (Dev::kprof, env GX_KPROF): after k_send's per-wave marks, GX_KPROF_MERGE_N counters
+// of the gossip merge's routing (k_merge_seg), accumulated over launches: [0] receivers with live
+// records, [1] routed to 16-lane segments, [2] to 32-lane segments, [3] to a whole wave, [4] merged
+// by a whole wave after their segment did not fit, [5] live records registered
+#define GX_KPROF_MERGE_N 64
+GXD unsigned long long *kprof_merge(const Dev &d) {
+  return d.kprof ? d.kprof + (size_t)((d.Hl + 63) / 64) * 4 * 8 : nullptr;
+}
 // Diagnostics: wall-clock mark k of this wave (k_send phases; Dev::kprof, env GX_KPROF).
 #define GX_KP(k)                                                                                   \
   do {                                                                                             \
@@ -1335,7 +1343,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       d.msg_dst[c.x] = c.peer;
       if (c.row && stored) {
         inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, GX_NOSLOT_W0);
-        d.mflag[rv] = 1;
+        flag_live(d, rv, stored);
       }
       stored_all = stored + ((c.row && stored) ? 2u : 0u);  // a header and its count ~ 2 records
     }
@@ -1453,8 +1461,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
             const bool pf = q < n0 && q < (uint32_t)T;
             const bool filt = d.sfilt && pos != 0xffffffffu;  // a packet registered in a local inbox
             l = get_broadcasts_team<T>(d, a, u, hs, cap, pk, lim, d.p.overhead_bytes, pf ? &pjs[q] : nullptr,
-                                       filt ? &d.view[(size_t)(pj - d.lo) * d.R] : nullptr,
-                                       filt ? &d.mflag[pj - d.lo] : nullptr);
+                                       filt ? &d.view[(size_t)(pj - d.lo) * d.R] : nullptr, pj - d.lo);
           }
           called = j + 1;
           if (lane == 0) kb += 32 + 32ull * l + (filt_used(d, pos) ? 8ull * l : 0);  // job, records in/out, slots
@@ -1615,7 +1622,7 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
 // the headers of its first DR packets, then the records the headers name (inline slots, only the
 // lengths given), then the view slot of every record. A receiver whose records are all no-ops
 // (stale, or no newer than the slot: see k_merge) is finished here, its merges and stale drops
-// counted. A receiver with a live record, or with more than DR packets, is flagged (mflag) and
+// counted. A receiver with a live record, or with more than DR packets, gets a routing count (mrec) and
 // merged in full by k_merge. Measured (profiles/ab_gossip.sh, cfg5): 16 lanes x 4 records per
 // batch 17.8 us; 32 x 4 22.6 us; 64 x 2 24.2 us; 8 x 4 21.1 us; loading the inline slots
 // speculatively with the count (one hop less) 19-23 us: the wasted bytes cost more than the hop.
@@ -1623,6 +1630,7 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
 // L2): 31.1 us vs 16.1 + 14.4 us, the merge body's 116 VGPRs halving the filter's occupancy.
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
+#define MERGE_SEG 16  // lanes per receiver in k_merge_seg's first pass
 #define MERGE_RANGE_DEF 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
 struct MergeLds {  // one wave's staging for one receiver at a time
   uint4 hdr[GX_DI_MAX];     // headers in sender order (inboxes of more than 64 packets use all of it)
@@ -2105,11 +2113,90 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
   return true;
 }
 
-#define MERGE_SEG 16
-// 64 / MERGE_SEG receivers per wave (merge_seg); a receiver whose inbox does not fit a segment is
-// merged afterwards by the whole wave (merge_receiver).
+// Phase 4 for the receivers with live records (mrec: the live records the senders registered for
+// each, a routing hint). A block takes MERGE_NR consecutive receivers and routes the ones with a
+// count to work items by it: one receiver with more than 32 live records per item (a whole wave,
+// merge_receiver), two of 17..32 (32-lane segments) or four of up to 16 (16-lane segments,
+// merge_seg). The items go to the block's waves in turn, so the large inboxes of a block are folded
+// side by side, not one after another by one wave. A receiver whose inbox does not fit its segment
+// after all (more packets than lanes, or a count that overstates nothing) is merged by a whole wave
+// at the end.
+#define MERGE_NR (MERGE_WAVES * (64 / MERGE_SEG))  // receivers per block
+#define MERGE_NONE 0xffffffffu
 template <bool K32, bool EV>
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_seg(Dev d) {
+__global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_eu(3))) void k_merge_seg(Dev d) {
+  __shared__ MergeLds s_l[MERGE_WAVES];
+  __shared__ uint32_t s_it[MERGE_NR][4];  // work items: up to 4 receivers (MERGE_NONE: empty)
+  __shared__ uint32_t s_ty[MERGE_NR];     // 0: four 16-lane segments, 1: two 32-lane, 2: one wave
+  __shared__ uint32_t s_fb[MERGE_NR], s_n[2];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t r0 = blockIdx.x * MERGE_NR;
+  if (wv == 0) {  // routing: lane k reads receiver r0 + k's count
+    const uint32_t vi = r0 + lane;
+    uint32_t t = 0;
+    if (lane < MERGE_NR && vi < d.Hl) t = d.mrec[vi];
+    if (t) d.mrec[vi] = 0;  // the senders count next round's
+    if (lane < MERGE_NR)
+      for (int q = 0; q < 4; q++) s_it[lane][q] = MERGE_NONE;
+    const bool sm = t && t <= 16, md = t > 16 && t <= 32, lg = t > 32;
+    const uint64_t bs = __ballot(sm), bm = __ballot(md), bl = __ballot(lg), below = (1ull << lane) - 1ull;
+    const uint32_t nl = (uint32_t)__popcll(bl), nm = (uint32_t)__popcll(bm), ns = (uint32_t)__popcll(bs);
+    const uint32_t nim = (nm + 1) / 2, nis = (ns + 3) / 4;
+    wave_sync();
+    if (lg) {
+      const uint32_t it = (uint32_t)__popcll(bl & below);
+      s_it[it][0] = vi;
+      s_ty[it] = 2;
+    } else if (md) {
+      const uint32_t q = (uint32_t)__popcll(bm & below), it = nl + q / 2;
+      s_it[it][q & 1] = vi;
+      s_ty[it] = 1;
+    } else if (sm) {
+      const uint32_t q = (uint32_t)__popcll(bs & below), it = nl + nim + q / 4;
+      s_it[it][q & 3] = vi;
+      s_ty[it] = 0;
+    }
+    if (lane == 0) {
+      s_n[0] = nl + nim + nis;
+      s_n[1] = 0;
+    }
+    if (unsigned long long *kp = kprof_merge(d); kp && lane == 0 && (nl | nm | ns)) {  // diagnostics
+      atomicAdd(&kp[0], (unsigned long long)(nl + nm + ns));
+      atomicAdd(&kp[1], (unsigned long long)ns);
+      atomicAdd(&kp[2], (unsigned long long)nm);
+      atomicAdd(&kp[3], (unsigned long long)nl);
+    }
+    if (unsigned long long *kp = kprof_merge(d); kp && t) atomicAdd(&kp[5], (unsigned long long)t);
+  }
+  __syncthreads();
+  const uint32_t ni = s_n[0];
+  if (ni == 0) return;  // block-uniform
+  for (uint32_t it = wv; it < ni; it += MERGE_WAVES) {  // wave-uniform item type
+    const uint32_t ty = s_ty[it];
+    if (ty == 2) {
+      merge_receiver<K32, EV>(d, s_it[it][0], s_l[wv]);
+    } else if (ty == 1) {
+      const uint32_t v = s_it[it][lane >> 5];
+      const bool act = v != MERGE_NONE;
+      const bool ok = merge_seg<K32, EV, 32>(d, act ? v : 0u, act, s_l[wv]);
+      if (!ok && (lane & 31) == 0) s_fb[atomicAdd(&s_n[1], 1u)] = v;
+    } else {
+      const uint32_t v = s_it[it][lane >> 4];
+      const bool act = v != MERGE_NONE;
+      const bool ok = merge_seg<K32, EV, 16>(d, act ? v : 0u, act, s_l[wv]);
+      if (!ok && (lane & 15) == 0) s_fb[atomicAdd(&s_n[1], 1u)] = v;
+    }
+  }
+  __syncthreads();
+  const uint32_t nf = s_n[1];
+  if (unsigned long long *kp = kprof_merge(d); kp && threadIdx.x == 0 && nf) atomicAdd(&kp[4], (unsigned long long)nf);
+  for (uint32_t k = wv; k < nf; k += MERGE_WAVES) merge_receiver<K32, EV>(d, s_fb[k], s_l[wv]);
+}
+
+// A/B (GX_AB_FLAGS bit 2048): round 2's merge, four consecutive receivers per wave in 16-lane
+// segments, a receiver that does not fit merged afterwards by the same wave.
+template <bool K32, bool EV>
+__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_seg_v1(Dev d) {
   __shared__ MergeLds s_l[MERGE_WAVES];
   constexpr uint32_t NS = 64 / MERGE_SEG;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63, seg = lane / MERGE_SEG;
@@ -2117,8 +2204,8 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_seg(Dev d) {
   if (r0 >= d.Hl) return;
   const uint32_t vi = r0 + seg;
   bool fl = false;
-  if (vi < d.Hl) fl = d.mflag[vi] != 0;
-  if (fl && d.sfilt && (lane & (MERGE_SEG - 1)) == 0) d.mflag[vi] = 0;  // the senders flag next round's
+  if (vi < d.Hl) fl = d.mrec[vi] != 0;
+  if (fl && (lane & (MERGE_SEG - 1)) == 0) d.mrec[vi] = 0;
   const bool done = merge_seg<K32, EV, MERGE_SEG>(d, vi, fl, s_l[wv]);
   uint64_t rest = __ballot(!done && (lane & (MERGE_SEG - 1)) == 0);
   for (; rest; rest &= rest - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)__builtin_ctzll(rest) / MERGE_SEG, s_l[wv]);
@@ -2134,14 +2221,9 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
   const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * MERGE_RANGE;
   if (r0 >= d.Hl) return;
   uint64_t fl = 0;
-  if (MERGE_RANGE == 8 && r0 + MERGE_RANGE <= d.Hl) {
-    fl = *reinterpret_cast<const uint64_t *>(&d.mflag[r0]);
-    if (fl && d.sfilt) *reinterpret_cast<uint64_t *>(&d.mflag[r0]) = 0;  // the senders flag next round's
-  } else {
-    for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)d.mflag[r0 + k] << (8 * k);
-    if (fl && d.sfilt)
-      for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) d.mflag[r0 + k] = 0;
-  }
+  for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)(d.mrec[r0 + k] != 0) << (8 * k);
+  if (fl && d.sfilt)
+    for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) d.mrec[r0 + k] = 0;  // the senders count next round's
   for (; fl; fl &= fl - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)(__builtin_ctzll(fl) >> 3), s_l[wv]);
 }
 
@@ -2192,7 +2274,7 @@ __global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
       }
     }
     if (defer) c_merge = c_stale = c_hdr = 0;  // k_merge merges and counts this receiver
-    if (l == 0) d.mflag[vi] = defer ? 1 : 0;
+    if (l == 0) d.mrec[vi] = defer ? 0xffffu : 0u;  // a deferred receiver is merged by a whole wave
   }
   c_merge = wave_sum(c_merge);
   c_stale = wave_sum(c_stale);
@@ -3585,7 +3667,7 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
       d.msg_len[e] = nlive;
       if (fcap) d.fd_len[e] = nfd;
       if (nlive || nfd) inbox_header(d, vi, inbox_claim(d, vi), key, (uint32_t)e, nlive, GX_NOSLOT_W0);
-      if (nlive) d.mflag[vi] = 1;
+      if (nlive) flag_live(d, vi, nlive);
       ctr_atomic(d, C_GOSSIP_MERGES, len);
       ctr_atomic(d, C_STALE, nstale);
       // 16 B per slot read, 8 B per receiver slot, 16 B per live record written, header + count
