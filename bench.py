@@ -288,10 +288,12 @@ def dissemination(lib, cfg, seed, local_rank, start=100, rounds=300):
 
 def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
     """Fresh cluster from round 0: chunks of `check_every` rounds, catalog agreement checked
-    between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run)."""
+    between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run,
+    disagreement samples): the records some live views disagree on, every 100 rounds."""
     c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier, device)
     wall = 0.0
     conv = None
+    samples = []
     try:
         while c.round < max_rounds:
             barrier()
@@ -299,7 +301,9 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
             c.run_rounds(check_every)
             barrier()
             wall += time.perf_counter() - t0
-            ok, _ = c.converged()
+            ok, bad = c.converged()
+            if c.round % 100 == 0 or ok:
+                samples.append([c.round, int(bad)])
             if ok:
                 lc = c.stats()["last_change_round"]
                 conv = lc + 1  # the catalog stopped changing after round lc and agrees
@@ -308,7 +312,7 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
                 # wall to convergence: the rounds past the convergence point are excluded pro rata
                 wall = wall * conv / c.round if c.round else wall
                 break
-        return conv, wall, c.round
+        return conv, wall, c.round, samples
     finally:
         c.close()
 
@@ -471,15 +475,18 @@ def main():
 
     conv = None
     if not args.no_converge:
-        r, w, ran = run_converge(lib, args.config, seed, rank, world, local_rank, barrier, args.converge_max,
-                                 args.check_every)
+        r, w, ran, dis_s = run_converge(lib, args.config, seed, rank, world, local_rank, barrier, args.converge_max,
+                                        args.check_every)
         conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
                 "rounds_run": ran, "simulated_s": (r * 0.2) if r else None}
+        if r is None:  # how far from agreement the catalog stays (records some live views disagree on)
+            conv["disagreeing_records"] = {"min": min(x[1] for x in dis_s) if dis_s else None,
+                                           "every_100_rounds": dis_s}
     conv_ref = None
     ref = CONFIGS[args.config].get("ref_variant")
     if ref and not args.no_converge:
-        r, w, ran = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
-                                 args.check_every)
+        r, w, ran, _ = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
+                                    args.check_every)
         conv_ref = {"config": workload_text(ref), "rounds_to_converge": r,
                     "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
                     "simulated_s": (r * 0.2) if r else None}

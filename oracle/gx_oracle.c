@@ -80,7 +80,7 @@ struct gx_engine {
   gx_member *mem;         /* H * H  member list of every host */
   gx_fd_host *fdh;        /* H */
   gx_fd_msg *fdm;         /* H * K * fd_msg_cap  memberlist messages of this round's packets */
-  uint32_t *fd_len;       /* H * K */
+  uint32_t *fd_len;       /* H * KE (one per packet entry) */
   uint32_t *fd_peers;     /* H * K  gossip targets (memberlist's choice) */
   uint32_t *fd_np;        /* H */
   uint32_t *name_rank;    /* R  ByService: rank of each record's Service.Name, NULL until set */
@@ -800,7 +800,7 @@ static void round_send(gx_engine *e) {
   if (e->p.fd_enable) for_hosts(e, n, ph_fd_tick, &now);
   for (size_t i = 0; i < (size_t)e->H * e->KE; i++) e->msg_len[i] = 0;
   if (e->p.fd_enable) {
-    memset(e->fd_len, 0, sizeof(uint32_t) * (size_t)e->H * (e->K ? e->K : 1));
+    memset(e->fd_len, 0, sizeof(uint32_t) * (size_t)e->H * (e->KE ? e->KE : 1));
     for_hosts(e, n, ph_fd_send, NULL);
   }
   for_hosts(e, n, ph_send, NULL);
@@ -1184,7 +1184,7 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
-  if (p->gossip_messages > 16 || (p->gossip_messages > 1 && p->fd_enable)) return GX_EINVAL;
+  if (p->gossip_messages > 16) return GX_EINVAL;
   if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
     return GX_EINVAL;
   if (p->inbox_slots > 256) return GX_EINVAL; /* engine bound (GX_DI_MAX) */
@@ -1304,7 +1304,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
     }
   }
   if (p->fd_enable) {
-    size_t k = e->K ? e->K : 1;
+    size_t k = e->KE ? e->KE : 1; /* packet entries (GossipMessages gathers per target) */
     e->mem = (gx_member *)malloc(sizeof(gx_member) * H * H);
     e->fdh = (gx_fd_host *)calloc(H, sizeof(gx_fd_host));
     e->fdm = (gx_fd_msg *)calloc(H * k * p->fd_msg_cap, sizeof(gx_fd_msg));

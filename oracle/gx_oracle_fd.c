@@ -398,16 +398,23 @@ static void ph_fd_tick(gx_engine *e, uint32_t i, void *ctx) {
 }
 static void ph_fd_send(gx_engine *e, uint32_t i, void *ctx) {
   (void)ctx;
-  uint32_t u = e->lo + i, K = e->K, cap = e->p.fd_msg_cap;
+  uint32_t u = e->lo + i, K = e->K, KE = e->KE, NG = e->NG, cap = e->p.fd_msg_cap;
   e->fd_np[u] = 0;
-  for (uint32_t j = 0; j < K; j++) e->fd_len[(size_t)u * K + j] = 0;
+  for (uint32_t j = 0; j < KE; j++) e->fd_len[(size_t)u * KE + j] = 0;
   if (departed(e, u)) return;
   uint32_t peers[64];
   uint32_t np = fd_sample_peers(e, u, peers), budget = fd_budget(e);
   e->fd_np[u] = np;
   for (uint32_t j = 0; j < np; j++) {
     e->fd_peers[(size_t)u * K + j] = peers[j];
-    e->fd_len[(size_t)u * K + j] = fd_get_broadcasts(e, u, budget, &e->fdm[((size_t)u * K + j) * cap]);
+    /* GossipMessages (the fork's gossip(): up to N gathers per target, memberlist's queue first in
+     * each); the queue only shrinks while gathering, so a gather that finds it empty ends its part */
+    for (uint32_t n = 0; n < NG; n++) {
+      size_t x = (size_t)u * KE + (size_t)j * NG + n;
+      uint32_t l = fd_get_broadcasts(e, u, budget, &e->fdm[x * cap]);
+      e->fd_len[x] = l;
+      if (!l) break;
+    }
   }
 }
 static void ph_fd_receive(gx_engine *e, uint32_t i, void *ctx) {

@@ -476,6 +476,7 @@ static int round_merge_impl(gx_engine *e) {
       else (ev ? k_merge_seg_v1<false, true> : k_merge_seg_v1<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else if (!(d.ab & 512u)) {  // receivers routed by their live records (A/B bit 512: a wave each)
       const unsigned g = nblk(d.Hl, MERGE_NR);
+      // 4 waves per SIMD (22 spilled registers) measured within noise of 3 (profiles/r03/ab)
       if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
       else (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else {
@@ -721,7 +722,7 @@ static int check_params(const gx_params *p) {
   if (p->limit_bytes > (1u << 24) || p->overhead_bytes > (1u << 16)) return GX_EINVAL;
   if (p->n_shards > 1 && (p->shard_id >= p->n_shards || p->n_shards > p->n_hosts || p->n_shards > 64)) return GX_EINVAL;
   if (p->depart_ppm > 1000000u) return GX_EINVAL;
-  if (p->gossip_messages > 16 || (p->gossip_messages > 1 && p->fd_enable)) return GX_EINVAL;
+  if (p->gossip_messages > 16) return GX_EINVAL;
   if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
     return GX_EINVAL;
   if (p->inbox_slots > GX_DI_MAX) return GX_EINVAL;

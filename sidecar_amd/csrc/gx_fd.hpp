@@ -600,8 +600,8 @@ __global__ __launch_bounds__(64) void k_fd_send(Dev d) {  // one thread per host
   FdAcc f;
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x, u = d.lo + idx;
   if (idx < d.Hl) {
-    const uint32_t K = d.K, cap = d.p.fd_msg_cap;
-    for (uint32_t j = 0; j < K; j++) d.fd_len[(size_t)idx * K + j] = 0;
+    const uint32_t K = d.K, KE = d.KE, NG = d.NG, cap = d.p.fd_msg_cap;
+    for (uint32_t j = 0; j < KE; j++) d.fd_len[(size_t)idx * KE + j] = 0;
     uint32_t np = 0;
     if (!departed(d, u)) {
       uint32_t peers[16];
@@ -609,7 +609,16 @@ __global__ __launch_bounds__(64) void k_fd_send(Dev d) {  // one thread per host
       const uint32_t budget = fd_budget(d);
       for (uint32_t j = 0; j < np; j++) {
         d.fd_peers[(size_t)idx * K + j] = peers[j];
-        d.fd_len[(size_t)idx * K + j] = fd_get_broadcasts(d, f, u, budget, &d.fdm[((size_t)idx * K + j) * cap]);
+        // GossipMessages: each of the target's gathers (packet entry j * NG + n) takes memberlist's
+        // messages first; the queue only shrinks during the gathers, so once a gather finds it
+        // empty the later ones do too (and the target's gathering goes on only while the
+        // delegate's part is not empty, k_send)
+        for (uint32_t n = 0; n < NG; n++) {
+          const size_t x = (size_t)idx * KE + (size_t)j * NG + n;
+          const uint32_t l = fd_get_broadcasts(d, f, u, budget, &d.fdm[x * cap]);
+          d.fd_len[x] = l;
+          if (!l) break;
+        }
       }
     }
     d.fd_np[idx] = np;

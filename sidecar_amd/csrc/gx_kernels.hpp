@@ -1057,7 +1057,10 @@ GXD unsigned long long *kprof_merge(const Dev &d) {
 // Batch records that stay pending are written to the ring after the chunk's loads, position p by
 // team lane p % T in call order (the sequential order of the ring writes).
 #define PLAN_CH 4  // calls planned per chunk
-#define PLAN_RECS 32  // records of a chunk in flight per team (32 / T per lane)
+#ifndef GX_PLAN_RECS
+#define GX_PLAN_RECS 32
+#endif
+#define PLAN_RECS GX_PLAN_RECS  // records of a chunk in flight per team (PLAN_RECS / T per lane)
 struct PlanCall {
   // batch item i (i < m) as the record phase builds it: EXPIRE {bw, rb + (emask ? nth set bit : i)},
   // SEND {list[i].w + bw, list[i].r}, RETX {bw, rb}
@@ -2121,22 +2124,23 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
 // side by side, not one after another by one wave. A receiver whose inbox does not fit its segment
 // after all (more packets than lanes, or a count that overstates nothing) is merged by a whole wave
 // at the end.
-#define MERGE_NR (MERGE_WAVES * (64 / MERGE_SEG))  // receivers per block
+#define MERGE_NR 64  // receivers per block (16 measured 3% slower in the accepting stretch, profiles/r03/ab)
 #define MERGE_NONE 0xffffffffu
-template <bool K32, bool EV>
+template <bool K32, bool EV, int NR = MERGE_NR>
 __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_eu(3))) void k_merge_seg(Dev d) {
+  static_assert(NR <= 64, "one routing lane per receiver");
   __shared__ MergeLds s_l[MERGE_WAVES];
-  __shared__ uint32_t s_it[MERGE_NR][4];  // work items: up to 4 receivers (MERGE_NONE: empty)
-  __shared__ uint32_t s_ty[MERGE_NR];     // 0: four 16-lane segments, 1: two 32-lane, 2: one wave
-  __shared__ uint32_t s_fb[MERGE_NR], s_n[2];
+  __shared__ uint32_t s_it[NR][4];  // work items: up to 4 receivers (MERGE_NONE: empty)
+  __shared__ uint32_t s_ty[NR];     // 0: four 16-lane segments, 1: two 32-lane, 2: one wave
+  __shared__ uint32_t s_fb[NR], s_n[2];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t r0 = blockIdx.x * MERGE_NR;
+  const uint32_t r0 = blockIdx.x * NR;
   if (wv == 0) {  // routing: lane k reads receiver r0 + k's count
     const uint32_t vi = r0 + lane;
     uint32_t t = 0;
-    if (lane < MERGE_NR && vi < d.Hl) t = d.mrec[vi];
+    if (lane < (uint32_t)NR && vi < d.Hl) t = d.mrec[vi];
     if (t) d.mrec[vi] = 0;  // the senders count next round's
-    if (lane < MERGE_NR)
+    if (lane < (uint32_t)NR)
       for (int q = 0; q < 4; q++) s_it[lane][q] = MERGE_NONE;
     const bool sm = t && t <= 16, md = t > 16 && t <= 32, lg = t > 32;
     const uint64_t bs = __ballot(sm), bm = __ballot(md), bl = __ballot(lg), below = (1ull << lane) - 1ull;

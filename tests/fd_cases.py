@@ -295,6 +295,12 @@ SCENARIOS = {
                                 packet_cap=48, ae_period_rounds=10, queue_cap=4096), 250),
     "depart_no_fd": (dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, depart_round=5, depart_ppm=100_000,
                           ae_period_rounds=10, queue_cap=4096), 200),
+    # GossipMessages with the detector: each of a target's gathers takes memberlist's queue first
+    "partition_heal_gm15": (dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, fd_enable=1, partition_start=0,
+                                 partition_end=40, ae_period_rounds=10, queue_cap=4096, gossip_messages=15), 260),
+    "depart_bytes_gm4": (dict(n_hosts=80, n_services=8, init_mode=INIT_OWN, fd_enable=1, depart_round=10,
+                              depart_ppm=60_000, churn_ppm=20_000, limit_bytes=1398, overhead_bytes=3,
+                              packet_cap=48, ae_period_rounds=10, queue_cap=4096, gossip_messages=4), 220),
     # the packets' memberlist messages walked in key order through overflowed inboxes
     "depart_inbox_overflow": (dict(n_hosts=64, n_services=8, init_mode=INIT_WARM, fd_enable=1, depart_round=5,
                                    depart_ppm=100_000, ae_period_rounds=10, queue_cap=4096, fanout=6,

@@ -31,6 +31,9 @@ SCEN = {
     # the push-pull initiator's decision travels in the digest header
     "fd": dict(n_hosts=64, n_services=8, init_mode=2, ae_period_rounds=5, partition_start=0,
                partition_end=45, depart_round=3, depart_ppm=100000, fd_enable=1, queue_cap=4096),
+    "fd_gm6": dict(n_hosts=56, n_services=6, init_mode=2, ae_period_rounds=5, partition_start=0,
+                   partition_end=30, depart_round=4, depart_ppm=80000, fd_enable=1, queue_cap=4096,
+                   gossip_messages=6),
     "fd_bytes": dict(n_hosts=50, n_services=6, init_mode=1, ae_period_rounds=4, churn_ppm=30000, depart_round=10,
                      depart_ppm=100000, fd_enable=1, limit_bytes=1398, packet_cap=48, queue_cap=2048),
     # received packets registered in overflowed inboxes (inbox_slots is an engine bound)
