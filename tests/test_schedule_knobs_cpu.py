@@ -49,9 +49,12 @@ def test_gossip_messages_drains_queues_faster(oracle_lib):
 
 def test_gossip_messages_validation(oracle_lib):
     from sidecar_amd.abi import GxError
-    for bad in (dict(gossip_messages=17), dict(gossip_messages=2, fd_enable=1)):
+    for bad in (dict(gossip_messages=17), dict(inbox_slots=257)):
         with pytest.raises(GxError):
             _eng(oracle_lib, n_hosts=16, n_services=2, **bad)
+    # GossipMessages runs with the failure detector too (each gather takes memberlist's queue first)
+    e = _eng(oracle_lib, n_hosts=16, n_services=2, gossip_messages=2, fd_enable=1)
+    e.run_rounds(3)
 
 
 def test_push_pull_initiate_every_host_starts_one(oracle_lib):
