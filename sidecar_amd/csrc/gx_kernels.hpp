@@ -26,28 +26,6 @@ GXD unsigned long long block_excl_scan64(unsigned long long x, unsigned long lon
   total = tot;
   return off + incl - x;
 }
-// The same scan with one barrier: the caller alternates two s_wave buffers between consecutive
-// scans (a buffer is rewritten only after every wave has passed the next scan's barrier, so after
-// it has read this one).
-GXD unsigned long long block_excl_scan64_1b(unsigned long long x, unsigned long long *s_wave,
-                                            unsigned long long &total) {
-  uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  unsigned long long incl = x;
-  for (int o = 1; o < 64; o <<= 1) {
-    unsigned long long y = __shfl_up(incl, o, 64);
-    if ((int)lane >= o) incl += y;
-  }
-  if (lane == 63) s_wave[w] = incl;
-  __syncthreads();
-  unsigned long long off = 0, tot = 0;
-  for (uint32_t i = 0; i < nw; i++) {
-    unsigned long long c = s_wave[i];
-    if (i < w) off += c;
-    tot += c;
-  }
-  total = tot;
-  return off + incl - x;
-}
 GXD uint32_t fld(unsigned long long x, int i) { return (uint32_t)((x >> (16 * i)) & 0xffffu); }
 
 // Block reduction of a counter -> one atomic on this block's shard.
@@ -2467,8 +2445,6 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   // last status change of the pass (state.LastChanged), events for listening views; key order
   __shared__ uint32_t s_lu[TILE_OWNERS], s_lc[TILE_OWNERS];
   __shared__ uint32_t s_last[2];
-  __shared__ unsigned long long s_wpp[2][4];  // retransmit scans, alternating
-  uint32_t scan_k = 0;                         // scans so far (block-uniform)
   if (t < 2) s_last[t] = 0;  // read after the pass's barriers
   const int32_t evka = __builtin_amdgcn_readfirstlane(d.ev_slot[li(d, a)]);
   const int32_t evkb = __builtin_amdgcn_readfirstlane(both ? d.ev_slot[li(d, b)] : -1);
@@ -2674,29 +2650,23 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       }
     }
     if (shfl_times) {
-      if (wave_acc && !(d.ab & 16384u)) {  // this wave accepted something (A/B diagnosis bit 16384: skip)
+      if (wave_acc) {  // this wave accepted something
         side_times_shfl(d, a, base, fl & 0xffu, nwa, lk_a, c_wr);  // server times count as written words
         if (both) side_times_shfl(d, b, base, (fl >> 8) & 0xffu, nwb, lk_b, c_wr);
       }
       // Both FIFOs full (block-uniform): every further retransmit is dropped, so its position no
       // longer matters; count it per thread and reduce once after the pass (no scan, no barrier).
-      // (A/B diagnosis bit 32768: as if full from the start)
-      if ((na >= rooma && (!both || nb >= roomb)) || (d.ab & 32768u)) {
+      if (na >= rooma && (!both || nb >= roomb)) {
         c_qa += fld(cnt, 0) + fld(cnt, 1);
         c_qb += fld(cnt, 2) + fld(cnt, 3);
         return;
       }
     }
-    unsigned long long tot, pre;
-    if (shfl_times && !(d.ab & 65536u)) {
-      // one barrier: the scan itself tells whether any foreign record was accepted (its two
-      // buffers alternate by scan; A/B bit 65536: a barrier-or first, then the two-barrier scan)
-      pre = block_excl_scan64_1b(cnt, s_wpp[scan_k++ & 1u], tot);
-      if (tot == 0) return;  // no foreign record accepted: no retransmits
-    } else {
-      if (shfl_times ? !__syncthreads_or(cnt != 0) : !__syncthreads_or(fl != 0)) return;
-      pre = block_excl_scan64(cnt, s_wave, tot);
-    }
+    // (a one-barrier scan with alternating buffers measured within noise at cfg 2, 4 and 5,
+    // profiles/r03/ab/ae_scan_barriers.txt)
+    if (shfl_times ? !__syncthreads_or(cnt != 0) : !__syncthreads_or(fl != 0)) return;
+    unsigned long long tot;
+    const unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
     uint32_t pa[4], pb[4];
     pa[0] = na + fld(pre, 0);
     pa[1] = pa[0] + fa[0];
