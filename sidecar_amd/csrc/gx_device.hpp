@@ -437,6 +437,11 @@ GXD void wake_host(const Dev &d, Acc &a, uint32_t v) {
   }
 }
 
+// (base + k) % q for base < q and k < q, without a division
+GXD uint32_t ring_add(uint32_t base, uint32_t k, uint32_t q) {
+  const uint32_t x = base + k;
+  return x >= q ? x - q : x;
+}
 GXD gx_job make_job(uint64_t a, uint64_t b, uint32_t c, uint32_t meta) {
   gx_job j;
   j.a = a;

@@ -2435,6 +2435,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t ta0 = ha->fifo_tail, ca0 = ta0 - ha->fifo_head;
   uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
   uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
+  const uint32_t ta0q = ta0 % d.Q, tb0q = tb0 % d.Q;  // ring positions of the tails (one division each)
   uint32_t na = 0, nb = 0;
   uint32_t c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0;  // per thread: < 2^32
   uint32_t c_qa = 0, c_qb = 0;  // retransmits counted after both FIFOs filled up (all dropped)
@@ -2680,9 +2681,9 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       if (fa[k] && pa[k] < rooma)
-        d.fifo[(size_t)li(d, a) * d.Q + ((ta0 + pa[k]) % d.Q)] = make_job(nwa[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+        d.fifo[(size_t)li(d, a) * d.Q + ring_add(ta0q, pa[k], d.Q)] = make_job(nwa[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
       if (fb[k] && pb[k] < roomb)
-        d.fifo[(size_t)li(d, b) * d.Q + ((tb0 + pb[k]) % d.Q)] = make_job(nwb[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+        d.fifo[(size_t)li(d, b) * d.Q + ring_add(tb0q, pb[k], d.Q)] = make_job(nwb[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
     }
     na += fld(tot, 0) + fld(tot, 1);
     nb += fld(tot, 2) + fld(tot, 3);
