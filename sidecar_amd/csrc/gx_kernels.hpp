@@ -811,6 +811,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   gx_host_state *h = &d.hs[vi];
   uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
   uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  const uint32_t tail0q = tail0 % d.Q;  // the tail's ring position (jobs land at tail0q + pos < 2Q)
   uint32_t jobs = 0, n_ev = 0;
   unsigned long long c_wr = 0, c_chg = 0;
   const uint64_t tomb = pack(d.now, GX_TOMBSTONE);
@@ -872,10 +873,9 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       uint64_t bj = __ballot(lead_live[c]);
       rank[c] = (uint32_t)__popcll(bj & ((1ull << lane) - 1));
       if (lane == 0) s_cnt[it][4 * c + wv] = (uint32_t)__popcll(bj);
-      if (lead_live[c]) {  // serverChanged (:204-215) for a live owner
+      if (lead_live[c]) {  // serverChanged (:204-215) for a live owner: both fields in one 16-B store
         gx_server_times *st = srv_times(d, v, lo + ((base + 512 * c + 2 * t) >> d.logS));
-        st->last_updated_ns = d.now;
-        st->last_changed_ns = d.now;
+        *reinterpret_cast<ulonglong2 *>(st) = make_ulonglong2((unsigned long long)d.now, (unsigned long long)d.now);
       }
       if (EV && evk >= 0) {  // events: owner order, then service order
         uint32_t ec = lead_live[c] ? (uint32_t)__popcll(pmask[c]) : 0u;
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       uint32_t pos = jobs + pre[c] + rank[c];
       if (lead_live[c] && pos < room) {
         uint32_t o = lo + ((base + 512 * c + 2 * t) >> d.logS);
-        d.fifo[(size_t)vi * d.Q + ((tail0 + pos) % d.Q)] =
+        d.fifo[(size_t)vi * d.Q + ring_add(tail0q, pos, d.Q)] =
             make_job((uint64_t)d.now, pmask[c], o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
       }
     }
