@@ -475,10 +475,20 @@ static int round_merge_impl(gx_engine *e) {
       if (d.R < (1u << 26)) (ev ? k_merge_seg_v1<true, true> : k_merge_seg_v1<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
       else (ev ? k_merge_seg_v1<false, true> : k_merge_seg_v1<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else if (!(d.ab & 512u)) {  // receivers routed by their live records (A/B bit 512: a wave each)
-      const unsigned g = nblk(d.Hl, MERGE_NR);
-      // 4 waves per SIMD (22 spilled registers) measured within noise of 3 (profiles/r03/ab)
-      if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      else (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      // 4 waves per SIMD (22 spilled registers) measured within noise of 3 (profiles/r03/ab).
+      // GossipMessages > 1: inboxes of hundreds of live records, each folded by a whole wave tile by
+      // tile, so more waves in flight (16 receivers per block); else 64 per block (3% faster at
+      // cfg 5). A/B bit 4096: the other choice.
+      const bool small = (d.NG > 1) != ((d.ab & 4096u) != 0);
+      const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
+      if (small) {
+        if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16> : k_merge_seg<true, false, 16>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+        else (ev ? k_merge_seg<false, true, 16> : k_merge_seg<false, false, 16>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      } else if (d.R < (1u << 26)) {
+        (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      } else {
+        (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      }
     } else {
       const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE_DEF);
       // 2 or 4 receivers per wave measured 14.2 / 13.7 vs 14.3 us (profiles/r02/gossip)
