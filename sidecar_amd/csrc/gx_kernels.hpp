@@ -2126,8 +2126,8 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
 // at the end.
 #define MERGE_NR 64  // receivers per block (16 measured 3% slower in the accepting stretch, profiles/r03/ab)
 #define MERGE_NONE 0xffffffffu
-template <bool K32, bool EV, int NR = MERGE_NR>
-__global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_eu(3))) void k_merge_seg(Dev d) {
+template <bool K32, bool EV, int NR = MERGE_NR, int WPE = 3>
+__global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge_seg(Dev d) {
   static_assert(NR <= 64, "one routing lane per receiver");
   __shared__ MergeLds s_l[MERGE_WAVES];
   __shared__ uint32_t s_it[NR][4];  // work items: up to 4 receivers (MERGE_NONE: empty)
