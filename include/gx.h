@@ -189,7 +189,9 @@ typedef struct gx_params {
   /* GossipMessages (config/config.go:46, main.go:257-259; README.md:180 "How many times to gather
    * messages per round", Sidecar's default 15): memberlist gathers up to this many GetBroadcasts
    * results per gossip target per round, each sent to that target as its own packet. 0 or 1 = one
-   * call per target. The memberlist fork is absent, so this reading is parity unpinned. */
+   * call per target. With fd_enable, each gather takes memberlist's queued messages first and the
+   * delegate's GetBroadcasts the bytes left. The memberlist fork is absent, so this reading is
+   * parity unpinned. */
   uint32_t gossip_messages;
   /* Push-pull pairing on anti-entropy rounds (memberlist pushPullTrigger every PushPullInterval,
    * config/config.go:45). GX_PP_MATCHING: a seeded perfect matching, every host in one exchange.

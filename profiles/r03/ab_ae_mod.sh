@@ -3,7 +3,7 @@
 # (libgx_prev.so), alternating processes on cfg2, cfg4, cfg5; then the parity tests on the new build.
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r03aem}
+O=gpurun_out/${TAG:-r03aent}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shards.py tests/test_gpu_codec.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 tail -1 $O/tests.log
