@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 5
+#define GX_ABI_VERSION 6
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -91,28 +91,58 @@ typedef struct gx_service {
   uint8_t flags;      /* reserved, 0 */
 } gx_service;
 
-/* Broadcast-queue job descriptor (read-back only, for parity checks).
+/* Broadcast-queue job descriptor, 16 B (the FIFO's entry; read-back for parity checks).
  *   kind NIL_BS / NIL_BT : the `Broadcasts <- nil` of an idle looper (services_state.go:569,628)
  *   kind RETX            : retransmit of one accepted record (services_state.go:377-392);
  *                          a = packed record word, c = record key r
  *   kind SEND            : SendServices job (services_state.go:579-604); list in the host's
  *                          list arena, c = slot | len << 16
  *   kind EXPIRE          : SendServices job of ExpireServer (services_state.go:150-192);
- *                          a = tombstone time ns, b = mask of tombstoned services, c = owner
- * meta = kind | pass << 8 | n_passes << 16; wake = round the job re-enters the FIFO (sleepers). */
+ *                          a = mask of tombstoned services, c = round of the call (the tombstones'
+ *                          Updated is that round's now), owner = the expired host
+ *   kind LOST            : a job whose contents the engine did not keep (below); dequeued as an
+ *                          empty batch and counted in gx_stats.queue_drops
+ * meta = kind | pass << 3 | n_passes << 9 | owner << 15 (GX_JOB_* accessors below).
+ *
+ * The FIFO holds every job the reference would hold: the reference's queue is unbounded (every
+ * blocked sender is a goroutine, services_state.go:94,384-391,581-603), so no job is ever
+ * refused. Each host stores the first queue_cap jobs of its queue (the "stored window", which
+ * the head dequeues from); a job pushed while the window is full, or behind such a job, is
+ * DEFERRED: counted in its place in the queue (fifo_tail) with its contents dropped. A deferred
+ * job is reached by GetBroadcasts only after all queue_cap stored jobs in front of it were
+ * dequeued, i.e. after at least queue_cap / (fanout * GossipMessages) rounds; until then every
+ * observable (every packet, every looper state) is the reference's. The loopers' nil sends are
+ * never lost (their positions are kept: nil_pos_bs / nil_pos_bt). A deferred job that reaches the
+ * head is dequeued as LOST: gx_stats.queue_drops counts those and first_drop_round holds the
+ * round of the first, so a run is faithful to the reference's queue iff queue_drops == 0. A
+ * SendServices job whose list does not fit the list arena (list_slots) is queued as LOST. */
 #define GX_JOB_NIL_BS 0
 #define GX_JOB_NIL_BT 1
 #define GX_JOB_RETX 2
 #define GX_JOB_SEND 3
 #define GX_JOB_EXPIRE 4
+#define GX_JOB_LOST 5
 typedef struct gx_job {
   uint64_t a;
-  uint64_t b;
   uint32_t c;
   uint32_t meta;
-  uint32_t wake;
-  uint32_t aux;
 } gx_job;
+/* A SendServices pass sleeping TOMBSTONE_RETRANSMIT before it re-enters the FIFO tail. */
+typedef struct gx_sleeper {
+  gx_job job;
+  uint32_t wake; /* round the pass re-enters the FIFO */
+  uint32_t pad[3];
+} gx_sleeper;
+#define GX_JOB_MAX_PASSES 63u   /* n_passes field: 6 bits (alive_count, tombstone_count <= 63) */
+#define GX_MAX_HOSTS (1u << 17) /* owner field: 17 bits */
+#define GX_MAX_LIST_SLOTS 1024u
+#define GX_MAX_ROUND ((int64_t)1 << 31) /* rounds are 32-bit in jobs and sleepers (2^31 x 200 ms = 13 years) */
+#define GX_JOB_KIND(m) ((m) & 7u)
+#define GX_JOB_PASS(m) (((m) >> 3) & 63u)
+#define GX_JOB_NPASSES(m) (((m) >> 9) & 63u)
+#define GX_JOB_OWNER(m) ((m) >> 15)
+#define GX_JOB_META(kind, pass, n_passes, owner) \
+  ((uint32_t)(kind) | (uint32_t)(pass) << 3 | (uint32_t)(n_passes) << 9 | (uint32_t)(owner) << 15)
 
 /* Engine parameters. gx_params_default() fills the reference constants. */
 #define GX_INIT_EMPTY 0 /* no view knows anything; owners announce at their first tick */
@@ -124,8 +154,8 @@ typedef struct gx_params {
   uint32_t fanout;                    /* k: peers per gossip round (memberlist GossipNodes, LAN 3) */
   uint32_t packet_cap;                /* records per GetBroadcasts packet (broadcast cap, 32) */
   uint32_t pending_cap;               /* MAX_PENDING_LENGTH, services_delegate.go:17 (100) */
-  uint32_t queue_cap;                 /* Q: broadcast FIFO jobs per host (engine bound) */
-  uint32_t list_slots;                /* A: live SendServices lists per host (engine bound, <=32) */
+  uint32_t queue_cap;                 /* Q: stored FIFO jobs per host (the stored window, see gx_job) */
+  uint32_t list_slots;                /* A: live SendServices lists per host (engine bound, <= 1024) */
   uint32_t gossip_stop_on_empty;      /* memberlist gossip(): stop the round at the first empty packet */
   uint32_t alive_interval_rounds;     /* ALIVE_SLEEP_INTERVAL 1s = 5 rounds (services_state.go:34) */
   uint32_t tombstone_interval_rounds; /* TOMBSTONE_SLEEP_INTERVAL 2s = 10 rounds (:30) */
@@ -212,12 +242,17 @@ typedef struct gx_host_state {
   uint32_t fifo_head, fifo_tail;   /* broadcast FIFO ring counters (count = tail - head) */
   uint32_t sleep_head, sleep_tail; /* SendServices jobs sleeping TOMBSTONE_RETRANSMIT */
   uint32_t dq_head, dq_len;        /* delegate pendingBroadcasts (dq_len <= pending_cap between calls) */
-  uint32_t arena_used;             /* bitmask of live SendServices lists */
+  uint32_t arena_used;             /* bit w: list slots [32w, 32w + 32) all live (the lowest free slot
+                                      is allocated: a two-level bitmap, slots >= list_slots count as live) */
   uint32_t flags;                  /* bit0 BroadcastServices blocked on nil, bit1 BroadcastTombstones blocked */
   int64_t bs_next;                 /* next BroadcastServices looper round */
   int64_t bt_next;                 /* next BroadcastTombstones looper round */
   int64_t last_bcast_ns;           /* BroadcastServices lastTime (services_state.go:526,560) */
   uint64_t running;                /* owner's local services currently running (discovery) */
+  uint32_t fifo_stored;            /* end of the stored window: jobs [fifo_head, fifo_stored) are kept,
+                                      [fifo_stored, fifo_tail) deferred (gx_job) */
+  uint32_t nil_pos_bs, nil_pos_bt; /* queue position of each looper's last nil send */
+  uint32_t pad;
 } gx_host_state;
 
 typedef struct gx_stats {
@@ -230,10 +265,12 @@ typedef struct gx_stats {
   uint64_t local_accepts;
   uint64_t stale_drops;      /* IsStale gate, services_state.go:302-308 */
   uint64_t retransmits;      /* RETX jobs enqueued */
-  uint64_t queue_drops;      /* jobs dropped because the FIFO was full (engine bound) */
-  uint64_t list_drops;       /* SendServices jobs dropped because the list arena was full */
-  uint64_t sleep_drops;      /* re-armed passes dropped because the sleep ring was full */
-  uint64_t pending_drops;    /* records cut by MAX_PENDING_LENGTH (services_delegate.go:111-112) */
+  uint64_t queue_drops;      /* LOST jobs dequeued: jobs the reference would have sent whose contents the
+                                engine did not keep (gx_job); 0 = the run is faithful to the queue */
+  uint64_t list_drops;       /* SendServices jobs queued as LOST because the list arena was full */
+  uint64_t sleep_drops;      /* re-armed passes dropped because the sleep ring was full (engine bound) */
+  uint64_t pending_drops;    /* records cut by MAX_PENDING_LENGTH (services_delegate.go:111-112):
+                                the reference's own truncation, not an engine bound */
   uint64_t dequeues;         /* batches taken off the FIFO (nil included) */
   uint64_t nil_batches;
   uint64_t packets;          /* non-empty GetBroadcasts results */
@@ -263,6 +300,8 @@ typedef struct gx_stats {
   uint64_t fd_msgs_sent;     /* memberlist broadcasts put into gossip packets */
   uint64_t fd_msgs_received; /* memberlist broadcasts handled by receivers */
   uint64_t fd_state_merges;  /* remote node states merged by push-pull (mergeState) */
+  uint64_t queue_deferred;   /* jobs queued past the stored window (kept as a count, gx_job) */
+  int64_t first_drop_round;  /* round of the first queue_drops dequeue, -1 = none */
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */
@@ -687,8 +726,9 @@ int gx_read_view(gx_engine *e, uint32_t view, int64_t *ts_ns, uint8_t *status);
 int gx_write_views(gx_engine *e, uint32_t view_lo, uint32_t view_hi, const uint64_t *words);
 int gx_write_slot(gx_engine *e, uint32_t view, const gx_service *svc); /* raw store, no merge rule */
 int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out);
+/* The host's stored FIFO jobs [fifo_head, fifo_stored) in queue order (n_out = their count). */
 int gx_read_queue(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out);
-int gx_read_sleepers(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out);
+int gx_read_sleepers(gx_engine *e, uint32_t host, gx_sleeper *out, uint32_t cap, uint32_t *n_out);
 int gx_read_pending(gx_engine *e, uint32_t host, gx_service *out, uint32_t cap, uint32_t *n_out);
 int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, uint32_t cap,
                  uint32_t *n_out);

@@ -58,9 +58,11 @@ struct gx_engine {
   uint8_t *own_status;  /* H * S local service status (discovery/health) */
   gx_host_state *hs;    /* H */
   gx_job *fifo;         /* H * Q */
-  gx_job *sleep;        /* H * SQ */
+  gx_sleeper *sleep;    /* H * SQ */
   grec *dq;             /* H * DQ  delegate pendingBroadcasts deque */
   grec *arena;          /* H * A * L SendServices lists */
+  uint32_t AW;          /* bitmap words per host, ceil(A / 32) */
+  uint32_t *arena_bits; /* H * AW  live lists (bit = slot; slots >= A stay set); hs.arena_used bit w = word w full */
   uint32_t *arena_len;  /* H * A */
   grec *msg;            /* H * KE * packet_cap  this round's packets */
   uint32_t *msg_len;    /* H * KE */
@@ -113,9 +115,7 @@ static inline int64_t now_of(const gx_engine *e) { return e->p.t0_ns + e->round 
  * reference holds as time.Unix(0, 0), services_state.go:62-63,95) */
 static inline int64_t abs_ts(const gx_engine *e, int64_t t) { return t + e->epoch; }
 static inline int64_t abs_tm(const gx_engine *e, int64_t t) { return t ? t + e->epoch : 0; }
-static inline uint32_t meta_of(int kind, uint32_t pass, uint32_t np) {
-  return (uint32_t)kind | (pass << 8) | (np << 16);
-}
+static inline uint32_t meta_of(int kind, uint32_t pass, uint32_t np) { return GX_JOB_META((uint32_t)kind, pass, np, 0); }
 static uint32_t pow2_at_least(uint32_t x) {
   uint32_t v = 1;
   while (v < x) v <<= 1;
@@ -151,9 +151,12 @@ static void stats_merge(gx_stats *dst, const gx_stats *src) {
   const size_t n = sizeof(gx_stats) / sizeof(uint64_t);
   const size_t i_round = offsetof(gx_stats, round) / sizeof(uint64_t);
   const size_t i_lcr = offsetof(gx_stats, last_change_round) / sizeof(uint64_t);
+  const size_t i_fdr = offsetof(gx_stats, first_drop_round) / sizeof(uint64_t);
   for (size_t i = 0; i < n; i++)
-    if (i != i_round && i != i_lcr) d[i] += s[i];
+    if (i != i_round && i != i_lcr && i != i_fdr) d[i] += s[i];
   if (src->last_change_round > dst->last_change_round) dst->last_change_round = src->last_change_round;
+  if (src->first_drop_round >= 0 && (dst->first_drop_round < 0 || src->first_drop_round < dst->first_drop_round))
+    dst->first_drop_round = src->first_drop_round;
 }
 #endif
 /* Threads the phase loops use (oracle-only symbol, not part of gx.h): bench.py reports it as
@@ -173,6 +176,7 @@ static void for_hosts(gx_engine *e, uint32_t n, host_fn fn, void *ctx) {
       gx_engine loc = *e;
       memset(&loc.st, 0, sizeof loc.st);
       loc.st.last_change_round = e->st.last_change_round;
+      loc.st.first_drop_round = -1;
 #pragma omp for schedule(dynamic, 4)
       for (uint32_t i = 0; i < n; i++) fn(&loc, i, ctx);
 #pragma omp critical
@@ -185,36 +189,75 @@ static void for_hosts(gx_engine *e, uint32_t n, host_fn fn, void *ctx) {
 }
 
 /* ------------------------------------------------------------------------ broadcast FIFO -- */
-static void free_list(gx_engine *e, uint32_t v, const gx_job *j) {
-  if ((j->meta & 0xff) == GX_JOB_SEND) e->hs[v].arena_used &= ~(1u << (j->c & 0xffff));
+/* List arena: the lowest free slot (gx.h list_slots), a two-level bitmap. */
+static int list_live(const gx_engine *e, uint32_t v, uint32_t slot) {
+  return slot < e->A && (e->arena_bits[(size_t)v * e->AW + slot / 32] >> (slot % 32)) & 1u;
 }
-
-/* Blocked senders on the unbuffered Broadcasts channel (services_state.go:94) form a FIFO.
- * Engine bound: at most Q jobs; two slots are reserved for the loopers' nil sends so a looper
- * can never be blocked forever. */
-static int push_job(gx_engine *e, uint32_t v, const gx_job *j) {
+static int alloc_list(gx_engine *e, uint32_t v) {
   gx_host_state *h = &e->hs[v];
-  uint32_t count = h->fifo_tail - h->fifo_head;
-  int is_nil = (j->meta & 0xff) <= GX_JOB_NIL_BT;
-  uint32_t limit = is_nil ? e->Q : e->Q - 2;
-  if (count >= limit) {
-    e->st.queue_drops++;
-    free_list(e, v, j);
-    return 0;
-  }
-  e->fifo[(size_t)v * e->Q + (h->fifo_tail % e->Q)] = *j;
-  h->fifo_tail++;
-  return 1;
+  const uint32_t wfree = ~h->arena_used & (e->AW >= 32 ? 0xffffffffu : ((1u << e->AW) - 1));
+  if (!wfree) return -1;
+  const uint32_t w = (uint32_t)__builtin_ctz(wfree);
+  uint32_t *word = &e->arena_bits[(size_t)v * e->AW + w];
+  const uint32_t b = (uint32_t)__builtin_ctz(~*word);
+  *word |= 1u << b;
+  if (*word == 0xffffffffu) h->arena_used |= 1u << w;
+  return (int)(w * 32 + b);
+}
+static void free_list(gx_engine *e, uint32_t v, const gx_job *j) {
+  if (GX_JOB_KIND(j->meta) != GX_JOB_SEND) return;
+  const uint32_t slot = j->c & 0xffff;
+  e->arena_bits[(size_t)v * e->AW + slot / 32] &= ~(1u << (slot % 32));
+  e->hs[v].arena_used &= ~(1u << (slot / 32));
 }
 
-static void push_sleep(gx_engine *e, uint32_t v, const gx_job *j) {
+/* Blocked senders on the unbuffered Broadcasts channel (services_state.go:94) form a FIFO, and
+ * the reference never refuses one (each is a goroutine). The first Q jobs of the queue are stored;
+ * a job pushed while the stored window is full, or behind a deferred job, is deferred: it keeps
+ * its place (fifo_tail) and loses its contents (gx.h gx_job). A looper's nil keeps its position. */
+static int fifo_can_store(const gx_engine *e, const gx_host_state *h) {
+  return h->fifo_stored == h->fifo_tail && h->fifo_stored - h->fifo_head < e->Q;
+}
+static void push_job(gx_engine *e, uint32_t v, const gx_job *j) {
+  gx_host_state *h = &e->hs[v];
+  const uint32_t kind = GX_JOB_KIND(j->meta);
+  if (kind == GX_JOB_NIL_BS) h->nil_pos_bs = h->fifo_tail;
+  else if (kind == GX_JOB_NIL_BT) h->nil_pos_bt = h->fifo_tail;
+  if (fifo_can_store(e, h)) {
+    e->fifo[(size_t)v * e->Q + (h->fifo_tail % e->Q)] = *j;
+    h->fifo_stored++;
+  } else {
+    e->st.queue_deferred++;
+    free_list(e, v, j); /* only a LOST dequeue could reach it */
+  }
+  h->fifo_tail++;
+}
+
+/* Take the FIFO head (fifo_head != fifo_tail). A deferred job at the head is a looper's nil if its
+ * position says so, else LOST (counted: the run stops being faithful here). */
+static gx_job pop_job(gx_engine *e, uint32_t v) {
+  gx_host_state *h = &e->hs[v];
+  const uint32_t p = h->fifo_head++;
+  gx_job j = {0, 0, 0};
+  if (p != h->fifo_stored) return e->fifo[(size_t)v * e->Q + (p % e->Q)];
+  h->fifo_stored = h->fifo_head; /* the stored window restarts behind the deferred job */
+  if ((h->flags & 1u) && p == h->nil_pos_bs) j.meta = meta_of(GX_JOB_NIL_BS, 0, 1);
+  else if ((h->flags & 2u) && p == h->nil_pos_bt) j.meta = meta_of(GX_JOB_NIL_BT, 0, 1);
+  else j.meta = meta_of(GX_JOB_LOST, 0, 1);
+  return j;
+}
+
+static void push_sleep(gx_engine *e, uint32_t v, const gx_job *j, uint32_t wake) {
   gx_host_state *h = &e->hs[v];
   if (h->sleep_tail - h->sleep_head >= e->SQ) {
     e->st.sleep_drops++;
     free_list(e, v, j);
     return;
   }
-  e->sleep[(size_t)v * e->SQ + (h->sleep_tail % e->SQ)] = *j;
+  gx_sleeper *s = &e->sleep[(size_t)v * e->SQ + (h->sleep_tail % e->SQ)];
+  memset(s, 0, sizeof *s);
+  s->job = *j;
+  s->wake = wake;
   h->sleep_tail++;
 }
 
@@ -223,9 +266,9 @@ static void push_sleep(gx_engine *e, uint32_t v, const gx_job *j) {
 static void wake_host(gx_engine *e, uint32_t v) {
   gx_host_state *h = &e->hs[v];
   while (h->sleep_head != h->sleep_tail) {
-    gx_job *j = &e->sleep[(size_t)v * e->SQ + (h->sleep_head % e->SQ)];
-    if ((int64_t)j->wake > e->round) break;
-    gx_job cp = *j;
+    gx_sleeper *s = &e->sleep[(size_t)v * e->SQ + (h->sleep_head % e->SQ)];
+    if ((int64_t)s->wake > e->round) break;
+    gx_job cp = s->job;
     h->sleep_head++;
     push_job(e, v, &cp);
   }
@@ -234,27 +277,29 @@ static void wake_host(gx_engine *e, uint32_t v) {
 /* SendServices(services, looper(n)), services_state.go:579-604. The list is copied at call
  * time. Only its first packet_cap + pending_cap records can ever leave a GetBroadcasts call
  * (services_delegate.go:104-115), so the stored list is truncated to that length. */
-static int create_send(gx_engine *e, uint32_t v, const grec *list, uint32_t n, uint32_t npasses) {
+static void create_send(gx_engine *e, uint32_t v, const grec *list, uint32_t n, uint32_t npasses) {
   gx_host_state *h = &e->hs[v];
-  uint32_t slot = 0;
-  while (slot < e->A && (h->arena_used >> slot) & 1u) slot++;
-  if (slot >= e->A) {
-    e->st.list_drops++;
-    return 0;
-  }
-  if (n > e->L) n = e->L;
-  h->arena_used |= 1u << slot;
-  grec *dst = &e->arena[((size_t)v * e->A + slot) * e->L];
-  for (uint32_t i = 0; i < n; i++) dst[i] = list[i];
-  e->arena_len[(size_t)v * e->A + slot] = n;
-  gx_job j = {0, 0, slot | (n << 16), meta_of(GX_JOB_SEND, 0, npasses), 0, 0};
   e->st.send_jobs++;
-  return push_job(e, v, &j);
+  if (n > e->L) n = e->L;
+  gx_job j = {0, 0, meta_of(GX_JOB_SEND, 0, npasses)};
+  if (fifo_can_store(e, h)) { /* a deferred job needs no list */
+    const int slot = alloc_list(e, v);
+    if (slot < 0) {
+      e->st.list_drops++;
+      j.meta = meta_of(GX_JOB_LOST, 0, 1);
+    } else {
+      grec *dst = &e->arena[((size_t)v * e->A + slot) * e->L];
+      for (uint32_t i = 0; i < n; i++) dst[i] = list[i];
+      e->arena_len[(size_t)v * e->A + slot] = n;
+      j.c = (uint32_t)slot | (n << 16);
+    }
+  }
+  push_job(e, v, &j);
 }
 
 /* Records of pass `pass` of a job: Updated + pass * 50ns (services_state.go:588-599). */
 static uint32_t expand(const gx_engine *e, uint32_t v, const gx_job *j, grec *out) {
-  uint32_t kind = j->meta & 0xff, pass = (j->meta >> 8) & 0xff;
+  uint32_t kind = GX_JOB_KIND(j->meta), pass = GX_JOB_PASS(j->meta);
   uint64_t dw = ((uint64_t)pass * (uint64_t)e->p.pass_increment_ns) << GX_TS_SHIFT;
   uint32_t n = 0;
   if (kind == GX_JOB_RETX) {
@@ -271,12 +316,13 @@ static uint32_t expand(const gx_engine *e, uint32_t v, const gx_job *j, grec *ou
       out[i].pad = 0;
     }
     n = len;
-  } else if (kind == GX_JOB_EXPIRE) {
-    uint64_t w = pack((int64_t)j->a, GX_TOMBSTONE) + dw;
+  } else if (kind == GX_JOB_EXPIRE) { /* Tombstone() at the call's now (services_state.go:176-181) */
+    uint64_t w = pack(e->p.t0_ns + (int64_t)j->c * e->p.round_ns, GX_TOMBSTONE) + dw;
+    uint32_t o = GX_JOB_OWNER(j->meta);
     for (uint32_t s = 0; s < e->S; s++)
-      if ((j->b >> s) & 1ull) {
+      if ((j->a >> s) & 1ull) {
         out[n].w = w;
-        out[n].r = j->c * e->S + s;
+        out[n].r = o * e->S + s;
         out[n].pad = 0;
         n++;
       }
@@ -316,12 +362,14 @@ static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *p
   grec batch[512];
   uint32_t m = 0;
   if (h->fifo_head != h->fifo_tail) { /* case broadcast = <-d.state.Broadcasts (:94) */
-    gx_job j = e->fifo[(size_t)v * e->Q + (h->fifo_head % e->Q)];
-    h->fifo_head++;
+    gx_job j = pop_job(e, v);
     e->st.dequeues++;
     m = expand(e, v, &j, batch);
-    uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff, np = (j.meta >> 16) & 0xff;
-    if (kind == GX_JOB_NIL_BS) { /* BroadcastServices looper unblocks (:569) */
+    uint32_t kind = GX_JOB_KIND(j.meta), pass = GX_JOB_PASS(j.meta), np = GX_JOB_NPASSES(j.meta);
+    if (kind == GX_JOB_LOST) { /* a deferred job reached the head: its batch is unknown */
+      e->st.queue_drops++;
+      if (e->st.first_drop_round < 0 || e->round < e->st.first_drop_round) e->st.first_drop_round = e->round;
+    } else if (kind == GX_JOB_NIL_BS) { /* BroadcastServices looper unblocks (:569) */
       e->st.nil_batches++;
       h->flags &= ~1u;
       h->bs_next = e->round + e->p.alive_interval_rounds;
@@ -331,14 +379,9 @@ static uint32_t get_broadcasts(gx_engine *e, uint32_t v, uint32_t limit, grec *p
       h->bt_next = e->round + e->p.tombstone_interval_rounds;
     } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
       if (pass + 1 < np) {
-        j.meta = meta_of((int)kind, pass + 1, np);
-        if (e->p.retransmit_rounds == 0) {
-          j.wake = (uint32_t)e->round;
-          push_job(e, v, &j);
-        } else {
-          j.wake = (uint32_t)(e->round + e->p.retransmit_rounds);
-          push_sleep(e, v, &j);
-        }
+        j.meta = GX_JOB_META(kind, pass + 1, np, GX_JOB_OWNER(j.meta));
+        if (e->p.retransmit_rounds == 0) push_job(e, v, &j);
+        else push_sleep(e, v, &j, (uint32_t)(e->round + e->p.retransmit_rounds));
       } else {
         free_list(e, v, &j);
       }
@@ -451,8 +494,9 @@ static int add_entry(gx_engine *e, uint32_t v, grec u, int64_t now, int src) {
   else if (src == SRC_AE) e->st.ae_accepts++;
   else e->st.local_accepts++;
   if (u.r / e->S != v) { /* retransmit only foreign records (:380-382) */
-    gx_job j = {nw, 0, u.r, meta_of(GX_JOB_RETX, 0, 1), 0, 0};
-    if (push_job(e, v, &j)) e->st.retransmits++;
+    gx_job j = {nw, u.r, meta_of(GX_JOB_RETX, 0, 1)};
+    push_job(e, v, &j);
+    e->st.retransmits++;
   }
   return 1;
 }
@@ -536,7 +580,8 @@ static int expire_server(gx_engine *e, uint32_t v, uint32_t o, int64_t now) {
       service_changed(e, v, o * e->S + s, row[s], prev);
     }
   e->st.expire_server++;
-  gx_job j = {(uint64_t)now, mask, o, meta_of(GX_JOB_EXPIRE, 0, e->p.tombstone_count), 0, 0};
+  (void)now; /* = now_of(e): the job keeps the round */
+  gx_job j = {mask, (uint32_t)e->round, GX_JOB_META(GX_JOB_EXPIRE, 0, e->p.tombstone_count, o)};
   push_job(e, v, &j); /* SendServices(tombstones, TOMBSTONE_COUNT) (:188-191) */
   return 1;
 }
@@ -567,7 +612,7 @@ static uint32_t bs_body(gx_engine *e, uint32_t o, const grec *list, uint32_t n, 
     h->last_bcast_ns = now;
     create_send(e, o, inc, m, any_new ? e->p.alive_count : 1);
   } else {
-    gx_job j = {0, 0, 0, meta_of(GX_JOB_NIL_BS, 0, 1), 0, 0};
+    gx_job j = {0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)};
     push_job(e, o, &j);
     h->flags |= 1u;
   }
@@ -588,7 +633,7 @@ static void bt_tick(gx_engine *e, uint32_t o, int64_t now) {
     create_send(e, o, list, n > e->L ? e->L : n, e->p.tombstone_count); /* (:620-624) */
     h->bt_next = e->round + e->p.tombstone_interval_rounds;
   } else {
-    gx_job j = {0, 0, 0, meta_of(GX_JOB_NIL_BT, 0, 1), 0, 0};
+    gx_job j = {0, 0, meta_of(GX_JOB_NIL_BT, 0, 1)};
     push_job(e, o, &j);
     h->flags |= 2u;
   }
@@ -1166,10 +1211,13 @@ void gx_params_default(gx_params *p) {
 static int check_params(const gx_params *p) {
   if (!p || p->n_hosts < 1 || p->n_services < 1 || p->n_services > 64) return GX_EINVAL;
   if (p->fanout > 16 || p->packet_cap < 1 || p->packet_cap > 256 || p->pending_cap > 256) return GX_EINVAL;
-  if (p->queue_cap < 3 || p->list_slots < 1 || p->list_slots > 32) return GX_EINVAL;
+  if (p->queue_cap < 1 || p->list_slots < 1 || p->list_slots > GX_MAX_LIST_SLOTS) return GX_EINVAL;
+  if (p->n_hosts > GX_MAX_HOSTS) return GX_EINVAL; /* gx_job owner field */
   if (p->alive_interval_rounds < 1 || p->tombstone_interval_rounds < 1) return GX_EINVAL;
   if (p->retransmit_rounds > 1000) return GX_EINVAL;
-  if (p->alive_count < 1 || p->alive_count > 255 || p->tombstone_count < 1 || p->tombstone_count > 255) return GX_EINVAL;
+  if (p->alive_count < 1 || p->alive_count > GX_JOB_MAX_PASSES || p->tombstone_count < 1 ||
+      p->tombstone_count > GX_JOB_MAX_PASSES)
+    return GX_EINVAL;
   if (p->init_mode > GX_INIT_WARM) return GX_EINVAL;
   if (p->t0_ns < 0 || p->t0_ns > ((int64_t)1 << 62) || p->round_ns <= 0) return GX_EINVAL;
   { /* lifespans stay far inside the half window before t0 (gx.h GX_TS_SHIFT) */
@@ -1229,6 +1277,8 @@ static void init_state(gx_engine *e) {
   for (uint32_t o = 0; o < H; o++) {
     gx_host_state *h = &e->hs[o];
     memset(h, 0, sizeof(*h));
+    for (uint32_t w = 0; w < e->AW; w++) /* slots past list_slots never free */
+      e->arena_bits[(size_t)o * e->AW + w] = e->A >= 32 * (w + 1) ? 0u : ~0u << (e->A - 32 * w);
     h->bs_next = (int64_t)(rng4(p->seed, ST_PHASE_BS, o, 0, 0) % p->alive_interval_rounds);
     h->bt_next = (int64_t)(rng4(p->seed, ST_PHASE_BT, o, 0, 0) % p->tombstone_interval_rounds);
     h->last_bcast_ns = p->init_mode == GX_INIT_WARM ? p->t0_ns : 0;
@@ -1236,6 +1286,7 @@ static void init_state(gx_engine *e) {
   }
   memset(&e->st, 0, sizeof(e->st));
   e->st.last_change_round = -1;
+  e->st.first_drop_round = -1;
   e->round = 0;
   fd_init(e);
 }
@@ -1269,10 +1320,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->own_status = (uint8_t *)malloc(H * e->S);
   e->hs = (gx_host_state *)calloc(H, sizeof(gx_host_state));
   e->fifo = (gx_job *)calloc(H * e->Q, sizeof(gx_job));
-  e->sleep = (gx_job *)calloc(H * e->SQ, sizeof(gx_job));
+  e->sleep = (gx_sleeper *)calloc(H * e->SQ, sizeof(gx_sleeper));
   e->dq = (grec *)calloc(H * e->DQ, sizeof(grec));
   e->arena = (grec *)calloc(H * e->A * e->L, sizeof(grec));
   e->arena_len = (uint32_t *)calloc(H * e->A, sizeof(uint32_t));
+  e->AW = (e->A + 31) / 32;
+  e->arena_bits = (uint32_t *)calloc(H * e->AW, sizeof(uint32_t));
   e->msg = (grec *)calloc(H * (e->KE ? e->KE : 1) * p->packet_cap, sizeof(grec));
   e->msg_len = (uint32_t *)calloc(H * (e->KE ? e->KE : 1), sizeof(uint32_t));
   e->msg_dst = (uint32_t *)calloc(H * (e->KE ? e->KE : 1), sizeof(uint32_t));
@@ -1339,6 +1392,7 @@ int gx_destroy(gx_engine *e) {
   free(e->dq);
   free(e->arena);
   free(e->arena_len);
+  free(e->arena_bits);
   free(e->msg);
   free(e->msg_len);
   free(e->msg_dst);
@@ -1373,7 +1427,7 @@ int gx_destroy(gx_engine *e) {
 }
 
 int gx_set_round(gx_engine *e, int64_t round) {
-  if (!e || round < e->round) return GX_EINVAL;
+  if (!e || round < e->round || round >= GX_MAX_ROUND) return GX_EINVAL;
   e->round = round;
   e->st.round = round;
   for (uint32_t v = 0; v < e->H; v++)
@@ -1396,7 +1450,7 @@ int gx_enable_timing(gx_engine *e, int on) {
 }
 
 int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
-  if (!e || e->G > 1) return GX_EINVAL;
+  if (!e || e->G > 1 || e->round + n_rounds >= GX_MAX_ROUND) return GX_EINVAL;
   for (uint32_t i = 0; i < n_rounds; i++) run_one_round(e);
   return GX_OK;
 }
@@ -1498,7 +1552,7 @@ int gx_expire_server(gx_engine *e, uint32_t view, uint32_t owner, int *expired) 
 int gx_notify_leave(gx_engine *e, uint32_t view, uint32_t node) { return gx_expire_server(e, view, node, NULL); }
 
 int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32_t n, uint32_t n_passes) {
-  if (!e || host >= e->H || (n && !svcs) || n_passes < 1 || n_passes > 255) return GX_EINVAL;
+  if (!e || host >= e->H || (n && !svcs) || n_passes < 1 || n_passes > GX_JOB_MAX_PASSES) return GX_EINVAL;
   grec *tmp = (grec *)malloc(sizeof(grec) * (n ? n : 1));
   for (uint32_t i = 0; i < n; i++)
     if (to_grec(e, &svcs[i], &tmp[i])) {
@@ -1829,12 +1883,12 @@ int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out) {
 int gx_read_queue(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
   if (!e || host >= e->H || (cap && !out)) return GX_EINVAL;
   gx_host_state *h = &e->hs[host];
-  uint32_t n = h->fifo_tail - h->fifo_head;
+  uint32_t n = h->fifo_stored - h->fifo_head;
   for (uint32_t i = 0; i < n && i < cap; i++) out[i] = e->fifo[(size_t)host * e->Q + ((h->fifo_head + i) % e->Q)];
   if (n_out) *n_out = n;
   return GX_OK;
 }
-int gx_read_sleepers(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
+int gx_read_sleepers(gx_engine *e, uint32_t host, gx_sleeper *out, uint32_t cap, uint32_t *n_out) {
   if (!e || host >= e->H || (cap && !out)) return GX_EINVAL;
   gx_host_state *h = &e->hs[host];
   uint32_t n = h->sleep_tail - h->sleep_head;
@@ -1852,7 +1906,7 @@ int gx_read_pending(gx_engine *e, uint32_t host, gx_service *out, uint32_t cap, 
 }
 int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, uint32_t cap, uint32_t *n_out) {
   if (!e || host >= e->H || slot >= e->A || (cap && !out)) return GX_EINVAL;
-  uint32_t n = (e->hs[host].arena_used >> slot) & 1u ? e->arena_len[(size_t)host * e->A + slot] : 0;
+  uint32_t n = list_live(e, host, slot) ? e->arena_len[(size_t)host * e->A + slot] : 0;
   for (uint32_t i = 0; i < n && i < cap; i++) to_svc(e, &e->arena[((size_t)host * e->A + slot) * e->L + i], &out[i]);
   if (n_out) *n_out = n;
   return GX_OK;
@@ -1861,18 +1915,20 @@ int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, ui
 static inline uint64_t feed(uint64_t h, uint64_t x) { return mix64(h ^ x); }
 static uint64_t feed_job(uint64_t h, const gx_job *j) {
   h = feed(h, j->a);
-  h = feed(h, j->b);
-  h = feed(h, (uint64_t)j->c | ((uint64_t)j->meta << 32));
-  return feed(h, (uint64_t)j->wake | ((uint64_t)j->aux << 32));
+  return feed(h, (uint64_t)j->c | ((uint64_t)j->meta << 32));
 }
 int gx_host_digests(gx_engine *e, uint64_t *out) {
   if (!e || !out) return GX_EINVAL;
   for (uint32_t v = e->lo; v < e->hi; v++) {
     const gx_host_state *s = &e->hs[v];
     uint64_t h = 0x243F6A8885A308D3ull;
-    for (uint32_t i = s->fifo_head; i != s->fifo_tail; i++) h = feed_job(h, &e->fifo[(size_t)v * e->Q + (i % e->Q)]);
+    for (uint32_t i = s->fifo_head; i != s->fifo_stored; i++) h = feed_job(h, &e->fifo[(size_t)v * e->Q + (i % e->Q)]);
     h = feed(h, 0xF1F0);
-    for (uint32_t i = s->sleep_head; i != s->sleep_tail; i++) h = feed_job(h, &e->sleep[(size_t)v * e->SQ + (i % e->SQ)]);
+    h = feed(h, (uint64_t)(s->fifo_tail - s->fifo_stored) | ((uint64_t)s->fifo_stored << 32));
+    for (uint32_t i = s->sleep_head; i != s->sleep_tail; i++) {
+      const gx_sleeper *z = &e->sleep[(size_t)v * e->SQ + (i % e->SQ)];
+      h = feed(h, feed_job(z->wake, &z->job));
+    }
     h = feed(h, 0x51EE);
     h = feed(h, s->dq_len);
     for (uint32_t i = 0; i < s->dq_len; i++) {
@@ -1882,7 +1938,7 @@ int gx_host_digests(gx_engine *e, uint64_t *out) {
     }
     h = feed(h, 0xA7E4);
     for (uint32_t a = 0; a < e->A; a++) {
-      if (!((s->arena_used >> a) & 1u)) continue;
+      if (!list_live(e, v, a)) continue;
       uint32_t len = e->arena_len[(size_t)v * e->A + a];
       h = feed(h, a);
       h = feed(h, len);

@@ -26,7 +26,7 @@ ALIVE, TOMBSTONE, UNHEALTHY, UNKNOWN, DRAINING, ABSENT = 0, 1, 2, 3, 4, 7
 SLOT_ABSENT = 7
 TS_SHIFT = 3
 
-JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE = 0, 1, 2, 3, 4
+JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE, JOB_LOST = 0, 1, 2, 3, 4, 5
 INIT_EMPTY, INIT_OWN, INIT_WARM = 0, 1, 2
 LIMIT_DEFAULT = 0xFFFFFFFF
 
@@ -45,23 +45,46 @@ class GxService(C.Structure):
 
 
 class GxJob(C.Structure):
-    _fields_ = [("a", C.c_uint64), ("b", C.c_uint64), ("c", C.c_uint32), ("meta", C.c_uint32),
-                ("wake", C.c_uint32), ("aux", C.c_uint32)]
+    """gx.h gx_job (16 B): meta = kind | pass << 3 | n_passes << 9 | owner << 15."""
+    _fields_ = [("a", C.c_uint64), ("c", C.c_uint32), ("meta", C.c_uint32)]
 
     @property
     def kind(self):
-        return self.meta & 0xFF
+        return self.meta & 7
 
     @property
     def pass_(self):
-        return (self.meta >> 8) & 0xFF
+        return (self.meta >> 3) & 63
 
     @property
     def n_passes(self):
-        return (self.meta >> 16) & 0xFF
+        return (self.meta >> 9) & 63
+
+    @property
+    def owner(self):
+        return self.meta >> 15
 
     def tup(self):
-        return (self.a, self.b, self.c, self.meta, self.wake, self.aux)
+        return (self.a, self.c, self.meta)
+
+
+class GxSleeper(C.Structure):
+    _fields_ = [("job", GxJob), ("wake", C.c_uint32), ("pad", C.c_uint32 * 3)]
+
+    @property
+    def kind(self):
+        return self.job.kind
+
+    @property
+    def pass_(self):
+        return self.job.pass_
+
+    @property
+    def n_passes(self):
+        return self.job.n_passes
+
+    def tup(self):
+        return self.job.tup() + (self.wake,)
 
 
 class GxParams(C.Structure):
@@ -112,7 +135,9 @@ class GxHostState(C.Structure):
     _fields_ = [("fifo_head", C.c_uint32), ("fifo_tail", C.c_uint32), ("sleep_head", C.c_uint32),
                 ("sleep_tail", C.c_uint32), ("dq_head", C.c_uint32), ("dq_len", C.c_uint32),
                 ("arena_used", C.c_uint32), ("flags", C.c_uint32), ("bs_next", C.c_int64),
-                ("bt_next", C.c_int64), ("last_bcast_ns", C.c_int64), ("running", C.c_uint64)]
+                ("bt_next", C.c_int64), ("last_bcast_ns", C.c_int64), ("running", C.c_uint64),
+                ("fifo_stored", C.c_uint32), ("nil_pos_bs", C.c_uint32), ("nil_pos_bt", C.c_uint32),
+                ("pad", C.c_uint32)]
 
 
 class GxStats(C.Structure):
@@ -126,7 +151,7 @@ class GxStats(C.Structure):
         ("listener_drops", C.c_uint64)] + [(n, C.c_uint64) for n in (
         "lost_packets", "fd_probes", "fd_probe_failures", "fd_suspicions", "fd_confirmations",
         "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received",
-        "fd_state_merges")]
+        "fd_state_merges", "queue_deferred")] + [("first_drop_round", C.c_int64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
@@ -236,7 +261,7 @@ def _declare(lib):
         "gx_write_slot": ([vp, u32, P(GxService)], i32),
         "gx_read_hosts": ([vp, u32, u32, P(GxHostState)], i32),
         "gx_read_queue": ([vp, u32, P(GxJob), u32, P(u32)], i32),
-        "gx_read_sleepers": ([vp, u32, P(GxJob), u32, P(u32)], i32),
+        "gx_read_sleepers": ([vp, u32, P(GxSleeper), u32, P(u32)], i32),
         "gx_read_pending": ([vp, u32, P(GxService), u32, P(u32)], i32),
         "gx_read_list": ([vp, u32, u32, P(GxService), u32, P(u32)], i32),
         "gx_host_digests": ([vp, vp], i32), "gx_stats_get": ([vp, P(GxStats)], i32),
@@ -618,7 +643,7 @@ class Engine:
     def sleepers(self, host: int):
         n = C.c_uint32()
         check(self.lib.gx_read_sleepers(self.h, host, None, 0, C.byref(n)))
-        out = (GxJob * max(1, n.value))()
+        out = (GxSleeper * max(1, n.value))()
         check(self.lib.gx_read_sleepers(self.h, host, out, n.value, C.byref(n)))
         return [out[i] for i in range(n.value)]
 

@@ -3,9 +3,10 @@
 // Layout in HBM (one engine = one GPU's cluster):
 //   view      u64 [H][R]      R = H*S packed slots (ts << 3 | status), one row per host view
 //   minexp    u64 [H]         lower bound of min over present slots of (ts + lifespan(status))
-//   hs        gx_host_state[H] per-host broadcast-queue / looper bookkeeping (64 B)
-//   fifo      gx_job [H][Q]   broadcast FIFO ring (the blocked senders of state.Broadcasts)
-//   sleep     gx_job [H][SQ]  SendServices passes sleeping TOMBSTONE_RETRANSMIT
+//   hs        gx_host_state[H] per-host broadcast-queue / looper bookkeeping (80 B)
+//   fifo      gx_job [H][Q]   broadcast FIFO ring: the stored window of the blocked senders of
+//                             state.Broadcasts (16 B jobs; later jobs are counted, gx.h gx_job)
+//   sleep     gx_sleeper [H][SQ] SendServices passes sleeping TOMBSTONE_RETRANSMIT
 //   dq        grec [H][DQ]    delegate pendingBroadcasts as a deque (push-front batch, pop packet)
 //   arena     grec [H][A][L]  SendServices lists (L = packet_cap + pending_cap)
 //   msg       grec [H][K][cap] this round's packets, msg_len/msg_dst [H][K]
@@ -71,7 +72,7 @@ enum {
   C_GOSSIP_MERGES, C_AE_MERGES, C_LOCAL_MERGES, C_GOSSIP_ACC, C_AE_ACC, C_LOCAL_ACC, C_STALE,
   C_RETX, C_QDROP, C_LDROP, C_SDROP, C_PDROP, C_DEQ, C_NIL, C_PACKETS, C_RECSENT, C_EXPIRED,
   C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_BYTESENT,
-  C_CAPCUT, C_CHG, C_NCTR
+  C_CAPCUT, C_CHG, C_QDEFER, C_NCTR
 };
 // Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
 enum {
@@ -89,6 +90,7 @@ struct DevCtr {
   unsigned long long last_change_p1[GX_SHARDS][8];  // last round with a slot change + 1
   unsigned long long bytes[GX_SHARDS][16];          // algorithmic HBM bytes per kernel class
   unsigned long long units[GX_SHARDS][16];          // slots / records per kernel class
+  unsigned long long first_drop[GX_SHARDS][8];      // first round a LOST job was dequeued (min; ~0 none)
 };
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
@@ -111,10 +113,12 @@ struct Dev {
   uint8_t *own_status;
   gx_host_state *hs;
   gx_job *fifo;
-  gx_job *sleep;
+  gx_sleeper *sleep;
   grec *dq;
   grec *arena;
   uint32_t *arena_len;
+  uint32_t AW;          // list bitmap words per host, ceil(A / 32)
+  uint32_t *arena_bits; // [Hl][AW] live lists (slots >= A stay set); hs.arena_used bit w = word w full
   grec *msg;
   uint64_t *msg_w0;    // [H*K][cap] the receiver's slot word each live record was filtered against
   uint32_t *msg_len;
@@ -167,10 +171,6 @@ struct Dev {
   uint64_t *snap;      // this round's k_send stores (round << 32 | work_cnt[GX_WC_SCANS]) here (pinned host memory), or null
   uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
   unsigned long long *kprof;  // diagnostics (env GX_KPROF): wall-clock phase marks of k_send per wave, or null
-  uint32_t ab;         // A/B measurement switches (env GX_AB_FLAGS, 0 = the shipped kernels): bit 2
-                       // expiry scans in k_scan, bit 3 owner ticks in k_owner (not inside k_send),
-                       // bit 4 default-policy storm stream, bit 5 default-policy k_ae, bit 7 the
-                       // receivers' own dead-record filter (k_merge_lean) instead of the senders'
 };
 
 // ------------------------------------------------------------------- schedule RNG (seeded) --
@@ -190,9 +190,6 @@ GXHD uint32_t unif(uint64_t x, uint32_t m) { return (uint32_t)(((x >> 32) * (uin
 GXHD int st_of(uint64_t w) { return (int)(w & 7u); }
 GXHD int64_t ts_of(uint64_t w) { return (int64_t)(w >> GX_TS_SHIFT); }
 GXHD uint64_t pack(int64_t ts, int st) { return ((uint64_t)ts << GX_TS_SHIFT) | (uint64_t)st; }
-GXHD uint32_t meta_of(int kind, uint32_t pass, uint32_t np) {
-  return (uint32_t)kind | (pass << 8) | (np << 16);
-}
 
 // Push-pull pairing bijection on [0, m): 4-round keyed Feistel + cycle walking.
 GXHD uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
@@ -394,47 +391,124 @@ GXD void svc_changed(const Dev &d, Acc &a, uint32_t v, uint32_t r, uint64_t nw, 
 }
 
 // ----------------------------------------------------------------------- broadcast FIFO --
-GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
-  if ((j.meta & 0xff) == GX_JOB_SEND) hst(d, v)->arena_used &= ~(1u << (j.c & 0xffff));
+// The unbuffered Broadcasts channel's blocked senders (services_state.go:94): the reference never
+// refuses one, so every push is accepted. The first Q jobs are stored; a job pushed while the
+// stored window is full, or behind a deferred job, is deferred (counted in place, contents
+// dropped); a looper's nil keeps its position (gx.h gx_job).
+GXD gx_job make_job(uint64_t a, uint32_t c, uint32_t meta) {
+  gx_job j;
+  j.a = a;
+  j.c = c;
+  j.meta = meta;
+  return j;
+}
+GXHD uint32_t meta_of(int kind, uint32_t pass, uint32_t np) { return GX_JOB_META((uint32_t)kind, pass, np, 0); }
+// Jobs a push of several may store at the tail: the window's free room, or 0 behind deferred jobs.
+GXD uint32_t fifo_room(const Dev &d, uint32_t head, uint32_t tail, uint32_t stored) {
+  return stored == tail ? d.Q - (stored - head) : 0u;
 }
 
-// The unbuffered Broadcasts channel's blocked senders (services_state.go:94) as a FIFO bounded
-// at Q jobs, 2 reserved for the loopers' nil sends.
-GXD bool push_job(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
-  gx_host_state *h = hst(d, v);
-  uint32_t count = h->fifo_tail - h->fifo_head;
-  bool nil = (j.meta & 0xff) <= GX_JOB_NIL_BT;
-  uint32_t limit = nil ? d.Q : d.Q - 2;
-  if (count >= limit) {
-    a.c[C_QDROP]++;
-    free_list(d, v, j);
-    return false;
+// List arena: the lowest free slot, a two-level bitmap (hs.arena_used bit w = bitmap word w full).
+// The bitmap word is read and written by one lane of the host's team (lane0).
+GXD uint32_t *list_bits(const Dev &d, uint32_t vi, uint32_t w) { return &d.arena_bits[(size_t)vi * d.AW + w]; }
+GXD void list_release(const Dev &d, uint32_t vi, uint32_t &arena_used, uint32_t slot, bool lane0) {
+  if (lane0) *list_bits(d, vi, slot >> 5) &= ~(1u << (slot & 31));
+  arena_used &= ~(1u << (slot >> 5));
+}
+// Allocates on the team-uniform register copy `arena_used`; -1 when every slot is live. Every
+// lane of the team of T lanes calls it; the team's lane 0 loads and stores the word.
+template <int T = 1>
+GXD int list_alloc(const Dev &d, uint32_t vi, uint32_t &arena_used, bool lane0) {
+  const uint32_t wfree = ~arena_used & (d.AW >= 32 ? 0xffffffffu : ((1u << d.AW) - 1u));
+  if (!wfree) return -1;
+  const uint32_t w = (uint32_t)__builtin_ctz(wfree);
+  uint32_t *p = list_bits(d, vi, w);
+  uint32_t word = lane0 ? *p : 0u;
+  if (T > 1) word = (uint32_t)__shfl((int)word, 0, T);
+  const uint32_t b = (uint32_t)__builtin_ctz(~word), nw = word | (1u << b);
+  if (lane0) *p = nw;
+  if (nw == 0xffffffffu) arena_used |= 1u << w;
+  return (int)(w * 32 + b);
+}
+GXD void free_list_r(const Dev &d, uint32_t vi, gx_host_state &hs, const gx_job &j, bool lane0) {
+  if (GX_JOB_KIND(j.meta) == GX_JOB_SEND) list_release(d, vi, hs.arena_used, j.c & 0xffff, lane0);
+}
+
+// The FIFO pushes of one host, on its register copy `hs` (the whole team holds the same copy;
+// lane 0 stores).
+GXD void push_job_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const gx_job &j, bool lane0) {
+  const uint32_t kind = GX_JOB_KIND(j.meta);
+  if (kind == GX_JOB_NIL_BS) hs.nil_pos_bs = hs.fifo_tail;
+  else if (kind == GX_JOB_NIL_BT) hs.nil_pos_bt = hs.fifo_tail;
+  if (fifo_room(d, hs.fifo_head, hs.fifo_tail, hs.fifo_stored)) {
+    if (lane0) d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_tail % d.Q)] = j;
+    hs.fifo_stored++;
+  } else {
+    if (lane0) a.c[C_QDEFER]++;
+    free_list_r(d, li(d, v), hs, j, lane0);  // only a LOST dequeue could reach it
   }
-  d.fifo[(size_t)li(d, v) * d.Q + (h->fifo_tail % d.Q)] = j;
-  h->fifo_tail++;
-  return true;
+  hs.fifo_tail++;
 }
-
-GXD void push_sleep(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
-  gx_host_state *h = hst(d, v);
-  if (h->sleep_tail - h->sleep_head >= d.SQ) {
-    a.c[C_SDROP]++;
-    free_list(d, v, j);
+GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const gx_job &j, uint32_t wake,
+                      bool lane0) {
+  if (hs.sleep_tail - hs.sleep_head >= d.SQ) {
+    if (lane0) a.c[C_SDROP]++;
+    free_list_r(d, li(d, v), hs, j, lane0);
     return;
   }
-  d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_tail % d.SQ)] = j;
-  h->sleep_tail++;
+  if (lane0) {
+    gx_sleeper z;
+    z.job = j;
+    z.wake = wake;
+    z.pad[0] = z.pad[1] = z.pad[2] = 0;
+    d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail % d.SQ)] = z;
+  }
+  hs.sleep_tail++;
+}
+// Scalar forms (one thread owns host v's bookkeeping).
+GXD void push_job(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
+  gx_host_state *h = hst(d, v);
+  gx_host_state hs = *h;
+  push_job_r(d, a, v, hs, j, true);
+  *h = hs;
+}
+GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
+  gx_host_state *h = hst(d, v);
+  uint32_t au = h->arena_used;
+  if (GX_JOB_KIND(j.meta) == GX_JOB_SEND) list_release(d, li(d, v), au, j.c & 0xffff, true);
+  h->arena_used = au;
 }
 
 // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO tail.
 GXD void wake_host(const Dev &d, Acc &a, uint32_t v) {
   gx_host_state *h = hst(d, v);
-  while (h->sleep_head != h->sleep_tail) {
-    gx_job j = d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_head % d.SQ)];
-    if ((int64_t)j.wake > d.round) break;
-    h->sleep_head++;
-    push_job(d, a, v, j);
+  gx_host_state hs = *h;
+  while (hs.sleep_head != hs.sleep_tail) {
+    const gx_sleeper &z = d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_head % d.SQ)];
+    if ((int64_t)z.wake > d.round) break;
+    const gx_job j = z.job;
+    hs.sleep_head++;
+    push_job_r(d, a, v, hs, j, true);
   }
+  *h = hs;
+}
+
+// Take the FIFO head (fifo_head != fifo_tail) on the register copy: a stored job, or, past the
+// stored window, a looper's nil at its kept position, else LOST (the caller counts it). `pj`:
+// the head job when the caller loaded it ahead (stored jobs only).
+GXD gx_job pop_job_r(const Dev &d, uint32_t vi, gx_host_state &hs, const gx_job *pj) {
+  const uint32_t p = hs.fifo_head++;
+  if (p != hs.fifo_stored) return pj ? *pj : d.fifo[(size_t)vi * d.Q + (p % d.Q)];
+  hs.fifo_stored = hs.fifo_head;  // the stored window restarts behind the deferred job
+  uint32_t kind = GX_JOB_LOST;
+  if ((hs.flags & 1u) && p == hs.nil_pos_bs) kind = GX_JOB_NIL_BS;
+  else if ((hs.flags & 2u) && p == hs.nil_pos_bt) kind = GX_JOB_NIL_BT;
+  return make_job(0, 0, meta_of((int)kind, 0, 1));
+}
+GXD void count_lost(const Dev &d, Acc &a, bool lane0) {
+  if (!lane0) return;
+  a.c[C_QDROP]++;
+  atomicMin(&d.ctr->first_drop[shard_id()][0], (unsigned long long)d.round);
 }
 
 // (base + k) % q for base < q and k < q, without a division
@@ -442,44 +516,37 @@ GXD uint32_t ring_add(uint32_t base, uint32_t k, uint32_t q) {
   const uint32_t x = base + k;
   return x >= q ? x - q : x;
 }
-GXD gx_job make_job(uint64_t a, uint64_t b, uint32_t c, uint32_t meta) {
-  gx_job j;
-  j.a = a;
-  j.b = b;
-  j.c = c;
-  j.meta = meta;
-  j.wake = 0;
-  j.aux = 0;
-  return j;
-}
 
-// Lowest free list slot, or -1 (list_drops).
+// Lowest free list slot, or -1 (the caller queues a LOST job: list_drops).
 GXD int alloc_list(const Dev &d, Acc &a, uint32_t v) {
-  uint32_t used = hst(d, v)->arena_used;
-  uint32_t free_bits = ~used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1));
-  if (!free_bits) {
-    a.c[C_LDROP]++;
-    return -1;
-  }
-  int slot = __builtin_ctz(free_bits);
-  hst(d, v)->arena_used = used | (1u << slot);
+  gx_host_state *h = hst(d, v);
+  uint32_t au = h->arena_used;
+  const int slot = list_alloc(d, li(d, v), au, true);
+  if (slot < 0) a.c[C_LDROP]++;
+  h->arena_used = au;
   return slot;
 }
 GXD grec *list_ptr(const Dev &d, uint32_t v, uint32_t slot) {
   return &d.arena[((size_t)li(d, v) * d.A + slot) * d.L];
 }
-// SendServices job over an allocated, filled list (services_state.go:579-604).
+// SendServices job over an allocated, filled list (services_state.go:579-604); slot < 0: the list
+// did not fit, the job is queued LOST.
 GXD void commit_send(const Dev &d, Acc &a, uint32_t v, int slot, uint32_t n, uint32_t npasses) {
-  d.arena_len[(size_t)li(d, v) * d.A + slot] = n;
-  a.c[C_SENDJOBS]++;
-  push_job(d, a, v, make_job(0, 0, (uint32_t)slot | (n << 16), meta_of(GX_JOB_SEND, 0, npasses)));
+  if (slot >= 0) d.arena_len[(size_t)li(d, v) * d.A + slot] = n;
+  push_job(d, a, v, slot >= 0 ? make_job(0, (uint32_t)slot | (n << 16), meta_of(GX_JOB_SEND, 0, npasses))
+                              : make_job(0, 0, meta_of(GX_JOB_LOST, 0, 1)));
+}
+// Whether the next push of host v is stored (a deferred SendServices job takes no list).
+GXD bool fifo_stores(const Dev &d, uint32_t v) {
+  const gx_host_state *h = hst(d, v);
+  return fifo_room(d, h->fifo_head, h->fifo_tail, h->fifo_stored) != 0;
 }
 
 GXD uint32_t job_len(const Dev &d, const gx_job &j) {
-  uint32_t kind = j.meta & 0xff;
+  uint32_t kind = GX_JOB_KIND(j.meta);
   if (kind == GX_JOB_RETX) return 1;
   if (kind == GX_JOB_SEND) return j.c >> 16;
-  if (kind == GX_JOB_EXPIRE) return (uint32_t)__popcll(j.b);
+  if (kind == GX_JOB_EXPIRE) return (uint32_t)__popcll(j.a);
   return 0;
 }
 
@@ -534,32 +601,6 @@ GXD uint32_t team_incl_scan(uint32_t x, uint32_t tl) {
   return x;
 }
 
-// The FIFO pushes of one host, on its register copy `hs` (the whole wave holds the same copy;
-// lane 0 stores).
-GXD void free_list_r(gx_host_state &hs, const gx_job &j) {
-  if ((j.meta & 0xff) == GX_JOB_SEND) hs.arena_used &= ~(1u << (j.c & 0xffff));
-}
-GXD void push_job_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const gx_job &j, bool lane0) {
-  uint32_t count = hs.fifo_tail - hs.fifo_head;
-  bool nil = (j.meta & 0xff) <= GX_JOB_NIL_BT;
-  if (count >= (nil ? d.Q : d.Q - 2)) {
-    if (lane0) a.c[C_QDROP]++;
-    free_list_r(hs, j);
-    return;
-  }
-  if (lane0) d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_tail % d.Q)] = j;
-  hs.fifo_tail++;
-}
-GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const gx_job &j, bool lane0) {
-  if (hs.sleep_tail - hs.sleep_head >= d.SQ) {
-    if (lane0) a.c[C_SDROP]++;
-    free_list_r(hs, j);
-    return;
-  }
-  if (lane0) d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail % d.SQ)] = j;
-  hs.sleep_tail++;
-}
-
 // GetBroadcasts (services_delegate.go:85-144) with packPacket (:186-223) by a team of T lanes
 // per host: the control state is the team-uniform register copy `hs`, the records move
 // lane-parallel. broadcast = batch ++ pendingBroadcasts is read as a virtual sequence (batch
@@ -576,15 +617,16 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
   const bool lane0 = tl == 0;
   const uint32_t mask = d.DQ - 1;
   grec *dq = &d.dq[(size_t)li(d, v) * d.DQ];
-  gx_job j = make_job(0, 0, 0, 0);
+  gx_job j = make_job(0, 0, 0);
   uint32_t m = 0;
   if (hs.fifo_head != hs.fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
-    j = pj ? *pj : d.fifo[(size_t)li(d, v) * d.Q + (hs.fifo_head % d.Q)];
-    hs.fifo_head++;
+    j = pop_job_r(d, li(d, v), hs, pj);
     if (lane0) a.c[C_DEQ]++;
     m = job_len(d, j);
-    uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff, np = (j.meta >> 16) & 0xff;
-    if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
+    uint32_t kind = GX_JOB_KIND(j.meta), pass = GX_JOB_PASS(j.meta), np = GX_JOB_NPASSES(j.meta);
+    if (kind == GX_JOB_LOST) {  // a deferred job reached the head: its batch is unknown
+      count_lost(d, a, lane0);
+    } else if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
       if (lane0) a.c[C_NIL]++;
       hs.flags &= ~1u;
       hs.bs_next = d.round + d.p.alive_interval_rounds;
@@ -595,23 +637,18 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
     } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
       if (pass + 1 < np) {  // the looper re-arms (services_state.go:585-601)
         gx_job nj = j;
-        nj.meta = meta_of((int)kind, pass + 1, np);
-        if (d.p.retransmit_rounds == 0) {
-          nj.wake = (uint32_t)d.round;
-          push_job_r(d, a, v, hs, nj, lane0);
-        } else {
-          nj.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
-          push_sleep_r(d, a, v, hs, nj, lane0);
-        }
+        nj.meta = GX_JOB_META(kind, pass + 1, np, GX_JOB_OWNER(j.meta));
+        if (d.p.retransmit_rounds == 0) push_job_r(d, a, v, hs, nj, lane0);
+        else push_sleep_r(d, a, v, hs, nj, (uint32_t)(d.round + d.p.retransmit_rounds), lane0);
       } else {
-        free_list_r(hs, j);  // the list is read below; nothing reallocates it in this call
+        free_list_r(d, li(d, v), hs, j, lane0);  // the list is read below; nothing reallocates it in this call
       }
     }
   } else if (hs.dq_len == 0) {  // default: nothing pending (:96-98)
     return 0;
   }
   const uint32_t head = hs.dq_head, n = m + hs.dq_len;
-  const uint32_t kind = j.meta & 0xff, pass = (j.meta >> 8) & 0xff;
+  const uint32_t kind = GX_JOB_KIND(j.meta), pass = GX_JOB_PASS(j.meta);
   const uint64_t dw = ((uint64_t)pass * (uint64_t)d.p.pass_increment_ns) << GX_TS_SHIFT;
   auto item = [&](uint32_t i) -> grec {  // element i of batch ++ pendingBroadcasts
     grec g;
@@ -624,9 +661,9 @@ GXD uint32_t get_broadcasts_team(const Dev &d, Acc &a, uint32_t v, gx_host_state
       grec s = list_ptr(d, v, j.c & 0xffff)[i];
       g.w = s.w + dw;
       g.r = s.r;
-    } else {  // EXPIRE: the i-th tombstoned service of the owner
-      g.w = pack((int64_t)j.a, GX_TOMBSTONE) + dw;
-      g.r = j.c * d.S + nth_set_bit(j.b, i);
+    } else {  // EXPIRE: the i-th tombstoned service of the owner, at the call's now
+      g.w = pack(d.p.t0_ns + (int64_t)j.c * d.p.round_ns, GX_TOMBSTONE) + dw;
+      g.r = GX_JOB_OWNER(j.meta) * d.S + nth_set_bit(j.a, i);
     }
     return g;
   };
@@ -761,7 +798,8 @@ GXD bool add_entry(const Dev &d, Acc &a, uint32_t v, grec u, int src) {
   }
   a.c[src == SRC_GOSSIP ? C_GOSSIP_ACC : src == SRC_AE ? C_AE_ACC : C_LOCAL_ACC]++;
   if (u.r / d.S != v) {  // retransmit foreign records only (services_state.go:377-392)
-    if (push_job(d, a, v, make_job(nw, 0, u.r, meta_of(GX_JOB_RETX, 0, 1)))) a.c[C_RETX]++;
+    push_job(d, a, v, make_job(nw, u.r, meta_of(GX_JOB_RETX, 0, 1)));
+    a.c[C_RETX]++;
   }
   return true;
 }
@@ -841,7 +879,7 @@ GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
   d.vlc[li(d, v)] = ts_of(nw);
   a.c[C_CHG] += (unsigned)__popcll(mask);
   a.c[C_EXPSRV]++;
-  push_job(d, a, v, make_job((uint64_t)d.now, mask, o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count)));
+  push_job(d, a, v, make_job(mask, (uint32_t)d.round, GX_JOB_META(GX_JOB_EXPIRE, 0, d.p.tombstone_count, o)));
   return true;
 }
 
@@ -868,16 +906,23 @@ GXD void bs_body_list(const Dev &d, Acc &a, uint32_t o, const grec *list, uint32
   inc_out = inc;
   if (inc) {
     h->last_bcast_ns = d.now;
-    int slot = alloc_list(d, a, o);
-    if (slot >= 0) {
-      grec *dst = list_ptr(d, o, slot);
-      uint32_t m = 0;
-      for (uint32_t i = 0; i < n && m < d.L; i++)
-        if ((inc >> i) & 1ull) dst[m++] = list[i];
+    a.c[C_SENDJOBS]++;
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n && m < d.L; i++) m += (inc >> i) & 1ull;
+    if (!fifo_stores(d, o)) {  // deferred: no list
+      push_job(d, a, o, make_job(0, 0, meta_of(GX_JOB_SEND, 0, any_new ? d.p.alive_count : 1)));
+    } else {
+      int slot = alloc_list(d, a, o);
+      if (slot >= 0) {
+        grec *dst = list_ptr(d, o, slot);
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < n && k < d.L; i++)
+          if ((inc >> i) & 1ull) dst[k++] = list[i];
+      }
       commit_send(d, a, o, slot, m, any_new ? d.p.alive_count : 1);  // ALIVE_COUNT if new (:555-558)
     }
   } else {
-    push_job(d, a, o, make_job(0, 0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)));  // Broadcasts <- nil (:569)
+    push_job(d, a, o, make_job(0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)));  // Broadcasts <- nil (:569)
     h->flags |= 1u;  // the looper blocks until the nil is consumed
   }
 }
@@ -889,7 +934,11 @@ GXD void bt_finish(const Dev &d, Acc &a, uint32_t o, uint64_t running, const gre
   uint64_t own = tombstone_services(d, a, o, running);
   uint32_t n_own = 2u * (uint32_t)__popcll(own);
   if (n_own + n_others > 0) {
-    int slot = alloc_list(d, a, o);
+    a.c[C_SENDJOBS]++;
+    int slot = fifo_stores(d, o) ? alloc_list(d, a, o) : -2;  // a deferred job takes no list
+    const uint32_t len = n_own + n_others < d.L ? n_own + n_others : d.L;
+    if (slot == -2) push_job(d, a, o, make_job(0, 0, meta_of(GX_JOB_SEND, 0, d.p.tombstone_count)));
+    else if (slot < 0) commit_send(d, a, o, slot, len, d.p.tombstone_count);
     if (slot >= 0) {
       grec *dst = list_ptr(d, o, slot);
       uint32_t m = 0;
@@ -907,7 +956,7 @@ GXD void bt_finish(const Dev &d, Acc &a, uint32_t o, uint64_t running, const gre
     }
     h->bt_next = d.round + d.p.tombstone_interval_rounds;
   } else {
-    push_job(d, a, o, make_job(0, 0, 0, meta_of(GX_JOB_NIL_BT, 0, 1)));  // Broadcasts <- nil (:628)
+    push_job(d, a, o, make_job(0, 0, meta_of(GX_JOB_NIL_BT, 0, 1)));  // Broadcasts <- nil (:628)
     h->flags |= 2u;
   }
 }

@@ -362,11 +362,10 @@ static int round_send_impl(gx_engine *e) {
   const bool bt_apart = d.p.fd_enable || storm;
   // a round without the detector or the storm: owner ticks, expiry scans and sends in one launch
   // (S <= 16: owner teams of the send's 4 lanes with up to 4 services each)
-  const bool fused = !bt_apart && d.K && d.S <= 16 && !(d.ab & 8u) && !e->scan_heavy;
+  const bool fused = !bt_apart && d.K && d.S <= 16 && !e->scan_heavy;
   // planned GetBroadcasts (send_planned): record budget, no detector or departures, re-armed
-  // passes sleep, senders' filter; teams of 4 lanes per host (A/B bit 256: the per-call path)
-  const bool plan = !d.p.limit_bytes && d.p.retransmit_rounds > 0 && d.sfilt && !d.departures && !d.p.fd_enable &&
-                    !(d.ab & 256u);
+  // passes sleep; teams of 4 lanes per host
+  const bool plan = !d.p.limit_bytes && d.p.retransmit_rounds > 0 && !d.departures && !d.p.fd_enable;
   if (fused && plan) {
     LaunchTimer t(e, GX_K_SEND);
     const unsigned g = nblk(d.Hl, 64);
@@ -408,7 +407,7 @@ static int round_send_impl(gx_engine *e) {
     owner_launch(d, s);
   }
   // with the tick finished in k_send, the expiry scans run in k_send's prologue (no k_scan launch)
-  const bool scan_in_send = !bt_apart && d.K && !(d.ab & 4u) && !e->scan_heavy;
+  const bool scan_in_send = !bt_apart && d.K && !e->scan_heavy;
   if (!scan_in_send) {
     LaunchTimer t(e, GX_K_SCAN);
     const bool ev = !e->log_views.empty();
@@ -424,10 +423,9 @@ static int round_send_impl(gx_engine *e) {
   if (storm) {
     LaunchTimer t(e, GX_K_STORM);
     const bool ev = !e->log_views.empty();
-    const bool nt = !(d.ab & 16u);  // nontemporal row stream (A/B bit 16: default loads/stores)
+    // nontemporal row stream: 30.3 -> 27.9 ms at cfg 5 (profiles/ab/storm_nt_ab_r02.log)
     if (d.S >= 2 && 64 % d.S == 0)
-      (ev ? (nt ? k_storm_p2<true, true> : k_storm_p2<true, false>)
-          : (nt ? k_storm_p2<false, true> : k_storm_p2<false, false>))<<<d.Hl, 256, 0, s>>>(d);
+      (ev ? k_storm_p2<true, true> : k_storm_p2<false, true>)<<<d.Hl, 256, 0, s>>>(d);
     else (ev ? k_storm<true> : k_storm<false>)<<<d.Hl, 256, 0, s>>>(d);
   }
   {
@@ -469,36 +467,19 @@ static int round_merge_impl(gx_engine *e) {
   if (d.K) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
-    if (!d.sfilt) k_merge_lean<<<nblk(d.Hl, 256 / LEAN_LPR), 256, 0, s>>>(d);  // else the senders filtered
-    if (d.ab & 2048u) {  // A/B: round 2's merge (consecutive receivers, a wave's fallbacks in turn)
-      const unsigned g = nblk(d.Hl, MERGE_WAVES * (64 / MERGE_SEG));
-      if (d.R < (1u << 26)) (ev ? k_merge_seg_v1<true, true> : k_merge_seg_v1<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      else (ev ? k_merge_seg_v1<false, true> : k_merge_seg_v1<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-    } else if (!(d.ab & 512u)) {  // receivers routed by their live records (A/B bit 512: a wave each)
-      // 4 waves per SIMD (22 spilled registers) measured within noise of 3 (profiles/r03/ab).
-      // GossipMessages > 1: inboxes of hundreds of live records, each folded by a whole wave tile by
-      // tile, so more waves in flight (16 receivers per block); else 64 per block (3% faster at
-      // cfg 5). A/B bit 4096: the other choice.
-      const bool small = (d.NG > 1) != ((d.ab & 4096u) != 0);
-      const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
-      // (GossipMessages > 1: 4 waves per SIMD, 22 spilled registers, 10% faster than 3 in the GM 15
-      // accepting stretch, profiles/r03/ab/merge_wpe_gm15.jsonl; A/B bit 8192: 6)
-      if (small && (d.ab & 8192u)) {
-        if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, 6> : k_merge_seg<true, false, 16, 6>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-        else (ev ? k_merge_seg<false, true, 16, 6> : k_merge_seg<false, false, 16, 6>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      } else if (small) {
-        if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, 4> : k_merge_seg<true, false, 16, 4>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-        else (ev ? k_merge_seg<false, true, 16, 4> : k_merge_seg<false, false, 16, 4>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      } else if (d.R < (1u << 26)) {
-        (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      } else {
-        (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      }
+    // receivers routed by their live records. GossipMessages > 1: inboxes of hundreds of live
+    // records, each folded by a whole wave tile by tile, so more waves in flight (16 receivers per
+    // block, 4 waves per SIMD: 10% faster than 3 in the GM 15 accepting stretch,
+    // profiles/r03/ab/merge_wpe_gm15.jsonl); else 64 receivers per block (3% faster at cfg 5)
+    const bool small = d.NG > 1;
+    const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
+    if (small) {
+      if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, 4> : k_merge_seg<true, false, 16, 4>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      else (ev ? k_merge_seg<false, true, 16, 4> : k_merge_seg<false, false, 16, 4>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+    } else if (d.R < (1u << 26)) {
+      (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else {
-      const unsigned g = nblk(d.Hl, MERGE_WAVES * MERGE_RANGE_DEF);
-      // 2 or 4 receivers per wave measured 14.2 / 13.7 vs 14.3 us (profiles/r02/gossip)
-      if (d.R < (1u << 26)) (ev ? k_merge<true, true> : k_merge<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);  // 32-bit keys
-      else (ev ? k_merge<false, true> : k_merge<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      (ev ? k_merge_seg<false, true> : k_merge_seg<false, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     }
   }
   if (d.p.fd_enable && d.K) {  // the packets' memberlist messages, after the catalog merge
@@ -599,10 +580,8 @@ static int ae_whole_impl(gx_engine *e) {
       // PF = 1: deeper prefetch measured within noise (profiles/ae_variants.sh)
       // the ChangeEvent variant only while some view has a listener
       const bool ev = !e->log_views.empty();
-      // nontemporal row loads and stores: -1% over the bench window (profiles/ab/ae_nt_ab_r02.log);
-      // A/B bit 32: default cache policy
-      if (vec && !ev && (d.ab & 32u)) k_ae<true><<<np, 256, 0, s>>>(d, key0, key1);
-      else if (vec && !ev) k_ae<true, 1, true, true><<<np, 256, 0, s>>>(d, key0, key1);
+      // nontemporal row loads and stores: -1% over the bench window (profiles/ab/ae_nt_ab_r02.log)
+      if (vec && !ev) k_ae<true, 1, true, true><<<np, 256, 0, s>>>(d, key0, key1);
       else if (vec) k_ae_ev<true><<<np, 256, 0, s>>>(d, key0, key1);
       else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
       else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);
@@ -720,10 +699,13 @@ int gx_fd_defaults(gx_params *p) {
 static int check_params(const gx_params *p) {
   if (!p || p->n_hosts < 1 || p->n_services < 1 || p->n_services > 64) return GX_EINVAL;
   if (p->fanout > 16 || p->packet_cap < 1 || p->packet_cap > 256 || p->pending_cap > 256) return GX_EINVAL;
-  if (p->queue_cap < 3 || p->list_slots < 1 || p->list_slots > 32) return GX_EINVAL;
+  if (p->queue_cap < 1 || p->list_slots < 1 || p->list_slots > GX_MAX_LIST_SLOTS) return GX_EINVAL;
+  if (p->n_hosts > GX_MAX_HOSTS) return GX_EINVAL;  // gx_job owner field
   if (p->alive_interval_rounds < 1 || p->tombstone_interval_rounds < 1) return GX_EINVAL;
   if (p->retransmit_rounds > 1000) return GX_EINVAL;
-  if (p->alive_count < 1 || p->alive_count > 255 || p->tombstone_count < 1 || p->tombstone_count > 255) return GX_EINVAL;
+  if (p->alive_count < 1 || p->alive_count > GX_JOB_MAX_PASSES || p->tombstone_count < 1 ||
+      p->tombstone_count > GX_JOB_MAX_PASSES)
+    return GX_EINVAL;
   if (p->init_mode > GX_INIT_WARM) return GX_EINVAL;
   if (p->t0_ns < 0 || p->t0_ns > ((int64_t)1 << 62) || p->round_ns <= 0) return GX_EINVAL;
   {  // lifespans stay far inside the half window before t0 (gx.h GX_TS_SHIFT)
@@ -893,10 +875,12 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.own_status, H * d.S);
   ALLOC(d.hs, sizeof(gx_host_state) * H);
   ALLOC(d.fifo, sizeof(gx_job) * H * d.Q);
-  ALLOC(d.sleep, sizeof(gx_job) * H * d.SQ);
+  ALLOC(d.sleep, sizeof(gx_sleeper) * H * d.SQ);
   ALLOC(d.dq, sizeof(grec) * H * d.DQ);
   ALLOC(d.arena, sizeof(grec) * H * d.A * d.L);
   ALLOC(d.arena_len, sizeof(uint32_t) * H * d.A);
+  d.AW = (d.A + 31) / 32;
+  ALLOC(d.arena_bits, sizeof(uint32_t) * H * d.AW);
   ALLOC(d.msg, sizeof(grec) * Hg * K * p->packet_cap);
   ALLOC(d.msg_w0, sizeof(uint64_t) * Hg * K * p->packet_cap);
   ALLOC(d.msg_len, sizeof(uint32_t) * Hg * K);
@@ -908,12 +892,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   // wave merge takes the wide inboxes instead of the serial overflow path
   d.DI = p->inbox_slots ? p->inbox_slots : (d.NG > 1 ? GX_DI_MAX : 64);
   d.DR = d.DI < 8 ? d.DI : 8;  // inline packets: 99.6% of Poisson(fanout 3) in-degrees fit 8 slots
-  d.ab = getenv("GX_AB_FLAGS") ? (uint32_t)atoi(getenv("GX_AB_FLAGS")) : 0;  // A/B measurements only
-  if (d.ab) fprintf(stderr, "gx: GX_AB_FLAGS=%u: A/B measurement kernel paths active\n", d.ab);
   // senders read their local receivers' view slots and drop no-op records; packets from other
-  // shards are filtered the same way on arrival (k_inbox_unpack). A/B bit 128: the receivers' own
-  // filter pass (k_merge_lean) instead.
-  d.sfilt = !(d.ab & 128u) ? 1u : 0u;
+  // shards are filtered the same way on arrival (k_inbox_unpack)
+  d.sfilt = 1u;
   ALLOC(d.in_hdr, sizeof(uint4) * H * d.DI);
   ALLOC(d.in_ovf, sizeof(uint4) * Hg * K);
   ALLOC(d.in_rec, sizeof(grec) * H * d.DR * p->packet_cap);
@@ -995,6 +976,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   uint64_t *rec_word = nullptr;
   ALLOC(rec_word, sizeof(uint64_t) * d.R);
   HIPCHK(hipMemsetAsync(d.ctr, 0, sizeof(DevCtr), s));
+  HIPCHK(hipMemsetAsync(d.ctr->first_drop, 0xff, sizeof(d.ctr->first_drop), s));  // min: none yet
   HIPCHK(hipMemsetAsync(d.arena_len, 0, sizeof(uint32_t) * H * d.A, s));
   HIPCHK(hipMemsetAsync(d.msg_len, 0, sizeof(uint32_t) * Hg * K, s));
   HIPCHK(hipMemsetAsync(e->in_cnt_buf, 0, sizeof(uint32_t) * 2 * H, s));
@@ -1023,7 +1005,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
 }
 
 int gx_set_round(gx_engine *e, int64_t round) {
-  if (!e || round < e->d.round) return GX_EINVAL;
+  if (!e || round < e->d.round || round >= GX_MAX_ROUND) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   if (round != e->d.round) {  // a jump: this round's and the next round's counters start empty
     HIPCHK(hipMemsetAsync(e->in_cnt_buf, 0, sizeof(uint32_t) * 2 * e->d.Hl, e->stream));
@@ -1048,7 +1030,7 @@ int gx_enable_timing(gx_engine *e, int on) {
 }
 
 int gx_run_rounds(gx_engine *e, uint32_t n_rounds) {
-  if (!e || e->d.G > 1) return GX_EINVAL;
+  if (!e || e->d.G > 1 || e->d.round + n_rounds >= GX_MAX_ROUND) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   for (uint32_t i = 0; i < n_rounds; i++) {
     int rc = run_one_round(e);
@@ -1219,7 +1201,7 @@ int gx_expire_server(gx_engine *e, uint32_t view, uint32_t owner, int *expired) 
 int gx_notify_leave(gx_engine *e, uint32_t view, uint32_t node) { return gx_expire_server(e, view, node, nullptr); }
 
 int gx_send_services(gx_engine *e, uint32_t host, const gx_service *svcs, uint32_t n, uint32_t n_passes) {
-  if (!e || !own(e, host) || (n && !svcs) || n_passes < 1 || n_passes > 255) return GX_EINVAL;
+  if (!e || !own(e, host) || (n && !svcs) || n_passes < 1 || n_passes > GX_JOB_MAX_PASSES) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
   grec *drec;
   int rc = stage_recs(e, svcs, n, 0, &drec);
@@ -1674,32 +1656,34 @@ int gx_read_hosts(gx_engine *e, uint32_t lo, uint32_t hi, gx_host_state *out) {
   return GX_OK;
 }
 
-static int read_ring(gx_engine *e, const gx_job *base, uint32_t ring, uint32_t head, uint32_t n, gx_job *out,
-                     uint32_t cap) {
-  uint32_t m = n < cap ? n : cap;
-  for (uint32_t i = 0; i < m;) {
-    uint32_t idx = (head + i) % ring;
-    uint32_t run = ring - idx;
-    if (run > m - i) run = m - i;
-    HIPCHK(hipMemcpy(&out[i], &base[idx], sizeof(gx_job) * run, hipMemcpyDeviceToHost));
-    i += run;
+#define GX_READ_RING(J)                                                                                     \
+  static int read_ring(gx_engine *e, const J *base, uint32_t ring, uint32_t head, uint32_t n, J *out, uint32_t cap) { \
+    uint32_t m = n < cap ? n : cap;                                                                         \
+    for (uint32_t i = 0; i < m;) {                                                                          \
+      uint32_t idx = (head + i) % ring;                                                                     \
+      uint32_t run = ring - idx;                                                                            \
+      if (run > m - i) run = m - i;                                                                         \
+      HIPCHK(hipMemcpy(&out[i], &base[idx], sizeof(J) * run, hipMemcpyDeviceToHost));                      \
+      i += run;                                                                                             \
+    }                                                                                                       \
+    return GX_OK;                                                                                           \
   }
-  return GX_OK;
-}
-
+GX_READ_RING(gx_job)
+GX_READ_RING(gx_sleeper)
+#undef GX_READ_RING
 int gx_read_queue(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
   if (!e || !own(e, host) || (cap && !out)) return GX_EINVAL;
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
   if (rc) return rc;
-  uint32_t n = h.fifo_tail - h.fifo_head;
+  uint32_t n = h.fifo_stored - h.fifo_head;  // the stored jobs (gx.h)
   rc = read_ring(e, &e->d.fifo[(size_t)(host - e->d.lo) * e->d.Q], e->d.Q, h.fifo_head % e->d.Q, n, out, cap);
   if (rc) return rc;
   if (n_out) *n_out = n;
   return GX_OK;
 }
 
-int gx_read_sleepers(gx_engine *e, uint32_t host, gx_job *out, uint32_t cap, uint32_t *n_out) {
+int gx_read_sleepers(gx_engine *e, uint32_t host, gx_sleeper *out, uint32_t cap, uint32_t *n_out) {
   if (!e || !own(e, host) || (cap && !out)) return GX_EINVAL;
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
@@ -1728,8 +1712,10 @@ int gx_read_list(gx_engine *e, uint32_t host, uint32_t slot, gx_service *out, ui
   gx_host_state h;
   int rc = gx_read_hosts(e, host, host + 1, &h);
   if (rc) return rc;
-  uint32_t n = 0;
-  if ((h.arena_used >> slot) & 1u)
+  uint32_t n = 0, bits = 0;
+  HIPCHK(hipMemcpy(&bits, &e->d.arena_bits[(size_t)(host - e->d.lo) * e->d.AW + slot / 32], sizeof(uint32_t),
+                   hipMemcpyDeviceToHost));
+  if ((bits >> (slot % 32)) & 1u)
     HIPCHK(hipMemcpy(&n, &e->d.arena_len[(size_t)(host - e->d.lo) * e->d.A + slot], sizeof(uint32_t), hipMemcpyDeviceToHost));
   uint32_t m = n < cap ? n : cap;
   if (m) {
@@ -2300,7 +2286,7 @@ int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
 }
 
 static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *last_p1, unsigned long long *bytes,
-                    unsigned long long *units) {
+                    unsigned long long *units, unsigned long long *first_drop = nullptr) {
   std::vector<DevCtr> tmp(1);
   HIPCHK(hipMemcpyAsync(tmp.data(), e->d.ctr, sizeof(DevCtr), hipMemcpyDeviceToHost, e->stream));
   int rc = sync_check(e);
@@ -2309,7 +2295,9 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
   for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] = 0;
   for (int i = 0; i < 16; i++) bytes[i] = units[i] = 0;
   *last_p1 = 0;
+  if (first_drop) *first_drop = ~0ull;
   for (int s = 0; s < GX_SHARDS; s++) {
+    if (first_drop && x.first_drop[s][0] < *first_drop) *first_drop = x.first_drop[s][0];
     for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] += x.c[s][i];
     for (int i = 0; i < 16; i++) {
       bytes[i] += x.bytes[s][i];
@@ -2323,10 +2311,12 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
 int gx_stats_get(gx_engine *e, gx_stats *out) {
   if (!e || !out) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[16], units[16];
-  int rc = read_ctr(e, c, &lp1, bytes, units);
+  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[16], units[16], fdr;
+  int rc = read_ctr(e, c, &lp1, bytes, units, &fdr);
   if (rc) return rc;
   memset(out, 0, sizeof(*out));
+  out->queue_deferred = c[C_QDEFER];
+  out->first_drop_round = fdr == ~0ull ? -1 : (int64_t)fdr;
   out->lost_packets = c[C_LOST];
   out->fd_probes = c[C_FD_PROBES];
   out->fd_probe_failures = c[C_FD_PROBE_FAIL];

@@ -133,6 +133,8 @@ __global__ void k_init_hosts(Dev d) {
   h.running = d.S == 64 ? ~0ull : ((1ull << d.S) - 1);
   d.hs[idx] = h;
   for (uint32_t s = 0; s < d.S; s++) d.own_status[(size_t)idx * d.S + s] = GX_ALIVE;
+  for (uint32_t w = 0; w < d.AW; w++)  // list slots past list_slots never free
+    d.arena_bits[(size_t)idx * d.AW + w] = d.A >= 32 * (w + 1) ? 0u : ~0u << (d.A - 32 * w);
 }
 
 // Exact per-view expiry bound (one block per view): used at create and after raw imports.
@@ -164,15 +166,18 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
       hs.sleep_head = c.z;
       hs.sleep_tail = c.w;
       hs.arena_used = h->arena_used;
+      hs.fifo_stored = h->fifo_stored;
       const uint32_t au0 = hs.arena_used;
-      while (hs.sleep_head != hs.sleep_tail) {
-        gx_job j = d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
-        if ((int64_t)j.wake > d.round) break;
+      while (hs.sleep_head != hs.sleep_tail) {  // re-armed passes: SEND / EXPIRE, never a nil
+        const gx_sleeper &z = d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
+        if ((int64_t)z.wake > d.round) break;
+        const gx_job j = z.job;
         hs.sleep_head++;
         push_job_r(d, a, d.lo + idx, hs, j, true);
       }
       if (hs.sleep_head != c.z) {
         h->fifo_tail = hs.fifo_tail;
+        h->fifo_stored = hs.fifo_stored;
         h->sleep_head = hs.sleep_head;
         if (hs.arena_used != au0) h->arena_used = hs.arena_used;
       }
@@ -202,14 +207,14 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
 // sleep-ring head, in the same round trip) and hands its register copy of the bookkeeping to the
 // sends, which then neither reload it nor wait for the jobs.
 struct TickFwd {
-  gx_job *pj;         // the team's T LDS job slots
+  gx_job *pj;         // the team's T LDS job slots (stored FIFO head jobs)
   uint32_t *peers;    // the team's peer slots (count in [16]), sampled while the tick's loads fly
   gx_host_state hs;   // the bookkeeping after the tick
   uint32_t pf0, npf;  // FIFO position of pj[0], jobs loaded
   uint32_t tick;      // d.tick[idx] as the tick set it
 };
 template <int T, int SPL = 1, bool FWD = false>
-GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd) {
+GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd &fwd) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lead = tl == 0;
   const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
@@ -245,8 +250,8 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd
     }
     if (tl == 0) mexp0 = d.minexp[idx];
     if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
-    if (FWD) {  // the tick pushes at the FIFO tail only: the jobs at the head stay where they are
-      const uint32_t q = hs.fifo_tail - hs.fifo_head;
+    if (FWD) {  // the tick pushes at the FIFO tail only: the stored jobs at the head stay where they are
+      const uint32_t q = hs.fifo_stored - hs.fifo_head;
       if (tl < q) fwd.pj[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
       fwd.pf0 = hs.fifo_head;
       fwd.npf = q < (uint32_t)T ? q : (uint32_t)T;
@@ -285,10 +290,10 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd
     } else {
       // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO in order
       for (uint32_t w = 0; hs.sleep_head != hs.sleep_tail; w++) {
-        const gx_job j = w < (uint32_t)T ? sj[w] : d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
-        if ((int64_t)j.wake > d.round) break;
+        const gx_sleeper z = w < (uint32_t)T ? sj[w] : d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
+        if ((int64_t)z.wake > d.round) break;
         hs.sleep_head++;
-        push_job_r(d, a, o, hs, j, lead);
+        push_job_r(d, a, o, hs, z.job, lead);
       }
       uint8_t ost[SPL];
 #pragma unroll
@@ -326,12 +331,20 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd
         const uint64_t incm = team_mask(inc);
         if (incm) {
           hs.last_bcast_ns = d.now;
-          const uint32_t freeb = ~hs.arena_used & (d.A >= 32 ? 0xffffffffu : ((1u << d.A) - 1u));
-          if (!freeb) {
+          // SendServices(list, ALIVE_COUNT if anything is new, else 1) (:555-558); a deferred job
+          // takes no list, a list that does not fit queues the job LOST
+          const uint32_t npass = newm ? d.p.alive_count : 1;
+          const uint32_t mlen = (uint32_t)__popcll(incm) < d.L ? (uint32_t)__popcll(incm) : d.L;
+          const bool stores = fifo_room(d, hs.fifo_head, hs.fifo_tail, hs.fifo_stored) != 0;
+          const int lslot = stores ? list_alloc<T>(d, idx, hs.arena_used, lead) : -1;
+          if (lead) a.c[C_SENDJOBS]++;
+          if (!stores) {
+            push_job_r(d, a, o, hs, make_job(0, 0, meta_of(GX_JOB_SEND, 0, npass)), lead);
+          } else if (lslot < 0) {
             if (lead) a.c[C_LDROP]++;
-          } else {  // SendServices(list, ALIVE_COUNT if anything is new, else 1) (:555-558)
-            const uint32_t li_ = (uint32_t)__builtin_ctz(freeb);
-            hs.arena_used |= 1u << li_;
+            push_job_r(d, a, o, hs, make_job(0, 0, meta_of(GX_JOB_LOST, 0, 1)), lead);
+          } else {
+            const uint32_t li_ = (uint32_t)lslot;
 #pragma unroll
             for (int i = 0; i < SPL; i++) {
               const uint32_t sv = tl + T * i;
@@ -344,13 +357,8 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd
                 list_ptr(d, o, li_)[rank] = g;
               }
             }
-            const uint32_t m = (uint32_t)__popcll(incm) < d.L ? (uint32_t)__popcll(incm) : d.L;
-            if (lead) {
-              d.arena_len[(size_t)idx * d.A + li_] = m;
-              a.c[C_SENDJOBS]++;
-            }
-            push_job_r(d, a, o, hs, make_job(0, 0, li_ | (m << 16), meta_of(GX_JOB_SEND, 0, newm ? d.p.alive_count : 1)),
-                       lead);
+            if (lead) d.arena_len[(size_t)idx * d.A + li_] = mlen;
+            push_job_r(d, a, o, hs, make_job(0, li_ | (mlen << 16), meta_of(GX_JOB_SEND, 0, npass)), lead);
           }
           hs.bs_next = d.round + d.p.alive_interval_rounds;
           // TrackNewServices: AddServiceEntry of every included record into the own view
@@ -399,7 +407,7 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd
             if (lead) d.ev_cnt[k] = ev0 + (uint32_t)__popcll(chgm);
           }
         } else {  // Broadcasts <- nil (:569): the looper blocks until the nil is consumed
-          push_job_r(d, a, o, hs, make_job(0, 0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)), lead);
+          push_job_r(d, a, o, hs, make_job(0, 0, meta_of(GX_JOB_NIL_BS, 0, 1)), lead);
           hs.flags |= 1u;
         }
       }
@@ -430,7 +438,7 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_job *sj, TickFwd &fwd
 
 template <int T, int B = 256>
 __global__ __launch_bounds__(B) void k_owner(Dev d) {
-  __shared__ gx_job s_sl[B];  // the head of each host's sleep ring, one job per team lane
+  __shared__ gx_sleeper s_sl[B];  // the head of each host's sleep ring, one sleeper per team lane
   Acc a;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next round's lists start empty
     *d.ovf_cnt_nx = 0;
@@ -693,8 +701,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
-  uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
-  uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  const uint32_t tail0 = h->fifo_tail, st0 = h->fifo_stored, room = fifo_room(d, h->fifo_head, tail0, st0);
   uint32_t jobs = 0, n_ev = 0;
   unsigned long long c_wr = 0, c_chg = 0;
   uint64_t tomb = pack(d.now, GX_TOMBSTONE);
@@ -739,7 +746,7 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
       uint32_t pos = (uint32_t)fld(pre, 0);
       if (live && jobs + pos < room)
         d.fifo[(size_t)vi * d.Q + ((tail0 + jobs + pos) % d.Q)] =
-            make_job((uint64_t)d.now, s_mask[i], ob + i, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
+            make_job(s_mask[i], (uint32_t)d.round, GX_JOB_META(GX_JOB_EXPIRE, 0, d.p.tombstone_count, ob + i));
       if (live) {
         gx_server_times *st = srv_times(d, v, ob + i);
         st->last_updated_ns = d.now;
@@ -776,14 +783,15 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
     ctr_atomic(d, C_CHG, c_chg);
   }
   if (t == 0) {
-    uint32_t ok = jobs < room ? jobs : room;
-    h->fifo_tail = tail0 + ok;
+    const uint32_t ok = jobs < room ? jobs : room;  // stored; the rest deferred (gx.h gx_job)
+    h->fifo_tail = tail0 + jobs;
+    h->fifo_stored = st0 + ok;
     if (jobs) d.vlc[vi] = d.now;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     // + 16 B of server times (LastUpdated, LastChanged) per live owner
-    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok + 16ull * jobs, (unsigned long long)(hi - lo) * d.S);
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 16ull * ok + 16ull * jobs, (unsigned long long)(hi - lo) * d.S);
     ctr_atomic(d, C_EXPSRV, jobs);
-    ctr_atomic(d, C_QDROP, jobs - ok);
+    ctr_atomic(d, C_QDEFER, jobs - ok);
   }
 }
 
@@ -809,8 +817,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
-  uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
-  uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  const uint32_t tail0 = h->fifo_tail, st0 = h->fifo_stored, room = fifo_room(d, h->fifo_head, tail0, st0);
   const uint32_t tail0q = tail0 % d.Q;  // the tail's ring position (jobs land at tail0q + pos < 2Q)
   uint32_t jobs = 0, n_ev = 0;
   unsigned long long c_wr = 0, c_chg = 0;
@@ -904,7 +911,7 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       if (lead_live[c] && pos < room) {
         uint32_t o = lo + ((base + 512 * c + 2 * t) >> d.logS);
         d.fifo[(size_t)vi * d.Q + ring_add(tail0q, pos, d.Q)] =
-            make_job((uint64_t)d.now, pmask[c], o, meta_of(GX_JOB_EXPIRE, 0, d.p.tombstone_count));
+            make_job(pmask[c], (uint32_t)d.round, GX_JOB_META(GX_JOB_EXPIRE, 0, d.p.tombstone_count, o));
       }
     }
     jobs += tot;
@@ -955,14 +962,15 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
     ctr_atomic(d, C_CHG, c_chg);
   }
   if (t == 0) {
-    uint32_t ok = jobs < room ? jobs : room;
-    h->fifo_tail = tail0 + ok;
+    const uint32_t ok = jobs < room ? jobs : room;  // stored; the rest deferred (gx.h gx_job)
+    h->fifo_tail = tail0 + jobs;
+    h->fifo_stored = st0 + ok;
     if (jobs) d.vlc[vi] = d.now;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     // + 16 B of server times (LastUpdated, LastChanged) per live owner
-    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 32ull * ok + 16ull * jobs, (unsigned long long)(hi - lo) * d.S);
+    kbytes(d, GX_K_STORM, 8ull * (hi - lo) * d.S + 16ull * ok + 16ull * jobs, (unsigned long long)(hi - lo) * d.S);
     ctr_atomic(d, C_EXPSRV, jobs);
-    ctr_atomic(d, C_QDROP, jobs - ok);
+    ctr_atomic(d, C_QDEFER, jobs - ok);
   }
 }
 
@@ -1141,22 +1149,27 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       c.key = u * d.KE + j * d.NG + n;
       bool empty = false;
       if (hs.fifo_head != hs.fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
-        uint32_t q = hs.fifo_head - pf0;
-        if (q >= npf) {  // load the next T head jobs
-          const uint32_t left = hs.fifo_tail - hs.fifo_head;
-          wave_sync();
-          if (tl < left) pjs[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
-          wave_sync();
-          pf0 = hs.fifo_head;
-          npf = left < (uint32_t)T ? left : (uint32_t)T;
-          q = 0;
-          if (lead) kb += 32ull * npf;
+        gx_job jb = make_job(0, 0, 0);
+        if (hs.fifo_head != hs.fifo_stored) {  // a stored job: from the LDS window
+          uint32_t q = hs.fifo_head - pf0;
+          if (q >= npf) {  // load the next T stored head jobs
+            const uint32_t left = hs.fifo_stored - hs.fifo_head;
+            wave_sync();
+            if (tl < left) pjs[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
+            wave_sync();
+            pf0 = hs.fifo_head;
+            npf = left < (uint32_t)T ? left : (uint32_t)T;
+            q = 0;
+            if (lead) kb += 16ull * npf;
+          }
+          jb = pjs[q];
         }
-        const gx_job jb = pjs[q];
-        hs.fifo_head++;
+        jb = pop_job_r(d, idx, hs, &jb);  // past the stored window: a looper's nil or LOST
         if (lead) a.c[C_DEQ]++;
-        const uint32_t kind = jb.meta & 0xff, pass = (jb.meta >> 8) & 0xff, npass = (jb.meta >> 16) & 0xff;
-        if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
+        const uint32_t kind = GX_JOB_KIND(jb.meta), pass = GX_JOB_PASS(jb.meta), npass = GX_JOB_NPASSES(jb.meta);
+        if (kind == GX_JOB_LOST) {  // a deferred job reached the head: its batch is unknown
+          count_lost(d, a, lead);
+        } else if (kind == GX_JOB_NIL_BS) {  // the BroadcastServices looper unblocks (services_state.go:569)
           if (lead) a.c[C_NIL]++;
           hs.flags &= ~1u;
           hs.bs_next = d.round + d.p.alive_interval_rounds;
@@ -1167,11 +1180,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         } else if (kind == GX_JOB_SEND || kind == GX_JOB_EXPIRE) {
           if (pass + 1 < npass) {  // the looper re-arms after TOMBSTONE_RETRANSMIT (:585-601)
             gx_job nj = jb;
-            nj.meta = meta_of((int)kind, pass + 1, npass);
-            nj.wake = (uint32_t)(d.round + d.p.retransmit_rounds);
-            push_sleep_r(d, a, u, hs, nj, lead);
+            nj.meta = GX_JOB_META(kind, pass + 1, npass, GX_JOB_OWNER(jb.meta));
+            push_sleep_r(d, a, u, hs, nj, (uint32_t)(d.round + d.p.retransmit_rounds), lead);
           } else {
-            free_list_r(hs, jb);  // read below; nothing reallocates it during the sends
+            free_list_r(d, idx, hs, jb, lead);  // read below; nothing reallocates it during the sends
           }
         }
         c.m = job_len(d, jb);
@@ -1183,10 +1195,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         } else if (kind == GX_JOB_SEND) {
           c.bw = dw;
           c.list = list_ptr(d, u, jb.c & 0xffff);
-        } else if (kind == GX_JOB_EXPIRE) {
-          c.bw = pack((int64_t)jb.a, GX_TOMBSTONE) + dw;
-          c.rb = jb.c * d.S;
-          c.emask = (uint32_t)__popcll(jb.b) == d.S ? 0ull : jb.b;
+        } else if (kind == GX_JOB_EXPIRE) {  // Tombstone() at the call's now
+          c.bw = pack(d.p.t0_ns + (int64_t)jb.c * d.p.round_ns, GX_TOMBSTONE) + dw;
+          c.rb = GX_JOB_OWNER(jb.meta) * d.S;
+          c.emask = (uint32_t)__popcll(jb.a) == d.S ? 0ull : jb.a;
         }
       } else if (hs.dq_len == 0) {  // default: nothing pending (:96-98)
         empty = true;
@@ -1424,7 +1436,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       // The jobs at the FIFO head that this round's calls will dequeue are loaded up front, one
       // per team lane (call c takes job c while c < the jobs queued at the start: later pushes go
       // to the tail and cannot overwrite them), so a call waits on its list records only.
-      const uint32_t head0 = hs.fifo_head, n0 = hs.fifo_tail - head0;
+      const uint32_t head0 = hs.fifo_head, n0 = hs.fifo_stored - head0;  // stored jobs only
       if (lane < n0 && lane < np * d.NG) pjs[lane] = d.fifo[(size_t)idx * d.Q + ((head0 + lane) % d.Q)];
       // A packet to a reachable peer on this shard takes its receiver inbox slot before it is
       // packed, so its records go straight into the receiver's inbox when the slot is one of the
@@ -1467,7 +1479,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
                                        filt ? &d.view[(size_t)(pj - d.lo) * d.R] : nullptr, pj - d.lo);
           }
           called = j + 1;
-          if (lane == 0) kb += 32 + 32ull * l + (filt_used(d, pos) ? 8ull * l : 0);  // job, records in/out, slots
+          if (lane == 0) kb += 16 + 32ull * l + (filt_used(d, pos) ? 8ull * l : 0);  // job, records in/out, slots
           const bool live = l || nf;
           if (lane == 0) {
             d.msg_len[x] = ok ? l : 0;
@@ -1504,7 +1516,7 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   __shared__ PlanCall s_pl[PLAN ? 256 / T : 1][PLAN_CH + 1];
   __shared__ ScanLds sm;
   __shared__ uint32_t s_scan[256 / T], s_nscan;
-  __shared__ gx_job s_sl[OWN ? 256 : 1];  // sleep-ring heads of the owner ticks
+  __shared__ gx_sleeper s_sl[OWN ? 256 : 1];  // sleep-ring heads of the owner ticks
   Acc a;
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
@@ -1615,26 +1627,14 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
     for (uint32_t x = 0; x < h.z; x++) add_entry(d, a, v, pk[x], SRC_GOSSIP);
     recs += h.z;
   }
-  if (d.sfilt) a.c[C_GOSSIP_MERGES] = a.c[C_STALE] = 0;  // counted by the senders
+  a.c[C_GOSSIP_MERGES] = a.c[C_STALE] = 0;  // counted by the senders
   kbytes(d, GX_K_MERGE, 28ull * recs + 16ull * cnt + 4, recs);
   for (int i = 0; i < C_NCTR; i++) ctr_atomic(d, i, a.c[i]);
   if (a.changed) mark_change(d);
 }
 
-// Phase 4a, LEAN_LPR lanes per receiver and three dependent loads: the receiver's inbox count and
-// the headers of its first DR packets, then the records the headers name (inline slots, only the
-// lengths given), then the view slot of every record. A receiver whose records are all no-ops
-// (stale, or no newer than the slot: see k_merge) is finished here, its merges and stale drops
-// counted. A receiver with a live record, or with more than DR packets, gets a routing count (mrec) and
-// merged in full by k_merge. Measured (profiles/ab_gossip.sh, cfg5): 16 lanes x 4 records per
-// batch 17.8 us; 32 x 4 22.6 us; 64 x 2 24.2 us; 8 x 4 21.1 us; loading the inline slots
-// speculatively with the count (one hop less) 19-23 us: the wasted bytes cost more than the hop.
-// Fused with k_merge (each wave merging its own flagged receivers after the filter, inbox still in
-// L2): 31.1 us vs 16.1 + 14.4 us, the merge body's 116 VGPRs halving the filter's occupancy.
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
-#define MERGE_SEG 16  // lanes per receiver in k_merge_seg's first pass
-#define MERGE_RANGE_DEF 1  // receivers per wave (8: flags read as one u64; measured slower in storm rounds)
 struct MergeLds {  // one wave's staging for one receiver at a time
   uint4 hdr[GX_DI_MAX];     // headers in sender order (inboxes of more than 64 packets use all of it)
   uint32_t pst[GX_DI_MAX];  // wide inboxes: keys while ranking, then each packet's first record index
@@ -1725,8 +1725,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
   auto p_slot = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].w : rdl(sh.w, k); };
   const uint32_t vtick = d.tick[vi];
   gx_host_state *h = &d.hs[vi];
-  const uint32_t tail0 = h->fifo_tail, count0 = tail0 - h->fifo_head;
-  const uint32_t room = count0 < d.Q - 2 ? d.Q - 2 - count0 : 0;
+  const uint32_t tail0 = h->fifo_tail, st0 = h->fifo_stored, room = fifo_room(d, h->fifo_head, tail0, st0);
   uint32_t n_retx = 0, n_ev = 0;
   unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, c_chg = 0, mexp = ~0ull;
   uint64_t *row = &d.view[(size_t)vi * d.R];
@@ -1872,8 +1871,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     unsigned long long m = __ballot(f);
     uint32_t pos = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     if (f && n_retx + pos < room)
-      d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] =
-          make_job(s_accw[lane], 0, key, meta_of(GX_JOB_RETX, 0, 1));
+      d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] = make_job(s_accw[lane], key, meta_of(GX_JOB_RETX, 0, 1));
     n_retx += (uint32_t)__popcll(m);
     wave_sync();
   }
@@ -1885,21 +1883,20 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
   c_chg = wave_sum(c_chg);
   mexp = wave_min(mexp);
   if (lane == 0) {
-    uint32_t ok = n_retx < room ? n_retx : room;
-    h->fifo_tail = tail0 + ok;
+    const uint32_t ok = n_retx < room ? n_retx : room;  // stored; the rest deferred (gx.h gx_job)
+    if (n_retx) {
+      h->fifo_tail = tail0 + n_retx;
+      h->fifo_stored = st0 + ok;
+    }
     if (vlc_set) d.vlc[vi] = vlc_ts;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     ctr_atomic(d, C_CHG, c_chg);
-    // 12 B per record (word + key) + 8 B per slot read / written + 32 B per retransmit job
-    // + 16 B per inbox header + the count
-    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 32ull * ok + 16ull * deg + 4, c_merge);
-    if (!d.sfilt) {  // else counted by the senders
-      ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
-      ctr_atomic(d, C_STALE, c_stale);
-    }
+    // 12 B per record (word + key) + 8 B per slot read / written + 16 B per stored retransmit job
+    // + 16 B per inbox header + the count (merges and stale drops: counted by the senders)
+    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 16ull * ok + 16ull * deg + 4, c_merge);
     ctr_atomic(d, C_GOSSIP_ACC, c_acc);
-    ctr_atomic(d, C_RETX, ok);
-    ctr_atomic(d, C_QDROP, n_retx - ok);
+    ctr_atomic(d, C_RETX, n_retx);
+    ctr_atomic(d, C_QDEFER, n_retx - ok);
     if (c_wr) {
       mark_change(d);
       atomicMin(&d.minexp[vi], mexp);
@@ -1938,7 +1935,7 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
   const uint32_t v = d.lo + vi;
   // hop 1: count, headers, FIFO counters and the event log slot together
   uint4 hd = make_uint4(0u, 0u, 0u, 0u);
-  uint32_t deg = 0, tail0 = 0, head0 = 0;
+  uint32_t deg = 0, tail0 = 0, head0 = 0, st0 = 0;
   int32_t evk = -1;
   uint32_t vtick = 2;
   if (act) {
@@ -1946,6 +1943,7 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
     deg = d.in_cnt[vi];
     tail0 = d.hs[vi].fifo_tail;
     head0 = d.hs[vi].fifo_head;
+    st0 = d.hs[vi].fifo_stored;
     vtick = d.tick[vi];
     if (EV) evk = d.ev_slot[vi];
   }
@@ -1989,7 +1987,7 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
     val = g.w;
     w0 = w0_fwd(d, pw, vtick, key, v) ? fw0 : row[key];
   }
-  const uint32_t room = tail0 - head0 < d.Q - 2 ? d.Q - 2 - (tail0 - head0) : 0;
+  const uint32_t room = fifo_room(d, head0, tail0, st0);
   const uint32_t ev0 = (EV && evk >= 0) ? d.ev_cnt[evk] : 0;
   const bool stale0 = valid && ts_of(val) < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
   const bool live = valid && !stale0 && (st_of(w0) == GX_ABSENT || ts_of(val) > ts_of(w0));
@@ -2082,7 +2080,7 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
   const bool f = s_accf[sl];  // ordered ballot compaction -> retransmit jobs (arrival order)
   const uint64_t m = sballot(f);
   const uint32_t pos = (uint32_t)__popcll(m & ((1ull << sl) - 1ull));
-  if (f && pos < room) d.fifo[(size_t)vi * d.Q + ((tail0 + pos) % d.Q)] = make_job(s_accw[sl], 0, key, meta_of(GX_JOB_RETX, 0, 1));
+  if (f && pos < room) d.fifo[(size_t)vi * d.Q + ((tail0 + pos) % d.Q)] = make_job(s_accw[sl], key, meta_of(GX_JOB_RETX, 0, 1));
   n_retx = (uint32_t)__popcll(m);
   c_wr = seg_sum<SEG>((uint32_t)c_wr);
   c_acc = seg_sum<SEG>(c_acc);
@@ -2093,20 +2091,20 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
     mexp = y < mexp ? y : mexp;
   }
   if (sl == 0) {
-    const uint32_t ok = n_retx < room ? n_retx : room;
-    if (ok) d.hs[vi].fifo_tail = tail0 + ok;
+    const uint32_t ok = n_retx < room ? n_retx : room;  // stored; the rest deferred (gx.h gx_job)
+    if (n_retx) {
+      d.hs[vi].fifo_tail = tail0 + n_retx;
+      d.hs[vi].fifo_stored = st0 + ok;
+    }
     if (mcmax) d.vlc[vi] = ts_of(s_accw[mcmax - 1]);  // state.LastChanged
     if (EV && evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     ctr_atomic(d, C_CHG, c_chg);
-    // 12 B per record + 8 B per slot read / written + 32 B per retransmit + 16 B per header + count
-    kbytes(d, GX_K_MERGE, 12ull * total + 8ull * (total + c_wr) + 32ull * ok + 16ull * deg + 4, total);
-    if (!d.sfilt) {  // else counted by the senders
-      ctr_atomic(d, C_GOSSIP_MERGES, total);
-      ctr_atomic(d, C_STALE, (unsigned long long)__popcll(sballot(stale0)) + 0 * stl);
-    }
+    // 12 B per record + 8 B per slot read / written + 16 B per stored retransmit + 16 B per header
+    // + count (merges and stale drops: counted by the senders)
+    kbytes(d, GX_K_MERGE, 12ull * total + 8ull * (total + c_wr) + 16ull * ok + 16ull * deg + 4, total);
     ctr_atomic(d, C_GOSSIP_ACC, c_acc);
-    ctr_atomic(d, C_RETX, ok);
-    ctr_atomic(d, C_QDROP, n_retx - ok);
+    ctr_atomic(d, C_RETX, n_retx);
+    ctr_atomic(d, C_QDEFER, n_retx - ok);
     if (c_wr) {
       mark_change(d);
       atomicMin(&d.minexp[vi], mexp);
@@ -2196,101 +2194,6 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
   if (unsigned long long *kp = kprof_merge(d); kp && threadIdx.x == 0 && nf) atomicAdd(&kp[4], (unsigned long long)nf);
   for (uint32_t k = wv; k < nf; k += MERGE_WAVES) merge_receiver<K32, EV>(d, s_fb[k], s_l[wv]);
 }
-
-// A/B (GX_AB_FLAGS bit 2048): round 2's merge, four consecutive receivers per wave in 16-lane
-// segments, a receiver that does not fit merged afterwards by the same wave.
-template <bool K32, bool EV>
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge_seg_v1(Dev d) {
-  __shared__ MergeLds s_l[MERGE_WAVES];
-  constexpr uint32_t NS = 64 / MERGE_SEG;
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63, seg = lane / MERGE_SEG;
-  const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * NS;
-  if (r0 >= d.Hl) return;
-  const uint32_t vi = r0 + seg;
-  bool fl = false;
-  if (vi < d.Hl) fl = d.mrec[vi] != 0;
-  if (fl && (lane & (MERGE_SEG - 1)) == 0) d.mrec[vi] = 0;
-  const bool done = merge_seg<K32, EV, MERGE_SEG>(d, vi, fl, s_l[wv]);
-  uint64_t rest = __ballot(!done && (lane & (MERGE_SEG - 1)) == 0);
-  for (; rest; rest &= rest - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)__builtin_ctzll(rest) / MERGE_SEG, s_l[wv]);
-}
-
-template <bool K32, bool EV, int MERGE_RANGE = MERGE_RANGE_DEF>
-__global__ __launch_bounds__(64 * MERGE_WAVES) void k_merge(Dev d) {
-  // one receiver per wave, MERGE_WAVES per block; the waves share nothing (wave-level sync only)
-  __shared__ MergeLds s_l[MERGE_WAVES];
-  const uint32_t wv = threadIdx.x >> 6;
-  // each wave takes the flags of MERGE_RANGE consecutive receivers and merges the flagged ones in
-  // turn (one receiver per wave measured fastest: the flagged receivers' chains run side by side)
-  const uint32_t r0 = (blockIdx.x * MERGE_WAVES + wv) * MERGE_RANGE;
-  if (r0 >= d.Hl) return;
-  uint64_t fl = 0;
-  for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) fl |= (uint64_t)(d.mrec[r0 + k] != 0) << (8 * k);
-  if (fl && d.sfilt)
-    for (uint32_t k = 0; k < MERGE_RANGE && r0 + k < d.Hl; k++) d.mrec[r0 + k] = 0;  // the senders count next round's
-  for (; fl; fl &= fl - 1) merge_receiver<K32, EV>(d, r0 + (uint32_t)(__builtin_ctzll(fl) >> 3), s_l[wv]);
-}
-
-#define LEAN_LPR 16
-#define LEAN_Q 4
-__global__ __launch_bounds__(256) void k_merge_lean(Dev d) {
-  const uint32_t lane = threadIdx.x & 63, l = threadIdx.x & (LEAN_LPR - 1);
-  const uint32_t vi = blockIdx.x * (256 / LEAN_LPR) + threadIdx.x / LEAN_LPR;
-  const uint32_t gbase = lane & ~(uint32_t)(LEAN_LPR - 1);
-  const uint64_t gmask = ((1ull << LEAN_LPR) - 1ull) << gbase;
-  unsigned long long c_merge = 0, c_stale = 0, c_hdr = 0;
-  if (vi < d.Hl) {
-    const uint32_t cap = d.p.packet_cap;
-    const grec *base = &d.in_rec[(size_t)vi * d.DR * cap];
-    const uint4 hd = l < d.DR ? d.in_hdr[(size_t)vi * d.DI + l] : make_uint4(0u, 0u, 0u, 0u);
-    const uint32_t cnt = d.in_cnt[vi];
-    bool defer = cnt > d.DR;
-    if (cnt && !defer) {
-      const uint64_t *row = &d.view[(size_t)vi * d.R];
-      const uint32_t npos = cnt * cap;
-      c_hdr = l == 0 ? cnt : 0;
-      for (uint32_t p0 = 0; p0 < npos; p0 += LEAN_LPR * LEAN_Q) {
-        grec g[LEAN_Q];
-        bool valid[LEAN_Q];
-#pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) {  // hop 2: the records of the packets' used slots
-          const uint32_t p = p0 + l + LEAN_LPR * q, sl = p / cap;
-          const uint32_t len = __shfl(hd.z, (int)(gbase + (sl < d.DR ? sl : 0)), 64);
-          valid[q] = p < npos && p - sl * cap < len;
-          if (valid[q]) g[q] = base[p];
-        }
-        uint64_t w0[LEAN_Q];
-#pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) w0[q] = valid[q] ? row[g[q].r] : 0;  // hop 3
-        bool live = false;
-#pragma unroll
-        for (int q = 0; q < LEAN_Q; q++) {
-          const int64_t ts = ts_of(g[q].w);
-          const bool stale = valid[q] && ts < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
-          live |= valid[q] && !stale && (st_of(w0[q]) == GX_ABSENT || ts > ts_of(w0[q]));
-          c_merge += valid[q];
-          c_stale += stale;
-        }
-        if (__ballot(live) & gmask) {
-          defer = true;
-          break;
-        }
-      }
-    }
-    if (defer) c_merge = c_stale = c_hdr = 0;  // k_merge merges and counts this receiver
-    if (l == 0) d.mrec[vi] = defer ? 0xffffu : 0u;  // a deferred receiver is merged by a whole wave
-  }
-  c_merge = wave_sum(c_merge);
-  c_stale = wave_sum(c_stale);
-  c_hdr = wave_sum(c_hdr);
-  if (lane == 0 && c_merge) {
-    // 12 B per record + 8 B per slot read, 16 B per inbox header + the count
-    kbytes(d, GX_K_MERGE, 20ull * c_merge + 16ull * c_hdr + 4ull * c_hdr, c_merge);
-    ctr_atomic(d, C_GOSSIP_MERGES, c_merge);
-    ctr_atomic(d, C_STALE, c_stale);
-  }
-}
-
 
 // ============================================================= phase 5: anti-entropy push-pull ==
 // Dense view-pair merge: a <- b and, when `both`, b <- a's pre-exchange words. VEC streams both
@@ -2432,13 +2335,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint64_t *A = vrow(d, a);
   uint64_t *B = xs ? A : ext ? const_cast<uint64_t *>(ext) : vrow(d, b);
   gx_host_state *ha = hst(d, a), *hb = both ? hst(d, b) : ha;
-  uint32_t ta0 = ha->fifo_tail, ca0 = ta0 - ha->fifo_head;
-  uint32_t tb0 = hb->fifo_tail, cb0 = tb0 - hb->fifo_head;
-  uint32_t rooma = ca0 < d.Q - 2 ? d.Q - 2 - ca0 : 0, roomb = cb0 < d.Q - 2 ? d.Q - 2 - cb0 : 0;
+  // retransmits: the first `room` of each side are stored, the rest deferred (gx.h gx_job)
+  const uint32_t ta0 = ha->fifo_tail, sa0 = ha->fifo_stored, rooma = fifo_room(d, ha->fifo_head, ta0, sa0);
+  const uint32_t tb0 = hb->fifo_tail, sb0 = hb->fifo_stored, roomb = fifo_room(d, hb->fifo_head, tb0, sb0);
   const uint32_t ta0q = ta0 % d.Q, tb0q = tb0 % d.Q;  // ring positions of the tails (one division each)
   uint32_t na = 0, nb = 0;
   uint32_t c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0;  // per thread: < 2^32
-  uint32_t c_qa = 0, c_qb = 0;  // retransmits counted after both FIFOs filled up (all dropped)
+  uint32_t c_qa = 0, c_qb = 0;  // retransmits counted once both stored windows are full (all deferred)
   unsigned long long ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
   const uint32_t TILE = 4 * blockDim.x;
@@ -2655,8 +2558,9 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         side_times_shfl(d, a, base, fl & 0xffu, nwa, lk_a, c_wr);  // server times count as written words
         if (both) side_times_shfl(d, b, base, (fl >> 8) & 0xffu, nwb, lk_b, c_wr);
       }
-      // Both FIFOs full (block-uniform): every further retransmit is dropped, so its position no
-      // longer matters; count it per thread and reduce once after the pass (no scan, no barrier).
+      // Both stored windows full (block-uniform): every further retransmit is deferred, a count
+      // whose order does not matter; count it per thread and reduce once after the pass (no
+      // scan, no barrier). Behind a deferred job this holds from the first tile.
       if (na >= rooma && (!both || nb >= roomb)) {
         c_qa += fld(cnt, 0) + fld(cnt, 1);
         c_qb += fld(cnt, 2) + fld(cnt, 3);
@@ -2681,9 +2585,9 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       if (fa[k] && pa[k] < rooma)
-        d.fifo[(size_t)li(d, a) * d.Q + ring_add(ta0q, pa[k], d.Q)] = make_job(nwa[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+        d.fifo[(size_t)li(d, a) * d.Q + ring_add(ta0q, pa[k], d.Q)] = make_job(nwa[k], r, meta_of(GX_JOB_RETX, 0, 1));
       if (fb[k] && pb[k] < roomb)
-        d.fifo[(size_t)li(d, b) * d.Q + ring_add(tb0q, pb[k], d.Q)] = make_job(nwb[k], 0, r, meta_of(GX_JOB_RETX, 0, 1));
+        d.fifo[(size_t)li(d, b) * d.Q + ring_add(tb0q, pb[k], d.Q)] = make_job(nwb[k], r, meta_of(GX_JOB_RETX, 0, 1));
     }
     na += fld(tot, 0) + fld(tot, 1);
     nb += fld(tot, 2) + fld(tot, 3);
@@ -2754,14 +2658,20 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   if (t == 0) {
     if (ma != ~0ull) atomicMin(&d.minexp[li(d, a)], ma);
     if (both && mb != ~0ull) atomicMin(&d.minexp[li(d, b)], mb);
-    uint32_t oka = na < rooma ? na : rooma, okb = nb < roomb ? nb : roomb;
-    ha->fifo_tail = ta0 + oka;
-    if (both) hb->fifo_tail = tb0 + okb;
-    ctr_atomic(d, C_RETX, oka + (both ? okb : 0));
-    ctr_atomic(d, C_QDROP, (na - oka) + (both ? nb - okb : 0));
+    const uint32_t oka = na < rooma ? na : rooma, okb = nb < roomb ? nb : roomb;
+    if (na) {
+      ha->fifo_tail = ta0 + na;
+      ha->fifo_stored = sa0 + oka;
+    }
+    if (both && nb) {
+      hb->fifo_tail = tb0 + nb;
+      hb->fifo_stored = sb0 + okb;
+    }
+    ctr_atomic(d, C_RETX, na + (both ? nb : 0));
+    ctr_atomic(d, C_QDEFER, (na - oka) + (both ? nb - okb : 0));
     ctr_atomic(d, C_AESLOTS, (unsigned long long)d.R * (both ? 2 : 1));
     const uint64_t loaded = d.R > xskip ? d.R - xskip : 0;  // cross pairs: matching blocks are not read
-    kbytes(d, GX_K_AE, 16ull * loaded + 32ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
+    kbytes(d, GX_K_AE, 16ull * loaded + 16ull * (oka + (both ? okb : 0)), (unsigned long long)d.R * (both ? 2 : 1));
     if (both || count_ex) ctr_atomic(d, C_AEX, 1);
   }
 }
@@ -3741,18 +3651,20 @@ __global__ void k_converged(Dev d, unsigned long long *bad) {
 GXD uint64_t feed(uint64_t h, uint64_t x) { return mix64(h ^ x); }
 GXD uint64_t feed_job(uint64_t h, const gx_job &j) {
   h = feed(h, j.a);
-  h = feed(h, j.b);
-  h = feed(h, (uint64_t)j.c | ((uint64_t)j.meta << 32));
-  return feed(h, (uint64_t)j.wake | ((uint64_t)j.aux << 32));
+  return feed(h, (uint64_t)j.c | ((uint64_t)j.meta << 32));
 }
 __global__ void k_digest(Dev d, uint64_t *out) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;  // local index
   if (v >= d.Hl) return;
   const gx_host_state s = d.hs[v];
   uint64_t h = 0x243F6A8885A308D3ull;
-  for (uint32_t i = s.fifo_head; i != s.fifo_tail; i++) h = feed_job(h, d.fifo[(size_t)v * d.Q + (i % d.Q)]);
+  for (uint32_t i = s.fifo_head; i != s.fifo_stored; i++) h = feed_job(h, d.fifo[(size_t)v * d.Q + (i % d.Q)]);
   h = feed(h, 0xF1F0);
-  for (uint32_t i = s.sleep_head; i != s.sleep_tail; i++) h = feed_job(h, d.sleep[(size_t)v * d.SQ + (i % d.SQ)]);
+  h = feed(h, (uint64_t)(s.fifo_tail - s.fifo_stored) | ((uint64_t)s.fifo_stored << 32));
+  for (uint32_t i = s.sleep_head; i != s.sleep_tail; i++) {
+    const gx_sleeper z = d.sleep[(size_t)v * d.SQ + (i % d.SQ)];
+    h = feed(h, feed_job(z.wake, z.job));
+  }
   h = feed(h, 0x51EE);
   h = feed(h, s.dq_len);
   for (uint32_t i = 0; i < s.dq_len; i++) {
@@ -3762,7 +3674,7 @@ __global__ void k_digest(Dev d, uint64_t *out) {
   }
   h = feed(h, 0xA7E4);
   for (uint32_t a = 0; a < d.A; a++) {
-    if (!((s.arena_used >> a) & 1u)) continue;
+    if (!((d.arena_bits[(size_t)v * d.AW + (a >> 5)] >> (a & 31)) & 1u)) continue;
     uint32_t len = d.arena_len[(size_t)v * d.A + a];
     h = feed(h, a);
     h = feed(h, len);
@@ -3879,12 +3791,17 @@ __global__ void k_api_expire(Dev d, uint32_t v, uint32_t o, uint32_t *out) {
 }
 __global__ void k_api_send(Dev d, uint32_t v, const grec *list, uint32_t n, uint32_t np) {
   Acc a;
-  if (threadIdx.x == 0) {
-    int slot = alloc_list(d, a, v);
-    if (slot >= 0) {
-      uint32_t m = n < d.L ? n : d.L;
-      grec *dst = list_ptr(d, v, slot);
-      for (uint32_t i = 0; i < m; i++) dst[i] = list[i];
+  if (threadIdx.x == 0) {  // SendServices (services_state.go:579-604)
+    a.c[C_SENDJOBS]++;
+    const uint32_t m = n < d.L ? n : d.L;
+    if (!fifo_stores(d, v)) {  // deferred: no list
+      push_job(d, a, v, make_job(0, 0, meta_of(GX_JOB_SEND, 0, np)));
+    } else {
+      int slot = alloc_list(d, a, v);
+      if (slot >= 0) {
+        grec *dst = list_ptr(d, v, slot);
+        for (uint32_t i = 0; i < m; i++) dst[i] = list[i];
+      }
       commit_send(d, a, v, slot, m, np);
     }
   }

@@ -76,6 +76,19 @@ SCENARIOS = {
     "pp_initiate_storm_depart": dict(n_hosts=80, n_services=4, init_mode=INIT_WARM, push_pull_mode=1,
                                      ae_period_rounds=4, partition_start=0, partition_end=20, storm_round=3,
                                      queue_cap=1024, depart_round=6, depart_ppm=50000),
+    # the FIFO's stored window (gx.h gx_job): push-pull retransmits and EXPIRE jobs past queue_cap
+    # are deferred (counted in place), the loopers' nils keep their positions behind them, deferred
+    # jobs reaching the head are LOST; both engines must defer and lose the same jobs
+    "window_cold_start": dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, ae_period_rounds=10, churn_ppm=50000,
+                              aged_ppm=50000, queue_cap=96),
+    "window_storm": dict(n_hosts=96, n_services=4, init_mode=INIT_WARM, ae_period_rounds=10, partition_start=0,
+                         partition_end=30, storm_round=3, churn_ppm=20000, queue_cap=96),
+    # a list arena of two bitmap words (list_slots > 32): long retransmit sleeps keep up to 40 lists
+    # live per host, SendServices jobs whose list does not fit are queued LOST
+    "lists_two_words": dict(n_hosts=48, n_services=16, init_mode=INIT_WARM, churn_ppm=300000, aged_ppm=100000,
+                            queue_cap=4096, list_slots=40, retransmit_rounds=40, tombstone_count=20),
+    "window_lists_gm4": dict(n_hosts=64, n_services=16, init_mode=INIT_OWN, ae_period_rounds=10, churn_ppm=200000,
+                             aged_ppm=50000, queue_cap=4096, list_slots=40, gossip_messages=4),
 }
 
 
