@@ -26,12 +26,19 @@ sys.path.insert(0, ROOT)
 METRIC = "record-merges/sec (whole node) + rounds-to-converge wall time, H=32768 S=16"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
+# queue_cap: the broadcast FIFO's stored window per host (gx.h gx_job). The reference's queue is
+# unbounded; the engine stores the first queue_cap jobs and counts the rest in place, and a run stays
+# faithful to the reference's queue while no deferred job reaches the head, which takes at least
+# queue_cap / (fanout * GossipMessages) rounds after the window first fills: 16384 / 3 = 5461 rounds,
+# 20480 / 3 = 6826 (cfg 5 also stores the storm's 16384 ExpireServer jobs per host), 139264 / 45 =
+# 3094 rounds at GossipMessages 15 (71 GB at H = 32768), all past --converge-max 3000.
+Q_GM1 = 16384
 CONFIGS = {
     # BASELINE.json configs[4]: 32768 x 16, 2-way partition for 50 rounds, departure storm, heal
     "cfg5": dict(desc="32768 hosts x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds "
                       "[0,50) + ExpireServer storm at round 5 + heal",
                  p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
-                        queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                        queue_cap=20480, list_slots=32, init_mode=2, partition_start=0,
                         partition_end=50, storm_round=5, ae_period_rounds=10),
                  ref_variant="cfg5_ref"),
     # cfg 5 at the reference's own anti-entropy cadence: PushPullInterval 20 s (config/config.go:45,
@@ -40,7 +47,7 @@ CONFIGS = {
     "cfg5_ref": dict(desc="cfg5 at Sidecar's default PushPullInterval 20 s: 32768 hosts x 16 services, fanout 3, "
                           "cap 32 records/msg, 2-way partition rounds [0,50) + ExpireServer storm at round 5 + heal",
                      p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
-                            queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                            queue_cap=20480, list_slots=32, init_mode=2, partition_start=0,
                             partition_end=50, storm_round=5, ae_period_rounds=100)),
     # cfg 5 at Sidecar's own defaults (config/config.go:45-47, main.go:252-259): PushPullInterval 20 s
     # (100 rounds) and GossipMessages 15 (up to 15 GetBroadcasts packets per gossip target per round)
@@ -48,21 +55,21 @@ CONFIGS = {
                                "x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds [0,50) + "
                                "ExpireServer storm at round 5 + heal",
                           p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
-                                 queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                                 queue_cap=139264, list_slots=32, init_mode=2, partition_start=0,
                                  partition_end=50, storm_round=5, ae_period_rounds=100, gossip_messages=15)),
     # configs[1]: 4096 x 16, fanout 3, cap 32, one GPU (cold start: every view knows its own records)
     "cfg2": dict(desc="4096 hosts x 16 services, fanout 3, cap 32 records/msg, own-records start, "
                       "push-pull every 10 rounds",
-                 p=dict(n_hosts=4096, n_services=16, fanout=3, packet_cap=32, queue_cap=4096,
-                        init_mode=1, ae_period_rounds=10)),
+                 p=dict(n_hosts=4096, n_services=16, fanout=3, packet_cap=32, queue_cap=Q_GM1,
+                        list_slots=32, init_mode=1, ae_period_rounds=10)),
     # configs[2]: 16384 x 16 with 5% churn/round and alive-lifespan expiry
     "cfg3": dict(desc="16384 hosts x 16 services, 5% of owners start/stop a service per round, 5% of "
                       "records aged U[0,100s] (alive-lifespan expiry), push-pull every 10 rounds",
-                 p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2,
+                 p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=Q_GM1, list_slots=32, init_mode=2,
                         churn_ppm=50000, aged_ppm=50000, ae_period_rounds=10)),
     # configs[3]: 8192 x 64, push-pull every 10 rounds
     "cfg4": dict(desc="8192 hosts x 64 services, push-pull full-state merge every 10 rounds",
-                 p=dict(n_hosts=8192, n_services=64, fanout=3, queue_cap=4096, init_mode=1,
+                 p=dict(n_hosts=8192, n_services=64, fanout=3, queue_cap=Q_GM1, list_slots=32, init_mode=1,
                         ae_period_rounds=10)),
     # cfg 5 driven by memberlist's failure detector instead of the scripted storm:
     # the partition drops packets, SWIM probes suspect the other half, Lifeguard timers decide
@@ -71,12 +78,12 @@ CONFIGS = {
                         "partition rounds [0,50), SWIM probes + Lifeguard suspicion, NotifyLeave -> "
                         "ExpireServer, push-pull every 10 rounds",
                    p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
-                          queue_cap=20480, list_slots=16, init_mode=2, partition_start=0,
+                          queue_cap=20480, list_slots=32, init_mode=2, partition_start=0,
                           partition_end=50, ae_period_rounds=10, fd_enable=1)),
     # host crashes detected by the failure detector: 2% of 16384 hosts crash at round 5
     "fd_depart": dict(desc="16384 hosts x 16 services, 2% of hosts crash at round 5, memberlist failure "
                            "detection (SWIM + Lifeguard) -> NotifyLeave -> ExpireServer, push-pull every 10 rounds",
-                      p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=4096, init_mode=2,
+                      p=dict(n_hosts=16384, n_services=16, fanout=3, queue_cap=Q_GM1, list_slots=32, init_mode=2,
                              ae_period_rounds=10, fd_enable=1, depart_round=5, depart_ppm=20000)),
     # plumbing case of the failure detector (CPU rehearsal of the sharded path)
     "cfg1fd": dict(desc="64 hosts x 8 services, fanout 3, 10% of hosts crash at round 5, memberlist failure "
@@ -119,6 +126,23 @@ def make_engine(lib, cfg, seed, device):
 
 def merges(st):
     return st["gossip_merges"] + st["ae_merges"] + st["local_merges"]
+
+
+def queue_report(cfg, st0, st1):
+    """The broadcast queues over a run (gx.h gx_job): jobs deferred past the stored window, jobs LOST
+    (deferred jobs GetBroadcasts reached: the reference would have sent them), the first round of a
+    LOST dequeue, SendServices lists that did not fit, sleep-ring overflow, and the reference's own
+    MAX_PENDING_LENGTH truncation (services_delegate.go:109-120, not a deviation). faithful: no job
+    the reference would deliver was lost (every packet and looper state is the reference's)."""
+    p = CONFIGS[cfg]["p"]
+    ke = p.get("fanout", 3) * max(1, p.get("gossip_messages", 0))
+    d = {k: st1[k] - (st0[k] if st0 else 0) for k in ("queue_deferred", "queue_drops", "list_drops", "sleep_drops",
+                                                       "pending_drops", "retransmits", "dequeues")}
+    return {"window_jobs_per_host": p["queue_cap"], "lossless_rounds_after_fill": p["queue_cap"] // ke,
+            "retransmits": d["retransmits"], "dequeues": d["dequeues"], "deferred": d["queue_deferred"],
+            "lost": d["queue_drops"], "first_lost_round": st1["first_drop_round"], "list_drops": d["list_drops"],
+            "sleep_drops": d["sleep_drops"], "pending_truncated": d["pending_drops"],
+            "faithful": d["queue_drops"] == 0 and d["sleep_drops"] == 0}
 
 
 class Cluster:
@@ -294,6 +318,7 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
     wall = 0.0
     conv = None
     samples = []
+    st_end = None
     try:
         while c.round < max_rounds:
             barrier()
@@ -312,7 +337,8 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
                 # wall to convergence: the rounds past the convergence point are excluded pro rata
                 wall = wall * conv / c.round if c.round else wall
                 break
-        return conv, wall, c.round, samples
+        st_end = c.stats()
+        return conv, wall, c.round, samples, queue_report(cfg, None, st_end)
     finally:
         c.close()
 
@@ -475,21 +501,21 @@ def main():
 
     conv = None
     if not args.no_converge:
-        r, w, ran, dis_s = run_converge(lib, args.config, seed, rank, world, local_rank, barrier, args.converge_max,
-                                        args.check_every)
+        r, w, ran, dis_s, qr = run_converge(lib, args.config, seed, rank, world, local_rank, barrier,
+                                            args.converge_max, args.check_every)
         conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
-                "rounds_run": ran, "simulated_s": (r * 0.2) if r else None}
+                "rounds_run": ran, "simulated_s": (r * 0.2) if r else None, "queues": qr}
         if r is None:  # how far from agreement the catalog stays (records some live views disagree on)
             conv["disagreeing_records"] = {"min": min(x[1] for x in dis_s) if dis_s else None,
                                            "every_100_rounds": dis_s}
     conv_ref = None
     ref = CONFIGS[args.config].get("ref_variant")
     if ref and not args.no_converge:
-        r, w, ran, _ = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
-                                    args.check_every)
+        r, w, ran, _, qr = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
+                                        args.check_every)
         conv_ref = {"config": workload_text(ref), "rounds_to_converge": r,
                     "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
-                    "simulated_s": (r * 0.2) if r else None}
+                    "simulated_s": (r * 0.2) if r else None, "queues": qr}
     dis = None
     if world == 1 and CONFIGS[args.config]["p"].get("churn_ppm") and not args.no_converge:
         dis = dissemination(lib, args.config, seed, local_rank)  # churn never converges: spread latency
@@ -511,7 +537,8 @@ def main():
                        "parallelism": (f"host-sharded over {world} ranks ("
                                        + ("RCCL all-to-all)" if backend == "nccl" else "gloo, host-staged all-to-all)")
                                        if world > 1 else "single GPU")},
-            "merges": split, "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
+            "merges": split, "queues": queue_report(args.config, st0, st1),
+            "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
             "dissemination": dis,
             "roofline": roof, "roofline_merge": roofline("merge"), "roofline_send": roofline("send"),
             "cpu_baseline": cpu, "kernels": kern,

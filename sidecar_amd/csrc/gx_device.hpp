@@ -249,6 +249,7 @@ struct Acc {
   unsigned c[C_NCTR];
   bool changed;
   GXD Acc() : changed(false) {
+#pragma unroll
     for (int i = 0; i < C_NCTR; i++) c[i] = 0;
   }
 };
@@ -264,6 +265,7 @@ GXD void kbytes(const Dev &d, int k, unsigned long long b, unsigned long long u)
   if (u) atomicAdd(&d.ctr->units[shard_id()][k], u);
 }
 GXD void acc_flush(const Dev &d, const Acc &a) {
+#pragma unroll  // constant indices keep Acc in registers (a rolled loop moves it to scratch)
   for (int i = 0; i < C_NCTR; i++) {
     if (__ballot(a.c[i] != 0) == 0) continue;  // most counters are zero in most waves
     unsigned long long x = wave_sum((unsigned long long)a.c[i]);
@@ -456,21 +458,39 @@ GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const
     free_list_r(d, li(d, v), hs, j, lane0);
     return;
   }
-  if (lane0) {
-    gx_sleeper z;
-    z.job = j;
-    z.wake = wake;
-    z.pad[0] = z.pad[1] = z.pad[2] = 0;
-    d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail % d.SQ)] = z;
+  if (lane0) {  // two 16-B stores: the job, then wake and padding
+    gx_sleeper *z = &d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail % d.SQ)];
+    gx_u32x4 x0, x1;
+    x0.x = (uint32_t)j.a;
+    x0.y = (uint32_t)(j.a >> 32);
+    x0.z = j.c;
+    x0.w = j.meta;
+    x1.x = wake;
+    x1.y = x1.z = x1.w = 0u;
+    gst4(&z->job, x0);
+    gst4(&z->wake, x1);
   }
   hs.sleep_tail++;
 }
-// Scalar forms (one thread owns host v's bookkeeping).
+// Scalar forms (one thread owns host v's bookkeeping), field by field (a copy of the whole
+// bookkeeping struct would go through scratch memory).
 GXD void push_job(const Dev &d, Acc &a, uint32_t v, const gx_job &j) {
   gx_host_state *h = hst(d, v);
-  gx_host_state hs = *h;
-  push_job_r(d, a, v, hs, j, true);
-  *h = hs;
+  const uint32_t kind = GX_JOB_KIND(j.meta), tail = h->fifo_tail, stored = h->fifo_stored;
+  if (kind == GX_JOB_NIL_BS) h->nil_pos_bs = tail;
+  else if (kind == GX_JOB_NIL_BT) h->nil_pos_bt = tail;
+  if (fifo_room(d, h->fifo_head, tail, stored)) {
+    d.fifo[(size_t)li(d, v) * d.Q + (tail % d.Q)] = j;
+    h->fifo_stored = stored + 1;
+  } else {
+    a.c[C_QDEFER]++;
+    if (kind == GX_JOB_SEND) {  // only a LOST dequeue could reach it
+      uint32_t au = h->arena_used;
+      list_release(d, li(d, v), au, j.c & 0xffff, true);
+      h->arena_used = au;
+    }
+  }
+  h->fifo_tail = tail + 1;
 }
 GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
   gx_host_state *h = hst(d, v);
@@ -482,15 +502,13 @@ GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
 // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO tail.
 GXD void wake_host(const Dev &d, Acc &a, uint32_t v) {
   gx_host_state *h = hst(d, v);
-  gx_host_state hs = *h;
-  while (hs.sleep_head != hs.sleep_tail) {
-    const gx_sleeper &z = d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_head % d.SQ)];
+  while (h->sleep_head != h->sleep_tail) {
+    const gx_sleeper &z = d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_head % d.SQ)];
     if ((int64_t)z.wake > d.round) break;
     const gx_job j = z.job;
-    hs.sleep_head++;
-    push_job_r(d, a, v, hs, j, true);
+    h->sleep_head++;
+    push_job(d, a, v, j);
   }
-  *h = hs;
 }
 
 // Take the FIFO head (fifo_head != fifo_tail) on the register copy: a stored job, or, past the

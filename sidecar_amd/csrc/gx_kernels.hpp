@@ -1163,8 +1163,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
             if (lead) kb += 16ull * npf;
           }
           jb = pjs[q];
+          hs.fifo_head++;
+        } else {
+          jb = pop_job_r(d, idx, hs, nullptr);  // past the stored window: a looper's nil or LOST
         }
-        jb = pop_job_r(d, idx, hs, &jb);  // past the stored window: a looper's nil or LOST
         if (lead) a.c[C_DEQ]++;
         const uint32_t kind = GX_JOB_KIND(jb.meta), pass = GX_JOB_PASS(jb.meta), npass = GX_JOB_NPASSES(jb.meta);
         if (kind == GX_JOB_LOST) {  // a deferred job reached the head: its batch is unknown
