@@ -310,6 +310,87 @@ def dissemination(lib, cfg, seed, local_rank, start=100, rounds=300):
         e.close()
 
 
+def version_spread(e, dev, heal, end, check_every=10, slots=16):
+    """Convergence figure that stays defined while owners keep restamping (Sidecar's 60 s refresh,
+    services_state.go:547) and expiry keeps re-tombstoning (:655-679): per record, how long an owner's
+    version takes to reach every live view. A view "holds" version T of record r when its word for r
+    has Updated >= T (a view's slot time only grows, services_state.go:321, so this is monotone).
+      heal:  T = the owner's own word at the heal round; rounds from the heal until every live view
+             holds it.
+      born:  every version an owner stamps itself after the heal (TrackNewServices / TombstoneServices
+             restamp Updated = now, services_state.go:446-453,703): rounds from the check that saw it
+             until every live view holds it. A version not held everywhere by `end` is unfinished.
+    Checked every `check_every` rounds (per-record min over live views, gx_view_minmax, and the
+    owners' words, gx_owner_words), so latencies are multiples of check_every."""
+    import torch
+    R = e.H * e.S
+    i64 = torch.int64
+    own = torch.empty(R, dtype=i64, device=dev)
+    mn = torch.empty(R, dtype=i64, device=dev)
+    mx = torch.empty(R, dtype=i64, device=dev)
+    SIGN = -(1 << 63)
+    M61 = (1 << 61) - 1
+
+    def ts(w):  # slot time of packed words held in int64 (a logical shift)
+        return torch.where((w & 7) == 7, torch.full_like(w, -1), (w >> 3) & M61)  # absent: no version
+
+    def min_ts():
+        e.view_minmax(mn.data_ptr(), mx.data_ptr())
+        return ts(mn ^ SIGN)  # the min word itself
+
+    e.run_rounds(heal - e.round)
+    e.owner_words(own.data_ptr())
+    prev = own.clone()
+    heal_T = ts(own)
+    heal_lat = torch.full((R,), -1, dtype=i64, device=dev)
+    pend_T = torch.full((R, slots), 1 << 62, dtype=i64, device=dev)
+    pend_b = torch.zeros((R, slots), dtype=i64, device=dev)
+    nxt = torch.zeros(R, dtype=i64, device=dev)
+    lats, overflow, born = [], 0, 0
+    rows = torch.arange(R, device=dev)
+    mt = min_ts()
+    heal_lat = torch.where((heal_T >= 0) & (mt >= heal_T), torch.zeros_like(heal_lat), heal_lat)
+    while e.round < end:
+        r0 = e.round
+        e.run_rounds(min(check_every, end - e.round))
+        e.owner_words(own.data_ptr())
+        t0_window = e.params.t0_ns - e.epoch + (r0 + 1) * e.params.round_ns  # stamped by the owner in the window
+        new = (own != prev) & (ts(own) >= t0_window)
+        prev.copy_(own)
+        if bool(new.any()):
+            idx = rows[new]
+            born += int(idx.numel())
+            full = pend_T[idx, nxt[idx] % slots] < (1 << 62)
+            overflow += int(full.sum())
+            pend_T[idx, nxt[idx] % slots] = ts(own[idx])
+            pend_b[idx, nxt[idx] % slots] = e.round
+            nxt[idx] += 1
+        mt = min_ts()
+        done = pend_T <= mt[:, None]
+        if bool(done.any()):
+            lats.append((e.round - pend_b[done]).cpu())
+            pend_T[done] = 1 << 62
+        hl = (heal_T >= 0) & (heal_lat < 0) & (mt >= heal_T)
+        heal_lat = torch.where(hl, torch.full_like(heal_lat, e.round - heal), heal_lat)
+
+    def q(x):
+        if not x.numel():
+            return None
+        x = x.double()
+        qs = torch.quantile(x, torch.tensor([0.5, 0.99], dtype=torch.float64)) if x.numel() < (1 << 24) else \
+            torch.tensor([float(x.median()), float(x.kthvalue(max(1, int(0.99 * x.numel())))[0])])
+        return {"p50_rounds": float(qs[0]), "p99_rounds": float(qs[1]), "max_rounds": float(x.max())}
+
+    hv = heal_lat[heal_T >= 0].cpu()
+    lat = torch.cat(lats) if lats else torch.empty(0, dtype=i64)
+    return {"definition": "a view holds version T of a record when its slot's Updated >= T; latency = rounds "
+                          "until every live view holds it (checked every %d rounds)" % check_every,
+            "rounds": [heal, end],
+            "heal_version": dict(q(hv[hv >= 0]) or {}, records=int(hv.numel()), unfinished=int((hv < 0).sum())),
+            "born_after_heal": dict(q(lat) or {}, versions=born, spread=int(lat.numel()),
+                                    unfinished=int((pend_T < (1 << 62)).sum()), ring_overflow=overflow)}
+
+
 def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
     """Fresh cluster from round 0: chunks of `check_every` rounds, catalog agreement checked
     between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run,
@@ -516,6 +597,14 @@ def main():
         conv_ref = {"config": workload_text(ref), "rounds_to_converge": r,
                     "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
                     "simulated_s": (r * 0.2) if r else None, "queues": qr}
+    spread = None
+    heal = CONFIGS[args.config]["p"].get("partition_end", 0)
+    if world == 1 and heal and not args.no_converge:  # per-version spread after the heal (defined at any cadence)
+        e = make_engine(lib, args.config, seed, local_rank)
+        try:
+            spread = version_spread(e, torch.device(f"cuda:{local_rank}"), heal, args.converge_max)
+        finally:
+            e.close()
     dis = None
     if world == 1 and CONFIGS[args.config]["p"].get("churn_ppm") and not args.no_converge:
         dis = dissemination(lib, args.config, seed, local_rank)  # churn never converges: spread latency
@@ -539,7 +628,7 @@ def main():
                                        if world > 1 else "single GPU")},
             "merges": split, "queues": queue_report(args.config, st0, st1),
             "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
-            "dissemination": dis,
+            "dissemination": dis, "version_spread": spread,
             "roofline": roof, "roofline_merge": roofline("merge"), "roofline_send": roofline("send"),
             "cpu_baseline": cpu, "kernels": kern,
             "kernels_scope": "whole engine" if world == 1 else "rank 0's shard (device time and bytes of its launches)",

@@ -444,6 +444,10 @@ int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */
  * shards order them like the unsigned words. All views agree on record r iff the reduced min
  * equals the reduced max. */
 int gx_view_minmax(gx_engine *e, uint64_t *min_out, uint64_t *max_out);
+/* The owner's own word of every record: out[r] = slot r of host r / S's own view (the version the
+ * owner holds), for the owners this engine holds, 0 for the others (R entries; device memory for
+ * the HIP engine, so a MAX reduction across shards gives every owner's word). */
+int gx_owner_words(gx_engine *e, uint64_t *out);
 
 /* ---- catalog.ServicesState ---------------------------------------------------------------- */
 /* AddServiceEntry, services_state.go:293-347, applied in array order (views[i] <- svcs[i]). */

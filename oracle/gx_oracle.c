@@ -1249,30 +1249,33 @@ static int check_params(const gx_params *p) {
 static void init_state(gx_engine *e) {
   const gx_params *p = &e->p;
   uint32_t H = e->H, S = e->S, R = e->R;
-  for (size_t i = 0; i < (size_t)H * R; i++) e->view[i] = GX_SLOT_ABSENT;
-  for (uint32_t r = 0; r < R && p->init_mode != GX_INIT_EMPTY; r++) {
+  /* the initial word of every record (ALIVE, t0 - U[0, 1 s), or aged), then the views row by row */
+  uint64_t *rec = (uint64_t *)malloc(sizeof(uint64_t) * R);
+  for (uint32_t r = 0; r < R; r++) {
     int64_t ts = p->t0_ns - (int64_t)(rng4(p->seed, ST_INIT_TS, r, 0, 0) % 1000000000ull);
     if (p->aged_ppm && (rng4(p->seed, ST_INIT_AGE, r, 0, 0) % 1000000ull) < p->aged_ppm && p->aged_max_ns > 0)
       ts = p->t0_ns - (int64_t)(rng4(p->seed, ST_INIT_AGE, r, 1, 0) % (uint64_t)p->aged_max_ns);
-    uint64_t w = pack(ts, GX_ALIVE);
-    if (p->init_mode == GX_INIT_OWN) {
-      e->view[(size_t)(r / S) * R + r] = w;
-    } else {
-      for (uint32_t v = 0; v < H; v++) e->view[(size_t)v * R + r] = w;
-    }
+    rec[r] = pack(ts, GX_ALIVE);
   }
   /* initial records count as inserted in key order (no events): LastUpdated = LastChanged = the
    * owner's last record, state.LastChanged = the view's last record */
-  memset(e->srvt, 0, sizeof(gx_server_times) * (size_t)H * H);
-  memset(e->vlc, 0, sizeof(int64_t) * H);
-  for (uint32_t v = 0; v < H && p->init_mode != GX_INIT_EMPTY; v++)
+#ifdef GX_ORACLE_OMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (uint32_t v = 0; v < H; v++) {
+    uint64_t *row = &e->view[(size_t)v * R];
+    gx_server_times *t = &e->srvt[(size_t)v * H];
+    memset(t, 0, sizeof(gx_server_times) * H);
+    e->vlc[v] = 0;
     for (uint32_t r = 0; r < R; r++) {
-      uint64_t w = e->view[(size_t)v * R + r];
-      if (st_of(w) == GX_ABSENT) continue;
-      e->srvt[(size_t)v * H + r / S].last_updated_ns = ts_of(w);
-      e->srvt[(size_t)v * H + r / S].last_changed_ns = ts_of(w);
-      e->vlc[v] = ts_of(w);
+      const int have = p->init_mode == GX_INIT_WARM || (p->init_mode == GX_INIT_OWN && r / S == v);
+      row[r] = have ? rec[r] : GX_SLOT_ABSENT;
+      if (!have) continue;
+      t[r / S].last_updated_ns = t[r / S].last_changed_ns = ts_of(rec[r]);
+      e->vlc[v] = ts_of(rec[r]);
     }
+  }
+  free(rec);
   memset(e->own_status, GX_ALIVE, (size_t)H * S);
   for (uint32_t o = 0; o < H; o++) {
     gx_host_state *h = &e->hs[o];
@@ -2491,6 +2494,15 @@ int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
       mn[r] ^= 1ull << 63;
       mx[r] ^= 1ull << 63;
     }
+  }
+  return GX_OK;
+}
+
+int gx_owner_words(gx_engine *e, uint64_t *out) {
+  if (!e || !out) return GX_EINVAL;
+  for (uint32_t r = 0; r < e->R; r++) {
+    const uint32_t o = r / e->S;
+    out[r] = is_local(e, o) ? e->view[(size_t)o * e->R + r] : 0;
   }
   return GX_OK;
 }

@@ -221,7 +221,7 @@ ABI_FUNCS = [
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_exchange_plan", "gx_outbox_pack_planned", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
-    "gx_view_minmax", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
+    "gx_view_minmax", "gx_owner_words", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_set_stream", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
     "gx_fd_defaults", "gx_fd_read_members", "gx_fd_read_hosts", "gx_fd_read_queue", "gx_fd_notify",
@@ -272,7 +272,7 @@ def _declare(lib):
         "gx_exchange_plan": ([vp, vp], i32), "gx_outbox_pack_planned": ([vp, vp, C.c_uint64], i32),
         "gx_round_merge": ([vp], i32), "gx_ae_bytes": ([vp, vp], i32),
         "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64, vp, C.c_uint64], i32),
-        "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32),
+        "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32), "gx_owner_words": ([vp, vp], i32),
         "gx_ae_merge_local": ([vp], i32),
         "gx_read_server_times": ([vp, u32, u32, u32, vp], i32),
         "gx_read_last_changed": ([vp, u32, u32, vp], i32),
@@ -815,6 +815,10 @@ class Engine:
 
     def view_minmax(self, ptr_min: int, ptr_max: int):
         check(self.lib.gx_view_minmax(self.h, C.c_void_p(ptr_min), C.c_void_p(ptr_max)), "gx_view_minmax")
+
+    def owner_words(self, ptr: int):
+        """R words at ptr (device memory for the HIP engine): each record's word in its owner's view."""
+        check(self.lib.gx_owner_words(self.h, C.c_void_p(ptr)), "gx_owner_words")
 
     # memberlist failure detection (SURVEY §8f-3) ---------------------------------------------
     def fd_members(self, host: int, lo: int = 0, hi: Optional[int] = None) -> bytes:

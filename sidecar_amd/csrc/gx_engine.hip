@@ -2278,6 +2278,13 @@ int gx_round_end(gx_engine *e) {
   return rc ? rc : phase_done(e);
 }
 
+int gx_owner_words(gx_engine *e, uint64_t *out) {
+  if (!e || !out) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  k_owner_words<<<nblk(e->d.R, 256), 256, 0, e->stream>>>(e->d, out);
+  return sync_check(e);
+}
+
 int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
   if (!e || !mn || !mx) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));

@@ -3632,6 +3632,13 @@ __global__ void k_view_minmax(Dev d, uint64_t *mn, uint64_t *mx) {
   mx[r] = b ^ (1ull << 63);
 }
 
+__global__ void k_owner_words(Dev d, uint64_t *out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= d.R) return;
+  const uint32_t o = owner_of(d, r);
+  out[r] = o - d.lo < d.Hl ? d.view[(size_t)(o - d.lo) * d.R + r] : 0ull;
+}
+
 // ================================================================ convergence / digests ==
 __global__ void k_converged(Dev d, unsigned long long *bad) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
