@@ -348,6 +348,9 @@ class Cluster {
     codec_dirty_ = false;
     codec_cluster_ = cluster;
   }
+  // Decoding does not depend on the cluster name: keep the one the codec holds (an Encode with a
+  // non-default name followed by a Decode would otherwise rebuild all H*S fragments twice).
+  void SyncCodecForDecode() { SyncCodec(codec_cluster_.empty() ? std::string("default") : codec_cluster_); }
   // Hands the engine the Service.Name of every record (gx_set_service_names) when one changed.
   void SyncNames() {
     if (!names_dirty_) return;
@@ -599,7 +602,7 @@ class ServicesState {
 // ok = false where the reference's UnmarshalJSON fails ("Decode() returns an error when handed
 // junk", services_state_test.go:109-114); the services are then empty.
 inline std::vector<Service> Decode(Cluster &c, const std::string &data, bool *ok = nullptr) {
-  c.SyncCodec();
+  c.SyncCodecForDecode();
   std::vector<gx_service> out(64);
   uint32_t n = 0;
   gx_decode_stats ds{};

@@ -25,7 +25,8 @@
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2u64 ldnt(const uint64_t *p) { return __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(p)); }
 
-template <int PF>
+// BAR: one __syncthreads_or per tile (k_ae's retransmit check); ALU: the merge rule's compares
+template <int PF, bool BAR = false, bool ALU = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_reg(const uint64_t *t, uint32_t R,
                                                                                       uint64_t *out) {
   const uint64_t *A = t + (size_t)(2 * blockIdx.x) * R, *B = A + R;
@@ -47,11 +48,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     for (int s = 0; s < PF; s++) {
       v2u64 wa[2] = {qa[s][0], qa[s][1]}, wb[2] = {qb[s][0], qb[s][1]};
       if (base + 1024u * (PF + s) < R) load(base + 1024u * (PF + s), qa[s], qb[s]);
+      uint32_t fl = 0;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        acc += (wa[h].x > wb[h].x) + (wa[h].y > wb[h].y);
+        if (ALU) {  // merge_word both ways: stale gate, absent, strictly newer, DRAINING stickiness
+          const uint64_t x[2] = {wa[h].x, wa[h].y}, y[2] = {wb[h].x, wb[h].y};
+#pragma unroll
+          for (int k = 0; k < 2; k++) {
+            const int64_t tx = (int64_t)(x[k] >> 3), ty = (int64_t)(y[k] >> 3);
+            const bool sx = tx < (int64_t)R, sy = ty < (int64_t)R;
+            const bool ax = (y[k] & 7) == 7 || (!sx && tx > ty), ay = (x[k] & 7) == 7 || (!sy && ty > tx);
+            const uint64_t nx = ax ? (((y[k] & 7) == 4 && (x[k] & 7) == 0) ? (x[k] & ~7ull) | 4 : x[k]) : y[k];
+            const uint64_t ny = ay ? x[k] : y[k];
+            acc += (nx != y[k]) + (ny != x[k]) + sx + sy;
+            fl |= (uint32_t)(ax | ay) << (2 * h + k);
+          }
+        } else {
+          acc += (wa[h].x > wb[h].x) + (wa[h].y > wb[h].y);
+        }
         acc ^= wa[h].x ^ wb[h].y;
       }
+      if (BAR && __syncthreads_or(fl != 0 && acc == 0x1234567)) out[blockIdx.x] = 1;
     }
   }
   if (acc == 0x1234567) out[blockIdx.x] = acc;
@@ -128,6 +145,16 @@ int main(int argc, char **argv) {
   };
   run("reg_pf1", [&] { k_reg<1><<<H / 2, 256>>>(t, R, out); });
   run("reg_pf2", [&] { k_reg<2><<<H / 2, 256>>>(t, R, out); });
+  run("reg_pf1_bar", [&] { k_reg<1, true><<<H / 2, 256>>>(t, R, out); });
+  run("reg_pf1_alu", [&] { k_reg<1, false, true><<<H / 2, 256>>>(t, R, out); });
+  run("reg_pf1_alu_bar", [&] { k_reg<1, true, true><<<H / 2, 256>>>(t, R, out); });
+  run("reg_pf2_alu_bar", [&] { k_reg<2, true, true><<<H / 2, 256>>>(t, R, out); });
+  // k_ae holds 123 VGPRs -> 4 waves/SIMD (4 blocks per CU); the reg kernels above fit 6-8. 36 KB of
+  // dynamic LDS per block pins them to 4 blocks per CU, k_ae's residency
+  const size_t occ4 = 36 * 1024;
+  run("reg_pf1_alu_bar_occ4", [&] { k_reg<1, true, true><<<H / 2, 256, occ4>>>(t, R, out); });
+  run("reg_pf2_alu_bar_occ4", [&] { k_reg<2, true, true><<<H / 2, 256, occ4>>>(t, R, out); });
+  run("reg_pf1_occ4", [&] { k_reg<1><<<H / 2, 256, occ4>>>(t, R, out); });
   run("glds_ring2", [&] { k_glds<2><<<H / 2, 256>>>(t, R, out); });
   run("glds_ring3", [&] { k_glds<3><<<H / 2, 256>>>(t, R, out); });
   run("glds_ring4", [&] { k_glds<4><<<H / 2, 256>>>(t, R, out); });

@@ -746,6 +746,13 @@ class Engine:
         check(self.lib.gx_exchange_plan(self.h, out.ctypes.data_as(C.c_void_p)), "gx_exchange_plan")
         return out.reshape(G, G)
 
+    def xplan_waits(self):
+        """(calls of gx_exchange_plan that waited on the host for their batch, all calls): a
+        diagnostics symbol of the HIP engine, not in gx.h."""
+        out = (C.c_uint64 * 2)()
+        check(self.lib.gx_xplan_waits(self.h, out), "gx_xplan_waits")
+        return int(out[0]), int(out[1])
+
     def outbox_pack_planned(self, ptr: int, cap: int):
         check(self.lib.gx_outbox_pack_planned(self.h, C.c_void_p(ptr), C.c_uint64(cap)), "gx_outbox_pack_planned")
 

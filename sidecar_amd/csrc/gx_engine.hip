@@ -145,6 +145,7 @@ struct gx_engine {
   uint32_t *xplan_dev;           // [XPLAN_BATCH][G][G]
   uint32_t *xplan_host;          // [2][XPLAN_BATCH][G][G] pinned
   int64_t xplan_start[2];
+  uint64_t xplan_waits[2];       // diagnostics: calls whose batch was not ready yet (a host wait) / all calls
   hipEvent_t xplan_ev[2];
   int64_t xbound_round;          // the round xbound holds
   XBound xbound;                 // this shard's slots per destination this round
@@ -931,6 +932,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->xplan_stream = nullptr;
   e->xplan_dev = e->xplan_host = nullptr;
   e->xplan_start[0] = e->xplan_start[1] = -1;
+  e->xplan_waits[0] = e->xplan_waits[1] = 0;
   e->xplan_ev[0] = e->xplan_ev[1] = nullptr;
   e->xbound_round = -1;
   e->kprof_n = 0;
@@ -1861,7 +1863,14 @@ static int xplan_counts(gx_engine *e, const uint32_t **out) {
   if (e->xplan_start[k] != start) rc = xplan_launch(e, k, start);
   if (!rc && e->xplan_start[k ^ 1] != start + XPLAN_BATCH) rc = xplan_launch(e, k ^ 1, start + XPLAN_BATCH);
   if (rc) return rc;
-  HIPCHK(hipEventSynchronize(e->xplan_ev[k]));
+  e->xplan_waits[1]++;
+  const hipError_t q = hipEventQuery(e->xplan_ev[k]);
+  if (q == hipErrorNotReady) {
+    e->xplan_waits[0]++;  // this call blocks the host
+    HIPCHK(hipEventSynchronize(e->xplan_ev[k]));
+  } else {
+    HIPCHK(q);
+  }
   *out = e->xplan_host + ((size_t)k * XPLAN_BATCH + (size_t)(d.round - start)) * d.G * d.G;
   return GX_OK;
 }
@@ -1896,7 +1905,6 @@ int gx_outbox_pack_planned(gx_engine *e, void *buf, uint64_t cap) {
   uint64_t slots = 0;
   for (uint32_t g = 0; g < d.G; g++) slots += e->xbound.n[g];
   if (cap < slots * slot_bytes(d)) return GX_EINVAL;
-  if (!slots) return GX_OK;
   HIPCHK(hipSetDevice(e->device));
   set_round_fields(e);
   const size_t ne = (size_t)d.Hl * d.KE;
@@ -1906,7 +1914,8 @@ int gx_outbox_pack_planned(gx_engine *e, void *buf, uint64_t cap) {
   k_ob_count<<<nchunk, 256, lds, e->stream>>>(d, ccnt);
   k_ob_scan<<<1, 256, 0, e->stream>>>(d, ccnt, nchunk, off, e->ob_counts);
   k_ob_fill<<<nchunk, 256, lds, e->stream>>>(d, off, e->ob_entries);
-  k_outbox_pack_planned<<<(unsigned)slots, 64, 0, e->stream>>>(d, e->ob_entries, e->ob_counts, e->xbound, (uint8_t *)buf);
+  // one block at least: block 0 checks every destination's packets against its plan bound
+  k_outbox_pack_planned<<<(unsigned)(slots ? slots : 1), 64, 0, e->stream>>>(d, e->ob_entries, e->ob_counts, e->xbound, (uint8_t *)buf);
   e->n_ob = 0;
   e->ob_async = false;
   return phase_done(e);
@@ -2535,6 +2544,15 @@ int gx_fd_converged(gx_engine *e, int *converged, uint64_t *n_disagree) {
   if (rc) return rc;
   if (converged) *converged = bad == 0;
   if (n_disagree) *n_disagree = bad;
+  return GX_OK;
+}
+
+// Diagnostics outside gx.h: out[0] = gx_exchange_plan calls that found their batch of slot bounds
+// not computed yet and waited on the host, out[1] = all calls.
+int gx_xplan_waits(gx_engine *e, uint64_t *out) {
+  if (!e || !out) return GX_EINVAL;
+  out[0] = e->xplan_waits[0];
+  out[1] = e->xplan_waits[1];
   return GX_OK;
 }
 

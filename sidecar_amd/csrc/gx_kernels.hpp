@@ -3484,6 +3484,9 @@ __global__ __launch_bounds__(256) void k_xplan(Dev d, int64_t r0, uint32_t *cnt)
 // first (ob_fill's entries for g, tot[g] of them), then empty ones (sender key GX_SLOT_EMPTY).
 __global__ void k_outbox_pack_planned(Dev d, const uint32_t *entry, const uint32_t *tot, XBound bound, uint8_t *out) {
   const uint32_t i = blockIdx.x;
+  if (i == 0 && threadIdx.x == 0)  // every destination, also one whose region has no slot (cannot happen)
+    for (uint32_t x = 0; x < d.G; x++)
+      if (tot[x] > bound.n[x]) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);
   uint32_t g = 0, acc = 0, eoff = 0;
   while (g < d.G && i >= acc + bound.n[g]) {
     acc += bound.n[g];
@@ -3494,7 +3497,6 @@ __global__ void k_outbox_pack_planned(Dev d, const uint32_t *entry, const uint32
   const uint32_t j = i - acc;
   const size_t sb = 16 + 16ull * d.p.packet_cap + 16ull * (d.p.fd_enable ? d.p.fd_msg_cap : 0);
   uint8_t *dst = out + (size_t)i * sb;
-  if (j == 0 && threadIdx.x == 0 && tot[g] > bound.n[g]) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);  // cannot happen
   if (j < tot[g]) {
     pack_slot(d, entry[eoff + j], dst);
   } else if (threadIdx.x == 0) {

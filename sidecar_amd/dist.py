@@ -117,7 +117,8 @@ class LocalShards:
         return t.cpu().numpy().astype(np.uint64)
 
     def run_rounds(self, n: int):
-        planned = not self.shards[0].e.params.fd_enable  # sizes from the seeded plan (gx_exchange_plan)
+        p0 = self.shards[0].e.params  # sizes from the seeded plan (gx_exchange_plan); see DistShard.run_rounds
+        planned = not p0.fd_enable and p0.gossip_messages == 1
         for _ in range(n):
             for s in self.shards:
                 s.e.round_send()
@@ -295,7 +296,10 @@ class DistShard:
 
     def run_rounds(self, n: int):
         e = self.e
-        planned = not e.params.fd_enable  # sizes from the seeded plan: no host wait in gossip rounds
+        # sizes from the seeded plan: no host wait in gossip rounds. The plan reserves GossipMessages
+        # slots per sampled peer, so past one message per round it ships mostly padding (GM 15:
+        # ~85 MB per rank per round at cfg 5, G = 8): there the exact sizes are gathered instead.
+        planned = not e.params.fd_enable and e.params.gossip_messages == 1
         for _ in range(n):
             e.round_send()
             if planned:

@@ -148,11 +148,17 @@ def test_gpu_planned_exchange_sync_free(gx_lib, oracle_lib):
     sh = LocalShards(gx_lib, 4, device="cuda:0", **kw)
     sh.run_rounds(11)
     torch.cuda.synchronize()
+    w0 = [s.xplan_waits() for s in sh.engines]
     torch.cuda.set_sync_debug_mode("error")
     try:
         sh.run_rounds(9)
     finally:
         torch.cuda.set_sync_debug_mode(0)
+    # the engine's own host waits, which torch cannot see: every batch of slot bounds was computed
+    # before the round that needed it
+    w1 = [s.xplan_waits() for s in sh.engines]
+    assert all(b[1] - a[1] == 9 for a, b in zip(w0, w1)), (w0, w1)
+    assert all(b[0] == a[0] for a, b in zip(w0, w1)), f"blocking plan waits in the sync-free stretch: {w0} -> {w1}"
     sh.run_rounds(40)  # the heal and the post-heal push-pull rounds
     whole.run_rounds(60)
     orc.run_rounds(60)
