@@ -3,7 +3,11 @@ read through gx_kprof_read (engine created with GX_KPROF set). Prints, per mark,
 waves relative to the launch's first start mark: how long the owner ticks, the block barrier, the
 plan and the record phase take, and which waves finish last.
 
-  GX_KPROF=1 python profiles/kprof.py [--config cfg5] [--rounds 21 51]
+  GX_KPROF=1 python profiles/kprof.py [--config cfg5] [--rounds 21 51] [--ae-rounds 10 20]
+
+With --ae-rounds: the push-pull launch of each such round, per block (start, end, CU): the block
+durations, how busy the CUs' slots were over the launch, and the launch's tail (when the CUs ran
+out of blocks).
 """
 import argparse
 import ctypes
@@ -28,7 +32,34 @@ def marks(e, lib):
     buf = (ctypes.c_uint64 * n.value)()
     assert lib.gx_kprof_read(e.h, buf, ctypes.c_uint64(n.value), ctypes.byref(n)) == 0
     a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
-    return a[:-MERGE_N].reshape(-1, 8), a[-MERGE_N:]
+    ns = a.size - MERGE_N - e.H  # layout: k_send marks, merge counters, push-pull block marks
+    return a[:ns].reshape(-1, 8), a[ns:ns + MERGE_N], a[ns + MERGE_N:].reshape(-1, 2)
+
+
+def summarize_ae(m):
+    m = m[m[:, 0] > 0]
+    start = m[:, 0] & ((1 << 48) - 1)
+    cu = m[:, 0] >> 48
+    end = m[:, 1]
+    t0 = start.min()
+    span = float(end.max() - t0)
+    dur = (end - start) / 100.0
+    out = {"blocks": int(m.shape[0]), "span_us": round(span / 100.0, 1),
+           "block_us": {q: round(float(np.percentile(dur, q)), 1) for q in (1, 10, 50, 90, 99)},
+           "block_us_max": round(float(dur.max()), 1)}
+    cus = np.unique(cu)
+    last = np.array([end[cu == c].max() - t0 for c in cus]) / 100.0
+    first = np.array([start[cu == c].min() - t0 for c in cus]) / 100.0
+    busy = np.array([dur[cu == c].sum() for c in cus])
+    nb = np.array([(cu == c).sum() for c in cus])
+    out["cus"] = int(cus.size)
+    out["blocks_per_cu"] = {"min": int(nb.min()), "max": int(nb.max())}
+    out["cu_first_start_us"] = {"p50": round(float(np.median(first)), 1), "max": round(float(first.max()), 1)}
+    out["cu_last_end_us"] = {"min": round(float(last.min()), 1), "p50": round(float(np.median(last)), 1),
+                             "max": round(float(last.max()), 1)}
+    # mean blocks resident per CU over the launch (sum of block durations / span)
+    out["resident_blocks_per_cu"] = round(float(busy.mean() / (span / 100.0)), 2)
+    return out
 
 
 def summarize(m):
@@ -50,7 +81,8 @@ def summarize(m):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg5")
-    ap.add_argument("--rounds", type=int, nargs="+", default=[21, 51])
+    ap.add_argument("--rounds", type=int, nargs="*", default=[21, 51])
+    ap.add_argument("--ae-rounds", type=int, nargs="*", default=[])
     a = ap.parse_args()
     import bench
     from sidecar_amd.abi import load_product
@@ -58,14 +90,17 @@ def main():
     lib.gx_kprof_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     e = bench.make_engine(lib, a.config, 0x5EED, 0)
     res = {}
-    for r in sorted(a.rounds):
+    for r in sorted(set(a.rounds) | set(a.ae_rounds)):
         e.run_rounds(r - e.round)
-        _, m0 = marks(e, lib)
-        e.run_rounds(1)  # round r: its k_send's marks, its merge's path counts
-        wm, m1 = marks(e, lib)
-        res[r] = summarize(wm)
-        res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES)}
-        print(json.dumps({"config": a.config, "round": r, **res[r]}), flush=True)
+        _, m0, _ = marks(e, lib)
+        e.run_rounds(1)  # round r: its k_send's marks, its merge's path counts, its push-pull blocks
+        wm, m1, am = marks(e, lib)
+        if r in a.rounds:
+            res[r] = summarize(wm)
+            res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES)}
+            print(json.dumps({"config": a.config, "round": r, **res[r]}), flush=True)
+        if r in a.ae_rounds:
+            print(json.dumps({"config": a.config, "round": r, "push_pull": summarize_ae(am)}), flush=True)
     e.close()
 
 

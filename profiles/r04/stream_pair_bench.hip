@@ -26,10 +26,14 @@ typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2u64 ldnt(const uint64_t *p) { return __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(p)); }
 
 // BAR: one __syncthreads_or per tile (k_ae's retransmit check); ALU: the merge rule's compares
-template <int PF, bool BAR = false, bool ALU = false>
+// PERM: the pair's rows are scattered over the table like k_ae's seeded pairing (odd-multiplier
+// permutation of the row numbers, H a power of two) instead of adjacent
+template <int PF, bool BAR = false, bool ALU = false, bool PERM = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_reg(const uint64_t *t, uint32_t R,
                                                                                       uint64_t *out) {
-  const uint64_t *A = t + (size_t)(2 * blockIdx.x) * R, *B = A + R;
+  const uint32_t H = 2 * gridDim.x, ra = PERM ? (2 * blockIdx.x * 0x9E3779B1u + 12345u) & (H - 1) : 2 * blockIdx.x;
+  const uint32_t rb = PERM ? ((2 * blockIdx.x + 1) * 0x9E3779B1u + 12345u) & (H - 1) : ra + 1;
+  const uint64_t *A = t + (size_t)ra * R, *B = t + (size_t)rb * R;
   const uint32_t tid = threadIdx.x;
   v2u64 qa[PF][2], qb[PF][2];
   auto load = [&](uint32_t base, v2u64 *xa, v2u64 *xb) {
@@ -154,6 +158,8 @@ int main(int argc, char **argv) {
   const size_t occ4 = 36 * 1024;
   run("reg_pf1_alu_bar_occ4", [&] { k_reg<1, true, true><<<H / 2, 256, occ4>>>(t, R, out); });
   run("reg_pf2_alu_bar_occ4", [&] { k_reg<2, true, true><<<H / 2, 256, occ4>>>(t, R, out); });
+  run("reg_pf1_alu_bar_perm", [&] { k_reg<1, true, true, true><<<H / 2, 256>>>(t, R, out); });
+  run("reg_pf1_alu_bar_perm_occ4", [&] { k_reg<1, true, true, true><<<H / 2, 256, occ4>>>(t, R, out); });
   run("reg_pf1_occ4", [&] { k_reg<1><<<H / 2, 256, occ4>>>(t, R, out); });
   run("glds_ring2", [&] { k_glds<2><<<H / 2, 256>>>(t, R, out); });
   run("glds_ring3", [&] { k_glds<3><<<H / 2, 256>>>(t, R, out); });

@@ -1039,6 +1039,9 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 GXD unsigned long long *kprof_merge(const Dev &d) {
   return d.kprof ? d.kprof + (size_t)((d.Hl + 63) / 64) * 4 * 8 : nullptr;
 }
+// Diagnostics: after the merge counters, two marks per push-pull block of the last k_ae launch:
+// [2i] start | CU << 48, [2i + 1] end (wall clock, 100 MHz)
+GXD unsigned long long *kprof_ae(const Dev &d) { return d.kprof ? kprof_merge(d) + GX_KPROF_MERGE_N : nullptr; }
 // Diagnostics: wall-clock mark k of this wave (k_send phases; Dev::kprof, env GX_KPROF).
 #define GX_KP(k)                                                                                   \
   do {                                                                                             \
@@ -2457,9 +2460,13 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         dec_pair_u(enc, r0 - blk * GX_DIGEST_SLOTS, v0, v1, &xb[2 * h]);
         continue;
       }
-      if (VEC && v0) {
-        ulonglong2 pa = ld16<NT>(&A[r0]);
-        ulonglong2 pb = ld16<NT>(Bp);
+      if (VEC) {
+        // unconditional loads (a tail tile's slots past R read slot 0 and are masked where the
+        // tile is merged): a guarded load here makes the compiler wait on the tile in flight
+        // inside the merge of the current one (profiles/r04/kprof_ae.jsonl)
+        const uint32_t rc = v0 ? r0 : 0;
+        ulonglong2 pa = ld16<NT>(&A[rc]);
+        ulonglong2 pb = ld16<NT>(&B[rc]);
         xa[2 * h] = pa.x;
         xa[2 * h + 1] = pa.y;
         xb[2 * h] = pb.x;
@@ -2477,12 +2484,18 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     uint64_t nwa[4], nwb[4];
     bool fa[4], fb[4];
     uint32_t accb = 0;  // bit k: side a accepted slot k, bit 8 + k: side b
+    // every element defined before the first merge: a partly defined array is copied as a vector
+    // whose undefined elements are whatever registers the next tile is loading into, and the copy
+    // then waits for those loads (the pipeline stalls inside the merge)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       nwa[k] = wa[k];
       nwb[k] = wb[k];
       fa[k] = fb[k] = false;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
       if (st_of(wb[k]) != GX_ABSENT) {  // a.Merge(b): every present record of b
         bool ac, st;
         c_merge++;
@@ -2618,6 +2631,11 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
           wa[k] = qa[s][k];
           wb[k] = qb[s][k];
         }
+        if (VEC && bs + TILE > d.R) {  // the tail tile (block-uniform): slots past R are absent
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (bs + 512 * (k >> 1) + 2 * t >= d.R) wa[k] = wb[k] = GX_SLOT_ABSENT;
+        }
         const uint32_t sk = qk[s];
         if (bs + PF * TILE < d.R) qk[s] = load_tile(bs + PF * TILE, qa[s], qb[s]);
         if (sk < 2) merge_tile(bs, wa, wb);  // block-uniform
@@ -2695,6 +2713,8 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
       key = key1;
     }
   }
+  unsigned long long *kp = kprof_ae(d);
+  if (kp && threadIdx.x == 0) kp[2 * blockIdx.x] = wall_clock64() | ((unsigned long long)__smid() << 48);
   uint32_t a = base + feistel_perm(key, 2 * q, m);
   uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
   // a crashed member skips the pair; with the failure detector the network path is needed and
@@ -2705,6 +2725,7 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
     if (!ok) return;
   }
   ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red);
+  if (kp && threadIdx.x == 0) kp[2 * blockIdx.x + 1] = wall_clock64();
 }
 
 // The push-pull kernel, without ChangeEvents (no listener anywhere): kept within 128 VGPRs so
