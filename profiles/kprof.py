@@ -32,8 +32,9 @@ def marks(e, lib):
     buf = (ctypes.c_uint64 * n.value)()
     assert lib.gx_kprof_read(e.h, buf, ctypes.c_uint64(n.value), ctypes.byref(n)) == 0
     a = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
-    ns = a.size - MERGE_N - e.H  # layout: k_send marks, merge counters, push-pull block marks
-    return a[:ns].reshape(-1, 8), a[ns:ns + MERGE_N], a[ns + MERGE_N:].reshape(-1, 2)
+    ns = a.size - MERGE_N - 3 * e.H  # layout: k_send marks, merge counters, push-pull block marks, scans
+    return a[:ns].reshape(-1, 8), a[ns:ns + MERGE_N], a[ns + MERGE_N:ns + MERGE_N + e.H].reshape(-1, 2), \
+        a[ns + MERGE_N + e.H:].reshape(-1, 2)
 
 
 def summarize_ae(m):
@@ -83,6 +84,7 @@ def main():
     ap.add_argument("--config", default="cfg5")
     ap.add_argument("--rounds", type=int, nargs="*", default=[21, 51])
     ap.add_argument("--ae-rounds", type=int, nargs="*", default=[])
+    ap.add_argument("--scan-rounds", type=int, nargs="*", default=[])
     a = ap.parse_args()
     import bench
     from sidecar_amd.abi import load_product
@@ -90,17 +92,20 @@ def main():
     lib.gx_kprof_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     e = bench.make_engine(lib, a.config, 0x5EED, 0)
     res = {}
-    for r in sorted(set(a.rounds) | set(a.ae_rounds)):
+    for r in sorted(set(a.rounds) | set(a.ae_rounds) | set(a.scan_rounds)):
         e.run_rounds(r - e.round)
-        _, m0, _ = marks(e, lib)
+        _, m0, _, sm0 = marks(e, lib)
         e.run_rounds(1)  # round r: its k_send's marks, its merge's path counts, its push-pull blocks
-        wm, m1, am = marks(e, lib)
+        wm, m1, am, sm = marks(e, lib)
         if r in a.rounds:
             res[r] = summarize(wm)
             res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES)}
             print(json.dumps({"config": a.config, "round": r, **res[r]}), flush=True)
         if r in a.ae_rounds:
             print(json.dumps({"config": a.config, "round": r, "push_pull": summarize_ae(am)}), flush=True)
+        if r in a.scan_rounds:
+            fresh = sm[:, 0] != sm0[:, 0]  # views this round's launch scanned (the region keeps older marks)
+            print(json.dumps({"config": a.config, "round": r, "scan": summarize_ae(sm[fresh])}), flush=True)
     e.close()
 
 

@@ -937,7 +937,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->xbound_round = -1;
   e->kprof_n = 0;
   if (getenv("GX_KPROF")) {  // diagnostics: phase marks of every k_send wave (gx_kprof_read)
-    e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8 + GX_KPROF_MERGE_N + d.H;  // + merge counts + push-pull blocks
+    e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8 + GX_KPROF_MERGE_N + 3ull * d.H;  // + merge counts + push-pull blocks + scans
     ALLOC(d.kprof, sizeof(unsigned long long) * e->kprof_n);
     HIPCHK(hipMemset(d.kprof, 0, sizeof(unsigned long long) * e->kprof_n));
   }

@@ -28,6 +28,36 @@ GXD unsigned long long block_excl_scan64(unsigned long long x, unsigned long lon
 }
 GXD uint32_t fld(unsigned long long x, int i) { return (uint32_t)((x >> (16 * i)) & 0xffffu); }
 
+// Diagnostics (Dev::kprof, env GX_KPROF): after k_send's per-wave marks, GX_KPROF_MERGE_N counters
+// of the gossip merge's routing (k_merge_seg), accumulated over launches: [0] receivers with live
+// records, [1] routed to 16-lane segments, [2] to 32-lane segments, [3] to a whole wave, [4] merged
+// by a whole wave after their segment did not fit, [5] live records registered
+#define GX_KPROF_MERGE_N 64
+GXD unsigned long long *kprof_merge(const Dev &d) {
+  return d.kprof ? d.kprof + (size_t)((d.Hl + 63) / 64) * 4 * 8 : nullptr;
+}
+// Diagnostics: after the merge counters, two marks per push-pull block of the last k_ae launch:
+// [2i] start | CU << 48, [2i + 1] end (wall clock, 100 MHz)
+GXD unsigned long long *kprof_ae(const Dev &d) { return d.kprof ? kprof_merge(d) + GX_KPROF_MERGE_N : nullptr; }
+// ... then two marks per view scanned by the last k_scan launch, by worklist position: [2w] start |
+// CU << 48, [2w + 1] end
+GXD unsigned long long *kprof_scan(const Dev &d) { return d.kprof ? kprof_ae(d) + d.H : nullptr; }
+
+// OR of p over a 256-thread block (4 waves), one barrier: the waves' votes alternate between the
+// two halves of s_any[8] (par flips per call), so a call's votes cannot be overwritten before every
+// wave has read them. HIP's __syncthreads_or reads the work-group size with a vector load each
+// call, and the wait on that load also waits for every tile load in flight (the streaming kernels
+// call it once per tile).
+GXD bool block_any256(bool p, uint32_t *s_any, uint32_t &par) {
+  const uint32_t b = __ballot(p) != 0;
+  if ((threadIdx.x & 63) == 0) s_any[par * 4 + (threadIdx.x >> 6)] = b;
+  __syncthreads();
+  const uint32_t *q = s_any + par * 4;
+  const bool r = (q[0] | q[1] | q[2] | q[3]) != 0;
+  par ^= 1u;
+  return r;
+}
+
 // Block reduction of a counter -> one atomic on this block's shard.
 GXD void block_ctr(const Dev &d, int idx, unsigned long long x, unsigned long long *s_red) {
   x = wave_sum(x);
@@ -459,10 +489,13 @@ typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 struct ScanLds {
   unsigned long long wave[4];
   unsigned long long red[4];
+  uint32_t any[8];  // block_any256
   uint32_t lu[TILE_OWNERS];
   uint32_t last;
 };
+#ifndef SCAN_PF
 #define SCAN_PF 1  // 4 tiles in flight (139 VGPRs, 3 waves/SIMD) measured slower on cfg 3: 1.59 vs 1.29 ms per round
+#endif
 template <bool VEC, bool EV>
 GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t *cnt_out, ScanLds &sm) {
   unsigned long long *s_wave = sm.wave, *s_red = sm.red;
@@ -502,6 +535,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   bool listing = true;     // block-uniform: list positions (or event positions) still needed
   uint32_t my_last = 0;    // 1 + this thread's last expired key (state.LastChanged)
   unsigned long long cnt_tail = 0;  // expirations counted per thread once the list is full
+  uint32_t any_par = 0;
   auto tile = [&](uint32_t base, const ulonglong2 *cur) {
     uint64_t w[4], nw[4];
     bool ex[4];
@@ -566,7 +600,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
       return;
     }
     // a tile without expirations (GC writes only) needs no compaction: one barrier
-    if (!__syncthreads_or(ex[0] || ex[1] || ex[2] || ex[3])) return;
+    if (!block_any256(ex[0] || ex[1] || ex[2] || ex[3], sm.any, any_par)) return;
     unsigned long long cnt = (unsigned long long)(ex[0] + ex[1]) | ((unsigned long long)(ex[2] + ex[3]) << 16);
     unsigned long long tot;
     unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
@@ -664,9 +698,12 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
     return;
   }
   const uint32_t n = *d.wl_cnt;
+  unsigned long long *kp = kprof_scan(d);
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const uint32_t oi = d.work[w];
+    if (kp && threadIdx.x == 0 && w < d.H) kp[2 * w] = wall_clock64() | ((unsigned long long)__smid() << 48);
     scan_view<VEC, EV>(d, oi, &list_base[(size_t)oi * list_stride], list_cap, &cnt_out[oi], sm);
+    if (kp && threadIdx.x == 0 && w < d.H) kp[2 * w + 1] = wall_clock64();
     __syncthreads();
   }
 }
@@ -1031,17 +1068,6 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
   return cnt;
 }
 
-// Diagnostics (Dev::kprof, env GX_KPROF): after k_send's per-wave marks, GX_KPROF_MERGE_N counters
-// of the gossip merge's routing (k_merge_seg), accumulated over launches: [0] receivers with live
-// records, [1] routed to 16-lane segments, [2] to 32-lane segments, [3] to a whole wave, [4] merged
-// by a whole wave after their segment did not fit, [5] live records registered
-#define GX_KPROF_MERGE_N 64
-GXD unsigned long long *kprof_merge(const Dev &d) {
-  return d.kprof ? d.kprof + (size_t)((d.Hl + 63) / 64) * 4 * 8 : nullptr;
-}
-// Diagnostics: after the merge counters, two marks per push-pull block of the last k_ae launch:
-// [2i] start | CU << 48, [2i + 1] end (wall clock, 100 MHz)
-GXD unsigned long long *kprof_ae(const Dev &d) { return d.kprof ? kprof_merge(d) + GX_KPROF_MERGE_N : nullptr; }
 // Diagnostics: wall-clock mark k of this wave (k_send phases; Dev::kprof, env GX_KPROF).
 #define GX_KP(k)                                                                                   \
   do {                                                                                             \
@@ -2347,6 +2373,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   uint32_t na = 0, nb = 0;
   uint32_t c_merge = 0, c_acc = 0, c_stale = 0, c_wr = 0, c_chg = 0;  // per thread: < 2^32
   uint32_t c_qa = 0, c_qb = 0;  // retransmits counted once both stored windows are full (all deferred)
+  const int64_t stale_cut = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;  // merge_word's stale gate
   unsigned long long ma = ~0ull, mb = ~0ull;
   uint32_t t = threadIdx.x;
   const uint32_t TILE = 4 * blockDim.x;
@@ -2354,6 +2381,8 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   // last status change of the pass (state.LastChanged), events for listening views; key order
   __shared__ uint32_t s_lu[TILE_OWNERS], s_lc[TILE_OWNERS];
   __shared__ uint32_t s_last[2];
+  __shared__ uint32_t s_any[8];  // block_any256
+  uint32_t any_par = 0;
   if (t < 2) s_last[t] = 0;  // read after the pass's barriers
   const int32_t evka = __builtin_amdgcn_readfirstlane(d.ev_slot[li(d, a)]);
   const int32_t evkb = __builtin_amdgcn_readfirstlane(both ? d.ev_slot[li(d, b)] : -1);
@@ -2493,6 +2522,20 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
       nwb[k] = wb[k];
       fa[k] = fb[k] = false;
     }
+    bool same = true;
+#pragma unroll
+    for (int k = 0; k < 4; k++) same &= wa[k] == wb[k];
+    if (__ballot(!same) == 0) {
+      // The wave's slots hold the same word on both sides (most of a pass outside an accepting
+      // stretch): each present record is merged both ways and is stale or not newer, so merging
+      // only counts (merge_word's rules with old == u); nothing is accepted or written
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t pres = st_of(wb[k]) != GX_ABSENT, stl = pres && ts_of(wb[k]) < stale_cut;
+        c_merge += both ? 2u * pres : pres;
+        c_stale += both ? 2u * stl : stl;
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
@@ -2551,6 +2594,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         if (nwb[2 * h + 1] != wb[2 * h + 1]) B[r0 + 1] = nwb[2 * h + 1];
       }
     }
+    }  // the wave's slots differ somewhere
     unsigned long long cnt = (unsigned long long)(fa[0] + fa[1]) | ((unsigned long long)(fa[2] + fa[3]) << 16) |
                              ((unsigned long long)(fb[0] + fb[1]) << 32) | ((unsigned long long)(fb[2] + fb[3]) << 48);
     // change flags and old statuses, packed so that they are all the bookkeeping below keeps
@@ -2584,7 +2628,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
     }
     // (a one-barrier scan with alternating buffers measured within noise at cfg 2, 4 and 5,
     // profiles/r03/ab/ae_scan_barriers.txt)
-    if (shfl_times ? !__syncthreads_or(cnt != 0) : !__syncthreads_or(fl != 0)) return;
+    if (!block_any256(shfl_times ? cnt != 0 : fl != 0, s_any, any_par)) return;
     unsigned long long tot;
     const unsigned long long pre = block_excl_scan64(cnt, s_wave, tot);
     uint32_t pa[4], pb[4];
