@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("GX_KPROF", "1")
 
 MERGE_N = 64  # GX_KPROF_MERGE_N: the merge path counters after the per-wave marks
-MERGE_NAMES = ["receivers", "seg16", "seg32", "wave", "fallback_wave", "live_records"]
+MERGE_NAMES = ["receivers", "seg16", "seg32", "wave", "fallback_wave", "live_records", "", "",
+               "wave_tile_cyc_loads", "wave_tile_cyc_sort", "wave_tile_cyc_fold", "wave_tile_cyc_rest", "wave_tiles"]
 NAMES = ["start", "ticks_done", "barrier", "sends_begin", "send_host", "chunk_planned", "chunk_stored", "sends_done"]
 
 
@@ -99,7 +100,7 @@ def main():
         wm, m1, am, sm = marks(e, lib)
         if r in a.rounds:
             res[r] = summarize(wm)
-            res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES)}
+            res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES) if k}
             print(json.dumps({"config": a.config, "round": r, **res[r]}), flush=True)
         if r in a.ae_rounds:
             print(json.dumps({"config": a.config, "round": r, "push_pull": summarize_ae(am)}), flush=True)

@@ -475,8 +475,8 @@ static int round_merge_impl(gx_engine *e) {
     const bool small = d.NG > 1;
     const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
     if (small) {
-      if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, 4> : k_merge_seg<true, false, 16, 4>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
-      else (ev ? k_merge_seg<false, true, 16, 4> : k_merge_seg<false, false, 16, 4>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, MERGE_WPE_GM> : k_merge_seg<true, false, 16, MERGE_WPE_GM>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
+      else (ev ? k_merge_seg<false, true, 16, MERGE_WPE_GM> : k_merge_seg<false, false, 16, MERGE_WPE_GM>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else if (d.R < (1u << 26)) {
       (ev ? k_merge_seg<true, true> : k_merge_seg<true, false>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
     } else {

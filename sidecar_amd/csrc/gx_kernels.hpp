@@ -1666,10 +1666,28 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
 
 #define INBOX_PREFETCH 8
 #define MERGE_WAVES 4
+#define MSET 512  // merge_receiver's written-key set (power of two)
+#define MSET_EMPTY 0xffffffffu
+GXD uint32_t mset_slot(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - 9); }
+GXD bool mset_has(const uint32_t *set, uint32_t key) {
+  for (uint32_t h = mset_slot(key), n = 0; n < MSET; n++, h = (h + 1) & (MSET - 1)) {
+    const uint32_t x = set[h];
+    if (x == key) return true;
+    if (x == MSET_EMPTY) return false;
+  }
+  return false;
+}
+GXD void mset_add(uint32_t *set, uint32_t key) {
+  for (uint32_t h = mset_slot(key), n = 0; n < MSET; n++, h = (h + 1) & (MSET - 1)) {
+    const uint32_t x = atomicCAS(&set[h], MSET_EMPTY, key);
+    if (x == MSET_EMPTY || x == key) return;
+  }
+}
 struct MergeLds {  // one wave's staging for one receiver at a time
   uint4 hdr[GX_DI_MAX];     // headers in sender order (inboxes of more than 64 packets use all of it)
   uint32_t pst[GX_DI_MAX];  // wide inboxes: keys while ranking, then each packet's first record index
   uint64_t accw[64];
+  uint32_t wset[MSET];  // keys written by earlier tiles of the receiver (merge_receiver)
   uint8_t accf[64], chg[64], prev[64];
 };
 // The full gather-then-merge of receiver vi by one wave (every lane calls it, wave-uniform vi).
@@ -1749,55 +1767,93 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     }
     wave_sync();
   }
-  // packet k's first record index, length, message entry and record slot (k wave-uniform)
-  auto p_start = [&](uint32_t k) -> uint32_t { return wide ? L.pst[k] : rdl(pstart, k); };
-  auto p_len = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].z : rdl(sh.z, k); };
-  auto p_entry = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].y : rdl(sh.y, k); };
-  auto p_slot = [&](uint32_t k) -> uint32_t { return wide ? s_hdr[k].w : rdl(sh.w, k); };
   const uint32_t vtick = d.tick[vi];
   gx_host_state *h = &d.hs[vi];
   const uint32_t tail0 = h->fifo_tail, st0 = h->fifo_stored, room = fifo_room(d, h->fifo_head, tail0, st0);
   uint32_t n_retx = 0, n_ev = 0;
-  unsigned long long c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, c_chg = 0, mexp = ~0ull;
+  uint32_t c_merge = 0, c_acc = 0, c_stale = 0, c_rd = 0, c_wr = 0, c_chg = 0;  // per lane: < 2^32
+  unsigned long long mexp = ~0ull;
   uint64_t *row = &d.view[(size_t)vi * d.R];
   const uint32_t INV = K32 ? 0x3ffffffu : 0xffffffffu;  // sorts after every real key
   const int32_t evk = d.ev_slot[vi];
   const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
   int64_t vlc_ts = 0;
   bool vlc_set = false;
-  uint32_t kc = 0;  // first packet that can overlap the tile
-  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
-    const uint32_t i = t0 + lane;
-    const bool valid = i < total;
-    while (kc < deg && p_start(kc) + p_len(kc) <= t0) kc++;
-    grec g;
+  // Records are prefetched a tile ahead (tile t + 1's while tile t is folded). Each record's slot
+  // word at the start of the merge came with it (msg_w0, read by its sender) wherever nothing can
+  // have changed the slot since (w0_fwd: not an own record, the view not scanned this round), so
+  // the receiver reads the slot itself only for the other records and for keys an earlier tile of
+  // this receiver wrote: an LDS set of the written keys (open addressing; once it holds more than
+  // MSET / 2 keys, every later record reads its slot).
+  // Record i's packet: the last with start <= i (a binary search of the sender-ordered starts in
+  // LDS), so a tile's records are one load per lane (and one of its msg_w0 word), whatever the
+  // packets' lengths: a fixed count of loads in flight, which the waits below can count past.
+  if (!wide) {
+    if (lane < deg) L.pst[lane] = pstart;
+    wave_sync();
+  }
+  auto load_recs = [&](uint32_t tb, grec &g, uint32_t &fslot, uint64_t &fw0) {
+    const uint32_t i = tb + lane;
     g.w = 0;
     g.r = INV;
     g.pad = 0;
-    uint64_t fw0 = 0;
-    uint32_t fslot = 0;
-    for (uint32_t k = kc; k < deg; k++) {  // hop 2: one predicated load per overlapping packet
-      const uint32_t st = p_start(k);
-      if (st >= t0 + 64) break;
-      const uint32_t off = i - st;
-      if (off < p_len(k)) {
-        fslot = p_slot(k);
-        const uint32_t en = p_entry(k);
-        g = packet_recs(d, vi, fslot, en)[off];
-        if (fslot == GX_NOSLOT_W0) fw0 = d.msg_w0[(size_t)en * d.p.packet_cap + off];
+    fw0 = 0;
+    fslot = 0;
+    if (i < total) {  // hop 2
+      uint32_t lo = 0, hi = deg;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.pst[mid] <= i) lo = mid;
+        else hi = mid;
       }
+      const uint4 hk = s_hdr[lo];  // {key, entry, len, slot}
+      const uint32_t off = i - L.pst[lo];
+      fslot = hk.w;
+      g = packet_recs(d, vi, hk.w, hk.y)[off];
+      if (hk.w == GX_NOSLOT_W0) fw0 = d.msg_w0[(size_t)hk.y * d.p.packet_cap + off];
     }
+  };
+  const bool track = total > 64;  // wave-uniform: later tiles consult the written-key set
+  if (track)
+    for (uint32_t q = lane; q < MSET; q += 64) L.wset[q] = MSET_EMPTY;
+  uint32_t nset = 0;  // keys in the set (wave-uniform)
+  grec gc, gn;
+  uint32_t fsc, fsn = 0;
+  uint64_t fwc, fwn = 0;
+  load_recs(0, gc, fsc, fwc);
+  gn.w = 0;
+  gn.r = INV;
+  gn.pad = 0;
+  if (64 < total) load_recs(64, gn, fsn, fwn);
+  wave_sync();
+  unsigned long long *kpm = kprof_merge(d);  // diagnostics: phase cycles of the whole-wave tiles
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, tk = 0;
+  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+    if (kpm) tk = __builtin_amdgcn_s_memtime();
+    const uint32_t i = t0 + lane;
+    const bool valid = i < total;
     uint32_t key = INV;
     uint64_t val = 0, w0 = 0;
+    bool rd = false;  // this record reads its slot (hop 3)
     if (valid) {
-      key = g.r;
-      val = g.w;
-      // hop 3 only where the sender's word can be stale: own records, a scanned view, and every
-      // tile after the first (an earlier tile may have written the slot)
-      w0 = (t0 == 0 && w0_fwd(d, fslot, vtick, key, v)) ? fw0 : row[key];
+      key = gc.r;
+      val = gc.w;
+      bool fwd = w0_fwd(d, fsc, vtick, key, v);
+      if (fwd && t0 > 0) fwd = nset <= MSET / 2 && !mset_has(L.wset, key);
+      rd = !fwd;
+      w0 = fwd ? fwc : row[key];
     }
+    // the tile after next's records, issued after this tile's slot reads so that waiting for
+    // those leaves them in flight
+    grec gnn;
+    uint32_t fsnn = 0;
+    uint64_t fwnn = 0;
+    gnn.w = 0;
+    gnn.r = INV;
+    gnn.pad = 0;
+    if (t0 + 128 < total) load_recs(t0 + 128, gnn, fsnn, fwnn);
     c_merge += valid;
-    c_rd += valid;  // one view slot read per inbound record
+    c_rd += rd;  // view slots read by the receiver
     // A record that is stale, or no newer than the slot's word at the start of the tile, is a
     // no-op whatever its position in the fold: the slot's timestamp only grows (an accept needs a
     // strictly newer one, services_state.go:321), and IsStale does not depend on the slot. Only the
@@ -1806,10 +1862,22 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     const bool stale0 = valid && ts_of(val) < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
     const bool live = valid && !stale0 && (st_of(w0) == GX_ABSENT || ts_of(val) > ts_of(w0));
     c_stale += stale0;
-    if (__ballot(live) == 0) continue;
+    const bool any_live = __ballot(live) != 0;
+    if (kpm) {  // [8] records and slots in (waits), [9] sort, [10] fold + writes, [11] the rest, [12] tiles
+      const unsigned long long x = __builtin_amdgcn_s_memtime();
+      ph[0] += x - tk;
+      tk = x;
+      ph[4]++;
+    }
+    if (any_live) {  // wave-uniform
     if (!live) key = INV;
     uint64_t sk = K32 ? (uint64_t)((key << 6) | lane) : (((uint64_t)key << 6) | lane);
     sk = bitonic64<K32>(sk, lane);
+    if (kpm) {
+      const unsigned long long x = __builtin_amdgcn_s_memtime() + (sk & 0);
+      ph[1] += x - tk;
+      tk = x;
+    }
     const uint32_t src = (uint32_t)(sk & 63), skey = (uint32_t)(sk >> 6);
     const bool vs = skey != INV;
     const uint64_t sval = __shfl(val, (int)src, 64), sw0 = __shfl(w0, (int)src, 64);
@@ -1841,13 +1909,21 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     }
     c_stale += stl;
     c_acc += acc;
-    if (head) {
-      if (wg != sw0) {
-        row[skey] = wg;
-        c_wr++;
-        unsigned long long x = exp_time(d.p, wg);
-        mexp = x < mexp ? x : mexp;
-      }
+    const bool wrote = head && wg != sw0;
+    if (wrote) {
+      row[skey] = wg;
+      c_wr++;
+      unsigned long long x = exp_time(d.p, wg);
+      mexp = x < mexp ? x : mexp;
+    }
+    if (track && nset <= MSET / 2) {  // later tiles read these keys' slots (at most MSET / 2 + 64 held)
+      if (wrote) mset_add(L.wset, skey);
+      nset += (uint32_t)__popcll(__ballot(wrote));
+    }
+    if (kpm) {
+      const unsigned long long x = __builtin_amdgcn_s_memtime() + (wg & 0);
+      ph[2] += x - tk;
+      tk = x;
     }
     // ServiceChanged: an insert, or a stored status that differs (:317-340)
     const bool chg = acc && (st_of(wprev) == GX_ABSENT || st_of(wprev) != st_of(wme));
@@ -1905,13 +1981,20 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
       d.fifo[(size_t)vi * d.Q + ((tail0 + n_retx + pos) % d.Q)] = make_job(s_accw[lane], key, meta_of(GX_JOB_RETX, 0, 1));
     n_retx += (uint32_t)__popcll(m);
     wave_sync();
+    }  // live records in the tile
+    if (kpm) ph[3] += __builtin_amdgcn_s_memtime() - tk;
+    gc = gn;
+    fsc = fsn;
+    fwc = fwn;
+    gn = gnn;
+    fsn = fsnn;
+    fwn = fwnn;
   }
-  c_merge = wave_sum(c_merge);
-  c_acc = wave_sum(c_acc);
-  c_stale = wave_sum(c_stale);
-  c_rd = wave_sum(c_rd);
-  c_wr = wave_sum(c_wr);
-  c_chg = wave_sum(c_chg);
+  if (kpm && lane == 0)
+    for (int q = 0; q < 5; q++) atomicAdd(&kpm[8 + q], ph[q]);
+  const unsigned long long m_merge = wave_sum(c_merge), m_acc = wave_sum(c_acc), m_rd = wave_sum(c_rd),
+                           m_wr = wave_sum(c_wr), m_chg = wave_sum(c_chg);
+  (void)c_stale;  // stale drops: counted by the senders
   mexp = wave_min(mexp);
   if (lane == 0) {
     const uint32_t ok = n_retx < room ? n_retx : room;  // stored; the rest deferred (gx.h gx_job)
@@ -1921,14 +2004,14 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     }
     if (vlc_set) d.vlc[vi] = vlc_ts;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
-    ctr_atomic(d, C_CHG, c_chg);
+    ctr_atomic(d, C_CHG, m_chg);
     // 12 B per record (word + key) + 8 B per slot read / written + 16 B per stored retransmit job
     // + 16 B per inbox header + the count (merges and stale drops: counted by the senders)
-    kbytes(d, GX_K_MERGE, 12ull * c_merge + 8ull * (c_rd + c_wr) + 16ull * ok + 16ull * deg + 4, c_merge);
-    ctr_atomic(d, C_GOSSIP_ACC, c_acc);
+    kbytes(d, GX_K_MERGE, 12ull * m_merge + 8ull * (m_rd + m_wr) + 16ull * ok + 16ull * deg + 4, m_merge);
+    ctr_atomic(d, C_GOSSIP_ACC, m_acc);
     ctr_atomic(d, C_RETX, n_retx);
     ctr_atomic(d, C_QDEFER, n_retx - ok);
-    if (c_wr) {
+    if (m_wr) {
       mark_change(d);
       atomicMin(&d.minexp[vi], mexp);
     }
@@ -2153,6 +2236,9 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
 // side by side, not one after another by one wave. A receiver whose inbox does not fit its segment
 // after all (more packets than lanes, or a count that overstates nothing) is merged by a whole wave
 // at the end.
+#ifndef MERGE_WPE_GM
+#define MERGE_WPE_GM 4  // waves per SIMD of the merge at GossipMessages > 1 (wide inboxes)
+#endif
 #define MERGE_NR 64  // receivers per block (16 measured 3% slower in the accepting stretch, profiles/r03/ab)
 #define MERGE_NONE 0xffffffffu
 template <bool K32, bool EV, int NR = MERGE_NR, int WPE = 3>
