@@ -2343,17 +2343,17 @@ GXD void side_times_shfl(const Dev &d, uint32_t x, uint32_t base, uint32_t f, co
     if (!bu_all) continue;  // changes only come with accepts
     // An owner's slots sit in its lane group in key order, so its last accepted (changed) slot is
     // in the group's highest lane with that flag: two ballots and one shuffle per field.
+    // The group's highest flagged lane holds the word, so it stores the field itself (no shuffle).
     const uint32_t g0 = lane & ~(lpo - 1);
     const uint64_t gmask = (lpo == 32 ? 0xffffffffull : ((1ull << lpo) - 1ull)) << g0;
     const uint64_t bu = bu_all & gmask, bc = __ballot(fc0 | fc1) & gmask;
-    const int64_t tu = ts_of(fa1 ? nw[2 * h + 1] : nw[2 * h]), tc = ts_of(fc1 ? nw[2 * h + 1] : nw[2 * h]);
-    const int lu = bu ? 63 - __clzll((long long)bu) : (int)lane, lc = bc ? 63 - __clzll((long long)bc) : (int)lane;
-    const int64_t gu = __shfl(tu, lu, 64), gc = __shfl(tc, lc, 64);
-    if (lane == g0 && (bu | bc)) {
+    const bool wu = bu && lane == 63u - (uint32_t)__clzll((long long)bu);
+    const bool wc = bc && lane == 63u - (uint32_t)__clzll((long long)bc);
+    if (wu || wc) {
       gx_server_times *st = srv_times(d, x, owner_of(d, r0));
-      if (bu) st->last_updated_ns = gu;
-      if (bc) st->last_changed_ns = gc;
-      words_written += (bu != 0) + (bc != 0);
+      if (wu) st->last_updated_ns = ts_of(fa1 ? nw[2 * h + 1] : nw[2 * h]);
+      if (wc) st->last_changed_ns = ts_of(fc1 ? nw[2 * h + 1] : nw[2 * h]);
+      words_written += (uint32_t)wu + (uint32_t)wc;
     }
     const uint32_t kc = fc1 ? r0 + 2 : (fc0 ? r0 + 1 : 0u);  // state.LastChanged: max over all lanes later
     lk = kc > lk ? kc : lk;
