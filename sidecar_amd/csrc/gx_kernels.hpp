@@ -2630,10 +2630,11 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         c_merge++;
         nwa[k] = merge_word(d, wa[k], wb[k], ac, st);
         c_stale += st;
-        if (ac) {
-          c_acc++;
+        if (ac) {  // an accepted word is a changed word (insert, or strictly newer)
           fa[k] = !owned_by(d, r, a);
           accb |= 1u << k;
+          const unsigned long long x = exp_time(d.p, nwa[k]);
+          ma = x < ma ? x : ma;
         }
       }
       if (both && st_of(wa[k]) != GX_ABSENT) {  // b.Merge(a's snapshot)
@@ -2642,28 +2643,20 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
         nwb[k] = merge_word(d, wb[k], wa[k], ac, st);
         c_stale += st;
         if (ac) {
-          c_acc++;
           fb[k] = !owned_by(d, r, b);
           accb |= 1u << (8 + k);
+          const unsigned long long x = exp_time(d.p, nwb[k]);
+          mb = x < mb ? x : mb;
         }
       }
-
-      if (nwa[k] != wa[k]) {
-        c_wr++;
-        unsigned long long x = exp_time(d.p, nwa[k]);
-        ma = x < ma ? x : ma;
-      }
-      if (nwb[k] != wb[k]) {
-        c_wr++;
-        unsigned long long x = exp_time(d.p, nwb[k]);
-        mb = x < mb ? x : mb;
-      }
     }
+    const uint32_t nacc = (uint32_t)__popc(accb);
+    c_acc += nacc;
+    c_wr += nacc;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       uint32_t r0 = VEC ? base + 512 * h + 2 * t : base + 2 * blockDim.x * h + 2 * t;
-      bool cha = nwa[2 * h] != wa[2 * h] || nwa[2 * h + 1] != wa[2 * h + 1];
-      bool chb = nwb[2 * h] != wb[2 * h] || nwb[2 * h + 1] != wb[2 * h + 1];
+      const bool cha = (accb >> (2 * h)) & 3u, chb = (accb >> (8 + 2 * h)) & 3u;
       if (VEC) {
         if (NTS) {  // nontemporal stores (A/B)
           typedef unsigned long long v2u64s __attribute__((ext_vector_type(2)));
@@ -2674,10 +2667,10 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
           if (chb) *reinterpret_cast<ulonglong2 *>(&B[r0]) = make_ulonglong2(nwb[2 * h], nwb[2 * h + 1]);
         }
       } else {
-        if (nwa[2 * h] != wa[2 * h]) A[r0] = nwa[2 * h];
-        if (nwa[2 * h + 1] != wa[2 * h + 1]) A[r0 + 1] = nwa[2 * h + 1];
-        if (nwb[2 * h] != wb[2 * h]) B[r0] = nwb[2 * h];
-        if (nwb[2 * h + 1] != wb[2 * h + 1]) B[r0 + 1] = nwb[2 * h + 1];
+        if ((accb >> (2 * h)) & 1u) A[r0] = nwa[2 * h];
+        if ((accb >> (2 * h + 1)) & 1u) A[r0 + 1] = nwa[2 * h + 1];
+        if ((accb >> (8 + 2 * h)) & 1u) B[r0] = nwb[2 * h];
+        if ((accb >> (8 + 2 * h + 1)) & 1u) B[r0 + 1] = nwb[2 * h + 1];
       }
     }
     }  // the wave's slots differ somewhere
