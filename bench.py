@@ -33,6 +33,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # 20480 / 3 = 6826 (cfg 5 also stores the storm's 16384 ExpireServer jobs per host), 139264 / 45 =
 # 3094 rounds at GossipMessages 15 (71 GB at H = 32768), all past --converge-max 3000.
 Q_GM1 = 16384
+# uniformly random 8-B gathers over a 137 GB table on MI355X (profiles/r04/gather_bench.hip; a
+# read-modify-write of the slot runs at the same rate, a blind scatter at 2.8e10/s)
+GATHER_CEILING_PER_S = 4.72e10
 CONFIGS = {
     # BASELINE.json configs[4]: 32768 x 16, 2-way partition for 50 rounds, departure storm, heal
     "cfg5": dict(desc="32768 hosts x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds "
@@ -258,12 +261,22 @@ def gossip_round_span(lib, cfg, seed, local_rank, start=None):
     m, acc, rx = (s1[k] - s0[k] for k in ("gossip_merges", "gossip_accepts", "retransmits"))
     byts = (22 * m + 9 * acc + 13 * rx) / n
     gbs = byts / (us * 1e3)
+    # Against the part's random-access ceiling: every gossip record-merge reads its receiver's
+    # 8-B view slot (the senders' filter, or the receiver), an accept writes it back (a
+    # read-modify-write runs at the gather rate): m slot accesses per stretch at the measured rate
+    # of uniformly random 8-B gathers over a 137 GB table
+    us_ceil = 1e6 * (m / n) / GATHER_CEILING_PER_S
     return round(us, 2), {"bound": "hbm", "scope": "whole gossip round (send + merge kernels), SURVEY 8(d) bytes",
                           "rounds": [start, start + n - 1],
                           "bytes_per_round": int(byts), "merges_per_round": m // n,
                           "accepts_per_round": acc // n, "accept_fraction": round(acc / m, 4) if m else None,
                           "achieved": round(gbs, 1),
-                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                          "gather_ceiling": {"slot_accesses_per_round": m // n,
+                                             "ceiling_per_s": GATHER_CEILING_PER_S,
+                                             "source": "profiles/r04/gather_bench.jsonl (gather, ILP 4-16)",
+                                             "us_per_round_at_ceiling": round(us_ceil, 2),
+                                             "frac": round(us_ceil / us, 4) if us else None}}
 
 
 def dissemination(lib, cfg, seed, local_rank, start=100, rounds=300):
