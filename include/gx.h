@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 6
+#define GX_ABI_VERSION 7
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -233,6 +233,32 @@ typedef struct gx_params {
    * gossip_messages > 1). A receiver with more packets in a round takes the serial overflow path;
    * results are identical. */
   uint32_t inbox_slots;
+  /* The ServicesState lock held by a blocked looper. BroadcastServices holds
+   * state.RLock() while it blocks on its `Broadcasts <- nil` (services_state.go:535-536,569) and
+   * BroadcastTombstones holds state.Lock() while it blocks on its own (:610-611,628), so while
+   * either looper waits for its nil to reach the FIFO head, AddServiceEntry's Lock() (:296),
+   * ExpireServer's Lock() (:151) and, behind a pending writer, LocalState's RLock()
+   * (services_delegate.go:148) all wait too. lock_model = 1 (default) models it:
+   *   - a host is locked for round n iff one of its loopers was blocked on its nil at the start of
+   *     round n (gx_host_state.lock holds that snapshot per round parity);
+   *   - a looper whose tick finds the other looper holding the lock waits for it: BroadcastServices
+   *     does not tick while BroadcastTombstones is blocked, and vice versa;
+   *   - gossip records sent to a locked host queue in its inbound pipeline in arrival order:
+   *     memberlist's handoff queue (HandoffQueueDepth 1024, config/config.go:48), the packet
+   *     handler blocked in NotifyMsg (1), the delegate's notifications channel (25,
+   *     services_delegate.go:38), its goroutine blocked in UpdateService (1), ServiceMsgs (25,
+   *     services_state.go:97) and ProcessServiceMsgs blocked in AddServiceEntry (1): lock_buffer
+   *     records (default 1077). memberlist drops what arrives at a full handoff queue
+   *     (gx_stats.lock_drops); the buffered records run through AddServiceEntry, in arrival order,
+   *     at the receive phase of the first round the host is unlocked, before that round's packets;
+   *   - a push-pull exchange with a locked side does not run (gx_stats.ae_locked): the locked
+   *     side's LocalState blocks behind the pending writer past memberlist's TCP deadline;
+   *   - ExpireServer calls (the storm's NotifyLeave, the failure detector's deaths) on a locked host
+   *     wait: they run in owner order at the end of the owner phase of its first unlocked round.
+   * lock_model = 0 lets merges proceed on locked hosts (rounds 1-4) and counts them
+   * (gx_stats.locked_merges). lock_buffer is 1..65535. */
+  uint32_t lock_model;
+  uint32_t lock_buffer;
 } gx_params;
 #define GX_PP_MATCHING 0
 #define GX_PP_INITIATE 1
@@ -252,8 +278,17 @@ typedef struct gx_host_state {
   uint32_t fifo_stored;            /* end of the stored window: jobs [fifo_head, fifo_stored) are kept,
                                       [fifo_stored, fifo_tail) deferred (gx_job) */
   uint32_t nil_pos_bs, nil_pos_bt; /* queue position of each looper's last nil send */
-  uint32_t pad;
+  uint32_t lock;                   /* the ServicesState lock (gx_params.lock_model): bit (n & 1) = a
+                                      looper held it at the start of round n (written for round n + 1
+                                      when the host's round-n GetBroadcasts calls end, and by calls
+                                      that block or unblock a looper between rounds); bit 2 =
+                                      ExpireServer calls wait for it; bits 8..31 = records in the
+                                      host's lock buffer */
 } gx_host_state;
+#define GX_LOCK_PENDING_EXPIRE 4u
+#define GX_LOCK_BUF_SHIFT 8
+#define GX_LOCK_AT(lock, round) (((lock) >> ((round) & 1)) & 1u)
+#define GX_LOCK_BUF(lock) ((lock) >> GX_LOCK_BUF_SHIFT)
 
 typedef struct gx_stats {
   int64_t round;             /* current round */
@@ -302,6 +337,16 @@ typedef struct gx_stats {
   uint64_t fd_state_merges;  /* remote node states merged by push-pull (mergeState) */
   uint64_t queue_deferred;   /* jobs queued past the stored window (kept as a count, gx_job) */
   int64_t first_drop_round;  /* round of the first queue_drops dequeue, -1 = none */
+  /* The ServicesState lock (gx_params.lock_model) */
+  uint64_t locked_merges;    /* lock_model = 0: gossip and push-pull AddServiceEntry calls applied on a
+                                host whose looper held the lock (the reference would have waited) */
+  int64_t first_locked_round;/* first round a locked host received gossip records or was in a push-pull
+                                pair, -1 = none (both modes) */
+  uint64_t lock_buffered;    /* records queued in a locked host's inbound pipeline */
+  uint64_t lock_drops;       /* records that found the pipeline full (memberlist's handoff queue) */
+  uint64_t lock_drained;     /* buffered records merged once the host was unlocked (also gossip_merges) */
+  uint64_t ae_locked;        /* push-pull exchanges that did not run: a side held the lock */
+  uint64_t expire_deferred;  /* ExpireServer calls that waited for the lock */
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */

@@ -87,6 +87,12 @@ struct gx_engine {
   uint32_t *fd_np;        /* H */
   uint32_t *name_rank;    /* R  ByService: rank of each record's Service.Name, NULL until set */
   int64_t *in_stamp;      /* H * KE  round a received slot last carried the sender key (sharded), lazy */
+  /* the ServicesState lock (gx.h lock_model) */
+  uint32_t C;             /* lock_buffer: records a locked host's inbound pipeline holds */
+  grec *lkb;              /* H * C  the records queued there, arrival order (count: hs.lock >> 8) */
+  uint32_t PW;            /* words per host of pexp, ceil(H / 32) */
+  uint32_t *pexp;         /* H * PW  owners whose ExpireServer waits for the host's lock (lazy) */
+  int in_round;           /* inside a round phase: the lock applies (ABI entry points act directly) */
   gx_stats st;
 };
 static void free_names(gx_engine *e);
@@ -129,6 +135,21 @@ static inline void set_slot(gx_engine *e, uint64_t *slot, uint64_t nw) {
   }
 }
 
+/* ------------------------------------------------- the ServicesState lock -- */
+/* BroadcastServices blocks on its nil holding state.RLock() (services_state.go:535-536,569),
+ * BroadcastTombstones holding state.Lock() (:610-611,628). Host v is locked for round n iff one of
+ * them was blocked at the start of round n: bit (n & 1) of hs.lock, written for round n + 1 when
+ * v's round-n GetBroadcasts calls end (lock_snapshot), so every phase of a round sees one value. */
+static inline int locked_at(const gx_engine *e, uint32_t v) { return (int)GX_LOCK_AT(e->hs[v].lock, e->round); }
+static inline int lock_on(const gx_engine *e) { return e->p.lock_model != 0 && e->in_round; }
+static void lock_snapshot(gx_engine *e, uint32_t v, int64_t round) {
+  const uint32_t b = 1u << (round & 1);
+  e->hs[v].lock = (e->hs[v].lock & ~b) | ((e->hs[v].flags & 3u) ? b : 0u);
+}
+static void note_locked(gx_engine *e) {
+  if (e->st.first_locked_round < 0 || e->round < e->st.first_locked_round) e->st.first_locked_round = e->round;
+}
+
 /* ------------------------------------------------------------- per-host parallel loops ---- */
 /* Every phase of a round touches only the state of the host it runs for (its view row, FIFO,
  * sleep ring, pending deque, lists, server times), so a phase is a loop over hosts whose
@@ -152,11 +173,14 @@ static void stats_merge(gx_stats *dst, const gx_stats *src) {
   const size_t i_round = offsetof(gx_stats, round) / sizeof(uint64_t);
   const size_t i_lcr = offsetof(gx_stats, last_change_round) / sizeof(uint64_t);
   const size_t i_fdr = offsetof(gx_stats, first_drop_round) / sizeof(uint64_t);
+  const size_t i_flr = offsetof(gx_stats, first_locked_round) / sizeof(uint64_t);
   for (size_t i = 0; i < n; i++)
-    if (i != i_round && i != i_lcr && i != i_fdr) d[i] += s[i];
+    if (i != i_round && i != i_lcr && i != i_fdr && i != i_flr) d[i] += s[i];
   if (src->last_change_round > dst->last_change_round) dst->last_change_round = src->last_change_round;
   if (src->first_drop_round >= 0 && (dst->first_drop_round < 0 || src->first_drop_round < dst->first_drop_round))
     dst->first_drop_round = src->first_drop_round;
+  if (src->first_locked_round >= 0 && (dst->first_locked_round < 0 || src->first_locked_round < dst->first_locked_round))
+    dst->first_locked_round = src->first_locked_round;
 }
 #endif
 /* Threads the phase loops use (oracle-only symbol, not part of gx.h): bench.py reports it as
@@ -177,6 +201,7 @@ static void for_hosts(gx_engine *e, uint32_t n, host_fn fn, void *ctx) {
       memset(&loc.st, 0, sizeof loc.st);
       loc.st.last_change_round = e->st.last_change_round;
       loc.st.first_drop_round = -1;
+      loc.st.first_locked_round = -1;
 #pragma omp for schedule(dynamic, 4)
       for (uint32_t i = 0; i < n; i++) fn(&loc, i, ctx);
 #pragma omp critical
@@ -586,6 +611,29 @@ static int expire_server(gx_engine *e, uint32_t v, uint32_t o, int64_t now) {
   return 1;
 }
 
+/* NotifyLeave -> go ExpireServer(node) (services_delegate.go:173-176) inside a round: ExpireServer
+ * takes state.Lock() (services_state.go:151), so on a locked host the call waits. The waiting
+ * calls run in owner order at the end of the owner phase of the host's first unlocked round
+ * (run_pending_expires). */
+static void defer_expire(gx_engine *e, uint32_t v, uint32_t o) {
+  uint32_t *w = &e->pexp[(size_t)v * e->PW + o / 32];
+  const uint32_t b = 1u << (o % 32);
+  e->st.expire_deferred++;
+  *w |= b;
+  e->hs[v].lock |= GX_LOCK_PENDING_EXPIRE;
+}
+static void notify_leave(gx_engine *e, uint32_t v, uint32_t o, int64_t now) {
+  if (lock_on(e) && locked_at(e, v)) defer_expire(e, v, o);
+  else expire_server(e, v, o, now);
+}
+static void run_pending_expires(gx_engine *e, uint32_t v, int64_t now) {
+  uint32_t *w = &e->pexp[(size_t)v * e->PW];
+  for (uint32_t k = 0; k < e->PW; k++)
+    for (uint32_t x = w[k]; x; x &= x - 1) expire_server(e, v, k * 32 + (uint32_t)__builtin_ctz(x), now);
+  memset(w, 0, 4ull * e->PW);
+  e->hs[v].lock &= ~GX_LOCK_PENDING_EXPIRE;
+}
+
 /* IsNewService, services_state.go:509-521. */
 static int is_new(const gx_engine *e, uint32_t o, grec s) {
   uint64_t w = e->view[(size_t)o * e->R + s.r];
@@ -729,6 +777,17 @@ static void fd_snapshot_row(const gx_engine *e, uint32_t v, uint64_t *out);
 static void fd_merge_state(gx_engine *e, uint32_t v, const uint64_t *remote);
 
 static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
+  /* the ServicesState lock (gx.h lock_model): a locked side's LocalState blocks behind the pending
+   * writer (services_delegate.go:148), so the exchange does not run; lock_model = 0 counts the
+   * merges it applies on a locked side */
+  const int la = locked_at(e, a), lb = locked_at(e, b);
+  if (la || lb) {
+    note_locked(e);
+    if (e->p.lock_model) {
+      e->st.ae_locked++;
+      return;
+    }
+  }
   uint64_t *sa = (uint64_t *)malloc(sizeof(uint64_t) * e->R);
   memcpy(sa, &e->view[(size_t)a * e->R], sizeof(uint64_t) * e->R);
   const uint64_t *vb = &e->view[(size_t)b * e->R];
@@ -736,11 +795,13 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
     if (st_of(vb[r]) == GX_ABSENT) continue;
     grec u = {vb[r], r, 0};
     add_entry(e, a, u, now, SRC_AE);
+    e->st.locked_merges += (uint64_t)la;
   }
   for (uint32_t r = 0; r < e->R; r++) { /* b.Merge(a's state snapshot) */
     if (st_of(sa[r]) == GX_ABSENT) continue;
     grec u = {sa[r], r, 0};
     add_entry(e, b, u, now, SRC_AE);
+    e->st.locked_merges += (uint64_t)lb;
   }
   e->st.ae_exchanges++;
   e->st.ae_slots += 2ull * e->R;
@@ -780,8 +841,12 @@ static void ph_owner(gx_engine *e, uint32_t i, void *ctx) {
   if (departed(e, o)) return; /* a crashed host runs no loopers */
   churn(e, o);
   gx_host_state *h = &e->hs[o];
-  if (!(h->flags & 1u) && h->bs_next <= e->round) bs_tick(e, o, now);
-  if (!(h->flags & 2u) && h->bt_next <= e->round) bt_tick(e, o, now);
+  /* with the lock modelled, a looper whose tick finds the other one blocked on its nil (holding
+   * the lock) waits for it: it ticks at the first owner phase after that nil was taken */
+  const int lm = e->p.lock_model != 0;
+  if (!(h->flags & 1u) && !(lm && (h->flags & 2u)) && h->bs_next <= e->round) bs_tick(e, o, now);
+  if (!(h->flags & 2u) && !(lm && (h->flags & 1u)) && h->bt_next <= e->round) bt_tick(e, o, now);
+  if ((h->lock & GX_LOCK_PENDING_EXPIRE) && !locked_at(e, o)) run_pending_expires(e, o, now);
 }
 /* SWIM departure storm: NotifyLeave -> ExpireServer for every host of the other half */
 static void ph_storm(gx_engine *e, uint32_t i, void *ctx) {
@@ -789,7 +854,7 @@ static void ph_storm(gx_engine *e, uint32_t i, void *ctx) {
   uint32_t v = e->lo + i, half = e->H / 2;
   if (departed(e, v)) return;
   uint32_t lo = v < half ? half : 0, hi = v < half ? e->H : half;
-  for (uint32_t o = lo; o < hi; o++) expire_server(e, v, o, now);
+  for (uint32_t o = lo; o < hi; o++) notify_leave(e, v, o, now);
 }
 /* gossip send: GetBroadcasts once per selected peer */
 /* With the failure detector, the targets are memberlist's (ph_fd_send took their memberlist
@@ -835,10 +900,12 @@ static void ph_send(gx_engine *e, uint32_t i, void *ctx) {
     }
     if (stop) break;
   }
+  lock_snapshot(e, u, e->round + 1); /* the lock for the next round: the loopers after these calls */
 }
 static void round_send(gx_engine *e) {
   int64_t now = now_of(e);
   uint32_t n = e->hi - e->lo;
+  e->in_round = 1;
   for_hosts(e, n, ph_wake, NULL);
   for_hosts(e, n, ph_owner, &now);
   if (e->p.storm_round >= 0 && e->round == e->p.storm_round) for_hosts(e, n, ph_storm, &now);
@@ -849,6 +916,7 @@ static void round_send(gx_engine *e) {
     for_hosts(e, n, ph_fd_send, NULL);
   }
   for_hosts(e, n, ph_send, NULL);
+  e->in_round = 0;
 }
 
 static int pkt_live(const gx_engine *e, size_t m) {
@@ -857,9 +925,44 @@ static int pkt_live(const gx_engine *e, size_t m) {
 
 /* Phase 4: packets to this engine's receivers in sender order -> NotifyMsg -> AddServiceEntry.
  * Packets from other shards were unpacked into the same H*K message table. */
+/* A locked receiver (gx.h lock_model): NotifyMsg -> notifications -> UpdateService -> ServiceMsgs
+ * -> ProcessServiceMsgs blocked in AddServiceEntry's Lock() (services_delegate.go:72-83,46-56,
+ * services_state.go:121-132,296): the records queue in arrival order behind memberlist's handoff
+ * queue, lock_buffer in all, and what arrives at a full pipeline is dropped (memberlist's handoff
+ * queue drops on overflow). The first unlocked round merges them before its own packets. */
 static void ph_receive(gx_engine *e, uint32_t i, void *ctx) {
   int64_t now = *(const int64_t *)ctx;
   uint32_t v = e->lo + i, cap = e->p.packet_cap;
+  gx_host_state *h = &e->hs[v];
+  const int locked = locked_at(e, v);
+  if (locked && e->in_cnt[v] != e->in_cnt[v + 1]) {
+    uint32_t nrec = 0;
+    for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) nrec += e->msg_len[e->in_list[x]];
+    if (nrec) note_locked(e);
+    if (e->p.lock_model) {
+      uint32_t nb = GX_LOCK_BUF(h->lock);
+      for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) {
+        uint32_t m = e->in_list[x];
+        for (uint32_t y = 0; y < e->msg_len[m]; y++) {
+          if (nb < e->C) {
+            e->lkb[(size_t)v * e->C + nb++] = e->msg[(size_t)m * cap + y];
+            e->st.lock_buffered++;
+          } else {
+            e->st.lock_drops++;
+          }
+        }
+      }
+      h->lock = (h->lock & ((1u << GX_LOCK_BUF_SHIFT) - 1)) | nb << GX_LOCK_BUF_SHIFT;
+      return;
+    }
+    e->st.locked_merges += nrec; /* lock_model = 0: they merge anyway (counted) */
+  }
+  if (!locked && GX_LOCK_BUF(h->lock) && !departed(e, v)) { /* the pipeline drains, in arrival order */
+    const uint32_t nb = GX_LOCK_BUF(h->lock);
+    h->lock &= (1u << GX_LOCK_BUF_SHIFT) - 1;
+    for (uint32_t k = 0; k < nb; k++) add_entry(e, v, e->lkb[(size_t)v * e->C + k], now, SRC_GOSSIP);
+    e->st.lock_drained += nb;
+  }
   for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) {
     uint32_t m = e->in_list[x];
     for (uint32_t y = 0; y < e->msg_len[m]; y++) add_entry(e, v, e->msg[(size_t)m * cap + y], now, SRC_GOSSIP);
@@ -877,8 +980,10 @@ static void round_merge(gx_engine *e) {
   for (size_t m = 0; m < (size_t)H * K; m++)
     if (pkt_live(e, m) && is_local(e, e->msg_dst[m])) e->in_list[cur[e->msg_dst[m]]++] = (uint32_t)m;
   free(cur);
+  e->in_round = 1;
   for_hosts(e, e->hi - e->lo, ph_receive, &now);
   if (e->p.fd_enable) for_hosts(e, e->hi - e->lo, ph_fd_receive, &now);
+  e->in_round = 0;
 }
 
 static int ae_round(const gx_engine *e) {
@@ -930,10 +1035,12 @@ static void ae_pair_at(const gx_engine *e, uint32_t t, uint32_t *a, uint32_t *b)
 
 /* x <- a remote host's row (one direction of a cross-shard push-pull pair). */
 static void ae_merge_row(gx_engine *e, uint32_t x, const uint64_t *row, int count_exchange, int64_t now) {
+  const int lx = locked_at(e, x); /* lock_model = 0 (a locked pair runs only then): counted */
   for (uint32_t r = 0; r < e->R; r++) {
     if (st_of(row[r]) == GX_ABSENT) continue;
     grec u = {row[r], r, 0};
     add_entry(e, x, u, now, SRC_AE);
+    e->st.locked_merges += (uint64_t)lx;
   }
   e->st.ae_slots += e->R;
   if (count_exchange) e->st.ae_exchanges++;
@@ -1205,6 +1312,8 @@ void gx_params_default(gx_params *p) {
   p->depart_round = -1;
   p->depart_ppm = 0;
   p->fd_push_pull_state = 1;
+  p->lock_model = 1;
+  p->lock_buffer = 1024 + 1 + 25 + 1 + 25 + 1; /* gx.h lock_model: handoff queue .. AddServiceEntry */
   gx_fd_defaults(p);
 }
 
@@ -1236,6 +1345,7 @@ static int check_params(const gx_params *p) {
   if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
     return GX_EINVAL;
   if (p->inbox_slots > 256) return GX_EINVAL; /* engine bound (GX_DI_MAX) */
+  if (p->lock_model > 1 || p->lock_buffer < 1 || p->lock_buffer > 65535) return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1290,7 +1400,10 @@ static void init_state(gx_engine *e) {
   memset(&e->st, 0, sizeof(e->st));
   e->st.last_change_round = -1;
   e->st.first_drop_round = -1;
+  e->st.first_locked_round = -1;
   e->round = 0;
+  if (e->lkb) memset(e->lkb, 0, sizeof(grec) * (size_t)H * e->C);
+  if (e->pexp) memset(e->pexp, 0, 4ull * H * e->PW);
   fd_init(e);
 }
 
@@ -1372,6 +1485,16 @@ int gx_create(const gx_params *p, gx_engine **out) {
       return GX_ENOMEM;
     }
   }
+  if (p->lock_model) { /* the locked hosts' inbound pipelines and waiting ExpireServer calls */
+    e->C = p->lock_buffer;
+    e->lkb = (grec *)malloc(sizeof(grec) * H * e->C);
+    e->PW = (e->H + 31) / 32;
+    if (p->storm_round >= 0 || p->fd_enable) e->pexp = (uint32_t *)malloc(4ull * H * e->PW);
+    if (!e->lkb || ((p->storm_round >= 0 || p->fd_enable) && !e->pexp)) {
+      gx_destroy(e);
+      return GX_ENOMEM;
+    }
+  }
   if (e->sbytes)
     for (uint32_t r = 0; r < e->R; r++) e->sbytes[r] = GX_STATIC_BYTES_DEFAULT;
   if (!e->sbytes || !e->srvt || !e->vlc || !e->view || !e->own_status || !e->hs || !e->fifo || !e->sleep || !e->dq || !e->arena ||
@@ -1424,6 +1547,8 @@ int gx_destroy(gx_engine *e) {
   free(e->fd_len);
   free(e->fd_peers);
   free(e->fd_np);
+  free(e->lkb);
+  free(e->pexp);
   free_names(e);
   free(e);
   return GX_OK;
@@ -1433,8 +1558,10 @@ int gx_set_round(gx_engine *e, int64_t round) {
   if (!e || round < e->round || round >= GX_MAX_ROUND) return GX_EINVAL;
   e->round = round;
   e->st.round = round;
-  for (uint32_t v = 0; v < e->H; v++)
+  for (uint32_t v = 0; v < e->H; v++) {
     if (!departed(e, v)) wake_host(e, v); /* a crashed host stays frozen */
+    lock_snapshot(e, v, round);
+  }
   return GX_OK;
 }
 int gx_get_round(gx_engine *e, int64_t *round) {
@@ -1577,6 +1704,7 @@ int gx_broadcast_services(gx_engine *e, uint32_t host, const gx_service *list, u
     }
   bs_body(e, host, tmp, n, now_of(e), tmp + n);
   free(tmp);
+  lock_snapshot(e, host, e->round); /* a nil blocks the looper from now on */
   return GX_OK;
 }
 
@@ -1591,6 +1719,7 @@ int gx_broadcast_tombstones(gx_engine *e, uint32_t host, const gx_service *list,
   e->hs[host].running = mask;
   bt_tick(e, host, now_of(e));
   e->hs[host].running = saved;
+  lock_snapshot(e, host, e->round);
   return GX_OK;
 }
 
@@ -1634,6 +1763,7 @@ int gx_get_broadcasts(gx_engine *e, uint32_t host, uint32_t limit, gx_service *o
   uint32_t l = get_broadcasts(e, host, limit, pk, 0, 0);
   for (uint32_t i = 0; i < l; i++) to_svc(e, &pk[i], &out[i]);
   *n_out = l;
+  lock_snapshot(e, host, e->round); /* a looper's nil may have been taken */
   return GX_OK;
 }
 
@@ -1648,6 +1778,7 @@ int gx_get_broadcasts_bytes(gx_engine *e, uint32_t host, uint32_t overhead, uint
   for (uint32_t i = 0; i < l; i++) to_svc(e, &pk[i], &out[i]);
   free(pk);
   *n_out = l;
+  lock_snapshot(e, host, e->round);
   return GX_OK;
 }
 
@@ -1951,6 +2082,15 @@ int gx_host_digests(gx_engine *e, uint64_t *out) {
         h = feed(h, g->r);
       }
     }
+    h = feed(h, 0x10C6); /* the lock buffer, then the owners whose ExpireServer waits */
+    for (uint32_t k = 0; k < GX_LOCK_BUF(s->lock); k++) {
+      const grec *g = &e->lkb[(size_t)v * e->C + k];
+      h = feed(h, g->w);
+      h = feed(h, g->r);
+    }
+    if (s->lock & GX_LOCK_PENDING_EXPIRE)
+      for (uint32_t k = 0; k < e->PW; k++)
+        if (e->pexp[(size_t)v * e->PW + k]) h = feed(h, (uint64_t)k << 32 | e->pexp[(size_t)v * e->PW + k]);
     h = feed(h, s->flags);
     h = feed(h, (uint64_t)s->bs_next);
     h = feed(h, (uint64_t)s->bt_next);
@@ -2170,9 +2310,11 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
   uint8_t *p = (uint8_t *)buf;
   for (uint32_t k = 0; k < e->x_n; k++) {
     uint8_t *m = p + (size_t)k * dig_bytes(e);
-    /* word 3: with the failure detector, the initiator's decision that the pair runs */
+    /* word 3: bit 0, with the failure detector, the initiator's decision that the pair runs; bit 1,
+     * this side's host holds the ServicesState lock this round (gx.h lock_model) */
     uint32_t hdr[4] = {e->x_t[k], e->x_mine[k], e->nblk,
-                       (uint32_t)(e->p.fd_enable && e->x_first[k] && ae_initiator_runs(e, e->x_mine[k], k))};
+                       (uint32_t)(e->p.fd_enable && e->x_first[k] && ae_initiator_runs(e, e->x_mine[k], k)) |
+                           (uint32_t)locked_at(e, e->x_mine[k]) << 1};
     memcpy(m, hdr, 16);
     const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
     for (uint32_t b = 0; b < e->nblk; b++) {
@@ -2222,6 +2364,13 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
     if (hdr[0] != e->x_t[k] || hdr[2] != e->nblk) rc = GX_EINVAL;
     e->x_run[k] = (uint8_t)(!e->p.fd_enable ||
                             (e->x_first[k] ? ae_initiator_runs(e, e->x_mine[k], k) : (hdr[3] & 1u) != 0));
+    if (e->x_run[k] && (locked_at(e, e->x_mine[k]) || (hdr[3] & 2u))) { /* a side holds the lock */
+      note_locked(e);
+      if (e->p.lock_model) {
+        e->x_run[k] = 0;
+        if (e->x_first[k]) e->st.ae_locked++;
+      }
+    }
     if (pp_state(e)) memcpy(&e->x_rsnap[(size_t)k * e->H], m + 16 + 16ull * e->nblk, 8ull * e->H);
     uint64_t sz = 16, in = 16;
     e->x_nlead[k] = e->x_nfol[k] = 0;

@@ -174,7 +174,7 @@ static void fd_dead_node(gx_engine *e, uint32_t v, const gx_fd_msg *d, int64_t n
   x->state = GX_M_DEAD;
   x->change_round = (int32_t)e->round;
   e->st.fd_deaths++;
-  expire_server(e, v, m, now);
+  notify_leave(e, v, m, now);
 }
 
 /* suspicion.Confirm: one confirmation per distinct accuser, at most k; the deadline moves to

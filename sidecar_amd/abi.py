@@ -29,6 +29,7 @@ TS_SHIFT = 3
 JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE, JOB_LOST = 0, 1, 2, 3, 4, 5
 INIT_EMPTY, INIT_OWN, INIT_WARM = 0, 1, 2
 LIMIT_DEFAULT = 0xFFFFFFFF
+LOCK_PENDING_EXPIRE, LOCK_BUF_SHIFT = 4, 8  # gx_host_state.lock (gx.h)
 
 K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode", "fd"]
 
@@ -112,6 +113,7 @@ class GxParams(C.Structure):
         ("fd_suspicion_rounds", C.c_uint32 * 8), ("depart_round", C.c_int32), ("depart_ppm", C.c_uint32),
         ("fd_push_pull_state", C.c_uint32),
         ("gossip_messages", C.c_uint32), ("push_pull_mode", C.c_uint32), ("inbox_slots", C.c_uint32),
+        ("lock_model", C.c_uint32), ("lock_buffer", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)
@@ -137,7 +139,15 @@ class GxHostState(C.Structure):
                 ("arena_used", C.c_uint32), ("flags", C.c_uint32), ("bs_next", C.c_int64),
                 ("bt_next", C.c_int64), ("last_bcast_ns", C.c_int64), ("running", C.c_uint64),
                 ("fifo_stored", C.c_uint32), ("nil_pos_bs", C.c_uint32), ("nil_pos_bt", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("lock", C.c_uint32)]
+
+    def locked_at(self, round_):
+        """A looper held the ServicesState lock at the start of round `round_` (gx.h lock)."""
+        return (self.lock >> (round_ & 1)) & 1
+
+    @property
+    def lock_buffered(self):
+        return self.lock >> LOCK_BUF_SHIFT
 
 
 class GxStats(C.Structure):
@@ -151,7 +161,9 @@ class GxStats(C.Structure):
         ("listener_drops", C.c_uint64)] + [(n, C.c_uint64) for n in (
         "lost_packets", "fd_probes", "fd_probe_failures", "fd_suspicions", "fd_confirmations",
         "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received",
-        "fd_state_merges", "queue_deferred")] + [("first_drop_round", C.c_int64)]
+        "fd_state_merges", "queue_deferred")] + [("first_drop_round", C.c_int64)] + [
+        ("locked_merges", C.c_uint64), ("first_locked_round", C.c_int64)] + [(n, C.c_uint64) for n in (
+        "lock_buffered", "lock_drops", "lock_drained", "ae_locked", "expire_deferred")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}

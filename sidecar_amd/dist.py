@@ -19,6 +19,9 @@ import torch
 
 from .abi import Engine, GxParams, default_params
 
+# stats that hold the earliest round something happened (-1: never): the minimum over shards
+FIRST_ROUND_STATS = ("first_drop_round", "first_locked_round")
+
 
 def _ptr(t: torch.Tensor) -> int:
     return t.data_ptr() if t.numel() else 0
@@ -161,7 +164,7 @@ class LocalShards:
         tot = {}
         for s in self.shards:
             for k, v in s.e.stats().items():
-                if k == "first_drop_round":  # the earliest over shards (-1: none)
+                if k in FIRST_ROUND_STATS:  # the earliest over shards (-1: none)
                     tot[k] = min(x for x in (tot.get(k, -1), v) if x >= 0) if max(tot.get(k, -1), v) >= 0 else -1
                 else:
                     tot[k] = max(tot.get(k, v), v) if k in ("round", "last_change_round") else tot.get(k, 0) + v
@@ -328,16 +331,16 @@ class DistShard:
         keys = sorted(st)
         t = torch.tensor([st[k] for k in keys], dtype=torch.int64, device=self.device)
         mx = t.clone()
-        fd = int(st["first_drop_round"])
-        mn = torch.tensor([fd if fd >= 0 else 1 << 62], dtype=torch.int64, device=self.device)
+        mn = torch.tensor([int(st[k]) if st[k] >= 0 else 1 << 62 for k in FIRST_ROUND_STATS],
+                          dtype=torch.int64, device=self.device)
         self._all_reduce(t, self.dist.ReduceOp.SUM)
         self._all_reduce(mx, self.dist.ReduceOp.MAX)
-        self._all_reduce(mn, self.dist.ReduceOp.MIN)  # the earliest LOST dequeue over shards
+        self._all_reduce(mn, self.dist.ReduceOp.MIN)  # the earliest LOST dequeue / lock over shards
         out = dict(zip(keys, t.tolist()))
         for k in ("round", "last_change_round"):
             out[k] = int(mx[keys.index(k)].item())
-        fd = int(mn.item())
-        out["first_drop_round"] = fd if fd < 1 << 62 else -1
+        for k, x in zip(FIRST_ROUND_STATS, mn.tolist()):
+            out[k] = int(x) if x < 1 << 62 else -1
         return out
 
     def converged(self):
