@@ -119,9 +119,9 @@ def workload_text(cfg):
     return f"{cfg}: {c['desc']}; {cad}{gms}"
 
 
-def make_engine(lib, cfg, seed, device):
+def make_engine(lib, cfg, seed, device, **over):
     from sidecar_amd.abi import Engine, default_params
-    p = default_params(lib, **CONFIGS[cfg]["p"])
+    p = default_params(lib, **dict(CONFIGS[cfg]["p"], **over))
     p.seed = seed
     p.device = device
     return Engine(p, lib=lib)
@@ -140,26 +140,45 @@ def queue_report(cfg, st0, st1):
     p = CONFIGS[cfg]["p"]
     ke = p.get("fanout", 3) * max(1, p.get("gossip_messages", 0))
     d = {k: st1[k] - (st0[k] if st0 else 0) for k in ("queue_deferred", "queue_drops", "list_drops", "sleep_drops",
-                                                       "pending_drops", "retransmits", "dequeues")}
+                                                       "pending_drops", "retransmits", "dequeues",
+                                                       "locked_merges")}
+    # faithful: no job the reference would deliver was lost, and no merge ran on a host whose
+    # looper held the ServicesState lock (locked_merges, only with lock_model = 0; gx.h)
     return {"window_jobs_per_host": p["queue_cap"], "lossless_rounds_after_fill": p["queue_cap"] // ke,
             "retransmits": d["retransmits"], "dequeues": d["dequeues"], "deferred": d["queue_deferred"],
             "lost": d["queue_drops"], "first_lost_round": st1["first_drop_round"], "list_drops": d["list_drops"],
             "sleep_drops": d["sleep_drops"], "pending_truncated": d["pending_drops"],
-            "faithful": d["queue_drops"] == 0 and d["sleep_drops"] == 0}
+            "locked_merges": d["locked_merges"],
+            "faithful": d["queue_drops"] == 0 and d["sleep_drops"] == 0 and d["locked_merges"] == 0}
+
+
+def lock_report(p, st0, st1, hosts=None, rnd=None):
+    """The ServicesState lock held by a blocked looper (gx.h lock_model) over a run:
+    records held in locked hosts' inbound pipelines, dropped at a full pipeline (memberlist's handoff
+    queue), merged at unlock; push-pull exchanges that did not run; ExpireServer calls that waited;
+    with lock_model = 0, the merges that ran on locked hosts anyway (the rounds-1..4 model)."""
+    d = {k: st1[k] - (st0[k] if st0 else 0) for k in ("locked_merges", "lock_buffered", "lock_drops",
+                                                       "lock_drained", "ae_locked", "expire_deferred")}
+    out = {"lock_model": int(p.lock_model), "pipeline_records": int(p.lock_buffer), **d,
+           "first_locked_round": st1["first_locked_round"]}
+    if hosts is not None:
+        out["hosts_locked_at_end"] = sum(h.locked_at(rnd) for h in hosts)
+        out["records_held_at_end"] = sum(h.lock_buffered for h in hosts)
+    return out
 
 
 class Cluster:
     """The benchmarked cluster: one engine (N=1) or this rank's shard (N>1, sidecar_amd.dist)."""
 
-    def __init__(self, lib, cfg, seed, rank, world, local_rank, barrier, device=None):
+    def __init__(self, lib, cfg, seed, rank, world, local_rank, barrier, device=None, **over):
         self.world = world
         self.barrier = barrier
         if world == 1:
-            self.e = make_engine(lib, cfg, seed, local_rank)
+            self.e = make_engine(lib, cfg, seed, local_rank, **over)
             self.shard = None
         else:
             from sidecar_amd.dist import DistShard
-            kw = dict(CONFIGS[cfg]["p"])
+            kw = dict(CONFIGS[cfg]["p"], **over)
             kw["seed"] = seed
             self.shard = DistShard(lib, rank, world, device or f"cuda:{local_rank}", **kw)
             self.e = self.shard.e
@@ -404,11 +423,14 @@ def version_spread(e, dev, heal, end, check_every=10, slots=16):
                                     unfinished=int((pend_T < (1 << 62)).sum()), ring_overflow=overflow)}
 
 
-def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None):
-    """Fresh cluster from round 0: chunks of `check_every` rounds, catalog agreement checked
-    between chunks (check time excluded). Returns (rounds_to_converge or None, wall_s, rounds run,
-    disagreement samples): the records some live views disagree on, every 100 rounds."""
-    c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier, device)
+def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, check_every, device=None,
+                 **over):
+    """Fresh cluster from round 0: chunks of `check_every` rounds (100 past round 1000; the round is
+    taken from the engine's last-change round, so the chunk only bounds when agreement is seen),
+    catalog agreement checked between chunks (check time excluded). Returns (rounds_to_converge or
+    None, wall_s, rounds run, disagreement samples, queue report, lock report): the samples are the
+    records some live views disagree on, every 100 rounds (every 1000 past round 10000)."""
+    c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier, device, **over)
     wall = 0.0
     conv = None
     samples = []
@@ -417,11 +439,11 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
         while c.round < max_rounds:
             barrier()
             t0 = time.perf_counter()
-            c.run_rounds(check_every)
+            c.run_rounds(min(check_every if c.round < 1000 else max(check_every, 100), max_rounds - c.round))
             barrier()
             wall += time.perf_counter() - t0
             ok, bad = c.converged()
-            if c.round % 100 == 0 or ok:
+            if (c.round % 100 == 0 and (c.round <= 10000 or c.round % 1000 == 0)) or ok:
                 samples.append([c.round, int(bad)])
             if ok:
                 lc = c.stats()["last_change_round"]
@@ -432,7 +454,8 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
                 wall = wall * conv / c.round if c.round else wall
                 break
         st_end = c.stats()
-        return conv, wall, c.round, samples, queue_report(cfg, None, st_end)
+        hosts = (c.e.hosts(), c.round) if world == 1 else (None, None)
+        return conv, wall, c.round, samples, queue_report(cfg, None, st_end), lock_report(c.e.params, None, st_end, *hosts)
     finally:
         c.close()
 
@@ -486,6 +509,9 @@ def main():
     ap.add_argument("--no-converge", action="store_true")
     ap.add_argument("--converge-max", type=int, default=3000)
     ap.add_argument("--check-every", type=int, default=10)
+    ap.add_argument("--spread-max", type=int, default=3000, help="last round of the version-spread run")
+    ap.add_argument("--no-lock-off", action="store_true",
+                    help="skip the same window with lock_model = 0 (the rounds-1..4 model, for comparison)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-split", action="store_true", help="skip the instrumented per-kernel pass")
     ap.add_argument("--cpu-hosts", type=int, default=16384, help="H of the multi-threaded CPU sample")
@@ -530,6 +556,7 @@ def main():
     st1 = c.stats()
     x1 = c.exchange_bytes()
     xfer = {k: x1[k] - x0[k] for k in x1} if x1 else None
+    lock = lock_report(c.e.params, st0, st1, *((c.e.hosts(), c.round) if world == 1 else (None, None)))
     c.close()
 
     split = {k: st1[k] - st0[k] for k in ("gossip_merges", "ae_merges", "local_merges")}
@@ -539,6 +566,28 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt_max = float(t.item())
+
+    # the same window without the ServicesState lock (lock_model = 0, the rounds-1..4 model): merges
+    # proceed on hosts whose looper holds the lock; reported for comparison, never the headline
+    lock_off = None
+    if world == 1 and not args.no_lock_off and c.e.params.lock_model:
+        c = Cluster(lib, args.config, seed, rank, world, local_rank, barrier, lock_model=0)
+        if args.warmup:
+            c.run_rounds(args.warmup)
+        s0 = c.stats()
+        barrier()
+        t0 = time.perf_counter()
+        c.run_rounds(args.steps)
+        barrier()
+        dto = time.perf_counter() - t0
+        s1 = c.stats()
+        c.close()
+        lock_off = {"value": (merges(s1) - merges(s0)) / dto, "ms_per_step": dto * 1000.0 / args.steps,
+                    "merges": {k: s1[k] - s0[k] for k in ("gossip_merges", "ae_merges", "local_merges")},
+                    "locked_merges": s1["locked_merges"] - s0["locked_merges"],
+                    "faithful": s1["locked_merges"] == s0["locked_merges"],
+                    "note": "lock_model = 0: merges run on hosts whose BroadcastServices / BroadcastTombstones looper "
+                            "holds the ServicesState lock (services_state.go:535,569 / :610,628); not the reference"}
 
     # per-kernel split: the same window again on a fresh cluster, with HIP events around every
     # launch on the engine's stream (device time per kernel class and algorithmic bytes)
@@ -594,28 +643,35 @@ def main():
                     lib, args.config, seed, local_rank, start=acc0)
 
     conv = None
+    conv_lock_off = None
     if not args.no_converge:
-        r, w, ran, dis_s, qr = run_converge(lib, args.config, seed, rank, world, local_rank, barrier,
-                                            args.converge_max, args.check_every)
+        r, w, ran, dis_s, qr, lr = run_converge(lib, args.config, seed, rank, world, local_rank, barrier,
+                                                args.converge_max, args.check_every)
         conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
-                "rounds_run": ran, "simulated_s": (r * 0.2) if r else None, "queues": qr}
+                "rounds_run": ran, "simulated_s": (r * 0.2) if r else None, "queues": qr, "lock": lr}
         if r is None:  # how far from agreement the catalog stays (records some live views disagree on)
             conv["disagreeing_records"] = {"min": min(x[1] for x in dis_s) if dis_s else None,
                                            "every_100_rounds": dis_s}
+        if world == 1 and not args.no_lock_off and lr["lock_model"]:  # the rounds-1..4 figure, for comparison
+            r, w, ran, _, qr, lr = run_converge(lib, args.config, seed, rank, world, local_rank, barrier,
+                                                min(args.converge_max, 3000), args.check_every, lock_model=0)
+            conv_lock_off = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
+                             "rounds_run": ran, "locked_merges": qr["locked_merges"], "faithful": qr["faithful"],
+                             "note": "lock_model = 0 (not the reference: merges run on locked hosts)"}
     conv_ref = None
     ref = CONFIGS[args.config].get("ref_variant")
     if ref and not args.no_converge:
-        r, w, ran, _, qr = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
-                                        args.check_every)
+        r, w, ran, _, qr, lr = run_converge(lib, ref, seed, rank, world, local_rank, barrier, args.converge_max,
+                                            args.check_every)
         conv_ref = {"config": workload_text(ref), "rounds_to_converge": r,
                     "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
-                    "simulated_s": (r * 0.2) if r else None, "queues": qr}
+                    "simulated_s": (r * 0.2) if r else None, "queues": qr, "lock": lr}
     spread = None
     heal = CONFIGS[args.config]["p"].get("partition_end", 0)
     if world == 1 and heal and not args.no_converge:  # per-version spread after the heal (defined at any cadence)
         e = make_engine(lib, args.config, seed, local_rank)
         try:
-            spread = version_spread(e, torch.device(f"cuda:{local_rank}"), heal, args.converge_max)
+            spread = version_spread(e, torch.device(f"cuda:{local_rank}"), heal, max(heal + 10, args.spread_max))
         finally:
             e.close()
     dis = None
@@ -639,8 +695,11 @@ def main():
                        "parallelism": (f"host-sharded over {world} ranks ("
                                        + ("RCCL all-to-all)" if backend == "nccl" else "gloo, host-staged all-to-all)")
                                        if world > 1 else "single GPU")},
-            "merges": split, "queues": queue_report(args.config, st0, st1),
-            "gossip": gossip, "converge": conv, "converge_ref_cadence": conv_ref,
+            "gossip_merges_per_s": split["gossip_merges"] / dt_max, "ae_merges_per_s": split["ae_merges"] / dt_max,
+            "merges": split, "queues": queue_report(args.config, st0, st1), "lock": lock,
+            "lock_off": lock_off,
+            "gossip": gossip, "converge": conv, "converge_lock_off": conv_lock_off,
+            "converge_ref_cadence": conv_ref,
             "dissemination": dis, "version_spread": spread,
             "roofline": roof, "roofline_merge": roofline("merge"), "roofline_send": roofline("send"),
             "cpu_baseline": cpu, "kernels": kern,

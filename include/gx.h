@@ -122,6 +122,9 @@ typedef struct gx_service {
 #define GX_JOB_SEND 3
 #define GX_JOB_EXPIRE 4
 #define GX_JOB_LOST 5
+/* c of a SendServices job queued past the stored window: it holds no list (only a LOST dequeue
+ * could reach it), so nothing is released for it */
+#define GX_LIST_NONE 0xffffu
 typedef struct gx_job {
   uint64_t a;
   uint32_t c;
@@ -338,8 +341,9 @@ typedef struct gx_stats {
   uint64_t queue_deferred;   /* jobs queued past the stored window (kept as a count, gx_job) */
   int64_t first_drop_round;  /* round of the first queue_drops dequeue, -1 = none */
   /* The ServicesState lock (gx_params.lock_model) */
-  uint64_t locked_merges;    /* lock_model = 0: gossip and push-pull AddServiceEntry calls applied on a
-                                host whose looper held the lock (the reference would have waited) */
+  uint64_t locked_merges;    /* lock_model = 0: AddServiceEntry calls the reference would not have made
+                                then: gossip records merged by a host whose looper held the lock, and
+                                both sides' merges of a push-pull exchange with such a host */
   int64_t first_locked_round;/* first round a locked host received gossip records or was in a push-pull
                                 pair, -1 = none (both modes) */
   uint64_t lock_buffered;    /* records queued in a locked host's inbound pipeline */

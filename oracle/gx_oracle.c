@@ -232,6 +232,7 @@ static int alloc_list(gx_engine *e, uint32_t v) {
 static void free_list(gx_engine *e, uint32_t v, const gx_job *j) {
   if (GX_JOB_KIND(j->meta) != GX_JOB_SEND) return;
   const uint32_t slot = j->c & 0xffff;
+  if (slot >= e->A) return; /* GX_LIST_NONE: a SendServices job queued deferred holds no list */
   e->arena_bits[(size_t)v * e->AW + slot / 32] &= ~(1u << (slot % 32));
   e->hs[v].arena_used &= ~(1u << (slot / 32));
 }
@@ -306,11 +307,12 @@ static void create_send(gx_engine *e, uint32_t v, const grec *list, uint32_t n, 
   gx_host_state *h = &e->hs[v];
   e->st.send_jobs++;
   if (n > e->L) n = e->L;
-  gx_job j = {0, 0, meta_of(GX_JOB_SEND, 0, npasses)};
+  gx_job j = {0, GX_LIST_NONE, meta_of(GX_JOB_SEND, 0, npasses)};
   if (fifo_can_store(e, h)) { /* a deferred job needs no list */
     const int slot = alloc_list(e, v);
     if (slot < 0) {
       e->st.list_drops++;
+      j.c = 0;
       j.meta = meta_of(GX_JOB_LOST, 0, 1);
     } else {
       grec *dst = &e->arena[((size_t)v * e->A + slot) * e->L];
@@ -795,13 +797,13 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
     if (st_of(vb[r]) == GX_ABSENT) continue;
     grec u = {vb[r], r, 0};
     add_entry(e, a, u, now, SRC_AE);
-    e->st.locked_merges += (uint64_t)la;
+    e->st.locked_merges += (uint64_t)(la | lb);
   }
   for (uint32_t r = 0; r < e->R; r++) { /* b.Merge(a's state snapshot) */
     if (st_of(sa[r]) == GX_ABSENT) continue;
     grec u = {sa[r], r, 0};
     add_entry(e, b, u, now, SRC_AE);
-    e->st.locked_merges += (uint64_t)lb;
+    e->st.locked_merges += (uint64_t)(la | lb);
   }
   e->st.ae_exchanges++;
   e->st.ae_slots += 2ull * e->R;
@@ -1034,13 +1036,13 @@ static void ae_pair_at(const gx_engine *e, uint32_t t, uint32_t *a, uint32_t *b)
 }
 
 /* x <- a remote host's row (one direction of a cross-shard push-pull pair). */
-static void ae_merge_row(gx_engine *e, uint32_t x, const uint64_t *row, int count_exchange, int64_t now) {
-  const int lx = locked_at(e, x); /* lock_model = 0 (a locked pair runs only then): counted */
+/* locked: a side of the pair holds the lock (lock_model = 0, where such a pair runs): counted */
+static void ae_merge_row(gx_engine *e, uint32_t x, const uint64_t *row, int count_exchange, int locked, int64_t now) {
   for (uint32_t r = 0; r < e->R; r++) {
     if (st_of(row[r]) == GX_ABSENT) continue;
     grec u = {row[r], r, 0};
     add_entry(e, x, u, now, SRC_AE);
-    e->st.locked_merges += (uint64_t)lx;
+    e->st.locked_merges += (uint64_t)locked;
   }
   e->st.ae_slots += e->R;
   if (count_exchange) e->st.ae_exchanges++;
@@ -1558,10 +1560,11 @@ int gx_set_round(gx_engine *e, int64_t round) {
   if (!e || round < e->round || round >= GX_MAX_ROUND) return GX_EINVAL;
   e->round = round;
   e->st.round = round;
-  for (uint32_t v = 0; v < e->H; v++) {
-    if (!departed(e, v)) wake_host(e, v); /* a crashed host stays frozen */
-    lock_snapshot(e, v, round);
-  }
+  for (uint32_t v = 0; v < e->H; v++)
+    if (!departed(e, v)) { /* a crashed host stays frozen */
+      wake_host(e, v);
+      lock_snapshot(e, v, round);
+    }
   return GX_OK;
 }
 int gx_get_round(gx_engine *e, int64_t *round) {
@@ -2369,6 +2372,8 @@ int gx_ae_delta_bytes(gx_engine *e, const void *digests, uint64_t bytes, uint64_
       if (e->p.lock_model) {
         e->x_run[k] = 0;
         if (e->x_first[k]) e->st.ae_locked++;
+      } else {
+        e->x_run[k] |= 2; /* runs anyway: its merges are counted (locked_merges) */
       }
     }
     if (pp_state(e)) memcpy(&e->x_rsnap[(size_t)k * e->H], m + 16 + 16ull * e->nblk, 8ull * e->H);
@@ -2595,7 +2600,7 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
         }
         memcpy(&row[lo], w, 8ull * n);
       }
-      ae_merge_row(e, e->x_mine[k], row, e->x_first[k], now);
+      ae_merge_row(e, e->x_mine[k], row, e->x_first[k], (e->x_run[k] & 2) != 0, now);
     }
     free(row);
     free(loff);
@@ -2613,7 +2618,7 @@ int gx_ae_merge_local(gx_engine *e) {
   return GX_OK;
 }
 int gx_round_end(gx_engine *e) {
-  if (!e) return GX_EINVAL;
+  if (!e || e->round + 1 >= GX_MAX_ROUND) return GX_EINVAL; /* rounds are 32-bit in jobs and sleepers */
   round_end(e);
   return GX_OK;
 }

@@ -72,14 +72,17 @@ enum {
   C_GOSSIP_MERGES, C_AE_MERGES, C_LOCAL_MERGES, C_GOSSIP_ACC, C_AE_ACC, C_LOCAL_ACC, C_STALE,
   C_RETX, C_QDROP, C_LDROP, C_SDROP, C_PDROP, C_DEQ, C_NIL, C_PACKETS, C_RECSENT, C_EXPIRED,
   C_GC, C_OWNTOMB, C_EXPSRV, C_SENDJOBS, C_AEX, C_CHURN, C_SCANSLOTS, C_AESLOTS, C_BYTESENT,
-  C_CAPCUT, C_CHG, C_QDEFER, C_NCTR
+  C_CAPCUT, C_CHG, C_QDEFER,
+  // the ServicesState lock (gx.h lock_model)
+  C_LOCKED_MERGES, C_LOCK_BUF, C_LOCK_DROP, C_LOCK_DRAIN, C_AE_LOCKED, C_NCTR
 };
 // Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
 enum {
   C_LOST = C_NCTR, C_FD_PROBES, C_FD_PROBE_FAIL, C_FD_SUSPECT, C_FD_CONFIRM, C_FD_DEATH, C_FD_REFUTE,
-  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_NCTR_ALL
+  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_NCTR_ALL
 };
 #define GX_NCTR_SLOTS 48
+static_assert(C_NCTR_ALL <= GX_NCTR_SLOTS, "counter slots");
 
 #define GX_SHARDS 64
 // inbox slots per receiver, upper bound (gx_params.inbox_slots): the wave merge ranks up to this
@@ -90,7 +93,8 @@ struct DevCtr {
   unsigned long long last_change_p1[GX_SHARDS][8];  // last round with a slot change + 1
   unsigned long long bytes[GX_SHARDS][16];          // algorithmic HBM bytes per kernel class
   unsigned long long units[GX_SHARDS][16];          // slots / records per kernel class
-  unsigned long long first_drop[GX_SHARDS][8];      // first round a LOST job was dequeued (min; ~0 none)
+  unsigned long long first_drop[GX_SHARDS][8];      // [0] first round a LOST job was dequeued, [1] first
+                                                    // round the lock held back work (min; ~0 none)
 };
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
@@ -170,6 +174,12 @@ struct Dev {
   uint32_t nblk_ae;    // digest blocks per row, ceil(R / GX_DIGEST_SLOTS)
   uint64_t *snap;      // this round's k_send stores (round << 32 | work_cnt[GX_WC_SCANS]) here (pinned host memory), or null
   uint32_t sfilt;      // senders pre-filter inbound records for their local receivers (1 shard; see k_send)
+  // the ServicesState lock held by a blocked looper (gx.h lock_model)
+  uint32_t C;          // lock_buffer: records a locked host's inbound pipeline holds
+  grec *lkb;           // [Hl][C] the records queued there, arrival order (count: hs.lock >> 8)
+  uint32_t PW;         // words per host of pexp, ceil(H / 32)
+  uint32_t *pexp;      // [Hl][PW] owners whose ExpireServer waits for the host's lock
+  int in_round;        // a round phase is running: ExpireServer waits for the lock (ABI calls act directly)
   unsigned long long *kprof;  // diagnostics (env GX_KPROF): wall-clock phase marks of k_send per wave, or null
 };
 
@@ -248,7 +258,8 @@ GXD unsigned long long wave_min(unsigned long long x) {
 struct Acc {
   unsigned c[C_NCTR];
   bool changed;
-  GXD Acc() : changed(false) {
+  bool locked;  // the ServicesState lock held back (or, lock_model = 0, would have held back) work
+  GXD Acc() : changed(false), locked(false) {
 #pragma unroll
     for (int i = 0; i < C_NCTR; i++) c[i] = 0;
   }
@@ -273,6 +284,8 @@ GXD void acc_flush(const Dev &d, const Acc &a) {
   }
   bool any = __ballot(a.changed) != 0;
   if ((threadIdx.x & 63) == 0 && any) mark_change(d);
+  if (__ballot(a.locked) != 0 && (threadIdx.x & 63) == 0)
+    atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
 }
 
 // Local index of an owned host (global id v in [lo, lo + Hl)).
@@ -362,6 +375,21 @@ GXD void set_slot(const Dev &d, Acc &a, uint32_t v, uint64_t *slot, uint64_t nw)
   }
 }
 
+// ------------------------------------------------ the ServicesState lock --
+// BroadcastServices blocks on its nil holding state.RLock() (services_state.go:535-536,569),
+// BroadcastTombstones holding state.Lock() (:610-611,628). Host v is locked for round n iff one of
+// them was blocked at the start of round n: bit (n & 1) of its lock word (gx.h gx_host_state.lock),
+// written for round n + 1 when v's round-n GetBroadcasts calls end, so every phase of a round reads
+// one value and another host's team may read it while v's team rewrites the other bit.
+GXD bool locked_in(const Dev &d, uint32_t lockw) { return GX_LOCK_AT(lockw, d.round) != 0u; }
+GXD bool host_locked(const Dev &d, uint32_t v) { return locked_in(d, gld(&hst(d, v)->lock)); }
+// the lock word with bit `round & 1` set from the loopers' state
+GXD uint32_t lock_snap(uint32_t lockw, uint32_t flags, int64_t round) {
+  const uint32_t b = 1u << (round & 1);
+  return (lockw & ~b) | ((flags & 3u) ? b : 0u);
+}
+GXD void note_locked(const Dev &d) { atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round); }
+
 // --------------------------------------------------- change bookkeeping --
 GXD gx_server_times *srv_times(const Dev &d, uint32_t v, uint32_t o) {
   return &d.srvt[(size_t)li(d, v) * d.H + o];
@@ -414,6 +442,7 @@ GXD uint32_t fifo_room(const Dev &d, uint32_t head, uint32_t tail, uint32_t stor
 // The bitmap word is read and written by one lane of the host's team (lane0).
 GXD uint32_t *list_bits(const Dev &d, uint32_t vi, uint32_t w) { return &d.arena_bits[(size_t)vi * d.AW + w]; }
 GXD void list_release(const Dev &d, uint32_t vi, uint32_t &arena_used, uint32_t slot, bool lane0) {
+  if (slot >= d.A) return;  // GX_LIST_NONE: a SendServices job queued deferred holds no list
   if (lane0) *list_bits(d, vi, slot >> 5) &= ~(1u << (slot & 31));
   arena_used &= ~(1u << (slot >> 5));
 }
@@ -901,6 +930,31 @@ GXD bool expire_server(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
   return true;
 }
 
+// NotifyLeave -> go ExpireServer(node) (services_delegate.go:173-176) inside a round phase:
+// ExpireServer takes state.Lock() (services_state.go:151), so on a locked host the call waits (a
+// bit in pexp); the waiting calls run in owner order at the end of the owner phase of the host's
+// first unlocked round (run_pending_expires). One thread owns host v here.
+GXD void notify_leave(const Dev &d, Acc &a, uint32_t v, uint32_t o) {
+  gx_host_state *h = hst(d, v);
+  if (d.p.lock_model && d.in_round && locked_in(d, h->lock)) {
+    d.pexp[(size_t)li(d, v) * d.PW + (o >> 5)] |= 1u << (o & 31);
+    h->lock |= GX_LOCK_PENDING_EXPIRE;
+    ctr_atomic(d, C_EXP_DEFER, 1);
+    return;
+  }
+  expire_server(d, a, v, o);
+}
+GXD void run_pending_expires(const Dev &d, Acc &a, uint32_t v) {
+  uint32_t *w = &d.pexp[(size_t)li(d, v) * d.PW];
+  for (uint32_t k = 0; k < d.PW; k++) {
+    uint32_t x = w[k];
+    if (!x) continue;
+    w[k] = 0;
+    for (; x; x &= x - 1) expire_server(d, a, v, k * 32 + (uint32_t)__builtin_ctz(x));
+  }
+  hst(d, v)->lock &= ~GX_LOCK_PENDING_EXPIRE;
+}
+
 GXD bool is_new(const Dev &d, uint32_t o, uint64_t sw, uint32_t r) {
   uint64_t w = vrow(d, o)[r];
   return st_of(w) == GX_ABSENT || (st_of(sw) != GX_TOMBSTONE && st_of(sw) != st_of(w));
@@ -928,7 +982,7 @@ GXD void bs_body_list(const Dev &d, Acc &a, uint32_t o, const grec *list, uint32
     uint32_t m = 0;
     for (uint32_t i = 0; i < n && m < d.L; i++) m += (inc >> i) & 1ull;
     if (!fifo_stores(d, o)) {  // deferred: no list
-      push_job(d, a, o, make_job(0, 0, meta_of(GX_JOB_SEND, 0, any_new ? d.p.alive_count : 1)));
+      push_job(d, a, o, make_job(0, GX_LIST_NONE, meta_of(GX_JOB_SEND, 0, any_new ? d.p.alive_count : 1)));
     } else {
       int slot = alloc_list(d, a, o);
       if (slot >= 0) {
@@ -955,7 +1009,7 @@ GXD void bt_finish(const Dev &d, Acc &a, uint32_t o, uint64_t running, const gre
     a.c[C_SENDJOBS]++;
     int slot = fifo_stores(d, o) ? alloc_list(d, a, o) : -2;  // a deferred job takes no list
     const uint32_t len = n_own + n_others < d.L ? n_own + n_others : d.L;
-    if (slot == -2) push_job(d, a, o, make_job(0, 0, meta_of(GX_JOB_SEND, 0, d.p.tombstone_count)));
+    if (slot == -2) push_job(d, a, o, make_job(0, GX_LIST_NONE, meta_of(GX_JOB_SEND, 0, d.p.tombstone_count)));
     else if (slot < 0) commit_send(d, a, o, slot, len, d.p.tombstone_count);
     if (slot >= 0) {
       grec *dst = list_ptr(d, o, slot);

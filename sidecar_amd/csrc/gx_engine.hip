@@ -351,6 +351,11 @@ static int scan_probe_end(gx_engine *e) {
 static int round_send_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
+  d.in_round = 1;  // ExpireServer waits for a held lock (gx.h lock_model); reset after the launches
+  struct InRound {
+    Dev &d;
+    ~InRound() { d.in_round = 0; }
+  } in_round_guard{d};
   {
     int rc = scan_probe_begin(e);
     if (rc) return rc;
@@ -464,6 +469,11 @@ static int round_send_impl(gx_engine *e) {
 static int round_merge_impl(gx_engine *e) {
   Dev &d = e->d;
   set_round_fields(e);
+  d.in_round = 1;
+  struct InRound {
+    Dev &d;
+    ~InRound() { d.in_round = 0; }
+  } in_round_guard{d};
   hipStream_t s = e->stream;
   if (d.K) {
     LaunchTimer t(e, GX_K_MERGE);
@@ -664,6 +674,8 @@ void gx_params_default(gx_params *p) {
   p->fd_gossip_dead_rounds = 150;
   p->depart_round = -1;
   p->fd_push_pull_state = 1;
+  p->lock_model = 1;
+  p->lock_buffer = 1024 + 1 + 25 + 1 + 25 + 1;  // gx.h lock_model: handoff queue .. AddServiceEntry
   gx_fd_defaults(p);
 }
 
@@ -724,6 +736,7 @@ static int check_params(const gx_params *p) {
   if (p->push_pull_mode > GX_PP_INITIATE || (p->push_pull_mode == GX_PP_INITIATE && (p->n_shards > 1 || p->fd_enable)))
     return GX_EINVAL;
   if (p->inbox_slots > GX_DI_MAX) return GX_EINVAL;
+  if (p->lock_model > 1 || p->lock_buffer < 1 || p->lock_buffer > 65535) return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -748,7 +761,7 @@ int gx_destroy(gx_engine *e) {
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_w0, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mrec, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
-                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap};
+                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap, d.lkb, d.pexp};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
@@ -927,6 +940,15 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(d.fd_peers, sizeof(uint32_t) * H * K);
     ALLOC(d.fd_np, sizeof(uint32_t) * H);
     if (p->fd_push_pull_state) ALLOC(d.fd_snap, sizeof(uint64_t) * H * Hg);
+  }
+  if (p->lock_model) {  // locked hosts' inbound pipelines and waiting ExpireServer calls (gx.h lock_model)
+    d.C = p->lock_buffer;
+    ALLOC(d.lkb, sizeof(grec) * H * d.C);
+    d.PW = (d.H + 31) / 32;
+    if (p->storm_round >= 0 || p->fd_enable) {
+      ALLOC(d.pexp, sizeof(uint32_t) * H * d.PW);
+      HIPCHK(hipMemset(d.pexp, 0, sizeof(uint32_t) * H * d.PW));
+    }
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
   e->xplan_stream = nullptr;
@@ -2278,7 +2300,7 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
 }
 
 int gx_round_end(gx_engine *e) {
-  if (!e) return GX_EINVAL;
+  if (!e || e->d.round + 1 >= GX_MAX_ROUND) return GX_EINVAL;  // rounds are 32-bit in jobs and sleepers
   HIPCHK(hipSetDevice(e->device));
   int rc = join_side(e);
   if (rc) return rc;
@@ -2302,7 +2324,8 @@ int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
 }
 
 static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *last_p1, unsigned long long *bytes,
-                    unsigned long long *units, unsigned long long *first_drop = nullptr) {
+                    unsigned long long *units, unsigned long long *first_drop = nullptr,
+                    unsigned long long *first_locked = nullptr) {
   std::vector<DevCtr> tmp(1);
   HIPCHK(hipMemcpyAsync(tmp.data(), e->d.ctr, sizeof(DevCtr), hipMemcpyDeviceToHost, e->stream));
   int rc = sync_check(e);
@@ -2312,8 +2335,10 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
   for (int i = 0; i < 16; i++) bytes[i] = units[i] = 0;
   *last_p1 = 0;
   if (first_drop) *first_drop = ~0ull;
+  if (first_locked) *first_locked = ~0ull;
   for (int s = 0; s < GX_SHARDS; s++) {
     if (first_drop && x.first_drop[s][0] < *first_drop) *first_drop = x.first_drop[s][0];
+    if (first_locked && x.first_drop[s][1] < *first_locked) *first_locked = x.first_drop[s][1];
     for (int i = 0; i < GX_NCTR_SLOTS; i++) c[i] += x.c[s][i];
     for (int i = 0; i < 16; i++) {
       bytes[i] += x.bytes[s][i];
@@ -2327,11 +2352,18 @@ static int read_ctr(gx_engine *e, unsigned long long *c, unsigned long long *las
 int gx_stats_get(gx_engine *e, gx_stats *out) {
   if (!e || !out) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));
-  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[16], units[16], fdr;
-  int rc = read_ctr(e, c, &lp1, bytes, units, &fdr);
+  unsigned long long c[GX_NCTR_SLOTS], lp1, bytes[16], units[16], fdr, flr;
+  int rc = read_ctr(e, c, &lp1, bytes, units, &fdr, &flr);
   if (rc) return rc;
   memset(out, 0, sizeof(*out));
   out->queue_deferred = c[C_QDEFER];
+  out->locked_merges = c[C_LOCKED_MERGES];
+  out->first_locked_round = flr == ~0ull ? -1 : (int64_t)flr;
+  out->lock_buffered = c[C_LOCK_BUF];
+  out->lock_drops = c[C_LOCK_DROP];
+  out->lock_drained = c[C_LOCK_DRAIN];
+  out->ae_locked = c[C_AE_LOCKED];
+  out->expire_deferred = c[C_EXP_DEFER];
   out->first_drop_round = fdr == ~0ull ? -1 : (int64_t)fdr;
   out->lost_packets = c[C_LOST];
   out->fd_probes = c[C_FD_PROBES];

@@ -216,7 +216,7 @@ GXD void fd_dead_node(const Dev &d, Acc &a, FdAcc &f, uint32_t v, const gx_fd_ms
   x->change_round = (int32_t)d.round;
   f.inc(C_FD_DEATH);
   if (died) *died = true;
-  else expire_server(d, a, v, m);
+  else notify_leave(d, a, v, m);
 }
 GXD bool fd_confirm(const Dev &d, FdAcc &f, uint32_t v, uint32_t m, gx_member *x, uint32_t from,
                     bool lanes = false) {
@@ -385,7 +385,7 @@ GXD void fd_timers_wave(const Dev &d, Acc &a, FdAcc &f, uint32_t v) {
       while (dm) {
         const uint32_t k = (uint32_t)__ffsll((long long)dm) - 1;
         dm &= dm - 1;
-        expire_server(d, a, v, base + k);
+        notify_leave(d, a, v, base + k);
       }
   }
 #pragma unroll
@@ -687,8 +687,10 @@ __global__ __launch_bounds__(128) void k_fd_pushpull_pair(Dev d, uint64_t key0, 
     }
   }
   const uint32_t a = base + feistel_perm(key, 2 * q, m), b = base + feistel_perm(key, 2 * q + 1, m);
-  if (threadIdx.x == 0)  // pp_runs on the lists as this phase starts (nothing merged yet)
-    s_run = !departed(d, a) && !departed(d, b) && reach(d, a, b) && (fd_snap_word(d, a, b) & 0xffu) == GX_M_ALIVE;
+  if (threadIdx.x == 0)  // pp_runs on the lists as this phase starts (nothing merged yet); a side that
+    // holds the ServicesState lock fails the whole exchange (gx.h lock_model)
+    s_run = !departed(d, a) && !departed(d, b) && reach(d, a, b) && (fd_snap_word(d, a, b) & 0xffu) == GX_M_ALIVE &&
+            !(d.p.lock_model && (host_locked(d, a) || host_locked(d, b)));
   __syncthreads();
   if (s_run) fd_merge_pair_lockstep(d, f, a, b, s_w);
   fd_flush(d, f);
@@ -703,8 +705,9 @@ __global__ __launch_bounds__(64) void k_fd_pushpull_plan(Dev d, const uint32_t *
   const uint32_t i = blockIdx.x >> 1, side = blockIdx.x & 1;
   const int32_t k = prow[i];
   if (k < 0) {
-    if (pp_runs(d, pa[i], pb[i])) fd_merge_state_wave(d, f, side ? pb[i] : pa[i], snap_row(d, side ? pa[i] : pb[i]));
-  } else if (side == 0 && !skip[k]) {
+    if (pp_runs(d, pa[i], pb[i]) && !(d.p.lock_model && (host_locked(d, pa[i]) || host_locked(d, pb[i]))))
+      fd_merge_state_wave(d, f, side ? pb[i] : pa[i], snap_row(d, side ? pa[i] : pb[i]));
+  } else if (side == 0 && !(skip[k] & 1u)) {
     fd_merge_state_wave(d, f, pa[i], &rsnap[(size_t)k * d.H]);
   }
   fd_flush(d, f);

@@ -188,6 +188,10 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < d.Hl && !departed(d, d.lo + idx)) {  // a crashed host stays frozen
     gx_host_state *h = &d.hs[idx];
+    {  // the ServicesState lock for this round: the loopers' state (unchanged since the last sends)
+      const uint32_t lw = h->lock, nl = lock_snap(lw, h->flags, d.round);
+      if (nl != lw) h->lock = nl;
+    }
     const uint4 c = *reinterpret_cast<const uint4 *>(h);  // fifo_head, fifo_tail, sleep_head, sleep_tail
     if (c.z != c.w) {
       gx_host_state hs;
@@ -342,7 +346,10 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
           if (lead) a.c[C_CHURN]++;
         }
       }
-      if (!(hs.flags & 1u) && hs.bs_next <= d.round) {
+      // with the lock modelled, a looper whose tick finds the other one blocked on its nil (holding
+      // the ServicesState lock) waits: it ticks at the first owner phase after that nil was taken
+      const bool lm = d.p.lock_model != 0;
+      if (!(hs.flags & 1u) && !(lm && (hs.flags & 2u)) && hs.bs_next <= d.round) {
         // fn(): the running services in key order, restamped now; lane tl holds services tl + T*i
         const bool refresh = (d.now - d.p.alive_broadcast_interval_ns) > hs.last_bcast_ns;  // (:547)
         bool run[SPL], isnew[SPL], inc[SPL];
@@ -369,7 +376,7 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
           const int lslot = stores ? list_alloc<T>(d, idx, hs.arena_used, lead) : -1;
           if (lead) a.c[C_SENDJOBS]++;
           if (!stores) {
-            push_job_r(d, a, o, hs, make_job(0, 0, meta_of(GX_JOB_SEND, 0, npass)), lead);
+            push_job_r(d, a, o, hs, make_job(0, GX_LIST_NONE, meta_of(GX_JOB_SEND, 0, npass)), lead);
           } else if (lslot < 0) {
             if (lead) a.c[C_LDROP]++;
             push_job_r(d, a, o, hs, make_job(0, 0, meta_of(GX_JOB_LOST, 0, 1)), lead);
@@ -441,7 +448,7 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
           hs.flags |= 1u;
         }
       }
-      const bool tick = !(hs.flags & 2u) && hs.bt_next <= d.round;
+      const bool tick = !(hs.flags & 2u) && !(lm && (hs.flags & 1u)) && hs.bt_next <= d.round;
       if (lead) {
         d.tick[idx] = tick ? 1 : 0;
         if (tick) {
@@ -711,12 +718,18 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
 
 // The rest of a BroadcastTombstones tick on its own, for rounds where other phases push to the
 // FIFO between the scan and the send (failure detector, storm); otherwise k_send runs it.
+// Then the ExpireServer calls that waited for the host's lock (run_pending_expires), ending the
+// owner phase.
 __global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
   Acc a;
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < d.Hl && d.tick[idx]) {
     uint32_t n = d.scan_cnt[idx];
     bt_finish(d, a, d.lo + idx, d.hs[idx].running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
+  }
+  if (idx < d.Hl && d.pexp) {
+    const uint32_t lw = d.hs[idx].lock;
+    if ((lw & GX_LOCK_PENDING_EXPIRE) && !locked_in(d, lw) && !departed(d, d.lo + idx)) run_pending_expires(d, a, d.lo + idx);
   }
   acc_flush(d, a);
 }
@@ -727,6 +740,20 @@ __global__ __launch_bounds__(256) void k_bt_finish(Dev d) {
 // owner's presence mask and liveness in LDS, tombstone the live owners' present slots, and
 // compact the EXPIRE jobs in owner order.
 #define STORM_TILE 1024
+// A locked viewer (gx.h lock_model): its ExpireServer calls for owners [lo, hi) wait for the lock
+// (pexp bits; run_pending_expires at its first unlocked round). Block-wide, one word per thread.
+GXD void storm_defer(const Dev &d, uint32_t vi, uint32_t lo, uint32_t hi) {
+  uint32_t *w = &d.pexp[(size_t)vi * d.PW];
+  for (uint32_t k = (lo >> 5) + threadIdx.x; hi > lo && k <= (hi - 1) >> 5; k += blockDim.x) {
+    const uint32_t a = k * 32 > lo ? k * 32 : lo, b = k * 32 + 32 < hi ? k * 32 + 32 : hi;
+    const uint32_t m = (b - a == 32 ? ~0u : ((1u << (b - a)) - 1u)) << (a & 31);
+    w[k] |= m;
+  }
+  if (threadIdx.x == 0) {
+    d.hs[vi].lock |= GX_LOCK_PENDING_EXPIRE;
+    ctr_atomic(d, C_EXP_DEFER, hi - lo);
+  }
+}
 template <bool EV>
 __global__ __launch_bounds__(256) void k_storm(Dev d) {
   __shared__ unsigned long long s_mask[STORM_TILE];
@@ -738,6 +765,10 @@ __global__ __launch_bounds__(256) void k_storm(Dev d) {
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
+  if (d.p.lock_model && locked_in(d, h->lock)) {  // block-uniform
+    storm_defer(d, vi, lo, hi);
+    return;
+  }
   const uint32_t tail0 = h->fifo_tail, st0 = h->fifo_stored, room = fifo_room(d, h->fifo_head, tail0, st0);
   uint32_t jobs = 0, n_ev = 0;
   unsigned long long c_wr = 0, c_chg = 0;
@@ -854,6 +885,10 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   uint32_t half = d.H / 2;
   uint32_t lo = v < half ? half : 0, hi = v < half ? d.H : half;
   gx_host_state *h = &d.hs[vi];
+  if (d.p.lock_model && locked_in(d, h->lock)) {  // block-uniform
+    storm_defer(d, vi, lo, hi);
+    return;
+  }
   const uint32_t tail0 = h->fifo_tail, st0 = h->fifo_stored, room = fifo_room(d, h->fifo_head, tail0, st0);
   const uint32_t tail0q = tail0 % d.Q;  // the tail's ring position (jobs land at tail0q + pos < 2Q)
   uint32_t jobs = 0, n_ev = 0;
@@ -1112,6 +1147,7 @@ struct PlanCall {
   uint32_t x, key;    // packet entry, global packet key
   uint32_t peer;      // receiver (global id)
   uint32_t lpre;      // records of the chunk's earlier calls
+  uint32_t lk;        // the receiver (on this shard) holds the ServicesState lock this round
 };
 static_assert(sizeof(PlanCall) >= 17 * sizeof(uint32_t), "a PlanCall slot holds a team's 16 peers and their count");
 #define GX_NOSLOT 0xffffffffu  // inbox header slot: the records are in the message entry
@@ -1160,6 +1196,16 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   uint32_t j = 0, n = 0;
   bool stop = np == 0;
   unsigned fm = 0, fs = 0;
+  // the receivers' ServicesState lock this round (gx.h lock_model): bit j = peer j, on this shard,
+  // holds it. A locked receiver's records all go to its pipeline (k_merge_seg), so they are stored
+  // unfiltered and the receiver counts them; with lock_model = 0 they merge and are counted as locked.
+  uint32_t lkm = 0;
+  for (uint32_t j0 = 0; j0 < np; j0 += T) {
+    const uint32_t jj = j0 + tl;
+    const bool lk = jj < np && peers[jj] - d.lo < d.Hl && host_locked(d, peers[jj]);
+    lkm |= (uint32_t)((__ballot(lk) >> (tw * T)) & tmask) << j0;
+  }
+  const bool lmod = d.p.lock_model != 0;
   while (!stop) {
     // ---- 1. plan up to PLAN_CH calls (control state only)
     uint32_t nc = 0, tot = 0;
@@ -1174,6 +1220,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       c.push = 0;
       c.peer = peers[j];
       c.row = c.peer - d.lo < d.Hl ? &d.view[(size_t)(c.peer - d.lo) * d.R] : nullptr;
+      c.lk = (lkm >> j) & 1u;
       c.x = idx * d.KE + j * d.NG + n;
       c.key = u * d.KE + j * d.NG + n;
       bool empty = false;
@@ -1257,8 +1304,13 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
           a.c[C_RECSENT] += l;
           // records read from a list or the ring, and the receiver slots the filter reads
           const uint32_t lb = l < c.m ? l : c.m;
-          kb += 16ull * ((c.kind == GX_JOB_SEND ? lb : 0u) + (l - lb)) + (c.row ? 8ull * l : 0ull);
-          if (c.row) fm += l;
+          const bool filt = c.row && !(lmod && c.lk);
+          kb += 16ull * ((c.kind == GX_JOB_SEND ? lb : 0u) + (l - lb)) + (filt ? 8ull * l : 0ull);
+          if (filt) fm += l;
+          if (c.lk) {
+            a.locked = true;
+            if (!lmod) a.c[C_LOCKED_MERGES] += l;
+          }
         }
       }
       c.l = l;
@@ -1345,8 +1397,9 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         const uint32_t k = ck[q];
         const PlanCall &c = pl[k];
         const bool valid = f < tot;
+        const bool filt = c.row && !(lmod && c.lk);
         bool live = valid;
-        if (valid && c.row) {
+        if (valid && filt) {
           const int64_t ts = ts_of(w[q]);
           const bool stale = ts < t_stale;
           const bool gc = st_of(w0[q]) == GX_TOMBSTONE && ts_of(w0[q]) < t_gc;
@@ -1360,14 +1413,14 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         uint32_t cbk = 0;
 #pragma unroll
         for (int kk = 1; kk < PLAN_CH; kk++) cbk = (uint32_t)kk == k ? cb[kk] : cbk;
-        const uint32_t rank = c.row ? run + (uint32_t)__popcll(lm & ((1ull << tl) - 1ull)) - cbk : f - c.lpre;
+        const uint32_t rank = filt ? run + (uint32_t)__popcll(lm & ((1ull << tl) - 1ull)) - cbk : f - c.lpre;
         if (live) {
           grec g;
           g.w = w[q];
           g.r = r[q];
           g.pad = 0;
           gst_rec(&d.msg[(size_t)c.x * cap + rank], g);
-          if (c.row) gst(&d.msg_w0[(size_t)c.x * cap + rank], w0[q]);
+          if (filt) gst(&d.msg_w0[(size_t)c.x * cap + rank], w0[q]);
         }
         run += (uint32_t)__popcll(lm);
       }
@@ -1387,8 +1440,8 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       if (!c.row) stored = c.l;  // another shard's receiver filters on arrival (k_inbox_unpack)
       d.msg_len[c.x] = stored;
       d.msg_dst[c.x] = c.peer;
-      if (c.row && stored) {
-        inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, GX_NOSLOT_W0);
+      if (c.row && stored) {  // a locked receiver reads its slots itself (no forwarded words)
+        inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, lmod && c.lk ? GX_NOSLOT : GX_NOSLOT_W0);
         flag_live(d, rv, stored);
       }
       stored_all = stored + ((c.row && stored) ? 2u : 0u);  // a header and its count ~ 2 records
@@ -1438,10 +1491,19 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       d.msg_len[(size_t)idx * d.KE + j] = 0;
       d.msg_key[(size_t)idx * d.KE + j] = u * d.KE + j;
     }
-    if (tick) {  // departed hosts never tick
+    // the ExpireServer calls that waited for the host's lock end its owner phase (gx.h lock_model)
+    const bool pend = do_bt && d.pexp && (hs.lock & GX_LOCK_PENDING_EXPIRE) && !locked_in(d, hs.lock) &&
+                      (!X || !departed(d, u));
+    if (tick || pend) {  // departed hosts never tick
       if (lane == 0) {
         const uint32_t n = d.scan_cnt[idx];
-        bt_finish(d, a, u, hs.running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
+        if (tick) bt_finish(d, a, u, hs.running, &d.scan_list[(size_t)idx * d.L], n < d.L ? n : d.L);
+        if (pend) {
+          run_pending_expires(d, a, u);
+          // other hosts' senders may have read this view's slots before the calls rewrote them: the
+          // merge reads its slots itself (as for a view scanned this round), not the forwarded words
+          d.tick[idx] = 2;
+        }
       }
       __threadfence_block();  // the team reads the host's bookkeeping below
       hs = *h;
@@ -1453,6 +1515,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       uint32_t *peers = reinterpret_cast<uint32_t *>(&pl[PLAN_CH]);  // the team's peers (k_send's prologue)
       const uint32_t np = peers[16];
       send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb, (pre && fwd.pf0 == hs.fifo_head) ? fwd.npf : 0u);
+      hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1);  // the lock for the next round
       if (lane == 0) *h = hs;
     } else if (!X || !departed(d, u)) {
       const bool fd = X && d.p.fd_enable;
@@ -1502,15 +1565,24 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
             call = lim > d.p.overhead_bytes;
           }
           grec *pk = pos < d.DR ? &d.in_rec[((size_t)(pj - d.lo) * d.DR + pos) * cap] : &d.msg[x * cap];
+          // the receiver holds the ServicesState lock this round (gx.h lock_model): its records all go
+          // to its pipeline unfiltered (k_merge_seg counts them); lock_model = 0 counts them as locked
+          const bool rlk = pos != 0xffffffffu && host_locked(d, pj);
           if (call) {
             const uint32_t q = hs.fifo_head - head0;
             const bool pf = q < n0 && q < (uint32_t)T;
-            const bool filt = d.sfilt && pos != 0xffffffffu;  // a packet registered in a local inbox
+            // a packet registered in a local inbox
+            const bool filt = d.sfilt && pos != 0xffffffffu && !(rlk && d.p.lock_model);
             l = get_broadcasts_team<T>(d, a, u, hs, cap, pk, lim, d.p.overhead_bytes, pf ? &pjs[q] : nullptr,
                                        filt ? &d.view[(size_t)(pj - d.lo) * d.R] : nullptr, pj - d.lo);
           }
+          if (rlk && l && lane == 0) {
+            a.locked = true;
+            if (d.p.lock_model) flag_live(d, pj - d.lo, l);  // routes the receiver (k_merge_seg)
+            else a.c[C_LOCKED_MERGES] += l;
+          }
           called = j + 1;
-          if (lane == 0) kb += 16 + 32ull * l + (filt_used(d, pos) ? 8ull * l : 0);  // job, records in/out, slots
+          if (lane == 0) kb += 16 + 32ull * l + (filt_used(d, pos) && !(rlk && d.p.lock_model) ? 8ull * l : 0);  // job, records in/out, slots
           const bool live = l || nf;
           if (lane == 0) {
             d.msg_len[x] = ok ? l : 0;
@@ -1528,6 +1600,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       // slots claimed for peers the round stopped before (gossip() returned at an empty packet)
       if (early && lane >= called && my_pos != 0xffffffffu)
         inbox_header(d, peers[lane] - d.lo, my_pos, u * d.KE + lane, (uint32_t)((size_t)idx * d.KE + lane), 0);
+      hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1);  // the lock for the next round
       if (lane == 0) *h = hs;
     }
   }
@@ -1645,12 +1718,41 @@ GXD uint64_t bitonic64(uint64_t x, uint32_t lane) {  // ascending across the 64 
 GXD uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
 
 // Overflowed inbox: one lane folds every packet in key order through the scalar path and
-// flushes its own counters.
-GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
+// flushes its own counters. The ServicesState lock (gx.h lock_model): a locked receiver appends the
+// records to its pipeline instead; an unlocked one with nbuf queued records merges those first.
+GXD void merge_inbox_serial(const Dev &d, uint32_t vi, bool lockd = false, uint32_t nbuf = 0) {
   Acc a;
   const uint32_t v = d.lo + vi, cnt = d.in_cnt[vi];
   int64_t after = -1;
   unsigned long long recs = 0;
+  grec *lkb = d.lkb ? &d.lkb[(size_t)vi * d.C] : nullptr;
+  if (lockd) {
+    uint32_t nb = GX_LOCK_BUF(d.hs[vi].lock);
+    for (uint32_t n = 0; n < cnt; n++) {
+      const uint4 h = inbox_next(d, vi, after);
+      after = h.x;
+      const grec *pk = packet_recs(d, vi, h.w, h.y);
+      for (uint32_t x = 0; x < h.z; x++) {
+        if (nb < d.C) {
+          lkb[nb++] = pk[x];
+          a.c[C_LOCK_BUF]++;
+        } else {
+          a.c[C_LOCK_DROP]++;
+        }
+      }
+      recs += h.z;
+    }
+    d.hs[vi].lock = (d.hs[vi].lock & ((1u << GX_LOCK_BUF_SHIFT) - 1u)) | nb << GX_LOCK_BUF_SHIFT;
+    kbytes(d, GX_K_MERGE, 32ull * recs + 16ull * cnt + 4, 0);
+    for (int i = 0; i < C_NCTR; i++) ctr_atomic(d, i, a.c[i]);
+    return;
+  }
+  for (uint32_t k = 0; k < nbuf; k++) add_entry(d, a, v, lkb[k], SRC_GOSSIP);  // the pipeline drains
+  const unsigned m0 = a.c[C_GOSSIP_MERGES], s0 = a.c[C_STALE];
+  if (nbuf) {
+    a.c[C_LOCK_DRAIN] += nbuf;
+    d.hs[vi].lock &= (1u << GX_LOCK_BUF_SHIFT) - 1u;
+  }
   for (uint32_t n = 0; n < cnt; n++) {
     const uint4 h = inbox_next(d, vi, after);
     after = h.x;
@@ -1658,7 +1760,9 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi) {
     for (uint32_t x = 0; x < h.z; x++) add_entry(d, a, v, pk[x], SRC_GOSSIP);
     recs += h.z;
   }
-  a.c[C_GOSSIP_MERGES] = a.c[C_STALE] = 0;  // counted by the senders
+  recs += nbuf;
+  a.c[C_GOSSIP_MERGES] = m0;  // the packets' merges and stale drops: counted by the senders
+  a.c[C_STALE] = s0;
   kbytes(d, GX_K_MERGE, 28ull * recs + 16ull * cnt + 4, recs);
   for (int i = 0; i < C_NCTR; i++) ctr_atomic(d, i, a.c[i]);
   if (a.changed) mark_change(d);
@@ -1701,9 +1805,19 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
   const uint32_t npre = d.DI < INBOX_PREFETCH ? d.DI : INBOX_PREFETCH;
   uint4 hd = lane < npre ? d.in_hdr[(size_t)vi * d.DI + lane] : make_uint4(0u, 0u, 0u, 0u);
   const uint32_t deg = d.in_cnt[vi];
-  if (deg == 0) return;
+  // the ServicesState lock (gx.h lock_model): a locked receiver appends its records to its pipeline
+  // (lkb) instead of merging them; an unlocked one with nbuf records queued there merges those
+  // first, as the first nbuf records of its fold
+  uint32_t lw = 0, nbuf = 0;
+  bool lockd = false;
+  if (d.p.lock_model) {
+    lw = __builtin_amdgcn_readfirstlane(d.hs[vi].lock);
+    lockd = locked_in(d, lw);
+    nbuf = lockd || departed(d, v) ? 0u : GX_LOCK_BUF(lw);
+  }
+  if (deg == 0 && nbuf == 0) return;
   if (deg > d.DI) {
-    if (lane == 0) merge_inbox_serial(d, vi);
+    if (lane == 0) merge_inbox_serial(d, vi, lockd, nbuf);
     return;
   }
   // wide inbox (more than 64 packets, GossipMessages > 1): the headers are ranked and staged in
@@ -1792,13 +1906,20 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     if (lane < deg) L.pst[lane] = pstart;
     wave_sync();
   }
+  const grec *lkb = nbuf ? &d.lkb[(size_t)vi * d.C] : nullptr;
+  const uint32_t ntot = nbuf + total;  // the fold: the drained pipeline, then the packets
   auto load_recs = [&](uint32_t tb, grec &g, uint32_t &fslot, uint64_t &fw0) {
-    const uint32_t i = tb + lane;
+    uint32_t i = tb + lane;
     g.w = 0;
     g.r = INV;
     g.pad = 0;
     fw0 = 0;
     fslot = 0;
+    if (i < nbuf) {  // a queued record reads its slot (fslot 0: no forwarded word)
+      g = gld_rec(&lkb[i]);
+      return;
+    }
+    i -= nbuf;
     if (i < total) {  // hop 2
       uint32_t lo = 0, hi = deg;
       while (hi - lo > 1) {
@@ -1813,7 +1934,27 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
       if (hk.w == GX_NOSLOT_W0) fw0 = d.msg_w0[(size_t)hk.y * d.p.packet_cap + off];
     }
   };
-  const bool track = total > 64;  // wave-uniform: later tiles consult the written-key set
+  if (lockd) {  // the pipeline takes the records in arrival order while it has room (gx.h lock_model)
+    const uint32_t nb0 = GX_LOCK_BUF(lw), room_l = d.C > nb0 ? d.C - nb0 : 0u;
+    const uint32_t keep = total < room_l ? total : room_l;
+    grec *dst = &d.lkb[(size_t)vi * d.C + nb0];
+    for (uint32_t t0 = 0; t0 < keep; t0 += 64) {
+      grec g;
+      uint32_t fs;
+      uint64_t fw;
+      load_recs(t0, g, fs, fw);
+      if (t0 + lane < keep) gst_rec(&dst[t0 + lane], g);
+    }
+    if (lane == 0) {
+      d.hs[vi].lock = (lw & ((1u << GX_LOCK_BUF_SHIFT) - 1u)) | (nb0 + keep) << GX_LOCK_BUF_SHIFT;
+      ctr_atomic(d, C_LOCK_BUF, keep);
+      ctr_atomic(d, C_LOCK_DROP, total - keep);
+      kbytes(d, GX_K_MERGE, 32ull * keep + 16ull * deg + 4, 0);  // records in and out, headers
+    }
+    wave_sync();
+    return;
+  }
+  const bool track = ntot > 64;  // wave-uniform: later tiles consult the written-key set
   if (track)
     for (uint32_t q = lane; q < MSET; q += 64) L.wset[q] = MSET_EMPTY;
   uint32_t nset = 0;  // keys in the set (wave-uniform)
@@ -1824,14 +1965,15 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
   gn.w = 0;
   gn.r = INV;
   gn.pad = 0;
-  if (64 < total) load_recs(64, gn, fsn, fwn);
+  if (64 < ntot) load_recs(64, gn, fsn, fwn);
   wave_sync();
   unsigned long long *kpm = kprof_merge(d);  // diagnostics: phase cycles of the whole-wave tiles
   unsigned long long ph[5] = {0, 0, 0, 0, 0}, tk = 0;
-  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+  uint32_t c_dstale = 0;  // stale drops among the drained records (the packets' counted by the senders)
+  for (uint32_t t0 = 0; t0 < ntot; t0 += 64) {
     if (kpm) tk = __builtin_amdgcn_s_memtime();
     const uint32_t i = t0 + lane;
-    const bool valid = i < total;
+    const bool valid = i < ntot;
     uint32_t key = INV;
     uint64_t val = 0, w0 = 0;
     bool rd = false;  // this record reads its slot (hop 3)
@@ -1851,7 +1993,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     gnn.w = 0;
     gnn.r = INV;
     gnn.pad = 0;
-    if (t0 + 128 < total) load_recs(t0 + 128, gnn, fsnn, fwnn);
+    if (t0 + 128 < ntot) load_recs(t0 + 128, gnn, fsnn, fwnn);
     c_merge += valid;
     c_rd += rd;  // view slots read by the receiver
     // A record that is stale, or no newer than the slot's word at the start of the tile, is a
@@ -1862,6 +2004,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     const bool stale0 = valid && ts_of(val) < d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
     const bool live = valid && !stale0 && (st_of(w0) == GX_ABSENT || ts_of(val) > ts_of(w0));
     c_stale += stale0;
+    c_dstale += stale0 && i < nbuf;
     const bool any_live = __ballot(live) != 0;
     if (kpm) {  // [8] records and slots in (waits), [9] sort, [10] fold + writes, [11] the rest, [12] tiles
       const unsigned long long x = __builtin_amdgcn_s_memtime();
@@ -1994,6 +2137,10 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     for (int q = 0; q < 5; q++) atomicAdd(&kpm[8 + q], ph[q]);
   const unsigned long long m_merge = wave_sum(c_merge), m_acc = wave_sum(c_acc), m_rd = wave_sum(c_rd),
                            m_wr = wave_sum(c_wr), m_chg = wave_sum(c_chg);
+  if (nbuf) {
+    const unsigned long long m_ds = wave_sum(c_dstale);
+    if (lane == 0) ctr_atomic(d, C_STALE, m_ds);
+  }
   (void)c_stale;  // stale drops: counted by the senders
   mexp = wave_min(mexp);
   if (lane == 0) {
@@ -2005,6 +2152,11 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     if (vlc_set) d.vlc[vi] = vlc_ts;
     if (evk >= 0) d.ev_cnt[evk] = ev0 + n_ev;
     ctr_atomic(d, C_CHG, m_chg);
+    if (nbuf) {  // the drained pipeline: AddServiceEntry calls of this round
+      d.hs[vi].lock = lw & ((1u << GX_LOCK_BUF_SHIFT) - 1u);
+      ctr_atomic(d, C_GOSSIP_MERGES, nbuf);
+      ctr_atomic(d, C_LOCK_DRAIN, nbuf);
+    }
     // 12 B per record (word + key) + 8 B per slot read / written + 16 B per stored retransmit job
     // + 16 B per inbox header + the count (merges and stale drops: counted by the senders)
     kbytes(d, GX_K_MERGE, 12ull * m_merge + 8ull * (m_rd + m_wr) + 16ull * ok + 16ull * deg + 4, m_merge);
@@ -2257,7 +2409,14 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
     if (t) d.mrec[vi] = 0;  // the senders count next round's
     if (lane < (uint32_t)NR)
       for (int q = 0; q < 4; q++) s_it[lane][q] = MERGE_NONE;
-    const bool sm = t && t <= 16, md = t > 16 && t <= 32, lg = t > 32;
+    // the ServicesState lock (gx.h lock_model): a locked receiver with records, and an unlocked one
+    // whose pipeline holds records to drain, take the whole-wave path (merge_receiver)
+    bool lkw = false;
+    if (d.p.lock_model && lane < (uint32_t)NR && vi < d.Hl) {
+      const uint32_t lw = d.hs[vi].lock;
+      lkw = locked_in(d, lw) ? t != 0 : (GX_LOCK_BUF(lw) != 0 && !departed(d, d.lo + vi));
+    }
+    const bool sm = !lkw && t && t <= 16, md = !lkw && t > 16 && t <= 32, lg = lkw || t > 32;
     const uint64_t bs = __ballot(sm), bm = __ballot(md), bl = __ballot(lg), below = (1ull << lane) - 1ull;
     const uint32_t nl = (uint32_t)__popcll(bl), nm = (uint32_t)__popcll(bm), ns = (uint32_t)__popcll(bs);
     const uint32_t nim = (nm + 1) / 2, nis = (ns + 3) / 4;
@@ -2445,10 +2604,12 @@ GXD void dec_pair_u(const uint64_t *enc, uint32_t s, bool v0, bool v1, uint64_t 
     if ((e ? v1 : v0) && !((om >> b) & 1ull)) w[e] = enc[16 + pre + __popcll(nm & ((2ull << b) - 1ull))];
   }
 }
+// locked: a side holds the ServicesState lock and the pair runs anyway (lock_model = 0): its merges
+// are counted as locked (gx.h gx_stats.locked_merges).
 template <bool VEC, int PF = 1, bool NT = false, bool EV = false, bool NTS = false>
 GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long long *s_wave,
                  unsigned long long *s_red, const uint64_t *ext = nullptr, bool count_ex = false,
-                 const XSrc *xs = nullptr) {
+                 const XSrc *xs = nullptr, bool locked = false) {
   uint64_t *A = vrow(d, a);
   uint64_t *B = xs ? A : ext ? const_cast<uint64_t *>(ext) : vrow(d, b);
   gx_host_state *ha = hst(d, a), *hb = both ? hst(d, b) : ha;
@@ -2796,6 +2957,7 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   unsigned long long cw = wave_sum((unsigned long long)c_wr);
   if ((t & 63) == 0) kbytes(d, GX_K_AE, 8ull * cw, 0);
   block_ctr(d, C_AE_MERGES, c_merge, s_red);
+  if (locked) block_ctr(d, C_LOCKED_MERGES, c_merge, s_red);  // block-uniform
   block_ctr(d, C_AE_ACC, c_acc, s_red);
   block_ctr(d, C_STALE, c_stale, s_red);
   if (t == 0) {
@@ -2819,6 +2981,18 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
   }
 }
 
+// The ServicesState lock of a push-pull pair whose hosts are both here (gx.h lock_model): a locked
+// side's LocalState blocks behind the pending writer, so the exchange does not run (returns true:
+// skip it); with lock_model = 0 it runs and `locked` says its merges are counted. Block-uniform.
+GXD bool ae_lock_skip(const Dev &d, uint32_t a, uint32_t b, bool &locked) {
+  locked = host_locked(d, a) || host_locked(d, b);
+  if (!locked) return false;
+  if (threadIdx.x == 0) {
+    atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
+    if (d.p.lock_model) ctr_atomic(d, C_AE_LOCKED, 1);
+  }
+  return d.p.lock_model != 0;
+}
 template <bool VEC, bool EV, int PF, bool NT, bool NTS = false>
 GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
   __shared__ unsigned long long s_wave[4];
@@ -2847,7 +3021,9 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
     if (ok && d.p.fd_enable) ok = reach(d, a, b) && memp(d, a, b)->state == GX_M_ALIVE;
     if (!ok) return;
   }
-  ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red);
+  bool locked;
+  if (ae_lock_skip(d, a, b, locked)) return;
+  ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red, nullptr, false, nullptr, locked);
   if (kp && threadIdx.x == 0) kp[2 * blockIdx.x + 1] = wall_clock64();
 }
 
@@ -2890,9 +3066,11 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
   int32_t k = prow[i];
   if (k < 0 && d.p.fd_enable && !(reach(d, pa[i], pb[i]) && memp(d, pa[i], pb[i])->state == GX_M_ALIVE))
     return;  // memberlist pushPull: the initiator (pa) needs the path and sees the partner alive
-  if (k >= 0 && skip[k]) return;  // the same decision for a cross-shard pair (digest flag)
+  if (k >= 0 && (skip[k] & 1u)) return;  // the same decision for a cross-shard pair (digest flag)
   if (k < 0) {
-    ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], true, s_wave, s_red);
+    bool locked;
+    if (ae_lock_skip(d, pa[i], pb[i], locked)) return;
+    ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], true, s_wave, s_red, nullptr, false, nullptr, locked);
   } else {
     const uint32_t nl = in.nlead[k];
     const uint8_t *rm = in.ret + in.rioff[k];
@@ -2904,7 +3082,7 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
     xs.fmask = in.fmask + (size_t)k * in.nmw;
     xs.lt = in.lt + (size_t)k * in.nblk;
     xs.bcnt = in.bcnt + (size_t)k * in.nblk;
-    ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, nullptr, pcount[i] != 0, &xs);
+    ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], false, s_wave, s_red, nullptr, pcount[i] != 0, &xs, (skip[k] & 2u) != 0);
   }
 }
 template <bool VEC>
@@ -2979,7 +3157,10 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
     hdr[0] = pair_t[k];
     hdr[1] = host[k];
     hdr[2] = nblk;
-    hdr[3] = d.p.fd_enable && first[k] && ae_initiator_runs(d, host[k], other[k]) ? 1u : 0u;
+    // bit 0: with the failure detector, the initiator's decision that the pair runs; bit 1: this
+    // side's host holds the ServicesState lock this round (gx.h lock_model)
+    hdr[3] = (d.p.fd_enable && first[k] && ae_initiator_runs(d, host[k], other[k]) ? 1u : 0u) |
+             (host_locked(d, host[k]) ? 2u : 0u);
   }
   const uint64_t *row = vrow(d, host[k]);
   // software pipeline: the wave's next block is in flight while this one is hashed and reduced
@@ -3054,8 +3235,16 @@ __global__ __launch_bounds__(256) void k_ae_mask(Dev d, const uint8_t *in, const
   const uint8_t *msg = in + (size_t)k * dig_stride(d, nblk);
   const uint32_t *hdr = reinterpret_cast<const uint32_t *>(msg);
   if (threadIdx.x == 0 && (hdr[0] != pair_t[k] || hdr[2] != nblk)) atomicOr(err, 1u);
-  const bool runs = !d.p.fd_enable || (first[k] ? ae_initiator_runs(d, host[k], other[k]) : (hdr[3] & 1u) != 0);
-  if (threadIdx.x == 0) skip[k] = runs ? 0 : 1;
+  bool runs = !d.p.fd_enable || (first[k] ? ae_initiator_runs(d, host[k], other[k]) : (hdr[3] & 1u) != 0);
+  // the ServicesState lock (gx.h lock_model): a side that holds it fails the exchange; with
+  // lock_model = 0 the pair runs and its merges count as locked (skip bit 1)
+  const bool lk = runs && (host_locked(d, host[k]) || (hdr[3] & 2u) != 0);
+  if (lk && threadIdx.x == 0) {
+    atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
+    if (d.p.lock_model && first[k]) ctr_atomic(d, C_AE_LOCKED, 1);
+  }
+  if (lk && d.p.lock_model) runs = false;
+  if (threadIdx.x == 0) skip[k] = (runs ? 0 : 1) | (lk && runs ? 2 : 0);
   unsigned long long n = 0, bl = 0, bi = 0;  // n: lead count | follow count << 32
   for (uint32_t w = threadIdx.x; w < nmw; w += blockDim.x) {
     uint32_t lb = 0, fb = 0;
@@ -3681,7 +3870,14 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
     return;
   }
   const uint32_t vi = dst - d.lo;
-  if (d.sfilt) {  // the receiver's filter: only live records are kept (compacted, see send_planned)
+  // the receiver holds the ServicesState lock this round (gx.h lock_model): every record goes to
+  // its pipeline unfiltered (k_merge_seg); lock_model = 0 merges them and counts them as locked
+  const bool rlk = host_locked(d, dst);
+  if (rlk && threadIdx.x == 0 && len) {
+    atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
+    if (!d.p.lock_model) ctr_atomic(d, C_LOCKED_MERGES, len);
+  }
+  if (d.sfilt && !(rlk && d.p.lock_model)) {  // the receiver's filter: only live records are kept (compacted, see send_planned)
     const uint64_t *row = &d.view[(size_t)vi * d.R];
     const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
     const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
@@ -3760,6 +3956,7 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
     d.msg_len[e] = len;
     if (fcap) d.fd_len[e] = nfd;
     if (len || nfd) inbox_header(d, vi, pos, key, (uint32_t)e, len);
+    if (rlk && d.sfilt && len) flag_live(d, vi, len);  // routes the locked receiver
   }
 }
 
@@ -3839,6 +4036,17 @@ __global__ void k_digest(Dev d, uint64_t *out) {
       h = feed(h, g.r);
     }
   }
+  h = feed(h, 0x10C6);  // the lock buffer, then the owners whose ExpireServer waits (gx.h lock_model)
+  for (uint32_t k = 0; k < GX_LOCK_BUF(s.lock); k++) {
+    const grec g = d.lkb[(size_t)v * d.C + k];
+    h = feed(h, g.w);
+    h = feed(h, g.r);
+  }
+  if (s.lock & GX_LOCK_PENDING_EXPIRE)
+    for (uint32_t k = 0; k < d.PW; k++) {
+      const uint32_t x = d.pexp[(size_t)v * d.PW + k];
+      if (x) h = feed(h, (uint64_t)k << 32 | x);
+    }
   h = feed(h, s.flags);
   h = feed(h, (uint64_t)s.bs_next);
   h = feed(h, (uint64_t)s.bt_next);
@@ -3950,7 +4158,7 @@ __global__ void k_api_send(Dev d, uint32_t v, const grec *list, uint32_t n, uint
     a.c[C_SENDJOBS]++;
     const uint32_t m = n < d.L ? n : d.L;
     if (!fifo_stores(d, v)) {  // deferred: no list
-      push_job(d, a, v, make_job(0, 0, meta_of(GX_JOB_SEND, 0, np)));
+      push_job(d, a, v, make_job(0, GX_LIST_NONE, meta_of(GX_JOB_SEND, 0, np)));
     } else {
       int slot = alloc_list(d, a, v);
       if (slot >= 0) {
@@ -3967,6 +4175,8 @@ __global__ void k_api_bs(Dev d, uint32_t v, const grec *list, uint32_t n) {
   if (threadIdx.x == 0) {
     uint64_t inc;
     bs_body_list(d, a, v, list, n, inc);
+    gx_host_state *h = hst(d, v);
+    h->lock = lock_snap(h->lock, h->flags, d.round);  // a nil blocks the looper from now on
   }
   acc_flush(d, a);
 }
@@ -3975,6 +4185,8 @@ __global__ void k_api_bt(Dev d, uint32_t v, uint64_t running, const grec *others
   if (threadIdx.x == 0) {
     uint32_t n = *n_others;
     bt_finish(d, a, v, running, others, n < d.L ? n : d.L);
+    gx_host_state *h = hst(d, v);
+    h->lock = lock_snap(h->lock, h->flags, d.round);
   }
   acc_flush(d, a);
 }
@@ -3988,6 +4200,7 @@ __global__ void k_api_getb(Dev d, uint32_t v, uint32_t limit, grec *out, uint32_
   Acc a;
   gx_host_state hs = *hst(d, v);
   uint32_t l = get_broadcasts_team<64>(d, a, v, hs, limit, out, limit_bytes, overhead);
+  hs.lock = lock_snap(hs.lock, hs.flags, d.round);  // a looper's nil may have been taken
   if (threadIdx.x == 0) {
     *hst(d, v) = hs;
     *n_out = l;

@@ -23,6 +23,15 @@ from .abi import Engine, GxParams, default_params
 FIRST_ROUND_STATS = ("first_drop_round", "first_locked_round")
 
 
+def planned_exchange(p: GxParams) -> bool:
+    """A gossip round exchanges fixed, seeded slot counts (gx_exchange_plan: no size collective, no
+    host wait) iff the failure detector is off and GossipMessages is at most one message per target
+    (0 and 1 both mean one). Past one message the plan reserves GossipMessages slots per sampled peer
+    and ships mostly padding (GM 15: ~85 MB per rank per round at cfg 5, G = 8), so the exact sizes
+    are gathered instead."""
+    return not p.fd_enable and p.gossip_messages <= 1
+
+
 def _ptr(t: torch.Tensor) -> int:
     return t.data_ptr() if t.numel() else 0
 
@@ -85,6 +94,7 @@ class LocalShards:
                 p.device = self.device.index or 0
             self.shards.append(_Shard(p, lib, self.device))
         self.wire = WireBytes(self.shards[0].e)
+        self.exchange_paths = {"planned": 0, "sized": 0}  # gossip rounds per exchange path (planned_exchange)
         self.trace_ae = False  # keep each push-pull round's digest and delta inboxes (host copies)
         self.ae_trace = []
 
@@ -120,11 +130,11 @@ class LocalShards:
         return t.cpu().numpy().astype(np.uint64)
 
     def run_rounds(self, n: int):
-        p0 = self.shards[0].e.params  # sizes from the seeded plan (gx_exchange_plan); see DistShard.run_rounds
-        planned = not p0.fd_enable and p0.gossip_messages <= 1
+        planned = planned_exchange(self.shards[0].e.params)
         for _ in range(n):
             for s in self.shards:
                 s.e.round_send()
+            self.exchange_paths["planned" if planned else "sized"] += 1
             if planned:
                 plan = self.shards[0].e.exchange_plan()
                 inb = self._exchange(lambda s: plan[s.e.params.shard_id].copy(),
@@ -202,6 +212,7 @@ class DistShard:
         self.s = _Shard(p, lib, self.device)
         self.e = self.s.e
         self.wire = WireBytes(self.e)
+        self.exchange_paths = {"planned": 0, "sized": 0}  # gossip rounds per exchange path (planned_exchange)
         # gloo has no device all-to-all / all-gather: a gloo group over device shards (the one-GPU
         # rehearsal of the RCCL path in tests/test_gpu_dist.py) stages collectives through the host
         self.stage = self.device.type == "cuda" and dist.get_backend(group) == "gloo"
@@ -299,12 +310,10 @@ class DistShard:
 
     def run_rounds(self, n: int):
         e = self.e
-        # sizes from the seeded plan: no host wait in gossip rounds. The plan reserves GossipMessages
-        # slots per sampled peer, so past one message per round it ships mostly padding (GM 15:
-        # ~85 MB per rank per round at cfg 5, G = 8): there the exact sizes are gathered instead.
-        planned = not e.params.fd_enable and e.params.gossip_messages <= 1  # 0: one message
+        planned = planned_exchange(e.params)  # sizes from the seeded plan: no host wait
         for _ in range(n):
             e.round_send()
+            self.exchange_paths["planned" if planned else "sized"] += 1
             if planned:
                 x = self._exchange_planned(e.exchange_plan(), e.outbox_pack_planned)
             else:

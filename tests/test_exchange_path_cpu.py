@@ -1,0 +1,92 @@
+"""Which gossip exchange a sharded round takes (sidecar_amd.dist.planned_exchange): the planned one
+(seeded slot counts, no size collective, no host wait; gx_exchange_plan) iff the failure detector is
+off and GossipMessages is at most one message per target, 0 included. Round 4 once sent
+GossipMessages 0 down the size-gathered exchange and only a sync-debug GPU test noticed; these tests
+pin the choice on the CPU, for LocalShards and for DistShard over gloo."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+
+from sidecar_amd.abi import Engine, default_params
+from sidecar_amd.dist import LocalShards, planned_exchange
+
+CASES = [  # (params, planned)
+    (dict(gossip_messages=0), True),
+    (dict(gossip_messages=1), True),
+    (dict(gossip_messages=2), False),
+    (dict(gossip_messages=15), False),
+    (dict(gossip_messages=0, fd_enable=1), False),
+    (dict(gossip_messages=1, fd_enable=1), False),
+]
+BASE = dict(n_hosts=32, n_services=4, init_mode=2, ae_period_rounds=5, partition_start=0, partition_end=6,
+            storm_round=2, queue_cap=2048)
+
+
+@pytest.mark.parametrize("kw,planned", CASES)
+def test_planned_exchange_predicate(oracle_lib, kw, planned):
+    assert planned_exchange(default_params(oracle_lib, **dict(BASE, **kw))) is planned
+
+
+@pytest.mark.parametrize("kw,planned", CASES)
+def test_local_shards_take_the_planned_exchange(oracle_lib, kw, planned):
+    kw = dict(BASE, **kw)
+    sh = LocalShards(oracle_lib, 2, **kw)
+    calls = {"plan": 0}
+    eng = sh.shards[0].e
+    orig = eng.exchange_plan
+
+    def counted():
+        calls["plan"] += 1
+        return orig()
+
+    eng.exchange_plan = counted
+    sh.run_rounds(7)
+    assert sh.exchange_paths == ({"planned": 7, "sized": 0} if planned else {"planned": 0, "sized": 7})
+    assert calls["plan"] == (7 if planned else 0)
+    whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    whole.run_rounds(7)
+    assert sh.stats()["gossip_merges"] == whole.stats()["gossip_merges"]
+
+
+def _worker(rank, world, port, kw, q):
+    import torch.distributed as dist
+    from sidecar_amd.dist import DistShard
+    from tests.oracle_lib import load_oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = DistShard(load_oracle(), rank, world, "cpu", **kw)
+    sh.run_rounds(6)
+    q.put((rank, dict(sh.exchange_paths), sh.stats()["gossip_merges"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("gm,planned", [(0, True), (1, True), (4, False)])
+def test_dist_shard_takes_the_planned_exchange(oracle_lib, gm, planned):
+    kw = dict(BASE, gossip_messages=gm)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, kw, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {"planned": 6, "sized": 0} if planned else {"planned": 0, "sized": 6}
+    assert all(r[1] == want for r in res), res
+    whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    whole.run_rounds(6)
+    assert res[0][2] == whole.stats()["gossip_merges"]

@@ -7,7 +7,7 @@ jobs, and that the LOST accounting starts exactly where the windows diverge.
 """
 import pytest
 
-from sidecar_amd.abi import INIT_OWN, INIT_WARM, JOB_LOST, Engine, default_params
+from sidecar_amd.abi import INIT_OWN, INIT_WARM, JOB_LOST, JOB_SEND, Engine, default_params
 
 IGNORE_STATS = {"queue_deferred", "queue_drops", "first_drop_round", "list_drops"}
 
@@ -84,3 +84,45 @@ def test_lost_job_counts_and_nil_positions(oracle_lib):
     assert hs.fifo_head == hs.fifo_tail == hs.fifo_stored
     e.add_service_entry(h, (2, 1, e.now() + 9, 0))  # stored again
     assert [j.kind for j in e.queue(h)] == [2] and JOB_LOST == 5
+
+
+def _list_refs(e, h):
+    """SendServices jobs of host h that hold a list (stored window and sleep ring): slot -> length."""
+    refs = {}
+    for j in list(e.queue(h)) + [s.job for s in e.sleepers(h)]:
+        if j.kind == JOB_SEND:
+            slot, n = j.c & 0xFFFF, j.c >> 16
+            assert slot not in refs, f"two live jobs share list {slot}"
+            refs[slot] = n
+    return refs
+
+
+def test_deferred_send_holds_no_list(oracle_lib):
+    """A SendServices job queued past the stored window holds no list (gx.h GX_LIST_NONE): queueing
+    it must not release the list of a live multi-pass job (slot 0 here), and after the first LOST
+    dequeue a new list must not take that slot while its job still sleeps between passes."""
+    e = Engine(default_params(oracle_lib, n_hosts=2, n_services=4, fanout=1, init_mode=INIT_OWN, queue_cap=2,
+                              list_slots=4, alive_interval_rounds=1000, tombstone_interval_rounds=1000),
+               lib=oracle_lib)
+    now = e.now()
+    a = [(0, s, now + 1000 * s) for s in range(4)]
+    e.send_services(0, a, 3)       # stored: list 0, three passes with TOMBSTONE_RETRANSMIT sleeps
+    e.send_services(0, a[:1], 1)   # stored: list 1 (the window of 2 is full)
+    e.send_services(0, a[1:], 1)   # deferred: no list
+    assert [j.c & 0xFFFF for j in e.queue(0)] == [0, 1]
+    assert e.hosts()[0].fifo_tail - e.hosts()[0].fifo_head == 3
+    before = [x.tup() for x in e.read_list(0, 0)]
+    assert len(before) == 4
+    for r in range(40):
+        e.run_rounds(1)
+        if r == 3:  # after the LOST dequeue the window stores again: a new list is allocated
+            e.send_services(0, [(0, 0, now + 99_999)], 1)
+        refs = _list_refs(e, 0)
+        if 0 in refs:
+            assert [x.tup() for x in e.read_list(0, 0)] == before, f"round {e.round}: list 0 overwritten"
+        for slot, n in refs.items():
+            assert len(e.read_list(0, slot)) == n, f"round {e.round}: list {slot}"
+    st = e.stats()
+    assert st["queue_drops"] >= 1 and st["list_drops"] == 0
+    assert not _list_refs(e, 0)  # every pass ran; no list leaked either
+    assert all(not e.read_list(0, s) for s in range(4))

@@ -86,3 +86,15 @@ def test_push_pull_initiate_validation(oracle_lib):
                 dict(push_pull_mode=1, n_shards=2, shard_id=0)):
         with pytest.raises(GxError):
             _eng(oracle_lib, n_hosts=16, n_services=2, **bad)
+
+
+def test_round_end_bounded(oracle_lib):
+    """Rounds are 32-bit in jobs and sleepers (gx.h GX_MAX_ROUND): the sharded stepping path refuses
+    to pass the bound like gx_set_round and gx_run_rounds do."""
+    from sidecar_amd.abi import Engine, GxError, default_params
+    e = Engine(default_params(oracle_lib, n_hosts=4, n_services=2), lib=oracle_lib)
+    e.set_round((1 << 31) - 2)
+    e.round_end()
+    assert e.round == (1 << 31) - 1
+    with pytest.raises(GxError):
+        e.round_end()
