@@ -1199,11 +1199,16 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   // the receivers' ServicesState lock this round (gx.h lock_model): bit j = peer j, on this shard,
   // holds it. A locked receiver's records all go to its pipeline (k_merge_seg), so they are stored
   // unfiltered and the receiver counts them; with lock_model = 0 they merge and are counted as locked.
-  uint32_t lkm = 0;
+  // A locked receiver whose pipeline was full when the round began (its count changes only in the
+  // merge) drops every record of this round (memberlist's handoff queue): the call's packet is
+  // counted as dropped here and neither stored nor registered (bit j of fullm).
+  uint32_t lkm = 0, fullm = 0;
   for (uint32_t j0 = 0; j0 < np; j0 += T) {
     const uint32_t jj = j0 + tl;
-    const bool lk = jj < np && peers[jj] - d.lo < d.Hl && host_locked(d, peers[jj]);
+    const uint32_t lw = jj < np && peers[jj] - d.lo < d.Hl ? gld(&hst(d, peers[jj])->lock) : 0u;
+    const bool lk = locked_in(d, lw);
     lkm |= (uint32_t)((__ballot(lk) >> (tw * T)) & tmask) << j0;
+    fullm |= (uint32_t)((__ballot(lk && GX_LOCK_BUF(lw) >= d.C) >> (tw * T)) & tmask) << j0;
   }
   const bool lmod = d.p.lock_model != 0;
   while (!stop) {
@@ -1220,7 +1225,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       c.push = 0;
       c.peer = peers[j];
       c.row = c.peer - d.lo < d.Hl ? &d.view[(size_t)(c.peer - d.lo) * d.R] : nullptr;
-      c.lk = (lkm >> j) & 1u;
+      c.lk = ((lkm >> j) & 1u) | (lmod ? ((fullm >> j) & 1u) << 1 : 0u);
       c.x = idx * d.KE + j * d.NG + n;
       c.key = u * d.KE + j * d.NG + n;
       bool empty = false;
@@ -1305,7 +1310,11 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
           // records read from a list or the ring, and the receiver slots the filter reads
           const uint32_t lb = l < c.m ? l : c.m;
           const bool filt = c.row && !(lmod && c.lk);
-          kb += 16ull * ((c.kind == GX_JOB_SEND ? lb : 0u) + (l - lb)) + (filt ? 8ull * l : 0ull);
+          if (c.lk & 2u) {
+            a.c[C_LOCK_DROP] += l;  // nothing of the packet is loaded or stored
+          } else {
+            kb += 16ull * ((c.kind == GX_JOB_SEND ? lb : 0u) + (l - lb)) + (filt ? 8ull * l : 0ull);
+          }
           if (filt) fm += l;
           if (c.lk) {
             a.locked = true;
@@ -1315,10 +1324,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       }
       c.l = l;
       c.lpre = tot;
-      if (l) {
+      if (l) {  // (a dropped packet stays in the plan for its pending-ring writes; no record of it loads)
         if (lead) pl[nc] = c;
         nc++;
-        tot += l;
+        if (!(c.lk & 2u)) tot += l;
       }
       // a call that leaves batch records pending ends the chunk: its ring writes follow the
       // chunk's loads, so no call of a chunk reads what another call of it wrote
@@ -1425,6 +1434,9 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         run += (uint32_t)__popcll(lm);
       }
     }
+#pragma unroll
+    for (int kk = 1; kk < PLAN_CH; kk++)  // dropped packets at the chunk's end start past its records
+      if (lp[kk] == tot) cb[kk] = run;
     uint32_t stored_all = 0;  // records this team stores: the packets' headers below
     // ---- packet headers: lane k registers call k's packet when it holds a record
     if (j <= PLAN_CH) GX_KP(6);
@@ -1438,6 +1450,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       }
       const uint32_t rv = c.peer - d.lo;
       if (!c.row) stored = c.l;  // another shard's receiver filters on arrival (k_inbox_unpack)
+      if (c.lk & 2u) stored = 0;
       d.msg_len[c.x] = stored;
       d.msg_dst[c.x] = c.peer;
       if (c.row && stored) {  // a locked receiver reads its slots itself (no forwarded words)
@@ -3872,10 +3885,33 @@ __global__ void k_inbox_unpack(Dev d, const uint8_t *in, uint32_t n) {
   const uint32_t vi = dst - d.lo;
   // the receiver holds the ServicesState lock this round (gx.h lock_model): every record goes to
   // its pipeline unfiltered (k_merge_seg); lock_model = 0 merges them and counts them as locked
-  const bool rlk = host_locked(d, dst);
+  const uint32_t rlw = gld(&d.hs[dst - d.lo].lock);
+  const bool rlk = locked_in(d, rlw);
   if (rlk && threadIdx.x == 0 && len) {
     atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
     if (!d.p.lock_model) ctr_atomic(d, C_LOCKED_MERGES, len);
+  }
+  if (rlk && d.p.lock_model && GX_LOCK_BUF(rlw) >= d.C) {  // a full pipeline drops the records (send_planned)
+    if (threadIdx.x == 0) {
+      ctr_atomic(d, C_LOCK_DROP, len);
+      d.msg_key[e] = key;
+      d.msg_dst[e] = dst;
+      d.msg_len[e] = 0;
+      if (fcap) d.fd_len[e] = nfd;
+    }
+    const uint4 *fm = reinterpret_cast<const uint4 *>(src + 16 + 16ull * d.p.packet_cap);
+    for (uint32_t x = threadIdx.x; x < nfd; x += blockDim.x) {
+      const uint4 w = fm[x];
+      gx_fd_msg g;
+      g.incarnation = w.x;
+      g.node = (uint16_t)(w.y & 0xffffu);
+      g.from = (uint16_t)(w.y >> 16);
+      g.kind = (uint8_t)w.z;
+      g.pad[0] = g.pad[1] = g.pad[2] = 0;
+      d.fdm[e * fcap + x] = g;
+    }
+    if (nfd && threadIdx.x == 0) inbox_header(d, dst - d.lo, inbox_claim(d, dst - d.lo), key, (uint32_t)e, 0u);
+    return;
   }
   if (d.sfilt && !(rlk && d.p.lock_model)) {  // the receiver's filter: only live records are kept (compacted, see send_planned)
     const uint64_t *row = &d.view[(size_t)vi * d.R];

@@ -203,9 +203,9 @@ def test_cfg5_full_h32768_parity(gx_lib):
     assert st["expire_server"] <= H * (H // 2) <= st["expire_server"] + st["expire_deferred"]
     assert st["ae_exchanges"] + st["ae_locked"] == 11 * (H // 2)
     # every host blocks behind the storm's 16384 jobs (3 GetBroadcasts calls per round) from round 7:
-    # the gossip of these rounds waits in the pipelines (nothing drains before round 101), and the
-    # push-pull pairs that still run find identical halves (no accepts)
-    assert st["gossip_accepts"] > 0 and st["lock_buffered"] > 0 and st["lock_drops"] > 0
+    # the gossip of these rounds waits in the pipelines (nothing drains before round 101); what
+    # gossip ran before carried records every view already held (warm start, storm on every host)
+    assert st["gossip_accepts"] == 0 and st["lock_buffered"] > 0 and st["lock_drops"] > 0
     assert st["lock_drained"] == 0 and st["first_locked_round"] == 7
     assert st["queue_drops"] == 0 and st["first_drop_round"] == -1  # faithful to the reference's queues
 
