@@ -35,7 +35,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 Q_GM1 = 16384
 # uniformly random 8-B gathers over a 137 GB table on MI355X (profiles/r04/gather_bench.hip; a
 # read-modify-write of the slot runs at the same rate, a blind scatter at 2.8e10/s)
-GATHER_CEILING_PER_S = 4.72e10
+# 128-B view lines per second when every access is a run of 16 consecutive 8-B slots of a random
+# line (profiles/r04/gather_bench.jsonl, gather_run16: 6.379e11 words/s over a 137 GB table)
+LINE_CEILING_PER_S = 6.379e11 / 16
 CONFIGS = {
     # BASELINE.json configs[4]: 32768 x 16, 2-way partition for 50 rounds, departure storm, heal
     "cfg5": dict(desc="32768 hosts x 16 services, fanout 3, cap 32 records/msg, 2-way partition rounds "
@@ -249,30 +251,31 @@ def gossip_stretch_start(cfg, accepting=False):
     return s
 
 
-def gossip_round_span(lib, cfg, seed, local_rank, start=None):
+def gossip_round_span(lib, cfg, seed, local_rank, start=None, **over):
     """Device time per gossip round without per-launch instrumentation: a stretch of period - 1
     gossip-only rounds from `start` (gossip_stretch_start), bracketed by two events on the engine's
     stream (the caller's torch stream). The per-class split above records an event pair around
-    every launch, which adds about 10 us per round."""
+    every launch, which adds about 10 us per round. `over`: parameter overrides (lock_model)."""
     import torch
     p = CONFIGS[cfg]["p"]
     period = min(p.get("ae_period_rounds", 0) or 10, 10)
     if start is None:
         start = gossip_stretch_start(cfg)
-    e = make_engine(lib, cfg, seed, local_rank)
+    e = make_engine(lib, cfg, seed, local_rank, **over)
     e.run_rounds(start - period)
     st = torch.cuda.Stream()  # a stream of its own (launches on the legacy default stream are slower)
     e.set_stream(st.cuda_stream, False)
     n = period - 1
     e.run_rounds(period)  # the first stretch on a new stream starts with ~0.15 ms of queue set-up
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s0 = e.stats()
+    s0, u0 = e.stats(), e.timing()["send"]["units"]
     a.record(st)
     e.run_rounds(n)  # (run_rounds ends with one wake-up kernel, ~8 us, inside the span)
     b.record(st)
     b.synchronize()
-    s1 = e.stats()
+    s1, u1 = e.stats(), e.timing()["send"]["units"]
     us = 1e3 * a.elapsed_time(b) / n
+    e_lock = e.params.lock_model
     e.set_stream(None, False)
     e.close()
     # SURVEY §8(d) algorithmic bytes of a gossip record-merge: 22 B (inbound record 13 + slot 9)
@@ -280,22 +283,25 @@ def gossip_round_span(lib, cfg, seed, local_rank, start=None):
     m, acc, rx = (s1[k] - s0[k] for k in ("gossip_merges", "gossip_accepts", "retransmits"))
     byts = (22 * m + 9 * acc + 13 * rx) / n
     gbs = byts / (us * 1e3)
-    # Against the part's random-access ceiling: every gossip record-merge reads its receiver's
-    # 8-B view slot (the senders' filter, or the receiver), an accept writes it back (a
-    # read-modify-write runs at the gather rate): m slot accesses per stretch at the measured rate
-    # of uniformly random 8-B gathers over a 137 GB table
-    us_ceil = 1e6 * (m / n) / GATHER_CEILING_PER_S
+    # Against the lines the round touches: the senders' filter reads each packet's receiver slots,
+    # a run of consecutive slots per batch (an ExpireServer batch is one owner's 16 services, one
+    # 128-B line of the receiver's row); k_send counts a line wherever a filtered record leaves the
+    # previous record's line (gx_timing units). Floor: those lines at the measured rate of random
+    # 16-slot runs (gather_run16)
+    lines = (u1 - u0) / n
+    us_ceil = 1e6 * lines / LINE_CEILING_PER_S
     return round(us, 2), {"bound": "hbm", "scope": "whole gossip round (send + merge kernels), SURVEY 8(d) bytes",
                           "rounds": [start, start + n - 1],
                           "bytes_per_round": int(byts), "merges_per_round": m // n,
                           "accepts_per_round": acc // n, "accept_fraction": round(acc / m, 4) if m else None,
                           "achieved": round(gbs, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                          "gather_ceiling": {"slot_accesses_per_round": m // n,
-                                             "ceiling_per_s": GATHER_CEILING_PER_S,
-                                             "source": "profiles/r04/gather_bench.jsonl (gather, ILP 4-16)",
-                                             "us_per_round_at_ceiling": round(us_ceil, 2),
-                                             "frac": round(us_ceil / us, 4) if us else None}}
+                          "lock_model": int(e_lock),
+                          "line_ceiling": {"view_lines_per_round": int(lines),
+                                           "ceiling_lines_per_s": LINE_CEILING_PER_S,
+                                           "source": "profiles/r04/gather_bench.jsonl (gather_run16)",
+                                           "us_per_round_at_ceiling": round(us_ceil, 2),
+                                           "frac": round(us_ceil / us, 4) if us and lines else None}}
 
 
 def dissemination(lib, cfg, seed, local_rank, start=100, rounds=300):
@@ -591,9 +597,8 @@ def main():
 
     # per-kernel split: the same window again on a fresh cluster, with HIP events around every
     # launch on the engine's stream (device time per kernel class and algorithmic bytes)
-    kern = {}
-    if not args.no_kernel_split:
-        c = Cluster(lib, args.config, seed, rank, world, local_rank, barrier)
+    def kernel_split(**over):
+        c = Cluster(lib, args.config, seed, rank, world, local_rank, barrier, **over)
         if args.warmup:
             c.run_rounds(args.warmup)
         c.e.enable_timing(True)
@@ -601,26 +606,36 @@ def main():
         c.run_rounds(args.steps)
         tm1 = c.e.timing()
         c.close()
+        out = {}
         for k in KNAMES:
             ms = tm1[k]["ms"] - tm0[k]["ms"]
             nl = tm1[k]["launches"] - tm0[k]["launches"]
             b = tm1[k]["bytes"] - tm0[k]["bytes"]
             if nl:
-                kern[k] = {"ms": round(ms, 4), "launches": nl, "bytes": b,
-                           "GBps": round(b / (ms * 1e6), 1) if ms > 0 else None}
+                out[k] = {"ms": round(ms, 4), "launches": nl, "bytes": b,
+                          "GBps": round(b / (ms * 1e6), 1) if ms > 0 else None}
+        return out
+
+    kern, kern_off = {}, None
+    if not args.no_kernel_split:
+        kern = kernel_split()
+        if world == 1 and not args.no_lock_off and lock["lock_model"]:
+            # the same window without the lock: every push-pull pair and every gossip receiver runs
+            # the merge path the locked reference hosts skip (kernel measurement, not the reference)
+            kern_off = kernel_split(lock_model=0)
     pmc = {}
     try:
         pmc = json.load(open(args.pmc)).get(args.config, {})
     except Exception:
         pass
 
-    def roofline(k):
+    def roofline(k, kern=kern, with_pmc=True):
         if k not in kern or not kern[k]["ms"]:
             return None
         ach = kern[k]["GBps"] or 0.0
         # PMC traffic is measured on the N = 1 run (profiles/pmc_summary.json): per launch of the
         # whole engine, so only comparable with this line at N = 1
-        traffic = (pmc.get(k) or {}).get("hbm_bytes_per_launch") if world == 1 else None
+        traffic = (pmc.get(k) or {}).get("hbm_bytes_per_launch") if world == 1 and with_pmc else None
         return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
                 "bytes_per_launch": kern[k]["bytes"] // max(1, kern[k]["launches"]),
@@ -629,6 +644,13 @@ def main():
 
     dom = max(kern, key=lambda k: kern[k]["ms"]) if kern else None
     roof = roofline(dom) if dom else None
+    roof_off = None
+    if kern_off:
+        dom_off = max(kern_off, key=lambda k: kern_off[k]["ms"])
+        roof_off = {"dominant": roofline(dom_off, kern_off, False),
+                    **{k: roofline(k, kern_off, False) for k in ("ae", "scan", "send", "merge") if k in kern_off},
+                    "note": "lock_model = 0 window: kernel measurement on merges the locked reference hosts "
+                            "skip (not the reference)"}
     gossip = None
     if kern:
         gms = sum(kern[k]["ms"] for k in GOSSIP_KERNELS if k in kern)
@@ -638,9 +660,21 @@ def main():
         if world == 1:  # without per-launch events: the span of a stretch of gossip-only rounds
             gossip["round_span_us"], gossip["roofline"] = gossip_round_span(lib, args.config, seed, local_rank)
             acc0 = gossip_stretch_start(args.config, accepting=True)
-            if acc0 is not None:  # the post-heal stretch, where gossip records are live
+            if acc0 is not None:  # the post-heal stretch, where gossip records are live without the lock
                 gossip["round_span_us_accepting"], gossip["roofline_accepting"] = gossip_round_span(
                     lib, args.config, seed, local_rank, start=acc0)
+            if not args.no_lock_off and lock["lock_model"]:
+                # The same stretches without the lock: where the reference's hosts are locked (their
+                # receivers only queue or drop) the kernels still run the whole merge path, which is
+                # what these measure (the rounds-1..4 comparison); never the headline
+                lo = {"note": "lock_model = 0: kernel measurement on the merge path the locked reference "
+                              "hosts skip; not the reference"}
+                lo["round_span_us"], lo["roofline"] = gossip_round_span(lib, args.config, seed, local_rank,
+                                                                        lock_model=0)
+                if acc0 is not None:
+                    lo["round_span_us_accepting"], lo["roofline_accepting"] = gossip_round_span(
+                        lib, args.config, seed, local_rank, start=acc0, lock_model=0)
+                gossip["lock_off"] = lo
 
     conv = None
     conv_lock_off = None
@@ -672,6 +706,13 @@ def main():
         e = make_engine(lib, args.config, seed, local_rank)
         try:
             spread = version_spread(e, torch.device(f"cuda:{local_rank}"), heal, max(heal + 10, args.spread_max))
+            if not spread["born_after_heal"]["versions"]:
+                # no owner stamped a version after the heal (its loopers held the lock throughout):
+                # a spread figure would be defined over nothing
+                spread = {"rounds": spread["rounds"], "versions_born_after_heal": 0,
+                          "hosts_locked_at_end": sum(h.locked_at(e.round) for h in e.hosts()),
+                          "note": "no owner refreshed after the heal: BroadcastServices never ran on a host "
+                                  "whose looper held the ServicesState lock (services_state.go:535,569)"}
         finally:
             e.close()
     dis = None
@@ -702,7 +743,8 @@ def main():
             "converge_ref_cadence": conv_ref,
             "dissemination": dis, "version_spread": spread,
             "roofline": roof, "roofline_merge": roofline("merge"), "roofline_send": roofline("send"),
-            "cpu_baseline": cpu, "kernels": kern,
+            "roofline_lock_off": roof_off,
+            "cpu_baseline": cpu, "kernels": kern, "kernels_lock_off": kern_off,
             "kernels_scope": "whole engine" if world == 1 else "rank 0's shard (device time and bytes of its launches)",
             "exchange": xfer,
         }

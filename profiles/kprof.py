@@ -86,12 +86,13 @@ def main():
     ap.add_argument("--rounds", type=int, nargs="*", default=[21, 51])
     ap.add_argument("--ae-rounds", type=int, nargs="*", default=[])
     ap.add_argument("--scan-rounds", type=int, nargs="*", default=[])
+    ap.add_argument("--lock-model", type=int, default=1)
     a = ap.parse_args()
     import bench
     from sidecar_amd.abi import load_product
     lib = load_product()
     lib.gx_kprof_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
-    e = bench.make_engine(lib, a.config, 0x5EED, 0)
+    e = bench.make_engine(lib, a.config, 0x5EED, 0, lock_model=a.lock_model)
     res = {}
     for r in sorted(set(a.rounds) | set(a.ae_rounds) | set(a.scan_rounds)):
         e.run_rounds(r - e.round)
@@ -101,7 +102,7 @@ def main():
         if r in a.rounds:
             res[r] = summarize(wm)
             res[r]["merge_paths"] = {k: int(m1[i] - m0[i]) for i, k in enumerate(MERGE_NAMES) if k}
-            print(json.dumps({"config": a.config, "round": r, **res[r]}), flush=True)
+            print(json.dumps({"config": a.config, "lock_model": a.lock_model, "round": r, **res[r]}), flush=True)
         if r in a.ae_rounds:
             print(json.dumps({"config": a.config, "round": r, "push_pull": summarize_ae(am)}), flush=True)
         if r in a.scan_rounds:

@@ -1182,7 +1182,8 @@ GXD grec plan_item(const Dev &d, const PlanCall &c, uint32_t i) {
 // kb: algorithmic bytes (the caller flushes them to GX_K_SEND).
 template <int T>
 GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_job *pjs, PlanCall *pl,
-                      const uint32_t *peers, uint32_t np, unsigned long long &kb, uint32_t npf0 = 0) {
+                      const uint32_t *peers, uint32_t np, unsigned long long &kb, unsigned long long &kl,
+                      uint32_t npf0 = 0) {
   constexpr int PLAN_Q = PLAN_RECS / T;
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lead = tl == 0;
@@ -1195,7 +1196,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   uint32_t pf0 = hs.fifo_head, npf = npf0;
   uint32_t j = 0, n = 0;
   bool stop = np == 0;
-  unsigned fm = 0, fs = 0;
+  unsigned fm = 0, fs = 0, nlines = 0;
   // the receivers' ServicesState lock this round (gx.h lock_model): bit j = peer j, on this shard,
   // holds it. A locked receiver's records all go to its pipeline (k_merge_seg), so they are stored
   // unfiltered and the receiver counts them; with lock_model = 0 they merge and are counted as locked.
@@ -1358,6 +1359,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       cb[k] = 0;
     }
     uint32_t run = 0;
+    uint32_t lcarry = 0xffffffffu;  // the view line of the team's last filtered record (diagnostic)
     for (uint32_t fb = 0; fb < tot; fb += T * PLAN_Q) {
       // Every load of the block is issued unconditionally (a record that needs none loads ring
       // slot 0, one past the end of the chunk loads it too) and used only after all are in flight:
@@ -1423,6 +1425,15 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
 #pragma unroll
         for (int kk = 1; kk < PLAN_CH; kk++) cbk = (uint32_t)kk == k ? cb[kk] : cbk;
         const uint32_t rank = filt ? run + (uint32_t)__popcll(lm & ((1ull << tl) - 1ull)) - cbk : f - c.lpre;
+        {  // 128-B receiver view lines the filter read: a filtered record on a line other than the
+           // previous record's (packet order) starts one (gx_timing.units of GX_K_SEND)
+          const uint32_t line = valid && filt ? (uint32_t)(((uint64_t)(c.peer - d.lo) * d.R + r[q]) >> 4) : 0xffffffffu;
+          const uint32_t tb = lane & ~(uint32_t)(T - 1);
+          const uint32_t up = (uint32_t)__shfl((int)line, (int)(tl ? lane - 1 : lane), 64);
+          const uint32_t prev = tl ? up : lcarry;
+          nlines += line != 0xffffffffu && line != prev;
+          lcarry = (uint32_t)__shfl((int)line, (int)(tb + T - 1), 64);
+        }
         if (live) {
           grec g;
           g.w = w[q];
@@ -1474,6 +1485,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
     wave_sync();  // the plan slots are rewritten by the next chunk
   }
   a.c[C_GOSSIP_MERGES] += fm;
+  kl += nlines;
   a.c[C_STALE] += fs;
 }
 
@@ -1490,7 +1502,7 @@ GXD bool filt_used(const Dev &d, uint32_t pos) { return d.sfilt && pos != 0xffff
 // sleep > 0, senders' filter).
 template <int T, bool X, bool PLAN = false, bool FWD = false>
 GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, unsigned &lost, PlanCall *pl,
-                   unsigned long long &kb, const TickFwd &fwd) {
+                   unsigned long long &kb, unsigned long long &kl, const TickFwd &fwd) {
   const uint32_t lane = threadIdx.x & (T - 1);
   {
     uint32_t u = d.lo + idx;
@@ -1527,7 +1539,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
     if (PLAN) {
       uint32_t *peers = reinterpret_cast<uint32_t *>(&pl[PLAN_CH]);  // the team's peers (k_send's prologue)
       const uint32_t np = peers[16];
-      send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb, (pre && fwd.pf0 == hs.fifo_head) ? fwd.npf : 0u);
+      send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb, kl, (pre && fwd.pf0 == hs.fifo_head) ? fwd.npf : 0u);
       hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1);  // the lock for the next round
       if (lane == 0) *h = hs;
     } else if (!X || !departed(d, u)) {
@@ -1683,18 +1695,20 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       __syncthreads();  // the list and count before the tick's finish reads them
     }
   }
-  unsigned long long kb = 0;
+  unsigned long long kb = 0, kl = 0;
   GX_KP(3);
   if (idx < d.Hl)  // (PLAN runs without departures: every host ticked)
     send_host<T, X, PLAN, PLAN && (OWN > 0)>(d, a, idx, s_pj[threadIdx.x / T], do_bt, lost,
-                                            s_pl[PLAN ? threadIdx.x / T : 0], kb, fwd);
+                                            s_pl[PLAN ? threadIdx.x / T : 0], kb, kl, fwd);
   GX_KP(7);
   acc_flush(d, a);
   if (X && lost) ctr_atomic(d, C_LOST, lost);
   // algorithmic bytes: bookkeeping, FIFO jobs, records read (lists, ring), receiver slots read,
   // records and headers written (send_planned; the record-budget path counts the same per record)
+  // units: the receiver view lines the senders' filter read (128 B each; send_planned only)
   kb = wave_sum(kb);
-  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SEND, kb, 0);
+  kl = wave_sum(kl);
+  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SEND, kb, kl);
 }
 
 
