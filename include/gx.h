@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 7
+#define GX_ABI_VERSION 8
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -488,6 +488,15 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
  * host is in at most one), so the result is identical either way. */
 int gx_ae_merge_local(gx_engine *e); /* phase 5 */
 int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */
+/* A planned gossip round in two calls (fewer host calls per round for an exchange layer; the same
+ * work as the calls they stand for):
+ *   gx_round_gossip_begin = gx_round_send + gx_exchange_plan(plan) + gx_outbox_pack_planned(buf, cap)
+ *   gx_round_gossip_end   = gx_inbox_unpack(buf, bytes) + gx_round_merge, then, unless this round
+ *                           is a push-pull round (*ae_round = 1: the caller runs the gx_ae_* steps
+ *                           and gx_round_end), gx_round_end (*ae_round = 0).
+ * plan: G * G entries as gx_exchange_plan. Same conditions and errors as those calls. */
+int gx_round_gossip_begin(gx_engine *e, uint64_t *plan, void *buf, uint64_t cap);
+int gx_round_gossip_end(gx_engine *e, const void *buf, uint64_t bytes, int *ae_round);
 /* Per-record min and max slot word over this engine's views (R entries each; device memory for
  * the HIP engine), written as (word XOR 2^63) so that signed 64-bit MIN/MAX reductions across
  * shards order them like the unsigned words. All views agree on record r iff the reduced min

@@ -2622,6 +2622,21 @@ int gx_round_end(gx_engine *e) {
   round_end(e);
   return GX_OK;
 }
+int gx_round_gossip_begin(gx_engine *e, uint64_t *plan, void *buf, uint64_t cap) {
+  if (!e || !plan) return GX_EINVAL;
+  int rc = gx_round_send(e);
+  if (!rc) rc = gx_exchange_plan(e, plan);
+  if (!rc) rc = gx_outbox_pack_planned(e, buf, cap);
+  return rc;
+}
+int gx_round_gossip_end(gx_engine *e, const void *buf, uint64_t bytes, int *ae) {
+  if (!e || !ae) return GX_EINVAL;
+  int rc = gx_inbox_unpack(e, buf, bytes);
+  if (!rc) rc = gx_round_merge(e);
+  if (rc) return rc;
+  *ae = ae_round(e);
+  return *ae ? GX_OK : gx_round_end(e);
+}
 /* Row-major: each chunk of records is folded over the views in view order (streaming reads). */
 int gx_view_minmax(gx_engine *e, uint64_t *mn, uint64_t *mx) {
   if (!e || !mn || !mx) return GX_EINVAL;

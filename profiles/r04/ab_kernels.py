@@ -23,12 +23,13 @@ ap.add_argument("--skip", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=30)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--libs", nargs="+", required=True)
+ap.add_argument("--lock-model", type=int, default=1)
 a = ap.parse_args()
 libs = {os.path.basename(p): load_library(p) for p in a.libs}
 res = {}
 for rep in range(a.reps):
     for ln, lib in libs.items():
-        e = bench.make_engine(lib, a.config, 0x5EED, 0)
+        e = bench.make_engine(lib, a.config, 0x5EED, 0, lock_model=a.lock_model)
         e.run_rounds(a.skip)
         e.enable_timing(True)
         t0 = e.timing()

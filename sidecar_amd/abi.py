@@ -233,6 +233,7 @@ ABI_FUNCS = [
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_exchange_plan", "gx_outbox_pack_planned", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
+    "gx_round_gossip_begin", "gx_round_gossip_end",
     "gx_view_minmax", "gx_owner_words", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_set_stream", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
@@ -285,6 +286,8 @@ def _declare(lib):
         "gx_round_merge": ([vp], i32), "gx_ae_bytes": ([vp, vp], i32),
         "gx_ae_pack": ([vp, vp, C.c_uint64], i32), "gx_ae_merge": ([vp, vp, C.c_uint64, vp, C.c_uint64], i32),
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32), "gx_owner_words": ([vp, vp], i32),
+        "gx_round_gossip_begin": ([vp, vp, vp, C.c_uint64], i32),
+        "gx_round_gossip_end": ([vp, vp, C.c_uint64, P(i32)], i32),
         "gx_ae_merge_local": ([vp], i32),
         "gx_read_server_times": ([vp, u32, u32, u32, vp], i32),
         "gx_read_last_changed": ([vp, u32, u32, vp], i32),
@@ -780,6 +783,19 @@ class Engine:
 
     def round_merge(self):
         check(self.lib.gx_round_merge(self.h), "gx_round_merge")
+
+    def round_gossip_begin(self, plan: np.ndarray, ptr: int, cap: int):
+        """round_send + exchange_plan (into `plan`, G*G uint64) + outbox_pack_planned in one call."""
+        check(self.lib.gx_round_gossip_begin(self.h, plan.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
+                                             C.c_uint64(cap)), "gx_round_gossip_begin")
+
+    def round_gossip_end(self, ptr: int, nbytes: int) -> bool:
+        """inbox_unpack + round_merge, then round_end unless this is a push-pull round (returns True:
+        the caller runs the push-pull steps and round_end)."""
+        ae = C.c_int(0)
+        check(self.lib.gx_round_gossip_end(self.h, C.c_void_p(ptr), C.c_uint64(nbytes), C.byref(ae)),
+              "gx_round_gossip_end")
+        return bool(ae.value)
 
     def ae_bytes(self) -> np.ndarray:
         out = np.zeros(self.G, dtype=np.uint64)

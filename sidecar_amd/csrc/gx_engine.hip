@@ -2309,6 +2309,23 @@ int gx_round_end(gx_engine *e) {
   return rc ? rc : phase_done(e);
 }
 
+int gx_round_gossip_begin(gx_engine *e, uint64_t *plan, void *buf, uint64_t cap) {
+  if (!e || !plan) return GX_EINVAL;
+  int rc = gx_round_send(e);
+  if (!rc) rc = gx_exchange_plan(e, plan);
+  if (!rc) rc = gx_outbox_pack_planned(e, buf, cap);
+  return rc;
+}
+
+int gx_round_gossip_end(gx_engine *e, const void *buf, uint64_t bytes, int *ae) {
+  if (!e || !ae) return GX_EINVAL;
+  int rc = gx_inbox_unpack(e, buf, bytes);
+  if (!rc) rc = gx_round_merge(e);
+  if (rc) return rc;
+  *ae = ae_round(e) ? 1 : 0;
+  return *ae ? GX_OK : gx_round_end(e);
+}
+
 int gx_owner_words(gx_engine *e, uint64_t *out) {
   if (!e || !out) return GX_EINVAL;
   HIPCHK(hipSetDevice(e->device));

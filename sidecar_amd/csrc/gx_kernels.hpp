@@ -240,14 +240,20 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
 // fwd (k_send's planned sends): the tick also loads the FIFO head jobs into fwd->pj (with the
 // sleep-ring head, in the same round trip) and hands its register copy of the bookkeeping to the
 // sends, which then neither reload it nor wait for the jobs.
+// FIFO head jobs a send team keeps in LDS: T (GossipMessages <= 1: a round's calls fit), or
+// GX_JPF * T under GossipMessages > 1 (fewer refills: each one waits on a global load)
+#define GX_JPF 3
+template <int T>
+GXD uint32_t pj_window(const Dev &d) { return d.NG > 1 ? (uint32_t)(GX_JPF * T) : (uint32_t)T; }
 struct TickFwd {
-  gx_job *pj;         // the team's T LDS job slots (stored FIFO head jobs)
+  gx_job *pj;         // the team's T * GX_JPF LDS job slots (stored FIFO head jobs)
   uint32_t *peers;    // the team's peer slots (count in [16]), sampled while the tick's loads fly
   gx_host_state hs;   // the bookkeeping after the tick
   uint32_t pf0, npf;  // FIFO position of pj[0], jobs loaded
   uint32_t tick;      // d.tick[idx] as the tick set it
 };
-template <int T, int SPL = 1, bool FWD = false>
+// SW: the team's LDS sleeper slots (the head of its sleep ring, refilled SW at a time).
+template <int T, int SPL = 1, bool FWD = false, int SW = T>
 GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd &fwd) {
   const uint32_t lane = threadIdx.x & 63, tl = lane & (T - 1), tw = lane / T;
   const bool lead = tl == 0;
@@ -283,12 +289,17 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
       }
     }
     if (tl == 0) mexp0 = d.minexp[idx];
-    if (tl < hs.sleep_tail - hs.sleep_head) sj[tl] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + tl) % d.SQ)];
+    {  // the sleep ring's head: T slots, or SW under GossipMessages > 1 (a round re-arms up to
+       // fanout * GossipMessages passes, and they wake together)
+      const uint32_t ns = hs.sleep_tail - hs.sleep_head, win = d.NG > 1 ? (uint32_t)SW : (uint32_t)T;
+      for (uint32_t x = tl; x < ns && x < win; x += T) sj[x] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + x) % d.SQ)];
+    }
     if (FWD) {  // the tick pushes at the FIFO tail only: the stored jobs at the head stay where they are
       const uint32_t q = hs.fifo_stored - hs.fifo_head;
-      if (tl < q) fwd.pj[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
+      const uint32_t win = pj_window<T>(d), nl = q < win ? q : win;
+      for (uint32_t x = tl; x < nl; x += T) fwd.pj[x] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + x) % d.Q)];
       fwd.pf0 = hs.fifo_head;
-      fwd.npf = q < (uint32_t)T ? q : (uint32_t)T;
+      fwd.npf = nl;
     }
   }
   if (FWD && tl == 0 && idx < d.Hl) {  // the sends' peers: ALU while the loads above are in flight
@@ -323,8 +334,17 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
       if (lead) d.tick[idx] = 0;
     } else {
       // TimedLooper re-arm (services_state.go:585-601): due passes re-enter the FIFO in order
+      const uint32_t win = d.NG > 1 ? (uint32_t)SW : (uint32_t)T;
       for (uint32_t w = 0; hs.sleep_head != hs.sleep_tail; w++) {
-        const gx_sleeper z = w < (uint32_t)T ? sj[w] : d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
+        if (w == win) {  // past the loaded slots: the next window, all its loads in flight together
+          const uint32_t ns = hs.sleep_tail - hs.sleep_head;
+          wave_sync();
+          for (uint32_t x = tl; x < ns && x < win; x += T)
+            sj[x] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + x) % d.SQ)];
+          wave_sync();
+          w = 0;
+        }
+        const gx_sleeper z = sj[w];
         if ((int64_t)z.wake > d.round) break;
         hs.sleep_head++;
         push_job_r(d, a, o, hs, z.job, lead);
@@ -876,10 +896,18 @@ GXD uint64_t spread32(uint64_t x) {  // bit i -> bit 2i
   x = (x | (x << 1)) & 0x5555555555555555ull;
   return x;
 }
-template <bool EV, bool NT>
+#ifndef GX_STORM_TM
+#define GX_STORM_TM 2  // 1024-word units per tile (one barrier per tile): 26.88 -> 26.41 ms at cfg 5
+#endif                 // over TM 1 (profiles/r05/ab/storm.jsonl; TM 1 PF 4 26.54, TM 2 PF 3 26.97)
+#ifndef GX_STORM_PF
+#define GX_STORM_PF 2  // tiles whose loads are in flight while one is folded
+#endif
+template <bool EV, bool NT, int TM = GX_STORM_TM, int PF = GX_STORM_PF>
 __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
-  __shared__ uint32_t s_cnt[2][8];
-  __shared__ uint32_t s_ecnt[2][8];
+  constexpr int NC = 2 * TM;     // 512-word chunks per tile (a thread takes 2 words of each)
+  constexpr uint32_t TW = 1024u * TM;
+  __shared__ uint32_t s_cnt[2][4 * NC];
+  __shared__ uint32_t s_ecnt[2][4 * NC];
   uint32_t vi = blockIdx.x, v = d.lo + vi;
   if (departed(d, v)) return;  // uniform per block
   uint32_t half = d.H / 2;
@@ -902,32 +930,33 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
   const bool leader = (lane & (LPO - 1)) == 0;
   uint64_t *row = &d.view[(size_t)vi * d.R + (size_t)lo * d.S];
   const uint32_t nw = (hi - lo) * d.S;
-  // two 1024-word tiles in flight while one is processed (q0: even tiles, q1: odd tiles)
-  ulonglong2 q0[2], q1[2];
-  auto load = [&](uint32_t base, ulonglong2 *q) {
+  // PF tiles of TW words in flight while one is folded (tile i in q[i % PF])
+  ulonglong2 q[PF][NC];
+  auto load = [&](uint32_t base, ulonglong2 *x) {
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
+    for (int c = 0; c < NC; c++) {
       uint32_t r0 = base + 512 * c + 2 * t;
       if (r0 < nw) {
         if (NT) {
-          v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r0]));
-          q[c] = make_ulonglong2(x.x, x.y);
+          v2u64 y = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r0]));
+          x[c] = make_ulonglong2(y.x, y.y);
         } else {
-          q[c] = *reinterpret_cast<const ulonglong2 *>(&row[r0]);
+          x[c] = *reinterpret_cast<const ulonglong2 *>(&row[r0]);
         }
       } else {
-        q[c] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+        x[c] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
       }
     }
   };
-  load(0, q0);
-  if (1024 < nw) load(1024, q1);
-  auto tile = [&](uint32_t base, uint32_t it, const ulonglong2 *w) {
-    bool lead_live[2], live_c[2];
-    uint64_t pmask[2];
-    uint32_t rank[2], erank[2], sh_c[2];
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
+  for (int s = 0; s < PF; s++)
+    if (s * TW < nw) load(s * TW, q[s]);
+  auto tile = [&](uint32_t base, uint32_t it, const ulonglong2 *w) {
+    bool lead_live[NC], live_c[NC];
+    uint64_t pmask[NC];
+    uint32_t rank[NC], erank[NC], sh_c[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
       bool p0 = st_of(w[c].x) != GX_ABSENT, p1 = st_of(w[c].y) != GX_ABSENT;
       bool l0 = p0 && st_of(w[c].x) != GX_TOMBSTONE, l1 = p1 && st_of(w[c].y) != GX_TOMBSTONE;
       uint64_t b0 = __ballot(p0), b1 = __ballot(p1), bl = __ballot(l0 || l1);
@@ -969,16 +998,21 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       }
     }
     __syncthreads();
-    uint32_t pre[2] = {0, 0}, tot = 0;
+    // job positions in key order: chunk-major, then wave (chunk c of wave w is slots
+    // base + 512c + 128w ..)
+    uint32_t pre[NC], tot = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int c = 0; c < NC; c++) pre[c] = 0;
+#pragma unroll
+    for (int k = 0; k < 4 * NC; k++) {
       uint32_t x = s_cnt[it][k];
-      if (k < (int)wv) pre[0] += x;
-      if (k < 4 + (int)wv) pre[1] += x;
+#pragma unroll
+      for (int c = 0; c < NC; c++)
+        if (k < 4 * c + (int)wv) pre[c] += x;
       tot += x;
     }
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
+    for (int c = 0; c < NC; c++) {
       uint32_t pos = jobs + pre[c] + rank[c];
       if (lead_live[c] && pos < room) {
         uint32_t o = lo + ((base + 512 * c + 2 * t) >> d.logS);
@@ -988,16 +1022,19 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
     }
     jobs += tot;
     if (EV && evk >= 0) {
-      uint32_t epre[2] = {0, 0}, etot = 0;
+      uint32_t epre[NC], etot = 0;
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+      for (int c = 0; c < NC; c++) epre[c] = 0;
+#pragma unroll
+      for (int k = 0; k < 4 * NC; k++) {
         uint32_t x = s_ecnt[it][k];
-        if (k < (int)wv) epre[0] += x;
-        if (k < 4 + (int)wv) epre[1] += x;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          if (k < 4 * c + (int)wv) epre[c] += x;
         etot += x;
       }
 #pragma unroll
-      for (int c = 0; c < 2; c++) {
+      for (int c = 0; c < NC; c++) {
         uint32_t ob = __shfl(erank[c], (int)sh_c[c], 64);  // the owner's first event
         uint32_t r0 = base + 512 * c + 2 * t, key0 = lo * d.S + r0;
         uint32_t s0 = r0 & (d.S - 1);
@@ -1010,16 +1047,20 @@ __global__ __launch_bounds__(256) void k_storm_p2(Dev d) {
       n_ev += etot;
     }
   };
-  for (uint32_t base = 0; base < nw; base += 2048) {
-    {
-      ulonglong2 w[2] = {q0[0], q0[1]};
-      if (base + 2048 < nw) load(base + 2048, q0);
-      tile(base, 0, w);
-    }
-    if (base + 1024 < nw) {
-      ulonglong2 w[2] = {q1[0], q1[1]};
-      if (base + 3072 < nw) load(base + 3072, q1);
-      tile(base + 1024, 1, w);
+  uint32_t it = 0;  // s_cnt buffer of the tile (alternates: the next tile's counts are written while
+                    // slower waves may still read this one's)
+  for (uint32_t base = 0; base < nw; base += PF * TW) {
+#pragma unroll
+    for (int s = 0; s < PF; s++) {
+      const uint32_t bs = base + s * TW;
+      if (bs < nw) {
+        ulonglong2 w[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) w[c] = q[s][c];
+        if (bs + PF * TW < nw) load(bs + PF * TW, q[s]);
+        tile(bs, it, w);
+        it ^= 1u;
+      }
     }
   }
   bool changed = c_wr != 0;
@@ -1129,6 +1170,38 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 // Batch records that stay pending are written to the ring after the chunk's loads, position p by
 // team lane p % T in call order (the sequential order of the ring writes).
 #define PLAN_CH 4  // calls planned per chunk
+// Diagnostics (build with -DGX_SEND_SPLIT, engine created with GX_KPROF set): per wave, the time
+// its lane-0 team spends in each part of the chunk loop, summed over chunks, in place of the
+// k_send phase marks 1..6: plan, records, headers, ring writes + sync, chunks, refills.
+#ifdef GX_SEND_SPLIT
+#define GX_SPLIT_DECL unsigned long long sp_t = wall_clock64(), sp_acc[4] = {0, 0, 0, 0}, sp_n = 0, sp_rf = 0;
+#define GX_SPLIT(k)                              \
+  do {                                           \
+    const unsigned long long t_ = wall_clock64(); \
+    sp_acc[k] += t_ - sp_t;                      \
+    sp_t = t_;                                   \
+  } while (0)
+#define GX_SPLIT_FLUSH()                                                                                 \
+  do {                                                                                                   \
+    if (d.kprof && (threadIdx.x & 63) == 0) {                                                           \
+      unsigned long long *k_ = &d.kprof[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8]; \
+      k_[1] = sp_acc[0];                                                                                 \
+      k_[2] = sp_acc[1];                                                                                 \
+      k_[3] = sp_acc[2];                                                                                 \
+      k_[4] = sp_acc[3];                                                                                 \
+      k_[5] = sp_n;                                                                                      \
+      k_[6] = sp_rf;                                                                                     \
+    }                                                                                                    \
+  } while (0)
+#else
+#define GX_SPLIT_DECL
+#define GX_SPLIT(k) \
+  do {              \
+  } while (0)
+#define GX_SPLIT_FLUSH() \
+  do {                   \
+  } while (0)
+#endif
 #ifndef GX_PLAN_RECS
 #define GX_PLAN_RECS 32
 #endif
@@ -1197,6 +1270,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   uint32_t j = 0, n = 0;
   bool stop = np == 0;
   unsigned fm = 0, fs = 0, nlines = 0;
+  GX_SPLIT_DECL
   // the receivers' ServicesState lock this round (gx.h lock_model): bit j = peer j, on this shard,
   // holds it. A locked receiver's records all go to its pipeline (k_merge_seg), so they are stored
   // unfiltered and the receiver counts them; with lock_model = 0 they merge and are counted as locked.
@@ -1213,6 +1287,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   }
   const bool lmod = d.p.lock_model != 0;
   while (!stop) {
+#ifdef GX_SEND_SPLIT
+    sp_n++;
+    sp_t = wall_clock64();
+#endif
     // ---- 1. plan up to PLAN_CH calls (control state only)
     uint32_t nc = 0, tot = 0;
     bool any_push = false;
@@ -1234,13 +1312,17 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         gx_job jb = make_job(0, 0, 0);
         if (hs.fifo_head != hs.fifo_stored) {  // a stored job: from the LDS window
           uint32_t q = hs.fifo_head - pf0;
-          if (q >= npf) {  // load the next T stored head jobs
-            const uint32_t left = hs.fifo_stored - hs.fifo_head;
+          if (q >= npf) {  // load the next stored head jobs (T, or GX_JPF * T under GossipMessages > 1)
+            const uint32_t left = hs.fifo_stored - hs.fifo_head, win = pj_window<T>(d);
+            const uint32_t nl = left < win ? left : win;
             wave_sync();
-            if (tl < left) pjs[tl] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + tl) % d.Q)];
+            for (uint32_t x = tl; x < nl; x += T) pjs[x] = d.fifo[(size_t)idx * d.Q + ((hs.fifo_head + x) % d.Q)];
             wave_sync();
+#ifdef GX_SEND_SPLIT
+            sp_rf++;
+#endif
             pf0 = hs.fifo_head;
-            npf = left < (uint32_t)T ? left : (uint32_t)T;
+            npf = nl;
             q = 0;
             if (lead) kb += 16ull * npf;
           }
@@ -1348,7 +1430,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
     }
     if (nc == 0) break;
     wave_sync();  // the plan in LDS
+#ifndef GX_SEND_SPLIT
     if (j <= PLAN_CH) GX_KP(5);
+#endif
+    GX_SPLIT(0);
     // ---- 2. the chunk's records: loads, receiver slots, compacted stores. Record f of the chunk
     // belongs to call k (lpre), its live rank in the packet is run(f) - run(lpre_k), where run(x)
     // counts the live records before x (ballot prefix over the team, call starts in cb[]).
@@ -1368,6 +1453,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       uint32_t r[PLAN_Q], ck[PLAN_Q];
       uint32_t sel[PLAN_Q];  // 0: computed from the job; 1: loaded list record (+ pass); 2: loaded ring record
       gx_u32x3 lx[PLAN_Q];   // the loads, kept apart from the computed words until all are issued
+      uint64_t w0[PLAN_Q];   // the receivers' slots (senders' filter)
 #pragma unroll
       for (int q = 0; q < PLAN_Q; q++) {
         const uint32_t f = fb + tl + T * q;
@@ -1390,17 +1476,32 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         lx[q] = gld3(src);
         w[q] = c.bw;  // computed: the job's word
         r[q] = c.rb + (c.kind == GX_JOB_EXPIRE ? (c.emask ? nth_set_bit(c.emask, i) : i) : 0u);
+        // the senders' filter reads the local receiver's slot; a computed record's key is known
+        // now, so its slot load goes out with the record loads (one round trip for both). Records
+        // nobody filters (a locked or remote receiver) load slot 0 of view 0 instead (one line).
+        const bool filt = valid && c.row && !(lmod && c.lk);
+        const uint64_t *row = filt ? c.row : d.view;
+        w0[q] = gld(&row[filt && sel[q] == 0 && r[q] < d.R ? r[q] : 0u]);
       }
-      uint64_t w0[PLAN_Q];
+      bool reload = false;  // a loaded record that is filtered: its slot load needs the record's key
 #pragma unroll
-      for (int q = 0; q < PLAN_Q; q++) {  // the senders' filter: the local receiver's slot
+      for (int q = 0; q < PLAN_Q; q++) {
         const PlanCall &c = pl[ck[q]];
         if (sel[q]) {  // loaded (+ pass * 50 ns for a list record, services_state.go:588-599)
           w[q] = ((uint64_t)lx[q].x | ((uint64_t)lx[q].y << 32)) + (sel[q] == 1 ? w[q] : 0ull);
           r[q] = lx[q].z;
+          reload |= c.row && !(lmod && c.lk);
         }
-        const uint64_t *row = c.row ? c.row : d.view;
-        w0[q] = gld(&row[r[q] < d.R ? r[q] : 0u]);
+      }
+      if (__ballot(reload)) {  // wave-uniform: a second round trip only where a wave needs it
+#pragma unroll
+        for (int q = 0; q < PLAN_Q; q++) {
+          const PlanCall &c = pl[ck[q]];
+          const bool fl = sel[q] && c.row && !(lmod && c.lk);
+          const uint64_t *row = fl ? c.row : d.view;
+          const uint64_t x = gld(&row[fl && r[q] < d.R ? r[q] : 0u]);
+          w0[q] = fl ? x : w0[q];
+        }
       }
 #pragma unroll
       for (int q = 0; q < PLAN_Q; q++) {
@@ -1450,7 +1551,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       if (lp[kk] == tot) cb[kk] = run;
     uint32_t stored_all = 0;  // records this team stores: the packets' headers below
     // ---- packet headers: lane k registers call k's packet when it holds a record
+#ifndef GX_SEND_SPLIT
     if (j <= PLAN_CH) GX_KP(6);
+#endif
+    GX_SPLIT(1);
     if (tl < nc) {
       const PlanCall &c = pl[tl];
       uint32_t stored = 0;
@@ -1471,6 +1575,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       stored_all = stored + ((c.row && stored) ? 2u : 0u);  // a header and its count ~ 2 records
     }
     kb += 16ull * stored_all;
+    GX_SPLIT(2);
     // ---- batch records left pending: position p by lane p % T, in call order
     if (any_push) {
       for (uint32_t k = 0; k < nc; k++) {
@@ -1483,7 +1588,9 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       __threadfence_block();  // the next chunk may read them on other lanes
     }
     wave_sync();  // the plan slots are rewritten by the next chunk
+    GX_SPLIT(3);
   }
+  GX_SPLIT_FLUSH();
   a.c[C_GOSSIP_MERGES] += fm;
   kl += nlines;
   a.c[C_STALE] += fs;
@@ -1640,12 +1747,12 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
 // state except the receivers' inbox counts, zeroed a round ahead (Dev::in_cnt_nx).
 template <int T, bool X, bool SCAN = false, bool VEC = false, bool EV = false, int OWN = 0, bool PLAN = false>
 __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
-  __shared__ gx_job s_pj[256 / T][T];  // FIFO head jobs of the block's hosts, loaded ahead
+  __shared__ gx_job s_pj[256 / T][T * GX_JPF];  // FIFO head jobs of the block's hosts, loaded ahead
   // send_planned's chunk plans, then the team's peers (16 u32 = one PlanCall's 64 B)
   __shared__ PlanCall s_pl[PLAN ? 256 / T : 1][PLAN_CH + 1];
   __shared__ ScanLds sm;
   __shared__ uint32_t s_scan[256 / T], s_nscan;
-  __shared__ gx_sleeper s_sl[OWN ? 256 : 1];  // sleep-ring heads of the owner ticks
+  __shared__ gx_sleeper s_sl[OWN ? 256 * GX_JPF : 1];  // sleep-ring heads of the owner ticks
   Acc a;
   const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T;
   unsigned lost = 0;
@@ -1674,7 +1781,7 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
       }
     }
     __syncthreads();
-    const bool q = owner_tick<T, OWN, PLAN>(d, a, idx, &s_sl[threadIdx.x & ~(uint32_t)(T - 1)], fwd);
+    const bool q = owner_tick<T, OWN, PLAN, T * GX_JPF>(d, a, idx, &s_sl[(threadIdx.x / T) * (T * GX_JPF)], fwd);
     if (q) s_scan[atomicAdd(&s_nscan, 1u)] = idx;  // lead lanes only
     GX_KP(1);
     __syncthreads();  // the block's ticks before its scans and sends read them

@@ -280,51 +280,53 @@ class DistShard:
         self.s.sync()
         return recv
 
-    def _exchange_planned(self, plan: np.ndarray, packer) -> torch.Tensor:
-        """all-to-all with split sizes every rank knows ahead (gx_exchange_plan): no size collective
-        and no wait on the device."""
-        ss = [int(x) for x in plan[self.rank]]
-        rs = [int(plan[src][self.rank]) for src in range(self.world)]
-        self.last_sizes = np.array(ss, dtype=np.uint64)
-        send = self.s.pack(self.last_sizes, packer)
-        recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
-        calls = (int(plan.max()) + self.CHUNK - 1) // self.CHUNK
-        if calls <= 1:
-            self._a2a(recv, send, rs, ss)
-            return recv
-        soff = np.concatenate([[0], np.cumsum(ss)])
-        roff = np.concatenate([[0], np.cumsum(rs)])
-        for c in range(calls):
-            lo = c * self.CHUNK
-            s_part = [max(0, min(self.CHUNK, n - lo)) for n in ss]
-            r_part = [max(0, min(self.CHUNK, n - lo)) for n in rs]
-            s_buf = torch.cat([send[int(soff[p]) + lo:int(soff[p]) + lo + s_part[p]] for p in range(self.world)])
-            r_buf = torch.empty(sum(r_part), dtype=torch.uint8, device=self.device)
-            self._a2a(r_buf, s_buf, r_part, s_part)
-            o = 0
-            for p in range(self.world):
-                if r_part[p]:
-                    recv[int(roff[p]) + lo:int(roff[p]) + lo + r_part[p]].copy_(r_buf[o:o + r_part[p]])
-                o += r_part[p]
-        return recv
+    def _planned_bufs(self):
+        """Send and receive buffers of the planned exchange, allocated once at their bounds: a
+        shard sends at most fanout packet slots per host, and receives at most that per host of
+        the other shards (gx.h gx_exchange_plan)."""
+        if getattr(self, "_pb", None) is None:
+            p = self.e.params
+            slot = 16 + 16 * p.packet_cap
+            hl = self.e.hi - self.e.lo
+            send = torch.empty(hl * p.fanout * slot, dtype=torch.uint8, device=self.device)
+            recv = torch.empty((p.n_hosts - hl) * p.fanout * slot, dtype=torch.uint8, device=self.device)
+            self._pb = (send, recv, np.zeros(self.world * self.world, dtype=np.uint64))
+        return self._pb
+
+    def _gossip_planned(self) -> bool:
+        """One planned gossip round in two engine calls around the all-to-all; True when it is a
+        push-pull round (the caller runs the push-pull steps and round_end)."""
+        e = self.e
+        send, recv, plan = self._planned_bufs()
+        e.round_gossip_begin(plan, _ptr(send), send.numel())
+        m = plan.reshape(self.world, self.world)
+        ss = [int(x) for x in m[self.rank]]
+        rs = [int(m[src][self.rank]) for src in range(self.world)]
+        self.last_sizes = m[self.rank].copy()
+        ns, nr = sum(ss), sum(rs)
+        if max(max(ss), max(rs)) > self.CHUNK or ns > send.numel() or nr > recv.numel():
+            raise RuntimeError("planned exchange larger than its bound")  # cannot happen (gx.h)
+        self._a2a(recv[:nr], send[:ns], rs, ss)
+        return e.round_gossip_end(_ptr(recv), nr)
 
     def run_rounds(self, n: int):
         e = self.e
         planned = planned_exchange(e.params)  # sizes from the seeded plan: no host wait
         for _ in range(n):
-            e.round_send()
             self.exchange_paths["planned" if planned else "sized"] += 1
             if planned:
-                x = self._exchange_planned(e.exchange_plan(), e.outbox_pack_planned)
+                ae = self._gossip_planned()
             else:
+                e.round_send()
                 ob = torch.zeros(self.world, dtype=torch.int64, device=self.device)
                 e.outbox_sizes_async(_ptr(ob))  # no host wait: the sizes join the size all-gather
                 x = self._exchange(ob, e.outbox_pack)
+                e.inbox_unpack(_ptr(x), x.numel())
+                e.round_merge()
+                ae = e.is_ae_round()
             self.wire.packets += int(self.last_sizes.sum())
-            e.inbox_unpack(_ptr(x), x.numel())
-            e.round_merge()
             # push-pull: digests, lead blocks, return blocks (local pairs overlap the exchanges)
-            if e.is_ae_round():
+            if ae:
                 dsz = e.ae_bytes()
                 dig = self._exchange(dsz, e.ae_pack, after_pack=e.ae_merge_local)
                 lsz = e.ae_delta_bytes(_ptr(dig), dig.numel())
@@ -333,7 +335,9 @@ class DistShard:
                 ret = self._exchange(rsz, lambda p, c: e.ae_return_pack(_ptr(lead), lead.numel(), p, c))
                 self.wire.add_ae(dsz, lsz, rsz)
                 e.ae_merge(_ptr(lead), lead.numel(), _ptr(ret), ret.numel())
-            e.round_end()
+                e.round_end()
+            elif not planned:
+                e.round_end()
 
     def stats(self) -> dict:
         st = self.e.stats()
