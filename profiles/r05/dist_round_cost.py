@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--start", type=int, default=21)
     ap.add_argument("--rounds", type=int, default=29)
     ap.add_argument("--lock-model", type=int, default=1)
+    ap.add_argument("--cprofile", action="store_true", help="profile the host side of the sharded rounds")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -51,9 +52,21 @@ def main():
             run(1)
             torch.cuda.synchronize()
             per.append((r, 1e3 * (time.perf_counter() - t0)))
+        prof = None
+        if a.cprofile and mode == "dist":
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         run(a.rounds)  # back to back, one sync at the end
         torch.cuda.synchronize()
+        if prof is not None:
+            prof.disable()
+            import io
+            import pstats
+            buf = io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+            print(buf.getvalue(), file=sys.stderr)
         out[mode] = {"ms_per_round_synced": {str(r): round(ms, 3) for r, ms in per},
                      "ms_per_round_back_to_back": round(1e3 * (time.perf_counter() - t0) / a.rounds, 3)}
         close()
