@@ -1263,6 +1263,9 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
   const uint32_t u = d.lo + idx, cap = d.p.packet_cap, mask = d.DQ - 1;
   grec *dq = &d.dq[(size_t)idx * d.DQ];
+  // the team's message entries (its packets' records and filter words): entry x = idx * KE + k
+  grec *const msg_t = &d.msg[(size_t)idx * d.KE * cap];
+  uint64_t *const w0_t = &d.msg_w0[(size_t)idx * d.KE * cap];
   const int64_t t_stale = d.now - d.p.tombstone_lifespan_ns - d.p.stale_fudge_ns;
   const int64_t t_gc = d.now - d.p.tombstone_lifespan_ns;
   // FIFO head jobs, T at a time: position pf0 + q in pjs[q], q < npf (npf0 already loaded)
@@ -1480,7 +1483,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         // now, so its slot load goes out with the record loads (one round trip for both). Records
         // nobody filters (a locked or remote receiver) load slot 0 of view 0 instead (one line).
         const bool filt = valid && c.row && !(lmod && c.lk);
-        const uint64_t *row = filt ? c.row : d.view;
+        const uint64_t *row = filt ? c.row : reinterpret_cast<const uint64_t *>(dq);  // (a line of the team's ring)
         w0[q] = gld(&row[filt && sel[q] == 0 && r[q] < d.R ? r[q] : 0u]);
       }
       bool reload = false;  // a loaded record that is filtered: its slot load needs the record's key
@@ -1498,7 +1501,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         for (int q = 0; q < PLAN_Q; q++) {
           const PlanCall &c = pl[ck[q]];
           const bool fl = sel[q] && c.row && !(lmod && c.lk);
-          const uint64_t *row = fl ? c.row : d.view;
+          const uint64_t *row = fl ? c.row : reinterpret_cast<const uint64_t *>(dq);
           const uint64_t x = gld(&row[fl && r[q] < d.R ? r[q] : 0u]);
           w0[q] = fl ? x : w0[q];
         }
@@ -1528,7 +1531,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
         const uint32_t rank = filt ? run + (uint32_t)__popcll(lm & ((1ull << tl) - 1ull)) - cbk : f - c.lpre;
         {  // 128-B receiver view lines the filter read: a filtered record on a line other than the
            // previous record's (packet order) starts one (gx_timing.units of GX_K_SEND)
-          const uint32_t line = valid && filt ? (uint32_t)(((uint64_t)(c.peer - d.lo) * d.R + r[q]) >> 4) : 0xffffffffu;
+          const uint32_t line = valid && filt ? ((c.peer << 15) | (r[q] >> 4)) : 0xffffffffu;  // exact for R <= 2^19
           const uint32_t tb = lane & ~(uint32_t)(T - 1);
           const uint32_t up = (uint32_t)__shfl((int)line, (int)(tl ? lane - 1 : lane), 64);
           const uint32_t prev = tl ? up : lcarry;
@@ -1540,8 +1543,9 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
           g.w = w[q];
           g.r = r[q];
           g.pad = 0;
-          gst_rec(&d.msg[(size_t)c.x * cap + rank], g);
-          if (filt) gst(&d.msg_w0[(size_t)c.x * cap + rank], w0[q]);
+          const uint32_t xo = (c.x - idx * d.KE) * cap + rank;  // within the team's entries
+          gst_rec(&msg_t[xo], g);
+          if (filt) gst(&w0_t[xo], w0[q]);
         }
         run += (uint32_t)__popcll(lm);
       }
