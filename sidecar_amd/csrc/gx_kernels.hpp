@@ -2529,6 +2529,65 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
 #ifndef MERGE_WPE_GM
 #define MERGE_WPE_GM 4  // waves per SIMD of the merge at GossipMessages > 1 (wide inboxes)
 #endif
+// A locked receiver's round (gx.h lock_model): its packets' records join its pipeline in arrival
+// order (ascending sender key) while it has room, the rest are dropped; nothing merges. SEG lanes
+// per receiver (four receivers per wave at SEG 16): the segment ranks the headers by key in
+// registers, finds each output record's packet by the ranked starts, and issues every record
+// load of a pass (RPL per lane) before its stores. Returns false (the caller takes the
+// whole-wave path) for an inbox of more than SEG packets; the result is the whole-wave path's.
+#define LOCK_RPL 4
+template <int SEG>
+GXD bool lock_append_seg(const Dev &d, uint32_t vi, bool act) {
+  const uint32_t lane = threadIdx.x & 63, sl = lane & (SEG - 1), sb = lane & ~(uint32_t)(SEG - 1);
+  const uint32_t deg = act ? d.in_cnt[vi] : 0u;
+  const uint32_t lw = act ? d.hs[vi].lock : 0u;
+  if (deg > (uint32_t)SEG || deg > d.DI) return false;  // segment-uniform
+  const uint4 hd = sl < deg ? d.in_hdr[(size_t)vi * d.DI + sl] : make_uint4(0xffffffffu, 0u, 0u, 0u);
+  uint32_t start = 0, total = 0;
+  for (uint32_t j = 0; j < (uint32_t)SEG; j++) {  // first record of this lane's packet in sender order
+    const uint32_t kj = (uint32_t)__shfl((int)hd.x, (int)(sb + j), 64);
+    const uint32_t lj = (uint32_t)__shfl((int)hd.z, (int)(sb + j), 64);
+    const bool before = j < deg && (kj < hd.x || (kj == hd.x && j < sl));
+    start += before ? lj : 0u;
+    total += j < deg ? lj : 0u;
+  }
+  const uint32_t nb0 = GX_LOCK_BUF(lw), room = d.C > nb0 ? d.C - nb0 : 0u;
+  const uint32_t keep = total < room ? total : room;
+  grec *dst = act ? &d.lkb[(size_t)vi * d.C + nb0] : d.lkb;
+  for (uint32_t o0 = 0; o0 < keep; o0 += SEG * LOCK_RPL) {
+    grec g[LOCK_RPL];
+#pragma unroll
+    for (int q = 0; q < LOCK_RPL; q++) {  // output record o: the packet whose [start, start + len) holds it
+      const uint32_t o = o0 + sl + SEG * q;
+      uint32_t entry = 0, slot = 0, off = 0;
+      for (uint32_t j = 0; j < deg; j++) {
+        const uint32_t sj = (uint32_t)__shfl((int)start, (int)(sb + j), 64);
+        const uint32_t lj = (uint32_t)__shfl((int)hd.z, (int)(sb + j), 64);
+        const uint32_t ej = (uint32_t)__shfl((int)hd.y, (int)(sb + j), 64);
+        const uint32_t wj = (uint32_t)__shfl((int)hd.w, (int)(sb + j), 64);
+        if (o >= sj && o < sj + lj) {
+          entry = ej;
+          slot = wj;
+          off = o - sj;
+        }
+      }
+      g[q] = gld_rec(&packet_recs(d, vi, slot, entry)[off]);  // past keep: a harmless inbox slot-0 read
+    }
+#pragma unroll
+    for (int q = 0; q < LOCK_RPL; q++) {
+      const uint32_t o = o0 + sl + SEG * q;
+      if (o < keep) gst_rec(&dst[o], g[q]);
+    }
+  }
+  if (act && sl == 0 && deg) {
+    d.hs[vi].lock = (lw & ((1u << GX_LOCK_BUF_SHIFT) - 1u)) | (nb0 + keep) << GX_LOCK_BUF_SHIFT;
+    ctr_atomic(d, C_LOCK_BUF, keep);
+    ctr_atomic(d, C_LOCK_DROP, total - keep);
+    kbytes(d, GX_K_MERGE, 32ull * keep + 16ull * deg + 4, 0);  // records in and out, headers
+  }
+  return true;
+}
+
 #define MERGE_NR 64  // receivers per block (16 measured 3% slower in the accepting stretch, profiles/r03/ab)
 #define MERGE_NONE 0xffffffffu
 template <bool K32, bool EV, int NR = MERGE_NR, int WPE = 3>
@@ -2536,7 +2595,7 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
   static_assert(NR <= 64, "one routing lane per receiver");
   __shared__ MergeLds s_l[MERGE_WAVES];
   __shared__ uint32_t s_it[NR][4];  // work items: up to 4 receivers (MERGE_NONE: empty)
-  __shared__ uint32_t s_ty[NR];     // 0: four 16-lane segments, 1: two 32-lane, 2: one wave
+  __shared__ uint32_t s_ty[NR];     // 0: four 16-lane segments, 1: two 32-lane, 2: one wave, 3: four locked
   __shared__ uint32_t s_fb[NR], s_n[2];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t r0 = blockIdx.x * NR;
@@ -2549,17 +2608,25 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
       for (int q = 0; q < 4; q++) s_it[lane][q] = MERGE_NONE;
     // the ServicesState lock (gx.h lock_model): a locked receiver with records, and an unlocked one
     // whose pipeline holds records to drain, take the whole-wave path (merge_receiver)
-    bool lkw = false;
+    // (round 5) a locked receiver takes a 16-lane pipeline append (lock_append_seg), four per wave
+    bool lkw = false, lka = false;
     if (d.p.lock_model && lane < (uint32_t)NR && vi < d.Hl) {
       const uint32_t lw = d.hs[vi].lock;
-      lkw = locked_in(d, lw) ? t != 0 : (GX_LOCK_BUF(lw) != 0 && !departed(d, d.lo + vi));
+      if (locked_in(d, lw)) lka = t != 0;
+      else lkw = GX_LOCK_BUF(lw) != 0 && !departed(d, d.lo + vi);
     }
-    const bool sm = !lkw && t && t <= 16, md = !lkw && t > 16 && t <= 32, lg = lkw || t > 32;
-    const uint64_t bs = __ballot(sm), bm = __ballot(md), bl = __ballot(lg), below = (1ull << lane) - 1ull;
+    const bool sm = !lkw && !lka && t && t <= 16, md = !lkw && !lka && t > 16 && t <= 32;
+    const bool lg = lkw || (!lka && t > 32);
+    const uint64_t bs = __ballot(sm), bm = __ballot(md), bl = __ballot(lg), ba = __ballot(lka), below = (1ull << lane) - 1ull;
     const uint32_t nl = (uint32_t)__popcll(bl), nm = (uint32_t)__popcll(bm), ns = (uint32_t)__popcll(bs);
-    const uint32_t nim = (nm + 1) / 2, nis = (ns + 3) / 4;
+    const uint32_t na = (uint32_t)__popcll(ba);
+    const uint32_t nim = (nm + 1) / 2, nis = (ns + 3) / 4, nia = (na + 3) / 4;
     wave_sync();
-    if (lg) {
+    if (lka) {
+      const uint32_t q = (uint32_t)__popcll(ba & below), it = nl + nim + nis + q / 4;
+      s_it[it][q & 3] = vi;
+      s_ty[it] = 3;
+    } else if (lg) {
       const uint32_t it = (uint32_t)__popcll(bl & below);
       s_it[it][0] = vi;
       s_ty[it] = 2;
@@ -2573,7 +2640,7 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
       s_ty[it] = 0;
     }
     if (lane == 0) {
-      s_n[0] = nl + nim + nis;
+      s_n[0] = nl + nim + nis + nia;
       s_n[1] = 0;
     }
     if (unsigned long long *kp = kprof_merge(d); kp && lane == 0 && (nl | nm | ns)) {  // diagnostics
@@ -2591,6 +2658,11 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
     const uint32_t ty = s_ty[it];
     if (ty == 2) {
       merge_receiver<K32, EV>(d, s_it[it][0], s_l[wv]);
+    } else if (ty == 3) {
+      const uint32_t v = s_it[it][lane >> 4];
+      const bool act = v != MERGE_NONE;
+      const bool ok = lock_append_seg<16>(d, act ? v : 0u, act);
+      if (!ok && (lane & 15) == 0) s_fb[atomicAdd(&s_n[1], 1u)] = v;
     } else if (ty == 1) {
       const uint32_t v = s_it[it][lane >> 5];
       const bool act = v != MERGE_NONE;
