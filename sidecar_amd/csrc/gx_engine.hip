@@ -592,10 +592,13 @@ static int ae_whole_impl(gx_engine *e) {
       // the ChangeEvent variant only while some view has a listener
       const bool ev = !e->log_views.empty();
       // nontemporal row loads and stores: -1% over the bench window (profiles/ab/ae_nt_ab_r02.log)
-      if (vec && !ev) k_ae<true, 1, true, true><<<np, 256, 0, s>>>(d, key0, key1);
-      else if (vec) k_ae_ev<true><<<np, 256, 0, s>>>(d, key0, key1);
-      else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
-      else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);
+      // chunks of pairs per block (ae_round_pair): a round whose pairs a lock skips costs one
+      // round trip per chunk, not a block per pair
+      const unsigned g = ae_grid(np, d.p.lock_model);
+      if (vec && !ev) k_ae<true, 1, true, true><<<g, 256, 0, s>>>(d, key0, key1, np);
+      else if (vec) k_ae_ev<true><<<g, 256, 0, s>>>(d, key0, key1, np);
+      else if (!ev) k_ae<false><<<g, 256, 0, s>>>(d, key0, key1, np);
+      else k_ae_ev<false><<<g, 256, 0, s>>>(d, key0, key1, np);
     }
     if (np && pp_state(d)) {  // pushPull's membership half (mergeState), from round-start lists
       LaunchTimer t(e, GX_K_FD);

@@ -3203,11 +3203,9 @@ GXD bool ae_lock_skip(const Dev &d, uint32_t a, uint32_t b, bool &locked) {
   }
   return d.p.lock_model != 0;
 }
-template <bool VEC, bool EV, int PF, bool NT, bool NTS = false>
-GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
-  __shared__ unsigned long long s_wave[4];
-  __shared__ unsigned long long s_red[4];
-  uint32_t t = blockIdx.x, base = 0, m = d.H, q = t;
+// Pair t of the round's perfect matching (halves while partitioned): hosts a, b.
+GXD void ae_pair_hosts(const Dev &d, uint32_t t, uint64_t key0, uint64_t key1, uint32_t &a, uint32_t &b) {
+  uint32_t base = 0, m = d.H, q = t;
   uint64_t key = key0;
   if (d.pair_split) {
     uint32_t m0 = d.H / 2, np0 = m0 / 2;
@@ -3220,33 +3218,78 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
       key = key1;
     }
   }
+  a = base + feistel_perm(key, 2 * q, m);
+  b = base + feistel_perm(key, 2 * q + 1, m);
+}
+// A block takes a chunk of up to 256 pairs (np / gridDim.x rounded up): each thread checks one
+// pair's members (a crashed member, the failure detector's view, the ServicesState lock) so the
+// chunk's skipped pairs cost one round trip together, then the block merges the pairs that run,
+// one after another. Pairs are disjoint, so their order does not matter.
+#define AE_GRID 4096
+template <bool VEC, bool EV, int PF, bool NT, bool NTS = false>
+GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1, uint32_t np) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  __shared__ uint32_t s_run[256];  // pair index | 1 << 31 when a side holds the lock (lock_model = 0)
+  __shared__ uint32_t s_nrun, s_nlock;
+  const uint32_t per = (np + gridDim.x - 1) / gridDim.x;  // <= 256 (the launch sizes the grid)
+  const uint32_t c0 = blockIdx.x * per, c1 = c0 + per < np ? c0 + per : np;
   unsigned long long *kp = kprof_ae(d);
   if (kp && threadIdx.x == 0) kp[2 * blockIdx.x] = wall_clock64() | ((unsigned long long)__smid() << 48);
-  uint32_t a = base + feistel_perm(key, 2 * q, m);
-  uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
-  // a crashed member skips the pair; with the failure detector the network path is needed and
-  // the initiator (a) must see b ALIVE (memberlist pushPull picks among alive nodes)
-  if (d.departures || d.p.fd_enable) {
-    bool ok = !departed(d, a) && !departed(d, b);
-    if (ok && d.p.fd_enable) ok = reach(d, a, b) && memp(d, a, b)->state == GX_M_ALIVE;
-    if (!ok) return;
+  if (threadIdx.x == 0) s_nrun = s_nlock = 0;
+  __syncthreads();
+  const uint32_t tq = c0 + threadIdx.x;
+  if (tq < c1) {
+    uint32_t a, b;
+    ae_pair_hosts(d, tq, key0, key1, a, b);
+    // a crashed member skips the pair; with the failure detector the network path is needed and
+    // the initiator (a) must see b ALIVE (memberlist pushPull picks among alive nodes)
+    bool ok = true;
+    if (d.departures || d.p.fd_enable) {
+      ok = !departed(d, a) && !departed(d, b);
+      if (ok && d.p.fd_enable) ok = reach(d, a, b) && memp(d, a, b)->state == GX_M_ALIVE;
+    }
+    if (ok) {
+      const bool locked = host_locked(d, a) || host_locked(d, b);
+      if (locked) atomicAdd(&s_nlock, 1u);
+      if (!(locked && d.p.lock_model)) s_run[atomicAdd(&s_nrun, 1u)] = tq | (locked ? 1u << 31 : 0u);
+    }
   }
-  bool locked;
-  if (ae_lock_skip(d, a, b, locked)) return;
-  ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red, nullptr, false, nullptr, locked);
+  __syncthreads();
+  const uint32_t nrun = s_nrun;
+  if (threadIdx.x == 0 && s_nlock) {
+    atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
+    if (d.p.lock_model) ctr_atomic(d, C_AE_LOCKED, s_nlock);
+  }
+  for (uint32_t k = 0; k < nrun; k++) {
+    const uint32_t x = s_run[k];
+    uint32_t a, b;
+    ae_pair_hosts(d, x & 0x7fffffffu, key0, key1, a, b);
+    ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red, nullptr, false, nullptr, (x >> 31) != 0);
+    __syncthreads();  // the next pair's shared state
+  }
   if (kp && threadIdx.x == 0) kp[2 * blockIdx.x + 1] = wall_clock64();
+}
+// Blocks of a push-pull launch: one pair per block without the lock model (blocks are scheduled as
+// CUs free up, which evens out pairs of different cost: static chunks of 4 pairs measured 4% slower
+// over the bench window, profiles/r05/c5), chunks of at most 256 pairs with it (a locked round's
+// pairs then cost 17 us instead of a contended counter atomic per pair).
+GXHD uint32_t ae_grid(uint32_t np, uint32_t lock_model) {
+  if (!lock_model) return np;
+  const uint32_t g = np < AE_GRID ? np : AE_GRID;
+  return g > (np + 255) / 256 ? g : (np + 255) / 256;
 }
 
 // The push-pull kernel, without ChangeEvents (no listener anywhere): kept within 128 VGPRs so
 // that 4 waves per SIMD stay resident; with events (listeners present) a separate entry point.
 template <bool VEC, int PF = 1, bool NT = false, bool NTS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae(Dev d, uint64_t key0,
-                                                                                   uint64_t key1) {
-  ae_round_pair<VEC, false, PF, NT, NTS>(d, key0, key1);
+                                                                                   uint64_t key1, uint32_t np) {
+  ae_round_pair<VEC, false, PF, NT, NTS>(d, key0, key1, np);
 }
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_ae_ev(Dev d, uint64_t key0, uint64_t key1) {
-  ae_round_pair<VEC, true, 1, false>(d, key0, key1);
+__global__ __launch_bounds__(256) void k_ae_ev(Dev d, uint64_t key0, uint64_t key1, uint32_t np) {
+  ae_round_pair<VEC, true, 1, false>(d, key0, key1, np);
 }
 
 template <bool VEC, bool EV>
