@@ -2539,10 +2539,13 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
 template <int SEG>
 GXD bool lock_append_seg(const Dev &d, uint32_t vi, bool act) {
   const uint32_t lane = threadIdx.x & 63, sl = lane & (SEG - 1), sb = lane & ~(uint32_t)(SEG - 1);
+  // the count, the lock word and the first SEG header slots in one round trip (slots past the
+  // count hold stale headers and are masked below)
   const uint32_t deg = act ? d.in_cnt[vi] : 0u;
   const uint32_t lw = act ? d.hs[vi].lock : 0u;
+  uint4 hd = d.in_hdr[(size_t)vi * d.DI + (sl < d.DI ? sl : 0u)];
   if (deg > (uint32_t)SEG || deg > d.DI) return false;  // segment-uniform
-  const uint4 hd = sl < deg ? d.in_hdr[(size_t)vi * d.DI + sl] : make_uint4(0xffffffffu, 0u, 0u, 0u);
+  if (sl >= deg) hd = make_uint4(0xffffffffu, 0u, 0u, 0u);
   uint32_t start = 0, total = 0;
   for (uint32_t j = 0; j < (uint32_t)SEG; j++) {  // first record of this lane's packet in sender order
     const uint32_t kj = (uint32_t)__shfl((int)hd.x, (int)(sb + j), 64);
