@@ -104,7 +104,7 @@ enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS =
 struct Dev {
   gx_params p;      // t0_ns epoch-relative (gx.h GX_TS_SHIFT)
   int64_t epoch;    // absolute time of slot time 0
-  uint32_t H, S, R, Q, A, L, SQ, DQ, K;
+  uint32_t H, S, R, Q, A, L, SQ, DQ, K;  // SQ and DQ are powers of two (ring index = position & (size - 1))
   uint32_t NG, KE;           // GossipMessages gathers per target; packet entries per host = K * NG
   uint32_t lo, Hl, G, gid;  // this engine owns hosts [lo, lo + Hl); per-host arrays are local
   uint32_t n_remote;        // packets received from other shards this round
@@ -443,7 +443,8 @@ GXD uint32_t fifo_room(const Dev &d, uint32_t head, uint32_t tail, uint32_t stor
 GXD uint32_t *list_bits(const Dev &d, uint32_t vi, uint32_t w) { return &d.arena_bits[(size_t)vi * d.AW + w]; }
 GXD void list_release(const Dev &d, uint32_t vi, uint32_t &arena_used, uint32_t slot, bool lane0) {
   if (slot >= d.A) return;  // GX_LIST_NONE: a SendServices job queued deferred holds no list
-  if (lane0) *list_bits(d, vi, slot >> 5) &= ~(1u << (slot & 31));
+  // (a non-returning atomic: the sends do not wait for the word; only this host's team touches it)
+  if (lane0) atomicAnd(list_bits(d, vi, slot >> 5), ~(1u << (slot & 31)));
   arena_used &= ~(1u << (slot >> 5));
 }
 // Allocates on the team-uniform register copy `arena_used`; -1 when every slot is live. Every
@@ -454,10 +455,12 @@ GXD int list_alloc(const Dev &d, uint32_t vi, uint32_t &arena_used, bool lane0) 
   if (!wfree) return -1;
   const uint32_t w = (uint32_t)__builtin_ctz(wfree);
   uint32_t *p = list_bits(d, vi, w);
-  uint32_t word = lane0 ? *p : 0u;
+  // atomic (L2) accesses: list_release clears bits with a non-returning atomic, which a plain load
+  // of the same launch could miss in the vector L1
+  uint32_t word = lane0 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   if (T > 1) word = (uint32_t)__shfl((int)word, 0, T);
   const uint32_t b = (uint32_t)__builtin_ctz(~word), nw = word | (1u << b);
-  if (lane0) *p = nw;
+  if (lane0) __hip_atomic_store(p, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (nw == 0xffffffffu) arena_used |= 1u << w;
   return (int)(w * 32 + b);
 }
@@ -488,7 +491,7 @@ GXD void push_sleep_r(const Dev &d, Acc &a, uint32_t v, gx_host_state &hs, const
     return;
   }
   if (lane0) {  // two 16-B stores: the job, then wake and padding
-    gx_sleeper *z = &d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail % d.SQ)];
+    gx_sleeper *z = &d.sleep[(size_t)li(d, v) * d.SQ + (hs.sleep_tail & (d.SQ - 1u))];
     gx_u32x4 x0, x1;
     x0.x = (uint32_t)j.a;
     x0.y = (uint32_t)(j.a >> 32);
@@ -532,7 +535,7 @@ GXD void free_list(const Dev &d, uint32_t v, const gx_job &j) {
 GXD void wake_host(const Dev &d, Acc &a, uint32_t v) {
   gx_host_state *h = hst(d, v);
   while (h->sleep_head != h->sleep_tail) {
-    const gx_sleeper &z = d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_head % d.SQ)];
+    const gx_sleeper &z = d.sleep[(size_t)li(d, v) * d.SQ + (h->sleep_head & (d.SQ - 1u))];
     if ((int64_t)z.wake > d.round) break;
     const gx_job j = z.job;
     h->sleep_head++;

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
       hs.fifo_stored = h->fifo_stored;
       const uint32_t au0 = hs.arena_used;
       while (hs.sleep_head != hs.sleep_tail) {  // re-armed passes: SEND / EXPIRE, never a nil
-        const gx_sleeper &z = d.sleep[(size_t)idx * d.SQ + (hs.sleep_head % d.SQ)];
+        const gx_sleeper &z = d.sleep[(size_t)idx * d.SQ + (hs.sleep_head & (d.SQ - 1u))];
         if ((int64_t)z.wake > d.round) break;
         const gx_job j = z.job;
         hs.sleep_head++;
@@ -292,7 +292,7 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
     {  // the sleep ring's head: T slots, or SW under GossipMessages > 1 (a round re-arms up to
        // fanout * GossipMessages passes, and they wake together)
       const uint32_t ns = hs.sleep_tail - hs.sleep_head, win = d.NG > 1 ? (uint32_t)SW : (uint32_t)T;
-      for (uint32_t x = tl; x < ns && x < win; x += T) sj[x] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + x) % d.SQ)];
+      for (uint32_t x = tl; x < ns && x < win; x += T) sj[x] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + x) & (d.SQ - 1u))];
     }
     if (FWD) {  // the tick pushes at the FIFO tail only: the stored jobs at the head stay where they are
       const uint32_t q = hs.fifo_stored - hs.fifo_head;
@@ -340,7 +340,7 @@ GXD bool owner_tick(const Dev &d, Acc &a, uint32_t idx, gx_sleeper *sj, TickFwd 
           const uint32_t ns = hs.sleep_tail - hs.sleep_head;
           wave_sync();
           for (uint32_t x = tl; x < ns && x < win; x += T)
-            sj[x] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + x) % d.SQ)];
+            sj[x] = d.sleep[(size_t)idx * d.SQ + ((hs.sleep_head + x) & (d.SQ - 1u))];
           wave_sync();
           w = 0;
         }
@@ -1263,6 +1263,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   const uint64_t tmask = T == 64 ? ~0ull : ((1ull << T) - 1ull);
   const uint32_t u = d.lo + idx, cap = d.p.packet_cap, mask = d.DQ - 1;
   grec *dq = &d.dq[(size_t)idx * d.DQ];
+  grec *const arena_t = &d.arena[(size_t)idx * d.A * d.L];  // the host's SendServices lists
   // the team's message entries (its packets' records and filter words): entry x = idx * KE + k
   grec *const msg_t = &d.msg[(size_t)idx * d.KE * cap];
   uint64_t *const w0_t = &d.msg_w0[(size_t)idx * d.KE * cap];
@@ -1363,7 +1364,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
           c.rb = jb.c;
         } else if (kind == GX_JOB_SEND) {
           c.bw = dw;
-          c.list = list_ptr(d, u, jb.c & 0xffff);
+          c.list = arena_t + (size_t)(jb.c & 0xffffu) * d.L;  // list_ptr(d, u, slot)
         } else if (kind == GX_JOB_EXPIRE) {  // Tombstone() at the call's now
           c.bw = pack(d.p.t0_ns + (int64_t)jb.c * d.p.round_ns, GX_TOMBSTONE) + dw;
           c.rb = GX_JOB_OWNER(jb.meta) * d.S;
@@ -4293,7 +4294,7 @@ __global__ void k_digest(Dev d, uint64_t *out) {
   h = feed(h, 0xF1F0);
   h = feed(h, (uint64_t)(s.fifo_tail - s.fifo_stored) | ((uint64_t)s.fifo_stored << 32));
   for (uint32_t i = s.sleep_head; i != s.sleep_tail; i++) {
-    const gx_sleeper z = d.sleep[(size_t)v * d.SQ + (i % d.SQ)];
+    const gx_sleeper z = d.sleep[(size_t)v * d.SQ + (i & (d.SQ - 1u))];
     h = feed(h, feed_job(z.wake, z.job));
   }
   h = feed(h, 0x51EE);
