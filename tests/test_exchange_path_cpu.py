@@ -90,3 +90,62 @@ def test_dist_shard_takes_the_planned_exchange(oracle_lib, gm, planned):
     whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
     whole.run_rounds(6)
     assert res[0][2] == whole.stats()["gossip_merges"]
+
+
+def test_fused_round_calls_equal_separate_calls(oracle_lib):
+    """gx_round_gossip_begin / _end (ABI 8, what DistShard's planned path calls) do exactly the work
+    of round_send + exchange_plan + outbox_pack_planned and inbox_unpack + round_merge (+ round_end
+    outside push-pull rounds): two 2-shard clusters, one stepped each way with the same in-process
+    exchange, end with equal digests, host bookkeeping and counters."""
+    import numpy as np
+    kw = dict(BASE, gossip_messages=1)
+
+    def cluster():
+        out = []
+        for g in range(2):
+            p = default_params(oracle_lib, **kw)
+            p.n_shards, p.shard_id = 2, g
+            out.append(Engine(p, lib=oracle_lib))
+        return out
+
+    def step(es, fused):
+        bufs, plans = [], []
+        for e in es:
+            plan = np.zeros(4, dtype=np.uint64)
+            cap = int(e.params.n_hosts * e.params.fanout * (16 + 16 * e.params.packet_cap))
+            buf = np.zeros(cap, dtype=np.uint8)
+            if fused:
+                e.round_gossip_begin(plan, buf.ctypes.data, cap)
+            else:
+                e.round_send()
+                plan[:] = e.exchange_plan().reshape(-1)
+                e.outbox_pack_planned(buf.ctypes.data, cap)
+            bufs.append(buf)
+            plans.append(plan.reshape(2, 2))
+        m = plans[0]
+        ae = []
+        for g, e in enumerate(es):
+            src = 1 - g
+            off = int(m[src][:g].sum())
+            n = int(m[src][g])
+            x = np.ascontiguousarray(bufs[src][off:off + n])
+            if fused:
+                ae.append(e.round_gossip_end(x.ctypes.data, n))
+            else:
+                e.inbox_unpack(x.ctypes.data, n)
+                e.round_merge()
+                ae.append(e.is_ae_round())
+        assert ae[0] == ae[1]
+        for e in es:  # (no push-pull round in these steps: the caller would run it before round_end)
+            if not fused or ae[0]:
+                e.round_end()
+
+    a, b = cluster(), cluster()
+    for _ in range(4):  # rounds 0..3: ae_period_rounds 5 keeps push-pull out
+        step(a, True)
+        step(b, False)
+    for ea, eb in zip(a, b):
+        assert ea.round == eb.round == 4
+        assert np.array_equal(ea.digests(), eb.digests())
+        assert [bytes(h) for h in ea.hosts()] == [bytes(h) for h in eb.hosts()]
+        assert ea.stats() == eb.stats()
