@@ -101,8 +101,11 @@ enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5, ST_INIT_AGE = 6,
        ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11 };
 
+#define XPLAN_BATCH 64  // rounds of planned-exchange slot bounds per k_xplan launch
+#define XPLAN_GMAX 64   // shards the planned exchange supports
+
 struct Dev {
-  gx_params p;      // t0_ns epoch-relative (gx.h GX_TS_SHIFT)
+  gx_params p;     // t0_ns epoch-relative (gx.h GX_TS_SHIFT)
   int64_t epoch;    // absolute time of slot time 0
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;  // SQ and DQ are powers of two (ring index = position & (size - 1))
   uint32_t NG, KE;           // GossipMessages gathers per target; packet entries per host = K * NG
@@ -180,6 +183,11 @@ struct Dev {
   uint32_t PW;         // words per host of pexp, ceil(H / 32)
   uint32_t *pexp;      // [Hl][PW] owners whose ExpireServer waits for the host's lock
   int in_round;        // a round phase is running: ExpireServer waits for the lock (ABI calls act directly)
+  // The planned exchange packed by k_send itself (gx_round_gossip_begin): a packet to another shard
+  // is written straight into its slot of the send buffer. Set only for that launch.
+  uint8_t *ob_buf;           // the send buffer (slots of 16 + 16 * packet_cap bytes), or null
+  const uint32_t *ob_cnt;    // [G] slots this shard sends each shard this round (k_xplan's row, on the device)
+  uint32_t *ob_claim;        // [XPLAN_GMAX] slots claimed per destination, [XPLAN_GMAX] blocks done; reset by the last block
   unsigned long long *kprof;  // diagnostics (env GX_KPROF): wall-clock phase marks of k_send per wave, or null
 };
 

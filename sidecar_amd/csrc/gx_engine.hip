@@ -142,13 +142,16 @@ struct gx_engine {
   // planned gossip exchange (gx_exchange_plan): slot bounds of XPLAN_BATCH rounds computed ahead on
   // xplan_stream into pinned host memory, two batches (the current one and the next)
   hipStream_t xplan_stream;
-  uint32_t *xplan_dev;           // [XPLAN_BATCH][G][G]
+  uint32_t *xplan_dev;           // [2][XPLAN_BATCH][G][G] (k_send of a packing round reads its row)
   uint32_t *xplan_host;          // [2][XPLAN_BATCH][G][G] pinned
   int64_t xplan_start[2];
   uint64_t xplan_waits[2];       // diagnostics: calls whose batch was not ready yet (a host wait) / all calls
   hipEvent_t xplan_ev[2];
+  hipEvent_t xplan_join;         // a batch is rewritten after the rounds queued before it (xplan_launch)
   int64_t xbound_round;          // the round xbound holds
   XBound xbound;                 // this shard's slots per destination this round
+  const uint32_t *xbound_dev;    // the same row on the device
+  uint32_t *ob_claim;            // Dev::ob_claim (gx_round_gossip_begin packing in k_send)
 };
 
 static void codec_free(gx_engine *e);  // gx_codec_host.hpp
@@ -501,6 +504,9 @@ static int round_merge_impl(gx_engine *e) {
   return GX_OK;
 }
 
+#ifndef GX_AE_PF_LOCK
+#define GX_AE_PF_LOCK 1  // 2 tiles in flight spill (92 B scratch): 0.98 vs 0.71 ms at cfg 5 lock on (profiles/r05/ab/ae_pf_lock.jsonl)
+#endif
 static bool ae_round(const gx_engine *e) {
   const Dev &d = e->d;
   return d.p.ae_period_rounds && (uint64_t)d.round % d.p.ae_period_rounds == d.p.ae_phase;
@@ -592,13 +598,14 @@ static int ae_whole_impl(gx_engine *e) {
       // the ChangeEvent variant only while some view has a listener
       const bool ev = !e->log_views.empty();
       // nontemporal row loads and stores: -1% over the bench window (profiles/ab/ae_nt_ab_r02.log)
-      // chunks of pairs per block (ae_round_pair): a round whose pairs a lock skips costs one
-      // round trip per chunk, not a block per pair
-      const unsigned g = ae_grid(np, d.p.lock_model);
-      if (vec && !ev) k_ae<true, 1, true, true><<<g, 256, 0, s>>>(d, key0, key1, np);
-      else if (vec) k_ae_ev<true><<<g, 256, 0, s>>>(d, key0, key1, np);
-      else if (!ev) k_ae<false><<<g, 256, 0, s>>>(d, key0, key1, np);
-      else k_ae_ev<false><<<g, 256, 0, s>>>(d, key0, key1, np);
+      // under the lock model chunks of pairs per block (ae_round_pairs): a round whose pairs a lock
+      // skips costs one round trip per chunk, not a block per pair
+      if (vec && !ev && d.p.lock_model)
+        k_ae_chunk<true, GX_AE_PF_LOCK, true, true><<<ae_grid(np, 1), 256, 0, s>>>(d, key0, key1, np);
+      else if (vec && !ev) k_ae<true, 1, true, true><<<np, 256, 0, s>>>(d, key0, key1);
+      else if (vec) k_ae_ev<true><<<np, 256, 0, s>>>(d, key0, key1);
+      else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
+      else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);
     }
     if (np && pp_state(d)) {  // pushPull's membership half (mergeState), from round-start lists
       LaunchTimer t(e, GX_K_FD);
@@ -760,7 +767,7 @@ int gx_destroy(gx_engine *e) {
     (void)hipEventDestroy(t.b);
   }
   Dev &d = e->d;
-  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, d.in_stamp, e->ob_entries, e->ob_counts, e->ob_total, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
+  void *ptrs[] = {e->ae_dig, e->ae_mask, e->ae_fmask, e->ae_lt, e->ae_retL, e->ae_bcnt, e->ae_cnt, e->ae_nfol, e->ae_sz, e->ae_off, e->ae_rioff, e->ae_err, d.msg_key, d.in_stamp, e->ob_entries, e->ob_counts, e->ob_total, e->ob_claim, e->ae_pa, e->ae_pb, e->ae_pack_host, e->ae_pack_t, e->ae_pack_other, e->ae_pack_first, e->ae_skip, e->fd_rsnap, e->ae_prow,
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_w0, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mrec, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
@@ -778,6 +785,7 @@ int gx_destroy(gx_engine *e) {
   if (e->xplan_host) (void)hipHostFree(e->xplan_host);
   for (int i = 0; i < 2; i++)
     if (e->xplan_ev[i]) (void)hipEventDestroy(e->xplan_ev[i]);
+  if (e->xplan_join) (void)hipEventDestroy(e->xplan_join);
   if (e->xplan_stream) (void)hipStreamDestroy(e->xplan_stream);
   delete e;
   return GX_OK;
@@ -826,6 +834,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->n_ob = 0;
   e->ob_async = false;
   e->ob_total = nullptr;
+  e->ob_claim = nullptr;
   e->ae_pa = e->ae_pb = e->ae_pack_host = e->ae_pack_t = e->ae_pack_other = nullptr;
   e->ae_pack_first = e->ae_skip = nullptr;
   e->fd_rsnap = nullptr;
@@ -959,7 +968,9 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->xplan_start[0] = e->xplan_start[1] = -1;
   e->xplan_waits[0] = e->xplan_waits[1] = 0;
   e->xplan_ev[0] = e->xplan_ev[1] = nullptr;
+  e->xplan_join = nullptr;
   e->xbound_round = -1;
+  e->xbound_dev = nullptr;
   e->kprof_n = 0;
   if (getenv("GX_KPROF")) {  // diagnostics: phase marks of every k_send wave (gx_kprof_read)
     e->kprof_n = (size_t)nblk(d.Hl, 64) * 4 * 8 + GX_KPROF_MERGE_N + 3ull * d.H;  // + merge counts + push-pull blocks + scans
@@ -972,6 +983,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
     ALLOC(d.in_stamp, sizeof(uint32_t) * Hg * K);
     HIPCHK(hipMemset(d.in_stamp, 0, sizeof(uint32_t) * Hg * K));
     ALLOC(e->ob_total, sizeof(uint32_t));
+    ALLOC(e->ob_claim, sizeof(uint32_t) * (XPLAN_GMAX + 1));
+    HIPCHK(hipMemset(e->ob_claim, 0, sizeof(uint32_t) * (XPLAN_GMAX + 1)));
     ALLOC(e->ob_counts, sizeof(uint32_t) * p->n_shards * (1 + 2 * ((H * K + 255) / 256)));
     size_t np = Hg / 2 + 1;
     ALLOC(e->ae_pa, sizeof(uint32_t) * np);
@@ -1859,10 +1872,14 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
 static int xplan_launch(gx_engine *e, int k, int64_t start) {
   Dev &d = e->d;
   const size_t n = (size_t)XPLAN_BATCH * d.G * d.G;
-  HIPCHK(hipMemsetAsync(e->xplan_dev, 0, sizeof(uint32_t) * n, e->xplan_stream));
-  k_xplan<<<dim3(nblk(d.H, 256), XPLAN_BATCH), 256, 0, e->xplan_stream>>>(d, start, e->xplan_dev);
+  uint32_t *dev = e->xplan_dev + (size_t)k * n;
+  // the rounds queued so far may read this half (a packing k_send): the rewrite waits for them
+  HIPCHK(hipEventRecord(e->xplan_join, e->stream));
+  HIPCHK(hipStreamWaitEvent(e->xplan_stream, e->xplan_join, 0));
+  HIPCHK(hipMemsetAsync(dev, 0, sizeof(uint32_t) * n, e->xplan_stream));
+  k_xplan<<<dim3(nblk(d.H, 256), XPLAN_BATCH), 256, 0, e->xplan_stream>>>(d, start, dev);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(e->xplan_host + (size_t)k * n, e->xplan_dev, sizeof(uint32_t) * n, hipMemcpyDeviceToHost,
+  HIPCHK(hipMemcpyAsync(e->xplan_host + (size_t)k * n, dev, sizeof(uint32_t) * n, hipMemcpyDeviceToHost,
                         e->xplan_stream));
   HIPCHK(hipEventRecord(e->xplan_ev[k], e->xplan_stream));
   e->xplan_start[k] = start;
@@ -1876,7 +1893,8 @@ static int xplan_counts(gx_engine *e, const uint32_t **out) {
     if (hipStreamCreateWithFlags(&e->xplan_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&e->xplan_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->xplan_ev[1], hipEventDisableTiming) != hipSuccess ||
-        hipMalloc((void **)&e->xplan_dev, sizeof(uint32_t) * XPLAN_BATCH * d.G * d.G) != hipSuccess ||
+        hipEventCreateWithFlags(&e->xplan_join, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc((void **)&e->xplan_dev, sizeof(uint32_t) * 2 * XPLAN_BATCH * d.G * d.G) != hipSuccess ||
         hipHostMalloc((void **)&e->xplan_host, sizeof(uint32_t) * 2 * XPLAN_BATCH * d.G * d.G) != hipSuccess) {
       (void)hipGetLastError();
       return GX_ENOMEM;
@@ -1896,7 +1914,9 @@ static int xplan_counts(gx_engine *e, const uint32_t **out) {
   } else {
     HIPCHK(q);
   }
-  *out = e->xplan_host + ((size_t)k * XPLAN_BATCH + (size_t)(d.round - start)) * d.G * d.G;
+  const size_t row = ((size_t)k * XPLAN_BATCH + (size_t)(d.round - start)) * d.G * d.G;
+  *out = e->xplan_host + row;
+  e->xbound_dev = e->xplan_dev + row + (size_t)d.gid * d.G;
   return GX_OK;
 }
 
@@ -2312,11 +2332,38 @@ int gx_round_end(gx_engine *e) {
   return rc ? rc : phase_done(e);
 }
 
+// A round whose k_send packs the planned exchange itself (Dev::ob_buf): send_planned's rounds
+// (round_send_impl's `plan`) with one message per target.
+static bool send_packs(const Dev &d) {
+  return d.G >= 2 && d.K && d.NG == 1 && !d.p.limit_bytes && d.p.retransmit_rounds > 0 && !d.departures &&
+         !d.p.fd_enable;
+}
+
 int gx_round_gossip_begin(gx_engine *e, uint64_t *plan, void *buf, uint64_t cap) {
-  if (!e || !plan) return GX_EINVAL;
-  int rc = gx_round_send(e);
-  if (!rc) rc = gx_exchange_plan(e, plan);
-  if (!rc) rc = gx_outbox_pack_planned(e, buf, cap);
+  if (!e || !plan || (cap && !buf)) return GX_EINVAL;
+  Dev &d = e->d;
+  if (!send_packs(d)) {
+    int rc = gx_round_send(e);
+    if (!rc) rc = gx_exchange_plan(e, plan);
+    if (!rc) rc = gx_outbox_pack_planned(e, buf, cap);
+    return rc;
+  }
+  // the plan first (its batch is on the device since the host saw it done), then one launch that
+  // sends and writes every slot of the buffer
+  int rc = gx_exchange_plan(e, plan);
+  if (rc) return rc;
+  uint64_t slots = 0;
+  for (uint32_t g = 0; g < d.G; g++) slots += e->xbound.n[g];
+  if (cap < slots * slot_bytes(d)) return GX_EINVAL;
+  d.ob_buf = (uint8_t *)buf;
+  d.ob_cnt = e->xbound_dev;
+  d.ob_claim = e->ob_claim;
+  rc = gx_round_send(e);
+  d.ob_buf = nullptr;
+  d.ob_cnt = nullptr;
+  d.ob_claim = nullptr;
+  e->n_ob = 0;
+  e->ob_async = false;
   return rc;
 }
 

@@ -1221,7 +1221,19 @@ struct PlanCall {
   uint32_t peer;      // receiver (global id)
   uint32_t lpre;      // records of the chunk's earlier calls
   uint32_t lk;        // the receiver (on this shard) holds the ServicesState lock this round
+  uint32_t oslot;     // the packet's slot in the planned send buffer (Dev::ob_buf), or GX_NOSLOT
 };
+// The receiver's shard (hosts in contiguous blocks, floor(g * H / G) the first of shard g).
+GXD uint32_t shard_of_d(const Dev &d, uint32_t v) {
+  uint32_t g = (uint32_t)(((uint64_t)v * d.G) / d.H);
+  while (g > 0 && (uint32_t)(((uint64_t)g * d.H) / d.G) > v) g--;
+  while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= v) g++;
+  return g;
+}
+// Slot header and records of the planned send buffer (k_outbox_pack_planned's layout).
+GXD uint32_t *ob_slot_hdr(const Dev &d, uint32_t slot) {
+  return reinterpret_cast<uint32_t *>(d.ob_buf + (size_t)slot * (16u + 16u * d.p.packet_cap));
+}
 static_assert(sizeof(PlanCall) >= 17 * sizeof(uint32_t), "a PlanCall slot holds a team's 16 peers and their count");
 #define GX_NOSLOT 0xffffffffu  // inbox header slot: the records are in the message entry
 // ... and each carries the receiver's slot word it was filtered against (msg_w0). Between that read
@@ -1275,6 +1287,68 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
   bool stop = np == 0;
   unsigned fm = 0, fs = 0, nlines = 0;
   GX_SPLIT_DECL
+  const bool lmod = d.p.lock_model != 0;
+  // The planned exchange packed here (Dev::ob_buf; GossipMessages 1, so entry j = peer j): every
+  // peer on another shard gets a slot of its shard's region up front (lane tl claims for peers
+  // tl + T * r), written with the packet's header and records, or as an empty slot at the end.
+  constexpr int NR = (16 + T - 1) / T;
+  const bool direct = d.ob_buf != nullptr;
+  uint32_t osl[NR];
+  uint32_t emit = 0;  // team-uniform: peers whose packet went into its slot
+#pragma unroll
+  for (int r = 0; r < NR; r++) osl[r] = GX_NOSLOT;
+  // One atomic per destination shard per wave (thousands of single claims on G counters queue
+  // at L2): the wave's claims for a shard take consecutive places in (r, lane) order, and the
+  // first of them claims the run; every run's atomic is in flight at once, beside the lock loads.
+  uint32_t og[NR], rk[NR], ksrc[NR], krun[NR], lc[NR], lb[NR], le[NR];
+  if (direct) {
+    unsigned long long pend[NR];
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      const uint32_t jj = (uint32_t)r * T + tl;
+      og[r] = jj < np && peers[jj] - d.lo >= d.Hl ? shard_of_d(d, peers[jj]) : d.G;
+      pend[r] = __ballot(og[r] < d.G);
+      rk[r] = ksrc[r] = krun[r] = lc[r] = 0;
+    }
+    for (;;) {  // wave-uniform: one pass per destination shard the wave sends to
+      int r0 = -1;
+#pragma unroll
+      for (int r = NR - 1; r >= 0; r--) r0 = pend[r] ? r : r0;
+      if (r0 < 0) break;
+      unsigned long long p0 = pend[0];
+      uint32_t g0 = og[0];
+#pragma unroll
+      for (int r = 1; r < NR; r++) {
+        p0 = r == r0 ? pend[r] : p0;
+        g0 = r == r0 ? og[r] : g0;
+      }
+      const uint32_t src = (uint32_t)__builtin_ctzll(p0);  // the run's first claim: (src, r0)
+      const uint32_t gs = (uint32_t)__shfl((int)g0, (int)src, 64);
+      uint32_t acc = 0;
+#pragma unroll
+      for (int r = 0; r < NR; r++) {
+        const unsigned long long m = __ballot(og[r] == gs);
+        if (og[r] == gs) {
+          rk[r] = acc + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          ksrc[r] = src;
+          krun[r] = (uint32_t)r0;
+        }
+        acc += (uint32_t)__popcll(m);
+        pend[r] &= ~m;
+      }
+#pragma unroll
+      for (int r = 0; r < NR; r++)
+        if (r == r0 && lane == src) lc[r] = acc;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; r++) {  // a run's places: its first claim's registers (used after the lock loads)
+      lb[r] = le[r] = 0;
+      if (lc[r]) {
+        lb[r] = atomicAdd(&d.ob_claim[og[r]], lc[r]);
+        le[r] = d.ob_cnt[og[r]];
+      }
+    }
+  }
   // the receivers' ServicesState lock this round (gx.h lock_model): bit j = peer j, on this shard,
   // holds it. A locked receiver's records all go to its pipeline (k_merge_seg), so they are stored
   // unfiltered and the receiver counts them; with lock_model = 0 they merge and are counted as locked.
@@ -1289,7 +1363,31 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
     lkm |= (uint32_t)((__ballot(lk) >> (tw * T)) & tmask) << j0;
     fullm |= (uint32_t)((__ballot(lk && GX_LOCK_BUF(lw) >= d.C) >> (tw * T)) & tmask) << j0;
   }
-  const bool lmod = d.p.lock_model != 0;
+  if (direct) {
+#pragma unroll
+    for (int r = 0; r < NR; r++) {  // [lb, le): the run's places in the buffer (region start + claim)
+      if (lc[r]) {  // a run starts at this claim
+        uint32_t st = 0;
+        for (uint32_t x = 0; x < og[r]; x++) st += d.ob_cnt[x];
+        if (lb[r] + lc[r] > le[r]) atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);  // past the plan's bound (cannot happen)
+        lb[r] += st;
+        le[r] += st;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      uint32_t b = 0, e = 0;
+#pragma unroll
+      for (int r2 = 0; r2 < NR; r2++) {
+        const uint32_t x = (uint32_t)__shfl((int)lb[r2], (int)ksrc[r], 64), y = (uint32_t)__shfl((int)le[r2], (int)ksrc[r], 64);
+        if (krun[r] == (uint32_t)r2) {
+          b = x;
+          e = y;
+        }
+      }
+      if (og[r] < d.G && b + rk[r] < e) osl[r] = b + rk[r];
+    }
+  }
   while (!stop) {
 #ifdef GX_SEND_SPLIT
     sp_n++;
@@ -1311,6 +1409,13 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       c.lk = ((lkm >> j) & 1u) | (lmod ? ((fullm >> j) & 1u) << 1 : 0u);
       c.x = idx * d.KE + j * d.NG + n;
       c.key = u * d.KE + j * d.NG + n;
+      c.oslot = GX_NOSLOT;
+      if (direct && !c.row) {  // peer j's claimed slot (lane j % T of the team, register j / T)
+        uint32_t v = osl[0];
+#pragma unroll
+        for (int r = 1; r < NR; r++) v = j / T == (uint32_t)r ? osl[r] : v;
+        c.oslot = (uint32_t)__shfl((int)v, (int)(j % T), T);
+      }
       bool empty = false;
       if (hs.fifo_head != hs.fifo_tail) {  // case broadcast = <-d.state.Broadcasts (:94)
         gx_job jb = make_job(0, 0, 0);
@@ -1412,6 +1517,7 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       c.l = l;
       c.lpre = tot;
       if (l) {  // (a dropped packet stays in the plan for its pending-ring writes; no record of it loads)
+        if (c.oslot != GX_NOSLOT) emit |= 1u << j;
         if (lead) pl[nc] = c;
         nc++;
         if (!(c.lk & 2u)) tot += l;
@@ -1545,7 +1651,8 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
           g.r = r[q];
           g.pad = 0;
           const uint32_t xo = (c.x - idx * d.KE) * cap + rank;  // within the team's entries
-          gst_rec(&msg_t[xo], g);
+          grec *to = c.oslot != GX_NOSLOT ? reinterpret_cast<grec *>(ob_slot_hdr(d, c.oslot) + 4) + rank : &msg_t[xo];
+          gst_rec(to, g);
           if (filt) gst(&w0_t[xo], w0[q]);
         }
         run += (uint32_t)__popcll(lm);
@@ -1573,6 +1680,8 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
       if (c.lk & 2u) stored = 0;
       d.msg_len[c.x] = stored;
       d.msg_dst[c.x] = c.peer;
+      if (c.oslot != GX_NOSLOT)  // the slot header (k_outbox_pack_planned's pack_slot)
+        *reinterpret_cast<uint4 *>(ob_slot_hdr(d, c.oslot)) = make_uint4(c.key, c.peer, stored, 0u);
       if (c.row && stored) {  // a locked receiver reads its slots itself (no forwarded words)
         inbox_header(d, rv, inbox_claim(d, rv), c.key, c.x, stored, lmod && c.lk ? GX_NOSLOT : GX_NOSLOT_W0);
         flag_live(d, rv, stored);
@@ -1596,6 +1705,10 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
     GX_SPLIT(3);
   }
   GX_SPLIT_FLUSH();
+#pragma unroll
+  for (int r = 0; r < NR; r++)  // claimed slots no packet went into: empty (the receiver skips them)
+    if (osl[r] != GX_NOSLOT && !((emit >> ((uint32_t)r * T + tl)) & 1u))
+      *reinterpret_cast<uint4 *>(ob_slot_hdr(d, osl[r])) = make_uint4(GX_SLOT_EMPTY, 0u, 0u, 0u);
   a.c[C_GOSSIP_MERGES] += fm;
   kl += nlines;
   a.c[C_STALE] += fs;
@@ -1821,6 +1934,21 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   kb = wave_sum(kb);
   kl = wave_sum(kl);
   if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SEND, kb, kl);
+  if (PLAN && d.ob_buf) {  // the last block to finish: every region filled exactly, claims reset
+    __shared__ uint32_t s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      s_last = atomicAdd(&d.ob_claim[XPLAN_GMAX], 1u) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      if (threadIdx.x < d.G && atomicExch(&d.ob_claim[threadIdx.x], 0u) != d.ob_cnt[threadIdx.x])
+        atomicOr(&d.work_cnt[GX_WC_ERR], GX_ERR_INBOX);  // a slot left unwritten (cannot happen)
+      if (threadIdx.x == 0) atomicExch(&d.ob_claim[XPLAN_GMAX], 0u);
+    }
+  }
 }
 
 
@@ -3231,7 +3359,41 @@ GXD void ae_pair_hosts(const Dev &d, uint32_t t, uint64_t key0, uint64_t key1, u
 // one after another. Pairs are disjoint, so their order does not matter.
 #define AE_GRID 4096
 template <bool VEC, bool EV, int PF, bool NT, bool NTS = false>
-GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1, uint32_t np) {
+GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  uint32_t t = blockIdx.x, base = 0, m = d.H, q = t;
+  uint64_t key = key0;
+  if (d.pair_split) {
+    uint32_t m0 = d.H / 2, np0 = m0 / 2;
+    if (t < np0) {
+      m = m0;
+    } else {
+      base = m0;
+      m = d.H - m0;
+      q = t - np0;
+      key = key1;
+    }
+  }
+  unsigned long long *kp = kprof_ae(d);
+  if (kp && threadIdx.x == 0) kp[2 * blockIdx.x] = wall_clock64() | ((unsigned long long)__smid() << 48);
+  uint32_t a = base + feistel_perm(key, 2 * q, m);
+  uint32_t b = base + feistel_perm(key, 2 * q + 1, m);
+  // a crashed member skips the pair; with the failure detector the network path is needed and
+  // the initiator (a) must see b ALIVE (memberlist pushPull picks among alive nodes)
+  if (d.departures || d.p.fd_enable) {
+    bool ok = !departed(d, a) && !departed(d, b);
+    if (ok && d.p.fd_enable) ok = reach(d, a, b) && memp(d, a, b)->state == GX_M_ALIVE;
+    if (!ok) return;
+  }
+  bool locked;
+  if (ae_lock_skip(d, a, b, locked)) return;
+  ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red, nullptr, false, nullptr, locked);
+  if (kp && threadIdx.x == 0) kp[2 * blockIdx.x + 1] = wall_clock64();
+}
+
+template <bool VEC, bool EV, int PF, bool NT, bool NTS = false>
+GXD void ae_round_pairs(const Dev &d, uint64_t key0, uint64_t key1, uint32_t np) {
   __shared__ unsigned long long s_wave[4];
   __shared__ unsigned long long s_red[4];
   __shared__ uint32_t s_run[256];  // pair index | 1 << 31 when a side holds the lock (lock_model = 0)
@@ -3288,12 +3450,18 @@ GXHD uint32_t ae_grid(uint32_t np, uint32_t lock_model) {
 // that 4 waves per SIMD stay resident; with events (listeners present) a separate entry point.
 template <bool VEC, int PF = 1, bool NT = false, bool NTS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae(Dev d, uint64_t key0,
-                                                                                   uint64_t key1, uint32_t np) {
-  ae_round_pair<VEC, false, PF, NT, NTS>(d, key0, key1, np);
+                                                                                   uint64_t key1) {
+  ae_round_pair<VEC, false, PF, NT, NTS>(d, key0, key1);
 }
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_ae_ev(Dev d, uint64_t key0, uint64_t key1, uint32_t np) {
-  ae_round_pair<VEC, true, 1, false>(d, key0, key1, np);
+__global__ __launch_bounds__(256) void k_ae_ev(Dev d, uint64_t key0, uint64_t key1) {
+  ae_round_pair<VEC, true, 1, false>(d, key0, key1);
+}
+// Under the lock model: chunks of pairs per block (ae_round_pairs), grid ae_grid(np, 1).
+template <bool VEC, int PF = 1, bool NT = false, bool NTS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae_chunk(Dev d, uint64_t key0,
+                                                                                         uint64_t key1, uint32_t np) {
+  ae_round_pairs<VEC, false, PF, NT, NTS>(d, key0, key1, np);
 }
 
 template <bool VEC, bool EV>
@@ -4032,17 +4200,9 @@ __global__ void k_outbox_pack(Dev d, const uint32_t *entry, uint32_t n, uint8_t 
 // round r of a batch and host u of the cluster, GossipMessages slots per sampled peer on another
 // shard, counted per (shard of u, shard of the peer). Every shard computes the same matrix, so the
 // collective's split sizes are known without waiting for the device.
-#define XPLAN_BATCH 64
-#define XPLAN_GMAX 64
 struct XBound {
   uint32_t n[XPLAN_GMAX];  // slots this shard sends each shard this round
 };
-GXD uint32_t shard_of_d(const Dev &d, uint32_t v) {
-  uint32_t g = (uint32_t)(((uint64_t)v * d.G) / d.H);
-  while (g > 0 && (uint32_t)(((uint64_t)g * d.H) / d.G) > v) g--;
-  while (g + 1 < d.G && (uint32_t)(((uint64_t)(g + 1) * d.H) / d.G) <= v) g++;
-  return g;
-}
 __global__ __launch_bounds__(256) void k_xplan(Dev d, int64_t r0, uint32_t *cnt) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x, rr = blockIdx.y;
   if (u >= d.H) return;

@@ -129,23 +129,52 @@ class LocalShards:
         s.e.outbox_sizes_async(_ptr(t))
         return t.cpu().numpy().astype(np.uint64)
 
+    def _planned_bufs(self):
+        """Each shard's send buffer of the planned exchange, allocated once at its bound (DistShard)."""
+        if getattr(self, "_pb", None) is None:
+            e = self.shards[0].e
+            p = e.params
+            slot = 16 + 16 * p.packet_cap
+            self._pb = [torch.empty((s.e.hi - s.e.lo) * p.fanout * slot, dtype=torch.uint8, device=self.device)
+                        for s in self.shards]
+        return self._pb
+
+    def _gossip_planned(self) -> bool:
+        """A planned gossip round through gx_round_gossip_begin / _end, as DistShard runs it; True
+        when it is a push-pull round (round_end is then the caller's)."""
+        G = self.G
+        bufs = self._planned_bufs()
+        plan = np.zeros(G * G, dtype=np.uint64)
+        for s, b in zip(self.shards, bufs):
+            s.e.round_gossip_begin(plan, _ptr(b), b.numel())
+        m = plan.reshape(G, G)
+        self.last_sizes = [m[g].copy() for g in range(G)]
+        ae = []
+        for dst, s in enumerate(self.shards):
+            parts = [bufs[src][int(m[src][:dst].sum()):int(m[src][:dst + 1].sum())] for src in range(G)]
+            x = torch.cat(parts)
+            ae.append(s.e.round_gossip_end(_ptr(x), x.numel()))
+        assert all(a == ae[0] for a in ae)
+        return ae[0]
+
     def run_rounds(self, n: int):
         planned = planned_exchange(self.shards[0].e.params)
         for _ in range(n):
-            for s in self.shards:
-                s.e.round_send()
             self.exchange_paths["planned" if planned else "sized"] += 1
             if planned:
-                plan = self.shards[0].e.exchange_plan()
-                inb = self._exchange(lambda s: plan[s.e.params.shard_id].copy(),
-                                     lambda e, p, c: e.outbox_pack_planned(p, c))
+                ae = self._gossip_planned()
+                self.wire.packets += int(sum(int(x.sum()) for x in self.last_sizes))
+                if not ae:
+                    continue
             else:
+                for s in self.shards:
+                    s.e.round_send()
                 inb = self._exchange(self._outbox_sizes, lambda e, p, c: e.outbox_pack(p, c))
-            self.wire.packets += int(sum(int(x.sum()) for x in self.last_sizes))
-            for s, x in zip(self.shards, inb):
-                s.e.inbox_unpack(_ptr(x), x.numel())
-            for s in self.shards:
-                s.e.round_merge()
+                self.wire.packets += int(sum(int(x.sum()) for x in self.last_sizes))
+                for s, x in zip(self.shards, inb):
+                    s.e.inbox_unpack(_ptr(x), x.numel())
+                for s in self.shards:
+                    s.e.round_merge()
             # push-pull: digests, the blocks each side leads, the partners' return blocks (gx.h);
             # shard-local pairs overlap the exchanges. Every shard agrees on the AE rounds.
             if self.shards[0].e.is_ae_round():

@@ -35,13 +35,13 @@ def test_local_shards_take_the_planned_exchange(oracle_lib, kw, planned):
     sh = LocalShards(oracle_lib, 2, **kw)
     calls = {"plan": 0}
     eng = sh.shards[0].e
-    orig = eng.exchange_plan
+    orig = eng.round_gossip_begin  # the planned round's first call (gx_exchange_plan inside)
 
-    def counted():
+    def counted(*a):
         calls["plan"] += 1
-        return orig()
+        return orig(*a)
 
-    eng.exchange_plan = counted
+    eng.round_gossip_begin = counted
     sh.run_rounds(7)
     assert sh.exchange_paths == ({"planned": 7, "sized": 0} if planned else {"planned": 0, "sized": 7})
     assert calls["plan"] == (7 if planned else 0)
