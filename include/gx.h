@@ -494,7 +494,12 @@ int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */
  *   gx_round_gossip_end   = gx_inbox_unpack(buf, bytes) + gx_round_merge, then, unless this round
  *                           is a push-pull round (*ae_round = 1: the caller runs the gx_ae_* steps
  *                           and gx_round_end), gx_round_end (*ae_round = 0).
- * plan: G * G entries as gx_exchange_plan. Same conditions and errors as those calls. */
+ * plan: G * G entries as gx_exchange_plan. Same conditions and errors as those calls. The HIP
+ * engine packs the buffer inside the send itself when GossipMessages is 1 and the planned
+ * GetBroadcasts path runs (record budget, no failure detector or departures): a packet for
+ * another shard is written straight into a slot of its destination's region, so the slots of a
+ * region are in arrival order rather than sender order (the receiver ranks packets by sender key;
+ * the merge is the same). gx_outbox_pack_planned must not be called after it for that round. */
 int gx_round_gossip_begin(gx_engine *e, uint64_t *plan, void *buf, uint64_t cap);
 int gx_round_gossip_end(gx_engine *e, const void *buf, uint64_t bytes, int *ae_round);
 /* Per-record min and max slot word over this engine's views (R entries each; device memory for
