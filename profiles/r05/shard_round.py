@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -58,13 +59,16 @@ def main():
     torch.cuda.synchronize()
     G = a.G
     bufs = sh._planned_bufs()
-    send_us, end_us, slots = [], [], []
+    send_us, end_us, slots, host_us = [], [], [], []
     for _ in range(a.rounds):
         plan = np.zeros(G * G, dtype=np.uint64)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2 * G)]
+        th = 0.0  # host time to issue the shards' calls (they return once queued)
         for g, (s, b) in enumerate(zip(sh.shards, bufs)):
             ev[g][0].record(stream)
+            h0 = time.perf_counter()
             s.e.round_gossip_begin(plan, _ptr(b), b.numel())
+            th += time.perf_counter() - h0
             ev[g][1].record(stream)
         m = plan.reshape(G, G)
         slots.append(int(m.sum()) // (16 + 16 * sh.shards[0].e.params.packet_cap))
@@ -72,11 +76,14 @@ def main():
         for dst, s in enumerate(sh.shards):
             x = torch.cat([bufs[src][int(m[src][:dst].sum()):int(m[src][:dst + 1].sum())] for src in range(G)])
             ev[G + dst][0].record(stream)
+            h0 = time.perf_counter()
             ae = s.e.round_gossip_end(_ptr(x), x.numel())
+            th += time.perf_counter() - h0
             ev[G + dst][1].record(stream)
         if ae:
             raise SystemExit("a push-pull round in the stretch: pick gossip-only rounds")
         torch.cuda.synchronize()
+        host_us.append(1e6 * th / G)
         send_us.append([1e3 * p.elapsed_time(q) for p, q in ev[:G]])
         end_us.append([1e3 * p.elapsed_time(q) for p, q in ev[G:]])
     S, E = np.array(send_us), np.array(end_us)
@@ -86,6 +93,7 @@ def main():
     out["per_shard_us"] = [round(float(x), 1) for x in per_shard]
     out["per_shard_over_unsharded_median"] = round(float(np.median(per_shard / np.array(per))), 3)
     out["slots_per_round"] = slots
+    out["per_shard_host_issue_us"] = [round(x, 1) for x in host_us]  # the two engine calls (ctypes included)
     for s in sh.shards:
         s.e.close()
     print(json.dumps(out), flush=True)

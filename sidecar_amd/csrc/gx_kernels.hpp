@@ -3448,8 +3448,11 @@ GXHD uint32_t ae_grid(uint32_t np, uint32_t lock_model) {
 
 // The push-pull kernel, without ChangeEvents (no listener anywhere): kept within 128 VGPRs so
 // that 4 waves per SIMD stay resident; with events (listeners present) a separate entry point.
+#ifndef GX_AE_WPE
+#define GX_AE_WPE 4  // 5 / 6 spill 47 / 87 VGPRs: 1.8x / 2.6x slower at cfg 2 (profiles/r05/ab/ae_wpe_cfg*.jsonl)
+#endif
 template <bool VEC, int PF = 1, bool NT = false, bool NTS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_ae(Dev d, uint64_t key0,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GX_AE_WPE))) void k_ae(Dev d, uint64_t key0,
                                                                                    uint64_t key1) {
   ae_round_pair<VEC, false, PF, NT, NTS>(d, key0, key1);
 }
