@@ -29,7 +29,7 @@ for name, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
     for k, (n, v) in acc.items():
         agg[k][ctr + "_KB_per_launch"] = v / n
         agg[k]["launches_" + name] = n
-cls = {"k_ae": "ae", "k_scan": "scan", "k_merge": "merge", "k_merge_seg": "merge", "k_storm": "storm", "k_storm_p2": "storm", "k_send": "send",
+cls = {"k_ae": "ae", "k_ae_chunk": "ae", "k_scan": "scan", "k_merge": "merge", "k_merge_seg": "merge", "k_storm": "storm", "k_storm_p2": "storm", "k_send": "send",
        "k_owner": "owner"}
 summary = {}
 for k, v in agg.items():
