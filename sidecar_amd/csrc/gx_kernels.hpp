@@ -2664,7 +2664,9 @@ GXD bool merge_seg(const Dev &d, const uint32_t vi, const bool act, MergeLds &L)
 // registers, finds each output record's packet by the ranked starts, and issues every record
 // load of a pass (RPL per lane) before its stores. Returns false (the caller takes the
 // whole-wave path) for an inbox of more than SEG packets; the result is the whole-wave path's.
-#define LOCK_RPL 4
+#ifndef LOCK_RPL
+#define LOCK_RPL 4  // 8 measured 13% slower in the buffering rounds (profiles/r05/ab/lock_rpl8_cfg5.jsonl)
+#endif
 template <int SEG>
 GXD bool lock_append_seg(const Dev &d, uint32_t vi, bool act) {
   const uint32_t lane = threadIdx.x & 63, sl = lane & (SEG - 1), sb = lane & ~(uint32_t)(SEG - 1);
