@@ -417,7 +417,9 @@ int gx_run_rounds(gx_engine *e, uint32_t n_rounds);
  *           message per cross-shard push-pull pair, grouped by destination shard, ascending pair.
  *           `runs` (fd_enable only, else 0): 1 if the sender holds the pair's initiator (first
  *           host) and the pair runs (path up, partner ALIVE in the initiator's list); the other
- *           side follows it, and a pair that does not run ships no blocks.
+ *           side follows it, and a pair that does not run ships no blocks. Bit 1 of `runs`: the
+ *           sender's host holds the ServicesState lock this round (lock_model): the pair fails, and
+ *           with lock_model = 1 the sender's digests are all zero (its row is not read).
  *   lead:   u32 pair index, u32 host, u32 n_lead, u32 0, then n_lead encoded blocks (below): the
  *           row's blocks whose digests differ from the partner's and that this side leads,
  *           ascending. The side whose block has fewer literals leads it (the count rides in the

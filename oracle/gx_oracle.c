@@ -2320,9 +2320,12 @@ int gx_ae_pack(gx_engine *e, void *buf, uint64_t cap) {
                            (uint32_t)locked_at(e, e->x_mine[k]) << 1};
     memcpy(m, hdr, 16);
     const uint64_t *row = &e->view[(size_t)e->x_mine[k] * e->R];
+    /* a side that holds the lock fails the pair (lock_model): zero digests, its row is not read */
+    const int skip = e->p.lock_model && locked_at(e, e->x_mine[k]);
     for (uint32_t b = 0; b < e->nblk; b++) {
       uint64_t *dg = &e->x_dig[((size_t)k * e->nblk + b) * 2];
-      block_digest(e, row, b, &dg[0], &dg[1]);
+      if (skip) dg[0] = dg[1] = 0;
+      else block_digest(e, row, b, &dg[0], &dg[1]);
       memcpy(m + 16 + 16ull * b, dg, 16);
     }
     if (pp_state(e)) { /* the member list pushPull sends, as of now (round start of the phase) */

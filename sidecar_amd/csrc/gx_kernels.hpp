@@ -3592,6 +3592,11 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
     hdr[3] = (d.p.fd_enable && first[k] && ae_initiator_runs(d, host[k], other[k]) ? 1u : 0u) |
              (host_locked(d, host[k]) ? 2u : 0u);
   }
+  if (d.p.lock_model && host_locked(d, host[k])) {  // the pair fails (gx.h digest): zero digests, no row read
+    for (uint32_t b = threadIdx.x; b < nblk; b += blockDim.x)
+      *reinterpret_cast<ulonglong2 *>(msg + 16 + 16ull * b) = make_ulonglong2(0ull, 0ull);
+    return;
+  }
   const uint64_t *row = vrow(d, host[k]);
   // software pipeline: the wave's next block is in flight while this one is hashed and reduced
   ulonglong2 cur[4], nxt[4];
