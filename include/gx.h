@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 8
+#define GX_ABI_VERSION 9
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -490,6 +490,14 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
  * host is in at most one), so the result is identical either way. */
 int gx_ae_merge_local(gx_engine *e); /* phase 5 */
 int gx_round_end(gx_engine *e);   /* round += 1, wake due sleepers */
+/* The ServicesState lock across shards (lock_model): *unlocked = this shard's hosts that do not
+ * hold the lock this round (a synchronizing call). When the sum over every shard is 0 at a
+ * push-pull round, every pair fails, and gx_ae_skip_locked stands for the whole exchange
+ * (gx_ae_bytes .. gx_ae_merge; then gx_round_end): the same counts (ae_locked once per pair, by
+ * the shard of its first host; first_locked_round), nothing moved. GX_EINVAL if a host here is
+ * free, for an unsharded engine (G = 1), or with the failure detector or departures. */
+int gx_lock_census(gx_engine *e, uint32_t *unlocked);
+int gx_ae_skip_locked(gx_engine *e);
 /* A planned gossip round in two calls (fewer host calls per round for an exchange layer; the same
  * work as the calls they stand for):
  *   gx_round_gossip_begin = gx_round_send + gx_exchange_plan(plan) + gx_outbox_pack_planned(buf, cap)

@@ -2620,6 +2620,39 @@ int gx_ae_merge_local(gx_engine *e) {
   if (e->G > 1) ae_phase_local(e);
   return GX_OK;
 }
+int gx_lock_census(gx_engine *e, uint32_t *unlocked) {
+  if (!e || !unlocked) return GX_EINVAL;
+  uint32_t n = 0;
+  for (uint32_t v = e->lo; v < e->hi; v++) n += !locked_at(e, v);
+  *unlocked = n;
+  return GX_OK;
+}
+
+/* A push-pull round in which every host of the cluster holds the lock (the caller's census over
+ * the shards): every pair fails as in gx_ae_bytes .. gx_ae_merge, counted once per pair by the
+ * shard of its first host (ae_exchange for local pairs, the digest step for cross pairs). */
+int gx_ae_skip_locked(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  if (!ae_round(e)) return GX_OK;
+  if (e->G < 2 || !e->p.lock_model || e->p.fd_enable || (e->p.depart_round >= 0 && e->p.depart_ppm)) return GX_EINVAL;
+  uint32_t unlocked = 0;
+  gx_lock_census(e, &unlocked);
+  if (unlocked) return GX_EINVAL;
+  uint32_t *pa = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
+  const uint32_t np = ae_pairs(e, pa, pb);
+  int any = 0;
+  for (uint32_t t = 0; t < np; t++) {
+    const int la = is_local(e, pa[t]), lb = is_local(e, pb[t]);
+    if (la) e->st.ae_locked++;
+    any |= la || lb;
+  }
+  if (any) note_locked(e);
+  free(pa);
+  free(pb);
+  return GX_OK;
+}
+
 int gx_round_end(gx_engine *e) {
   if (!e || e->round + 1 >= GX_MAX_ROUND) return GX_EINVAL; /* rounds are 32-bit in jobs and sleepers */
   round_end(e);

@@ -233,7 +233,7 @@ ABI_FUNCS = [
     "gx_read_sleepers", "gx_read_pending", "gx_read_list", "gx_host_digests", "gx_stats_get",
     "gx_timing_get", "gx_converged", "gx_round_send", "gx_outbox_bytes", "gx_outbox_pack",
     "gx_inbox_unpack", "gx_exchange_plan", "gx_outbox_pack_planned", "gx_round_merge", "gx_ae_bytes", "gx_ae_pack", "gx_ae_merge", "gx_round_end",
-    "gx_round_gossip_begin", "gx_round_gossip_end",
+    "gx_round_gossip_begin", "gx_round_gossip_end", "gx_lock_census", "gx_ae_skip_locked",
     "gx_view_minmax", "gx_owner_words", "gx_read_server_times", "gx_read_last_changed", "gx_add_listener",
     "gx_remove_listener", "gx_listener_drain", "gx_ae_merge_local", "gx_ae_delta_bytes", "gx_ae_delta_pack", "gx_ae_return_bytes", "gx_ae_return_pack", "gx_set_stream", "gx_get_broadcasts_bytes", "gx_set_static_bytes", "gx_message_bytes",
     "gx_set_names", "gx_local_state_json", "gx_decode_state_json", "gx_merge_remote_state_json",
@@ -288,6 +288,7 @@ def _declare(lib):
         "gx_round_end": ([vp], i32), "gx_view_minmax": ([vp, vp, vp], i32), "gx_owner_words": ([vp, vp], i32),
         "gx_round_gossip_begin": ([vp, vp, vp, C.c_uint64], i32),
         "gx_round_gossip_end": ([vp, vp, C.c_uint64, P(i32)], i32),
+        "gx_lock_census": ([vp, P(u32)], i32), "gx_ae_skip_locked": ([vp], i32),
         "gx_ae_merge_local": ([vp], i32),
         "gx_read_server_times": ([vp, u32, u32, u32, vp], i32),
         "gx_read_last_changed": ([vp, u32, u32, vp], i32),
@@ -847,6 +848,16 @@ class Engine:
 
     def round_end(self):
         check(self.lib.gx_round_end(self.h), "gx_round_end")
+
+    def lock_census(self) -> int:
+        """This shard's hosts that do not hold the ServicesState lock this round (gx_lock_census)."""
+        n = C.c_uint32(0)
+        check(self.lib.gx_lock_census(self.h, C.byref(n)), "gx_lock_census")
+        return int(n.value)
+
+    def ae_skip_locked(self):
+        """A push-pull round with every host of the cluster locked: its counts only (gx_ae_skip_locked)."""
+        check(self.lib.gx_ae_skip_locked(self.h), "gx_ae_skip_locked")
 
     def view_minmax(self, ptr_min: int, ptr_max: int):
         check(self.lib.gx_view_minmax(self.h, C.c_void_p(ptr_min), C.c_void_p(ptr_max)), "gx_view_minmax")

@@ -2322,6 +2322,61 @@ int gx_ae_merge(gx_engine *e, const void *lead, uint64_t lead_bytes, const void 
   return phase_done(e);
 }
 
+int gx_lock_census(gx_engine *e, uint32_t *unlocked) {
+  if (!e || !unlocked) return GX_EINVAL;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = ensure_api(e, sizeof(uint32_t));
+  if (rc) return rc;
+  set_round_fields(e);
+  uint32_t *dv = (uint32_t *)e->api_dev;
+  HIPCHK(hipMemsetAsync(dv, 0, sizeof(uint32_t), e->stream));
+  if (e->d.Hl) k_lock_census<<<nblk(e->d.Hl, 256), 256, 0, e->stream>>>(e->d, dv);
+  HIPCHK(hipMemcpyAsync(unlocked, dv, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  return sync_check(e);
+}
+
+// A push-pull round in which every host of the cluster holds the lock (the caller's collective
+// census): every pair fails, so the round is only its counts, as the full exchange would make them
+// (gx_ae_bytes .. gx_ae_merge): ae_locked once per pair, by the shard of its first host.
+int gx_ae_skip_locked(gx_engine *e) {
+  if (!e) return GX_EINVAL;
+  Dev &d = e->d;
+  if (!ae_round(e)) return GX_OK;
+  // sharded engines only (one engine runs its push-pull itself; the pair buffers exist when G > 1)
+  if (d.G < 2 || !e->ae_pa || !d.p.lock_model || d.departures || d.p.fd_enable) return GX_EINVAL;
+  uint32_t unlocked = 0;
+  int rc = gx_lock_census(e, &unlocked);
+  if (rc) return rc;
+  if (unlocked) return GX_EINVAL;  // a host here is free: the pairs must run the exchange
+  set_round_fields(e);
+  uint32_t base[2] = {0, d.H / 2}, len[2] = {d.H, 0};
+  int ng = 1;
+  if (d.pair_split) {
+    len[0] = d.H / 2;
+    len[1] = d.H - d.H / 2;
+    ng = 2;
+  }
+  const uint32_t n0 = len[0] / 2, n1 = ng > 1 ? len[1] / 2 : 0, np = n0 + n1;
+  if (!np) return GX_OK;
+  const uint64_t key0 = rng4(d.p.seed, ST_AE, (uint64_t)d.round, base[0], 0);
+  const uint64_t key1 = ng > 1 ? rng4(d.p.seed, ST_AE, (uint64_t)d.round, base[1], 0) : 0;
+  std::vector<uint32_t> pa(np), pb(np);
+  k_ae_pairs<<<(np + 255) / 256, 256, 0, e->stream>>>(base[0], len[0], key0, base[1], ng > 1 ? len[1] : 0, key1, n0,
+                                                       np, e->ae_pa, e->ae_pb);
+  HIPCHK(hipMemcpyAsync(pa.data(), e->ae_pa, 4ull * np, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(pb.data(), e->ae_pb, 4ull * np, hipMemcpyDeviceToHost, e->stream));
+  rc = sync_check(e);
+  if (rc) return rc;
+  uint32_t n_first = 0, any = 0;
+  for (uint32_t t = 0; t < np; t++) {
+    const bool la = own(e, pa[t]), lb = own(e, pb[t]);
+    n_first += la ? 1u : 0u;
+    any |= (la || lb) ? 1u : 0u;
+  }
+  k_ae_locked_note<<<1, 64, 0, e->stream>>>(d, n_first, any);
+  return phase_done(e);
+}
+
 int gx_round_end(gx_engine *e) {
   if (!e || e->d.round + 1 >= GX_MAX_ROUND) return GX_EINVAL;  // rounds are 32-bit in jobs and sleepers
   HIPCHK(hipSetDevice(e->device));

@@ -3656,6 +3656,20 @@ __global__ __launch_bounds__(256) void k_ae_digest(Dev d, const uint32_t *host, 
   }
 }
 
+// gx_lock_census: this shard's hosts that do not hold the ServicesState lock this round.
+__global__ __launch_bounds__(256) void k_lock_census(Dev d, uint32_t *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool free_ = i < d.Hl && !host_locked(d, d.lo + i);
+  const unsigned long long m = __ballot(free_);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(out, (uint32_t)__popcll(m));
+}
+// gx_ae_skip_locked: the counts of a push-pull round whose every pair fails on the lock.
+__global__ void k_ae_locked_note(Dev d, uint32_t n_first, uint32_t any) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (n_first) ctr_atomic(d, C_AE_LOCKED, n_first);
+  if (any) atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
+}
+
 // Compare own digests with the partner's (message k of `in`): the blocks that differ, and who
 // leads each (fewer literals; ties: the pair's first host). Per pair: lead and follow counts, the
 // size of this side's lead message and of the partner's. A pair that does not run (failure
@@ -3681,28 +3695,37 @@ __global__ __launch_bounds__(256) void k_ae_mask(Dev d, const uint8_t *in, const
   if (lk && d.p.lock_model) runs = false;
   if (threadIdx.x == 0) skip[k] = (runs ? 0 : 1) | (lk && runs ? 2 : 0);
   unsigned long long n = 0, bl = 0, bi = 0;  // n: lead count | follow count << 32
-  for (uint32_t w = threadIdx.x; w < nmw; w += blockDim.x) {
-    uint32_t lb = 0, fb = 0;
-    for (uint32_t j = 0; j < 32; j++) {
-      uint32_t b = w * 32 + j;
-      if (b >= nblk) break;
-      ulonglong2 x = own[(size_t)k * nblk + b];
-      ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(msg + 16 + 16ull * b);
-      uint32_t lm = (uint32_t)(x.y >> 54), ly = (uint32_t)(y.y >> 54);
-      lt[(size_t)k * nblk + b] = (uint16_t)ly;
-      if (runs && (x.x != y.x || x.y != y.y)) {
-        if (lm < ly || (lm == ly && first[k])) {
-          lb |= 1u << j;
-          bl += 128 + 8ull * lm;
-        } else {
-          fb |= 1u << j;
-          bi += 128 + 8ull * ly;
+  if (!runs) {  // block-uniform: a pair that does not run leads and follows nothing (its digests unread)
+    for (uint32_t w = threadIdx.x; w < nmw; w += blockDim.x) {
+      lmask[(size_t)k * nmw + w] = 0;
+      fmask[(size_t)k * nmw + w] = 0;
+    }
+  } else {
+    // one block per thread, 256 at a time: a wave's 64 blocks are two mask words (ballots)
+    const uint32_t lane = threadIdx.x & 63, wvb = threadIdx.x >> 6;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += blockDim.x) {
+      const uint32_t b = b0 + threadIdx.x;
+      bool lead = false, fol = false;
+      if (b < nblk) {
+        const ulonglong2 x = own[(size_t)k * nblk + b];
+        const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(msg + 16 + 16ull * b);
+        const uint32_t lm = (uint32_t)(x.y >> 54), ly = (uint32_t)(y.y >> 54);
+        lt[(size_t)k * nblk + b] = (uint16_t)ly;
+        if (x.x != y.x || x.y != y.y) {
+          lead = lm < ly || (lm == ly && first[k]);
+          fol = !lead;
+          if (lead) bl += 128 + 8ull * lm;
+          else bi += 128 + 8ull * ly;
         }
       }
+      const unsigned long long ml = __ballot(lead), mf = __ballot(fol);
+      const uint32_t w0 = (b0 + 64 * wvb) >> 5;  // the wave's first mask word
+      if (lane < 2 && w0 + lane < nmw) {
+        lmask[(size_t)k * nmw + w0 + lane] = (uint32_t)(ml >> (32 * lane));
+        fmask[(size_t)k * nmw + w0 + lane] = (uint32_t)(mf >> (32 * lane));
+      }
+      n += (unsigned long long)lead | ((unsigned long long)fol << 32);
     }
-    lmask[(size_t)k * nmw + w] = lb;
-    fmask[(size_t)k * nmw + w] = fb;
-    n += __popc(lb) | ((unsigned long long)__popc(fb) << 32);
   }
   n = wave_sum(n);
   bl = wave_sum(bl);

@@ -32,6 +32,12 @@ def planned_exchange(p: GxParams) -> bool:
     return not p.fd_enable and p.gossip_messages <= 1
 
 
+def lock_shortcut(p: GxParams) -> bool:
+    """A push-pull round may be replaced by gx_ae_skip_locked when every host holds the lock: the
+    lock model on, no failure detector (its membership half runs regardless), no departures."""
+    return bool(p.lock_model) and not p.fd_enable and not (p.depart_round >= 0 and p.depart_ppm)
+
+
 def _ptr(t: torch.Tensor) -> int:
     return t.data_ptr() if t.numel() else 0
 
@@ -97,6 +103,8 @@ class LocalShards:
         self.exchange_paths = {"planned": 0, "sized": 0}  # gossip rounds per exchange path (planned_exchange)
         self.trace_ae = False  # keep each push-pull round's digest and delta inboxes (host copies)
         self.ae_trace = []
+        self.ae_skipped = 0  # push-pull rounds with every host locked (gx_ae_skip_locked)
+        self.skip_locked = True  # False: run the whole exchange even then (wire tests)
 
     @property
     def engines(self) -> List[Engine]:
@@ -176,8 +184,14 @@ class LocalShards:
                 for s in self.shards:
                     s.e.round_merge()
             # push-pull: digests, the blocks each side leads, the partners' return blocks (gx.h);
-            # shard-local pairs overlap the exchanges. Every shard agrees on the AE rounds.
-            if self.shards[0].e.is_ae_round():
+            # shard-local pairs overlap the exchanges. Every shard agrees on the AE rounds. With
+            # every host of the cluster locked, every pair fails: the counts only (gx_ae_skip_locked)
+            if self.shards[0].e.is_ae_round() and self.G > 1 and self.skip_locked and lock_shortcut(self.shards[0].e.params) and \
+                    sum(s.e.lock_census() for s in self.shards) == 0:
+                for s in self.shards:
+                    s.e.ae_skip_locked()
+                self.ae_skipped += 1
+            elif self.shards[0].e.is_ae_round():
                 dig = self._exchange(lambda s: s.e.ae_bytes(), lambda e, p, c: e.ae_pack(p, c),
                                      after_pack=lambda e: e.ae_merge_local())
                 dig_sizes = self.last_sizes
@@ -242,6 +256,8 @@ class DistShard:
         self.e = self.s.e
         self.wire = WireBytes(self.e)
         self.exchange_paths = {"planned": 0, "sized": 0}  # gossip rounds per exchange path (planned_exchange)
+        self.ae_skipped = 0  # push-pull rounds with every host locked (gx_ae_skip_locked)
+        self.skip_locked = True  # False: run the whole exchange even then
         # gloo has no device all-to-all / all-gather: a gloo group over device shards (the one-GPU
         # rehearsal of the RCCL path in tests/test_gpu_dist.py) stages collectives through the host
         self.stage = self.device.type == "cuda" and dist.get_backend(group) == "gloo"
@@ -338,6 +354,14 @@ class DistShard:
         self._a2a(recv[:nr], send[:ns], rs, ss)
         return e.round_gossip_end(_ptr(recv), nr)
 
+    def _all_locked(self) -> bool:
+        """Every host of every shard holds the ServicesState lock this round (gx_lock_census)."""
+        if self.world < 2 or not (self.skip_locked and lock_shortcut(self.e.params)):
+            return False
+        t = torch.tensor([self.e.lock_census()], dtype=torch.int64, device=self.device)
+        self._all_reduce(t, self.dist.ReduceOp.SUM)
+        return int(t.item()) == 0
+
     def run_rounds(self, n: int):
         e = self.e
         planned = planned_exchange(e.params)  # sizes from the seeded plan: no host wait
@@ -354,8 +378,13 @@ class DistShard:
                 e.round_merge()
                 ae = e.is_ae_round()
             self.wire.packets += int(self.last_sizes.sum())
-            # push-pull: digests, lead blocks, return blocks (local pairs overlap the exchanges)
-            if ae:
+            # push-pull: digests, lead blocks, return blocks (local pairs overlap the exchanges);
+            # with every host of the cluster locked (one census collective) every pair fails
+            if ae and self._all_locked():
+                e.ae_skip_locked()
+                e.round_end()
+                self.ae_skipped += 1
+            elif ae:
                 dsz = e.ae_bytes()
                 dig = self._exchange(dsz, e.ae_pack, after_pack=e.ae_merge_local)
                 lsz = e.ae_delta_bytes(_ptr(dig), dig.numel())

@@ -45,6 +45,7 @@ def test_gpu_push_pull_wire_identical_to_oracle(gx_lib, oracle_lib):
     g = LocalShards(gx_lib, 3, device="cuda:0", **kw)
     o = LocalShards(oracle_lib, 3, **kw)
     g.trace_ae = o.trace_ae = True
+    g.skip_locked = o.skip_locked = False  # the whole exchange each push-pull round (byte comparison)
     g.run_rounds(30)
     o.run_rounds(30)
     assert len(g.ae_trace) == len(o.ae_trace) > 0

@@ -96,7 +96,7 @@ def _worker(rank, world, port, kw, rounds, q):
     sh.run_rounds(rounds)
     st = sh.stats()
     conv = sh.converged()
-    q.put((rank, sh.e.read_views(), host_tuples(sh.e), sh.e.digests(), st, conv))
+    q.put((rank, sh.e.read_views(), host_tuples(sh.e), sh.e.digests(), st, conv, sh.ae_skipped))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -109,9 +109,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("name", ["storm", "churn_odd"])
+LOCKED = dict(n_hosts=64, n_services=16, init_mode=2, ae_period_rounds=10, partition_start=0,
+              partition_end=30, storm_round=5, queue_cap=2048)  # every host locked from round ~10
+
+
+@pytest.mark.parametrize("name", ["storm", "churn_odd", "locked"])
 def test_gloo_world2_matches_whole(oracle_lib, name):
-    kw, rounds, world = SCEN[name], 45, 2
+    kw, rounds, world = (LOCKED if name == "locked" else SCEN[name]), 45, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -129,6 +133,8 @@ def test_gloo_world2_matches_whole(oracle_lib, name):
     assert np.array_equal(np.concatenate([r[3] for r in res]), whole.digests())
     assert res[0][4] == whole.stats()
     assert res[0][5] == whole.converged()
+    if name == "locked":  # the census collective found every host locked: the exchange was skipped
+        assert res[0][6] == res[1][6] > 0
 
 
 def test_delta_ships_only_differing_blocks(oracle_lib):
@@ -159,3 +165,25 @@ def test_corrupt_inbox_slot_refused(oracle_lib, field):
     from tests.corrupt_inbox import run, run_valid
     assert run_valid(oracle_lib, torch.device("cpu")) >= 0
     assert run(oracle_lib, torch.device("cpu"), field) == "einval"
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_locked_push_pull_rounds_skip_the_exchange(oracle_lib, G):
+    """A push-pull round with every host of the cluster holding the ServicesState lock is replaced
+    by gx_ae_skip_locked after one census (gx_lock_census summed over the shards): the same
+    counts as the whole exchange (ae_locked once per pair, first_locked_round) and the same state,
+    against the unsharded engine and against the shards running the exchange anyway."""
+    kw = dict(n_hosts=64, n_services=16, init_mode=2, ae_period_rounds=10, partition_start=0,
+              partition_end=30, storm_round=5, queue_cap=2048)
+    whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    fast = LocalShards(oracle_lib, G, **kw)
+    full = LocalShards(oracle_lib, G, **kw)
+    full.skip_locked = False
+    for sh in (fast, full):
+        sh.run_rounds(41)
+    whole.run_rounds(41)
+    assert fast.ae_skipped > 0 and full.ae_skipped == 0
+    assert whole.stats()["ae_locked"] > 0
+    assert_sharded_equal(whole, fast, "skipped locked push-pull rounds")
+    assert_sharded_equal(whole, full, "whole exchanges")
+    assert fast.wire.ae_digest < full.wire.ae_digest  # nothing moved in the skipped rounds

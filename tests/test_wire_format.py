@@ -150,6 +150,7 @@ def test_push_pull_messages_follow_the_spec(oracle_lib, name, lock_model):
     whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
     sh = LocalShards(oracle_lib, 2, **kw)
     sh.trace_ae = True
+    sh.skip_locked = False  # the whole exchange even when every host is locked (its digests are checked)
     p = whole.params
     R = whole.H * whole.S
     nblk = (R + BLK - 1) // BLK
