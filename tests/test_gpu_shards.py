@@ -168,3 +168,21 @@ def test_gpu_planned_exchange_sync_free(gx_lib, oracle_lib):
     assert_sharded_equal(whole, sh, "planned exchange, round 60")
     assert_sharded_equal(orc, sh, "planned exchange vs oracle, round 60")
     assert sh.wire.as_dict()["packets"] > 0
+
+
+def test_gpu_locked_push_pull_rounds_skip_the_exchange(gx_lib, oracle_lib):
+    """HIP shards take the census shortcut on the same rounds as the oracle's (gx_lock_census,
+    gx_ae_skip_locked) and end identical to the unsharded HIP engine and to the oracle's shards."""
+    from tests.test_shards_cpu import LOCKED
+    kw = dict(LOCKED, n_hosts=96)
+    whole = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    g = LocalShards(gx_lib, 3, device="cuda:0", **kw)
+    o = LocalShards(oracle_lib, 3, **kw)
+    for sh in (g, o):
+        sh.run_rounds(41)
+    whole.run_rounds(41)
+    assert g.ae_skipped == o.ae_skipped > 0
+    assert [e.lock_census() for e in g.engines] == [e.lock_census() for e in o.engines]
+    assert_sharded_equal(whole, g, "HIP shards, locked push-pull rounds skipped")
+    assert g.stats() == o.stats()
+    assert all((a.read_views() == b.read_views()).all() for a, b in zip(g.engines, o.engines))
