@@ -468,6 +468,9 @@ static int round_send_impl(gx_engine *e) {
   return scan_probe_end(e);
 }
 
+#ifndef GX_MERGE_SMALL_HL
+#define GX_MERGE_SMALL_HL 0  // > 0: 16 receivers per block below this many local hosts (an A/B, unmeasured)
+#endif
 // Phase 4: gather-then-merge of every receiver's inbox (local and received packets).
 static int round_merge_impl(gx_engine *e) {
   Dev &d = e->d;
@@ -485,7 +488,9 @@ static int round_merge_impl(gx_engine *e) {
     // records, each folded by a whole wave tile by tile, so more waves in flight (16 receivers per
     // block, 4 waves per SIMD: 10% faster than 3 in the GM 15 accepting stretch,
     // profiles/r03/ab/merge_wpe_gm15.jsonl); else 64 receivers per block (3% faster at cfg 5)
-    const bool small = d.NG > 1;
+    // ... and when 64 receivers per block leave most CUs idle (a shard, a small cluster): a block's
+    // waves fold their receivers one item after another, so fewer per block shortens the launch
+    const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL;
     const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
     if (small) {
       if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, MERGE_WPE_GM> : k_merge_seg<true, false, 16, MERGE_WPE_GM>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
