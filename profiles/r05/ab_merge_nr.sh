@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of the merge with 16 receivers per block below 16384 local hosts (libgx_nr16) against the
-# product (64 always): a shard of cfg 5 at G = 8, and cfg 2 / cfg 4 on one engine, lock on and off.
+# A/B of the merge with 16 receivers per block below 16384 local hosts (libgx_nr16, now the product) against
+# 64 always: a shard of cfg 5 at G = 8, and cfg 2 / cfg 4 on one engine, lock on and off.
 set -e
 O=gpurun_out/r05/mnr
 mkdir -p $O

@@ -469,7 +469,8 @@ static int round_send_impl(gx_engine *e) {
 }
 
 #ifndef GX_MERGE_SMALL_HL
-#define GX_MERGE_SMALL_HL 0  // > 0: 16 receivers per block below this many local hosts (an A/B, unmeasured)
+#define GX_MERGE_SMALL_HL 16384  // 16 receivers per block below this many local hosts: merge 2.0 -> 1.1 ms (cfg 2)
+                                 // and 2.4 -> 1.5 ms (cfg 4) over 60 rounds lock off (profiles/r05/ab/merge_nr16_*)
 #endif
 // Phase 4: gather-then-merge of every receiver's inbox (local and received packets).
 static int round_merge_impl(gx_engine *e) {
