@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 9
+#define GX_ABI_VERSION 10
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -259,10 +259,27 @@ typedef struct gx_params {
    *   - ExpireServer calls (the storm's NotifyLeave, the failure detector's deaths) on a locked host
    *     wait: they run in owner order at the end of the owner phase of its first unlocked round.
    * lock_model = 0 lets merges proceed on locked hosts (rounds 1-4) and counts them
-   * (gx_stats.locked_merges). lock_buffer is 1..65535. */
+   * (gx_stats.locked_merges). lock_buffer is 1..65535. Memory: every engine keeps lock_buffer
+   * records of 16 B for each of its hosts (ceil(n_hosts / n_shards)), allocated at create; more
+   * than GX_LOCK_BUF_MAX_BYTES of them is GX_EINVAL (the default 1077 at 131072 hosts: 2.3 GB). */
   uint32_t lock_model;
   uint32_t lock_buffer;
+  /* memberlist piggybacks the delegate's broadcasts on every UDP message it sends, not only on
+   * gossip(): sendMsg -> getBroadcasts (memberlist net.go, the absent fork). probe_piggyback = 1
+   * adds the probe traffic of the scripted model (fd_enable = 0) as GetBroadcasts calls: every
+   * fd_probe_rounds (ProbeInterval 1 s) at a seeded phase a host pings one target, the target of
+   * a keyed Feistel permutation of the hosts for that round (a host drawing itself does not
+   * probe), and the ping carries one GetBroadcasts result; a target the ping reaches answers with
+   * an ack that carries one GetBroadcasts result of its own. Both calls run before the host's
+   * owner phase (ping, then ack), are their own packets (entries K * NG and K * NG + 1 of the host,
+   * so a receiver folds them after the sender's gossip packets) and do not stop on an empty
+   * result; a ping across the partition or to a departed host is lost after GetBroadcasts took
+   * its records, and gets no ack. In byte mode the ping or ack message takes fd_msg_bytes + 2 of
+   * limit_bytes. Parity unpinned (the fork is absent); 0 (default) = gossip() only, the rounds 1-5
+   * model. Unsharded engines without the failure detector only (GX_EINVAL otherwise). */
+  uint32_t probe_piggyback;
 } gx_params;
+#define GX_LOCK_BUF_MAX_BYTES (1ull << 36) /* 64 GiB of lock_buffer records per engine */
 #define GX_PP_MATCHING 0
 #define GX_PP_INITIATE 1
 
@@ -351,6 +368,9 @@ typedef struct gx_stats {
   uint64_t lock_drained;     /* buffered records merged once the host was unlocked (also gossip_merges) */
   uint64_t ae_locked;        /* push-pull exchanges that did not run: a side held the lock */
   uint64_t expire_deferred;  /* ExpireServer calls that waited for the lock */
+  uint64_t false_expiries;   /* of `expired`: alive-lifespan expiries (services_state.go:655-679) of a
+                                record whose owner host has not departed (the owner is live; with
+                                churn it may have stopped the service and its tombstone not arrived) */
 } gx_stats;
 
 /* Device time per kernel class, accumulated since create (HIP events; zeros for the oracle). */

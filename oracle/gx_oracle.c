@@ -31,12 +31,13 @@ typedef struct grec {
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
 enum { X_SAME = 0, X_LEAD = 1, X_FOLLOW = 2 }; /* a cross pair's row block in the push-pull delta */
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5,
-       ST_INIT_AGE = 6, ST_AE = 7 };
+       ST_INIT_AGE = 6, ST_AE = 7, ST_PROBE = 12 };
 
 struct gx_engine {
   gx_params p;
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;
-  uint32_t NG, KE; /* GossipMessages gathers per target; packet entries per host = K * NG */
+  uint32_t NG, KE; /* GossipMessages gathers per target; packet entries per host = K * NG (+ 2 probe) */
+  uint32_t KG;     /* gossip packet entries per host, K * NG (the probe ping and ack follow them) */
   uint32_t G, gid, lo, hi; /* shards; this engine owns hosts [lo, hi). Arrays stay H-sized. */
   /* cross-shard push-pull pairs of this AE round, in (partner shard, pair index) order, which is
    * the order of the digest and delta messages in both directions */
@@ -528,6 +529,8 @@ static int add_entry(gx_engine *e, uint32_t v, grec u, int64_t now, int src) {
   return 1;
 }
 
+static int departed(const gx_engine *e, uint32_t u); /* gx_oracle_fd.c */
+
 /* TombstoneOthersServices, services_state.go:635-683. Key order replaces Go map order.
  * Writes the first `cap` tombstoned records to out; returns the total. */
 static uint32_t scan_view(gx_engine *e, uint32_t v, int64_t now, grec *out, uint32_t cap) {
@@ -551,6 +554,7 @@ static uint32_t scan_view(gx_engine *e, uint32_t v, int64_t now, grec *out, uint
         set_slot(e, &row[r], nw);
         service_changed(e, v, r, nw, st); /* (:673-676) */
         e->st.expired++;
+        e->st.false_expiries += !departed(e, r / e->S); /* the owner is live (gx.h false_expiries) */
         if (n < cap) {
           out[n].w = nw;
           out[n].r = r;
@@ -774,6 +778,28 @@ static uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
   return x;
 }
 
+/* The inverse of feistel_perm: q = feistel_perm(key, x, m) <=> x = feistel_inv(key, q, m) (each
+ * pass inverts the four rounds; cycle walking inverts by walking the inverse cycle). */
+static uint32_t feistel_inv(uint64_t key, uint32_t q, uint32_t m) {
+  uint32_t b = 0;
+  while ((1u << b) < m) b++;
+  uint32_t hb = (b + 1) / 2;
+  if (hb == 0) hb = 1;
+  uint32_t hmask = (1u << hb) - 1;
+  uint32_t x = q;
+  do {
+    uint32_t L = x >> hb, Rr = x & hmask;
+    for (int i = 3; i >= 0; i--) { /* round i: (L, R) -> (R, L ^ F_i(R)) */
+      uint32_t pr = L;
+      uint32_t pl = Rr ^ ((uint32_t)(mix64(key ^ ((uint64_t)i << 32) ^ pr)) & hmask);
+      L = pl;
+      Rr = pr;
+    }
+    x = (L << hb) | Rr;
+  } while (x >= m);
+  return x;
+}
+
 /* gx_oracle_fd.c: memberlist push-pull membership merge */
 static void fd_snapshot_row(const gx_engine *e, uint32_t v, uint64_t *out);
 static void fd_merge_state(gx_engine *e, uint32_t v, const uint64_t *remote);
@@ -858,6 +884,53 @@ static void ph_storm(gx_engine *e, uint32_t i, void *ctx) {
   uint32_t lo = v < half ? half : 0, hi = v < half ? e->H : half;
   for (uint32_t o = lo; o < hi; o++) notify_leave(e, v, o, now);
 }
+/* memberlist's probe traffic (gx.h probe_piggyback): sendMsg piggybacks getBroadcasts on every UDP
+ * message (memberlist net.go, the absent fork; parity unpinned). Host u probes every
+ * fd_probe_rounds rounds at its seeded phase (the detector's phase, gx_oracle_fd.c probe_tick);
+ * its target is u's image under a keyed Feistel permutation of the hosts for the round, so the
+ * one host that may have pinged v this round is the permutation's preimage of v. */
+static int probe_tick_of(const gx_engine *e, uint32_t u) {
+  const uint32_t P = e->p.fd_probe_rounds;
+  return (uint64_t)e->round % P == rng4(e->p.seed, ST_FD_PHASE, u, 0, 0) % P;
+}
+static uint64_t probe_key(const gx_engine *e) { return rng4(e->p.seed, ST_PROBE, (uint64_t)e->round, 0, 0); }
+/* host u pings *t this round */
+static int probe_target(const gx_engine *e, uint32_t u, uint32_t *t) {
+  if (departed(e, u) || !probe_tick_of(e, u)) return 0;
+  *t = feistel_perm(probe_key(e), u, e->H);
+  return *t != u;
+}
+/* host v acks *u this round: u pinged v and the ping arrived */
+static int probe_pinger(const gx_engine *e, uint32_t v, uint32_t *u) {
+  *u = feistel_inv(probe_key(e), v, e->H);
+  return *u != v && !departed(e, *u) && probe_tick_of(e, *u) && reach(e, *u, v);
+}
+/* The ping and the ack, each one GetBroadcasts call and its own packet (entries KG, KG + 1). */
+static void ph_probe(gx_engine *e, uint32_t i, void *ctx) {
+  (void)ctx;
+  const uint32_t u = e->lo + i, cap = e->p.packet_cap;
+  if (departed(e, u)) return;
+  for (uint32_t c = 0; c < 2; c++) {
+    uint32_t peer;
+    if (!(c == 0 ? probe_target(e, u, &peer) : probe_pinger(e, u, &peer))) continue;
+    const size_t x = (size_t)u * e->KE + e->KG + c;
+    uint32_t l = 0;
+    if (e->p.limit_bytes) { /* the ping or ack message takes its bytes first */
+      const uint32_t used = e->p.fd_msg_bytes + 2;
+      const uint32_t avail = e->p.limit_bytes > used ? e->p.limit_bytes - used : 0;
+      if (avail > e->p.overhead_bytes) l = get_broadcasts(e, u, cap, &e->msg[x * cap], avail, e->p.overhead_bytes);
+    } else {
+      l = get_broadcasts(e, u, cap, &e->msg[x * cap], 0, e->p.overhead_bytes);
+    }
+    e->msg_len[x] = l;
+    e->msg_dst[x] = peer;
+    if (l && !reach(e, u, peer)) { /* the ping is lost on the wire */
+      e->st.lost_packets++;
+      e->msg_len[x] = 0;
+    }
+  }
+}
+
 /* gossip send: GetBroadcasts once per selected peer */
 /* With the failure detector, the targets are memberlist's (ph_fd_send took their memberlist
  * messages first; getBroadcasts gives the delegate the bytes left, and stops the round when a
@@ -908,11 +981,12 @@ static void round_send(gx_engine *e) {
   int64_t now = now_of(e);
   uint32_t n = e->hi - e->lo;
   e->in_round = 1;
+  for (size_t i = 0; i < (size_t)e->H * e->KE; i++) e->msg_len[i] = 0;
   for_hosts(e, n, ph_wake, NULL);
+  if (e->p.probe_piggyback) for_hosts(e, n, ph_probe, NULL);
   for_hosts(e, n, ph_owner, &now);
   if (e->p.storm_round >= 0 && e->round == e->p.storm_round) for_hosts(e, n, ph_storm, &now);
   if (e->p.fd_enable) for_hosts(e, n, ph_fd_tick, &now);
-  for (size_t i = 0; i < (size_t)e->H * e->KE; i++) e->msg_len[i] = 0;
   if (e->p.fd_enable) {
     memset(e->fd_len, 0, sizeof(uint32_t) * (size_t)e->H * (e->KE ? e->KE : 1));
     for_hosts(e, n, ph_fd_send, NULL);
@@ -1348,6 +1422,11 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL;
   if (p->inbox_slots > 256) return GX_EINVAL; /* engine bound (GX_DI_MAX) */
   if (p->lock_model > 1 || p->lock_buffer < 1 || p->lock_buffer > 65535) return GX_EINVAL;
+  if (p->lock_model && (((uint64_t)p->n_hosts + (p->n_shards > 1 ? p->n_shards : 1) - 1) / (p->n_shards > 1 ? p->n_shards : 1)) *
+                               p->lock_buffer * 16ull > GX_LOCK_BUF_MAX_BYTES)
+    return GX_EINVAL; /* the pipelines' records (gx.h lock_buffer) */
+  if (p->probe_piggyback > 1 || (p->probe_piggyback && (p->fd_enable || p->n_shards > 1 || p->fd_probe_rounds < 1)))
+    return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1426,7 +1505,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   e->L = p->packet_cap + p->pending_cap;
   e->K = p->fanout;
   e->NG = p->gossip_messages > 1 ? p->gossip_messages : 1;
-  e->KE = e->K * e->NG;
+  e->KG = e->K * e->NG;
+  e->KE = e->KG + (p->probe_piggyback ? 2u : 0u);
   e->G = p->n_shards > 1 ? p->n_shards : 1;
   e->gid = e->G > 1 ? p->shard_id : 0;
   e->lo = shard_lo(e, e->gid);

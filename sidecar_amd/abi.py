@@ -113,7 +113,7 @@ class GxParams(C.Structure):
         ("fd_suspicion_rounds", C.c_uint32 * 8), ("depart_round", C.c_int32), ("depart_ppm", C.c_uint32),
         ("fd_push_pull_state", C.c_uint32),
         ("gossip_messages", C.c_uint32), ("push_pull_mode", C.c_uint32), ("inbox_slots", C.c_uint32),
-        ("lock_model", C.c_uint32), ("lock_buffer", C.c_uint32),
+        ("lock_model", C.c_uint32), ("lock_buffer", C.c_uint32), ("probe_piggyback", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)
@@ -163,7 +163,7 @@ class GxStats(C.Structure):
         "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received",
         "fd_state_merges", "queue_deferred")] + [("first_drop_round", C.c_int64)] + [
         ("locked_merges", C.c_uint64), ("first_locked_round", C.c_int64)] + [(n, C.c_uint64) for n in (
-        "lock_buffered", "lock_drops", "lock_drained", "ae_locked", "expire_deferred")]
+        "lock_buffered", "lock_drops", "lock_drained", "ae_locked", "expire_deferred", "false_expiries")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}

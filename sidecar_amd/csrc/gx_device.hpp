@@ -79,7 +79,7 @@ enum {
 // Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
 enum {
   C_LOST = C_NCTR, C_FD_PROBES, C_FD_PROBE_FAIL, C_FD_SUSPECT, C_FD_CONFIRM, C_FD_DEATH, C_FD_REFUTE,
-  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_NCTR_ALL
+  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_FEXP, C_NCTR_ALL
 };
 #define GX_NCTR_SLOTS 48
 static_assert(C_NCTR_ALL <= GX_NCTR_SLOTS, "counter slots");
@@ -99,7 +99,7 @@ struct DevCtr {
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5, ST_INIT_AGE = 6,
-       ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11 };
+       ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11, ST_PROBE = 12 };
 
 #define XPLAN_BATCH 64  // rounds of planned-exchange slot bounds per k_xplan launch
 #define XPLAN_GMAX 64   // shards the planned exchange supports
@@ -108,7 +108,8 @@ struct Dev {
   gx_params p;     // t0_ns epoch-relative (gx.h GX_TS_SHIFT)
   int64_t epoch;    // absolute time of slot time 0
   uint32_t H, S, R, Q, A, L, SQ, DQ, K;  // SQ and DQ are powers of two (ring index = position & (size - 1))
-  uint32_t NG, KE;           // GossipMessages gathers per target; packet entries per host = K * NG
+  uint32_t NG, KE;           // GossipMessages gathers per target; packet entries per host = K * NG (+ 2 probe)
+  uint32_t KG;               // gossip packet entries per host, K * NG (the probe ping and ack follow, gx.h)
   uint32_t lo, Hl, G, gid;  // this engine owns hosts [lo, lo + Hl); per-host arrays are local
   uint32_t n_remote;        // packets received from other shards this round
   uint32_t *msg_key;        // [H*KE] global sender * KE + j * NG + n of each packet entry
@@ -224,6 +225,26 @@ GXHD uint32_t feistel_perm(uint64_t key, uint32_t q, uint32_t m) {
       uint32_t t = Rr;
       Rr = L ^ F;
       L = t;
+    }
+    x = (L << hb) | Rr;
+  } while (x >= m);
+  return x;
+}
+// Its inverse: feistel_perm(key, feistel_inv(key, q, m), m) == q (each pass runs the four rounds
+// backwards; cycle walking inverts by walking the inverse cycle).
+GXHD uint32_t feistel_inv(uint64_t key, uint32_t q, uint32_t m) {
+  uint32_t b = 0;
+  while ((1u << b) < m) b++;
+  uint32_t hb = (b + 1) / 2;
+  if (hb == 0) hb = 1;
+  uint32_t hmask = (1u << hb) - 1;
+  uint32_t x = q;
+  do {
+    uint32_t L = x >> hb, Rr = x & hmask;
+    for (int i = 3; i >= 0; i--) {  // round i: (L, R) -> (R, L ^ F_i(R))
+      const uint32_t pr = L;
+      L = Rr ^ ((uint32_t)(mix64(key ^ ((uint64_t)i << 32) ^ pr)) & hmask);
+      Rr = pr;
     }
     x = (L << hb) | Rr;
   } while (x >= m);

@@ -365,6 +365,10 @@ static int round_send_impl(gx_engine *e) {
   }
   d.n_remote = 0;
   hipStream_t s = e->stream;
+  if (d.p.probe_piggyback) {  // the probe ping and ack calls come before the owner phase (gx.h)
+    LaunchTimer t(e, GX_K_SEND);
+    k_probe<4><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
+  }
   bool vec = (d.R % 2) == 0;
   const bool storm = d.p.storm_round >= 0 && d.round == d.p.storm_round && d.H >= 2;
   // BroadcastTombstones' SendServices is queued before the detector's and the storm's jobs
@@ -753,6 +757,11 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL;
   if (p->inbox_slots > GX_DI_MAX) return GX_EINVAL;
   if (p->lock_model > 1 || p->lock_buffer < 1 || p->lock_buffer > 65535) return GX_EINVAL;
+  if (p->lock_model && (((uint64_t)p->n_hosts + (p->n_shards > 1 ? p->n_shards : 1) - 1) / (p->n_shards > 1 ? p->n_shards : 1)) *
+                               p->lock_buffer * 16ull > GX_LOCK_BUF_MAX_BYTES)
+    return GX_EINVAL; // the pipelines' records (gx.h lock_buffer)
+  if (p->probe_piggyback > 1 || (p->probe_piggyback && (p->fd_enable || p->n_shards > 1 || p->fd_probe_rounds < 1)))
+    return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -872,7 +881,8 @@ int gx_create(const gx_params *p, gx_engine **out) {
   d.L = p->packet_cap + p->pending_cap;
   d.K = p->fanout;
   d.NG = p->gossip_messages > 1 ? p->gossip_messages : 1;
-  d.KE = d.K * d.NG;
+  d.KG = d.K * d.NG;
+  d.KE = d.KG + (p->probe_piggyback ? 2u : 0u);  // the probe ping and ack entries (gx.h probe_piggyback)
   d.divS = d.S > 1 ? ~0ull / d.S + 1 : 0;
   d.logS = 0;
   while ((1u << d.logS) < d.S) d.logS++;  // used where S divides 64 (a power of two)
@@ -2492,6 +2502,7 @@ int gx_stats_get(gx_engine *e, gx_stats *out) {
   out->lock_drained = c[C_LOCK_DRAIN];
   out->ae_locked = c[C_AE_LOCKED];
   out->expire_deferred = c[C_EXP_DEFER];
+  out->false_expiries = c[C_FEXP];
   out->first_drop_round = fdr == ~0ull ? -1 : (int64_t)fdr;
   out->lost_packets = c[C_LOST];
   out->fd_probes = c[C_FD_PROBES];

@@ -533,7 +533,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   const uint32_t ev0 = evk >= 0 ? d.ev_cnt[evk] : 0;
   uint32_t last_key = 0;  // 1 + the last expired key (state.LastChanged)
   uint32_t n_exp = 0;
-  unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, mexp = ~0ull;
+  unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, mexp = ~0ull, c_dep = 0;
   uint32_t t = threadIdx.x;
   // VEC: the next tile's two 16-B words per thread are in flight while this tile is processed
   // (nontemporal: a scanned row is not re-read soon)
@@ -588,6 +588,13 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
       c_gc += gc;
       unsigned long long x = exp_time(d.p, nw[k]);
       mexp = x < mexp ? x : mexp;
+    }
+    if (d.departures) {  // gx.h false_expiries: the expiries of departed owners' records are not
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t r = (VEC ? base + 512 * (k >> 1) + 2 * t : base + 2 * blockDim.x * (k >> 1) + 2 * t) + (k & 1);
+        if (ex[k]) c_dep += departed(d, owner_of(d, r));
+      }
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -710,6 +717,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   if (threadIdx.x == 0)
     kbytes(d, GX_K_SCAN, (unsigned long long)d.R * 8 + 16ull * (n_exp < list_cap ? n_exp : list_cap), d.R);
   block_ctr(d, C_EXPIRED, c_exp, s_red);
+  block_ctr(d, C_FEXP, c_exp - c_dep, s_red);
   block_ctr(d, C_GC, c_gc, s_red);
   block_ctr(d, C_SCANSLOTS, threadIdx.x == 0 ? d.R : 0, s_red);
 }
@@ -1737,7 +1745,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
     gx_host_state hs = FWD ? fwd.hs : *h;
     const bool tick = do_bt && (FWD ? fwd.tick != 0 : d.tick[idx] != 0);
     bool pre = FWD;  // the FIFO head jobs the tick loaded are still at the head
-    for (uint32_t j = lane; j < d.KE; j += T) {
+    for (uint32_t j = lane; j < d.KG; j += T) {  // (the probe entries past KG were written by k_probe)
       d.msg_len[(size_t)idx * d.KE + j] = 0;
       d.msg_key[(size_t)idx * d.KE + j] = u * d.KE + j;
     }
@@ -1951,6 +1959,83 @@ __global__ __launch_bounds__(256) void k_send(Dev d, int do_bt) {
   }
 }
 
+
+// ================================================ memberlist probe traffic (gx.h probe_piggyback) ==
+// memberlist's sendMsg piggybacks getBroadcasts on every UDP message (the absent fork; parity
+// unpinned). With probe_piggyback, each host's probe ping (every fd_probe_rounds at its seeded
+// phase, to its image under the round's keyed Feistel permutation) and its ack to the one host
+// that may have pinged it (the permutation's preimage) are one GetBroadcasts call each, before
+// the round's owner phase: packet entries KG (ping) and KG + 1 (ack), registered in the
+// receivers' inboxes like send_host's packets (unplanned path: the receiver's filter at the
+// sender, a locked receiver's records unfiltered to its pipeline). A team of T lanes per host.
+GXD bool probe_tick_of(const Dev &d, uint32_t u) {
+  const uint32_t P = d.p.fd_probe_rounds;
+  return (uint64_t)d.round % P == rng4(d.p.seed, ST_FD_PHASE, u, 0, 0) % P;
+}
+template <int T>
+__global__ __launch_bounds__(256) void k_probe(Dev d) {
+  Acc a;
+  const uint32_t idx = blockIdx.x * (256 / T) + threadIdx.x / T, lane = threadIdx.x & (T - 1);
+  unsigned lost = 0;
+  unsigned long long kb = 0;
+  if (idx < d.Hl) {
+    const uint32_t u = d.lo + idx, cap = d.p.packet_cap;
+    gx_host_state *h = &d.hs[idx];
+    gx_host_state hs = *h;
+    const uint64_t key = rng4(d.p.seed, ST_PROBE, (uint64_t)d.round, 0, 0);
+    for (uint32_t c = 0; c < 2; c++) {
+      const size_t x = (size_t)idx * d.KE + d.KG + c;
+      if (lane == 0) {
+        d.msg_len[x] = 0;
+        d.msg_key[x] = u * d.KE + d.KG + c;
+      }
+      if (departed(d, u)) continue;
+      uint32_t peer;
+      if (c == 0) {  // the ping: u's image, when u probes this round
+        if (!probe_tick_of(d, u)) continue;
+        peer = feistel_perm(key, u, d.H);
+        if (peer == u) continue;
+      } else {  // the ack: to the preimage, when its ping reached u
+        peer = feistel_inv(key, u, d.H);
+        if (peer == u || departed(d, peer) || !probe_tick_of(d, peer) || !reach(d, peer, u)) continue;
+      }
+      const bool ok = reach(d, u, peer), local = peer - d.lo < d.Hl;
+      uint32_t pos = lane == 0 && ok && local ? inbox_claim(d, peer - d.lo) : 0xffffffffu;
+      pos = (uint32_t)__shfl((int)pos, 0, T);
+      uint32_t lim = d.p.limit_bytes;
+      bool call = true;
+      if (lim) {  // the ping or ack message takes its bytes first
+        const uint32_t used = d.p.fd_msg_bytes + 2;
+        lim = lim > used ? lim - used : 0;
+        call = lim > d.p.overhead_bytes;
+      }
+      grec *pk = pos < d.DR ? &d.in_rec[((size_t)(peer - d.lo) * d.DR + pos) * cap] : &d.msg[x * cap];
+      const bool rlk = pos != 0xffffffffu && host_locked(d, peer);
+      const bool filt = d.sfilt && pos != 0xffffffffu && !(rlk && d.p.lock_model);
+      uint32_t l = 0;
+      if (call)
+        l = get_broadcasts_team<T>(d, a, u, hs, cap, pk, lim, d.p.overhead_bytes, nullptr,
+                                   filt ? &d.view[(size_t)(peer - d.lo) * d.R] : nullptr, peer - d.lo);
+      if (rlk && l && lane == 0) {
+        a.locked = true;
+        if (d.p.lock_model) flag_live(d, peer - d.lo, l);
+        else a.c[C_LOCKED_MERGES] += l;
+      }
+      if (lane == 0) {
+        kb += 16 + 32ull * l + (filt ? 8ull * l : 0);
+        d.msg_len[x] = ok ? l : 0;
+        lost += l && !ok;
+        d.msg_dst[x] = peer;
+        if (pos != 0xffffffffu) inbox_header(d, peer - d.lo, pos, u * d.KE + d.KG + c, (uint32_t)x, l);
+      }
+    }
+    if (lane == 0) *h = hs;
+  }
+  acc_flush(d, a);
+  if (lost) ctr_atomic(d, C_LOST, lost);
+  kb = wave_sum(kb);
+  if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SEND, kb, 0);
+}
 
 // ============================================================== phase 4: gather-then-merge ==
 // One wave per receiver. Its inbox (the packet headers the senders registered, in arrival order)
