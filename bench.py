@@ -154,6 +154,33 @@ def queue_report(cfg, st0, st1):
             "faithful": d["queue_drops"] == 0 and d["sleep_drops"] == 0 and d["locked_merges"] == 0}
 
 
+def expiry_report(st0, st1):
+    """Alive-lifespan expiries over a run (TombstoneOthersServices, services_state.go:655-679), and
+    the false ones: expiries of records whose owner host is live (gx.h false_expiries). A faithful
+    steady-state figure where the catalog never agrees bit for bit: live owners restamp every 60 s
+    (services_state.go:547) and a view that has not heard a refresh for ALIVE_LIFESPAN (80 s) tombstones
+    the record."""
+    return {k: st1[k] - (st0[k] if st0 else 0) for k in ("expired", "false_expiries")}
+
+
+def merges_by_source(st0, st1):
+    """Record-merges of the window by where the record came from: gossip packets merged on arrival,
+    records that waited in a locked host's inbound pipeline (merged at its unlock), push-pull Merge of
+    a partner's full state, and the owners' own TrackNewServices merges."""
+    d = {k: st1[k] - st0[k] for k in ("gossip_merges", "ae_merges", "local_merges", "lock_drained")}
+    return {"gossip_packets": d["gossip_merges"] - d["lock_drained"], "lock_pipeline_drained": d["lock_drained"],
+            "push_pull": d["ae_merges"], "owner_local": d["local_merges"]}
+
+
+def device_time_share(kern):
+    """Each kernel class's share of the window's device time (the per-launch-event pass); says what
+    the headline's wall time is spent on (e.g. the ExpireServer storm, not merging)."""
+    if not kern:
+        return None
+    tot = sum(v["ms"] for v in kern.values())
+    return {k: round(v["ms"] / tot, 4) for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["ms"])} if tot else None
+
+
 def lock_report(p, st0, st1, hosts=None, rnd=None):
     """The ServicesState lock held by a blocked looper (gx.h lock_model) over a run:
     records held in locked hosts' inbound pipelines, dropped at a full pipeline (memberlist's handoff
@@ -220,7 +247,10 @@ class Cluster:
         return dict(zip(keys, [int(x) for x in t.tolist()]))
 
     def close(self):
-        self.e.close()
+        if self.shard is not None:
+            self.shard.close()  # drains the engine's streams before the process group goes
+        else:
+            self.e.close()
 
 
 def gossip_stretch_start(cfg, accepting=False):
@@ -461,7 +491,9 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
                 break
         st_end = c.stats()
         hosts = (c.e.hosts(), c.round) if world == 1 else (None, None)
-        return conv, wall, c.round, samples, queue_report(cfg, None, st_end), lock_report(c.e.params, None, st_end, *hosts)
+        lr = lock_report(c.e.params, None, st_end, *hosts)
+        lr["expiries"] = expiry_report(None, st_end)
+        return conv, wall, c.round, samples, queue_report(cfg, None, st_end), lr
     finally:
         c.close()
 
@@ -701,8 +733,10 @@ def main():
                     "converge_wall_s": round(w, 3) if r else None, "rounds_run": ran,
                     "simulated_s": (r * 0.2) if r else None, "queues": qr, "lock": lr}
     spread = None
+    # per-version spread after the heal, or from round 0 where there is no partition (defined at any
+    # cadence, on every line)
     heal = CONFIGS[args.config]["p"].get("partition_end", 0)
-    if world == 1 and heal and not args.no_converge:  # per-version spread after the heal (defined at any cadence)
+    if world == 1 and not args.no_converge:
         e = make_engine(lib, args.config, seed, local_rank)
         try:
             spread = version_spread(e, torch.device(f"cuda:{local_rank}"), heal, max(heal + 10, args.spread_max))
@@ -737,7 +771,10 @@ def main():
                                        + ("RCCL all-to-all)" if backend == "nccl" else "gloo, host-staged all-to-all)")
                                        if world > 1 else "single GPU")},
             "gossip_merges_per_s": split["gossip_merges"] / dt_max, "ae_merges_per_s": split["ae_merges"] / dt_max,
-            "merges": split, "queues": queue_report(args.config, st0, st1), "lock": lock,
+            "merges": split, "merges_by_source": merges_by_source(st0, st1),
+            "device_time_share": device_time_share(kern),
+            "expiries": expiry_report(st0, st1),
+            "queues": queue_report(args.config, st0, st1), "lock": lock,
             "lock_off": lock_off,
             "gossip": gossip, "converge": conv, "converge_lock_off": conv_lock_off,
             "converge_ref_cadence": conv_ref,
@@ -753,6 +790,9 @@ def main():
                 "lost_packets", "expire_server")}
         print(json.dumps(out), flush=True)
     if dist is not None:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         dist.destroy_process_group()
 
 

@@ -278,6 +278,14 @@ typedef struct gx_params {
    * limit_bytes. Parity unpinned (the fork is absent); 0 (default) = gossip() only, the rounds 1-5
    * model. Unsharded engines without the failure detector only (GX_EINVAL otherwise). */
   uint32_t probe_piggyback;
+  /* GX_PP_INITIATE only: 1 = memberlist's staggered push-pull timers (pushPullTrigger waits a random
+   * stagger in [0, PushPullInterval) before its first tick, so the nodes' exchanges spread over the
+   * interval instead of all starting together): host i initiates in the rounds with
+   * round % ae_period_rounds == its seeded phase, every round being a push-pull round for some
+   * hosts. 0 (default) = every live host initiates in the rounds with round % period == ae_phase.
+   * Parity unpinned (the fork is absent). memberlist also scales the interval with the cluster
+   * size (pushPullScale: x (ceil(log2 n - 5) + 1) above 32 nodes); that is ae_period_rounds. */
+  uint32_t push_pull_stagger;
 } gx_params;
 #define GX_LOCK_BUF_MAX_BYTES (1ull << 36) /* 64 GiB of lock_buffer records per engine */
 #define GX_PP_MATCHING 0

@@ -31,7 +31,7 @@ typedef struct grec {
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
 enum { X_SAME = 0, X_LEAD = 1, X_FOLLOW = 2 }; /* a cross pair's row block in the push-pull delta */
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5,
-       ST_INIT_AGE = 6, ST_AE = 7, ST_PROBE = 12 };
+       ST_INIT_AGE = 6, ST_AE = 7, ST_PROBE = 12, ST_PP_PHASE = 13 };
 
 struct gx_engine {
   gx_params p;
@@ -1063,7 +1063,13 @@ static void round_merge(gx_engine *e) {
 }
 
 static int ae_round(const gx_engine *e) {
+  if (e->p.ae_period_rounds && e->p.push_pull_stagger) return 1; /* some host's staggered timer, every round */
   return e->p.ae_period_rounds && (uint64_t)e->round % e->p.ae_period_rounds == e->p.ae_phase;
+}
+/* gx.h push_pull_stagger: host i's push-pull timer fires in the rounds of its seeded phase */
+static int pp_initiates(const gx_engine *e, uint32_t i) {
+  if (!e->p.push_pull_stagger) return 1;
+  return (uint64_t)e->round % e->p.ae_period_rounds == rng4(e->p.seed, ST_PP_PHASE, i, 0, 0) % e->p.ae_period_rounds;
 }
 
 /* Push-pull pairs of this round in global pair order t: (a, b). Returns the count. */
@@ -1185,7 +1191,7 @@ static uint32_t pp_batches(const gx_engine *e, uint32_t *pa, uint32_t *pb, uint3
   uint32_t n = 0, nb = 0;
   for (uint32_t i = 0; i < e->H; i++) {
     uint32_t b;
-    if (departed(e, i) || !ae_partner(e, i, &b) || departed(e, b)) continue;
+    if (!pp_initiates(e, i) || departed(e, i) || !ae_partner(e, i, &b) || departed(e, b)) continue;
     const uint32_t k = 1 + (last[i] > last[b] ? last[i] : last[b]);
     last[i] = last[b] = k;
     ia[n] = i;
@@ -1426,6 +1432,8 @@ static int check_params(const gx_params *p) {
                                p->lock_buffer * 16ull > GX_LOCK_BUF_MAX_BYTES)
     return GX_EINVAL; /* the pipelines' records (gx.h lock_buffer) */
   if (p->probe_piggyback > 1 || (p->probe_piggyback && (p->fd_enable || p->n_shards > 1 || p->fd_probe_rounds < 1)))
+    return GX_EINVAL;
+  if (p->push_pull_stagger > 1 || (p->push_pull_stagger && (p->push_pull_mode != GX_PP_INITIATE || !p->ae_period_rounds)))
     return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;

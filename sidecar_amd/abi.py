@@ -114,6 +114,7 @@ class GxParams(C.Structure):
         ("fd_push_pull_state", C.c_uint32),
         ("gossip_messages", C.c_uint32), ("push_pull_mode", C.c_uint32), ("inbox_slots", C.c_uint32),
         ("lock_model", C.c_uint32), ("lock_buffer", C.c_uint32), ("probe_piggyback", C.c_uint32),
+        ("push_pull_stagger", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)

@@ -99,7 +99,7 @@ struct DevCtr {
 
 enum { SRC_GOSSIP = 0, SRC_AE = 1, SRC_LOCAL = 2 };
 enum { ST_PEER = 1, ST_PHASE_BS = 2, ST_PHASE_BT = 3, ST_CHURN = 4, ST_INIT_TS = 5, ST_INIT_AGE = 6,
-       ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11, ST_PROBE = 12 };
+       ST_AE = 7, ST_FD_PHASE = 8, ST_FD_PERM = 9, ST_FD_RELAY = 10, ST_DEPART = 11, ST_PROBE = 12, ST_PP_PHASE = 13 };
 
 #define XPLAN_BATCH 64  // rounds of planned-exchange slot bounds per k_xplan launch
 #define XPLAN_GMAX 64   // shards the planned exchange supports

@@ -519,7 +519,13 @@ static int round_merge_impl(gx_engine *e) {
 #endif
 static bool ae_round(const gx_engine *e) {
   const Dev &d = e->d;
+  if (d.p.ae_period_rounds && d.p.push_pull_stagger) return true;  // some host's staggered timer, every round
   return d.p.ae_period_rounds && (uint64_t)d.round % d.p.ae_period_rounds == d.p.ae_phase;
+}
+// gx.h push_pull_stagger: host i's push-pull timer fires in the rounds of its seeded phase
+static bool pp_initiates(const Dev &d, uint32_t i) {
+  if (!d.p.push_pull_stagger) return true;
+  return (uint64_t)d.round % d.p.ae_period_rounds == rng4(d.p.seed, ST_PP_PHASE, i, 0, 0) % d.p.ae_period_rounds;
 }
 
 // GX_PP_INITIATE (unsharded engines): every live host starts one exchange with a partner drawn
@@ -547,7 +553,9 @@ static int ae_initiate(gx_engine *e) {
   uint32_t nb = 0;
   for (uint32_t i = 0; i < d.H; i++) {
     uint32_t b;
-    if ((dep && departed_at(d.p, d.round, i)) || !ae_partner(d, i, &b) || (dep && departed_at(d.p, d.round, b))) continue;
+    if (!pp_initiates(d, i) || (dep && departed_at(d.p, d.round, i)) || !ae_partner(d, i, &b) ||
+        (dep && departed_at(d.p, d.round, b)))
+      continue;
     const uint32_t k = 1 + std::max(last[i], last[b]);
     last[i] = last[b] = k;
     ia.push_back(i);
@@ -762,6 +770,8 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL; // the pipelines' records (gx.h lock_buffer)
   if (p->probe_piggyback > 1 || (p->probe_piggyback && (p->fd_enable || p->n_shards > 1 || p->fd_probe_rounds < 1)))
     return GX_EINVAL;
+  if (p->push_pull_stagger > 1 || (p->push_pull_stagger && (p->push_pull_mode != GX_PP_INITIATE || !p->ae_period_rounds)))
+    return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -775,8 +785,12 @@ static int check_params(const gx_params *p) {
 int gx_destroy(gx_engine *e) {
   if (!e) return GX_EINVAL;
   (void)hipSetDevice(e->device);
+  // every stream that may still run a kernel over the engine's buffers, before any is freed (the
+  // planned exchange's look-ahead k_xplan batch on xplan_stream included: it was synchronized only
+  // after the frees before round 6)
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->side_stream) (void)hipStreamSynchronize(e->side_stream);
+  if (e->xplan_stream) (void)hipStreamSynchronize(e->xplan_stream);
   for (auto &t : e->pending_ev) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
@@ -795,7 +809,6 @@ int gx_destroy(gx_engine *e) {
   if (e->side_start) (void)hipEventDestroy(e->side_start);
   if (e->side_done) (void)hipEventDestroy(e->side_done);
   if (e->scan_snap) (void)hipHostFree(e->scan_snap);
-  if (e->xplan_stream) (void)hipStreamSynchronize(e->xplan_stream);
   if (e->xplan_dev) (void)hipFree(e->xplan_dev);
   if (e->xplan_host) (void)hipHostFree(e->xplan_host);
   for (int i = 0; i < 2; i++)
@@ -1884,14 +1897,18 @@ int gx_outbox_pack(gx_engine *e, void *buf, uint64_t cap) {
   return phase_done(e);
 }
 
+static bool send_packs(const Dev &d);
 // Batch `start` of slot bounds into host slot k (asynchronous, on xplan_stream).
 static int xplan_launch(gx_engine *e, int k, int64_t start) {
   Dev &d = e->d;
   const size_t n = (size_t)XPLAN_BATCH * d.G * d.G;
   uint32_t *dev = e->xplan_dev + (size_t)k * n;
-  // the rounds queued so far may read this half (a packing k_send): the rewrite waits for them
-  HIPCHK(hipEventRecord(e->xplan_join, e->stream));
-  HIPCHK(hipStreamWaitEvent(e->xplan_stream, e->xplan_join, 0));
+  // the rounds queued so far may read this half (a packing k_send, Dev::ob_cnt): the rewrite waits
+  // for them; without packing sends only the host half is read, so the look-ahead runs at once
+  if (send_packs(d)) {
+    HIPCHK(hipEventRecord(e->xplan_join, e->stream));
+    HIPCHK(hipStreamWaitEvent(e->xplan_stream, e->xplan_join, 0));
+  }
   HIPCHK(hipMemsetAsync(dev, 0, sizeof(uint32_t) * n, e->xplan_stream));
   k_xplan<<<dim3(nblk(d.H, 256), XPLAN_BATCH), 256, 0, e->xplan_stream>>>(d, start, dev);
   HIPCHK(hipGetLastError());

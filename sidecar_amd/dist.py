@@ -303,11 +303,18 @@ class DistShard:
         if after_pack is not None:
             after_pack()  # shard-local pairs on the engine's side stream, beside the collective
         recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
-        # every rank runs the same number of calls: ceil(largest per-peer segment / CHUNK)
-        calls = (max(max(r) for r in m) + self.CHUNK - 1) // self.CHUNK
-        if calls == 1:
+        self._a2a_chunked(recv, send, rs, ss, max(max(r) for r in m))
+        self.s.sync()
+        return recv
+
+    def _a2a_chunked(self, recv, send, rs, ss, largest):
+        """all_to_all_single of per-peer segments, split into calls of at most CHUNK bytes per peer.
+        `largest`: the largest segment between any two ranks (every rank knows the whole size
+        matrix), so every rank makes the same number of calls, ceil(largest / CHUNK)."""
+        calls = (int(largest) + self.CHUNK - 1) // self.CHUNK
+        if calls <= 1:
             self._a2a(recv, send, rs, ss)
-            calls = 0
+            return
         soff = np.concatenate([[0], np.cumsum(ss)])
         roff = np.concatenate([[0], np.cumsum(rs)])
         for c in range(calls):
@@ -322,36 +329,44 @@ class DistShard:
                 if r_part[p]:
                     recv[int(roff[p]) + lo:int(roff[p]) + lo + r_part[p]].copy_(r_buf[o:o + r_part[p]])
                 o += r_part[p]
-        self.s.sync()
-        return recv
 
     def _planned_bufs(self):
-        """Send and receive buffers of the planned exchange, allocated once at their bounds: a
-        shard sends at most fanout packet slots per host, and receives at most that per host of
-        the other shards (gx.h gx_exchange_plan)."""
+        """The send buffer of the planned exchange, allocated once at its bound (k_send writes the
+        slots straight into it, before the round's counts reach the host: a shard sends at most
+        fanout packet slots per host, gx.h gx_exchange_plan), and the plan matrix."""
         if getattr(self, "_pb", None) is None:
             p = self.e.params
             slot = 16 + 16 * p.packet_cap
             hl = self.e.hi - self.e.lo
             send = torch.empty(hl * p.fanout * slot, dtype=torch.uint8, device=self.device)
-            recv = torch.empty((p.n_hosts - hl) * p.fanout * slot, dtype=torch.uint8, device=self.device)
-            self._pb = (send, recv, np.zeros(self.world * self.world, dtype=np.uint64))
+            self._pb = (send, np.zeros(self.world * self.world, dtype=np.uint64))
+            self._precv = torch.empty(0, dtype=torch.uint8, device=self.device)
         return self._pb
+
+    def _planned_recv(self, nr: int) -> torch.Tensor:
+        """The receive buffer, grown to this round's planned size when a round needs more (with a
+        quarter of headroom); the bound, every other shard's fanout slots per host, is only reached
+        when every packet of the cluster comes here."""
+        if nr > self._precv.numel():
+            self._precv = torch.empty(nr + nr // 4, dtype=torch.uint8, device=self.device)
+        return self._precv
 
     def _gossip_planned(self) -> bool:
         """One planned gossip round in two engine calls around the all-to-all; True when it is a
-        push-pull round (the caller runs the push-pull steps and round_end)."""
+        push-pull round (the caller runs the push-pull steps and round_end). A per-peer segment over
+        CHUNK goes in several calls, like _exchange's."""
         e = self.e
-        send, recv, plan = self._planned_bufs()
+        send, plan = self._planned_bufs()
         e.round_gossip_begin(plan, _ptr(send), send.numel())
         m = plan.reshape(self.world, self.world)
         ss = [int(x) for x in m[self.rank]]
         rs = [int(m[src][self.rank]) for src in range(self.world)]
         self.last_sizes = m[self.rank].copy()
         ns, nr = sum(ss), sum(rs)
-        if max(max(ss), max(rs)) > self.CHUNK or ns > send.numel() or nr > recv.numel():
+        if ns > send.numel():
             raise RuntimeError("planned exchange larger than its bound")  # cannot happen (gx.h)
-        self._a2a(recv[:nr], send[:ns], rs, ss)
+        recv = self._planned_recv(nr)
+        self._a2a_chunked(recv[:nr], send[:ns], rs, ss, int(m.max()))
         return e.round_gossip_end(_ptr(recv), nr)
 
     def _all_locked(self) -> bool:
@@ -396,6 +411,20 @@ class DistShard:
                 e.round_end()
             elif not planned:
                 e.round_end()
+
+    def close(self):
+        """Wait for the engine's work (its stream and the planned exchange's look-ahead stream) and
+        free it, before the caller tears the process group down: RCCL's communicator teardown
+        must not race the engine's kernels or buffers."""
+        if getattr(self, "e", None) is None:
+            return
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.e.close()
+        self._pb = None
+        self._precv = None
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def stats(self) -> dict:
         st = self.e.stats()

@@ -50,7 +50,7 @@ def test_local_shards_take_the_planned_exchange(oracle_lib, kw, planned):
     assert sh.stats()["gossip_merges"] == whole.stats()["gossip_merges"]
 
 
-def _worker(rank, world, port, kw, q):
+def _worker(rank, world, port, kw, q, chunk=None, rounds=6):
     import torch.distributed as dist
     from sidecar_amd.dist import DistShard
     from tests.oracle_lib import load_oracle
@@ -58,9 +58,13 @@ def _worker(rank, world, port, kw, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sh = DistShard(load_oracle(), rank, world, "cpu", **kw)
-    sh.run_rounds(6)
-    q.put((rank, dict(sh.exchange_paths), sh.stats()["gossip_merges"]))
+    if chunk:
+        sh.CHUNK = chunk  # every per-peer segment in several all-to-all calls
+    sh.run_rounds(rounds)
+    st = sh.stats()
+    q.put((rank, dict(sh.exchange_paths), st["gossip_merges"], st, sh.e.digests()))
     dist.barrier()
+    sh.close()
     dist.destroy_process_group()
 
 
@@ -149,3 +153,29 @@ def test_fused_round_calls_equal_separate_calls(oracle_lib):
         assert np.array_equal(ea.digests(), eb.digests())
         assert [bytes(h) for h in ea.hosts()] == [bytes(h) for h in eb.hosts()]
         assert ea.stats() == eb.stats()
+
+
+def test_dist_shard_planned_exchange_in_chunks(oracle_lib):
+    """A planned round whose per-peer segment exceeds CHUNK goes in several all-to-all calls over
+    the persistent buffers (every rank makes ceil(largest / CHUNK) of them): with CHUNK below one
+    packet slot (528 B) every gossip round is chunked, and the two gloo ranks end equal to the
+    unsharded oracle (counters summed over the shards)."""
+    kw = dict(BASE, gossip_messages=1, partition_end=0, n_hosts=48)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, kw, q, 200, 12)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] == {"planned": 12, "sized": 0} for r in res), res
+    whole = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    whole.run_rounds(12)
+    assert res[0][3] == whole.stats()
+    import numpy as np
+    dig = whole.digests()
+    half = kw["n_hosts"] // 2  # each rank's digests are its own hosts'
+    assert np.array_equal(res[0][4], dig[:half]) and np.array_equal(res[1][4], dig[half:])

@@ -35,7 +35,7 @@ def _worker(rank, world, port, kw, rounds, q):
         fd = sh.e.fd_converged()[1] if kw.get("fd_enable") else 0
         q.put((rank, sh.e.read_views(), host_tuples(sh.e), sh.e.digests(), st, (conv, fd), None))
         dist.barrier()
-        sh.e.close()
+        sh.close()
         dist.destroy_process_group()
     except Exception as ex:  # reported to the parent instead of a silent hang on q.get
         q.put((rank, None, None, None, None, None, repr(ex)))

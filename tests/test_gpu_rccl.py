@@ -67,7 +67,8 @@ def _worker(port, kw, rounds, q):
         st = sh.stats()
         conv = sh.converged()
         q.put((sh.e.read_views(), host_tuples(sh.e), sh.e.digests(), st, conv, ok_a2a, ok_red, None))
-        sh.e.close()
+        sh.close()  # the engine's streams drained and its buffers freed before RCCL's teardown
+        torch.cuda.synchronize()
         dist.destroy_process_group()
     except Exception as ex:  # reported to the parent instead of a silent hang on q.get
         q.put((None,) * 7 + (repr(ex),))

@@ -74,3 +74,29 @@ def test_false_expiries_count_live_owners(oracle_lib):
     d.run_rounds(600)
     sd = d.stats()
     assert 0 < sd["false_expiries"] < sd["expired"]
+
+
+@pytest.mark.parametrize("bad", [dict(push_pull_stagger=2), dict(push_pull_stagger=1),
+                                 dict(push_pull_stagger=1, push_pull_mode=1, ae_period_rounds=0)])
+def test_push_pull_stagger_rejects_unsupported_modes(oracle_lib, bad):
+    kw = dict(n_hosts=16, n_services=4, ae_period_rounds=10)
+    kw.update(bad)
+    with pytest.raises(GxError):
+        _eng(oracle_lib, **kw)
+
+
+def test_push_pull_stagger_spreads_the_exchanges(oracle_lib):
+    """memberlist's staggered push-pull timers (gx.h push_pull_stagger): every host still initiates
+    once per interval, but in the rounds of its own phase, so exchanges happen in most rounds and the
+    total over whole intervals equals the aligned model's."""
+    kw = dict(n_hosts=64, n_services=4, init_mode=INIT_WARM, push_pull_mode=1, ae_period_rounds=10, queue_cap=4096,
+              lock_model=0)
+    al, st = _eng(oracle_lib, **kw), _eng(oracle_lib, push_pull_stagger=1, **kw)
+    rounds_with = 0
+    for _ in range(40):
+        a0 = st.stats()["ae_exchanges"]
+        st.run_rounds(1)
+        rounds_with += st.stats()["ae_exchanges"] > a0
+    al.run_rounds(40)
+    assert al.stats()["ae_exchanges"] == st.stats()["ae_exchanges"] == 4 * 64
+    assert rounds_with >= 30
