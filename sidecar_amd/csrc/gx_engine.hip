@@ -367,6 +367,9 @@ static int round_send_impl(gx_engine *e) {
   hipStream_t s = e->stream;
   if (d.p.probe_piggyback) {  // the probe ping and ack calls come before the owner phase (gx.h)
     LaunchTimer t(e, GX_K_SEND);
+    // phase 0 first: inside a gx_run_rounds call the due sleepers re-enter the FIFOs in the owner
+    // tick (the oracle's ph_wake opens the round), which runs after these calls
+    k_wake<<<nblk(d.Hl, 64), 64, 0, s>>>(d);
     k_probe<4><<<nblk(d.Hl, 64), 256, 0, s>>>(d);
   }
   bool vec = (d.R % 2) == 0;
