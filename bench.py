@@ -66,7 +66,8 @@ CONFIGS = {
     "cfg2": dict(desc="4096 hosts x 16 services, fanout 3, cap 32 records/msg, own-records start, "
                       "push-pull every 10 rounds",
                  p=dict(n_hosts=4096, n_services=16, fanout=3, packet_cap=32, queue_cap=Q_GM1,
-                        list_slots=32, init_mode=1, ae_period_rounds=10)),
+                        list_slots=32, init_mode=1, ae_period_rounds=10),
+                 converge=dict(max_rounds=60000, over=dict(queue_cap=1 << 20))),
     # configs[2]: 16384 x 16 with 5% churn/round and alive-lifespan expiry
     "cfg3": dict(desc="16384 hosts x 16 services, 5% of owners start/stop a service per round, 5% of "
                       "records aged U[0,100s] (alive-lifespan expiry), push-pull every 10 rounds",
@@ -75,7 +76,8 @@ CONFIGS = {
     # configs[3]: 8192 x 64, push-pull every 10 rounds
     "cfg4": dict(desc="8192 hosts x 64 services, push-pull full-state merge every 10 rounds",
                  p=dict(n_hosts=8192, n_services=64, fanout=3, queue_cap=Q_GM1, list_slots=32, init_mode=1,
-                        ae_period_rounds=10)),
+                        ae_period_rounds=10),
+                 converge=dict(max_rounds=60000, over=dict(queue_cap=1 << 20))),
     # cfg 5 driven by memberlist's failure detector instead of the scripted storm:
     # the partition drops packets, SWIM probes suspect the other half, Lifeguard timers decide
     # (for a 10 s partition at this size they do not expire: refutations win after the heal)
@@ -133,13 +135,15 @@ def merges(st):
     return st["gossip_merges"] + st["ae_merges"] + st["local_merges"]
 
 
-def queue_report(cfg, st0, st1):
+def queue_report(cfg, st0, st1, queue_cap=None):
     """The broadcast queues over a run (gx.h gx_job): jobs deferred past the stored window, jobs LOST
     (deferred jobs GetBroadcasts reached: the reference would have sent them), the first round of a
     LOST dequeue, SendServices lists that did not fit, sleep-ring overflow, and the reference's own
     MAX_PENDING_LENGTH truncation (services_delegate.go:109-120, not a deviation). faithful: no job
     the reference would deliver was lost (every packet and looper state is the reference's)."""
-    p = CONFIGS[cfg]["p"]
+    p = dict(CONFIGS[cfg]["p"])
+    if queue_cap:
+        p["queue_cap"] = queue_cap  # the run's own stored window (a converge run may widen it)
     ke = p.get("fanout", 3) * max(1, p.get("gossip_messages", 0))
     d = {k: st1[k] - (st0[k] if st0 else 0) for k in ("queue_deferred", "queue_drops", "list_drops", "sleep_drops",
                                                        "pending_drops", "retransmits", "dequeues",
@@ -465,11 +469,12 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
     taken from the engine's last-change round, so the chunk only bounds when agreement is seen),
     catalog agreement checked between chunks (check time excluded). Returns (rounds_to_converge or
     None, wall_s, rounds run, disagreement samples, queue report, lock report): the samples are the
-    records some live views disagree on, every 100 rounds (every 1000 past round 10000)."""
+    records some live views disagree on, every 100 rounds (every 1000 past round 10000). Without
+    agreement the lock report carries `steady_state` (steady_state())."""
     c = Cluster(lib, cfg, seed, rank, world, local_rank, barrier, device, **over)
     wall = 0.0
     conv = None
-    samples = []
+    samples, state = [], []
     st_end = None
     try:
         while c.round < max_rounds:
@@ -481,6 +486,15 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
             ok, bad = c.converged()
             if (c.round % 100 == 0 and (c.round <= 10000 or c.round % 1000 == 0)) or ok:
                 samples.append([c.round, int(bad)])
+                if world == 1 and not ok:
+                    hs = c.e.hosts()
+                    st = c.stats()
+                    depth = [h.fifo_tail - h.fifo_head for h in hs]
+                    state.append({"round": c.round, "disagreeing": int(bad),
+                                  "hosts_locked": sum(h.locked_at(c.round) for h in hs),
+                                  "mean_fifo_depth": sum(depth) / len(depth), "max_fifo_depth": max(depth),
+                                  "false_expiries": st["false_expiries"], "ae_exchanges": st["ae_exchanges"],
+                                  "queue_drops": st["queue_drops"]})
             if ok:
                 lc = c.stats()["last_change_round"]
                 conv = lc + 1  # the catalog stopped changing after round lc and agrees
@@ -493,9 +507,47 @@ def run_converge(lib, cfg, seed, rank, world, local_rank, barrier, max_rounds, c
         hosts = (c.e.hosts(), c.round) if world == 1 else (None, None)
         lr = lock_report(c.e.params, None, st_end, *hosts)
         lr["expiries"] = expiry_report(None, st_end)
-        return conv, wall, c.round, samples, queue_report(cfg, None, st_end), lr
+        if conv is None and state:
+            lr["steady_state"] = steady_state(state, c.e.params.n_hosts)
+        return conv, wall, c.round, samples, queue_report(cfg, None, st_end, c.e.params.queue_cap), lr
     finally:
         c.close()
+
+
+def steady_state(state, n_hosts):
+    """What a run that never agrees settles into, from the samples of its second half: the share of
+    hosts whose looper holds the ServicesState lock, broadcast-queue depth, records the views disagree
+    on, and the false-expiry and push-pull rates, with each quantity's change between the third and the
+    fourth quarter of the run (`drift`, relative): a stationary regime (|drift| small) whose sampled
+    state never reaches agreement is the documented answer where rounds-to-converge does not exist."""
+    half = state[len(state) // 2:]
+    if len(half) < 4:
+        return None
+    q3, q4 = half[:len(half) // 2], half[len(half) // 2:]
+
+    def mean(rows, k):
+        return sum(r[k] for r in rows) / len(rows)
+
+    def rate(rows, k):
+        return (rows[-1][k] - rows[0][k]) / max(1, rows[-1]["round"] - rows[0]["round"])
+
+    out = {"rounds": [half[0]["round"], half[-1]["round"]], "samples": len(half),
+           "hosts_locked_frac": round(mean(half, "hosts_locked") / n_hosts, 4),
+           "hosts_locked_min": min(r["hosts_locked"] for r in half),
+           "mean_fifo_depth": round(mean(half, "mean_fifo_depth"), 1),
+           "max_fifo_depth": max(r["max_fifo_depth"] for r in half),
+           "disagreeing_min": min(r["disagreeing"] for r in half),
+           "false_expiries_per_round": round(rate(half, "false_expiries"), 2),
+           "push_pull_exchanges_per_round": round(rate(half, "ae_exchanges"), 4),
+           "queue_drops": half[-1]["queue_drops"]}
+    drift = {}
+    for k, f in (("hosts_locked", mean), ("mean_fifo_depth", mean), ("disagreeing", mean)):
+        a, b = f(q3, k), f(q4, k)
+        drift[k] = round((b - a) / a, 4) if a else None
+    a, b = rate(q3, "false_expiries"), rate(q4, "false_expiries")
+    drift["false_expiries_per_round"] = round((b - a) / a, 4) if a else None
+    out["drift_q3_to_q4"] = drift
+    return out
 
 
 def _oracle_rate(lib, cfg, h_sample, warmup, steps):
@@ -711,8 +763,13 @@ def main():
     conv = None
     conv_lock_off = None
     if not args.no_converge:
+        # a config may follow its converge run further, with a stored FIFO window that keeps it
+        # lossless that long (CONFIGS[...]["converge"]; the window's size does not change any result
+        # while no job is LOST, gx.h gx_job)
+        cv = CONFIGS[args.config].get("converge", {})
+        cmax = args.converge_max if args.converge_max != 3000 else cv.get("max_rounds", 3000)
         r, w, ran, dis_s, qr, lr = run_converge(lib, args.config, seed, rank, world, local_rank, barrier,
-                                                args.converge_max, args.check_every)
+                                                cmax, args.check_every, **cv.get("over", {}))
         conv = {"rounds_to_converge": r, "converge_wall_s": round(w, 3) if r else None,
                 "rounds_run": ran, "simulated_s": (r * 0.2) if r else None, "queues": qr, "lock": lr}
         if r is None:  # how far from agreement the catalog stays (records some live views disagree on)

@@ -92,7 +92,7 @@ def main():
                if any(s["all_at"] is not None for s in spread) else None,
                bs_blocked_host_rounds=blocked_bs, max_fifo_depth=int(maxdepth),
                stats={k: st[k] for k in ("gossip_accepts", "ae_accepts", "retransmits", "dequeues", "expired",
-                                         "ae_exchanges", "ae_locked", "lock_drops")})
+                                         "ae_exchanges", "ae_locked", "lock_drops", "false_expiries")})
     print(json.dumps(out))
 
 
