@@ -520,7 +520,8 @@ def steady_state(state, n_hosts):
     on, and the false-expiry and push-pull rates, with each quantity's change between the third and the
     fourth quarter of the run (`drift`, relative): a stationary regime (|drift| small) whose sampled
     state never reaches agreement is the documented answer where rounds-to-converge does not exist."""
-    half = state[len(state) // 2:]
+    last = state[-1]["round"]
+    half = [r for r in state if r["round"] >= last // 2]  # the second half of the run's rounds
     if len(half) < 4:
         return None
     q3, q4 = half[:len(half) // 2], half[len(half) // 2:]
@@ -605,7 +606,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-split", action="store_true", help="skip the instrumented per-kernel pass")
     ap.add_argument("--cpu-hosts", type=int, default=16384, help="H of the multi-threaded CPU sample")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+    # HBM bytes per launch of each kernel class over the window's own launches (profiles/r06/pmc_window.py)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06", "pmc_window.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -717,7 +719,7 @@ def main():
         if k not in kern or not kern[k]["ms"]:
             return None
         ach = kern[k]["GBps"] or 0.0
-        # PMC traffic is measured on the N = 1 run (profiles/pmc_summary.json): per launch of the
+        # PMC traffic is measured on the N = 1 run (profiles/r06/pmc_window.json): per launch of the
         # whole engine, so only comparable with this line at N = 1
         traffic = (pmc.get(k) or {}).get("hbm_bytes_per_launch") if world == 1 and with_pmc else None
         return {"bound": "hbm", "kernel": k, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
