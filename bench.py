@@ -313,9 +313,14 @@ def gossip_round_span(lib, cfg, seed, local_rank, start=None, **over):
     e.set_stream(None, False)
     e.close()
     # SURVEY §8(d) algorithmic bytes of a gossip record-merge: 22 B (inbound record 13 + slot 9)
-    # + 9 B per accept + 13 B per retransmit queued; the stretch holds gossip rounds only
-    m, acc, rx = (s1[k] - s0[k] for k in ("gossip_merges", "gossip_accepts", "retransmits"))
-    byts = (22 * m + 9 * acc + 13 * rx) / n
+    # + 9 B per accept + 13 B per retransmit queued; the stretch holds gossip rounds only. With the
+    # ServicesState lock (gx.h lock_model) a locked receiver's records are not merged that round:
+    # each one appended to its inbound pipeline is 13 B read + 13 B written, each one that finds the
+    # pipeline full 13 B read (sent, then dropped), so a locked stretch's roofline is not 0 by
+    # construction
+    m, acc, rx, buf, drop = (s1[k] - s0[k] for k in ("gossip_merges", "gossip_accepts", "retransmits",
+                                                       "lock_buffered", "lock_drops"))
+    byts = (22 * m + 9 * acc + 13 * rx + 26 * buf + 13 * drop) / n
     gbs = byts / (us * 1e3)
     # Against the lines the round touches: the senders' filter reads each packet's receiver slots,
     # a run of consecutive slots per batch (an ExpireServer batch is one owner's 16 services, one
@@ -328,6 +333,7 @@ def gossip_round_span(lib, cfg, seed, local_rank, start=None, **over):
                           "rounds": [start, start + n - 1],
                           "bytes_per_round": int(byts), "merges_per_round": m // n,
                           "accepts_per_round": acc // n, "accept_fraction": round(acc / m, 4) if m else None,
+                          "pipeline_appends_per_round": buf // n, "pipeline_drops_per_round": drop // n,
                           "achieved": round(gbs, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                           "lock_model": int(e_lock),
