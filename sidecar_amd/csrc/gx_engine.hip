@@ -152,6 +152,11 @@ struct gx_engine {
   XBound xbound;                 // this shard's slots per destination this round
   const uint32_t *xbound_dev;    // the same row on the device
   uint32_t *ob_claim;            // Dev::ob_claim (gx_round_gossip_begin packing in k_send)
+  // the worklist expiry scan's row split (k_scan_split / k_scan_join): chunks per row, chunk length,
+  // each chunk's first L expirations and its result
+  uint32_t scan_nch, scan_clen;
+  grec *scan_tmp;
+  ScanChunk *scan_chunk;
 };
 
 static void codec_free(gx_engine *e);  // gx_codec_host.hpp
@@ -428,8 +433,13 @@ static int round_send_impl(gx_engine *e) {
     LaunchTimer t(e, GX_K_SCAN);
     const bool ev = !e->log_views.empty();
     const unsigned grid = d.Hl < SCAN_GRID ? d.Hl : SCAN_GRID;
-    (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
-        <<<grid, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
+    if (vec && !ev && e->scan_nch > 1) {  // rows split over blocks, then joined per view
+      k_scan_split<true><<<SCAN_GRID, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch, e->scan_clen);
+      k_scan_join<<<grid, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
+    } else {
+      (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
+          <<<grid, 256, 0, s>>>(d, d.scan_list, d.L, d.L, d.scan_cnt, -1);
+    }
     if (bt_apart) k_bt_finish<<<nblk(d.Hl, 256), 256, 0, s>>>(d);
   }
   if (d.p.fd_enable) {  // suspicion timers -> deadNode -> NotifyLeave; probe ticks
@@ -813,6 +823,8 @@ int gx_destroy(gx_engine *e) {
   if (e->side_done) (void)hipEventDestroy(e->side_done);
   if (e->scan_snap) (void)hipHostFree(e->scan_snap);
   if (e->xplan_dev) (void)hipFree(e->xplan_dev);
+  if (e->scan_tmp) (void)hipFree(e->scan_tmp);
+  if (e->scan_chunk) (void)hipFree(e->scan_chunk);
   if (e->xplan_host) (void)hipHostFree(e->xplan_host);
   for (int i = 0; i < 2; i++)
     if (e->xplan_ev[i]) (void)hipEventDestroy(e->xplan_ev[i]);
@@ -968,6 +980,16 @@ int gx_create(const gx_params *p, gx_engine **out) {
   ALLOC(d.minexp, sizeof(unsigned long long) * H);
   ALLOC(d.scan_list, sizeof(grec) * H * d.L);
   ALLOC(d.scan_cnt, sizeof(uint32_t) * H);
+  // worklist scans split rows of at least 64K slots into chunks of >= 32K (S | 128: owners never
+  // straddle a chunk; the split path runs without listeners)
+  e->scan_nch = 1;
+  if (d.R >= 65536 && d.S >= 2 && 128 % d.S == 0) {
+    e->scan_nch = d.R / 32768 < 16 ? d.R / 32768 : 16;
+    e->scan_clen = (d.R / e->scan_nch + 1023) / 1024 * 1024;
+    e->scan_nch = (d.R + e->scan_clen - 1) / e->scan_clen;
+    ALLOC(e->scan_tmp, sizeof(grec) * H * e->scan_nch * d.L);
+    ALLOC(e->scan_chunk, sizeof(ScanChunk) * H * e->scan_nch);
+  }
   ALLOC(d.tick, H);
   ALLOC(d.sbytes, sizeof(uint16_t) * d.R);
   ALLOC(d.srvt, sizeof(gx_server_times) * H * Hg);

@@ -523,8 +523,19 @@ struct ScanLds {
 #ifndef SCAN_PF
 #define SCAN_PF 1  // 4 tiles in flight (139 VGPRs, 3 waves/SIMD) measured slower on cfg 3: 1.59 vs 1.29 ms per round
 #endif
+// A chunk's result of a row split over blocks (k_scan_split, joined per view by k_scan_join).
+struct ScanChunk {
+  uint32_t cnt;              // expirations in the chunk (its first list_cap are listed)
+  uint32_t last;             // 1 + the chunk's last expired key, 0 = none
+  unsigned long long mexp;   // the chunk's exact expiry bound
+};
+// [r0, r1): the slots this block streams (tile-aligned; the whole row by default). co: chunk mode,
+// the view's bookkeeping (list count, expiry bound, state.LastChanged, scan count) goes to *co for
+// k_scan_join instead of the view.
 template <bool VEC, bool EV>
-GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t *cnt_out, ScanLds &sm) {
+GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t *cnt_out, ScanLds &sm,
+                   uint32_t r0 = 0, uint32_t r1 = 0xffffffffu, ScanChunk *co = nullptr) {
+  if (r1 > d.R) r1 = d.R;
   unsigned long long *s_wave = sm.wave, *s_red = sm.red;
   uint32_t *s_lu = sm.lu;
   uint32_t &s_last = sm.last;
@@ -542,9 +553,9 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   auto ld_into = [&](uint32_t base, ulonglong2 *dst) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      const uint32_t r0 = base + 512 * h + 2 * t;
-      if (r0 < d.R) {
-        v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r0]));
+      const uint32_t q0 = base + 512 * h + 2 * t;
+      if (q0 < r1) {
+        v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[q0]));
         dst[h] = make_ulonglong2(x.x, x.y);
       } else {
         dst[h] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
@@ -553,7 +564,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   };
   if (VEC) {
 #pragma unroll
-    for (int q = 0; q < SCAN_PF; q++) ld_into(1024u * q, nx[q]);
+    for (int q = 0; q < SCAN_PF; q++) ld_into(r0 + 1024u * q, nx[q]);
   }
   // S | 128: an owner's slots sit in S/2 adjacent lanes of one wave, so the server times of a
   // tile's owners (the last expired record of each, key order) come from a ballot, with no LDS
@@ -684,13 +695,13 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
     n_exp += tn;
     listing = ev_on || !wave_times || n_exp < list_cap;  // without wave_times the LDS path keeps the server times
   };
-  for (uint32_t base = 0; base < d.R; base += SCAN_PF * 1024u) {
+  for (uint32_t base = r0; base < r1; base += SCAN_PF * 1024u) {
 #pragma unroll
     for (int q = 0; q < SCAN_PF; q++) {
       const uint32_t b = base + 1024u * q;
-      if (b >= d.R) break;
+      if (b >= r1) break;
       ulonglong2 cur[2] = {nx[q][0], nx[q][1]};
-      if (VEC && b + SCAN_PF * 1024u < d.R) ld_into(b + SCAN_PF * 1024u, nx[q]);
+      if (VEC && b + SCAN_PF * 1024u < r1) ld_into(b + SCAN_PF * 1024u, nx[q]);
       tile(b, cur);
     }
   }
@@ -702,7 +713,11 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
     last_key = (uint32_t)lk;
   }
   mexp = block_min(mexp, s_red);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && co) {  // chunk mode: k_scan_join finishes the view
+    co->cnt = n_exp;
+    co->last = last_key;
+    co->mexp = mexp;
+  } else if (threadIdx.x == 0) {
     atomicAdd(&d.work_cnt[GX_WC_SCANS], 1u);
     *cnt_out = n_exp;
     d.minexp[oi] = mexp;  // exact bound after the scan
@@ -715,11 +730,11 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   c_wr = wave_sum(c_wr);
   if ((threadIdx.x & 63) == 0) kbytes(d, GX_K_SCAN, c_wr * 8, 0);
   if (threadIdx.x == 0)
-    kbytes(d, GX_K_SCAN, (unsigned long long)d.R * 8 + 16ull * (n_exp < list_cap ? n_exp : list_cap), d.R);
+    kbytes(d, GX_K_SCAN, (unsigned long long)(r1 - r0) * 8 + 16ull * (n_exp < list_cap ? n_exp : list_cap), r1 - r0);
   block_ctr(d, C_EXPIRED, c_exp, s_red);
   block_ctr(d, C_FEXP, c_exp - c_dep, s_red);
   block_ctr(d, C_GC, c_gc, s_red);
-  block_ctr(d, C_SCANSLOTS, threadIdx.x == 0 ? d.R : 0, s_red);
+  block_ctr(d, C_SCANSLOTS, threadIdx.x == 0 ? r1 - r0 : 0, s_red);
 }
 
 // only_host >= 0: that one view (the API's TombstoneOthersServices), list at list_base, count in
@@ -743,6 +758,55 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
   }
 }
 
+
+// The worklist's rows split into nch tile-aligned chunks of `clen` slots, one block per (view,
+// chunk) (round 6): a row streamed by one block keeps too few bytes in flight, and a worklist of
+// fewer rows than resident blocks leaves CUs idle (cfg 3: 1,600 rows of 2 MB). Each chunk lists its
+// first list_cap expirations in key order at tmp[(oi * nch + c) * list_cap], writes its result to
+// chunk[oi * nch + c], and k_scan_join concatenates them: the same list, count, expiry bound and
+// state.LastChanged as scan_view over the whole row. Owners never straddle chunks (S | 128, the
+// wave_times path; no listeners).
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_scan_split(Dev d, grec *tmp, ScanChunk *chunk, uint32_t nch, uint32_t clen) {
+  __shared__ ScanLds sm;
+  const uint32_t n = *d.wl_cnt * nch;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t oi = d.work[w / nch], c = w % nch;
+    const size_t k = (size_t)oi * nch + c;
+    scan_view<VEC, false>(d, oi, &tmp[k * d.L], d.L, nullptr, sm, c * clen, (c + 1) * clen, &chunk[k]);
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(256) void k_scan_join(Dev d, const grec *tmp, const ScanChunk *chunk, uint32_t nch) {
+  __shared__ uint32_t s_pre[65];
+  const uint32_t n = *d.wl_cnt, L = d.L;
+  for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
+    const uint32_t oi = d.work[w];
+    const ScanChunk *ch = &chunk[(size_t)oi * nch];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0, last = 0;
+      unsigned long long mexp = ~0ull;
+      for (uint32_t c = 0; c < nch; c++) {
+        s_pre[c] = tot;
+        tot += ch[c].cnt;
+        mexp = ch[c].mexp < mexp ? ch[c].mexp : mexp;
+        if (ch[c].last) last = ch[c].last;
+      }
+      s_pre[nch] = tot;
+      d.scan_cnt[oi] = tot;
+      d.minexp[oi] = mexp;  // exact bound after the scan
+      if (last) d.vlc[oi] = ts_of(d.view[(size_t)oi * d.R + last - 1]);
+      atomicAdd(&d.work_cnt[GX_WC_SCANS], 1u);
+    }
+    __syncthreads();
+    grec *out = &d.scan_list[(size_t)oi * L];
+    for (uint32_t c = 0; c < nch && s_pre[c] < L; c++) {
+      const uint32_t nc = s_pre[c + 1] - s_pre[c], take = nc < L - s_pre[c] ? nc : L - s_pre[c];
+      for (uint32_t i = threadIdx.x; i < take; i += blockDim.x) out[s_pre[c] + i] = tmp[((size_t)oi * nch + c) * L + i];
+    }
+  }
+}
 
 // The rest of a BroadcastTombstones tick on its own, for rounds where other phases push to the
 // FIFO between the scan and the send (failure detector, storm); otherwise k_send runs it.
