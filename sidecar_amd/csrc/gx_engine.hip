@@ -154,7 +154,7 @@ struct gx_engine {
   uint32_t *ob_claim;            // Dev::ob_claim (gx_round_gossip_begin packing in k_send)
   // the worklist expiry scan's row split (k_scan_split / k_scan_join): chunks per row, chunk length,
   // each chunk's first L expirations and its result
-  uint32_t scan_nch, scan_clen;
+  uint32_t scan_nch;
   grec *scan_tmp;
   ScanChunk *scan_chunk;
 };
@@ -434,7 +434,7 @@ static int round_send_impl(gx_engine *e) {
     const bool ev = !e->log_views.empty();
     const unsigned grid = d.Hl < SCAN_GRID ? d.Hl : SCAN_GRID;
     if (vec && !ev && e->scan_nch > 1) {  // rows split over blocks, then joined per view
-      k_scan_split<true><<<SCAN_GRID, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch, e->scan_clen);
+      k_scan_split<true><<<SCAN_GRID, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
       k_scan_join<<<grid, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
     } else {
       (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
@@ -984,9 +984,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   // straddle a chunk; the split path runs without listeners)
   e->scan_nch = 1;
   if (d.R >= 65536 && d.S >= 2 && 128 % d.S == 0) {
-    e->scan_nch = d.R / 32768 < 16 ? d.R / 32768 : 16;
-    e->scan_clen = (d.R / e->scan_nch + 1023) / 1024 * 1024;
-    e->scan_nch = (d.R + e->scan_clen - 1) / e->scan_clen;
+    e->scan_nch = d.R / 32768 < 16 ? d.R / 32768 : 16;  // the most chunks a row takes (scan_chunks)
     ALLOC(e->scan_tmp, sizeof(grec) * H * e->scan_nch * d.L);
     ALLOC(e->scan_chunk, sizeof(ScanChunk) * H * e->scan_nch);
   }

@@ -766,23 +766,39 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
 // chunk[oi * nch + c], and k_scan_join concatenates them: the same list, count, expiry bound and
 // state.LastChanged as scan_view over the whole row. Owners never straddle chunks (S | 128, the
 // wave_times path; no listeners).
+// Chunks per row this round (both kernels derive the same from the worklist count n): enough
+// items for about SCAN_ITEMS blocks, at most nch (the allocation's stride); a long worklist keeps
+// whole rows (each chunk restarts the tile pipeline: 1,600 rows of cfg 3 in 8 chunks measured 8%
+// slower than whole rows, 400 rows 1.9x faster). clen: the chunk length, tile-aligned.
+#ifndef SCAN_ITEMS
+#define SCAN_ITEMS 4096u
+#endif
+GXD uint32_t scan_chunks(const Dev &d, uint32_t n, uint32_t nch, uint32_t &clen) {
+  uint32_t c = n ? (SCAN_ITEMS + n - 1) / n : 1;
+  c = c < nch ? c : nch;
+  clen = (d.R / c + 1023u) / 1024u * 1024u;
+  return (d.R + clen - 1) / clen;
+}
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_scan_split(Dev d, grec *tmp, ScanChunk *chunk, uint32_t nch, uint32_t clen) {
+__global__ __launch_bounds__(256) void k_scan_split(Dev d, grec *tmp, ScanChunk *chunk, uint32_t nch) {
   __shared__ ScanLds sm;
-  const uint32_t n = *d.wl_cnt * nch;
+  uint32_t clen;
+  const uint32_t nc = scan_chunks(d, *d.wl_cnt, nch, clen), n = *d.wl_cnt * nc;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
-    const uint32_t oi = d.work[w / nch], c = w % nch;
+    const uint32_t oi = d.work[w / nc], c = w % nc;
     const size_t k = (size_t)oi * nch + c;
     scan_view<VEC, false>(d, oi, &tmp[k * d.L], d.L, nullptr, sm, c * clen, (c + 1) * clen, &chunk[k]);
     __syncthreads();
   }
 }
-__global__ __launch_bounds__(256) void k_scan_join(Dev d, const grec *tmp, const ScanChunk *chunk, uint32_t nch) {
+__global__ __launch_bounds__(256) void k_scan_join(Dev d, const grec *tmp, const ScanChunk *chunk, uint32_t nch_max) {
   __shared__ uint32_t s_pre[65];
   const uint32_t n = *d.wl_cnt, L = d.L;
+  uint32_t clen;
+  const uint32_t nch = scan_chunks(d, n, nch_max, clen);
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const uint32_t oi = d.work[w];
-    const ScanChunk *ch = &chunk[(size_t)oi * nch];
+    const ScanChunk *ch = &chunk[(size_t)oi * nch_max];
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t tot = 0, last = 0;
@@ -803,7 +819,7 @@ __global__ __launch_bounds__(256) void k_scan_join(Dev d, const grec *tmp, const
     grec *out = &d.scan_list[(size_t)oi * L];
     for (uint32_t c = 0; c < nch && s_pre[c] < L; c++) {
       const uint32_t nc = s_pre[c + 1] - s_pre[c], take = nc < L - s_pre[c] ? nc : L - s_pre[c];
-      for (uint32_t i = threadIdx.x; i < take; i += blockDim.x) out[s_pre[c] + i] = tmp[((size_t)oi * nch + c) * L + i];
+      for (uint32_t i = threadIdx.x; i < take; i += blockDim.x) out[s_pre[c] + i] = tmp[((size_t)oi * nch_max + c) * L + i];
     }
   }
 }
