@@ -91,6 +91,11 @@ struct gx_engine {
   /* the ServicesState lock (gx.h lock_model) */
   uint32_t C;             /* lock_buffer: records a locked host's inbound pipeline holds */
   grec *lkb;              /* H * C  the records queued there, arrival order (count: hs.lock >> 8) */
+  /* diagnostic (gx_oracle_ro_runnable): the loopers holding each host's lock at the
+   * start of each round parity (flags & 3 of lock_snapshot), and the push-pull exchanges the model
+   * failed although every locked side held only BroadcastServices' read lock with no writer waiting */
+  uint8_t *lk_flags;
+  uint64_t ro_runnable;
   uint32_t PW;            /* words per host of pexp, ceil(H / 32) */
   uint32_t *pexp;         /* H * PW  owners whose ExpireServer waits for the host's lock (lazy) */
   int in_round;           /* inside a round phase: the lock applies (ABI entry points act directly) */
@@ -146,6 +151,16 @@ static inline int lock_on(const gx_engine *e) { return e->p.lock_model != 0 && e
 static void lock_snapshot(gx_engine *e, uint32_t v, int64_t round) {
   const uint32_t b = 1u << (round & 1);
   e->hs[v].lock = (e->hs[v].lock & ~b) | ((e->hs[v].flags & 3u) ? b : 0u);
+  if (e->lk_flags) e->lk_flags[2 * (size_t)v + (round & 1)] = (uint8_t)(e->hs[v].flags & 3u);
+}
+/* Go's RWMutex lets LocalState's RLock (services_delegate.go:148) through while the only holder is
+ * BroadcastServices' read lock (services_state.go:535) and no writer waits: no record in the host's
+ * pipeline (ProcessServiceMsgs would wait in AddServiceEntry's Lock), no waiting ExpireServer, no
+ * BroadcastTombstones tick due. The model fails such exchanges; this only counts them. */
+static int ro_runnable_side(const gx_engine *e, uint32_t v) {
+  const gx_host_state *h = &e->hs[v];
+  return e->lk_flags && e->lk_flags[2 * (size_t)v + (e->round & 1)] == 1u && !(h->flags & 2u) &&
+         GX_LOCK_BUF(h->lock) == 0 && !(h->lock & GX_LOCK_PENDING_EXPIRE) && h->bt_next > e->round;
 }
 static void note_locked(gx_engine *e) {
   if (e->st.first_locked_round < 0 || e->round < e->st.first_locked_round) e->st.first_locked_round = e->round;
@@ -813,6 +828,8 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
     note_locked(e);
     if (e->p.lock_model) {
       e->st.ae_locked++;
+      if ((!la || ro_runnable_side(e, a)) && (!lb || ro_runnable_side(e, b)))
+        __atomic_fetch_add(&e->ro_runnable, 1ull, __ATOMIC_RELAXED);
       return;
     }
   }
@@ -1346,6 +1363,13 @@ static void run_one_round(gx_engine *e) {
 
 /* ---------------------------------------------------------------------------- ABI ------- */
 int gx_abi_version(void) { return GX_ABI_VERSION; }
+/* Oracle-only diagnostic (not in gx.h): push-pull exchanges failed by the lock model although every
+ * locked side held only BroadcastServices' read lock with no writer waiting (ro_runnable_side). */
+int gx_oracle_ro_runnable(gx_engine *e, uint64_t *n) {
+  if (!e || !n) return GX_EINVAL;
+  *n = e->ro_runnable;
+  return GX_OK;
+}
 const char *gx_backend(void) { return "oracle-cpu"; }
 
 void gx_params_default(gx_params *p) {
@@ -1577,6 +1601,7 @@ int gx_create(const gx_params *p, gx_engine **out) {
   }
   if (p->lock_model) { /* the locked hosts' inbound pipelines and waiting ExpireServer calls */
     e->C = p->lock_buffer;
+    e->lk_flags = (uint8_t *)calloc(2 * (size_t)H, 1);
     e->lkb = (grec *)malloc(sizeof(grec) * H * e->C);
     e->PW = (e->H + 31) / 32;
     if (p->storm_round >= 0 || p->fd_enable) e->pexp = (uint32_t *)malloc(4ull * H * e->PW);
@@ -1638,6 +1663,7 @@ int gx_destroy(gx_engine *e) {
   free(e->fd_peers);
   free(e->fd_np);
   free(e->lkb);
+  free(e->lk_flags);
   free(e->pexp);
   free_names(e);
   free(e);
