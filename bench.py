@@ -45,6 +45,9 @@ CONFIGS = {
                  p=dict(n_hosts=32768, n_services=16, fanout=3, packet_cap=32, pending_cap=100,
                         queue_cap=20480, list_slots=32, init_mode=2, partition_start=0,
                         partition_end=50, storm_round=5, ae_period_rounds=10),
+                 # to ~12,000 rounds: past the first unlock (~5,460) and the relock, inside the stored
+                 # window's lossless horizon (~12,300)
+                 converge=dict(max_rounds=12000),
                  ref_variant="cfg5_ref"),
     # cfg 5 at the reference's own anti-entropy cadence: PushPullInterval 20 s (config/config.go:45,
     # main.go:252-256) = 100 rounds of GossipInterval 200 ms; reported beside cfg5 for its
