@@ -13,3 +13,8 @@ timeout -k 10 400 python -u profiles/r04/ab_kernels.py --config cfg3 --skip 100 
   --libs profiles/r06/ablib/libgx_base.so /tmp/libgx_si4096.so profiles/r06/ablib/libgx_si2048.so > $O/ab_scan_cfg3_lm$lm.jsonl 2>&1 || { echo ab failed; tail $O/ab_scan_cfg3_lm$lm.jsonl; exit 1; }
 tail -1 $O/ab_scan_cfg3_lm$lm.jsonl
 done
+# merge blocks of 16 receivers at cfg 5 (GX_MERGE_SMALL_HL raised): gossip stretches, lock on and off
+if [ -f profiles/r06/ablib/libgx_nr16.so ]; then
+timeout -k 10 600 python -u profiles/r06/ab_spans.py --libs /tmp/libgx_si4096.so profiles/r06/ablib/libgx_nr16.so --reps 3 > $O/ab_nr16.jsonl 2>&1 || { echo ab nr16 failed; tail $O/ab_nr16.jsonl; exit 1; }
+tail -1 $O/ab_nr16.jsonl
+fi

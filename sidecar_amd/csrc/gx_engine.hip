@@ -508,7 +508,11 @@ static int round_merge_impl(gx_engine *e) {
     // profiles/r03/ab/merge_wpe_gm15.jsonl); else 64 receivers per block (3% faster at cfg 5)
     // ... and when 64 receivers per block leave most CUs idle (a shard, a small cluster): a block's
     // waves fold their receivers one item after another, so fewer per block shortens the launch
-    const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL;
+    // ... and with the lock modelled (round 6): a locked receiver's pipeline append is a short
+    // dependent chain, and 64 receivers per block run a wave's four of them one after another; 16 per
+    // block spread them over more waves (cfg 5, locked gossip rounds 93.7 -> 87.7 us; lock off the
+    // 64-receiver blocks stay 3-5% faster, profiles/r06/ab/merge_nr16_cfg5.jsonl)
+    const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL || d.p.lock_model;
     const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
     if (small) {
       if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, MERGE_WPE_GM> : k_merge_seg<true, false, 16, MERGE_WPE_GM>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);

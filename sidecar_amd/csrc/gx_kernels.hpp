@@ -771,7 +771,7 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t l
 // whole rows (each chunk restarts the tile pipeline: 1,600 rows of cfg 3 in 8 chunks measured 8%
 // slower than whole rows, 400 rows 1.9x faster). clen: the chunk length, tile-aligned.
 #ifndef SCAN_ITEMS
-#define SCAN_ITEMS 4096u
+#define SCAN_ITEMS 2048u
 #endif
 GXD uint32_t scan_chunks(const Dev &d, uint32_t n, uint32_t nch, uint32_t &clen) {
   uint32_t c = n ? (SCAN_ITEMS + n - 1) / n : 1;
