@@ -73,3 +73,12 @@ def test_fd_defaults_identical(oracle_lib, n):
     if k:
         assert rounds[k] == math.ceil(tmin_ms / 200)  # k confirmations: the minimum
         assert rounds[0] >= rounds[1] >= rounds[2]
+
+
+def test_libgx_is_built_from_these_sources():
+    """The in-tree library the GPU tiers load was compiled from the sources in the tree (build.py's
+    content stamp, written by the build that produced it): a stale binary cannot pass for HEAD."""
+    from sidecar_amd import build
+    if build.needs_build():
+        build.build()
+    assert build.built_hash() == build.source_hash()
