@@ -180,7 +180,8 @@ def test_cfg5_full_h32768_parity(gx_lib, lock_readers):
     GX_ENOMEM and so does this test (no skip). With lock_readers = 1 (gx.h: an exchange whose locked
     sides hold only BroadcastServices' read lock with no writer waiting runs) the lock words carry
     the write-lock bits and the few exchanges that qualify (2 of 10240 at H = 2048 on the oracle,
-    all before the storm's jobs fill the pipelines) merge one way now and one way later."""
+    all before the storm's jobs fill the pipelines) merge one way now and one way later, or lose the
+    waiting half when the host's pool slot is taken (both engines count it in ae_defer_lost)."""
     orc = _omp_oracle()
     H = 32768
     _progress("cfg5@32768: creating the HIP engine and the OpenMP oracle")
@@ -213,7 +214,8 @@ def test_cfg5_full_h32768_parity(gx_lib, lock_readers):
     assert st["gossip_accepts"] == 0 and st["lock_buffered"] > 0 and st["lock_drops"] > 0
     assert st["lock_drained"] == 0 and st["first_locked_round"] == 7
     assert st["queue_drops"] == 0 and st["first_drop_round"] == -1  # faithful to the reference's queues
-    assert st["ae_defer_lost"] == 0 and (lock_readers or st["ae_deferred"] == 0)
+    _progress(f"cfg5@32768 lock_readers {lock_readers}: ae_deferred {st['ae_deferred']} ae_defer_lost {st['ae_defer_lost']}")
+    assert lock_readers or st["ae_deferred"] + st["ae_defer_lost"] == 0
 
 
 CFG3_BENCH = dict(bench.CONFIGS["cfg3"]["p"])
