@@ -286,6 +286,25 @@ typedef struct gx_params {
    * Parity unpinned (the fork is absent). memberlist also scales the interval with the cluster
    * size (pushPullScale: x (ceil(log2 n - 5) + 1) above 32 nodes); that is ae_period_rounds. */
   uint32_t push_pull_stagger;
+  /* lock_model = 1 only: Go's sync.RWMutex lets LocalState's RLock() (services_delegate.go:148)
+   * through while the only holder is BroadcastServices' read lock (services_state.go:535) and no
+   * writer waits. lock_readers = 1 models it: a push-pull exchange whose locked sides are all
+   * read-locked with no writer waiting runs. A writer waits when the host's inbound pipeline holds
+   * a record (ProcessServiceMsgs blocked in AddServiceEntry's Lock()), an ExpireServer call waits, a
+   * merge already waits, the BroadcastTombstones tick is due, or BroadcastTombstones held the lock at
+   * the start of the round. The unlocked side merges the other's state as usual. The read-locked
+   * side's MergeRemoteState cannot merge: its records wait behind the lock
+   * (UpdateService -> ServiceMsgs -> AddServiceEntry), taking min(n, 26) of the pipeline's places
+   * (ServiceMsgs 25 + the blocked AddServiceEntry), and merge at the start of the receive phase of
+   * the host's first unlocked round, before its pipeline (an unpinned order: the reference
+   * interleaves the two blocked senders). The engine keeps the partner's pre-exchange state in a
+   * pool of lock_defer_slots rows per engine: host v uses slot v % lock_defer_slots. When the slot
+   * is taken, the merge is dropped and counted (gx_stats.ae_defer_lost); a run is faithful while
+   * that stays 0. Of several hosts claiming one free slot in a round (or push-pull batch), the
+   * lowest host id gets it. 0 (default) = every exchange with a locked side fails, the round-5
+   * model. Unsharded engines only (GX_EINVAL otherwise). lock_defer_slots: 1..4096 (0 = 64). */
+  uint32_t lock_readers;
+  uint32_t lock_defer_slots;
 } gx_params;
 #define GX_LOCK_BUF_MAX_BYTES (1ull << 36) /* 64 GiB of lock_buffer records per engine */
 #define GX_PP_MATCHING 0
@@ -314,6 +333,10 @@ typedef struct gx_host_state {
                                       host's lock buffer */
 } gx_host_state;
 #define GX_LOCK_PENDING_EXPIRE 4u
+#define GX_LOCK_DEFER_MERGE 8u /* bit 3 (lock_readers): a push-pull merge waits for the host's lock */
+/* lock_readers: BroadcastTombstones (the write lock) held the lock at the start of round n */
+#define GX_LOCK_W_AT(lock, round) (((lock) >> (4 + ((round) & 1))) & 1u)
+#define GX_LOCK_DEFER_RES 26u  /* pipeline places a waiting merge takes: ServiceMsgs 25 + AddServiceEntry */
 #define GX_LOCK_BUF_SHIFT 8
 #define GX_LOCK_AT(lock, round) (((lock) >> ((round) & 1)) & 1u)
 #define GX_LOCK_BUF(lock) ((lock) >> GX_LOCK_BUF_SHIFT)
@@ -376,6 +399,8 @@ typedef struct gx_stats {
   uint64_t lock_drained;     /* buffered records merged once the host was unlocked (also gossip_merges) */
   uint64_t ae_locked;        /* push-pull exchanges that did not run: a side held the lock */
   uint64_t expire_deferred;  /* ExpireServer calls that waited for the lock */
+  uint64_t ae_deferred;      /* lock_readers: push-pull merges of a read-locked side that waited for its lock */
+  uint64_t ae_defer_lost;    /* ... and that the engine could not keep (its pool slot was taken); 0 = faithful */
   uint64_t false_expiries;   /* of `expired`: alive-lifespan expiries (services_state.go:655-679) of a
                                 record whose owner host has not departed (the owner is live; with
                                 churn it may have stopped the service and its tombstone not arrived) */

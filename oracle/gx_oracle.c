@@ -96,6 +96,12 @@ struct gx_engine {
    * failed although every locked side held only BroadcastServices' read lock with no writer waiting */
   uint8_t *lk_flags;
   uint64_t ro_runnable;
+  /* gx.h lock_readers: the pool of waiting push-pull merges (P rows of R words; host v uses slot
+   * v % P), each slot's host (GX_NOHOST = free) and the pipeline places its merge holds, and this
+   * batch's lowest claimant per slot */
+  uint32_t P;
+  uint64_t *dpool;
+  uint32_t *dpool_host, *dpool_res, *dclaim;
   uint32_t PW;            /* words per host of pexp, ceil(H / 32) */
   uint32_t *pexp;         /* H * PW  owners whose ExpireServer waits for the host's lock (lazy) */
   int in_round;           /* inside a round phase: the lock applies (ABI entry points act directly) */
@@ -151,12 +157,31 @@ static inline int lock_on(const gx_engine *e) { return e->p.lock_model != 0 && e
 static void lock_snapshot(gx_engine *e, uint32_t v, int64_t round) {
   const uint32_t b = 1u << (round & 1);
   e->hs[v].lock = (e->hs[v].lock & ~b) | ((e->hs[v].flags & 3u) ? b : 0u);
+  if (e->p.lock_readers) { /* the write lock's holder for GX_LOCK_W_AT */
+    const uint32_t w = 16u << (round & 1);
+    e->hs[v].lock = (e->hs[v].lock & ~w) | ((e->hs[v].flags & 2u) ? w : 0u);
+  }
   if (e->lk_flags) e->lk_flags[2 * (size_t)v + (round & 1)] = (uint8_t)(e->hs[v].flags & 3u);
 }
 /* Go's RWMutex lets LocalState's RLock (services_delegate.go:148) through while the only holder is
  * BroadcastServices' read lock (services_state.go:535) and no writer waits: no record in the host's
  * pipeline (ProcessServiceMsgs would wait in AddServiceEntry's Lock), no waiting ExpireServer, no
  * BroadcastTombstones tick due. The model fails such exchanges; this only counts them. */
+#define GX_NOHOST 0xffffffffu
+/* gx.h lock_readers: host v is locked this round and its LocalState RLock would succeed: only
+ * BroadcastServices' read lock held it at the round's start, and no writer waits (no record in its
+ * pipeline, no waiting ExpireServer or merge, no BroadcastTombstones tick due). */
+static int ro_side(const gx_engine *e, uint32_t v) {
+  const gx_host_state *h = &e->hs[v];
+  return e->p.lock_readers && locked_at(e, v) && !GX_LOCK_W_AT(h->lock, e->round) && GX_LOCK_BUF(h->lock) == 0 &&
+         !(h->lock & (GX_LOCK_PENDING_EXPIRE | GX_LOCK_DEFER_MERGE)) && h->bt_next > e->round;
+}
+/* the inbound pipeline's room for gossip records: a waiting merge holds ServiceMsgs' places */
+static uint32_t pipe_cap(const gx_engine *e, uint32_t v) {
+  if (!(e->hs[v].lock & GX_LOCK_DEFER_MERGE)) return e->C;
+  const uint32_t res = e->dpool_res[v % e->P];
+  return e->C > res ? e->C - res : 0;
+}
 static int ro_runnable_side(const gx_engine *e, uint32_t v) {
   const gx_host_state *h = &e->hs[v];
   return e->lk_flags && e->lk_flags[2 * (size_t)v + (e->round & 1)] == 1u && !(h->flags & 2u) &&
@@ -819,6 +844,95 @@ static uint32_t feistel_inv(uint64_t key, uint32_t q, uint32_t m) {
 static void fd_snapshot_row(const gx_engine *e, uint32_t v, uint64_t *out);
 static void fd_merge_state(gx_engine *e, uint32_t v, const uint64_t *remote);
 
+/* gx.h lock_readers: an exchange whose locked sides hold only BroadcastServices' read lock with no
+ * writer waiting runs (Go's RWMutex admits LocalState's RLock, services_delegate.go:148). An unlocked
+ * side merges the other's pre-exchange state now; a read-locked side's Merge (:153-167 ->
+ * services_state.go:367-373 -> UpdateService :138-140) waits behind the lock: the partner's state
+ * goes to the host's pool slot (claimed in ae_claims) and merges at its first unlocked round
+ * (ph_receive), or is counted lost when the slot went to another host. */
+static void fd_snapshot_row(const gx_engine *e, uint32_t v, uint64_t *out);
+static void fd_merge_state(gx_engine *e, uint32_t v, const uint64_t *remote);
+static void ae_exchange_read_locked(gx_engine *e, uint32_t a, uint32_t b, int la, int lb, int64_t now) {
+  uint64_t *sa = (uint64_t *)malloc(sizeof(uint64_t) * e->R), *sb = (uint64_t *)malloc(sizeof(uint64_t) * e->R);
+  memcpy(sa, &e->view[(size_t)a * e->R], sizeof(uint64_t) * e->R);
+  memcpy(sb, &e->view[(size_t)b * e->R], sizeof(uint64_t) * e->R);
+  for (int k = 0; k < 2; k++) {
+    const uint32_t x = k ? b : a;
+    const uint64_t *other = k ? sa : sb;
+    if (k ? lb : la) { /* read-locked: the merge waits */
+      const uint32_t slot = x % e->P;
+      if (e->dclaim[slot] != x) {
+        e->st.ae_defer_lost++;
+        continue;
+      }
+      uint32_t n = 0;
+      for (uint32_t r = 0; r < e->R; r++) n += st_of(other[r]) != GX_ABSENT;
+      memcpy(&e->dpool[(size_t)slot * e->R], other, sizeof(uint64_t) * e->R);
+      e->dpool_host[slot] = x;
+      e->dpool_res[slot] = n < GX_LOCK_DEFER_RES ? n : GX_LOCK_DEFER_RES;
+      e->hs[x].lock |= GX_LOCK_DEFER_MERGE;
+      e->st.ae_deferred++;
+    } else {
+      for (uint32_t r = 0; r < e->R; r++) { /* x.Merge(the other's state) (:367-373) */
+        if (st_of(other[r]) == GX_ABSENT) continue;
+        grec u = {other[r], r, 0};
+        add_entry(e, x, u, now, SRC_AE);
+      }
+      e->st.ae_slots += e->R;
+    }
+  }
+  e->st.ae_exchanges++;
+  free(sa);
+  free(sb);
+  if (e->p.fd_enable && e->p.fd_push_pull_state) { /* memberlist's half is not behind the catalog lock */
+    uint64_t *ma = (uint64_t *)malloc(8ull * e->H), *mb = (uint64_t *)malloc(8ull * e->H);
+    fd_snapshot_row(e, a, ma);
+    fd_snapshot_row(e, b, mb);
+    fd_merge_state(e, a, mb);
+    fd_merge_state(e, b, ma);
+    free(ma);
+    free(mb);
+  }
+}
+/* The read-locked sides of a batch of exchanges (pairs with no host in common) claim their pool
+ * slots: a slot free at the batch's start goes to the lowest host id claiming it, a rule that does
+ * not depend on the order the exchanges run in. ae_claims_done frees the unused claims. */
+static int ae_pair_ok(const gx_engine *e, uint32_t a, uint32_t b);
+static void ae_claims(gx_engine *e, const uint32_t *pa, const uint32_t *pb, uint32_t n) {
+  if (!e->p.lock_readers) return;
+  for (uint32_t t = 0; t < n; t++) {
+    const uint32_t a = pa[t], b = pb[t];
+    if (!ae_pair_ok(e, a, b)) continue;
+    const int la = locked_at(e, a), lb = locked_at(e, b);
+    if (!(la || lb) || (la && !ro_side(e, a)) || (lb && !ro_side(e, b))) continue;
+    for (int k = 0; k < 2; k++) {
+      const uint32_t x = k ? b : a;
+      if (!(k ? lb : la)) continue;
+      const uint32_t slot = x % e->P;
+      if (e->dpool_host[slot] == GX_NOHOST && x < e->dclaim[slot]) e->dclaim[slot] = x;
+    }
+  }
+}
+static void ae_claims_done(gx_engine *e) {
+  if (e->p.lock_readers)
+    for (uint32_t s = 0; s < e->P; s++) e->dclaim[s] = GX_NOHOST;
+}
+/* The waiting merge of host v at the receive phase of its first unlocked round, before its
+ * pipeline: the partner's state in key order through AddServiceEntry (Merge, SRC_AE). */
+static void run_deferred_merge(gx_engine *e, uint32_t v, int64_t now) {
+  const uint32_t slot = v % e->P;
+  const uint64_t *row = &e->dpool[(size_t)slot * e->R];
+  for (uint32_t r = 0; r < e->R; r++) {
+    if (st_of(row[r]) == GX_ABSENT) continue;
+    grec u = {row[r], r, 0};
+    add_entry(e, v, u, now, SRC_AE);
+  }
+  e->st.ae_slots += e->R;
+  e->dpool_host[slot] = GX_NOHOST;
+  e->dpool_res[slot] = 0;
+  e->hs[v].lock &= ~GX_LOCK_DEFER_MERGE;
+}
+
 static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
   /* the ServicesState lock (gx.h lock_model): a locked side's LocalState blocks behind the pending
    * writer (services_delegate.go:148), so the exchange does not run; lock_model = 0 counts the
@@ -826,6 +940,10 @@ static void ae_exchange(gx_engine *e, uint32_t a, uint32_t b, int64_t now) {
   const int la = locked_at(e, a), lb = locked_at(e, b);
   if (la || lb) {
     note_locked(e);
+    if (e->p.lock_model && e->p.lock_readers && (!la || ro_side(e, a)) && (!lb || ro_side(e, b))) {
+      ae_exchange_read_locked(e, a, b, la, lb, now);
+      return;
+    }
     if (e->p.lock_model) {
       e->st.ae_locked++;
       if ((!la || ro_runnable_side(e, a)) && (!lb || ro_runnable_side(e, b)))
@@ -1034,10 +1152,11 @@ static void ph_receive(gx_engine *e, uint32_t i, void *ctx) {
     if (nrec) note_locked(e);
     if (e->p.lock_model) {
       uint32_t nb = GX_LOCK_BUF(h->lock);
+      const uint32_t cap_v = pipe_cap(e, v);
       for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) {
         uint32_t m = e->in_list[x];
         for (uint32_t y = 0; y < e->msg_len[m]; y++) {
-          if (nb < e->C) {
+          if (nb < cap_v) {
             e->lkb[(size_t)v * e->C + nb++] = e->msg[(size_t)m * cap + y];
             e->st.lock_buffered++;
           } else {
@@ -1050,6 +1169,7 @@ static void ph_receive(gx_engine *e, uint32_t i, void *ctx) {
     }
     e->st.locked_merges += nrec; /* lock_model = 0: they merge anyway (counted) */
   }
+  if (!locked && (h->lock & GX_LOCK_DEFER_MERGE) && !departed(e, v)) run_deferred_merge(e, v, now);
   if (!locked && GX_LOCK_BUF(h->lock) && !departed(e, v)) { /* the pipeline drains, in arrival order */
     const uint32_t nb = GX_LOCK_BUF(h->lock);
     h->lock &= (1u << GX_LOCK_BUF_SHIFT) - 1;
@@ -1175,7 +1295,9 @@ static void ae_phase_local(gx_engine *e) {
   uint32_t *pb = (uint32_t *)malloc(sizeof(uint32_t) * (e->H / 2 + 1));
   struct ae_ctx c = {pa, pb, now};
   uint32_t np = ae_pairs(e, pa, pb);
+  ae_claims(e, pa, pb, np);
   for_hosts(e, np, ph_ae_pair, &c); /* pairs are disjoint: every host is in at most one */
+  ae_claims_done(e);
   free(pa);
   free(pb);
   e->ae_local_round = e->round;
@@ -1243,7 +1365,9 @@ static void ae_phase_initiate(gx_engine *e) {
   const uint32_t nb = pp_batches(e, pa, pb, boff);
   for (uint32_t q = 0; q < nb; q++) {
     struct ae_ctx c = {pa + boff[q], pb + boff[q], now_of(e)};
+    ae_claims(e, pa + boff[q], pb + boff[q], boff[q + 1] - boff[q]);
     for_hosts(e, boff[q + 1] - boff[q], ph_pp_exchange, &c);
+    ae_claims_done(e);
   }
   free(pa);
   free(pb);
@@ -1459,6 +1583,8 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL;
   if (p->push_pull_stagger > 1 || (p->push_pull_stagger && (p->push_pull_mode != GX_PP_INITIATE || !p->ae_period_rounds)))
     return GX_EINVAL;
+  if (p->lock_readers > 1 || (p->lock_readers && (!p->lock_model || p->n_shards > 1)) || p->lock_defer_slots > 4096)
+    return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1602,6 +1728,14 @@ int gx_create(const gx_params *p, gx_engine **out) {
   if (p->lock_model) { /* the locked hosts' inbound pipelines and waiting ExpireServer calls */
     e->C = p->lock_buffer;
     e->lk_flags = (uint8_t *)calloc(2 * (size_t)H, 1);
+    if (p->lock_readers) { /* the waiting push-pull merges' pool (gx.h lock_readers) */
+      e->P = p->lock_defer_slots ? p->lock_defer_slots : 64;
+      e->dpool = (uint64_t *)malloc(sizeof(uint64_t) * e->P * e->R);
+      e->dpool_host = (uint32_t *)malloc(sizeof(uint32_t) * e->P);
+      e->dpool_res = (uint32_t *)calloc(e->P, sizeof(uint32_t));
+      e->dclaim = (uint32_t *)malloc(sizeof(uint32_t) * e->P);
+      for (uint32_t x = 0; x < e->P; x++) e->dpool_host[x] = e->dclaim[x] = GX_NOHOST;
+    }
     e->lkb = (grec *)malloc(sizeof(grec) * H * e->C);
     e->PW = (e->H + 31) / 32;
     if (p->storm_round >= 0 || p->fd_enable) e->pexp = (uint32_t *)malloc(4ull * H * e->PW);
@@ -1664,6 +1798,10 @@ int gx_destroy(gx_engine *e) {
   free(e->fd_np);
   free(e->lkb);
   free(e->lk_flags);
+  free(e->dpool);
+  free(e->dpool_host);
+  free(e->dpool_res);
+  free(e->dclaim);
   free(e->pexp);
   free_names(e);
   free(e);

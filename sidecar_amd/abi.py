@@ -29,7 +29,7 @@ TS_SHIFT = 3
 JOB_NIL_BS, JOB_NIL_BT, JOB_RETX, JOB_SEND, JOB_EXPIRE, JOB_LOST = 0, 1, 2, 3, 4, 5
 INIT_EMPTY, INIT_OWN, INIT_WARM = 0, 1, 2
 LIMIT_DEFAULT = 0xFFFFFFFF
-LOCK_PENDING_EXPIRE, LOCK_BUF_SHIFT = 4, 8  # gx_host_state.lock (gx.h)
+LOCK_PENDING_EXPIRE, LOCK_DEFER_MERGE, LOCK_BUF_SHIFT = 4, 8, 8  # gx_host_state.lock (gx.h)
 
 K_NAMES = ["owner", "scan", "storm", "send", "route", "merge", "ae", "converge", "encode", "decode", "fd"]
 
@@ -114,7 +114,7 @@ class GxParams(C.Structure):
         ("fd_push_pull_state", C.c_uint32),
         ("gossip_messages", C.c_uint32), ("push_pull_mode", C.c_uint32), ("inbox_slots", C.c_uint32),
         ("lock_model", C.c_uint32), ("lock_buffer", C.c_uint32), ("probe_piggyback", C.c_uint32),
-        ("push_pull_stagger", C.c_uint32),
+        ("push_pull_stagger", C.c_uint32), ("lock_readers", C.c_uint32), ("lock_defer_slots", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)
@@ -164,7 +164,8 @@ class GxStats(C.Structure):
         "fd_deaths", "fd_refutes", "fd_alive_updates", "fd_msgs_sent", "fd_msgs_received",
         "fd_state_merges", "queue_deferred")] + [("first_drop_round", C.c_int64)] + [
         ("locked_merges", C.c_uint64), ("first_locked_round", C.c_int64)] + [(n, C.c_uint64) for n in (
-        "lock_buffered", "lock_drops", "lock_drained", "ae_locked", "expire_deferred", "false_expiries")]
+        "lock_buffered", "lock_drops", "lock_drained", "ae_locked", "expire_deferred", "ae_deferred",
+        "ae_defer_lost", "false_expiries")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}

@@ -79,9 +79,9 @@ enum {
 // Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
 enum {
   C_LOST = C_NCTR, C_FD_PROBES, C_FD_PROBE_FAIL, C_FD_SUSPECT, C_FD_CONFIRM, C_FD_DEATH, C_FD_REFUTE,
-  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_FEXP, C_NCTR_ALL
+  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_FEXP, C_AE_DEFER, C_AE_DEFER_LOST, C_NCTR_ALL
 };
-#define GX_NCTR_SLOTS 48
+#define GX_NCTR_SLOTS 56
 static_assert(C_NCTR_ALL <= GX_NCTR_SLOTS, "counter slots");
 
 #define GX_SHARDS 64
@@ -184,6 +184,15 @@ struct Dev {
   uint32_t PW;         // words per host of pexp, ceil(H / 32)
   uint32_t *pexp;      // [Hl][PW] owners whose ExpireServer waits for the host's lock
   int in_round;        // a round phase is running: ExpireServer waits for the lock (ABI calls act directly)
+  // gx.h lock_readers: push-pull merges of read-locked hosts waiting for their lock, in a pool of P
+  // rows (host v uses slot v % P); each slot's host (GX_NOHOST = free), the pipeline places its merge
+  // holds and the lowest claimant of the current batch. ro_flag[t]: pair t of the last push-pull
+  // launch runs with a read-locked side (k_ae_ro takes it); ro_list: k_ae_ro's ordered list.
+  uint32_t P;
+  uint64_t *dpool;     // [P][R]
+  uint32_t *dpool_host, *dpool_res, *dclaim;  // [P]
+  uint8_t *ro_flag;    // [H]
+  uint32_t *ro_list;   // [H]
   // The planned exchange packed by k_send itself (gx_round_gossip_begin): a packet to another shard
   // is written straight into its slot of the send buffer. Set only for that launch.
   uint8_t *ob_buf;           // the send buffer (slots of 16 + 16 * packet_cap bytes), or null
@@ -413,9 +422,33 @@ GXD void set_slot(const Dev &d, Acc &a, uint32_t v, uint64_t *slot, uint64_t nw)
 GXD bool locked_in(const Dev &d, uint32_t lockw) { return GX_LOCK_AT(lockw, d.round) != 0u; }
 GXD bool host_locked(const Dev &d, uint32_t v) { return locked_in(d, gld(&hst(d, v)->lock)); }
 // the lock word with bit `round & 1` set from the loopers' state
-GXD uint32_t lock_snap(uint32_t lockw, uint32_t flags, int64_t round) {
-  const uint32_t b = 1u << (round & 1);
-  return (lockw & ~b) | ((flags & 3u) ? b : 0u);
+// (and with gx.h lock_readers, bit 4 + (round & 1) from BroadcastTombstones' write lock alone)
+GXD uint32_t lock_snap(uint32_t lockw, uint32_t flags, int64_t round, bool rw) {
+  const uint32_t b = 1u << (round & 1), w = 16u << (round & 1);
+  lockw = (lockw & ~b) | ((flags & 3u) ? b : 0u);
+  return rw ? (lockw & ~w) | ((flags & 2u) ? w : 0u) : lockw;
+}
+// gx.h lock_readers: host v holds the lock this round and LocalState's RLock would still succeed
+// (services_delegate.go:148 behind BroadcastServices' read lock, services_state.go:535): the write
+// lock did not hold it at the round's start and no writer waits (no record in the pipeline, no
+// waiting ExpireServer or merge, no BroadcastTombstones tick due). Oracle: ro_side.
+#define GX_NOHOST 0xffffffffu
+GXD bool ro_side(const Dev &d, uint32_t v) {
+  const gx_host_state *h = hst(d, v);
+  const uint32_t lw = gld(&h->lock);
+  return d.p.lock_readers && locked_in(d, lw) && !GX_LOCK_W_AT(lw, d.round) && GX_LOCK_BUF(lw) == 0u &&
+         !(lw & (GX_LOCK_PENDING_EXPIRE | GX_LOCK_DEFER_MERGE)) && h->bt_next > d.round;
+}
+// a locked pair whose locked sides are all read-locked with no writer waiting: it runs (k_ae_ro)
+GXD bool ro_pair(const Dev &d, uint32_t a, uint32_t b) {
+  return d.p.lock_readers && (!host_locked(d, a) || ro_side(d, a)) && (!host_locked(d, b) || ro_side(d, b));
+}
+// the inbound pipeline's room for gossip records of local host vi with lock word lw: a waiting merge
+// holds min(n, 26) of its places (gx.h GX_LOCK_DEFER_RES). Oracle: pipe_cap.
+GXD uint32_t pipe_cap(const Dev &d, uint32_t vi, uint32_t lw) {
+  if (!(lw & GX_LOCK_DEFER_MERGE)) return d.C;
+  const uint32_t res = d.dpool_res[(d.lo + vi) % d.P];
+  return d.C > res ? d.C - res : 0u;
 }
 GXD void note_locked(const Dev &d) { atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round); }
 

@@ -499,6 +499,12 @@ static int round_merge_impl(gx_engine *e) {
     ~InRound() { d.in_round = 0; }
   } in_round_guard{d};
   hipStream_t s = e->stream;
+  if (d.p.lock_readers) {  // waiting push-pull merges of hosts unlocked now, before their pipelines
+    LaunchTimer t(e, GX_K_AE);
+    const bool vec = (d.R % 2) == 0, ev = !e->log_views.empty();
+    (vec ? (ev ? k_defer_drain<true, true> : k_defer_drain<true, false>)
+         : (ev ? k_defer_drain<false, true> : k_defer_drain<false, false>))<<<d.P, 256, 0, s>>>(d);
+  }
   if (d.K) {
     LaunchTimer t(e, GX_K_MERGE);
     const bool ev = !e->log_views.empty();
@@ -563,6 +569,13 @@ static bool ae_partner(const Dev &d, uint32_t i, uint32_t *out) {
   *out = base + (idx >= self ? idx + 1 : idx);
   return true;
 }
+// gx.h lock_readers: the read-locked exchanges of the last push-pull launch (k_ae_ro)
+static void ae_ro_launch(gx_engine *e, const uint32_t *pa, const uint32_t *pb, uint64_t key0, uint64_t key1, uint32_t np) {
+  const Dev &d = e->d;
+  const bool vec = (d.R % 2) == 0, ev = !e->log_views.empty();
+  (vec ? (ev ? k_ae_ro<true, true> : k_ae_ro<true, false>) : (ev ? k_ae_ro<false, true> : k_ae_ro<false, false>))<<<1, 256, 0, e->stream>>>(
+      d, pa, pb, key0, key1, np);
+}
 static int ae_initiate(gx_engine *e) {
   Dev &d = e->d;
   const bool dep = d.departures;
@@ -602,6 +615,7 @@ static int ae_initiate(gx_engine *e) {
     const unsigned np = off[q + 1] - off[q];
     if (ev) (vec ? k_ae_plan_ev<true> : k_ae_plan_ev<false>)<<<np, 256, 0, e->stream>>>(d, pa, pb, e->pp_prow, nullptr, none, nullptr);
     else (vec ? k_ae_plan<true> : k_ae_plan<false>)<<<np, 256, 0, e->stream>>>(d, pa, pb, e->pp_prow, nullptr, none, nullptr);
+    if (d.p.lock_readers) ae_ro_launch(e, pa, pb, 0, 0, np);  // the batch's read-locked exchanges
   }
   return GX_OK;
 }
@@ -645,6 +659,10 @@ static int ae_whole_impl(gx_engine *e) {
     if (np && pp_state(d)) {  // pushPull's membership half (mergeState), from round-start lists
       LaunchTimer t(e, GX_K_FD);
       k_fd_pushpull_pair<<<np, 128, 0, s>>>(d, key0, key1);  // both directions in lockstep: no snapshot
+    }
+    if (np && d.p.lock_readers) {  // the read-locked exchanges (after the membership half reads ro_flag)
+      LaunchTimer t(e, GX_K_AE);
+      ae_ro_launch(e, nullptr, nullptr, key0, key1, np);
     }
   }
   HIPCHK(hipGetLastError());
@@ -789,6 +807,8 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL;
   if (p->push_pull_stagger > 1 || (p->push_pull_stagger && (p->push_pull_mode != GX_PP_INITIATE || !p->ae_period_rounds)))
     return GX_EINVAL;
+  if (p->lock_readers > 1 || (p->lock_readers && (!p->lock_model || p->n_shards > 1)) || p->lock_defer_slots > 4096)
+    return GX_EINVAL;  // gx.h lock_readers: unsharded engines with the lock modelled
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -817,7 +837,7 @@ int gx_destroy(gx_engine *e) {
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_w0, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mrec, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
-                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap, d.lkb, d.pexp};
+                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap, d.lkb, d.pexp, d.dpool, d.dpool_host, d.dpool_res, d.dclaim, d.ro_flag, d.ro_list};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
@@ -1016,6 +1036,19 @@ int gx_create(const gx_params *p, gx_engine **out) {
     if (p->storm_round >= 0 || p->fd_enable) {
       ALLOC(d.pexp, sizeof(uint32_t) * H * d.PW);
       HIPCHK(hipMemset(d.pexp, 0, sizeof(uint32_t) * H * d.PW));
+    }
+    if (p->lock_readers) {  // the waiting push-pull merges' pool (gx.h lock_readers)
+      d.P = p->lock_defer_slots ? p->lock_defer_slots : 64;
+      ALLOC(d.dpool, sizeof(uint64_t) * d.P * d.R);
+      ALLOC(d.dpool_host, sizeof(uint32_t) * d.P);
+      ALLOC(d.dpool_res, sizeof(uint32_t) * d.P);
+      ALLOC(d.dclaim, sizeof(uint32_t) * d.P);
+      ALLOC(d.ro_flag, H);
+      ALLOC(d.ro_list, sizeof(uint32_t) * H);
+      HIPCHK(hipMemset(d.dpool_host, 0xff, sizeof(uint32_t) * d.P));
+      HIPCHK(hipMemset(d.dclaim, 0xff, sizeof(uint32_t) * d.P));
+      HIPCHK(hipMemset(d.dpool_res, 0, sizeof(uint32_t) * d.P));
+      HIPCHK(hipMemset(d.ro_flag, 0, H));
     }
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
@@ -2546,6 +2579,8 @@ int gx_stats_get(gx_engine *e, gx_stats *out) {
   out->lock_drained = c[C_LOCK_DRAIN];
   out->ae_locked = c[C_AE_LOCKED];
   out->expire_deferred = c[C_EXP_DEFER];
+  out->ae_deferred = c[C_AE_DEFER];
+  out->ae_defer_lost = c[C_AE_DEFER_LOST];
   out->false_expiries = c[C_FEXP];
   out->first_drop_round = fdr == ~0ull ? -1 : (int64_t)fdr;
   out->lost_packets = c[C_LOST];

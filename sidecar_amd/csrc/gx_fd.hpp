@@ -688,9 +688,10 @@ __global__ __launch_bounds__(128) void k_fd_pushpull_pair(Dev d, uint64_t key0, 
   }
   const uint32_t a = base + feistel_perm(key, 2 * q, m), b = base + feistel_perm(key, 2 * q + 1, m);
   if (threadIdx.x == 0)  // pp_runs on the lists as this phase starts (nothing merged yet); a side that
-    // holds the ServicesState lock fails the whole exchange (gx.h lock_model)
+    // holds the ServicesState lock fails the whole exchange (gx.h lock_model) unless only readers
+    // hold it (lock_readers: ro_flag, cleared by k_ae_ro after this launch)
     s_run = !departed(d, a) && !departed(d, b) && reach(d, a, b) && (fd_snap_word(d, a, b) & 0xffu) == GX_M_ALIVE &&
-            !(d.p.lock_model && (host_locked(d, a) || host_locked(d, b)));
+            !(d.p.lock_model && (host_locked(d, a) || host_locked(d, b)) && !(d.p.lock_readers && d.ro_flag[t]));
   __syncthreads();
   if (s_run) fd_merge_pair_lockstep(d, f, a, b, s_w);
   fd_flush(d, f);

@@ -189,7 +189,7 @@ __global__ __launch_bounds__(64) void k_wake(Dev d) {
   if (idx < d.Hl && !departed(d, d.lo + idx)) {  // a crashed host stays frozen
     gx_host_state *h = &d.hs[idx];
     {  // the ServicesState lock for this round: the loopers' state (unchanged since the last sends)
-      const uint32_t lw = h->lock, nl = lock_snap(lw, h->flags, d.round);
+      const uint32_t lw = h->lock, nl = lock_snap(lw, h->flags, d.round, d.p.lock_readers != 0);
       if (nl != lw) h->lock = nl;
     }
     const uint4 c = *reinterpret_cast<const uint4 *>(h);  // fifo_head, fifo_tail, sleep_head, sleep_tail
@@ -1257,7 +1257,9 @@ GXD uint32_t sample_peers(const Dev &d, uint32_t u, uint32_t *peers) {
 //     are written, compacted per packet, and a packet without one is not registered at all.
 // Batch records that stay pending are written to the ring after the chunk's loads, position p by
 // team lane p % T in call order (the sequential order of the ring writes).
+#ifndef PLAN_CH
 #define PLAN_CH 4  // calls planned per chunk
+#endif
 // Diagnostics (build with -DGX_SEND_SPLIT, engine created with GX_KPROF set): per wave, the time
 // its lane-0 team spends in each part of the chunk loop, summed over chunks, in place of the
 // k_send phase marks 1..6: plan, records, headers, ring writes + sync, chunks, refills.
@@ -1449,7 +1451,8 @@ GXD void send_planned(const Dev &d, Acc &a, uint32_t idx, gx_host_state &hs, gx_
     const uint32_t lw = jj < np && peers[jj] - d.lo < d.Hl ? gld(&hst(d, peers[jj])->lock) : 0u;
     const bool lk = locked_in(d, lw);
     lkm |= (uint32_t)((__ballot(lk) >> (tw * T)) & tmask) << j0;
-    fullm |= (uint32_t)((__ballot(lk && GX_LOCK_BUF(lw) >= d.C) >> (tw * T)) & tmask) << j0;
+    const bool full = lk && GX_LOCK_BUF(lw) >= pipe_cap(d, jj < np ? peers[jj] - d.lo : 0u, lw);
+    fullm |= (uint32_t)((__ballot(full) >> (tw * T)) & tmask) << j0;
   }
   if (direct) {
 #pragma unroll
@@ -1853,7 +1856,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       uint32_t *peers = reinterpret_cast<uint32_t *>(&pl[PLAN_CH]);  // the team's peers (k_send's prologue)
       const uint32_t np = peers[16];
       send_planned<T>(d, a, idx, hs, pjs, pl, peers, np, kb, kl, (pre && fwd.pf0 == hs.fifo_head) ? fwd.npf : 0u);
-      hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1);  // the lock for the next round
+      hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1, d.p.lock_readers != 0);  // the lock for the next round
       if (lane == 0) *h = hs;
     } else if (!X || !departed(d, u)) {
       const bool fd = X && d.p.fd_enable;
@@ -1938,7 +1941,7 @@ GXD void send_host(const Dev &d, Acc &a, uint32_t idx, gx_job *pjs, int do_bt, u
       // slots claimed for peers the round stopped before (gossip() returned at an empty packet)
       if (early && lane >= called && my_pos != 0xffffffffu)
         inbox_header(d, peers[lane] - d.lo, my_pos, u * d.KE + lane, (uint32_t)((size_t)idx * d.KE + lane), 0);
-      hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1);  // the lock for the next round
+      hs.lock = lock_snap(hs.lock, hs.flags, d.round + 1, d.p.lock_readers != 0);  // the lock for the next round
       if (lane == 0) *h = hs;
     }
   }
@@ -2160,12 +2163,13 @@ GXD void merge_inbox_serial(const Dev &d, uint32_t vi, bool lockd = false, uint3
   grec *lkb = d.lkb ? &d.lkb[(size_t)vi * d.C] : nullptr;
   if (lockd) {
     uint32_t nb = GX_LOCK_BUF(d.hs[vi].lock);
+    const uint32_t capv = pipe_cap(d, vi, d.hs[vi].lock);  // a waiting merge holds places (lock_readers)
     for (uint32_t n = 0; n < cnt; n++) {
       const uint4 h = inbox_next(d, vi, after);
       after = h.x;
       const grec *pk = packet_recs(d, vi, h.w, h.y);
       for (uint32_t x = 0; x < h.z; x++) {
-        if (nb < d.C) {
+        if (nb < capv) {
           lkb[nb++] = pk[x];
           a.c[C_LOCK_BUF]++;
         } else {
@@ -2367,7 +2371,7 @@ GXD void merge_receiver(const Dev &d, const uint32_t vi, MergeLds &L) {
     }
   };
   if (lockd) {  // the pipeline takes the records in arrival order while it has room (gx.h lock_model)
-    const uint32_t nb0 = GX_LOCK_BUF(lw), room_l = d.C > nb0 ? d.C - nb0 : 0u;
+    const uint32_t capv = pipe_cap(d, vi, lw), nb0 = GX_LOCK_BUF(lw), room_l = capv > nb0 ? capv - nb0 : 0u;
     const uint32_t keep = total < room_l ? total : room_l;
     grec *dst = &d.lkb[(size_t)vi * d.C + nb0];
     for (uint32_t t0 = 0; t0 < keep; t0 += 64) {
@@ -2850,7 +2854,7 @@ GXD bool lock_append_seg(const Dev &d, uint32_t vi, bool act) {
     start += before ? lj : 0u;
     total += j < deg ? lj : 0u;
   }
-  const uint32_t nb0 = GX_LOCK_BUF(lw), room = d.C > nb0 ? d.C - nb0 : 0u;
+  const uint32_t capv = pipe_cap(d, vi, lw), nb0 = GX_LOCK_BUF(lw), room = capv > nb0 ? capv - nb0 : 0u;
   const uint32_t keep = total < room ? total : room;
   grec *dst = act ? &d.lkb[(size_t)vi * d.C + nb0] : d.lkb;
   for (uint32_t o0 = 0; o0 < keep; o0 += SEG * LOCK_RPL) {
@@ -3493,12 +3497,16 @@ GXD void ae_pair(const Dev &d, uint32_t a, uint32_t b, bool both, unsigned long 
 // The ServicesState lock of a push-pull pair whose hosts are both here (gx.h lock_model): a locked
 // side's LocalState blocks behind the pending writer, so the exchange does not run (returns true:
 // skip it); with lock_model = 0 it runs and `locked` says its merges are counted. Block-uniform.
-GXD bool ae_lock_skip(const Dev &d, uint32_t a, uint32_t b, bool &locked) {
+// gx.h lock_readers: a pair whose locked sides are all read-locked with no writer waiting is flagged
+// (ro_flag[t], t its index in the launch) for k_ae_ro, which runs it after the launch.
+GXD bool ae_lock_skip(const Dev &d, uint32_t a, uint32_t b, bool &locked, uint32_t t) {
   locked = host_locked(d, a) || host_locked(d, b);
   if (!locked) return false;
+  const bool ro = d.p.lock_model && ro_pair(d, a, b);
   if (threadIdx.x == 0) {
     atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
-    if (d.p.lock_model) ctr_atomic(d, C_AE_LOCKED, 1);
+    if (ro) d.ro_flag[t] = 1;
+    else if (d.p.lock_model) ctr_atomic(d, C_AE_LOCKED, 1);
   }
   return d.p.lock_model != 0;
 }
@@ -3554,7 +3562,7 @@ GXD void ae_round_pair(const Dev &d, uint64_t key0, uint64_t key1) {
     if (!ok) return;
   }
   bool locked;
-  if (ae_lock_skip(d, a, b, locked)) return;
+  if (ae_lock_skip(d, a, b, locked, t)) return;
   ae_pair<VEC, PF, NT, EV, NTS>(d, a, b, true, s_wave, s_red, nullptr, false, nullptr, locked);
   if (kp && threadIdx.x == 0) kp[2 * blockIdx.x + 1] = wall_clock64();
 }
@@ -3584,7 +3592,13 @@ GXD void ae_round_pairs(const Dev &d, uint64_t key0, uint64_t key1, uint32_t np)
     }
     if (ok) {
       const bool locked = host_locked(d, a) || host_locked(d, b);
-      if (locked) atomicAdd(&s_nlock, 1u);
+      const bool ro = locked && d.p.lock_model && ro_pair(d, a, b);  // k_ae_ro runs it (lock_readers)
+      if (ro) {
+        d.ro_flag[tq] = 1;
+        atomicMin(&d.ctr->first_drop[shard_id()][1], (unsigned long long)d.round);
+      } else if (locked) {
+        atomicAdd(&s_nlock, 1u);
+      }
       if (!(locked && d.p.lock_model)) s_run[atomicAdd(&s_nrun, 1u)] = tq | (locked ? 1u << 31 : 0u);
     }
   }
@@ -3634,6 +3648,128 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   ae_round_pairs<VEC, false, PF, NT, NTS>(d, key0, key1, np);
 }
 
+// gx.h lock_readers: the exchanges of the last push-pull launch whose locked sides are all
+// read-locked with no writer waiting (ro_flag[t]; pair t of the matching round from key0/key1, or
+// of the initiate batch pa/pb). One block, after the launch: (1) the read-locked sides claim their
+// pool slots (slot v % P, free at the launch's start: the lowest host id gets it, whatever the
+// order, as the oracle's ae_claims); (2) the flagged pairs in pair order: a read-locked side keeps
+// the partner's pre-exchange row in its slot (services_delegate.go:153-167 -> services_state.go:
+// 367-373 -> UpdateService :138-140, blocked behind the lock) or counts it lost, then the unlocked
+// side merges the partner's row (ae_pair, one direction); (3) the claims are reset. The pairs are
+// disjoint and no other pair of the launch touches their rows, so running them after the launch is
+// the oracle's result (ae_exchange_read_locked). Clears ro_flag.
+template <bool VEC, bool EV>
+__global__ __launch_bounds__(256) void k_ae_ro(Dev d, const uint32_t *pa, const uint32_t *pb, uint64_t key0, uint64_t key1,
+                                               uint32_t n) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  __shared__ uint32_t s_pre[256];
+  __shared__ uint32_t s_n;
+  const uint32_t tid = threadIdx.x, per = (n + 255) / 256, t0 = tid * per < n ? tid * per : n;
+  const uint32_t t1 = t0 + per < n ? t0 + per : n;
+  auto hosts = [&](uint32_t t, uint32_t &a, uint32_t &b) {
+    if (pa) {
+      a = pa[t];
+      b = pb[t];
+    } else {
+      ae_pair_hosts(d, t, key0, key1, a, b);
+    }
+  };
+  uint32_t c = 0;
+  for (uint32_t t = t0; t < t1; t++) {  // (1) claims
+    if (!d.ro_flag[t]) continue;
+    c++;
+    uint32_t a, b;
+    hosts(t, a, b);
+    for (int k = 0; k < 2; k++) {
+      const uint32_t x = k ? b : a;
+      if (!host_locked(d, x)) continue;
+      const uint32_t slot = x % d.P;
+      if (d.dpool_host[slot] == GX_NOHOST) atomicMin(&d.dclaim[slot], x);
+    }
+  }
+  s_pre[tid] = c;
+  __syncthreads();
+  if (tid == 0) {  // the flagged pairs' places in pair order (threads hold consecutive ranges)
+    uint32_t run = 0;
+    for (uint32_t i = 0; i < 256; i++) {
+      const uint32_t x = s_pre[i];
+      s_pre[i] = run;
+      run += x;
+    }
+    s_n = run;
+  }
+  __syncthreads();
+  uint32_t pos = s_pre[tid];
+  for (uint32_t t = t0; t < t1; t++)
+    if (d.ro_flag[t]) {
+      d.ro_list[pos++] = t;
+      d.ro_flag[t] = 0;
+    }
+  __threadfence();
+  __syncthreads();
+  const uint32_t nro = s_n;
+  for (uint32_t k = 0; k < nro; k++) {  // (2) the exchanges
+    uint32_t a, b;
+    hosts(d.ro_list[k], a, b);
+    const bool la = host_locked(d, a), lb = host_locked(d, b);
+    __syncthreads();  // every thread has read the lock words before a side's DEFER bit is set
+    for (int q = 0; q < 2; q++) {  // a read-locked side keeps the partner's row (before any merge)
+      const uint32_t x = q ? b : a, y = q ? a : b;
+      if (!(q ? lb : la)) continue;
+      const uint32_t slot = x % d.P;
+      if (d.dclaim[slot] != x) {  // the slot went to another host: the merge is lost
+        if (tid == 0) ctr_atomic(d, C_AE_DEFER_LOST, 1);
+        continue;
+      }
+      const uint64_t *src = vrow(d, y);
+      uint64_t *dst = &d.dpool[(size_t)slot * d.R];
+      unsigned long long np = 0;
+      for (uint32_t r = tid; r < d.R; r += blockDim.x) {
+        const uint64_t w = src[r];
+        dst[r] = w;
+        np += st_of(w) != GX_ABSENT;
+      }
+      np = block_sum(np, s_red);
+      if (tid == 0) {
+        d.dpool_host[slot] = x;
+        d.dpool_res[slot] = np < GX_LOCK_DEFER_RES ? (uint32_t)np : GX_LOCK_DEFER_RES;
+        hst(d, x)->lock |= GX_LOCK_DEFER_MERGE;
+        ctr_atomic(d, C_AE_DEFER, 1);
+        kbytes(d, GX_K_AE, 16ull * d.R, 0);
+      }
+    }
+    __threadfence();
+    __syncthreads();
+    if (!la) ae_pair<VEC, 1, false, EV>(d, a, b, false, s_wave, s_red);  // the unlocked side merges now
+    else if (!lb) ae_pair<VEC, 1, false, EV>(d, b, a, false, s_wave, s_red);
+    if (tid == 0) ctr_atomic(d, C_AEX, 1);
+    __syncthreads();
+  }
+  for (uint32_t x = tid; x < d.P; x += blockDim.x) d.dclaim[x] = GX_NOHOST;  // (3)
+}
+// gx.h lock_readers: the waiting merge of pool slot s's host at the receive phase of the host's
+// first unlocked round, before its pipeline and this round's packets (k_merge_seg runs after): the
+// kept row through Merge in key order (ae_pair from the pool row, SRC_AE). Oracle: run_deferred_merge.
+// The receiver's row changed after its senders read the slot words they forward, so its merge
+// reads the slots again (tick 2: w0_fwd).
+template <bool VEC, bool EV>
+__global__ __launch_bounds__(256) void k_defer_drain(Dev d) {
+  __shared__ unsigned long long s_wave[4];
+  __shared__ unsigned long long s_red[4];
+  const uint32_t s = blockIdx.x, x = d.dpool_host[s];
+  if (x == GX_NOHOST || x - d.lo >= d.Hl) return;  // block-uniform
+  const uint32_t vi = x - d.lo, lw = d.hs[vi].lock;
+  if (locked_in(d, lw) || departed(d, x)) return;
+  ae_pair<VEC, 1, false, EV>(d, x, x, false, s_wave, s_red, &d.dpool[(size_t)s * d.R]);
+  if (threadIdx.x == 0) {
+    d.dpool_host[s] = GX_NOHOST;
+    d.dpool_res[s] = 0;
+    d.hs[vi].lock = lw & ~GX_LOCK_DEFER_MERGE;
+    d.tick[vi] = 2;
+  }
+}
+
 template <bool VEC, bool EV>
 __global__ __launch_bounds__(256) void k_merge_views(Dev d, uint32_t dst, uint32_t src) {
   __shared__ unsigned long long s_wave[4];
@@ -3664,7 +3800,7 @@ GXD void ae_plan_pair(Dev d, const uint32_t *pa, const uint32_t *pb, const int32
   if (k >= 0 && (skip[k] & 1u)) return;  // the same decision for a cross-shard pair (digest flag)
   if (k < 0) {
     bool locked;
-    if (ae_lock_skip(d, pa[i], pb[i], locked)) return;
+    if (ae_lock_skip(d, pa[i], pb[i], locked, i)) return;
     ae_pair<VEC, PF, false, EV>(d, pa[i], pb[i], true, s_wave, s_red, nullptr, false, nullptr, locked);
   } else {
     const uint32_t nl = in.nlead[k];
@@ -4814,7 +4950,7 @@ __global__ void k_api_bs(Dev d, uint32_t v, const grec *list, uint32_t n) {
     uint64_t inc;
     bs_body_list(d, a, v, list, n, inc);
     gx_host_state *h = hst(d, v);
-    h->lock = lock_snap(h->lock, h->flags, d.round);  // a nil blocks the looper from now on
+    h->lock = lock_snap(h->lock, h->flags, d.round, d.p.lock_readers != 0);  // a nil blocks the looper from now on
   }
   acc_flush(d, a);
 }
@@ -4824,7 +4960,7 @@ __global__ void k_api_bt(Dev d, uint32_t v, uint64_t running, const grec *others
     uint32_t n = *n_others;
     bt_finish(d, a, v, running, others, n < d.L ? n : d.L);
     gx_host_state *h = hst(d, v);
-    h->lock = lock_snap(h->lock, h->flags, d.round);
+    h->lock = lock_snap(h->lock, h->flags, d.round, d.p.lock_readers != 0);
   }
   acc_flush(d, a);
 }
@@ -4838,7 +4974,7 @@ __global__ void k_api_getb(Dev d, uint32_t v, uint32_t limit, grec *out, uint32_
   Acc a;
   gx_host_state hs = *hst(d, v);
   uint32_t l = get_broadcasts_team<64>(d, a, v, hs, limit, out, limit_bytes, overhead);
-  hs.lock = lock_snap(hs.lock, hs.flags, d.round);  // a looper's nil may have been taken
+  hs.lock = lock_snap(hs.lock, hs.flags, d.round, d.p.lock_readers != 0);  // a looper's nil may have been taken
   if (threadIdx.x == 0) {
     *hst(d, v) = hs;
     *n_out = l;

@@ -14,7 +14,7 @@ round; tests/test_lock_cpu.py runs them on the oracle, tests/test_gpu_lock.py on
 against the oracle. The reference has no test for this behaviour (its unit tests never block a
 looper behind a queue), so the cases pin the restatement, not a reference fixture.
 """
-from sidecar_amd.abi import (INIT_OWN, INIT_WARM, LOCK_PENDING_EXPIRE, TOMBSTONE, Engine,
+from sidecar_amd.abi import (INIT_OWN, INIT_WARM, LOCK_DEFER_MERGE, LOCK_PENDING_EXPIRE, TOMBSTONE, Engine,
                              default_params)
 
 # loopers tick only when a case makes them (their phase is seeded within a 1000-round interval)
@@ -149,7 +149,77 @@ def pipeline_overflow(lib, k=10):
     return e
 
 
+def push_pull_read_locked_side(lib, k=6):
+    """gx.h lock_readers: host 1's only lock holder is its blocked BroadcastServices (the read lock)
+    and no writer waits (empty pipeline, QUIET loopers), so LocalState's RLock succeeds
+    (services_delegate.go:148) and round 0's exchange with host 1 runs. The partner merges host 1's
+    state at once. Host 1's merge waits behind the lock: its pool slot holds the partner's state,
+    and it merges in host 1's first unlocked round (p + 1). While that merge waits, a writer is
+    waiting too, so host 1's later exchanges fail."""
+    e = _engine(lib, n_hosts=4, n_services=2, fanout=1, init_mode=INIT_OWN, ae_period_rounds=1, lock_readers=1,
+                **QUIET)
+    p = _block_bs(e, 1, k)
+    e.run_rounds(1)
+    st = e.stats()
+    assert st["ae_deferred"] == 1 and st["ae_locked"] == 0 and st["ae_exchanges"] == 2, st
+    assert e.hosts()[1].lock & LOCK_DEFER_MERGE
+    partner = [x for x in (0, 2, 3) if _has(e, x, 1)]
+    assert len(partner) == 1, partner  # host 1's state reached its partner only
+    x = partner[0]
+    assert not _has(e, 1, x)
+    while e.round <= p:
+        e.run_rounds(1)
+        assert not _has(e, 1, x) and e.hosts()[1].lock & LOCK_DEFER_MERGE
+    e.run_rounds(1)  # round p + 1: host 1 is unlocked, the waiting merge runs first
+    assert _has(e, 1, x) and not e.hosts()[1].lock & LOCK_DEFER_MERGE
+    st = e.stats()
+    assert st["ae_locked"] >= 1 and st["ae_deferred"] == 1 and st["ae_defer_lost"] == 0, st
+    return e
+
+
+def push_pull_read_locked_writer_waiting(lib, k=6):
+    """gx.h lock_readers: host 1 read-locked, but a gossip record from host 0 reached its pipeline
+    earlier in the round (ProcessServiceMsgs waits in AddServiceEntry's Lock: a writer is pending),
+    so LocalState's RLock waits too and the exchange fails, as it does when BroadcastTombstones holds
+    the write lock."""
+    e = _engine(lib, n_hosts=2, n_services=2, fanout=1, init_mode=INIT_OWN, ae_period_rounds=1, lock_readers=1,
+                **QUIET)
+    _block_bs(e, 1, k)
+    e.send_services(0, [(0, s, e.now()) for s in range(e.S)], 1)
+    e.run_rounds(1)
+    st = e.stats()
+    assert st["lock_buffered"] > 0 and st["ae_locked"] == 1 and st["ae_deferred"] == 0, st
+    w = _engine(lib, n_hosts=2, n_services=2, fanout=1, init_mode=INIT_OWN, ae_period_rounds=1, lock_readers=1,
+                **QUIET)
+    own = [(1, s, w.now()) for s in range(w.S)]
+    for _ in range(k):
+        w.send_services(1, own, 1)
+    w.broadcast_tombstones(1, own)  # BroadcastTombstones blocks holding the write lock
+    w.run_rounds(1)
+    st = w.stats()
+    assert st["ae_locked"] == 1 and st["ae_deferred"] == 0, st
+    return e
+
+
+def push_pull_read_locked_slot_taken(lib, k=6):
+    """gx.h lock_readers with one pool slot: hosts 1 and 2 are both read-locked with no writer
+    waiting, so both of round 0's exchanges run, but only the lowest host id keeps its waiting
+    merge; host 2's is dropped and counted (ae_defer_lost)."""
+    e = _engine(lib, n_hosts=4, n_services=2, fanout=1, init_mode=INIT_OWN, ae_period_rounds=1, lock_readers=1,
+                lock_defer_slots=1, **QUIET)
+    _block_bs(e, 1, k)
+    _block_bs(e, 2, k)
+    e.run_rounds(1)
+    st = e.stats()
+    assert st["ae_deferred"] == 1 and st["ae_defer_lost"] == 1 and st["ae_locked"] == 0, st
+    assert e.hosts()[1].lock & LOCK_DEFER_MERGE and not e.hosts()[2].lock & LOCK_DEFER_MERGE
+    return e
+
+
 CASES = {
+    "push_pull_read_locked_side": push_pull_read_locked_side,
+    "push_pull_read_locked_writer_waiting": push_pull_read_locked_writer_waiting,
+    "push_pull_read_locked_slot_taken": push_pull_read_locked_slot_taken,
     "bs_nil_blocks_receive": bs_nil_blocks_receive,
     "bs_nil_blocks_receive_lock_off": lambda lib: bs_nil_blocks_receive(lib, lock_model=0),
     "bt_nil_holds_write_lock": bt_nil_holds_write_lock,

@@ -23,8 +23,9 @@ def check(lib, name):
     extra = {k: v for k, v in got_stats.items() if k not in ref_stats}
     fd = {k for k in extra if k.startswith("fd_")} | {"lost_packets"}
     # (round 6) false_expiries: every alive-lifespan expiry of a live owner's record, so `expired`
-    # itself in these cases (no departures)
-    assert set(extra) <= {"bytes_sent", "cap_cuts", "change_events", "listener_drops", "false_expiries"} | fd
+    # itself in these cases (no departures); ae_deferred / ae_defer_lost (lock_readers, off here)
+    assert set(extra) <= {"bytes_sent", "cap_cuts", "change_events", "listener_drops", "false_expiries",
+                          "ae_deferred", "ae_defer_lost"} | fd
     assert all(extra[k] == 0 for k in extra if k not in ("change_events", "false_expiries"))
     if "false_expiries" in extra:
         assert extra["false_expiries"] == got_stats["expired"]

@@ -168,7 +168,8 @@ def _progress(msg):  # past pytest's capture: a long test shows it is alive
     print(msg, file=sys.__stderr__, flush=True)
 
 
-def test_cfg5_full_h32768_parity(gx_lib):
+@pytest.mark.parametrize("lock_readers", [0, 1])
+def test_cfg5_full_h32768_parity(gx_lib, lock_readers):
     """The bench's own workload, cfg 5 at its full size (H = 32768, S = 16: 2-way partition for rounds
     [0, 50), ExpireServer storm of the other half at round 5, heal, push-pull every 10 rounds,
     queue_cap 20480), against the OpenMP oracle for rounds 0..101: the storm (5.4e8 ExpireServer
@@ -176,12 +177,17 @@ def test_cfg5_full_h32768_parity(gx_lib):
     checkpoint: every counter, every host's queue digest and bookkeeping, the per-record min and max
     word over all 32768 views, 24 full rows with their server times, and state.LastChanged of every
     view. The oracle holds 155 GB of host memory; if the box cannot give it, gx_create fails with
-    GX_ENOMEM and so does this test (no skip)."""
+    GX_ENOMEM and so does this test (no skip). With lock_readers = 1 (gx.h: an exchange whose locked
+    sides hold only BroadcastServices' read lock with no writer waiting runs) the lock words carry
+    the write-lock bits and the few exchanges that qualify (2 of 10240 at H = 2048 on the oracle,
+    all before the storm's jobs fill the pipelines) merge one way now and one way later, or lose the
+    waiting half when the host's pool slot is taken (both engines count it in ae_defer_lost)."""
     orc = _omp_oracle()
     H = 32768
     _progress("cfg5@32768: creating the HIP engine and the OpenMP oracle")
-    g = Engine(default_params(gx_lib, **CFG5), lib=gx_lib)
-    o = Engine(default_params(orc, **CFG5), lib=orc)
+    kw = dict(CFG5, lock_readers=lock_readers)
+    g = Engine(default_params(gx_lib, **kw), lib=gx_lib)
+    o = Engine(default_params(orc, **kw), lib=orc)
     sample = np.linspace(0, H - 1, 24).astype(int)
     for stop in (6, 51, 101):
         n = stop - g.round
@@ -208,6 +214,8 @@ def test_cfg5_full_h32768_parity(gx_lib):
     assert st["gossip_accepts"] == 0 and st["lock_buffered"] > 0 and st["lock_drops"] > 0
     assert st["lock_drained"] == 0 and st["first_locked_round"] == 7
     assert st["queue_drops"] == 0 and st["first_drop_round"] == -1  # faithful to the reference's queues
+    _progress(f"cfg5@32768 lock_readers {lock_readers}: ae_deferred {st['ae_deferred']} ae_defer_lost {st['ae_defer_lost']}")
+    assert lock_readers or st["ae_deferred"] + st["ae_defer_lost"] == 0
 
 
 CFG3_BENCH = dict(bench.CONFIGS["cfg3"]["p"])
