@@ -2915,7 +2915,8 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
     bool lkw = false, lka = false;
     if (d.p.lock_model && lane < (uint32_t)NR && vi < d.Hl) {
       const uint32_t lw = d.hs[vi].lock;
-      if (locked_in(d, lw)) lka = t != 0;
+      if (locked_in(d, lw) && d.p.fd_handoff_shared) t = 0;  // k_fd_recv takes its items (fd_handoff_locked)
+      else if (locked_in(d, lw)) lka = t != 0;
       else lkw = GX_LOCK_BUF(lw) != 0 && !departed(d, d.lo + vi);
     }
     const bool sm = !lkw && !lka && t && t <= 16, md = !lkw && !lka && t > 16 && t <= 32;
