@@ -434,7 +434,8 @@ static int round_send_impl(gx_engine *e) {
     const bool ev = !e->log_views.empty();
     const unsigned grid = d.Hl < SCAN_GRID ? d.Hl : SCAN_GRID;
     if (vec && !ev && e->scan_nch > 1) {  // rows split over blocks, then joined per view
-      k_scan_split<true><<<SCAN_GRID, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
+      k_scan_split<true><<<SCAN_GRID, 256, GX_SCAN_WAVE ? 4 * sizeof(grec) * d.L : 0, s>>>(d, e->scan_tmp, e->scan_chunk,
+                                                                                         e->scan_nch);
       k_scan_join<<<grid, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
     } else {
       (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
@@ -485,6 +486,12 @@ static int round_send_impl(gx_engine *e) {
   return scan_probe_end(e);
 }
 
+#ifndef GX_LOCK_APPEND
+#define GX_LOCK_APPEND 1
+#endif
+#ifndef GX_LOCK_APPEND_HL
+#define GX_LOCK_APPEND_HL 32768
+#endif
 #ifndef GX_MERGE_SMALL_HL
 #define GX_MERGE_SMALL_HL 16384  // 16 receivers per block below this many local hosts: merge 2.0 -> 1.1 ms (cfg 2)
                                  // and 2.4 -> 1.5 ms (cfg 4) over 60 rounds lock off (profiles/r05/ab/merge_nr16_*)
@@ -518,6 +525,13 @@ static int round_merge_impl(gx_engine *e) {
     // dependent chain, and 64 receivers per block run a wave's four of them one after another; 16 per
     // block spread them over more waves (cfg 5, locked gossip rounds 93.7 -> 87.7 us; lock off the
     // 64-receiver blocks stay 3-5% faster, profiles/r06/ab/merge_nr16_cfg5.jsonl)
+    // locked receivers' pipeline appends first, at high occupancy (k_lock_append), where k_merge_seg's
+    // item waves would take several passes over the receivers: cfg 5 (32768 receivers) lock-on gossip
+    // rounds 88.3 -> 79.6 us; at 16384 receivers (cfg 3) the extra launch cost 7.7 us per round, and
+    // with GossipMessages 15 most locked inboxes exceed a segment (+4%), so neither takes it
+    // (profiles/r06/ab/lock_append_*.jsonl)
+    if (GX_LOCK_APPEND && d.p.lock_model && !d.p.fd_handoff_shared && d.NG == 1 && d.Hl >= GX_LOCK_APPEND_HL)
+      k_lock_append<<<nblk(d.Hl, 16), 256, 0, s>>>(d);
     const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL || d.p.lock_model;
     const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
     if (small) {
