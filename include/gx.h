@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define GX_ABI_VERSION 10
+#define GX_ABI_VERSION 11
 
 #define GX_OK 0
 #define GX_EIO (-5)
@@ -305,7 +305,22 @@ typedef struct gx_params {
    * model. Unsharded engines only (GX_EINVAL otherwise). lock_defer_slots: 1..4096 (0 = 64). */
   uint32_t lock_readers;
   uint32_t lock_defer_slots;
+  /* lock_model = 1 with fd_enable, unsharded engines: memberlist's own alive / suspect / dead
+   * messages share the packet handler's handoff queue with the delegate's user messages (upstream
+   * memberlist's net.go handleCommand at the fork's date queues all four kinds on one handoff
+   * channel that one packetHandler goroutine drains in order; the fork, github.com/NinesStack/
+   * memberlist cfac2b5cf519, is absent, so parity unpinned). While the host's catalog lock blocks
+   * NotifyMsg, the handler stops once it holds the 53rd record of the pipeline (1 + notifications 25 +
+   * 1 + ServiceMsgs 25 + 1, gx.h lock_buffer): a memberlist message of a packet arriving before that
+   * is handled at once; after it, it queues in the handoff queue in arrival order (memberlist's own
+   * messages come first in a compound packet: gossip() takes its broadcasts before the delegate's)
+   * and takes a place of the pipeline, or is dropped at a full one (gx_stats.fd_handoff_drops). The
+   * queued messages are handled in the memberlist phase of the host's first unlocked round, before
+   * that round's packets' (gx_fd_host.hq_len). 0 (default) = memberlist messages never wait for the
+   * catalog lock (the round-5 model). */
+  uint32_t fd_handoff_shared;
 } gx_params;
+#define GX_LOCK_HANDLER_AT 53u /* pipeline records at which memberlist's packet handler blocks */
 #define GX_LOCK_BUF_MAX_BYTES (1ull << 36) /* 64 GiB of lock_buffer records per engine */
 #define GX_PP_MATCHING 0
 #define GX_PP_INITIATE 1
@@ -401,6 +416,8 @@ typedef struct gx_stats {
   uint64_t expire_deferred;  /* ExpireServer calls that waited for the lock */
   uint64_t ae_deferred;      /* lock_readers: push-pull merges of a read-locked side that waited for its lock */
   uint64_t ae_defer_lost;    /* ... and that the engine could not keep (its pool slot was taken); 0 = faithful */
+  uint64_t fd_handoff_queued; /* fd_handoff_shared: memberlist messages queued behind a blocked handler */
+  uint64_t fd_handoff_drops;  /* ... and dropped at a full pipeline */
   uint64_t false_expiries;   /* of `expired`: alive-lifespan expiries (services_state.go:655-679) of a
                                 record whose owner host has not departed (the owner is live; with
                                 churn it may have stopped the service and its tombstone not arrived) */
@@ -809,6 +826,7 @@ typedef struct gx_fd_host {
   uint32_t q_len;             /* queued memberlist messages */
   uint32_t departed;          /* 1 from depart_round on if this host crashed */
   uint16_t q_head[GX_FD_MAX_TX]; /* per transmit count: the newest queued node */
+  uint32_t hq_len;            /* fd_handoff_shared: memberlist messages waiting in the handoff queue */
 } gx_fd_host;
 typedef struct gx_fd_msg {    /* alive / suspect / dead message (memberlist net.go) */
   uint32_t incarnation;

@@ -102,6 +102,10 @@ struct gx_engine {
   uint32_t P;
   uint64_t *dpool;
   uint32_t *dpool_host, *dpool_res, *dclaim;
+  /* gx.h fd_handoff_shared: memberlist messages waiting in each host's handoff queue (HQ per host,
+   * count gx_fd_host.hq_len), arrival order */
+  uint32_t HQ;
+  gx_fd_msg *fdq;
   uint32_t PW;            /* words per host of pexp, ceil(H / 32) */
   uint32_t *pexp;         /* H * PW  owners whose ExpireServer waits for the host's lock (lazy) */
   int in_round;           /* inside a round phase: the lock applies (ABI entry points act directly) */
@@ -1153,10 +1157,22 @@ static void ph_receive(gx_engine *e, uint32_t i, void *ctx) {
     if (e->p.lock_model) {
       uint32_t nb = GX_LOCK_BUF(h->lock);
       const uint32_t cap_v = pipe_cap(e, v);
+      uint32_t *nq = e->p.fd_handoff_shared ? &e->fdh[v].hq_len : NULL;
       for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) {
         uint32_t m = e->in_list[x];
+        if (nq && e->fd_len[m] && nb + *nq >= GX_LOCK_HANDLER_AT) { /* the handler is blocked: they queue */
+          for (uint32_t y = 0; y < e->fd_len[m]; y++) {
+            if (nb + *nq < cap_v) {
+              e->fdq[(size_t)v * e->HQ + (*nq)++] = e->fdm[(size_t)m * e->p.fd_msg_cap + y];
+              e->st.fd_handoff_queued++;
+            } else {
+              e->st.fd_handoff_drops++;
+            }
+          }
+          e->fd_len[m] = 0; /* (the others are handled now, in ph_fd_receive) */
+        }
         for (uint32_t y = 0; y < e->msg_len[m]; y++) {
-          if (nb < cap_v) {
+          if (nb + (nq ? *nq : 0) < cap_v) {
             e->lkb[(size_t)v * e->C + nb++] = e->msg[(size_t)m * cap + y];
             e->st.lock_buffered++;
           } else {
@@ -1585,6 +1601,8 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL;
   if (p->lock_readers > 1 || (p->lock_readers && (!p->lock_model || p->n_shards > 1)) || p->lock_defer_slots > 4096)
     return GX_EINVAL;
+  if (p->fd_handoff_shared > 1 || (p->fd_handoff_shared && (!p->fd_enable || !p->lock_model || p->n_shards > 1)))
+    return GX_EINVAL;
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -1737,6 +1755,10 @@ int gx_create(const gx_params *p, gx_engine **out) {
       for (uint32_t x = 0; x < e->P; x++) e->dpool_host[x] = e->dclaim[x] = GX_NOHOST;
     }
     e->lkb = (grec *)malloc(sizeof(grec) * H * e->C);
+    if (p->fd_handoff_shared) { /* the handoff queue's places after the 53 the handler's chain holds */
+      e->HQ = e->C > GX_LOCK_HANDLER_AT ? e->C - GX_LOCK_HANDLER_AT : 0;
+      e->fdq = (gx_fd_msg *)malloc(sizeof(gx_fd_msg) * H * (e->HQ ? e->HQ : 1));
+    }
     e->PW = (e->H + 31) / 32;
     if (p->storm_round >= 0 || p->fd_enable) e->pexp = (uint32_t *)malloc(4ull * H * e->PW);
     if (!e->lkb || ((p->storm_round >= 0 || p->fd_enable) && !e->pexp)) {
@@ -1802,6 +1824,7 @@ int gx_destroy(gx_engine *e) {
   free(e->dpool_host);
   free(e->dpool_res);
   free(e->dclaim);
+  free(e->fdq);
   free(e->pexp);
   free_names(e);
   free(e);

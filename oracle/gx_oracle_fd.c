@@ -421,6 +421,11 @@ static void ph_fd_receive(gx_engine *e, uint32_t i, void *ctx) {
   int64_t now = *(const int64_t *)ctx;
   uint32_t v = e->lo + i, cap = e->p.fd_msg_cap;
   if (departed(e, v)) return;
+  if (e->fdh[v].hq_len && !locked_at(e, v)) { /* gx.h fd_handoff_shared: the handoff queue drains first */
+    const uint32_t n = e->fdh[v].hq_len;
+    e->fdh[v].hq_len = 0;
+    for (uint32_t k = 0; k < n; k++) fd_handle(e, v, &e->fdq[(size_t)v * e->HQ + k], now);
+  }
   for (uint32_t x = e->in_cnt[v]; x < e->in_cnt[v + 1]; x++) {
     uint32_t m = e->in_list[x];
     for (uint32_t y = 0; y < e->fd_len[m]; y++) fd_handle(e, v, &e->fdm[(size_t)m * cap + y], now);

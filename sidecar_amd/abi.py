@@ -115,6 +115,7 @@ class GxParams(C.Structure):
         ("gossip_messages", C.c_uint32), ("push_pull_mode", C.c_uint32), ("inbox_slots", C.c_uint32),
         ("lock_model", C.c_uint32), ("lock_buffer", C.c_uint32), ("probe_piggyback", C.c_uint32),
         ("push_pull_stagger", C.c_uint32), ("lock_readers", C.c_uint32), ("lock_defer_slots", C.c_uint32),
+        ("fd_handoff_shared", C.c_uint32),
     ]
 
     # fields memberlist derives from the cluster size (gx_fd_defaults)
@@ -165,7 +166,7 @@ class GxStats(C.Structure):
         "fd_state_merges", "queue_deferred")] + [("first_drop_round", C.c_int64)] + [
         ("locked_merges", C.c_uint64), ("first_locked_round", C.c_int64)] + [(n, C.c_uint64) for n in (
         "lock_buffered", "lock_drops", "lock_drained", "ae_locked", "expire_deferred", "ae_deferred",
-        "ae_defer_lost", "false_expiries")]
+        "ae_defer_lost", "fd_handoff_queued", "fd_handoff_drops", "false_expiries")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
@@ -186,7 +187,7 @@ class GxMember(C.Structure):
 class GxFdHost(C.Structure):
     _fields_ = [("probe_pass", C.c_uint32), ("probe_index", C.c_uint32), ("wrap_round", C.c_int32),
                 ("min_deadline", C.c_int32), ("q_len", C.c_uint32), ("departed", C.c_uint32),
-                ("q_head", C.c_uint16 * 32)]
+                ("q_head", C.c_uint16 * 32), ("hq_len", C.c_uint32)]
 
 
 class GxFdMsg(C.Structure):

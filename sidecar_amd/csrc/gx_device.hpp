@@ -79,7 +79,7 @@ enum {
 // Counters outside Acc (their own accumulators): packet loss and memberlist failure detection.
 enum {
   C_LOST = C_NCTR, C_FD_PROBES, C_FD_PROBE_FAIL, C_FD_SUSPECT, C_FD_CONFIRM, C_FD_DEATH, C_FD_REFUTE,
-  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_FEXP, C_AE_DEFER, C_AE_DEFER_LOST, C_NCTR_ALL
+  C_FD_ALIVE, C_FD_SENT, C_FD_RECV, C_FD_STATE_MERGE, C_EXP_DEFER, C_FEXP, C_AE_DEFER, C_AE_DEFER_LOST, C_FD_HQ, C_FD_HQ_DROP, C_NCTR_ALL
 };
 #define GX_NCTR_SLOTS 56
 static_assert(C_NCTR_ALL <= GX_NCTR_SLOTS, "counter slots");
@@ -193,6 +193,10 @@ struct Dev {
   uint32_t *dpool_host, *dpool_res, *dclaim;  // [P]
   uint8_t *ro_flag;    // [H]
   uint32_t *ro_list;   // [H]
+  // gx.h fd_handoff_shared: memberlist messages waiting in each host's handoff queue (HQ places per
+  // host, count gx_fd_host.hq_len), arrival order
+  uint32_t HQ;
+  gx_fd_msg *fdq;      // [Hl][HQ]
   // The planned exchange packed by k_send itself (gx_round_gossip_begin): a packet to another shard
   // is written straight into its slot of the send buffer. Set only for that launch.
   uint8_t *ob_buf;           // the send buffer (slots of 16 + 16 * packet_cap bytes), or null

@@ -434,7 +434,8 @@ static int round_send_impl(gx_engine *e) {
     const bool ev = !e->log_views.empty();
     const unsigned grid = d.Hl < SCAN_GRID ? d.Hl : SCAN_GRID;
     if (vec && !ev && e->scan_nch > 1) {  // rows split over blocks, then joined per view
-      k_scan_split<true><<<SCAN_GRID, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
+      k_scan_split<true><<<SCAN_GRID, 256, GX_SCAN_WAVE ? 4 * sizeof(grec) * d.L : 0, s>>>(d, e->scan_tmp, e->scan_chunk,
+                                                                                         e->scan_nch);
       k_scan_join<<<grid, 256, 0, s>>>(d, e->scan_tmp, e->scan_chunk, e->scan_nch);
     } else {
       (vec ? (ev ? k_scan<true, true> : k_scan<true, false>) : (ev ? k_scan<false, true> : k_scan<false, false>))
@@ -485,6 +486,12 @@ static int round_send_impl(gx_engine *e) {
   return scan_probe_end(e);
 }
 
+#ifndef GX_LOCK_APPEND
+#define GX_LOCK_APPEND 1
+#endif
+#ifndef GX_LOCK_APPEND_HL
+#define GX_LOCK_APPEND_HL 32768
+#endif
 #ifndef GX_MERGE_SMALL_HL
 #define GX_MERGE_SMALL_HL 16384  // 16 receivers per block below this many local hosts: merge 2.0 -> 1.1 ms (cfg 2)
                                  // and 2.4 -> 1.5 ms (cfg 4) over 60 rounds lock off (profiles/r05/ab/merge_nr16_*)
@@ -518,6 +525,13 @@ static int round_merge_impl(gx_engine *e) {
     // dependent chain, and 64 receivers per block run a wave's four of them one after another; 16 per
     // block spread them over more waves (cfg 5, locked gossip rounds 93.7 -> 87.7 us; lock off the
     // 64-receiver blocks stay 3-5% faster, profiles/r06/ab/merge_nr16_cfg5.jsonl)
+    // locked receivers' pipeline appends first, at high occupancy (k_lock_append), where k_merge_seg's
+    // item waves would take several passes over the receivers: cfg 5 (32768 receivers) lock-on gossip
+    // rounds 88.3 -> 79.6 us; at 16384 receivers (cfg 3) the extra launch cost 7.7 us per round, and
+    // with GossipMessages 15 most locked inboxes exceed a segment (+4%), so neither takes it
+    // (profiles/r06/ab/lock_append_*.jsonl)
+    if (GX_LOCK_APPEND && d.p.lock_model && !d.p.fd_handoff_shared && d.NG == 1 && d.Hl >= GX_LOCK_APPEND_HL)
+      k_lock_append<<<nblk(d.Hl, 16), 256, 0, s>>>(d);
     const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL || d.p.lock_model;
     const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
     if (small) {
@@ -809,6 +823,8 @@ static int check_params(const gx_params *p) {
     return GX_EINVAL;
   if (p->lock_readers > 1 || (p->lock_readers && (!p->lock_model || p->n_shards > 1)) || p->lock_defer_slots > 4096)
     return GX_EINVAL;  // gx.h lock_readers: unsharded engines with the lock modelled
+  if (p->fd_handoff_shared > 1 || (p->fd_handoff_shared && (!p->fd_enable || !p->lock_model || p->n_shards > 1)))
+    return GX_EINVAL;  // gx.h fd_handoff_shared
   if (p->fd_enable) {
     if (p->n_hosts > 65534 || p->fanout > 16) return GX_EINVAL;
     if (p->fd_probe_rounds < 1 || p->fd_indirect_checks > 16 || p->fd_msg_cap < 1 || p->fd_msg_cap > 64) return GX_EINVAL;
@@ -837,7 +853,7 @@ int gx_destroy(gx_engine *e) {
                   e->ae_pcount, d.view, d.minexp, d.own_status, d.hs, d.fifo, d.sleep, d.dq, d.arena, d.arena_len, d.msg, d.msg_w0, d.msg_len,
                   d.msg_dst, e->in_cnt_buf, d.scan_list, d.scan_cnt, d.tick,
                   d.sbytes, d.srvt, d.vlc, d.ev_slot, d.ev_log, d.ev_cnt, d.ctr, d.in_hdr, d.in_ovf, d.in_rec, d.work_cnt, d.work, d.mrec, e->pp_dev, e->pp_prow, e->name_rank, e->api_dev, e->conv_bad, e->digest_buf, d.kprof,
-                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap, d.lkb, d.pexp, d.dpool, d.dpool_host, d.dpool_res, d.dclaim, d.ro_flag, d.ro_list};
+                  d.mem, d.fd_dl, d.fdh, d.fdm, d.fd_len, d.fd_peers, d.fd_np, d.fd_snap, d.lkb, d.pexp, d.dpool, d.dpool_host, d.dpool_res, d.dclaim, d.ro_flag, d.ro_list, d.fdq};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   codec_free(e);
@@ -1049,6 +1065,10 @@ int gx_create(const gx_params *p, gx_engine **out) {
       HIPCHK(hipMemset(d.dclaim, 0xff, sizeof(uint32_t) * d.P));
       HIPCHK(hipMemset(d.dpool_res, 0, sizeof(uint32_t) * d.P));
       HIPCHK(hipMemset(d.ro_flag, 0, H));
+    }
+    if (p->fd_handoff_shared) {  // the handoff queue's places after the 53 the handler's chain holds
+      d.HQ = d.C > GX_LOCK_HANDLER_AT ? d.C - GX_LOCK_HANDLER_AT : 0;
+      ALLOC(d.fdq, sizeof(gx_fd_msg) * H * (d.HQ ? d.HQ : 1));
     }
   }
   ALLOC(e->conv_bad, sizeof(unsigned long long));
@@ -2581,6 +2601,8 @@ int gx_stats_get(gx_engine *e, gx_stats *out) {
   out->expire_deferred = c[C_EXP_DEFER];
   out->ae_deferred = c[C_AE_DEFER];
   out->ae_defer_lost = c[C_AE_DEFER_LOST];
+  out->fd_handoff_queued = c[C_FD_HQ];
+  out->fd_handoff_drops = c[C_FD_HQ_DROP];
   out->false_expiries = c[C_FEXP];
   out->first_drop_round = fdr == ~0ull ? -1 : (int64_t)fdr;
   out->lost_packets = c[C_LOST];

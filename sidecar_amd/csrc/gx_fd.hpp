@@ -576,6 +576,7 @@ __global__ void k_fd_init(Dev d) {
     h.min_deadline = GX_FD_NO_DEADLINE;
     h.q_len = 0;
     h.departed = 0;
+    h.hq_len = 0;
     for (int b = 0; b < GX_FD_MAX_TX; b++) h.q_head[b] = GX_FD_NONE;
     d.fdh[v] = h;
   }
@@ -626,12 +627,65 @@ __global__ __launch_bounds__(64) void k_fd_send(Dev d) {  // one thread per host
   fd_flush(d, f);
 }
 
+// gx.h fd_handoff_shared: a receiver whose catalog lock blocks NotifyMsg takes its packets' items
+// in arrival order, memberlist's messages of a packet before its records (k_merge_seg leaves such
+// receivers to this kernel): a memberlist message is handled at once while the handler is not yet
+// blocked (fewer than GX_LOCK_HANDLER_AT items held), else it queues in the handoff queue or is
+// dropped at a full pipeline; records go to the pipeline as in k_merge_seg. Oracle: ph_receive.
+GXD void fd_handoff_locked(const Dev &d, Acc &a, FdAcc &f, uint32_t vi, uint32_t lw) {
+  const uint32_t v = d.lo + vi, cnt = d.in_cnt[vi], capv = pipe_cap(d, vi, lw), fcap = d.p.fd_msg_cap;
+  const bool now_ok = !departed(d, v);
+  uint32_t nb = GX_LOCK_BUF(lw), nq = d.fdh[vi].hq_len;
+  grec *lkb = &d.lkb[(size_t)vi * d.C];
+  gx_fd_msg *q = &d.fdq[(size_t)vi * d.HQ];
+  int64_t after = -1;
+  for (uint32_t n = 0; n < cnt; n++) {
+    const uint4 hx = inbox_next(d, vi, after);
+    after = hx.x;
+    const uint32_t nf = d.fd_len[hx.y];
+    const gx_fd_msg *pk = &d.fdm[(size_t)hx.y * fcap];
+    if (nb + nq < GX_LOCK_HANDLER_AT) {
+      if (now_ok)
+        for (uint32_t y = 0; y < nf; y++) fd_handle(d, a, f, v, pk[y]);
+    } else {
+      for (uint32_t y = 0; y < nf; y++) {
+        if (nb + nq < capv) {
+          q[nq++] = pk[y];
+          f.inc(C_FD_HQ);
+        } else {
+          f.inc(C_FD_HQ_DROP);
+        }
+      }
+    }
+    const grec *pr = packet_recs(d, vi, hx.w, hx.y);
+    for (uint32_t x = 0; x < hx.z; x++) {
+      if (nb + nq < capv) {
+        lkb[nb++] = pr[x];
+        a.c[C_LOCK_BUF]++;
+      } else {
+        a.c[C_LOCK_DROP]++;
+      }
+    }
+  }
+  if (cnt) {  // (a deadNode handled above may have set the waiting-ExpireServer bit: reread the word)
+    d.hs[vi].lock = (d.hs[vi].lock & ((1u << GX_LOCK_BUF_SHIFT) - 1u)) | nb << GX_LOCK_BUF_SHIFT;
+    d.fdh[vi].hq_len = nq;
+  }
+}
 __global__ __launch_bounds__(64) void k_fd_recv(Dev d) {  // one thread per receiver of this engine
   Acc a;
   FdAcc f;
   const uint32_t vi = blockIdx.x * blockDim.x + threadIdx.x, v = d.lo + vi;
-  if (vi < d.Hl && !departed(d, v)) {
+  const uint32_t lw = vi < d.Hl && d.p.fd_handoff_shared ? d.hs[vi].lock : 0u;
+  if (vi < d.Hl && d.p.fd_handoff_shared && locked_in(d, lw)) {
+    fd_handoff_locked(d, a, f, vi, lw);
+  } else if (vi < d.Hl && !departed(d, v)) {
     const uint32_t cap = d.p.fd_msg_cap;
+    if (d.p.fd_handoff_shared && d.fdh[vi].hq_len) {  // the handoff queue drains first (unlocked now)
+      const uint32_t n = d.fdh[vi].hq_len;
+      d.fdh[vi].hq_len = 0;
+      for (uint32_t k = 0; k < n; k++) fd_handle(d, a, f, v, d.fdq[(size_t)vi * d.HQ + k]);
+    }
     // the packets' messages are read-only here: the next one is loaded before the current
     // message's handler runs, so its load is not ordered behind the handler's row writes
     // the inbox in sender order (a selection walk over the few headers)

@@ -531,8 +531,9 @@ struct ScanChunk {
 };
 // [r0, r1): the slots this block streams (tile-aligned; the whole row by default). co: chunk mode,
 // the view's bookkeeping (list count, expiry bound, state.LastChanged, scan count) goes to *co for
-// k_scan_join instead of the view.
-template <bool VEC, bool EV>
+// k_scan_join instead of the view. WT: S | 128 known at compile time (the LDS server-time path is
+// not compiled: fewer registers, k_scan_split).
+template <bool VEC, bool EV, bool WT = false>
 GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t *cnt_out, ScanLds &sm,
                    uint32_t r0 = 0, uint32_t r1 = 0xffffffffu, ScanChunk *co = nullptr) {
   if (r1 > d.R) r1 = d.R;
@@ -568,7 +569,7 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
   }
   // S | 128: an owner's slots sit in S/2 adjacent lanes of one wave, so the server times of a
   // tile's owners (the last expired record of each, key order) come from a ballot, with no LDS
-  const bool wave_times = VEC && d.S >= 2 && (128 % d.S) == 0;
+  const bool wave_times = WT || (VEC && d.S >= 2 && (128 % d.S) == 0);
   const bool ev_on = EV && evk >= 0;
   bool listing = true;     // block-uniform: list positions (or event positions) still needed
   uint32_t my_last = 0;    // 1 + this thread's last expired key (state.LastChanged)
@@ -739,8 +740,13 @@ GXD void scan_view(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uin
 
 // only_host >= 0: that one view (the API's TombstoneOthersServices), list at list_base, count in
 // cnt_out[0]. Otherwise the round's worklist, block-strided; view oi's list at oi * list_stride.
+#ifdef GX_SCAN_WPE
+#define GX_SCAN_ATTR __attribute__((amdgpu_waves_per_eu(GX_SCAN_WPE)))
+#else
+#define GX_SCAN_ATTR
+#endif
 template <bool VEC, bool EV>
-__global__ __launch_bounds__(256) void k_scan(Dev d, grec *list_base, uint32_t list_stride, uint32_t list_cap,
+__global__ __launch_bounds__(256) GX_SCAN_ATTR void k_scan(Dev d, grec *list_base, uint32_t list_stride, uint32_t list_cap,
                                                uint32_t *cnt_out, int only_host) {
   __shared__ ScanLds sm;
   if (only_host >= 0) {
@@ -779,15 +785,163 @@ GXD uint32_t scan_chunks(const Dev &d, uint32_t n, uint32_t nch, uint32_t &clen)
   clen = (d.R / c + 1023u) / 1024u * 1024u;
   return (d.R + clen - 1) / clen;
 }
+// One chunk [r0, r1) of view oi by a block whose four waves each stream a contiguous quarter on
+// their own (round 6): no block barrier per tile, SCAN_WPF 256-slot tiles in flight per wave, few
+// registers (8 waves per SIMD). Each wave lists its first list_cap expirations in LDS (wave prefix
+// from ballots); one barrier at the end concatenates the four lists in key order into `list` and
+// writes the chunk's result, as scan_view's chunk mode does (S | 128: an owner's slots sit in S/2
+// adjacent lanes of a 128-slot half-tile, so server times come from ballots). VEC, no listeners.
+#ifndef SCAN_WPF
+#define SCAN_WPF 2  // cfg 3 scan, 30 rounds: block scan 34.8 ms, WPF 2 / 3 / 4 29.3 / 29.5 / 34.5 (profiles/r06/ab/scan_wave_cfg3_lm0.jsonl)
+#endif
+GXD void scan_chunk_waves(const Dev &d, uint32_t oi, grec *list, uint32_t list_cap, uint32_t r0, uint32_t r1,
+                          ScanChunk *co, grec *s_sub, uint32_t *s_wcnt, uint32_t *s_wlast,
+                          unsigned long long *s_wmexp, unsigned long long *s_red) {
+  if (r1 > d.R) r1 = d.R;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t q = ((r1 - r0) / 4 + 255u) / 256u * 256u;  // a wave's range, tile-aligned
+  const uint32_t w0 = r0 + wv * q < r1 ? r0 + wv * q : r1, w1 = w0 + q < r1 ? w0 + q : r1;
+  uint64_t *row = &d.view[(size_t)oi * d.R];
+  grec *sub = &s_sub[(size_t)wv * list_cap];
+  const uint32_t lpo = d.S / 2, gb = lane & ~(lpo - 1);
+  const uint64_t gm = (lpo == 64 ? ~0ull : ((1ull << lpo) - 1ull)) << gb, lt = (1ull << lane) - 1ull;
+  uint32_t n_exp = 0, my_last = 0;
+  unsigned long long c_exp = 0, c_gc = 0, c_wr = 0, c_dep = 0, mexp = ~0ull;
+  ulonglong2 nx[SCAN_WPF][2];
+  auto ld = [&](uint32_t base, ulonglong2 *dst) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t r = base + 128 * h + 2 * lane;
+      if (r < w1) {
+        v2u64 x = __builtin_nontemporal_load(reinterpret_cast<const v2u64 *>(&row[r]));
+        dst[h] = make_ulonglong2(x.x, x.y);
+      } else {
+        dst[h] = make_ulonglong2(GX_SLOT_ABSENT, GX_SLOT_ABSENT);
+      }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < SCAN_WPF; k++) ld(w0 + 256u * k, nx[k]);
+  for (uint32_t base = w0; base < w1; base += SCAN_WPF * 256u) {
+#pragma unroll
+    for (int k = 0; k < SCAN_WPF; k++) {
+      const uint32_t b = base + 256u * k;
+      if (b >= w1) break;  // wave-uniform
+      const ulonglong2 cur[2] = {nx[k][0], nx[k][1]};
+      if (b + SCAN_WPF * 256u < w1) ld(b + SCAN_WPF * 256u, nx[k]);
+      uint64_t wd[4] = {cur[0].x, cur[0].y, cur[1].x, cur[1].y}, nw[4];
+      bool ex[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        bool gc;
+        nw[j] = expiry_word(d, wd[j], ex[j], gc);
+        c_exp += ex[j];
+        c_gc += gc;
+        const unsigned long long x = exp_time(d.p, nw[j]);
+        mexp = x < mexp ? x : mexp;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t r = b + 128 * h + 2 * lane;
+        const bool ch0 = nw[2 * h] != wd[2 * h], ch1 = nw[2 * h + 1] != wd[2 * h + 1];
+        c_wr += ch0 + ch1;
+        if (ch0 || ch1) *reinterpret_cast<ulonglong2 *>(&row[r]) = make_ulonglong2(nw[2 * h], nw[2 * h + 1]);
+        if (d.departures) {  // gx.h false_expiries
+          if (ex[2 * h]) c_dep += departed(d, owner_of(d, r));
+          if (ex[2 * h + 1]) c_dep += departed(d, owner_of(d, r + 1));
+        }
+        if (ex[2 * h]) my_last = r + 1;
+        if (ex[2 * h + 1]) my_last = r + 2;
+        const uint64_t gbits = __ballot(ex[2 * h] || ex[2 * h + 1]) & gm;  // server times: owner's last expiry
+        if (gbits && lane == 63u - (uint32_t)__clzll(gbits)) {
+          const bool e1 = ex[2 * h + 1];
+          gx_server_times *st = srv_times(d, oi + d.lo, (r + (e1 ? 1u : 0u)) / d.S);
+          const int64_t ts = ts_of(e1 ? nw[2 * h + 1] : nw[2 * h]);
+          st->last_updated_ns = ts;
+          st->last_changed_ns = ts;
+        }
+      }
+      const uint64_t b0 = __ballot(ex[0]), b1 = __ballot(ex[1]), b2 = __ballot(ex[2]), b3 = __ballot(ex[3]);
+      const uint32_t tn = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+      if (tn && n_exp < list_cap) {  // key order: half 0 (lanes, 2 slots each), then half 1
+        const uint32_t h1 = (uint32_t)(__popcll(b0) + __popcll(b1));
+        uint32_t pos[4];
+        pos[0] = n_exp + (uint32_t)(__popcll(b0 & lt) + __popcll(b1 & lt));
+        pos[1] = pos[0] + ex[0];
+        pos[2] = n_exp + h1 + (uint32_t)(__popcll(b2 & lt) + __popcll(b3 & lt));
+        pos[3] = pos[2] + ex[2];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (ex[j] && pos[j] < list_cap) {
+            grec g;
+            g.w = nw[j];
+            g.r = b + 128 * (j >> 1) + 2 * lane + (j & 1);
+            g.pad = 0;
+            sub[pos[j]] = g;
+          }
+        }
+      }
+      n_exp += tn;
+    }
+  }
+  // the wave's results, then the block's: the four lists in key order
+  my_last = (uint32_t)~wave_min(~(unsigned long long)my_last);
+  const unsigned long long wm = wave_min(mexp);
+  if (lane == 0) {
+    s_wcnt[wv] = n_exp;
+    s_wlast[wv] = my_last;
+    s_wmexp[wv] = wm;
+  }
+  __syncthreads();
+  uint32_t tot = 0, last = 0, off[4];
+  unsigned long long m = ~0ull;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    off[w] = tot;
+    tot += s_wcnt[w];
+    if (s_wlast[w]) last = s_wlast[w];
+    m = s_wmexp[w] < m ? s_wmexp[w] : m;
+  }
+  for (uint32_t i = threadIdx.x; i < 4 * list_cap; i += blockDim.x) {
+    const uint32_t w = i / list_cap, j = i - w * list_cap;
+    const uint32_t nw_ = s_wcnt[w] < list_cap ? s_wcnt[w] : list_cap;
+    if (j < nw_ && off[w] + j < list_cap) list[off[w] + j] = s_sub[i];
+  }
+  if (threadIdx.x == 0) {
+    co->cnt = tot;
+    co->last = last;
+    co->mexp = m;
+  }
+  block_ctr(d, C_CHG, c_exp, s_red);
+  if (__ballot(c_wr != 0) != 0 && lane == 0) mark_change(d);
+  c_wr = wave_sum(c_wr);
+  if (lane == 0) kbytes(d, GX_K_SCAN, c_wr * 8, 0);
+  if (threadIdx.x == 0)
+    kbytes(d, GX_K_SCAN, (unsigned long long)(r1 - r0) * 8 + 16ull * (tot < list_cap ? tot : list_cap), r1 - r0);
+  block_ctr(d, C_EXPIRED, c_exp, s_red);
+  block_ctr(d, C_FEXP, c_exp - c_dep, s_red);
+  block_ctr(d, C_GC, c_gc, s_red);
+  block_ctr(d, C_SCANSLOTS, threadIdx.x == 0 ? r1 - r0 : 0, s_red);
+}
+#ifndef GX_SCAN_WAVE
+#define GX_SCAN_WAVE 1
+#endif
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_scan_split(Dev d, grec *tmp, ScanChunk *chunk, uint32_t nch) {
+__global__ __launch_bounds__(256) GX_SCAN_ATTR void k_scan_split(Dev d, grec *tmp, ScanChunk *chunk, uint32_t nch) {
   __shared__ ScanLds sm;
+  extern __shared__ grec s_sub[];  // GX_SCAN_WAVE: [4][d.L] (dynamic)
+  __shared__ uint32_t s_wcnt[4], s_wlast[4];
+  __shared__ unsigned long long s_wmexp[4];
   uint32_t clen;
   const uint32_t nc = scan_chunks(d, *d.wl_cnt, nch, clen), n = *d.wl_cnt * nc;
   for (uint32_t w = blockIdx.x; w < n; w += gridDim.x) {
     const uint32_t oi = d.work[w / nc], c = w % nc;
     const size_t k = (size_t)oi * nch + c;
-    scan_view<VEC, false>(d, oi, &tmp[k * d.L], d.L, nullptr, sm, c * clen, (c + 1) * clen, &chunk[k]);
+    if (GX_SCAN_WAVE && VEC)
+      scan_chunk_waves(d, oi, &tmp[k * d.L], d.L, c * clen, (c + 1) * clen, &chunk[k], s_sub, s_wcnt, s_wlast, s_wmexp,
+                       sm.red);
+    else
+      scan_view<VEC, false, VEC>(d, oi, &tmp[k * d.L], d.L, nullptr, sm, c * clen, (c + 1) * clen, &chunk[k]);
     __syncthreads();
   }
 }
@@ -2891,6 +3045,22 @@ GXD bool lock_append_seg(const Dev &d, uint32_t vi, bool act) {
   return true;
 }
 
+// The ServicesState lock (gx.h lock_model), ahead of k_merge_seg: the pipeline appends of locked
+// receivers, 16 lanes per receiver (lock_append_seg) at 8 waves per SIMD, so a round whose receivers
+// are all locked keeps more of these short dependent chains in flight than k_merge_seg's item
+// waves (3 per SIMD, sized for the merge path). A receiver done here has its routing count cleared
+// (k_merge_seg skips it); one with more packets than a segment takes stays for k_merge_seg.
+#ifndef GX_LOCK_APPEND_WPE
+#define GX_LOCK_APPEND_WPE 8
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GX_LOCK_APPEND_WPE))) void k_lock_append(Dev d) {
+  const uint32_t vi = (blockIdx.x * 256u + threadIdx.x) >> 4;
+  bool act = false;
+  if (vi < d.Hl) act = d.mrec[vi] != 0 && locked_in(d, d.hs[vi].lock);  // segment-uniform
+  const bool ok = lock_append_seg<16>(d, act ? vi : 0u, act);
+  if (act && ok && (threadIdx.x & 15) == 0) d.mrec[vi] = 0;
+}
+
 #define MERGE_NR 64  // receivers per block (16 measured 3% slower in the accepting stretch, profiles/r03/ab)
 #define MERGE_NONE 0xffffffffu
 template <bool K32, bool EV, int NR = MERGE_NR, int WPE = 3>
@@ -2915,7 +3085,8 @@ __global__ __launch_bounds__(64 * MERGE_WAVES) __attribute__((amdgpu_waves_per_e
     bool lkw = false, lka = false;
     if (d.p.lock_model && lane < (uint32_t)NR && vi < d.Hl) {
       const uint32_t lw = d.hs[vi].lock;
-      if (locked_in(d, lw)) lka = t != 0;
+      if (locked_in(d, lw) && d.p.fd_handoff_shared) t = 0;  // k_fd_recv takes its items (fd_handoff_locked)
+      else if (locked_in(d, lw)) lka = t != 0;
       else lkw = GX_LOCK_BUF(lw) != 0 && !departed(d, d.lo + vi);
     }
     const bool sm = !lkw && !lka && t && t <= 16, md = !lkw && !lka && t > 16 && t <= 32;

@@ -25,7 +25,7 @@ def test_libgx_exports_every_symbol():
     lib = load_library(LIBGX_PATH)
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.gx_abi_version() == 10
+    assert lib.gx_abi_version() == 11
     assert lib.gx_backend().decode() == "hip-gfx950"
 
 

@@ -3,7 +3,7 @@ tests (tests/fd_cases.py), round-model invariants of the detector scenarios, and
 OpenMP build with the serial checker."""
 import pytest
 
-from sidecar_amd.abi import GX_EINVAL, M_ALIVE, M_DEAD, TOMBSTONE, Engine, GxError, default_params
+from sidecar_amd.abi import GX_EINVAL, INIT_OWN, M_ALIVE, M_DEAD, TOMBSTONE, Engine, GxError, default_params
 from tests import fd_cases
 from tests.fd_parity import assert_same_fd
 from tests.oracle_lib import load_oracle
@@ -109,3 +109,32 @@ def test_fd_omp_equals_serial(oracle_lib, name):
         assert_same(a, b, f"{name} round {a.round}")
         if kw.get("fd_enable"):
             assert_same_fd(a, b, f"{name} round {a.round}")
+
+
+@pytest.mark.parametrize("bad", [dict(fd_handoff_shared=2), dict(fd_handoff_shared=1, fd_enable=0),
+                                 dict(fd_handoff_shared=1, lock_model=0),
+                                 dict(fd_handoff_shared=1, n_shards=2, shard_id=0)])
+def test_fd_handoff_rejects_unsupported_modes(oracle_lib, bad):
+    kw = dict(n_hosts=16, n_services=4, fd_enable=1)
+    kw.update(bad)
+    with pytest.raises(GxError):
+        Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+
+
+def test_fd_handoff_shared_queues_and_drops(oracle_lib):
+    """gx.h fd_handoff_shared: with small pipelines that fill, memberlist messages to hosts whose
+    handler is blocked queue (and drain once unlocked) or drop; every message sent is either handled,
+    queued or dropped; with the knob off none waits. Departures are still all detected."""
+    kw = dict(n_hosts=64, n_services=8, init_mode=INIT_OWN, fd_enable=1, depart_round=3, depart_ppm=100000,
+              ae_period_rounds=10, queue_cap=4096, lock_buffer=80)
+    off = Engine(default_params(oracle_lib, **kw), lib=oracle_lib)
+    on = Engine(default_params(oracle_lib, fd_handoff_shared=1, **kw), lib=oracle_lib)
+    off.run_rounds(200)
+    on.run_rounds(200)
+    a, b = off.stats(), on.stats()
+    assert a["fd_handoff_queued"] == a["fd_handoff_drops"] == 0
+    assert b["fd_handoff_queued"] > 0 and b["fd_handoff_drops"] > 0
+    waiting = sum(h.hq_len for h in on.fd_hosts())
+    assert b["fd_msgs_received"] + waiting + b["fd_handoff_drops"] <= b["fd_msgs_sent"]
+    assert b["fd_msgs_received"] < a["fd_msgs_received"]
+    assert b["fd_deaths"] >= 64 * 0.05 and a["fd_deaths"] >= 64 * 0.05
