@@ -22,7 +22,7 @@ a = ap.parse_args()
 import torch  # noqa: E402
 torch.cuda.init()
 libs = [(os.path.basename(p), load_library(p)) for p in a.libs]
-cases = [("off_dead", 0, 21), ("off_acc", 0, 51), ("on_fill", 1, 11), ("on_full", 1, 21)]
+cases = [("off_dead", 0, 21), ("off_acc", 0, 51), ("on_fill", 1, 11), ("on_full", 1, 21), ("on_full51", 1, 51)]
 res = {}
 for rep in range(a.reps):
     for case, lm, start in cases:

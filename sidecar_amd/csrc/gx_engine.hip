@@ -527,7 +527,8 @@ static int round_merge_impl(gx_engine *e) {
     // 64-receiver blocks stay 3-5% faster, profiles/r06/ab/merge_nr16_cfg5.jsonl)
     // locked receivers' pipeline appends first, at high occupancy (k_lock_append), where k_merge_seg's
     // item waves would take several passes over the receivers: cfg 5 (32768 receivers) lock-on gossip
-    // rounds 88.3 -> 79.6 us; at 16384 receivers (cfg 3) the extra launch cost 7.7 us per round, and
+    // rounds 88.1 -> 79.8 us, a round whose pipelines are all full 30.0 -> 32.3 us (the launch with
+    // nothing to append); at 16384 receivers (cfg 3) the extra launch cost 7.7 us per round, and
     // with GossipMessages 15 most locked inboxes exceed a segment (+4%), so neither takes it
     // (profiles/r06/ab/lock_append_*.jsonl)
     if (GX_LOCK_APPEND && d.p.lock_model && !d.p.fd_handoff_shared && d.NG == 1 && d.Hl >= GX_LOCK_APPEND_HL)

@@ -3057,6 +3057,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GX_LOCK_APP
   const uint32_t vi = (blockIdx.x * 256u + threadIdx.x) >> 4;
   bool act = false;
   if (vi < d.Hl) act = d.mrec[vi] != 0 && locked_in(d, d.hs[vi].lock);  // segment-uniform
+  if (__ballot(act) == 0) return;  // wave-uniform: nothing to append (a round whose pipelines are full)
   const bool ok = lock_append_seg<16>(d, act ? vi : 0u, act);
   if (act && ok && (threadIdx.x & 15) == 0) d.mrec[vi] = 0;
 }
