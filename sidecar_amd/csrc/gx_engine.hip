@@ -552,6 +552,14 @@ static int round_merge_impl(gx_engine *e) {
   return GX_OK;
 }
 
+// lock off, cfg 2's window (two push-pull rounds): 0.94 ms as built; two tiles in flight 1.01, plain
+// row loads and stores 0.98, two tiles at 3 waves per SIMD 1.08 (profiles/r06/ab/ae_cfg2_variants.jsonl)
+#ifndef GX_AE_PF_OFF
+#define GX_AE_PF_OFF 1  // lock off: tiles in flight per pair
+#endif
+#ifndef GX_AE_NT_OFF
+#define GX_AE_NT_OFF true  // lock off: nontemporal row loads and stores
+#endif
 #ifndef GX_AE_PF_LOCK
 #define GX_AE_PF_LOCK 1  // 2 tiles in flight spill (92 B scratch): 0.98 vs 0.71 ms at cfg 5 lock on (profiles/r05/ab/ae_pf_lock.jsonl)
 #endif
@@ -666,7 +674,7 @@ static int ae_whole_impl(gx_engine *e) {
       // skips costs one round trip per chunk, not a block per pair
       if (vec && !ev && d.p.lock_model)
         k_ae_chunk<true, GX_AE_PF_LOCK, true, true><<<ae_grid(np, 1), 256, 0, s>>>(d, key0, key1, np);
-      else if (vec && !ev) k_ae<true, 1, true, true><<<np, 256, 0, s>>>(d, key0, key1);
+      else if (vec && !ev) k_ae<true, GX_AE_PF_OFF, GX_AE_NT_OFF, GX_AE_NT_OFF><<<np, 256, 0, s>>>(d, key0, key1);
       else if (vec) k_ae_ev<true><<<np, 256, 0, s>>>(d, key0, key1);
       else if (!ev) k_ae<false><<<np, 256, 0, s>>>(d, key0, key1);
       else k_ae_ev<false><<<np, 256, 0, s>>>(d, key0, key1);
