@@ -489,6 +489,11 @@ static int round_send_impl(gx_engine *e) {
 #ifndef GX_LOCK_APPEND
 #define GX_LOCK_APPEND 1
 #endif
+// with k_lock_append taking the locked receivers, the merge's 64-receiver blocks are faster again:
+// cfg 5 lock on, filling 80.7 -> 77.9 us, full 32.8 -> 30.6 us (profiles/r06/ab/merge_nr64_lapp_cfg5.jsonl)
+#ifndef GX_MERGE_LAPP_NR64
+#define GX_MERGE_LAPP_NR64 1
+#endif
 #ifndef GX_LOCK_APPEND_HL
 #define GX_LOCK_APPEND_HL 32768
 #endif
@@ -531,9 +536,9 @@ static int round_merge_impl(gx_engine *e) {
     // nothing to append); at 16384 receivers (cfg 3) the extra launch cost 7.7 us per round, and
     // with GossipMessages 15 most locked inboxes exceed a segment (+4%), so neither takes it
     // (profiles/r06/ab/lock_append_*.jsonl)
-    if (GX_LOCK_APPEND && d.p.lock_model && !d.p.fd_handoff_shared && d.NG == 1 && d.Hl >= GX_LOCK_APPEND_HL)
-      k_lock_append<<<nblk(d.Hl, 16), 256, 0, s>>>(d);
-    const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL || d.p.lock_model;
+    const bool lapp = GX_LOCK_APPEND && d.p.lock_model && !d.p.fd_handoff_shared && d.NG == 1 && d.Hl >= GX_LOCK_APPEND_HL;
+    if (lapp) k_lock_append<<<nblk(d.Hl, 16), 256, 0, s>>>(d);
+    const bool small = d.NG > 1 || d.Hl < GX_MERGE_SMALL_HL || (d.p.lock_model && !(GX_MERGE_LAPP_NR64 && lapp));
     const unsigned g = nblk(d.Hl, small ? 16u : (unsigned)MERGE_NR);
     if (small) {
       if (d.R < (1u << 26)) (ev ? k_merge_seg<true, true, 16, MERGE_WPE_GM> : k_merge_seg<true, false, 16, MERGE_WPE_GM>)<<<g, 64 * MERGE_WAVES, 0, s>>>(d);
