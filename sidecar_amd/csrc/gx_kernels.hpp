@@ -777,8 +777,8 @@ __global__ __launch_bounds__(256) GX_SCAN_ATTR void k_scan(Dev d, grec *list_bas
 // whole rows (each chunk restarts the tile pipeline: 1,600 rows of cfg 3 in 8 chunks measured 8%
 // slower than whole rows, 400 rows 1.9x faster). clen: the chunk length, tile-aligned.
 #ifndef SCAN_ITEMS
-#define SCAN_ITEMS 2048u
-#endif
+#define SCAN_ITEMS 2048u  // wave-level chunks, cfg 3 over 30 rounds: 1024 / 2048 / 4096 items 32.9 / 29.3 / 30.3 ms
+#endif                    // lock off, 7.59 / 6.55 / 6.55 lock on (profiles/r06/ab/scan_wave_items_cfg3_*.jsonl)
 GXD uint32_t scan_chunks(const Dev &d, uint32_t n, uint32_t nch, uint32_t &clen) {
   uint32_t c = n ? (SCAN_ITEMS + n - 1) / n : 1;
   c = c < nch ? c : nch;
